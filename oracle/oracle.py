@@ -1,0 +1,336 @@
+"""ctypes binding of the CPU ORACLE (oracle/owsched_oracle.c) -- test infrastructure only.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.  It is the
+checker for the HIP path and the CPU baseline ("kind": "port"); the product path (openwhisk_amd) never
+loads it.  See owsched_oracle.h for the reference lines each function restates.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libowsched_oracle.so")
+
+NONE = -1
+THROW_INDEX = -2
+THROW_ARG = -3
+THROW_NOSUCHELEMENT = -4
+THROW_OVERFLOW = -5
+
+HEALTHY, UNHEALTHY, UNRESPONSIVE, OFFLINE = 0, 1, 2, 3
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        i32, u32, i64, u64, dbl = C.c_int32, C.c_uint32, C.c_int64, C.c_uint64, C.c_double
+        P = C.c_void_p
+        sig = {
+            "owo_java_hash": (i32, [C.c_char_p, i32]),
+            "owo_generate_hash": (i32, [C.c_char_p, i32, C.c_char_p, i32]),
+            "owo_gcd": (i32, [i32, i32]),
+            "owo_pairwise_coprime": (i32, [i32, P, i32]),
+            "owo_rng_index": (u32, [u64, u64, u32]),
+            "owo_rs_init": (None, [P, i32, i32]),
+            "owo_rs_try_acquire": (C.c_int, [P, i32]),
+            "owo_rs_release": (C.c_int, [P, i32, C.c_int]),
+            "owo_ns_new": (P, [i32, C.c_int]),
+            "owo_ns_free": (None, [P]),
+            "owo_ns_try_acquire": (C.c_int, [P, i32]),
+            "owo_ns_force_acquire": (C.c_int, [P, i32]),
+            "owo_ns_release": (C.c_int, [P, i32]),
+            "owo_ns_available": (i32, [P]),
+            "owo_ns_try_acquire_concurrent": (C.c_int, [P, u32, i32, i32]),
+            "owo_ns_force_acquire_concurrent": (C.c_int, [P, u32, i32, i32]),
+            "owo_ns_release_concurrent": (C.c_int, [P, u32, i32, i32]),
+            "owo_ns_concurrent_state": (C.c_int, [P, u32, P, P]),
+            "owo_ns_concurrent_size": (i32, [P]),
+            "owo_slots_new": (P, [i32, i32, C.c_int]),
+            "owo_slots_free": (None, [P]),
+            "owo_slots_count": (i32, [P]),
+            "owo_slots_get": (P, [P, i32]),
+            "owo_schedule": (C.c_int, [P, i32, u32, i32, P, P, i32, i32, i32, u64, u64, P, P]),
+            "owo_state_new": (P, [dbl, dbl, i64, u64, C.c_int]),
+            "owo_state_free": (None, [P]),
+            "owo_update_invokers": (C.c_int, [P, i32, P, P, P]),
+            "owo_update_cluster": (C.c_int, [P, i32]),
+            "owo_cluster_size": (i32, [P]),
+            "owo_n_invokers": (i32, [P]),
+            "owo_managed_size": (i32, [P]),
+            "owo_blackbox_size": (i32, [P]),
+            "owo_managed_steps": (i32, [P, P, i32]),
+            "owo_blackbox_steps": (i32, [P, P, i32]),
+            "owo_state_slots": (P, [P]),
+            "owo_read_permits": (i32, [P, P, i32]),
+            "owo_register_action": (i32, [P, C.c_char_p, i32, C.c_char_p, i32, u32, i32, i32, i32]),
+            "owo_action_hash": (i32, [P, i32]),
+            "owo_publish": (C.c_int, [P, i32, u64, P, P]),
+            "owo_release": (C.c_int, [P, i32, i32]),
+            "owo_replay": (C.c_int, [P, i32, P, P, P, P, u64, P, P, P]),
+            "owo_replay_parallel": (C.c_int, [P, i32, i32, P, P, P, P, u64, P, P, P]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+# ---------------------------------------------------------------------------------------------- primitives
+def java_hash(s: str) -> int:
+    b = s.encode("ascii")
+    return lib().owo_java_hash(b, len(b))
+
+
+def generate_hash(namespace: str, action_path: str) -> int:
+    a, b = namespace.encode("ascii"), action_path.encode("ascii")
+    return lib().owo_generate_hash(a, len(a), b, len(b))
+
+
+def pairwise_coprime_numbers_until(x: int) -> list[int]:
+    cap = max(x, 1)
+    out = np.zeros(cap, dtype=np.int32)
+    n = lib().owo_pairwise_coprime(x, _ptr(out), cap)
+    return out[:n].tolist()
+
+
+def rng_index(seed: int, seq: int, n: int) -> int:
+    return lib().owo_rng_index(seed, seq, n)
+
+
+# ---------------------------------------------------------------------------------------------- semaphores
+class ResizableSemaphore(C.Structure):
+    """RS:33-115 (state: permits c, operationCount ops, reductionSize R)."""
+
+    _fields_ = [("c", C.c_int32), ("ops", C.c_int32), ("R", C.c_int32)]
+
+    def __init__(self, max_allowed: int, reduction_size: int):
+        super().__init__()
+        lib().owo_rs_init(C.byref(self), max_allowed, reduction_size)
+
+    def try_acquire(self, acquires: int = 1) -> bool:
+        r = lib().owo_rs_try_acquire(C.byref(self), acquires)
+        if r < 0:
+            raise ValueError("require failed")
+        return bool(r)
+
+    def release(self, acquires: int, op_complete: bool) -> tuple[bool, bool]:
+        r = lib().owo_rs_release(C.byref(self), acquires, int(op_complete))
+        if r < 0:
+            raise ValueError("require failed")
+        return bool(r & 1), bool(r & 2)
+
+    @property
+    def available_permits(self) -> int:
+        return self.c
+
+    @property
+    def counter(self) -> int:
+        return self.ops
+
+
+class NestedSemaphore:
+    """NS:29-116 over FS:37-124.  `owned=False` wraps a semaphore that lives inside a slots vector/state."""
+
+    def __init__(self, memory_permits: int = 0, zombies: bool = True, _handle=None):
+        self._owned = _handle is None
+        self.h = _handle if _handle is not None else lib().owo_ns_new(memory_permits, int(zombies))
+
+    def __del__(self):
+        if getattr(self, "_owned", False) and self.h:
+            lib().owo_ns_free(self.h)
+            self.h = None
+
+    @staticmethod
+    def _chk(r):
+        if r == THROW_ARG:
+            raise ValueError("require failed")
+        if r == THROW_NOSUCHELEMENT:
+            raise KeyError("NoSuchElementException")
+        if r == THROW_OVERFLOW:
+            raise OverflowError("Maximum permit count exceeded")
+        return r
+
+    def try_acquire(self, acquires: int = 1) -> bool:
+        return bool(self._chk(lib().owo_ns_try_acquire(self.h, acquires)))
+
+    def force_acquire(self, acquires: int = 1) -> None:
+        self._chk(lib().owo_ns_force_acquire(self.h, acquires))
+
+    def release(self, acquires: int = 1) -> None:
+        self._chk(lib().owo_ns_release(self.h, acquires))
+
+    @property
+    def available_permits(self) -> int:
+        return lib().owo_ns_available(self.h)
+
+    def try_acquire_concurrent(self, key: int, max_concurrent: int, memory: int) -> bool:
+        return bool(self._chk(lib().owo_ns_try_acquire_concurrent(self.h, key, max_concurrent, memory)))
+
+    def force_acquire_concurrent(self, key: int, max_concurrent: int, memory: int) -> None:
+        self._chk(lib().owo_ns_force_acquire_concurrent(self.h, key, max_concurrent, memory))
+
+    def release_concurrent(self, key: int, max_concurrent: int, memory: int) -> None:
+        self._chk(lib().owo_ns_release_concurrent(self.h, key, max_concurrent, memory))
+
+    def concurrent_state(self, key: int):
+        c, ops = C.c_int32(), C.c_int32()
+        if lib().owo_ns_concurrent_state(self.h, key, C.byref(c), C.byref(ops)):
+            return c.value, ops.value
+        return None
+
+    def concurrent_size(self) -> int:
+        return lib().owo_ns_concurrent_size(self.h)
+
+
+class Slots:
+    """IndexedSeq[NestedSemaphore] (the `dispatched` argument of schedule)."""
+
+    def __init__(self, count: int = 0, permits: int = 0, zombies: bool = True, _handle=None):
+        self._owned = _handle is None
+        self.h = _handle if _handle is not None else lib().owo_slots_new(count, permits, int(zombies))
+
+    def __del__(self):
+        if getattr(self, "_owned", False) and self.h:
+            lib().owo_slots_free(self.h)
+            self.h = None
+
+    def __len__(self):
+        return lib().owo_slots_count(self.h)
+
+    def __getitem__(self, i) -> NestedSemaphore:
+        hh = lib().owo_slots_get(self.h, i)
+        if not hh:
+            raise IndexError(i)
+        return NestedSemaphore(_handle=hh)
+
+
+def schedule(max_concurrent, key, invokers, dispatched: Slots, slots, index, step, seq=0, rng_seed=0):
+    """SCPB:398-436.  invokers: list of (id, status).  Returns None, (id, overload) or raises IndexError."""
+    n = len(invokers)
+    ids = np.array([i for i, _ in invokers] or [0], dtype=np.int32)
+    st = np.array([s for _, s in invokers] or [0], dtype=np.uint8)
+    out = C.c_int32()
+    fl = C.c_uint8()
+    r = lib().owo_schedule(dispatched.h, max_concurrent, key, n, _ptr(ids), _ptr(st), slots, index, step, rng_seed, seq,
+                           C.byref(out), C.byref(fl))
+    if r == THROW_INDEX:
+        raise IndexError("IndexOutOfBoundsException")
+    if r == THROW_ARG:
+        raise ValueError("require failed")
+    if r == 0:
+        return None
+    return out.value, bool(fl.value & 1)
+
+
+# ---------------------------------------------------------------------------------------------- state
+class BalancerState:
+    """ShardingContainerPoolBalancerState (SCPB:449-585) + publish/releaseInvoker (SCPB:257-331)."""
+
+    def __init__(self, managed_fraction=0.9, blackbox_fraction=0.1, min_memory_mb=128, rng_seed=0, zombies=True):
+        self.h = lib().owo_state_new(managed_fraction, blackbox_fraction, min_memory_mb * 1024 * 1024, rng_seed,
+                                     int(zombies))
+        self._keep = []
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().owo_state_free(self.h)
+            self.h = None
+
+    def update_invokers(self, ids, user_memory_bytes, status):
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        mem = np.ascontiguousarray(user_memory_bytes, dtype=np.int64)
+        st = np.ascontiguousarray(status, dtype=np.uint8)
+        lib().owo_update_invokers(self.h, len(ids), _ptr(ids), _ptr(mem), _ptr(st))
+
+    def update_cluster(self, size: int):
+        lib().owo_update_cluster(self.h, size)
+
+    @property
+    def cluster_size(self):
+        return lib().owo_cluster_size(self.h)
+
+    @property
+    def n_invokers(self):
+        return lib().owo_n_invokers(self.h)
+
+    @property
+    def managed_size(self):
+        return lib().owo_managed_size(self.h)
+
+    @property
+    def blackbox_size(self):
+        return lib().owo_blackbox_size(self.h)
+
+    def _steps(self, fn):
+        cap = max(self.n_invokers, 1) + 1
+        out = np.zeros(cap, dtype=np.int32)
+        n = fn(self.h, _ptr(out), cap)
+        return out[:n].tolist()
+
+    @property
+    def managed_step_sizes(self):
+        return self._steps(lib().owo_managed_steps)
+
+    @property
+    def blackbox_step_sizes(self):
+        return self._steps(lib().owo_blackbox_steps)
+
+    @property
+    def invoker_slots(self) -> Slots:
+        return Slots(_handle=lib().owo_state_slots(self.h))
+
+    def permits(self) -> np.ndarray:
+        n = len(self.invoker_slots)
+        out = np.zeros(max(n, 1), dtype=np.int32)
+        lib().owo_read_permits(self.h, _ptr(out), n)
+        return out[:n]
+
+    def register_action(self, namespace, action_path, key, mem_mb, max_conc=1, blackbox=False) -> int:
+        a, b = namespace.encode("ascii"), action_path.encode("ascii")
+        return lib().owo_register_action(self.h, a, len(a), b, len(b), key, mem_mb, max_conc, int(blackbox))
+
+    def action_hash(self, action: int) -> int:
+        return lib().owo_action_hash(self.h, action)
+
+    def publish(self, action: int, seq: int):
+        out = C.c_int32()
+        fl = C.c_uint8()
+        lib().owo_publish(self.h, action, seq, C.byref(out), C.byref(fl))
+        return out.value, fl.value
+
+    def release(self, invoker: int, action: int) -> int:
+        return lib().owo_release(self.h, invoker, action)
+
+    def replay(self, stream) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Replay a Stream (openwhisk_amd.workload.Stream-like: acq_off, act, rel_off, rel_aid, seq_base)."""
+        n = len(stream.act)
+        out = np.full(max(n, 1), -9, dtype=np.int32)
+        fl = np.zeros(max(n, 1), dtype=np.uint8)
+        rf = np.zeros(max(len(stream.rel_aid), 1), dtype=np.uint8)
+        acq_off = np.ascontiguousarray(stream.acq_off, dtype=np.int64)
+        rel_off = np.ascontiguousarray(stream.rel_off, dtype=np.int64)
+        act = np.ascontiguousarray(stream.act, dtype=np.int32)
+        rel = np.ascontiguousarray(stream.rel_aid, dtype=np.int64)
+        lib().owo_replay(self.h, len(acq_off) - 1, _ptr(acq_off), _ptr(act), _ptr(rel_off), _ptr(rel),
+                         int(stream.seq_base), _ptr(out), _ptr(fl), _ptr(rf))
+        return out[:n], fl[:n], rf[: len(stream.rel_aid)]
