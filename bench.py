@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""Benchmark: bit-exact scheduling decisions/s of ShardingContainerPoolBalancer.schedule() semantics on MI355X.
+
+One step = one replay of a controller shard's activation stream (1M activations in capacity-calibrated batches,
+each batch = completion releases then publishes; workload.py "headline": 10k invokers, Zipf actions, 128..2048 MB,
+concurrent + blackbox actions, 2 % unhealthy).  Inputs are resident in HBM before the timed region; the slot state is
+restored before every step (included in the timed region).  N GPUs = N controller shards (clusterSize = N, one stream
+each, weak scaling, no data-path collective); for N > 1 the invoker health vector is all-gathered over RCCL once per
+step (the reference's controllers all consume the same health topic, SCPB:355).
+
+Prints ONE JSON line on rank 0.  The value counts only when every rank's assignment vector is bit-exact with the
+CPU oracle (checked after timing).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="headline")
+    ap.add_argument("--n-activations", type=int, default=1_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def algorithmic_bytes(w) -> int:
+    """Minimum HBM bytes one replay must move: stream in/out once, action table and slot state once."""
+    s = w.stream
+    n, r = len(s.act), len(s.rel_aid)
+    n_slots = len(w.inv_ids)
+    per_act = 4 + 4 + 1             # action id in, invoker out, flags out
+    per_rel = 8 + 4 + 4 + 1         # release id in, its invoker and action (gathered), release flag out
+    table = len(w.actions) * (16 + 4)  # {home, step, mem, meta} + slot key
+    state = n_slots * 4 * 2 + (w.inv_ids.size + 64) * 4  # permits load + store, pool words
+    offs = (s.n_batches + 1) * 16
+    return n * per_act + r * per_rel + table + state + offs
+
+
+def cpu_baseline(args, world):
+    """Oracle replay on the host cores: T threads, each replaying an independent shard stream of the same config."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ctypes as C
+
+    import oracle as O
+    from openwhisk_amd import workload as W
+
+    T = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    ws = [W.config(args.config, n_activations=args.n_activations, shard=t, n_shards=world) for t in range(T)]
+    sts = [O.state_for(w) for w in ws]
+    # identical batch structure is required by owo_replay_parallel: use shard 0's offsets for all threads
+    s0 = ws[0].stream
+    acts = [np.ascontiguousarray(w.stream.act, dtype=np.int32) for w in ws]
+    outs = [np.zeros(len(a), dtype=np.int32) for a in acts]
+    fls = [np.zeros(len(a), dtype=np.uint8) for a in acts]
+    acq = np.ascontiguousarray(s0.acq_off, dtype=np.int64)
+    rel = np.ascontiguousarray(s0.rel_off, dtype=np.int64)
+    aid = np.ascontiguousarray(s0.rel_aid, dtype=np.int64)
+    P = C.c_void_p
+    arr = lambda xs: (P * len(xs))(*[x.ctypes.data_as(P) for x in xs])  # noqa: E731
+    sarr = (P * T)(*[s.h for s in sts])
+    t0 = time.perf_counter()
+    O.lib().owo_replay_parallel(sarr, T, len(acq) - 1, acq.ctypes.data_as(P), arr(acts), rel.ctypes.data_as(P),
+                                aid.ctypes.data_as(P), 0, arr(outs), arr(fls), None)
+    dt = time.perf_counter() - t0
+    total = sum(len(a) for a in acts)
+    return {"value": total / dt, "unit": "decisions/s", "cores": T, "kind": "port",
+            "sample": f"{T} threads x one {args.config} shard stream of {args.n_activations} activations each "
+                      f"(oracle/owsched_oracle.c, -O3), {dt:.2f} s wall"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from openwhisk_amd import GpuShardingContainerPoolBalancer
+    from openwhisk_amd import workload as W
+
+    w = W.config(args.config, n_activations=args.n_activations, shard=rank, n_shards=world)
+    b = GpuShardingContainerPoolBalancer(managed_fraction=w.managed_fraction, blackbox_fraction=w.blackbox_fraction,
+                                         rng_seed=w.rng_seed, device=torch.cuda.current_device())
+    b.update_invokers_arrays(w.inv_ids, w.inv_mem, w.inv_status)
+    b.update_cluster(w.cluster_size)
+    b.register_actions(w.actions)
+    b.snapshot()
+
+    s = w.stream
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
+    d_acq, d_rel = t(s.acq_off, np.int64), t(s.rel_off, np.int64)
+    d_act, d_aid = t(s.act, np.int32), t(s.rel_aid if len(s.rel_aid) else np.zeros(1), np.int64)
+    d_out = torch.empty(len(s.act), dtype=torch.int32, device=dev)
+    d_fl = torch.empty(len(s.act), dtype=torch.uint8, device=dev)
+    d_rf = torch.empty(max(len(s.rel_aid), 1), dtype=torch.uint8, device=dev)
+    health = torch.from_numpy(w.inv_status.copy()).to(dev)
+    gathered = torch.empty((world, len(w.inv_status)), dtype=torch.uint8, device=dev) if world > 1 else None
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+
+    def step():
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, health)
+            b.update_health_device(len(w.inv_status), gathered[0].data_ptr(), sp)
+        b.restore(sp)
+        b.replay_device(s.n_batches, d_acq.data_ptr(), d_act.data_ptr(), d_rel.data_ptr(), d_aid.data_ptr(),
+                        s.seq_base, d_out.data_ptr(), d_fl.data_ptr(), d_rf.data_ptr(), sp)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, health)
+            b.update_health_device(len(w.inv_status), gathered[0].data_ptr(), sp)
+        b.restore(sp)
+        evs[k][0].record(stream)
+        b.replay_device(s.n_batches, d_acq.data_ptr(), d_act.data_ptr(), d_rel.data_ptr(), d_aid.data_ptr(),
+                        s.seq_base, d_out.data_ptr(), d_fl.data_ptr(), d_rf.data_ptr(), sp)
+        evs[k][1].record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(c) for a, c in evs]))
+    stats = b.stats()
+
+    exact = True
+    if not args.no_check:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+
+        st = O.state_for(w)
+        o_inv, o_fl, o_rf = st.replay(s)
+        exact = (np.array_equal(o_inv, d_out.cpu().numpy()) and np.array_equal(o_fl, d_fl.cpu().numpy())
+                 and np.array_equal(o_rf, d_rf.cpu().numpy()[: len(o_rf)])
+                 and np.array_equal(st.permits(), b.permits()))
+
+    n_dec = len(s.act)
+    t_step = wall / args.steps
+    if dist:
+        v = torch.tensor([t_step, 0.0 if exact else 1.0, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        t_step, bad, kern_ms = float(v[0]), float(v[1]), float(v[2])
+        exact = bad == 0.0
+    value = world * n_dec / t_step
+    algo = algorithmic_bytes(w)
+    achieved = algo / (kern_ms * 1e-3) / 1e9
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args, world)
+        line = {
+            "metric": "scheduling decisions/sec (whole node) at 10k invokers, 1M-activation batch",
+            "value": value if exact else 0.0,
+            "unit": "decisions/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_step * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (workload.py, seeded Zipf stream)",
+            "bit_exact": exact,
+            "config": {"workload": args.config, "invokers": int(len(w.inv_ids)), "activations_per_shard": n_dec,
+                       "batches": s.n_batches, "batch": w.info["batch"], "releases": int(len(s.rel_aid)),
+                       "cluster_size": w.cluster_size, "parallelism": f"{world} controller shard(s), 1 per GPU"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "owgs_engine_kernel", "kernel_ms": kern_ms, "algorithmic_bytes": algo},
+            "engine_stats": stats,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

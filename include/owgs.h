@@ -1,0 +1,164 @@
+/*
+ * owgs.h -- C ABI of the MI355X-native batched invoker scheduler ("GPU sharding" balancer).
+ *
+ * This is the drop-in boundary for OpenWhisk's controller-side invoker assignment hot path.  A JVM shim
+ * (GpuShardingContainerPoolBalancer) binds these symbols over JNI and keeps everything
+ * else of CommonLoadBalancer (activation bookkeeping, Kafka send, ack feed) on the JVM side.
+ * Paths below are relative to the reference repository root; abbreviations:
+ *   SCPB = core/controller/src/main/scala/org/apache/openwhisk/core/loadBalancer/ShardingContainerPoolBalancer.scala
+ *   CLB  = core/controller/src/main/scala/org/apache/openwhisk/core/loadBalancer/CommonLoadBalancer.scala
+ *   LB   = core/controller/src/main/scala/org/apache/openwhisk/core/loadBalancer/LoadBalancer.scala
+ *   NS   = common/scala/src/main/scala/org/apache/openwhisk/common/NestedSemaphore.scala
+ *
+ * Conventions
+ *   - Every entry point returns 0 on success or a negative OWGS_E* code; nothing throws or aborts across the ABI.
+ *     owgs_last_error() describes the last failure of a context.
+ *   - Buffers are owned by the caller.  Functions without a _device suffix take HOST pointers; *_device functions
+ *     take HIP device pointers (HBM-resident) and an optional hipStream_t passed as void*.
+ *   - Per-activation outcome: out_invoker >= 0 is the chosen invoker id; OWGS_NONE (-1) is the reference's None
+ *     ("No invokers available", SCPB:305-316); OWGS_THROW_INDEX (-2) marks an input for which the reference's
+ *     schedule() throws IndexOutOfBoundsException (Int.MinValue hash, SCPB:266-268/411, or an invoker id outside
+ *     invokerSlots, SCPB:413/422).  out_flags bit0 (OWGS_FLAG_OVERLOAD) = overload random fallback + forceAcquire
+ *     (SCPB:417-424); the JVM shim turns it into the MANAGED/BLACKBOX_SYSTEM_OVERLOAD counter (SCPB:277-286).
+ *   - Release flags: bit0 NoSuchElementException (NS:103), bit1 permit overflow Error (ForcibleSemaphore.scala:48-50),
+ *     bit2 activation has no entry (it was never scheduled: CLB:278-279 finds no ActivationEntry).
+ *   - Sequential semantics: a batch is equivalent to the reference executing, in array order, one schedule()
+ *     (or releaseInvoker()) per element against the single-writer context.  The random overload fallback draws
+ *     its index with the counter RNG keyed by (rng_seed, seq) documented in DESIGN.md (replaces ThreadLocalRandom,
+ *     SCPB:421).
+ *   - One context = one controller shard (SCPB horizontal sharding, SCPB:126-133); contexts are single-writer.
+ */
+#ifndef OWGS_H
+#define OWGS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OWGS_ABI_VERSION 1
+
+#define OWGS_OK 0
+#define OWGS_EINVAL (-22)  /* bad argument */
+#define OWGS_ENOMEM (-12)  /* allocation failed (host or device) */
+#define OWGS_EDEVICE (-5)  /* HIP runtime error */
+#define OWGS_ERANGE (-34)  /* state too large for the engine (see owgs_limits) */
+#define OWGS_ENOENT (-2)   /* unknown action / invoker */
+
+#define OWGS_NONE (-1)
+#define OWGS_THROW_INDEX (-2)
+#define OWGS_FLAG_OVERLOAD 1u
+
+#define OWGS_REL_NOSUCHELEMENT 1u
+#define OWGS_REL_OVERFLOW 2u
+#define OWGS_REL_NOENTRY 4u
+
+/* InvokerState (core/controller/.../loadBalancer/InvokerSupervision.scala:47-66): only HEALTHY is usable. */
+#define OWGS_HEALTHY 0
+#define OWGS_UNHEALTHY 1
+#define OWGS_UNRESPONSIVE 2
+#define OWGS_OFFLINE 3
+
+typedef struct owgs_ctx owgs_ctx;
+
+typedef struct owgs_config {
+    double managed_fraction;  /* whisk.loadbalancer.managed-fraction  (core/controller/src/main/resources/reference.conf:22-32) */
+    double blackbox_fraction; /* whisk.loadbalancer.blackbox-fraction */
+    int64_t min_memory_bytes; /* MemoryLimit.MIN_MEMORY (common/scala/src/main/resources/application.conf:377) */
+    int32_t cluster_size;     /* initial cluster size (SCPB:457 default 1) */
+    int32_t device;           /* HIP device ordinal */
+    uint64_t rng_seed;        /* overload-fallback RNG seed (DESIGN.md "Counter RNG") */
+} owgs_config;
+
+/* Replaces: object ShardingContainerPoolBalancer.instance(...) building the balancer (SCPB:336-365) and
+ * ShardingContainerPoolBalancerState() (SCPB:449-470). */
+int owgs_create(const owgs_config* cfg, owgs_ctx** out);
+void owgs_destroy(owgs_ctx* ctx);
+const char* owgs_last_error(const owgs_ctx* ctx);
+int owgs_abi_version(void);
+/* max invokers / slots the engine holds on chip (LDS); larger pools return OWGS_ERANGE from update_invokers */
+int owgs_limits(int32_t* max_invokers, int32_t* max_slots);
+
+/* Replaces: ShardingContainerPoolBalancerState.updateInvokers(newInvokers: IndexedSeq[InvokerHealth]) (SCPB:512-551),
+ * driven by the monitor actor on CurrentInvokerPoolState (SCPB:226-227).  status: OWGS_HEALTHY..OWGS_OFFLINE. */
+int owgs_update_invokers(owgs_ctx* ctx, int32_t n, const int32_t* ids, const int64_t* user_memory_bytes,
+                         const uint8_t* status);
+
+/* Replaces: ShardingContainerPoolBalancerState.updateCluster(newSize) (SCPB:561-584), driven by the Akka cluster
+ * membership events in the monitor actor (SCPB:230-248). */
+int owgs_update_cluster(owgs_ctx* ctx, int32_t new_size);
+
+/* Registers actions (the per-activation inputs of publish, SCPB:260-276).  For action i:
+ *   namespace  = msg.user.namespace.name.asString   (SCPB:266, hashed)
+ *   path       = action.fullyQualifiedName(false).asString, e.g. "ns/pkg/name" (SCPB:266, hashed)
+ *   key        = action.fullyQualifiedName(true).asString ("ns/pkg/name@0.0.1"): the NestedSemaphore map key (SCPB:271)
+ *   mem_mb     = action.limits.memory.megabytes (SCPB:274);  max_conc = action.limits.concurrency.maxConcurrent (SCPB:270)
+ *   blackbox   = action.exec.pull (SCPB:260)
+ * Strings are concatenated in *_bytes with offsets *_off[0..n] (n+1 entries).  generateHash (SCPB:370-372) runs on the
+ * GPU; out_hash (optional) receives it, out_action receives the action handle used by the batch calls. */
+int owgs_register_actions(owgs_ctx* ctx, int32_t n, const char* ns_bytes, const int32_t* ns_off,
+                          const char* path_bytes, const int32_t* path_off, const char* key_bytes,
+                          const int32_t* key_off, const int32_t* mem_mb, const int32_t* max_conc,
+                          const uint8_t* blackbox, int32_t* out_action, int32_t* out_hash);
+
+/* Replaces: the scheduling half of ShardingContainerPoolBalancer.publish (SCPB:257-290) -- pool selection, hash,
+ * home invoker, step size and ShardingContainerPoolBalancer.schedule (SCPB:398-436) with NestedSemaphore
+ * tryAcquireConcurrent / forceAcquireConcurrent (NS:32-91) -- for n activations in array order.
+ * seq[i] keys the overload RNG (may be NULL: seq = seq_base + i). */
+int owgs_publish_batch(owgs_ctx* ctx, int32_t n, const int32_t* action, const uint64_t* seq, uint64_t seq_base,
+                       int32_t* out_invoker, uint8_t* out_flags);
+
+/* Replaces: ShardingContainerPoolBalancer.releaseInvoker (SCPB:327-331) reached from CommonLoadBalancer
+ * .processCompletion (CLB:260-346): invokerSlots.lift(invoker).foreach(_.releaseConcurrent(fqn, maxConcurrent, mem)).
+ * invoker < 0 means "no ActivationEntry" (flag OWGS_REL_NOENTRY, no state change). out_flags may be NULL. */
+int owgs_release_batch(owgs_ctx* ctx, int32_t n, const int32_t* invoker, const int32_t* action, uint8_t* out_flags);
+
+/* Replaces: ShardingContainerPoolBalancer.schedule(maxConcurrent, fqn, invokers, dispatched, slots, index, step)
+ * (SCPB:398-436) called directly with an explicit walk, as the reference unit tests do (ShardingContainerPoolBalancer
+ * Tests.scala:244-412).  pool = 0 managed / 1 blackbox pool of the context; key = slot-key id (see owgs_key_id). */
+int owgs_schedule_walks(owgs_ctx* ctx, int32_t n, const uint8_t* pool, const int32_t* index, const int32_t* step,
+                        const int32_t* mem_mb, const int32_t* max_conc, const int32_t* key, const uint64_t* seq,
+                        int32_t* out_invoker, uint8_t* out_flags);
+
+/* Test seam mirroring `protected[loadBalancer] var _invokerSlots` (SCPB:455): replace the slot vector with n fresh
+ * NestedSemaphores of the given memory permits (concurrency maps emptied). */
+int owgs_set_slots(owgs_ctx* ctx, int32_t n, const int32_t* permits);
+/* Replaces the pool vectors for the explicit-walk tests: managed pool = (ids, status) as given. */
+int owgs_set_pool(owgs_ctx* ctx, int32_t pool, int32_t n, const int32_t* ids, const uint8_t* status);
+
+/* Introspection (ForcibleSemaphore.availablePermits / NestedSemaphore.concurrentState / state getters). */
+int owgs_read_permits(owgs_ctx* ctx, int32_t* out, int32_t cap, int32_t* n_slots);
+int owgs_read_concurrent(owgs_ctx* ctx, int32_t invoker, int32_t key, int32_t* permits, int32_t* op_count);
+int owgs_key_id(owgs_ctx* ctx, int32_t action);
+int owgs_state_info(owgs_ctx* ctx, int32_t* n_invokers, int32_t* managed, int32_t* blackbox, int32_t* cluster_size);
+int owgs_step_sizes(owgs_ctx* ctx, int32_t pool, int32_t* out, int32_t cap, int32_t* n);
+
+/* Stream replay with HBM-resident buffers (bench / batching thread).  Batch b first releases the activations
+ * rel_aid[rel_off[b]..rel_off[b+1]) (ids into this stream; their invoker is this stream's own earlier output),
+ * then publishes activations [acq_off[b], acq_off[b+1]) with action act[i] and seq = seq_base + i.
+ * All pointers are device pointers; stream is a hipStream_t (NULL = default stream).  Asynchronous. */
+int owgs_replay_device(owgs_ctx* ctx, int32_t n_batches, const int64_t* acq_off, const int32_t* act,
+                       const int64_t* rel_off, const int64_t* rel_aid, uint64_t seq_base, int32_t* out_invoker,
+                       uint8_t* out_flags, uint8_t* rel_flags, void* stream);
+/* Same with host buffers (copies in and out, synchronous). */
+int owgs_replay(owgs_ctx* ctx, int32_t n_batches, const int64_t* acq_off, const int32_t* act, const int64_t* rel_off,
+                const int64_t* rel_aid, uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags,
+                uint8_t* rel_flags);
+
+/* Restore the slot state captured by owgs_snapshot (bench: every timed step starts from the same state). */
+int owgs_snapshot(owgs_ctx* ctx);
+int owgs_restore(owgs_ctx* ctx, void* stream);
+
+/* Health all-gather hook (RCCL over xGMI, done by the caller): overwrite the status vector from a device buffer of
+ * n bytes (InvokerState codes), e.g. the rank-0 row of an all_gather of CurrentInvokerPoolState. */
+int owgs_update_health_device(owgs_ctx* ctx, int32_t n, const uint8_t* status_dev, void* stream);
+
+/* Engine counters of the last replay (diagnostics): [0] chunk iterations, [1] walk probes, [2] fallbacks,
+ * [3] long walks, [4] conflict groups. */
+int owgs_read_stats(owgs_ctx* ctx, uint64_t* out, int32_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,252 @@
+"""Host-side mirror of the reference's balancer interface over the HIP engine (libowgs.so).
+
+`GpuShardingContainerPoolBalancer` keeps the names, argument meaning and error behaviour of
+ShardingContainerPoolBalancer / ShardingContainerPoolBalancerState
+(core/controller/src/main/scala/org/apache/openwhisk/core/loadBalancer/ShardingContainerPoolBalancer.scala, "SCPB")
+for the scheduling hot path, batched: one call schedules or releases many activations with the sequential
+semantics of calling the reference once per activation in array order.  There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import (FLAG_OVERLOAD, HEALTHY, NONE, OFFLINE, THROW_INDEX, UNHEALTHY, UNRESPONSIVE, OwgsError,
+                   owgs_config)
+
+__all__ = ["GpuShardingContainerPoolBalancer", "InvokerHealth", "Action", "NONE", "THROW_INDEX", "FLAG_OVERLOAD",
+           "HEALTHY", "UNHEALTHY", "UNRESPONSIVE", "OFFLINE", "OwgsError"]
+
+MB = 1024 * 1024
+
+
+@dataclass(frozen=True)
+class InvokerHealth:
+    """InvokerHealth(InvokerInstanceId(id, userMemory), status) (LoadBalancer.scala:37-44)."""
+
+    id: int
+    user_memory_bytes: int
+    status: int = HEALTHY
+
+
+@dataclass(frozen=True)
+class Action:
+    """What publish() reads from an ExecutableWhiskActionMetaData + ActivationMessage (SCPB:260-276)."""
+
+    namespace: str        # msg.user.namespace.name (invoking namespace, hashed)
+    path: str             # action.fullyQualifiedName(false).asString ("ns/pkg/name", hashed)
+    version: str = "0.0.1"
+    mem_mb: int = 256     # action.limits.memory.megabytes
+    max_concurrent: int = 1
+    blackbox: bool = False  # action.exec.pull
+
+    @property
+    def key(self) -> str:  # fullyQualifiedName(true).asString: NestedSemaphore map key
+        return f"{self.path}@{self.version}"
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _pack(strings: list[str]) -> tuple[bytes, np.ndarray]:
+    enc = [s.encode("ascii") for s in strings]
+    off = np.zeros(len(enc) + 1, dtype=np.int32)
+    off[1:] = np.cumsum([len(b) for b in enc])
+    return b"".join(enc), off
+
+
+class GpuShardingContainerPoolBalancer:
+    """One controller shard (SCPB:147-332) backed by the MI355X engine."""
+
+    def __init__(self, managed_fraction: float = 0.9, blackbox_fraction: float = 0.1, min_memory_mb: int = 128,
+                 cluster_size: int = 1, device: int = 0, rng_seed: int = 0):
+        L = _lib.lib()
+        cfg = owgs_config(managed_fraction, blackbox_fraction, min_memory_mb * MB, cluster_size, device, rng_seed)
+        h = C.c_void_p()
+        rc = L.owgs_create(C.byref(cfg), C.byref(h))
+        if rc != 0:
+            raise OwgsError(rc, "owgs_create failed (is an MI355X visible?)")
+        self._h = h
+        self._L = L
+        self.rng_seed = rng_seed
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.owgs_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def _chk(self, rc: int) -> int:
+        if rc < 0:
+            raise OwgsError(rc, (self._L.owgs_last_error(self._h) or b"").decode())
+        return rc
+
+    # ------------------------------------------------------------------ state (SCPB:449-585)
+    def update_invokers(self, invokers: list[InvokerHealth]):
+        ids = np.array([i.id for i in invokers] or [0], dtype=np.int32)
+        mem = np.array([i.user_memory_bytes for i in invokers] or [0], dtype=np.int64)
+        st = np.array([i.status for i in invokers] or [0], dtype=np.uint8)
+        self._chk(self._L.owgs_update_invokers(self._h, len(invokers), _p(ids), _p(mem), _p(st)))
+
+    def update_invokers_arrays(self, ids, user_memory_bytes, status):
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        mem = np.ascontiguousarray(user_memory_bytes, dtype=np.int64)
+        st = np.ascontiguousarray(status, dtype=np.uint8)
+        self._chk(self._L.owgs_update_invokers(self._h, len(ids), _p(ids), _p(mem), _p(st)))
+
+    def update_cluster(self, new_size: int):
+        self._chk(self._L.owgs_update_cluster(self._h, new_size))
+
+    def _info(self):
+        v = [C.c_int32() for _ in range(4)]
+        self._chk(self._L.owgs_state_info(self._h, *[C.byref(x) for x in v]))
+        return [x.value for x in v]
+
+    @property
+    def cluster_size(self) -> int:
+        return self._info()[3]
+
+    @property
+    def managed_size(self) -> int:
+        return self._info()[1]
+
+    @property
+    def blackbox_size(self) -> int:
+        return self._info()[2]
+
+    def _steps(self, pool):
+        n = C.c_int32()
+        self._chk(self._L.owgs_step_sizes(self._h, pool, None, 0, C.byref(n)))
+        out = np.zeros(max(n.value, 1), dtype=np.int32)
+        self._chk(self._L.owgs_step_sizes(self._h, pool, _p(out), n.value, None))
+        return out[: n.value].tolist()
+
+    @property
+    def managed_step_sizes(self):
+        return self._steps(0)
+
+    @property
+    def blackbox_step_sizes(self):
+        return self._steps(1)
+
+    def permits(self) -> np.ndarray:
+        """availablePermits of every NestedSemaphore in invokerSlots."""
+        n = C.c_int32()
+        self._chk(self._L.owgs_read_permits(self._h, None, 0, C.byref(n)))
+        out = np.zeros(max(n.value, 1), dtype=np.int32)
+        self._chk(self._L.owgs_read_permits(self._h, _p(out), n.value, None))
+        return out[: n.value]
+
+    def concurrent_state(self, invoker: int, key: int):
+        """NestedSemaphore(invoker).concurrentState(key) -> (availablePermits, counter) or None."""
+        c, o = C.c_int32(), C.c_int32()
+        r = self._chk(self._L.owgs_read_concurrent(self._h, invoker, key, C.byref(c), C.byref(o)))
+        return (c.value, o.value) if r == 1 else None
+
+    def set_slots(self, permits):
+        p = np.ascontiguousarray(permits, dtype=np.int32)
+        self._chk(self._L.owgs_set_slots(self._h, len(p), _p(p) if len(p) else None))
+
+    def set_pool(self, pool: int, invokers: list[tuple[int, int]]):
+        ids = np.array([i for i, _ in invokers] or [0], dtype=np.int32)
+        st = np.array([s for _, s in invokers] or [0], dtype=np.uint8)
+        self._chk(self._L.owgs_set_pool(self._h, pool, len(invokers), _p(ids), _p(st)))
+
+    # ------------------------------------------------------------------ actions
+    def register_actions(self, actions: list[Action]) -> tuple[np.ndarray, np.ndarray]:
+        """Returns (action handles, generateHash values computed on the GPU)."""
+        n = len(actions)
+        nsb, nso = _pack([a.namespace for a in actions])
+        pb, po = _pack([a.path for a in actions])
+        kb, ko = _pack([a.key for a in actions])
+        mem = np.array([a.mem_mb for a in actions], dtype=np.int32)
+        mc = np.array([a.max_concurrent for a in actions], dtype=np.int32)
+        bb = np.array([1 if a.blackbox else 0 for a in actions], dtype=np.uint8)
+        out = np.zeros(max(n, 1), dtype=np.int32)
+        hs = np.zeros(max(n, 1), dtype=np.int32)
+        nsb_a = np.frombuffer(nsb or b"\0", dtype=np.uint8)
+        pb_a = np.frombuffer(pb or b"\0", dtype=np.uint8)
+        kb_a = np.frombuffer(kb or b"\0", dtype=np.uint8)
+        self._chk(self._L.owgs_register_actions(self._h, n, _p(nsb_a), _p(nso), _p(pb_a), _p(po), _p(kb_a), _p(ko),
+                                                _p(mem), _p(mc), _p(bb), _p(out), _p(hs)))
+        return out[:n], hs[:n]
+
+    def key_id(self, action: int) -> int:
+        return self._chk(self._L.owgs_key_id(self._h, action))
+
+    # ------------------------------------------------------------------ hot path
+    def publish(self, actions, seq=None, seq_base: int = 0) -> tuple[np.ndarray, np.ndarray]:
+        """Scheduling half of publish (SCPB:257-290) for each activation, in order.
+        Returns (invoker ids | NONE | THROW_INDEX, flags with bit0 = overload)."""
+        a = np.ascontiguousarray(actions, dtype=np.int32)
+        n = len(a)
+        out = np.zeros(max(n, 1), dtype=np.int32)
+        fl = np.zeros(max(n, 1), dtype=np.uint8)
+        sq = None if seq is None else np.ascontiguousarray(seq, dtype=np.uint64)
+        self._chk(self._L.owgs_publish_batch(self._h, n, _p(a), None if sq is None else _p(sq), seq_base, _p(out),
+                                             _p(fl)))
+        return out[:n], fl[:n]
+
+    def release_invoker(self, invokers, actions) -> np.ndarray:
+        """releaseInvoker (SCPB:327-331) per completion; returns release flags."""
+        inv = np.ascontiguousarray(invokers, dtype=np.int32)
+        a = np.ascontiguousarray(actions, dtype=np.int32)
+        fl = np.zeros(max(len(a), 1), dtype=np.uint8)
+        self._chk(self._L.owgs_release_batch(self._h, len(a), _p(inv), _p(a), _p(fl)))
+        return fl[: len(a)]
+
+    def schedule(self, max_concurrent, key, slots, index, step, pool=0, seq=None):
+        """ShardingContainerPoolBalancer.schedule(maxConcurrent, fqn, invokers(pool), dispatched, slots, index, step)
+        for arrays of calls (SCPB:398-436).  Scalars are broadcast.  Returns (ids, flags)."""
+        n = max(np.size(x) for x in (max_concurrent, key, slots, index, step, pool))
+        b = lambda x, dt: np.ascontiguousarray(np.broadcast_to(np.asarray(x, dtype=dt), (n,)))  # noqa: E731
+        pl, ix, st = b(pool, np.uint8), b(index, np.int32), b(step, np.int32)
+        mm, mc, ky = b(slots, np.int32), b(max_concurrent, np.int32), b(key, np.int32)
+        sq = None if seq is None else b(seq, np.uint64)
+        out = np.zeros(n, dtype=np.int32)
+        fl = np.zeros(n, dtype=np.uint8)
+        self._chk(self._L.owgs_schedule_walks(self._h, n, _p(pl), _p(ix), _p(st), _p(mm), _p(mc), _p(ky),
+                                              None if sq is None else _p(sq), _p(out), _p(fl)))
+        return out, fl
+
+    def replay(self, stream) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Replay a workload.Stream with host buffers."""
+        acq = np.ascontiguousarray(stream.acq_off, dtype=np.int64)
+        rel = np.ascontiguousarray(stream.rel_off, dtype=np.int64)
+        act = np.ascontiguousarray(stream.act, dtype=np.int32)
+        aid = np.ascontiguousarray(stream.rel_aid, dtype=np.int64)
+        n, nr = len(act), len(aid)
+        out = np.zeros(max(n, 1), dtype=np.int32)
+        fl = np.zeros(max(n, 1), dtype=np.uint8)
+        rf = np.zeros(max(nr, 1), dtype=np.uint8)
+        self._chk(self._L.owgs_replay(self._h, len(acq) - 1, _p(acq), _p(act), _p(rel), _p(aid if nr else
+                                      np.zeros(1, np.int64)), int(stream.seq_base), _p(out), _p(fl), _p(rf)))
+        return out[:n], fl[:n], rf[:nr]
+
+    def replay_device(self, n_batches, acq_off, act, rel_off, rel_aid, seq_base, out_inv, out_flags, rel_flags,
+                      stream=None):
+        """Replay with HBM-resident buffers given as device addresses (ints, e.g. torch tensor.data_ptr())."""
+        vp = lambda x: C.c_void_p(int(x)) if x else None  # noqa: E731
+        self._chk(self._L.owgs_replay_device(self._h, n_batches, vp(acq_off), vp(act), vp(rel_off), vp(rel_aid),
+                                             seq_base, vp(out_inv), vp(out_flags), vp(rel_flags), vp(stream)))
+
+    def snapshot(self):
+        self._chk(self._L.owgs_snapshot(self._h))
+
+    def restore(self, stream=None):
+        self._chk(self._L.owgs_restore(self._h, C.c_void_p(int(stream)) if stream else None))
+
+    def update_health_device(self, n: int, status_dev_ptr: int, stream=None):
+        self._chk(self._L.owgs_update_health_device(self._h, n, C.c_void_p(int(status_dev_ptr)),
+                                                    C.c_void_p(int(stream)) if stream else None))
+
+    def stats(self) -> dict:
+        out = (C.c_uint64 * 8)()
+        self._chk(self._L.owgs_read_stats(self._h, out, 8))
+        return {"iterations": out[0], "probes": out[1], "fallbacks": out[2], "long_walks": out[3],
+                "conflict_groups": out[4]}

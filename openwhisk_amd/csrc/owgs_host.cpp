@@ -1,0 +1,770 @@
+// owgs_host.cpp -- host runtime behind include/owgs.h.
+//
+// Holds the controller-shard structure that changes rarely (invoker list, managed/blackbox split, step sizes,
+// cluster size) and mirrors ShardingContainerPoolBalancerState (SCPB:449-585) line by line; everything touched per
+// activation (slot permits, concurrency maps, outputs) lives in HBM and is updated by the HIP engine
+// (owgs_kernels.hip).  No CPU fallback exists: without a HIP device every compute entry point fails.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/owgs.h"
+#include "owgs_internal.h"
+
+typedef unsigned long long u64;
+
+extern "C" hipError_t owgs_launch_hash(const OwgsHashArgs* a, hipStream_t s);
+extern "C" hipError_t owgs_launch_lookup(const OwgsLookupArgs* a, hipStream_t s);
+extern "C" hipError_t owgs_launch_prepare(const OwgsPrepArgs* a, hipStream_t s);
+extern "C" hipError_t owgs_launch_engine(const OwgsEngineArgs* a, hipStream_t s);
+extern "C" size_t owgs_engine_lds_bytes(int n_slots, int nm, int nb);
+
+namespace {
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t reserve(size_t m) {
+        if (m <= n && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        size_t bytes = (m ? m : 1) * sizeof(T);
+        hipError_t e = hipMalloc((void**)&p, bytes);
+        if (e == hipSuccess) n = m ? m : 1;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+int32_t d2i(double d) {  // Scala Double.toInt
+    if (d != d) return 0;
+    if (d >= 2147483647.0) return 2147483647;
+    if (d <= -2147483648.0) return (-2147483647 - 1);
+    return (int32_t)d;
+}
+
+int32_t gcd(int32_t a, int32_t b) {  // SCPB:375-376
+    while (b != 0) {
+        int32_t t = (b == -1) ? 0 : a % b;
+        a = b;
+        b = t;
+    }
+    return a;
+}
+
+std::vector<int32_t> pairwise_coprime(int32_t x) {  // SCPB:379-384
+    std::vector<int32_t> out;
+    for (int32_t cur = 1; cur <= x && cur > 0; ++cur) {
+        if (gcd(cur, x) != 1) continue;
+        bool ok = true;
+        for (int32_t v : out)
+            if (gcd(v, cur) != 1) {
+                ok = false;
+                break;
+            }
+        if (ok) out.push_back(cur);
+    }
+    return out;
+}
+
+constexpr uint32_t kCtabLog2 = 20;
+
+}  // namespace
+
+struct owgs_ctx {
+    owgs_config cfg{};
+    double mf = 0, bf = 0;
+    std::string err;
+    hipStream_t stream = nullptr;
+
+    // ShardingContainerPoolBalancerState mirror
+    std::vector<int32_t> ids;
+    std::vector<int64_t> mem;
+    std::vector<uint8_t> status;
+    int32_t managed = 0, blackboxes = 0;
+    std::vector<int32_t> msteps, bsteps;
+    int32_t cluster = 1;
+    int32_t n_slots = 0;
+    bool pool_override[2] = {false, false};
+    std::vector<int32_t> ov_ids[2];
+    std::vector<uint8_t> ov_status[2];
+
+    // derived pools
+    int32_t nm = 0, nb = 0, hm = 0, hb = 0, shortcut_ok = 3;
+
+    // actions
+    std::vector<int32_t> a_mem, a_maxc, a_slot, a_hash;
+    std::vector<uint8_t> a_bb;
+    std::unordered_map<std::string, int32_t> slot_ids;
+
+    // device
+    DevBuf<int32_t> d_permits, d_pool_words, d_hlist, d_act_slot, d_act_hash, d_act_mem, d_act_maxc, d_msteps,
+        d_bsteps, d_err;
+    DevBuf<uint8_t> d_act_bb;
+    DevBuf<int4> d_act_info;
+    DevBuf<u64> d_ctab_key, d_stats;
+    DevBuf<int2> d_ctab_val;
+    uint32_t ctab_mask = 0;
+    // scratch for host-buffer entry points
+    DevBuf<int64_t> d_off;
+    DevBuf<int32_t> d_a, d_b, d_out;
+    DevBuf<uint8_t> d_flags, d_rflags;
+    DevBuf<u64> d_seq;
+    DevBuf<int4> d_xw;
+    DevBuf<int64_t> d_rel;
+    // snapshot
+    DevBuf<int32_t> s_permits;
+    DevBuf<u64> s_ctab_key;
+    DevBuf<int2> s_ctab_val;
+    bool has_snap = false;
+    int32_t snap_slots = 0;
+
+    int fail(int code, const char* what, hipError_t e = hipSuccess) {
+        err = what;
+        if (e != hipSuccess) {
+            err += ": ";
+            err += hipGetErrorString(e);
+        }
+        return code;
+    }
+};
+
+#define HIPCHK(ctx, call)                                                     \
+    do {                                                                      \
+        hipError_t _e = (call);                                               \
+        if (_e != hipSuccess) return (ctx)->fail(OWGS_EDEVICE, #call, _e);    \
+    } while (0)
+
+static int32_t invoker_slot_mb(const owgs_ctx* c, int64_t mem_bytes) {  // SCPB:485-499, Size.scala:70,97-99
+    int64_t shard = mem_bytes / c->cluster;
+    if (shard < c->cfg.min_memory_bytes) shard = c->cfg.min_memory_bytes;
+    return (int32_t)(shard / 1024 / 1024);
+}
+
+template <class T>
+static hipError_t upload(DevBuf<T>& d, const T* h, size_t n, hipStream_t s) {
+    hipError_t e = d.reserve(n);
+    if (e != hipSuccess) return e;
+    if (n == 0) return hipSuccess;
+    return hipMemcpyAsync(d.p, h, n * sizeof(T), hipMemcpyHostToDevice, s);
+}
+
+// managed = take(managed), blackbox = takeRight(blackboxes) (SCPB:522-523) -> pool words, healthy lists
+static int rebuild_pools(owgs_ctx* c) {
+    std::vector<int32_t> words, hl;
+    int32_t cnt[2], hcnt[2];
+    c->shortcut_ok = 3;
+    for (int p = 0; p < 2; ++p) {
+        const int32_t* pid;
+        const uint8_t* pst;
+        int32_t n;
+        if (c->pool_override[p]) {
+            pid = c->ov_ids[p].data();
+            pst = c->ov_status[p].data();
+            n = (int32_t)c->ov_ids[p].size();
+        } else {
+            const int32_t N = (int32_t)c->ids.size();
+            const int32_t k = p == 0 ? std::min(c->managed, N) : std::min(c->blackboxes, N);
+            const int32_t base = p == 0 ? 0 : N - k;
+            pid = c->ids.data() + base;
+            pst = c->status.data() + base;
+            n = k;
+        }
+        cnt[p] = n;
+        hcnt[p] = 0;
+        for (int32_t i = 0; i < n; ++i) {
+            int32_t w = OWGS_PW_UNUSABLE;
+            if (pst[i] == OWGS_HEALTHY) {
+                w = (pid[i] >= 0 && pid[i] < c->n_slots) ? pid[i] : OWGS_PW_BADID;
+                if (w == OWGS_PW_BADID) c->shortcut_ok &= ~(1 << p);
+                hl.push_back(pid[i]);
+                hcnt[p]++;
+            }
+            words.push_back(w);
+        }
+    }
+    c->nm = cnt[0];
+    c->nb = cnt[1];
+    c->hm = hcnt[0];
+    c->hb = hcnt[1];
+    HIPCHK(c, upload(c->d_pool_words, words.data(), words.size(), c->stream));
+    HIPCHK(c, upload(c->d_hlist, hl.data(), hl.size(), c->stream));
+    return OWGS_OK;
+}
+
+static int prepare_actions(owgs_ctx* c) {
+    const int32_t n = (int32_t)c->a_mem.size();
+    if (n == 0) return OWGS_OK;
+    HIPCHK(c, upload(c->d_msteps, c->msteps.data(), c->msteps.size(), c->stream));
+    HIPCHK(c, upload(c->d_bsteps, c->bsteps.data(), c->bsteps.size(), c->stream));
+    HIPCHK(c, c->d_act_info.reserve(n));
+    OwgsPrepArgs a{};
+    a.hash = c->d_act_hash.p;
+    a.mem = c->d_act_mem.p;
+    a.maxc = c->d_act_maxc.p;
+    a.bb = c->d_act_bb.p;
+    a.n = n;
+    a.nm = c->nm;
+    a.nb = c->nb;
+    a.msteps = c->d_msteps.p;
+    a.n_msteps = (int32_t)c->msteps.size();
+    a.bsteps = c->d_bsteps.p;
+    a.n_bsteps = (int32_t)c->bsteps.size();
+    a.act_info = c->d_act_info.p;
+    HIPCHK(c, owgs_launch_prepare(&a, c->stream));
+    return OWGS_OK;
+}
+
+static int lds_check(owgs_ctx* c) {
+    if (owgs_engine_lds_bytes(c->n_slots, c->nm, c->nb) > OWGS_LDS_BYTES)
+        return c->fail(OWGS_ERANGE, "slot + pool state exceeds the engine's on-chip (LDS) capacity");
+    return OWGS_OK;
+}
+
+static int reset_ctab(owgs_ctx* c) {
+    HIPCHK(c, hipMemsetAsync(c->d_ctab_key.p, 0, c->d_ctab_key.n * sizeof(u64), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_ctab_val.p, 0, c->d_ctab_val.n * sizeof(int2), c->stream));
+    return OWGS_OK;
+}
+
+static void base_args(owgs_ctx* c, OwgsEngineArgs& A) {
+    memset(&A, 0, sizeof(A));
+    A.permits = c->d_permits.p;
+    A.n_slots = c->n_slots;
+    A.pool_words = c->d_pool_words.p;
+    A.nm = c->nm;
+    A.nb = c->nb;
+    A.hlist = c->d_hlist.p;
+    A.hm = c->hm;
+    A.hb = c->hb;
+    A.shortcut_ok = c->shortcut_ok;
+    A.act_info = c->d_act_info.p;
+    A.act_slot = c->d_act_slot.p;
+    A.ctab_key = c->d_ctab_key.p;
+    A.ctab_val = c->d_ctab_val.p;
+    A.ctab_mask = c->ctab_mask;
+    A.rng_seed = c->cfg.rng_seed;
+    A.stats = c->d_stats.p;
+    A.err = c->d_err.p;
+}
+
+static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s) {
+    int rc = lds_check(c);
+    if (rc) return rc;
+    HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, 8 * sizeof(u64), s));
+    HIPCHK(c, owgs_launch_engine(&A, s));
+    return OWGS_OK;
+}
+
+static int check_err_word(owgs_ctx* c) {
+    int32_t e = 0;
+    HIPCHK(c, hipMemcpy(&e, c->d_err.p, sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (e) {
+        HIPCHK(c, hipMemset(c->d_err.p, 0, sizeof(int32_t)));
+        return c->fail(OWGS_ENOMEM, "concurrency table full");
+    }
+    return OWGS_OK;
+}
+
+extern "C" {
+
+int owgs_abi_version(void) { return OWGS_ABI_VERSION; }
+
+int owgs_limits(int32_t* max_invokers, int32_t* max_slots) {
+    const int32_t words = OWGS_LDS_BYTES / 4 - 2 * OWGS_STAMP_BUCKETS - 8;
+    if (max_invokers) *max_invokers = words / 2;
+    if (max_slots) *max_slots = words / 2;
+    return OWGS_OK;
+}
+
+int owgs_create(const owgs_config* cfg, owgs_ctx** out) {
+    if (!cfg || !out) return OWGS_EINVAL;
+    *out = nullptr;
+    owgs_ctx* c = new (std::nothrow) owgs_ctx();
+    if (!c) return OWGS_ENOMEM;
+    c->cfg = *cfg;
+    // SCPB:467-468
+    c->mf = std::max(0.0, std::min(1.0, cfg->managed_fraction));
+    c->bf = std::max(1.0 - c->mf, std::min(1.0, cfg->blackbox_fraction));
+    c->cluster = 1;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0 || cfg->device < 0 || cfg->device >= ndev) {
+        delete c;
+        return OWGS_EDEVICE;
+    }
+    if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return OWGS_EDEVICE;
+    }
+    const size_t cap = (size_t)1 << kCtabLog2;
+    if (c->d_ctab_key.reserve(cap) || c->d_ctab_val.reserve(cap) || c->d_stats.reserve(8) || c->d_err.reserve(1) ||
+        c->d_permits.reserve(1)) {
+        owgs_destroy(c);
+        return OWGS_ENOMEM;
+    }
+    c->ctab_mask = (uint32_t)(cap - 1);
+    if (reset_ctab(c) || hipMemset(c->d_err.p, 0, sizeof(int32_t)) != hipSuccess) {
+        owgs_destroy(c);
+        return OWGS_EDEVICE;
+    }
+    c->msteps = pairwise_coprime(0);
+    c->bsteps = pairwise_coprime(0);
+    int rc = rebuild_pools(c);
+    if (rc) {
+        owgs_destroy(c);
+        return rc;
+    }
+    if (cfg->cluster_size > 1) owgs_update_cluster(c, cfg->cluster_size);
+    (void)hipStreamSynchronize(c->stream);
+    *out = c;
+    return OWGS_OK;
+}
+
+void owgs_destroy(owgs_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->cfg.device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    DevBuf<int32_t>* i32s[] = {&c->d_permits, &c->d_pool_words, &c->d_hlist, &c->d_act_slot, &c->d_act_hash,
+                               &c->d_act_mem, &c->d_act_maxc, &c->d_msteps, &c->d_bsteps, &c->d_err, &c->d_a,
+                               &c->d_b, &c->d_out, &c->s_permits};
+    for (auto* b : i32s) b->release();
+    c->d_act_bb.release();
+    c->d_act_info.release();
+    c->d_ctab_key.release();
+    c->d_stats.release();
+    c->d_ctab_val.release();
+    c->d_off.release();
+    c->d_flags.release();
+    c->d_rflags.release();
+    c->d_seq.release();
+    c->d_xw.release();
+    c->d_rel.release();
+    c->s_ctab_key.release();
+    c->s_ctab_val.release();
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* owgs_last_error(const owgs_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+// SCPB:512-551
+int owgs_update_invokers(owgs_ctx* c, int32_t n, const int32_t* ids, const int64_t* user_memory_bytes,
+                         const uint8_t* status) {
+    if (!c || n < 0 || (n > 0 && (!ids || !user_memory_bytes || !status))) return OWGS_EINVAL;
+    (void)hipSetDevice(c->cfg.device);
+    const int32_t old_size = (int32_t)c->ids.size();
+    const int32_t new_size = n;
+    int32_t managed = d2i(std::ceil((double)new_size * c->mf));
+    if (managed < 1) managed = 1;
+    int32_t blackboxes = d2i(std::floor((double)new_size * c->bf));
+    if (blackboxes < 1) blackboxes = 1;
+    c->ids.assign(ids, ids + n);
+    c->mem.assign(user_memory_bytes, user_memory_bytes + n);
+    c->status.assign(status, status + n);
+    c->managed = managed;
+    c->blackboxes = blackboxes;
+    c->pool_override[0] = c->pool_override[1] = false;
+    if (old_size != new_size) {
+        c->msteps = pairwise_coprime(managed);
+        c->bsteps = pairwise_coprime(blackboxes);
+        if (old_size < new_size && n > c->n_slots) {
+            // keep existing semaphores; append NestedSemaphore(getInvokerSlot(userMemory).toMB) for new ones
+            std::vector<int32_t> tail;
+            for (int32_t i = c->n_slots; i < n; ++i) tail.push_back(invoker_slot_mb(c, c->mem[i]));
+            DevBuf<int32_t> nb;
+            HIPCHK(c, nb.reserve((size_t)n));
+            if (c->n_slots > 0)
+                HIPCHK(c, hipMemcpyAsync(nb.p, c->d_permits.p, (size_t)c->n_slots * 4, hipMemcpyDeviceToDevice, c->stream));
+            HIPCHK(c, hipMemcpyAsync(nb.p + c->n_slots, tail.data(), tail.size() * 4, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            c->d_permits.release();
+            c->d_permits = nb;
+            nb.p = nullptr;
+            c->n_slots = n;
+        }
+    }
+    int rc = rebuild_pools(c);
+    if (!rc) rc = prepare_actions(c);
+    if (!rc) HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (!rc) rc = lds_check(c);
+    return rc;
+}
+
+// SCPB:561-584
+int owgs_update_cluster(owgs_ctx* c, int32_t new_size) {
+    if (!c) return OWGS_EINVAL;
+    (void)hipSetDevice(c->cfg.device);
+    const int32_t actual = new_size > 1 ? new_size : 1;
+    if (c->cluster == actual) return OWGS_OK;
+    c->cluster = actual;
+    const int32_t n = (int32_t)c->ids.size();
+    std::vector<int32_t> p(n);
+    for (int32_t i = 0; i < n; ++i) p[i] = invoker_slot_mb(c, c->mem[i]);
+    HIPCHK(c, upload(c->d_permits, p.data(), p.size(), c->stream));
+    c->n_slots = n;
+    int rc = reset_ctab(c);
+    if (!rc) rc = rebuild_pools(c);
+    if (!rc) HIPCHK(c, hipStreamSynchronize(c->stream));
+    return rc;
+}
+
+int owgs_register_actions(owgs_ctx* c, int32_t n, const char* ns_bytes, const int32_t* ns_off,
+                          const char* path_bytes, const int32_t* path_off, const char* key_bytes,
+                          const int32_t* key_off, const int32_t* mem_mb, const int32_t* max_conc,
+                          const uint8_t* blackbox, int32_t* out_action, int32_t* out_hash) {
+    if (!c || n < 0) return OWGS_EINVAL;
+    if (n == 0) return OWGS_OK;
+    if (!ns_off || !path_off || !key_off || !mem_mb || !max_conc || !blackbox || !key_bytes || !out_action)
+        return OWGS_EINVAL;
+    for (int32_t i = 0; i < n; ++i) {
+        // MemoryLimit/ConcurrencyLimit guarantee positive values (MemoryLimit.scala:68-69); the reference's
+        // require(...) checks (FS:96, NS:85) would throw on anything else
+        if (mem_mb[i] <= 0 || max_conc[i] < 1 || max_conc[i] > OWGS_META_MAXC_MASK) return c->fail(OWGS_EINVAL, "mem/maxConcurrent");
+        if (ns_off[i + 1] < ns_off[i] || path_off[i + 1] < path_off[i] || key_off[i + 1] < key_off[i])
+            return c->fail(OWGS_EINVAL, "offsets");
+    }
+    (void)hipSetDevice(c->cfg.device);
+    const int32_t base = (int32_t)c->a_mem.size();
+    for (int32_t i = 0; i < n; ++i) {
+        std::string k(key_bytes + key_off[i], (size_t)(key_off[i + 1] - key_off[i]));
+        auto it = c->slot_ids.find(k);
+        int32_t sid;
+        if (it == c->slot_ids.end()) {
+            sid = (int32_t)c->slot_ids.size();
+            c->slot_ids.emplace(std::move(k), sid);
+        } else {
+            sid = it->second;
+        }
+        c->a_slot.push_back(sid);
+        c->a_mem.push_back(mem_mb[i]);
+        c->a_maxc.push_back(max_conc[i]);
+        c->a_bb.push_back(blackbox[i] ? 1 : 0);
+        out_action[i] = base + i;
+    }
+    const int32_t total = (int32_t)c->a_mem.size();
+    // strings -> device, hash on the GPU
+    DevBuf<char> dns, dpath;
+    DevBuf<int32_t> dnso, dpo, dh;
+    const size_t nsb = (size_t)ns_off[n], pb = (size_t)path_off[n];
+    HIPCHK(c, upload(dns, ns_bytes, nsb, c->stream));
+    HIPCHK(c, upload(dpath, path_bytes, pb, c->stream));
+    HIPCHK(c, upload(dnso, ns_off, (size_t)n + 1, c->stream));
+    HIPCHK(c, upload(dpo, path_off, (size_t)n + 1, c->stream));
+    HIPCHK(c, dh.reserve((size_t)n));
+    OwgsHashArgs ha{dns.p, dnso.p, dpath.p, dpo.p, n, 0, dh.p};
+    HIPCHK(c, owgs_launch_hash(&ha, c->stream));
+    std::vector<int32_t> h(n);
+    HIPCHK(c, hipMemcpyAsync(h.data(), dh.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    dns.release();
+    dpath.release();
+    dnso.release();
+    dpo.release();
+    dh.release();
+    for (int32_t i = 0; i < n; ++i) {
+        c->a_hash.push_back(h[i]);
+        if (out_hash) out_hash[i] = h[i];
+    }
+    HIPCHK(c, upload(c->d_act_hash, c->a_hash.data(), (size_t)total, c->stream));
+    HIPCHK(c, upload(c->d_act_slot, c->a_slot.data(), (size_t)total, c->stream));
+    HIPCHK(c, upload(c->d_act_mem, c->a_mem.data(), (size_t)total, c->stream));
+    HIPCHK(c, upload(c->d_act_maxc, c->a_maxc.data(), (size_t)total, c->stream));
+    HIPCHK(c, upload(c->d_act_bb, c->a_bb.data(), (size_t)total, c->stream));
+    int rc = prepare_actions(c);
+    if (!rc) HIPCHK(c, hipStreamSynchronize(c->stream));
+    return rc;
+}
+
+int owgs_publish_batch(owgs_ctx* c, int32_t n, const int32_t* action, const uint64_t* seq, uint64_t seq_base,
+                       int32_t* out_invoker, uint8_t* out_flags) {
+    if (!c || n < 0 || (n > 0 && (!action || !out_invoker || !out_flags))) return OWGS_EINVAL;
+    if (n == 0) return OWGS_OK;
+    const int32_t na = (int32_t)c->a_mem.size();
+    for (int32_t i = 0; i < n; ++i)
+        if (action[i] < 0 || action[i] >= na) return c->fail(OWGS_ENOENT, "unknown action");
+    (void)hipSetDevice(c->cfg.device);
+    const int64_t off[2] = {0, n};
+    HIPCHK(c, upload(c->d_off, off, 2, c->stream));
+    HIPCHK(c, upload(c->d_a, action, (size_t)n, c->stream));
+    if (seq) HIPCHK(c, upload(c->d_seq, (const u64*)seq, (size_t)n, c->stream));
+    HIPCHK(c, c->d_out.reserve((size_t)n));
+    HIPCHK(c, c->d_flags.reserve((size_t)n));
+    OwgsEngineArgs A;
+    base_args(c, A);
+    A.n_batches = 1;
+    A.acq_off = c->d_off.p;
+    A.act = c->d_a.p;
+    A.seq_base = seq_base;
+    A.seq = seq ? c->d_seq.p : nullptr;
+    A.out_inv = c->d_out.p;
+    A.out_flags = c->d_flags.p;
+    int rc = run_engine(c, A, c->stream);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(out_invoker, c->d_out.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out_flags, c->d_flags.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return check_err_word(c);
+}
+
+int owgs_release_batch(owgs_ctx* c, int32_t n, const int32_t* invoker, const int32_t* action, uint8_t* out_flags) {
+    if (!c || n < 0 || (n > 0 && (!invoker || !action))) return OWGS_EINVAL;
+    if (n == 0) return OWGS_OK;
+    const int32_t na = (int32_t)c->a_mem.size();
+    for (int32_t i = 0; i < n; ++i)
+        if (action[i] < 0 || action[i] >= na) return c->fail(OWGS_ENOENT, "unknown action");
+    (void)hipSetDevice(c->cfg.device);
+    const int64_t off[4] = {0, 0, 0, n};  // acq_off = {0,0}, rel_off = {0,n}
+    HIPCHK(c, upload(c->d_off, off, 4, c->stream));
+    HIPCHK(c, upload(c->d_a, invoker, (size_t)n, c->stream));
+    HIPCHK(c, upload(c->d_b, action, (size_t)n, c->stream));
+    HIPCHK(c, c->d_rflags.reserve((size_t)n));
+    OwgsEngineArgs A;
+    base_args(c, A);
+    A.n_batches = 1;
+    A.acq_off = c->d_off.p;
+    A.rel_off = c->d_off.p + 2;
+    A.rel_inv = c->d_a.p;
+    A.rel_act = c->d_b.p;
+    A.rel_flags = c->d_rflags.p;
+    int rc = run_engine(c, A, c->stream);
+    if (rc) return rc;
+    if (out_flags)
+        HIPCHK(c, hipMemcpyAsync(out_flags, c->d_rflags.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return check_err_word(c);
+}
+
+int owgs_schedule_walks(owgs_ctx* c, int32_t n, const uint8_t* pool, const int32_t* index, const int32_t* step,
+                        const int32_t* mem_mb, const int32_t* max_conc, const int32_t* key, const uint64_t* seq,
+                        int32_t* out_invoker, uint8_t* out_flags) {
+    if (!c || n < 0 || (n > 0 && (!pool || !index || !step || !mem_mb || !max_conc || !key || !out_invoker || !out_flags)))
+        return OWGS_EINVAL;
+    if (n == 0) return OWGS_OK;
+    std::vector<int4> xw(n);
+    for (int32_t i = 0; i < n; ++i) {
+        if (mem_mb[i] <= 0 || max_conc[i] < 1 || max_conc[i] > OWGS_META_MAXC_MASK || step[i] < 0 || step[i] > (1 << 30))
+            return c->fail(OWGS_EINVAL, "mem/maxConcurrent/step");
+        const int p = pool[i] ? 1 : 0;
+        const int32_t np = p ? c->nb : c->nm;
+        uint32_t meta = (uint32_t)max_conc[i] | ((uint32_t)p << OWGS_META_POOL_SHIFT);
+        if (np == 0) meta |= OWGS_META_EMPTY;
+        else if (index[i] < 0 || index[i] >= np) meta |= OWGS_META_THROW;
+        xw[i] = make_int4(index[i], step[i], mem_mb[i], (int)meta);
+    }
+    (void)hipSetDevice(c->cfg.device);
+    const int64_t off[2] = {0, n};
+    HIPCHK(c, upload(c->d_off, off, 2, c->stream));
+    HIPCHK(c, upload(c->d_xw, xw.data(), (size_t)n, c->stream));
+    HIPCHK(c, upload(c->d_b, key, (size_t)n, c->stream));
+    if (seq) HIPCHK(c, upload(c->d_seq, (const u64*)seq, (size_t)n, c->stream));
+    HIPCHK(c, c->d_out.reserve((size_t)n));
+    HIPCHK(c, c->d_flags.reserve((size_t)n));
+    OwgsEngineArgs A;
+    base_args(c, A);
+    A.n_batches = 1;
+    A.acq_off = c->d_off.p;
+    A.xw_info = c->d_xw.p;
+    A.xw_slot = c->d_b.p;
+    A.seq = seq ? c->d_seq.p : nullptr;
+    A.out_inv = c->d_out.p;
+    A.out_flags = c->d_flags.p;
+    int rc = run_engine(c, A, c->stream);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(out_invoker, c->d_out.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out_flags, c->d_flags.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return check_err_word(c);
+}
+
+int owgs_set_slots(owgs_ctx* c, int32_t n, const int32_t* permits) {
+    if (!c || n < 0 || (n > 0 && !permits)) return OWGS_EINVAL;
+    (void)hipSetDevice(c->cfg.device);
+    HIPCHK(c, upload(c->d_permits, permits, (size_t)n, c->stream));
+    c->n_slots = n;
+    int rc = reset_ctab(c);
+    if (!rc) rc = rebuild_pools(c);
+    if (!rc) HIPCHK(c, hipStreamSynchronize(c->stream));
+    return rc;
+}
+
+int owgs_set_pool(owgs_ctx* c, int32_t pool, int32_t n, const int32_t* ids, const uint8_t* status) {
+    if (!c || (pool != 0 && pool != 1) || n < 0 || (n > 0 && (!ids || !status))) return OWGS_EINVAL;
+    (void)hipSetDevice(c->cfg.device);
+    c->pool_override[pool] = true;
+    c->ov_ids[pool].assign(ids, ids + n);
+    c->ov_status[pool].assign(status, status + n);
+    int rc = rebuild_pools(c);
+    if (!rc) rc = prepare_actions(c);
+    if (!rc) HIPCHK(c, hipStreamSynchronize(c->stream));
+    return rc;
+}
+
+int owgs_read_permits(owgs_ctx* c, int32_t* out, int32_t cap, int32_t* n_slots) {
+    if (!c) return OWGS_EINVAL;
+    if (n_slots) *n_slots = c->n_slots;
+    if (!out || cap <= 0 || c->n_slots == 0) return OWGS_OK;
+    (void)hipSetDevice(c->cfg.device);
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(out, c->d_permits.p, (size_t)std::min(cap, c->n_slots) * 4, hipMemcpyDeviceToHost));
+    return OWGS_OK;
+}
+
+int owgs_read_concurrent(owgs_ctx* c, int32_t invoker, int32_t key, int32_t* permits, int32_t* op_count) {
+    if (!c) return OWGS_EINVAL;
+    (void)hipSetDevice(c->cfg.device);
+    DevBuf<int32_t> di, dk;
+    DevBuf<int2> dv;
+    HIPCHK(c, upload(di, &invoker, 1, c->stream));
+    HIPCHK(c, upload(dk, &key, 1, c->stream));
+    HIPCHK(c, dv.reserve(1));
+    OwgsLookupArgs la{c->d_ctab_key.p, c->d_ctab_val.p, c->ctab_mask, di.p, dk.p, 1, dv.p};
+    HIPCHK(c, owgs_launch_lookup(&la, c->stream));
+    int2 v;
+    HIPCHK(c, hipMemcpyAsync(&v, dv.p, sizeof(int2), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    di.release();
+    dk.release();
+    dv.release();
+    if (v.y <= 0) return 0;  // absent (NestedSemaphore.concurrentState has no entry)
+    if (permits) *permits = v.x;
+    if (op_count) *op_count = v.y;
+    return 1;
+}
+
+int owgs_key_id(owgs_ctx* c, int32_t action) {
+    if (!c || action < 0 || action >= (int32_t)c->a_slot.size()) return OWGS_ENOENT;
+    return c->a_slot[action];
+}
+
+int owgs_state_info(owgs_ctx* c, int32_t* n_invokers, int32_t* managed, int32_t* blackbox, int32_t* cluster_size) {
+    if (!c) return OWGS_EINVAL;
+    if (n_invokers) *n_invokers = (int32_t)c->ids.size();
+    if (managed) *managed = c->nm;
+    if (blackbox) *blackbox = c->nb;
+    if (cluster_size) *cluster_size = c->cluster;
+    return OWGS_OK;
+}
+
+int owgs_step_sizes(owgs_ctx* c, int32_t pool, int32_t* out, int32_t cap, int32_t* n) {
+    if (!c || (pool != 0 && pool != 1)) return OWGS_EINVAL;
+    const std::vector<int32_t>& v = pool ? c->bsteps : c->msteps;
+    if (n) *n = (int32_t)v.size();
+    for (int32_t i = 0; out && i < cap && i < (int32_t)v.size(); ++i) out[i] = v[i];
+    return OWGS_OK;
+}
+
+int owgs_replay_device(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const int32_t* act,
+                       const int64_t* rel_off, const int64_t* rel_aid, uint64_t seq_base, int32_t* out_invoker,
+                       uint8_t* out_flags, uint8_t* rel_flags, void* stream) {
+    if (!c || n_batches < 0 || !acq_off || !act || !out_invoker || !out_flags) return OWGS_EINVAL;
+    if (n_batches == 0) return OWGS_OK;
+    (void)hipSetDevice(c->cfg.device);
+    OwgsEngineArgs A;
+    base_args(c, A);
+    A.n_batches = n_batches;
+    A.acq_off = acq_off;
+    A.act = act;
+    A.rel_off = rel_off;
+    A.rel_aid = rel_aid;
+    A.seq_base = seq_base;
+    A.out_inv = out_invoker;
+    A.out_flags = out_flags;
+    A.rel_flags = rel_flags;
+    return run_engine(c, A, stream ? (hipStream_t)stream : c->stream);
+}
+
+int owgs_replay(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const int32_t* act, const int64_t* rel_off,
+                const int64_t* rel_aid, uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags,
+                uint8_t* rel_flags) {
+    if (!c || n_batches < 0 || !acq_off || !act || !out_invoker || !out_flags || !rel_off) return OWGS_EINVAL;
+    if (n_batches == 0) return OWGS_OK;
+    (void)hipSetDevice(c->cfg.device);
+    const int64_t n_act = acq_off[n_batches], n_rel = rel_off[n_batches];
+    const int32_t na = (int32_t)c->a_mem.size();
+    for (int64_t i = 0; i < n_act; ++i)
+        if (act[i] < 0 || act[i] >= na) return c->fail(OWGS_ENOENT, "unknown action");
+    for (int64_t r = 0; r < n_rel; ++r)
+        if (rel_aid[r] < 0 || rel_aid[r] >= n_act) return c->fail(OWGS_EINVAL, "release id outside the stream");
+    std::vector<int64_t> offs((size_t)2 * (n_batches + 1));
+    memcpy(offs.data(), acq_off, (size_t)(n_batches + 1) * 8);
+    memcpy(offs.data() + n_batches + 1, rel_off, (size_t)(n_batches + 1) * 8);
+    HIPCHK(c, upload(c->d_off, offs.data(), offs.size(), c->stream));
+    HIPCHK(c, upload(c->d_a, act, (size_t)n_act, c->stream));
+    HIPCHK(c, upload(c->d_rel, rel_aid, (size_t)n_rel, c->stream));
+    HIPCHK(c, c->d_out.reserve((size_t)n_act));
+    HIPCHK(c, c->d_flags.reserve((size_t)n_act));
+    HIPCHK(c, c->d_rflags.reserve((size_t)n_rel));
+    int rc = owgs_replay_device(c, n_batches, c->d_off.p, c->d_a.p, c->d_off.p + n_batches + 1, c->d_rel.p, seq_base,
+                                c->d_out.p, c->d_flags.p, c->d_rflags.p, nullptr);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(out_invoker, c->d_out.p, (size_t)n_act * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out_flags, c->d_flags.p, (size_t)n_act, hipMemcpyDeviceToHost, c->stream));
+    if (rel_flags && n_rel)
+        HIPCHK(c, hipMemcpyAsync(rel_flags, c->d_rflags.p, (size_t)n_rel, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return check_err_word(c);
+}
+
+int owgs_snapshot(owgs_ctx* c) {
+    if (!c) return OWGS_EINVAL;
+    (void)hipSetDevice(c->cfg.device);
+    HIPCHK(c, c->s_permits.reserve((size_t)std::max(c->n_slots, 1)));
+    HIPCHK(c, c->s_ctab_key.reserve(c->d_ctab_key.n));
+    HIPCHK(c, c->s_ctab_val.reserve(c->d_ctab_val.n));
+    if (c->n_slots)
+        HIPCHK(c, hipMemcpyAsync(c->s_permits.p, c->d_permits.p, (size_t)c->n_slots * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->s_ctab_key.p, c->d_ctab_key.p, c->d_ctab_key.n * 8, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->s_ctab_val.p, c->d_ctab_val.p, c->d_ctab_val.n * 8, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->has_snap = true;
+    c->snap_slots = c->n_slots;
+    return OWGS_OK;
+}
+
+int owgs_restore(owgs_ctx* c, void* stream) {
+    if (!c || !c->has_snap || c->snap_slots != c->n_slots) return OWGS_EINVAL;
+    (void)hipSetDevice(c->cfg.device);
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (c->n_slots)
+        HIPCHK(c, hipMemcpyAsync(c->d_permits.p, c->s_permits.p, (size_t)c->n_slots * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->d_ctab_key.p, c->s_ctab_key.p, c->d_ctab_key.n * 8, hipMemcpyDeviceToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->d_ctab_val.p, c->s_ctab_val.p, c->d_ctab_val.n * 8, hipMemcpyDeviceToDevice, s));
+    return OWGS_OK;
+}
+
+int owgs_update_health_device(owgs_ctx* c, int32_t n, const uint8_t* status_dev, void* stream) {
+    if (!c || n != (int32_t)c->status.size() || (n > 0 && !status_dev)) return OWGS_EINVAL;
+    (void)hipSetDevice(c->cfg.device);
+    if (n) {
+        HIPCHK(c, hipMemcpyAsync(c->status.data(), status_dev, (size_t)n, hipMemcpyDeviceToHost,
+                                 stream ? (hipStream_t)stream : c->stream));
+        HIPCHK(c, hipStreamSynchronize(stream ? (hipStream_t)stream : c->stream));
+    }
+    int rc = rebuild_pools(c);
+    if (!rc) HIPCHK(c, hipStreamSynchronize(c->stream));
+    return rc;
+}
+
+int owgs_read_stats(owgs_ctx* c, uint64_t* out, int32_t cap) {
+    if (!c || !out) return OWGS_EINVAL;
+    (void)hipSetDevice(c->cfg.device);
+    u64 v[8];
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipMemcpy(v, c->d_stats.p, sizeof(v), hipMemcpyDeviceToHost));
+    for (int32_t i = 0; i < cap && i < 8; ++i) out[i] = v[i];
+    return OWGS_OK;
+}
+
+}  // extern "C"

@@ -334,3 +334,17 @@ class BalancerState:
         lib().owo_replay(self.h, len(acq_off) - 1, _ptr(acq_off), _ptr(act), _ptr(rel_off), _ptr(rel),
                          int(stream.seq_base), _ptr(out), _ptr(fl), _ptr(rf))
         return out[:n], fl[:n], rf[: len(stream.rel_aid)]
+
+
+def state_for(workload, zombies: bool = True, slot_keys: dict | None = None) -> BalancerState:
+    """Oracle BalancerState set up like the workload (invokers, cluster size, actions); returns the state.
+    Slot keys are interned from action.key (fqn@version) exactly as owgs_register_actions does."""
+    st = BalancerState(workload.managed_fraction, workload.blackbox_fraction, rng_seed=workload.rng_seed,
+                       zombies=zombies)
+    st.update_invokers(workload.inv_ids, workload.inv_mem, workload.inv_status)
+    st.update_cluster(workload.cluster_size)
+    keys = {} if slot_keys is None else slot_keys
+    for a in workload.actions:
+        k = keys.setdefault(a.key, len(keys))
+        st.register_action(a.namespace, a.path, k, a.mem_mb, a.max_concurrent, a.blackbox)
+    return st

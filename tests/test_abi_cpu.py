@@ -1,0 +1,78 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library loads and exports every symbol include/owgs.h declares,
+and refuses to run without a GPU (no silent CPU fallback).  No compute calls."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import openwhisk_amd as ow
+from openwhisk_amd import _lib
+from openwhisk_amd import workload as W
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not os.path.exists(_lib.LIB_PATH):
+        _lib.build()
+    return _lib.lib()
+
+
+def test_header_declares_the_boundary():
+    fns = ow.header_functions()
+    for required in ["owgs_create", "owgs_destroy", "owgs_update_invokers", "owgs_update_cluster",
+                     "owgs_register_actions", "owgs_publish_batch", "owgs_release_batch", "owgs_schedule_walks",
+                     "owgs_replay_device", "owgs_last_error"]:
+        assert required in fns
+
+
+def test_library_exports_every_header_symbol(L):
+    missing = [f for f in ow.header_functions() if not hasattr(L, f)]
+    assert not missing, missing
+
+
+def test_abi_version_and_limits(L):
+    assert L.owgs_abi_version() == 1
+    mi, ms = C.c_int32(), C.c_int32()
+    assert L.owgs_limits(C.byref(mi), C.byref(ms)) == 0
+    assert mi.value >= 10_000 and ms.value >= 10_000  # BASELINE: 10k invokers fit on chip
+
+
+def test_no_cpu_fallback_without_gpu(L):
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("GPU present")
+    except ImportError:
+        pass
+    with pytest.raises(ow.OwgsError):
+        ow.GpuShardingContainerPoolBalancer()
+
+
+def test_null_arguments_are_rejected_not_crashing(L):
+    assert L.owgs_create(None, None) == _lib.EINVAL
+    assert L.owgs_update_cluster(None, 2) == _lib.EINVAL
+    assert L.owgs_publish_batch(None, 0, None, None, 0, None, None) == _lib.EINVAL
+    assert L.owgs_last_error(None) == b"null context"
+
+
+def test_workload_streams_are_well_formed():
+    for name in ["c1", "c2", "c3", "c4", "headline"]:
+        w = W.config(name, n_activations=20_000)
+        s = w.stream
+        n = len(s.act)
+        assert s.acq_off[0] == 0 and s.acq_off[-1] == n and np.all(np.diff(s.acq_off) >= 0)
+        assert s.rel_off[0] == 0 and s.rel_off[-1] == len(s.rel_aid) and np.all(np.diff(s.rel_off) >= 0)
+        assert s.act.min() >= 0 and s.act.max() < len(w.actions)
+        # releases only reference activations of strictly earlier batches
+        for b in range(s.n_batches):
+            r = s.rel_aid[s.rel_off[b]:s.rel_off[b + 1]]
+            assert np.all(r < s.acq_off[b])
+        assert len(np.unique(s.rel_aid)) == len(s.rel_aid)
+
+
+def test_workload_is_deterministic():
+    a = W.config("headline", n_activations=5000)
+    b = W.config("headline", n_activations=5000)
+    assert np.array_equal(a.stream.act, b.stream.act) and np.array_equal(a.stream.rel_aid, b.stream.rel_aid)
+    assert a.actions == b.actions

@@ -1,0 +1,248 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU oracle and the reference's golden vectors.
+
+Bar: bit-exact assignment vectors, overload flags, release flags and final slot state.  Run on an MI355X
+(pytest -m gpu).  All cases run in this one process.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from openwhisk_amd import GpuShardingContainerPoolBalancer, InvokerHealth
+from openwhisk_amd import workload as W
+from openwhisk_amd.balancer import Action, HEALTHY, NONE, OFFLINE, THROW_INDEX, UNHEALTHY
+
+pytestmark = pytest.mark.gpu
+MB = 1024 * 1024
+ST = {"healthy": HEALTHY, "unhealthy": UNHEALTHY, "offline": OFFLINE}
+
+
+def gpu(**kw):
+    return GpuShardingContainerPoolBalancer(**kw)
+
+
+# ----------------------------------------------------------------------------------------------- hashing
+def test_generate_hash_on_gpu_matches_jls():
+    names = [("invocationSpace", "testspace/testname"), ("", "polygenelubricants"), ("a", "b"), ("ns", "x" * 300),
+             ("guest", "guest/pkg/act"), ("Aa", "BB")]
+    b = gpu()
+    acts = [Action(ns, p, "0.0.1", 256) for ns, p in names]
+    _, h = b.register_actions(acts)
+    assert h.tolist() == [O.generate_hash(ns, p) for ns, p in names]
+    assert h[1] == -2**31  # Int.MinValue.abs stays negative (SCPB:371)
+    w = W.config("headline", n_activations=10)
+    b2 = gpu()
+    _, h2 = b2.register_actions(w.actions)
+    assert h2.tolist() == [O.generate_hash(a.namespace, a.path) for a in w.actions]
+
+
+# ----------------------------------------------------------------------------------------------- schedule goldens
+@pytest.mark.parametrize("name", ["schedule_empty_invokers", "schedule_no_healthy", "schedule_step_then_overload",
+                                  "schedule_ignore_unhealthy_offline", "schedule_enough_free_slots",
+                                  "schedule_concurrent_actions"])
+def test_schedule_golden(golden, name):
+    c = golden[name]
+    b = gpu(rng_seed=99)
+    b.set_slots([c["slots"]["permits"]] * c["slots"]["count"])
+    b.set_pool(0, [(i, ST[s]) for i, s in c["invokers"]])
+    key = 7
+    # one call per batch element; the whole sequence is a single batch with sequential semantics
+    calls = c["calls"]
+    ids, fl = b.schedule(c["max_concurrent"], key, [x["mem"] for x in calls], [x["index"] for x in calls],
+                         [x["step"] for x in calls], seq=np.arange(len(calls)))
+    for k, call in enumerate(calls):
+        exp = call["expect"]
+        if exp is None:
+            assert ids[k] == NONE
+        else:
+            assert [ids[k], bool(fl[k] & 1)] == exp
+    # concurrency expectations are checked call by call
+    if any("concurrent_permits_after" in x for x in calls):
+        b2 = gpu()
+        b2.set_slots([c["slots"]["permits"]] * c["slots"]["count"])
+        b2.set_pool(0, [(i, ST[s]) for i, s in c["invokers"]])
+        for call in calls:
+            i2, _ = b2.schedule(c["max_concurrent"], key, call["mem"], call["index"], call["step"])
+            cp = call["concurrent_permits_after"]
+            assert i2[0] == call["expect"][0]
+            assert b2.concurrent_state(cp["invoker"], key)[0] == cp["permits"]
+    if "then_overload" in c:
+        t = c["then_overload"]
+        r, f = b.schedule(c["max_concurrent"], key, t["mem"], t["index"], t["step"], seq=np.arange(t["calls"]))
+        assert set(t["ids_contain_all"]) <= set(r.tolist()) <= set(t["ids_subset_of"])
+        assert np.all(f & 1)
+        # oracle agreement of the random fallback (same counter RNG)
+        inv = [(i, ST[s]) for i, s in c["invokers"]]
+        slots = O.Slots(c["slots"]["count"], c["slots"]["permits"])
+        for call in calls:
+            O.schedule(c["max_concurrent"], key, inv, slots, call["mem"], call["index"], call["step"],
+                       seq=0, rng_seed=99)
+        exp = [O.schedule(c["max_concurrent"], key, inv, slots, t["mem"], t["index"], t["step"], seq=s, rng_seed=99)
+               for s in range(t["calls"])]
+        assert r.tolist() == [e[0] for e in exp]
+    if "final_permits" in c:
+        assert b.permits().tolist() == c["final_permits"]
+
+
+# ----------------------------------------------------------------------------------------------- state goldens
+@pytest.mark.parametrize("name", ["state_grow_keep_old", "state_update_cluster", "state_cluster_below_one",
+                                  "state_cluster_min_memory"])
+def test_state_golden(golden, name):
+    c = golden[name]
+    b = gpu(managed_fraction=c["managed_fraction"], blackbox_fraction=c["blackbox_fraction"])
+    act = None
+    for step in c["steps"]:
+        if "update_invokers" in step:
+            b.update_invokers([InvokerHealth(i, m, ST[s]) for i, m, s in step["update_invokers"]])
+        if "try_acquire" in step:
+            i, m = step["try_acquire"]
+            # NestedSemaphore.tryAcquire(m) on slot i == a schedule() of one maxConcurrent=1 action pinned to i
+            b.set_pool(0, [(i, HEALTHY)])
+            r, _ = b.schedule(1, 0, m, 0, 1)
+            assert r[0] == i
+        if "update_cluster" in step:
+            b.update_cluster(step["update_cluster"])
+        e = step.get("expect", {})
+        if "permits" in e:
+            assert b.permits().tolist() == e["permits"]
+        if "managed_steps" in e:
+            assert b.managed_step_sizes == e["managed_steps"]
+            assert b.blackbox_step_sizes == e["blackbox_steps"]
+        if "managed" in e:
+            assert b.managed_size == len(e["managed"]) and b.blackbox_size == len(e["blackbox"])
+    del act
+
+
+def test_state_overlap_sizes(golden):
+    c = golden["state_overlap_small_n"]
+    bs = {}
+    for row in c["rows"][::7]:
+        bf = row["bf"]
+        b = bs.setdefault(bf, gpu(managed_fraction=1.0 - bf, blackbox_fraction=bf))
+        i = row["i"]
+        b.update_invokers([InvokerHealth(1, c["user_memory_mb"] * MB)] * i)
+        assert b.blackbox_size == row["blackbox_size"]
+        assert b.managed_size + b.blackbox_size == row["managed_plus_blackbox"]
+
+
+# ----------------------------------------------------------------------------------------------- component golden
+def test_balancer_activation_batch(golden):
+    c = golden["balancer_activation_batch"]
+    n_inv = c["n_invokers"]
+    for row in c["rows"][::5]:
+        b = gpu(managed_fraction=c["managed_fraction"], blackbox_fraction=c["blackbox_fraction"])
+        b.update_invokers([InvokerHealth(i, c["invoker_memory_mb"] * MB) for i in range(n_inv)])
+        (a,), (h,) = b.register_actions([Action(c["namespace"], c["action_path"], "0.0.1", c["action_memory_mb"],
+                                                c["max_concurrent"])])
+        key = b.key_id(a)
+        steps = b.managed_step_sizes
+        home, step = h % n_inv, steps[h % len(steps)]
+        inv, fl = b.publish(np.full(row["activations"], a))
+        assert np.all(fl == 0)
+        nxt = home
+        for g in row["groups_in_walk_order"]:
+            assert b.concurrent_state(nxt, key) == (g["remaining"], g["count"])
+            nxt = (nxt + step) % n_inv
+        rf = b.release_invoker(inv, np.full(len(inv), a))
+        assert np.all(rf == 0)
+        assert b.permits().tolist() == c["after_release"]["permits"]
+        assert all(b.concurrent_state(i, key) is None for i in range(n_inv))
+
+
+# ----------------------------------------------------------------------------------------------- stream parity
+def gpu_for(w):
+    b = gpu(managed_fraction=w.managed_fraction, blackbox_fraction=w.blackbox_fraction, rng_seed=w.rng_seed)
+    b.update_invokers_arrays(w.inv_ids, w.inv_mem, w.inv_status)
+    b.update_cluster(w.cluster_size)
+    b.register_actions(w.actions)
+    return b
+
+
+def check_stream(w, zombies=False):
+    st = O.state_for(w, zombies=zombies)
+    o_inv, o_fl, o_rf = st.replay(w.stream)
+    b = gpu_for(w)
+    g_inv, g_fl, g_rf = b.replay(w.stream)
+    bad = np.nonzero(o_inv != g_inv)[0]
+    assert len(bad) == 0, f"{w.name}: first mismatch at {bad[:5]} oracle={o_inv[bad[:5]]} gpu={g_inv[bad[:5]]}"
+    assert np.array_equal(o_fl, g_fl)
+    assert np.array_equal(o_rf, g_rf)
+    assert np.array_equal(st.permits(), b.permits())
+    return b, g_inv, g_fl
+
+
+@pytest.mark.parametrize("name,n", [("c1", None), ("c2", 200_000), ("c3", 60_000), ("c4", 200_000),
+                                    ("headline", 300_000)])
+def test_stream_parity(name, n):
+    w = W.config(name, n_activations=n)
+    check_stream(w)
+
+
+def test_stream_parity_literal_zombie_oracle():
+    # the literal oracle (entries created on failed tries, NS:61-62) gives the same answers on valid streams
+    w = W.config("c4", n_activations=50_000)
+    check_stream(w, zombies=True)
+
+
+def test_headline_full_size_parity_and_determinism():
+    w = W.config("headline")
+    b, g1, f1 = check_stream(w)
+    b2 = gpu_for(w)
+    g2, f2, _ = b2.replay(w.stream)
+    assert np.array_equal(g1, g2) and np.array_equal(f1, f2)
+
+
+def test_multi_shard_cluster_parity():
+    # C5-style shards: clusterSize 8, each shard its own stream; shard state = 1/8 of every invoker
+    for g in (0, 7):
+        w = W.config("headline", shard=g, n_shards=8, n_activations=100_000)
+        check_stream(w)
+
+
+# ----------------------------------------------------------------------------------------------- edge cases
+def test_no_invokers_is_none():
+    b = gpu()
+    (a,), _ = b.register_actions([Action("ns", "ns/a", "0.0.1", 256)])
+    inv, fl = b.publish([a, a])
+    assert inv.tolist() == [NONE, NONE]
+
+
+def test_int_min_hash_throws_like_reference():
+    b = gpu()
+    b.update_invokers([InvokerHealth(i, 4096 * MB) for i in range(10)])  # managed 9: 2^31 % 9 != 0
+    (a,), (h,) = b.register_actions([Action("", "polygenelubricants", "0.0.1", 256)])
+    assert h == -2**31
+    inv, _ = b.publish([a])
+    assert inv[0] == THROW_INDEX
+    assert b.permits().tolist() == [4096] * 10
+
+
+def test_invoker_id_outside_slots_throws():
+    b = gpu()
+    b.set_slots([10, 10])
+    b.set_pool(0, [(0, HEALTHY), (5, HEALTHY)])
+    r, _ = b.schedule(1, 0, [10, 10], 0, 1)
+    assert r.tolist() == [0, THROW_INDEX]
+
+
+def test_release_flags():
+    b = gpu()
+    b.update_invokers([InvokerHealth(i, 1024 * MB) for i in range(4)])
+    acts, _ = b.register_actions([Action("ns", "ns/a", "0.0.1", 256, 1), Action("ns", "ns/c", "0.0.1", 256, 4)])
+    inv, _ = b.publish([acts[1]])
+    # unknown concurrent key on another invoker -> NoSuchElementException; out-of-range invoker -> lift no-op;
+    # never-scheduled activation -> no entry
+    other = (inv[0] + 1) % 4
+    rf = b.release_invoker([other, 99, -1, inv[0], inv[0]], [acts[1], acts[0], acts[0], acts[1], acts[1]])
+    assert rf.tolist() == [1, 0, 4, 0, 1]
+    assert b.permits().tolist() == [1024] * 4
+
+
+def test_release_after_cluster_change_is_nosuchelement():
+    b = gpu()
+    b.update_invokers([InvokerHealth(i, 1024 * MB) for i in range(2)])
+    (a,), _ = b.register_actions([Action("ns", "ns/c", "0.0.1", 128, 3)])
+    inv, _ = b.publish([a])
+    b.update_cluster(2)  # throws all state away (SCPB:566-568)
+    rf = b.release_invoker(inv, [a])
+    assert rf.tolist() == [1]
+    assert b.permits().tolist() == [512, 512]
