@@ -120,7 +120,9 @@ def main():
     d_rf = torch.empty(max(len(s.rel_aid), 1), dtype=torch.uint8, device=dev)
     health = torch.from_numpy(w.inv_status.copy()).to(dev)
     gathered = torch.empty((world, len(w.inv_status)), dtype=torch.uint8, device=dev) if world > 1 else None
-    stream = torch.cuda.current_stream()
+    torch.cuda.synchronize()
+    stream = torch.cuda.Stream()  # a real (non-null) HIP stream: the engine and the timing events share it
+    torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
 
     def step():

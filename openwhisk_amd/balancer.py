@@ -203,7 +203,7 @@ class GpuShardingContainerPoolBalancer:
     def schedule(self, max_concurrent, key, slots, index, step, pool=0, seq=None):
         """ShardingContainerPoolBalancer.schedule(maxConcurrent, fqn, invokers(pool), dispatched, slots, index, step)
         for arrays of calls (SCPB:398-436).  Scalars are broadcast.  Returns (ids, flags)."""
-        n = max(np.size(x) for x in (max_concurrent, key, slots, index, step, pool))
+        n = max(np.size(x) for x in (max_concurrent, key, slots, index, step, pool, 1 if seq is None else seq))
         b = lambda x, dt: np.ascontiguousarray(np.broadcast_to(np.asarray(x, dtype=dt), (n,)))  # noqa: E731
         pl, ix, st = b(pool, np.uint8), b(index, np.int32), b(step, np.int32)
         mm, mc, ky = b(slots, np.int32), b(max_concurrent, np.int32), b(key, np.int32)

@@ -22,7 +22,7 @@ extern "C" hipError_t owgs_launch_hash(const OwgsHashArgs* a, hipStream_t s);
 extern "C" hipError_t owgs_launch_lookup(const OwgsLookupArgs* a, hipStream_t s);
 extern "C" hipError_t owgs_launch_prepare(const OwgsPrepArgs* a, hipStream_t s);
 extern "C" hipError_t owgs_launch_engine(const OwgsEngineArgs* a, hipStream_t s);
-extern "C" size_t owgs_engine_lds_bytes(int n_slots, int nm, int nb);
+extern "C" size_t owgs_engine_lds_bytes(int n_slots, int nm, int nb, int n_cursors);
 
 namespace {
 
@@ -78,7 +78,7 @@ std::vector<int32_t> pairwise_coprime(int32_t x) {  // SCPB:379-384
     return out;
 }
 
-constexpr uint32_t kCtabLog2 = 20;
+constexpr uint32_t kCtabLog2 = 19;  // 512k entries x 8 B = 4 MiB: one XCD L2
 
 }  // namespace
 
@@ -105,16 +105,16 @@ struct owgs_ctx {
 
     // actions
     std::vector<int32_t> a_mem, a_maxc, a_slot, a_hash;
-    std::vector<uint8_t> a_bb;
+    std::vector<uint8_t> a_bb, a_cok;
+    std::vector<int32_t> slot_uses, slot_maxc, slot_mem;
     std::unordered_map<std::string, int32_t> slot_ids;
 
     // device
     DevBuf<int32_t> d_permits, d_pool_words, d_hlist, d_act_slot, d_act_hash, d_act_mem, d_act_maxc, d_msteps,
         d_bsteps, d_err;
-    DevBuf<uint8_t> d_act_bb;
+    DevBuf<uint8_t> d_act_bb, d_act_cok;
     DevBuf<int4> d_act_info;
-    DevBuf<u64> d_ctab_key, d_stats;
-    DevBuf<int2> d_ctab_val;
+    DevBuf<u64> d_ctab, d_stats;
     uint32_t ctab_mask = 0;
     // scratch for host-buffer entry points
     DevBuf<int64_t> d_off;
@@ -125,8 +125,7 @@ struct owgs_ctx {
     DevBuf<int64_t> d_rel;
     // snapshot
     DevBuf<int32_t> s_permits;
-    DevBuf<u64> s_ctab_key;
-    DevBuf<int2> s_ctab_val;
+    DevBuf<u64> s_ctab;
     bool has_snap = false;
     int32_t snap_slots = 0;
 
@@ -214,6 +213,7 @@ static int prepare_actions(owgs_ctx* c) {
     a.mem = c->d_act_mem.p;
     a.maxc = c->d_act_maxc.p;
     a.bb = c->d_act_bb.p;
+    a.cursor_ok = c->d_act_cok.p;
     a.n = n;
     a.nm = c->nm;
     a.nb = c->nb;
@@ -226,15 +226,20 @@ static int prepare_actions(owgs_ctx* c) {
     return OWGS_OK;
 }
 
+static int32_t n_cursors(const owgs_ctx* c) {
+    const int32_t na = (int32_t)c->a_mem.size();
+    return owgs_engine_lds_bytes(c->n_slots, c->nm, c->nb, na) <= OWGS_LDS_BYTES ? na : 0;
+}
+
 static int lds_check(owgs_ctx* c) {
-    if (owgs_engine_lds_bytes(c->n_slots, c->nm, c->nb) > OWGS_LDS_BYTES)
+    if (c->n_slots > OWGS_MAX_SLOTS_CT) return c->fail(OWGS_ERANGE, "invoker ids beyond the concurrency-map key range");
+    if (owgs_engine_lds_bytes(c->n_slots, c->nm, c->nb, 0) > OWGS_LDS_BYTES)
         return c->fail(OWGS_ERANGE, "slot + pool state exceeds the engine's on-chip (LDS) capacity");
     return OWGS_OK;
 }
 
 static int reset_ctab(owgs_ctx* c) {
-    HIPCHK(c, hipMemsetAsync(c->d_ctab_key.p, 0, c->d_ctab_key.n * sizeof(u64), c->stream));
-    HIPCHK(c, hipMemsetAsync(c->d_ctab_val.p, 0, c->d_ctab_val.n * sizeof(int2), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_ctab.p, 0, c->d_ctab.n * sizeof(u64), c->stream));
     return OWGS_OK;
 }
 
@@ -251,9 +256,9 @@ static void base_args(owgs_ctx* c, OwgsEngineArgs& A) {
     A.shortcut_ok = c->shortcut_ok;
     A.act_info = c->d_act_info.p;
     A.act_slot = c->d_act_slot.p;
-    A.ctab_key = c->d_ctab_key.p;
-    A.ctab_val = c->d_ctab_val.p;
+    A.ctab = c->d_ctab.p;
     A.ctab_mask = c->ctab_mask;
+    A.n_cursors = n_cursors(c);
     A.rng_seed = c->cfg.rng_seed;
     A.stats = c->d_stats.p;
     A.err = c->d_err.p;
@@ -309,7 +314,7 @@ int owgs_create(const owgs_config* cfg, owgs_ctx** out) {
         return OWGS_EDEVICE;
     }
     const size_t cap = (size_t)1 << kCtabLog2;
-    if (c->d_ctab_key.reserve(cap) || c->d_ctab_val.reserve(cap) || c->d_stats.reserve(8) || c->d_err.reserve(1) ||
+    if (c->d_ctab.reserve(cap) || c->d_stats.reserve(8) || c->d_err.reserve(1) ||
         c->d_permits.reserve(1)) {
         owgs_destroy(c);
         return OWGS_ENOMEM;
@@ -341,18 +346,17 @@ void owgs_destroy(owgs_ctx* c) {
                                &c->d_b, &c->d_out, &c->s_permits};
     for (auto* b : i32s) b->release();
     c->d_act_bb.release();
+    c->d_act_cok.release();
     c->d_act_info.release();
-    c->d_ctab_key.release();
+    c->d_ctab.release();
     c->d_stats.release();
-    c->d_ctab_val.release();
     c->d_off.release();
     c->d_flags.release();
     c->d_rflags.release();
     c->d_seq.release();
     c->d_xw.release();
     c->d_rel.release();
-    c->s_ctab_key.release();
-    c->s_ctab_val.release();
+    c->s_ctab.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -431,9 +435,33 @@ int owgs_register_actions(owgs_ctx* c, int32_t n, const char* ns_bytes, const in
     for (int32_t i = 0; i < n; ++i) {
         // MemoryLimit/ConcurrencyLimit guarantee positive values (MemoryLimit.scala:68-69); the reference's
         // require(...) checks (FS:96, NS:85) would throw on anything else
-        if (mem_mb[i] <= 0 || max_conc[i] < 1 || max_conc[i] > OWGS_META_MAXC_MASK) return c->fail(OWGS_EINVAL, "mem/maxConcurrent");
+        if (mem_mb[i] <= 0 || max_conc[i] < 1 || max_conc[i] > OWGS_MAX_CONC) return c->fail(OWGS_EINVAL, "mem/maxConcurrent");
         if (ns_off[i + 1] < ns_off[i] || path_off[i + 1] < path_off[i] || key_off[i + 1] < key_off[i])
             return c->fail(OWGS_EINVAL, "offsets");
+    }
+    // validate before mutating: one fqn@version has one set of limits (the action document is versioned)
+    {
+        std::unordered_map<std::string, std::pair<int32_t, int32_t>> seen;
+        size_t fresh = 0;
+        for (int32_t i = 0; i < n; ++i) {
+            std::string k(key_bytes + key_off[i], (size_t)(key_off[i + 1] - key_off[i]));
+            auto it = c->slot_ids.find(k);
+            std::pair<int32_t, int32_t> lim{max_conc[i], mem_mb[i]};
+            if (it != c->slot_ids.end()) {
+                if (c->slot_maxc[it->second] != lim.first || c->slot_mem[it->second] != lim.second)
+                    return c->fail(OWGS_EINVAL, "same fqn@version registered with different limits");
+                continue;
+            }
+            auto sj = seen.find(k);
+            if (sj == seen.end()) {
+                seen.emplace(std::move(k), lim);
+                ++fresh;
+            } else if (sj->second != lim) {
+                return c->fail(OWGS_EINVAL, "same fqn@version registered with different limits");
+            }
+        }
+        if (c->slot_ids.size() + fresh > (size_t)OWGS_MAX_SLOTKEYS + 1)
+            return c->fail(OWGS_ERANGE, "too many fqn@version keys");
     }
     (void)hipSetDevice(c->cfg.device);
     const int32_t base = (int32_t)c->a_mem.size();
@@ -444,9 +472,13 @@ int owgs_register_actions(owgs_ctx* c, int32_t n, const char* ns_bytes, const in
         if (it == c->slot_ids.end()) {
             sid = (int32_t)c->slot_ids.size();
             c->slot_ids.emplace(std::move(k), sid);
+            c->slot_uses.push_back(0);
+            c->slot_maxc.push_back(max_conc[i]);
+            c->slot_mem.push_back(mem_mb[i]);
         } else {
             sid = it->second;
         }
+        c->slot_uses[sid]++;
         c->a_slot.push_back(sid);
         c->a_mem.push_back(mem_mb[i]);
         c->a_maxc.push_back(max_conc[i]);
@@ -482,6 +514,10 @@ int owgs_register_actions(owgs_ctx* c, int32_t n, const char* ns_bytes, const in
     HIPCHK(c, upload(c->d_act_mem, c->a_mem.data(), (size_t)total, c->stream));
     HIPCHK(c, upload(c->d_act_maxc, c->a_maxc.data(), (size_t)total, c->stream));
     HIPCHK(c, upload(c->d_act_bb, c->a_bb.data(), (size_t)total, c->stream));
+    // a walk cursor is exact for maxConcurrent==1 actions and for fqns invoked on a single walk
+    c->a_cok.resize((size_t)total);
+    for (int32_t a = 0; a < total; ++a) c->a_cok[a] = (c->a_maxc[a] == 1 || c->slot_uses[c->a_slot[a]] == 1) ? 1 : 0;
+    HIPCHK(c, upload(c->d_act_cok, c->a_cok.data(), (size_t)total, c->stream));
     int rc = prepare_actions(c);
     if (!rc) HIPCHK(c, hipStreamSynchronize(c->stream));
     return rc;
@@ -554,7 +590,8 @@ int owgs_schedule_walks(owgs_ctx* c, int32_t n, const uint8_t* pool, const int32
     if (n == 0) return OWGS_OK;
     std::vector<int4> xw(n);
     for (int32_t i = 0; i < n; ++i) {
-        if (mem_mb[i] <= 0 || max_conc[i] < 1 || max_conc[i] > OWGS_META_MAXC_MASK || step[i] < 0 || step[i] > (1 << 30))
+        if (mem_mb[i] <= 0 || max_conc[i] < 1 || max_conc[i] > OWGS_MAX_CONC || step[i] < 0 || step[i] > (1 << 30) ||
+            key[i] < 0 || key[i] > OWGS_MAX_SLOTKEYS)
             return c->fail(OWGS_EINVAL, "mem/maxConcurrent/step");
         const int p = pool[i] ? 1 : 0;
         const int32_t np = p ? c->nb : c->nm;
@@ -629,7 +666,7 @@ int owgs_read_concurrent(owgs_ctx* c, int32_t invoker, int32_t key, int32_t* per
     HIPCHK(c, upload(di, &invoker, 1, c->stream));
     HIPCHK(c, upload(dk, &key, 1, c->stream));
     HIPCHK(c, dv.reserve(1));
-    OwgsLookupArgs la{c->d_ctab_key.p, c->d_ctab_val.p, c->ctab_mask, di.p, dk.p, 1, dv.p};
+    OwgsLookupArgs la{c->d_ctab.p, c->ctab_mask, di.p, dk.p, 1, dv.p};
     HIPCHK(c, owgs_launch_lookup(&la, c->stream));
     int2 v;
     HIPCHK(c, hipMemcpyAsync(&v, dv.p, sizeof(int2), hipMemcpyDeviceToHost, c->stream));
@@ -721,12 +758,10 @@ int owgs_snapshot(owgs_ctx* c) {
     if (!c) return OWGS_EINVAL;
     (void)hipSetDevice(c->cfg.device);
     HIPCHK(c, c->s_permits.reserve((size_t)std::max(c->n_slots, 1)));
-    HIPCHK(c, c->s_ctab_key.reserve(c->d_ctab_key.n));
-    HIPCHK(c, c->s_ctab_val.reserve(c->d_ctab_val.n));
+    HIPCHK(c, c->s_ctab.reserve(c->d_ctab.n));
     if (c->n_slots)
         HIPCHK(c, hipMemcpyAsync(c->s_permits.p, c->d_permits.p, (size_t)c->n_slots * 4, hipMemcpyDeviceToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->s_ctab_key.p, c->d_ctab_key.p, c->d_ctab_key.n * 8, hipMemcpyDeviceToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->s_ctab_val.p, c->d_ctab_val.p, c->d_ctab_val.n * 8, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->s_ctab.p, c->d_ctab.p, c->d_ctab.n * 8, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->has_snap = true;
     c->snap_slots = c->n_slots;
@@ -739,8 +774,7 @@ int owgs_restore(owgs_ctx* c, void* stream) {
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     if (c->n_slots)
         HIPCHK(c, hipMemcpyAsync(c->d_permits.p, c->s_permits.p, (size_t)c->n_slots * 4, hipMemcpyDeviceToDevice, s));
-    HIPCHK(c, hipMemcpyAsync(c->d_ctab_key.p, c->s_ctab_key.p, c->d_ctab_key.n * 8, hipMemcpyDeviceToDevice, s));
-    HIPCHK(c, hipMemcpyAsync(c->d_ctab_val.p, c->s_ctab_val.p, c->d_ctab_val.n * 8, hipMemcpyDeviceToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->d_ctab.p, c->s_ctab.p, c->d_ctab.n * 8, hipMemcpyDeviceToDevice, s));
     return OWGS_OK;
 }
 

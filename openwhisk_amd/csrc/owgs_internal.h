@@ -8,9 +8,10 @@
 //   act_info[n_actions]     i4   {home, step, mem_mb, meta}; meta = maxConcurrent | pool<<24 | throw<<25 | empty<<26
 //   act_slot[n_actions]     i32  slot-key id (fullyQualifiedName(true) interned)
 //   act_hash[n_actions]     i32  generateHash(namespace, fqn(false))
-//   ctab_key[cap] u64 / ctab_val[cap] i2   NestedSemaphore concurrency maps of all invokers, one open-addressing
-//                                 table keyed by (invoker id, slot key); value {permits c, operationCount}.  An entry
-//                                 with operationCount 0 is "absent" (the reference removes it, NS:109-111).
+//   ctab[cap]               u64  NestedSemaphore concurrency maps of all invokers: one open-addressing table keyed by
+//                                 (invoker id, slot key), value {permits c, operationCount} packed in one 8-byte entry
+//                                 (one load per probe).  operationCount 0 means "absent" (the reference removes the
+//                                 entry, NS:109-111).
 #pragma once
 #include <stdint.h>
 
@@ -18,6 +19,16 @@
 #define OWGS_META_POOL_SHIFT 24
 #define OWGS_META_THROW (1u << 25)
 #define OWGS_META_EMPTY (1u << 26)
+#define OWGS_META_CURSOR (1u << 27)  // walk cursor valid: maxConcurrent == 1 or the fqn is invoked on one walk only
+
+// concurrency-map entry (8 bytes): key32 << 32 | val32, key32 = (invoker+1) | slot << 15, val32 = c | ops << 12
+#define OWGS_CT_SLOT_SHIFT 15
+#define OWGS_CT_C_BITS 12
+#define OWGS_CT_C_MASK 0xFFFu
+#define OWGS_MAX_SLOTS_CT 32767      // invoker ids representable in key32
+#define OWGS_MAX_SLOTKEYS 131071     // fqn@version keys representable in key32
+#define OWGS_MAX_CONC 4095           // maxConcurrent representable in val32 (c < maxConcurrent)
+#define OWGS_MAX_OPS 1048575
 
 #define OWGS_NONE_V (-1)
 #define OWGS_THROW_V (-2)
@@ -42,9 +53,9 @@ struct OwgsEngineArgs {
     int32_t shortcut_ok; // bit0 managed, bit1 blackbox: pool has no usable out-of-range id
     const int4* act_info;
     const int32_t* act_slot;
-    unsigned long long* ctab_key;
-    int2* ctab_val;
+    unsigned long long* ctab;
     uint32_t ctab_mask;
+    int32_t n_cursors;  // actions with an LDS walk cursor (0 = cursors off)
     // stream
     int32_t n_batches;
     const int64_t* acq_off;
@@ -79,8 +90,7 @@ struct OwgsHashArgs {
 };
 
 struct OwgsLookupArgs {
-    const unsigned long long* ctab_key;
-    const int2* ctab_val;
+    const unsigned long long* ctab;
     uint32_t ctab_mask;
     const int32_t* inv;
     const int32_t* slot;
@@ -93,6 +103,7 @@ struct OwgsPrepArgs {
     const int32_t* mem;
     const int32_t* maxc;
     const uint8_t* bb;
+    const uint8_t* cursor_ok;
     int32_t n;
     int32_t nm, nb;
     const int32_t* msteps;

@@ -1,25 +1,30 @@
 // owgs_kernels.hip -- CDNA4 (gfx950) kernels of the batched invoker scheduler.
 //
 // Kernels
-//   owgs_hash_kernel     java.lang.String.hashCode of many strings, one wave per string: lane i sums
-//                        c[i + 64k] * 31^(L-1-i-64k) (mod 2^32) and the wave reduces (SCPB:370-372 call site).
-//   owgs_prepare_kernel  per action: generateHash combine, home = hash % n, step = stepSizes(hash % k),
-//                        meta bits (SCPB:262-268).
+//   owgs_hash_kernel     generateHash(namespace, action) (SCPB:370-372): java.lang.String.hashCode of both strings,
+//                        one wave per action; lane i sums c[i+64k] * 31^(L-1-i-64k) (mod 2^32), the wave reduces.
+//   owgs_prepare_kernel  per action: home = hash % n, step = stepSizes(hash % k), meta bits (SCPB:262-268).
+//   owgs_lookup_kernel   NestedSemaphore.concurrentState reads (introspection).
 //   owgs_engine_kernel   the hot path: releases (SCPB:327-331 -> NS:98-113) and schedule() (SCPB:398-436 with
 //                        NS:32-91) for a whole stream of batches, replaying the reference's SEQUENTIAL semantics.
 //
-// Engine design (DESIGN.md "Engine"): one wavefront owns one controller shard.  The slot permits and the pool
-// vectors live in LDS for the whole stream (HBM is read once and written once).  Activations are taken 64 at a
-// time (one per lane, in stream order).  Every lane speculates its walk target against the current state, which is
-// the exact state at the chunk frontier f.  Because memory permits never increase inside a batch (releases happen
-// only at batch boundaries), a probe that fails against an earlier state fails at every later time, so the
-// speculated target is never EARLIER than the true one.  It is exactly the true one iff the permits consumed at that
-// invoker by earlier lanes of the chunk still leave room: lanes are grouped by target (LDS stamp table + ballot),
-// an exclusive prefix sum of the consumed memory inside each group gives every lane its remaining permits, and the
-// first lane l* that does not fit is a TRUE rejection (every earlier lane fitted, so the prefix it saw is exact).
-// Lanes [f, l*) are committed, l* advances its walk, and the chunk iterates with f = l*.  Concurrency slots (maxConc
-// > 1) can increase when an earlier lane of the same action starts a container, so a lane with an earlier
-// same-action lane in [f, lane) is treated as uncertain and resolved once it is the frontier.
+// Engine design (DESIGN.md "Engine").  One wavefront owns one controller shard.  Slot permits, pool vectors and a
+// per-action walk cursor live in LDS for the whole stream (HBM is read once and written once); the concurrency maps
+// live in one 8-byte-entry open-addressing table (L2-resident).  Activations are taken 64 at a time (one per lane, in
+// stream order) and resolved by speculation + exact validation:
+//   * memory permits never increase inside a batch (releases are applied at batch boundaries), so a probe that
+//     fails against the state at the chunk frontier f fails at every later time: a lane's speculated target is never
+//     EARLIER in its walk than its true target, and the per-action cursor (first walk step that may still be feasible)
+//     only moves forward inside a batch;
+//   * lanes are grouped by target invoker (LDS stamp table + ballot); inside a group an exclusive prefix sum of the
+//     memory consumed by earlier lanes gives each lane the permits left at its own time, and concurrency slots are
+//     modelled per (target, action) from the rank inside the group;
+//   * the first lane l* whose speculation does not hold is a TRUE rejection (every earlier lane was exact), lanes
+//     [f, l*) commit, l* (and the later lanes of the same maxConcurrent==1 action at the same target) step past the
+//     target, and the chunk iterates with f = l*.  The frontier lane is always exact, so every iteration commits.
+//   * cases whose speculation cannot be validated cheaply (an earlier lane of the chunk that may create concurrency
+//     slots for the same fqn on another walk, or a forced acquire) are treated as uncertain and resolved when they
+//     reach the frontier.
 #include <hip/hip_runtime.h>
 
 #include "owgs_internal.h"
@@ -52,7 +57,15 @@ __device__ __forceinline__ int jmod_step(int pos, int step, int n) {
     return (int)((int)((unsigned)pos + (unsigned)step) % n);  // Java (index + step) % numInvokers
 }
 
+// pool position of walk step s: (home + s*step) mod n  (home in [0,n), step >= 0)
+__device__ __forceinline__ int walk_pos(int home, int s, int step, int n) {
+    return (int)(((long long)home + (long long)s * (long long)step) % (long long)n);
+}
+
 __device__ __forceinline__ int ffs64(u64 m) { return __ffsll((long long)m) - 1; }
+__device__ __forceinline__ int fls64(u64 m) { return 63 - __clzll((long long)m); }
+
+__device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
 __device__ __forceinline__ int wave_excl_scan(int v) {
     const int lane = __lane_id();
@@ -77,49 +90,56 @@ __device__ __forceinline__ int wave_min(int v) {
     return v;
 }
 
-__device__ __forceinline__ uint32_t ctab_hash(u64 k) {
-    k ^= k >> 33;
-    k *= 0xff51afd7ed558ccdULL;
-    k ^= k >> 33;
-    k *= 0xc4ceb9fe1a85ec53ULL;
-    k ^= k >> 33;
-    return (uint32_t)k;
+// ---- concurrency table: entry = key32 << 32 | val32; key32 = (inv+1) | slot << 15; val32 = c | ops << 12
+__device__ __forceinline__ uint32_t ct_key(int inv, int slot) {
+    return (uint32_t)(inv + 1) | ((uint32_t)slot << OWGS_CT_SLOT_SHIFT);
+}
+__device__ __forceinline__ uint32_t ct_hash(uint32_t k) {
+    k ^= k >> 16;
+    k *= 0x7feb352dU;
+    k ^= k >> 15;
+    k *= 0x846ca68bU;
+    k ^= k >> 16;
+    return k;
+}
+__device__ __forceinline__ int ct_c(u64 e) { return (int)((uint32_t)e & OWGS_CT_C_MASK); }
+__device__ __forceinline__ int ct_ops(u64 e) { return (int)((uint32_t)e >> OWGS_CT_C_BITS); }
+__device__ __forceinline__ u64 ct_entry(uint32_t key, int c, int ops) {
+    return ((u64)key << 32) | (u64)((uint32_t)c | ((uint32_t)ops << OWGS_CT_C_BITS));
 }
 
-__device__ __forceinline__ u64 ctab_keyof(int inv, int slot) { return ((u64)(uint32_t)(inv + 1) << 32) | (uint32_t)slot; }
-
-__device__ int ctab_find(const u64* keys, uint32_t mask, u64 key) {
-    uint32_t h = ctab_hash(key) & mask;
+// returns table index or -1; *e = entry (0 if absent)
+__device__ int ct_find(const u64* tab, uint32_t mask, uint32_t key, u64* e) {
+    uint32_t h = ct_hash(key) & mask;
     for (uint32_t p = 0; p <= mask; ++p) {
-        u64 k = keys[h];
-        if (k == key) return (int)h;
-        if (k == 0) return -1;
+        const u64 v = tab[h];
+        if ((uint32_t)(v >> 32) == key) {
+            *e = v;
+            return (int)h;
+        }
+        if (v == 0) break;
         h = (h + 1) & mask;
     }
+    *e = 0;
     return -1;
 }
 
-__device__ int ctab_insert(u64* keys, uint32_t mask, u64 key) {
-    uint32_t h = ctab_hash(key) & mask;
+__device__ int ct_insert(u64* tab, uint32_t mask, uint32_t key) {
+    uint32_t h = ct_hash(key) & mask;
     for (uint32_t p = 0; p <= mask; ++p) {
-        u64 k = keys[h];
-        if (k == key) return (int)h;
-        if (k == 0) {
-            keys[h] = key;
-            return (int)h;
-        }
+        const u64 v = tab[h];
+        if (v == 0 || (uint32_t)(v >> 32) == key) return (int)h;
         h = (h + 1) & mask;
     }
     return -1;
 }
 
 // c of NestedSemaphore(inv).actionConcurrentSlotsMap(slot); absent entries (operationCount 0) read as c = 0
-__device__ __forceinline__ int conc_c(const OwgsEngineArgs& A, int inv, int slot, int* eidx) {
-    int e = ctab_find(A.ctab_key, A.ctab_mask, ctab_keyof(inv, slot));
-    *eidx = e;
-    if (e < 0) return 0;
-    int2 v = A.ctab_val[e];
-    return v.y > 0 ? v.x : 0;
+__device__ __forceinline__ int conc_lookup(const OwgsEngineArgs& A, int inv, int slot, int* idx, int* ops) {
+    u64 e;
+    *idx = ct_find(A.ctab, A.ctab_mask, ct_key(inv, slot), &e);
+    *ops = ct_ops(e);
+    return *ops > 0 ? ct_c(e) : 0;
 }
 
 // ------------------------------------------------------------------------------------------------ hashing
@@ -161,11 +181,12 @@ __global__ __launch_bounds__(256) void owgs_hash_kernel(OwgsHashArgs a) {
 __global__ __launch_bounds__(256) void owgs_lookup_kernel(OwgsLookupArgs a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
-    const int e = ctab_find(a.ctab_key, a.ctab_mask, ctab_keyof(a.inv[i], a.slot[i]));
-    a.out[i] = e < 0 ? make_int2(0, 0) : a.ctab_val[e];
+    u64 e;
+    ct_find(a.ctab, a.ctab_mask, ct_key(a.inv[i], a.slot[i]), &e);
+    a.out[i] = make_int2(ct_c(e), ct_ops(e));
 }
 
-// generateHash combine + home/step selection (SCPB:266-268)
+// home/step selection (SCPB:266-268)
 __global__ __launch_bounds__(256) void owgs_prepare_kernel(OwgsPrepArgs a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
@@ -174,6 +195,7 @@ __global__ __launch_bounds__(256) void owgs_prepare_kernel(OwgsPrepArgs a) {
     const int k = pool ? a.n_bsteps : a.n_msteps;
     const int32_t* steps = pool ? a.bsteps : a.msteps;
     uint32_t meta = (uint32_t)(a.maxc[i] & OWGS_META_MAXC_MASK) | ((uint32_t)pool << OWGS_META_POOL_SHIFT);
+    if (a.cursor_ok[i]) meta |= OWGS_META_CURSOR;
     int home = 0, step = 0;
     if (n <= 0) {
         meta |= OWGS_META_EMPTY;
@@ -190,13 +212,6 @@ __global__ __launch_bounds__(256) void owgs_prepare_kernel(OwgsPrepArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------ engine
-struct Lds {
-    int32_t* perm;
-    int32_t* pw;
-    uint32_t* stT;
-    uint32_t* stS;
-};
-
 // fallback target (SCPB:417-424): H = usable pool members in pool order, r = H[rng(seq) mod |H|]
 __device__ __forceinline__ void fallback_target(const OwgsEngineArgs& A, int pool, u64 seq, int* kind, int* tgt) {
     const int hc = pool ? A.hb : A.hm;
@@ -213,28 +228,38 @@ __device__ __forceinline__ void fallback_target(const OwgsEngineArgs& A, int poo
     *tgt = r;
 }
 
+// concurrency slots an acquisition finds, given c0 at state f and q earlier same-fqn lanes at the same invoker
+__device__ __forceinline__ int c_now_of(int c0, int q, int R) {
+    const int x = q - c0;
+    if (x < 0) return c0 - q;
+    const int r = x % R;
+    return r == 0 ? 0 : R - r;
+}
+
 __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
     extern __shared__ __attribute__((aligned(16))) int32_t lds_raw[];
     const int lane = threadIdx.x;
     const int nsl_al = (A.n_slots + 3) & ~3;
     const int npw_al = (A.nm + A.nb + 3) & ~3;
-    Lds L;
-    L.perm = lds_raw;
-    L.pw = lds_raw + nsl_al;
-    L.stT = (uint32_t*)(L.pw + npw_al);
-    L.stS = L.stT + OWGS_STAMP_BUCKETS;
+    int32_t* perm = lds_raw;
+    int32_t* pw = lds_raw + nsl_al;
+    uint32_t* stT = (uint32_t*)(pw + npw_al);
+    uint32_t* stS = stT + OWGS_STAMP_BUCKETS;
+    int32_t* cur = (int32_t*)(stS + OWGS_STAMP_BUCKETS);
+    const int n_cur = A.n_cursors;
 
-    for (int i = lane; i < A.n_slots; i += 64) L.perm[i] = A.permits[i];
-    for (int i = lane; i < A.nm + A.nb; i += 64) L.pw[i] = A.pool_words[i];
-    for (int i = lane; i < 2 * OWGS_STAMP_BUCKETS; i += 64) L.stT[i] = 0xFFFFFFFFu;
+    for (int i = lane; i < A.n_slots; i += 64) perm[i] = A.permits[i];
+    for (int i = lane; i < A.nm + A.nb; i += 64) pw[i] = A.pool_words[i];
+    for (int i = lane; i < 2 * OWGS_STAMP_BUCKETS; i += 64) stT[i] = 0xFFFFFFFFu;
     __syncthreads();
 
     u64 st_iter = 0, st_probe = 0, st_fb = 0, st_long = 0, st_grp = 0;
     uint32_t iter = 0;
     const u64 lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+    const u64 self_bit = 1ull << lane;
 
     for (int b = 0; b < A.n_batches; ++b) {
-        // ================================================================ releases (SCPB:327-331)
+        // ================================================================ releases (SCPB:327-331, NS:98-113)
         const int64_t r_beg = A.rel_off ? A.rel_off[b] : 0, r_end = A.rel_off ? A.rel_off[b + 1] : 0;
         for (int64_t r0 = r_beg; r0 < r_end; r0 += 64) {
             const int64_t r = r0 + lane;
@@ -260,33 +285,35 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
             uint8_t flag = 0;
             bool simple = false, conc = false;
             if (valid) {
-                if (inv < 0) flag = OWGS_REL_NOENTRY_BIT;
-                else if (inv >= A.n_slots) flag = 0;  // invokerSlots.lift -> no-op
+                if (inv < 0) flag = OWGS_REL_NOENTRY_BIT;  // no ActivationEntry (CLB:278-279)
+                else if (inv >= A.n_slots) flag = 0;        // invokerSlots.lift -> no-op
                 else if (maxc == 1) simple = true;
                 else conc = true;
             }
-            int eidx = -1;
+            int idx = -1, c0 = 0, o0 = 0;
             if (conc) {
-                eidx = ctab_find(A.ctab_key, A.ctab_mask, ctab_keyof(inv, slot));
-                int2 v = eidx >= 0 ? A.ctab_val[eidx] : make_int2(0, 0);
-                if (eidx < 0 || v.y <= 0) {
+                u64 e;
+                idx = ct_find(A.ctab, A.ctab_mask, ct_key(inv, slot), &e);
+                c0 = ct_c(e);
+                o0 = ct_ops(e);
+                if (idx < 0 || o0 <= 0) {
                     conc = false;
-                    flag = OWGS_REL_NOSUCH_BIT;  // actionConcurrentSlotsMap(actionid) throws NS:103
+                    flag = OWGS_REL_NOSUCH_BIT;  // actionConcurrentSlotsMap(actionid) throws (NS:103)
                 }
             }
-            // group concurrent releases of the same entry: rank in stream order, group size
+            // releases of one entry inside this group of 64: rank in stream order and group size
             int rank = 0, gsz = 1;
             {
                 ++iter;
                 const uint32_t stamp = ((0x03FFFFFFu - (iter & 0x03FFFFFFu)) << 6) | (uint32_t)lane;
-                if (conc) atomicMin(&L.stT[eidx & (OWGS_STAMP_BUCKETS - 1)], stamp);
-                __syncthreads();
-                const bool leader = conc && L.stT[eidx & (OWGS_STAMP_BUCKETS - 1)] == stamp;
+                if (conc) atomicMin(&stT[idx & (OWGS_STAMP_BUCKETS - 1)], stamp);
+                wave_fence();
+                const bool leader = conc && stT[idx & (OWGS_STAMP_BUCKETS - 1)] == stamp;
                 u64 pend = __ballot(conc && !leader);
                 while (pend) {
                     const int j = ffs64(pend);
-                    const int e = __builtin_amdgcn_readlane(eidx, j);
-                    const u64 G = __ballot(conc && eidx == e);
+                    const int e = __builtin_amdgcn_readlane(idx, j);
+                    const u64 G = __ballot(conc && idx == e);
                     if ((G >> lane) & 1) {
                         rank = __popcll(G & lt_mask);
                         gsz = __popcll(G);
@@ -295,64 +322,57 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                 }
             }
             bool mem_rel = false;
-            int2 v0 = make_int2(0, 0);
-            if (conc) v0 = A.ctab_val[eidx];
             if (conc) {
-                // NS:98-113 / RS:99-108 applied rank+1 times to (c0, ops0), R = maxConcurrent
-                const int c0 = v0.x, o = v0.y;
-                if (rank < o) {
-                    mem_rel = ((c0 + rank + 1) % maxc) == 0;
-                } else {
-                    flag = OWGS_REL_NOSUCH_BIT;  // entry already removed by an earlier release of this batch
-                }
+                // RS.release(1, opComplete = true) applied rank+1 times to (c0, o0), reductionSize = maxConcurrent
+                if (rank < o0) mem_rel = ((c0 + rank + 1) % maxc) == 0;
+                else flag = OWGS_REL_NOSUCH_BIT;  // entry already removed by an earlier release in this group
             }
-            __syncthreads();
             if (conc && rank == 0) {
-                const int c0 = v0.x, o = v0.y;
-                const int j = min(gsz, o);
+                const int j = min(gsz, o0);
                 int c1 = (c0 + j) % maxc;
-                const int o1 = o - j;
+                const int o1 = o0 - j;
                 if (o1 == 0) c1 = 0;  // actionRelease: entry removed (NS:109-111)
-                A.ctab_val[eidx] = make_int2(c1, o1);
+                A.ctab[idx] = ct_entry(ct_key(inv, slot), c1, o1);
             }
             if (simple || mem_rel) {
-                const int old = atomicAdd(&L.perm[inv], mem);
+                const int old = atomicAdd(&perm[inv], mem);
                 if (old > 0x7FFFFFFF - mem) {  // ForcibleSemaphore overflow -> Error, state unchanged (FS:48-50)
-                    atomicSub(&L.perm[inv], mem);
+                    atomicSub(&perm[inv], mem);
                     flag |= OWGS_REL_OVERFLOW_BIT;
                 }
             }
             if (valid && A.rel_flags) A.rel_flags[r] = flag;
-            __threadfence_block();
-            __syncthreads();
+            wave_fence();
         }
 
-        // ================================================================ per-batch pool bounds
+        // ================================================================ per-batch bounds and cursors
         // U[p] >= max permits over usable members of pool p; permits only fall until the next batch.
         int U[2];
         for (int p = 0; p < 2; ++p) {
             const int base = p ? A.nm : 0, n = p ? A.nb : A.nm;
             int m = (int)0x80000000;
             for (int i = lane; i < n; i += 64) {
-                const int w = L.pw[base + i];
-                if (w >= 0) m = max(m, L.perm[w]);
+                const int w = pw[base + i];
+                if (w >= 0) m = max(m, perm[w]);
             }
             U[p] = wave_max(m);
         }
+        for (int i = lane; i < n_cur; i += 64) cur[i] = 0;
+        wave_fence();
 
-        // ================================================================ acquires (SCPB:398-436)
+        // ================================================================ acquires (SCPB:398-436, NS:32-91)
         const int64_t a_beg = A.acq_off[b], a_end = A.acq_off[b + 1];
-        for (int64_t c0 = a_beg; c0 < a_end; c0 += 64) {
-            const int64_t i = c0 + lane;
+        for (int64_t c0i = a_beg; c0i < a_end; c0i += 64) {
+            const int64_t i = c0i + lane;
             bool pending = i < a_end;
-            int home = 0, step = 0, mem = 0, meta = 0, slot = 0;
+            int a = -1, home = 0, step = 0, mem = 0, meta = 0, slot = 0;
             if (pending) {
                 int4 info;
                 if (A.xw_info) {
                     info = A.xw_info[i];
                     slot = A.xw_slot[i];
                 } else {
-                    const int a = A.act[i];
+                    a = A.act[i];
                     info = A.act_info[a];
                     slot = A.act_slot[a];
                 }
@@ -361,71 +381,64 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                 mem = info.z;
                 meta = info.w;
             }
-            const u64 seq = A.seq ? A.seq[i < a_end ? i : a_beg] : (A.seq_base + (u64)i);
+            const u64 seq = A.seq ? A.seq[pending ? i : a_beg] : (A.seq_base + (u64)i);
             const int maxc = meta & OWGS_META_MAXC_MASK;
             const int pool = (meta >> OWGS_META_POOL_SHIFT) & 1;
             const int n = pool ? A.nb : A.nm;
             const int pwb = pool ? A.nm : 0;
-            int pos = home, s = 0;
-            int out_kind = K_NONE, out_tgt = -1;
-            bool fullwalk = false;
+            const bool cok = (meta & OWGS_META_CURSOR) && a >= 0 && a < n_cur;
+            int s = 0;
 
             if (pending) {
-                if (meta & OWGS_META_EMPTY) {
-                    out_kind = K_NONE;
-                    pending = false;
-                } else if ((meta & OWGS_META_THROW) || home < 0 || home >= n || step < 0) {
-                    out_kind = K_THROW;
-                    pending = false;
-                }
-                if (!pending) {
-                    A.out_inv[i] = out_kind == K_NONE ? OWGS_NONE_V : OWGS_THROW_V;
+                int ok_kind = -1;
+                if (meta & OWGS_META_EMPTY) ok_kind = K_NONE;
+                else if ((meta & OWGS_META_THROW) || home < 0 || home >= n || step < 0) ok_kind = K_THROW;
+                if (ok_kind >= 0) {
+                    A.out_inv[i] = ok_kind == K_NONE ? OWGS_NONE_V : OWGS_THROW_V;
                     A.out_flags[i] = 0;
+                    pending = false;
                 }
             }
 
             int f = 0;
             while (__ballot(pending)) {
                 ++st_iter;
-                // -------------------------------------------------------- speculate targets
-                int kind = K_NONE, tgt = -1, cval = 0, eidx = -1;
+                // -------------------------------------------------------- speculate targets against state at f
+                int kind = K_NONE, tgt = -1, c0 = 0, cidx = -1, ops0 = 0;
+                bool fullwalk = false;
                 const bool act = pending && lane >= f;
                 if (act) {
+                    if (cok) s = max(s, cur[a]);
                     if (maxc == 1 && mem > U[pool] && ((A.shortcut_ok >> pool) & 1)) {
-                        fallback_target(A, pool, seq, &kind, &tgt);
-                        fullwalk = false;
+                        fallback_target(A, pool, seq, &kind, &tgt);  // every usable permit < mem: walk fails
                     } else {
                         kind = K_LONG;
+                        int pos = walk_pos(home, s, step, n);
                         for (int k = 0; k < KPROBE; ++k) {
                             if (s >= n) {  // every pool position probed: the n+2-probe walk fails (SCPB:417)
                                 fallback_target(A, pool, seq, &kind, &tgt);
                                 fullwalk = true;
                                 break;
                             }
-                            if (pos < 0 || pos >= n) {
-                                kind = K_THROW;
-                                break;
-                            }
-                            const int w = L.pw[pwb + pos];
+                            const int w = pw[pwb + pos];
                             ++st_probe;
                             if (w == OWGS_PW_BADID) {
                                 kind = K_THROW;
                                 break;
                             }
                             if (w >= 0) {
-                                bool feas = L.perm[w] >= mem;
+                                bool feas = perm[w] >= mem;
+                                int c = 0, ix = -1, o = 0;
                                 if (maxc > 1) {
-                                    int e;
-                                    const int c = conc_c(A, w, slot, &e);
-                                    if (c >= 1) feas = true;
-                                    if (feas) {
-                                        cval = c;
-                                        eidx = e;
-                                    }
+                                    c = conc_lookup(A, w, slot, &ix, &o);
+                                    feas = feas || c >= 1;
                                 }
                                 if (feas) {
                                     kind = K_TARGET;
                                     tgt = w;
+                                    c0 = c;
+                                    cidx = ix;
+                                    ops0 = o;
                                     break;
                                 }
                             }
@@ -435,33 +448,31 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                     }
                 }
                 // -------------------------------------------------------- frontier lane with a long walk:
-                // wave-cooperative scan of 64 walk positions per step (ballot picks the first feasible one)
-                const int kf = __builtin_amdgcn_readlane(kind, f);
-                if (kf == K_LONG) {
+                // wave-cooperative scan of 64 walk steps per round (ballot picks the first feasible one)
+                if (__builtin_amdgcn_readlane(kind, f) == K_LONG) {
                     ++st_long;
-                    int p0 = __builtin_amdgcn_readlane(pos, f);
                     int s0 = __builtin_amdgcn_readlane(s, f);
+                    const int hm = __builtin_amdgcn_readlane(home, f);
                     const int stp = __builtin_amdgcn_readlane(step, f);
                     const int nn = __builtin_amdgcn_readlane(n, f);
                     const int pb = __builtin_amdgcn_readlane(pwb, f);
                     const int m = __builtin_amdgcn_readlane(mem, f);
                     const int mc = __builtin_amdgcn_readlane(maxc, f);
                     const int sl = __builtin_amdgcn_readlane(slot, f);
-                    int fk = K_LONG, ft = -1, fpos = p0, fs = s0, fc = 0, fe = -1;
+                    int fk = K_LONG, ft = -1, fs = s0, fc = 0, fix = -1, fo = 0;
                     while (s0 < nn) {
                         const int sk = s0 + lane;
-                        const int p = (int)(((long long)p0 + (long long)lane * (long long)stp) % (long long)nn);
                         bool feas = false;
-                        int w = -1, c = 0, e = -1;
+                        int w = -1, c = 0, ix = -1, o = 0;
                         if (sk < nn) {
-                            w = L.pw[pb + p];
+                            w = pw[pb + walk_pos(hm, sk, stp, nn)];
                             if (w == OWGS_PW_BADID) {
                                 feas = true;
                             } else if (w >= 0) {
-                                feas = L.perm[w] >= m;
+                                feas = perm[w] >= m;
                                 if (mc > 1) {
-                                    c = conc_c(A, w, sl, &e);
-                                    if (c >= 1) feas = true;
+                                    c = conc_lookup(A, w, sl, &ix, &o);
+                                    feas = feas || c >= 1;
                                 }
                             }
                         }
@@ -470,15 +481,14 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                         if (fm) {
                             const int j = ffs64(fm);
                             ft = __builtin_amdgcn_readlane(w, j);
-                            fpos = __builtin_amdgcn_readlane(p, j);
                             fc = __builtin_amdgcn_readlane(c, j);
-                            fe = __builtin_amdgcn_readlane(e, j);
+                            fix = __builtin_amdgcn_readlane(ix, j);
+                            fo = __builtin_amdgcn_readlane(o, j);
                             fs = s0 + j;
                             fk = (ft == OWGS_PW_BADID) ? K_THROW : K_TARGET;
                             break;
                         }
                         s0 += 64;
-                        p0 = (int)(((long long)p0 + 64ll * (long long)stp) % (long long)nn);
                     }
                     if (lane == f) {
                         if (fk == K_LONG) {
@@ -488,35 +498,35 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                         } else {
                             kind = fk;
                             tgt = ft;
-                            pos = fpos;
                             s = fs;
-                            cval = fc;
-                            eidx = fe;
+                            c0 = fc;
+                            cidx = fix;
+                            ops0 = fo;
                         }
                     }
                 }
-                if (act && kind == K_FALLBACK && maxc > 1) {
-                    int e;
-                    cval = conc_c(A, tgt, slot, &e);
-                    eidx = e;
-                }
-                // -------------------------------------------------------- conflict groups
+                if (act && kind == K_FALLBACK && maxc > 1) c0 = conc_lookup(A, tgt, slot, &cidx, &ops0);
+
+                // -------------------------------------------------------- group by target / by fqn (slot key)
                 const bool part = act && (kind == K_TARGET || kind == K_FALLBACK);
-                const int cons = part ? ((kind == K_TARGET && maxc > 1 && cval >= 1) ? 0 : mem) : 0;
                 const bool cpart = part && maxc > 1;
                 ++iter;
                 if ((iter & 0x03FFFFFFu) == 0) {
-                    for (int t = lane; t < 2 * OWGS_STAMP_BUCKETS; t += 64) L.stT[t] = 0xFFFFFFFFu;
-                    __syncthreads();
+                    for (int t = lane; t < 2 * OWGS_STAMP_BUCKETS; t += 64) stT[t] = 0xFFFFFFFFu;
+                    wave_fence();
                     ++iter;
                 }
                 const uint32_t stamp = ((0x03FFFFFFu - (iter & 0x03FFFFFFu)) << 6) | (uint32_t)lane;
-                if (part) atomicMin(&L.stT[tgt & (OWGS_STAMP_BUCKETS - 1)], stamp);
-                if (cpart) atomicMin(&L.stS[slot & (OWGS_STAMP_BUCKETS - 1)], stamp);
-                __syncthreads();
-                const bool leadT = part && L.stT[tgt & (OWGS_STAMP_BUCKETS - 1)] == stamp;
-                const bool leadS = cpart && L.stS[slot & (OWGS_STAMP_BUCKETS - 1)] == stamp;
-                int E = 0;
+                if (part) atomicMin(&stT[tgt & (OWGS_STAMP_BUCKETS - 1)], stamp);
+                if (cpart) atomicMin(&stS[slot & (OWGS_STAMP_BUCKETS - 1)], stamp);
+                wave_fence();
+                const bool leadT = part && stT[tgt & (OWGS_STAMP_BUCKETS - 1)] == stamp;
+                const bool leadS = cpart && stS[slot & (OWGS_STAMP_BUCKETS - 1)] == stamp;
+
+                // q = earlier lanes of the same fqn at the same invoker; cons = memory this lane takes; E = memory
+                // taken by earlier lanes at the same invoker
+                int q = 0, E = 0;
+                int cons = part ? (maxc == 1 ? mem : (c_now_of(c0, 0, maxc) >= 1 ? 0 : mem)) : 0;
                 u64 pend = __ballot(part && !leadT);
                 while (pend) {
                     ++st_grp;
@@ -524,18 +534,36 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                     const int t = __builtin_amdgcn_readlane(tgt, j);
                     const u64 G = __ballot(part && tgt == t);
                     const bool in = (G >> lane) & 1;
+                    u64 Cg = G & __ballot(cpart);
+                    while (Cg) {
+                        const int j2 = ffs64(Cg);
+                        const int sl = __builtin_amdgcn_readlane(slot, j2);
+                        const u64 H = Cg & __ballot(slot == sl);
+                        if ((H >> lane) & 1) q = __popcll(H & lt_mask);
+                        Cg &= ~H;
+                    }
+                    if (in && maxc > 1) cons = c_now_of(c0, q, maxc) >= 1 ? 0 : mem;
                     const int ex = wave_excl_scan(in ? cons : 0);
                     if (in) E = ex;
                     pend &= ~G;
                 }
-                bool ssl = false;  // an earlier lane of this chunk may change this action's concurrency slots
+                // an earlier lane of the same fqn on another walk, or an earlier forced acquire of the same fqn,
+                // may create concurrency slots this lane's speculation did not see -> uncertain
+                bool unc = false;
                 pend = __ballot(cpart && !leadS);
                 while (pend) {
                     const int j = ffs64(pend);
                     const int sl = __builtin_amdgcn_readlane(slot, j);
-                    const u64 G = __ballot(cpart && slot == sl);
-                    if (((G >> lane) & 1) && (G & lt_mask)) ssl = true;
-                    pend &= ~G;
+                    const u64 Gs = __ballot(cpart && slot == sl);
+                    const int a0 = __builtin_amdgcn_readlane(a, ffs64(Gs));
+                    const u64 D = Gs & __ballot(a != a0);
+                    const u64 FB = Gs & __ballot(kind == K_FALLBACK);
+                    if ((Gs >> lane) & 1) {
+                        const bool lower = (Gs & lt_mask) != 0;
+                        if (kind == K_FALLBACK) unc = lower;
+                        else unc = lower && (((FB & lt_mask) != 0) || ((D & (lt_mask | self_bit)) != 0) || a < 0);
+                    }
+                    pend &= ~Gs;
                 }
                 // -------------------------------------------------------- decide
                 bool ok = false, rej = false;
@@ -543,14 +571,14 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                     if (kind == K_NONE || kind == K_THROW) {
                         ok = true;
                     } else if (kind == K_FALLBACK) {
-                        ok = !(maxc > 1 && ssl);
+                        ok = !(maxc > 1 && unc);
                     } else if (kind == K_TARGET) {
-                        const long long room = (long long)L.perm[tgt] - (long long)E;
+                        const long long room = (long long)perm[tgt] - (long long)E;
                         if (maxc == 1) {
                             ok = room >= mem;
                             rej = !ok;
-                        } else if (!ssl) {
-                            ok = (cval >= 1) || room >= mem;
+                        } else if (!unc) {
+                            ok = c_now_of(c0, q, maxc) >= 1 || room >= mem;
                             rej = !ok;
                         }
                     }
@@ -558,36 +586,43 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                 const u64 stop = __ballot(act && !ok);
                 const int ls = stop ? ffs64(stop) : 64;
                 const bool commit = act && lane < ls;
+
                 // -------------------------------------------------------- commit lanes [f, l*)
-                if (commit && part && maxc == 1) atomicSub(&L.perm[tgt], mem);
-                if (commit && part && maxc > 1) {
-                    // NS:63-81: concurrency slot if available, else memory (try or force) + release(maxConc-1)
-                    if (cons > 0) atomicSub(&L.perm[tgt], mem);
+                if (commit && part && cons > 0) atomicSub(&perm[tgt], mem);
+                // concurrency map: the last committed lane of each (invoker, fqn) group writes the entry
+                u64 W = __ballot(commit && cpart);
+                bool writer = false;
+                while (W) {
+                    const int j = ffs64(W);
+                    const int t = __builtin_amdgcn_readlane(tgt, j);
+                    const int sl = __builtin_amdgcn_readlane(slot, j);
+                    const u64 K = W & __ballot(tgt == t && slot == sl);
+                    if (lane == fls64(K)) writer = true;
+                    W &= ~K;
                 }
                 {
-                    u64 ins = __ballot(commit && part && maxc > 1 && eidx < 0);
+                    u64 ins = __ballot(writer && cidx < 0);
                     while (ins) {
                         const int j = ffs64(ins);
                         if (lane == j) {
-                            eidx = ctab_insert(A.ctab_key, A.ctab_mask, ctab_keyof(tgt, slot));
-                            if (eidx < 0) atomicOr(A.err, 1);
-                            else A.ctab_val[eidx] = make_int2(0, 0);
+                            cidx = ct_insert(A.ctab, A.ctab_mask, ct_key(tgt, slot));
+                            if (cidx < 0) atomicOr(A.err, 1);
+                            else A.ctab[cidx] = ct_entry(ct_key(tgt, slot), 0, 0);
                         }
-                        __threadfence_block();
+                        wave_fence();
                         ins &= ins - 1;
                     }
                 }
-                if (commit && part && maxc > 1 && eidx >= 0) {
-                    int2 v = A.ctab_val[eidx];
-                    int c = v.y > 0 ? v.x : 0, o = v.y > 0 ? v.y : 0;
-                    if (c >= 1) {
-                        c -= 1;
-                    } else {
-                        const int next2 = c + (maxc - 1);
-                        c = (next2 % maxc == 0) ? next2 - maxc : next2;
+                if (writer && cidx >= 0) {
+                    const int cn = c_now_of(c0, q, maxc);
+                    int c1;
+                    if (cn >= 1) {
+                        c1 = cn - 1;  // RS.tryAcquire(1)
+                    } else {        // memory (try or force) + RS.release(maxConcurrent - 1, false)
+                        const int next2 = cn + (maxc - 1);
+                        c1 = (next2 % maxc == 0) ? next2 - maxc : next2;
                     }
-                    o += 1;
-                    A.ctab_val[eidx] = make_int2(c, o);
+                    A.ctab[cidx] = ct_entry(ct_key(tgt, slot), c1, (ops0 > 0 ? ops0 : 0) + q + 1);
                 }
                 if (commit) {
                     int oi;
@@ -598,29 +633,37 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                     A.out_flags[i] = (kind == K_FALLBACK) ? 1 : 0;
                     if (kind == K_FALLBACK) ++st_fb;
                 }
+                // cursors (LDS, per action): steps before the committed target / after a full walk are infeasible
+                if (commit && cok && (kind == K_TARGET || (kind == K_FALLBACK && maxc == 1)))
+                    atomicMax(&cur[a], kind == K_TARGET ? s : n);
+                wave_fence();
+                if (commit && cok && kind == K_FALLBACK && maxc > 1) cur[a] = 0;  // forced slots may lie anywhere
                 // a failed full walk proves every usable pool member has permits < mem from now on
                 for (int p = 0; p < 2; ++p) {
                     const bool t = commit && kind == K_FALLBACK && fullwalk && maxc == 1 && pool == p;
-                    const int mm = wave_min(t ? mem - 1 : 0x7FFFFFFF);
-                    U[p] = min(U[p], mm);
+                    U[p] = min(U[p], wave_min(t ? mem - 1 : 0x7FFFFFFF));
                 }
                 if (commit) pending = false;
-                if (lane == ls && rej) {  // true rejection at tgt: continue the walk past it
-                    pos = jmod_step(pos, step, n);
-                    ++s;
+                // true rejection at l*: it, and every later lane of the same maxConcurrent==1 action speculated at
+                // the same walk step, continue past that step
+                if (ls < 64 && __builtin_amdgcn_readlane((int)rej, ls)) {
+                    const int as = __builtin_amdgcn_readlane(a, ls);
+                    const int ss = __builtin_amdgcn_readlane(s, ls);
+                    const int ms = __builtin_amdgcn_readlane(maxc, ls);
+                    bool adv = lane == ls;
+                    if (as >= 0 && ms == 1) adv = adv || (act && lane > ls && a == as && kind == K_TARGET && s == ss);
+                    if (adv) ++s;
+                    if (lane == ls && cok) atomicMax(&cur[a], s);
                 }
-                __threadfence_block();
-                __syncthreads();
+                wave_fence();
                 f = ls;
             }
         }
-        __threadfence_block();
-        __syncthreads();
+        wave_fence();
     }
 
-    for (int i = lane; i < A.n_slots; i += 64) A.permits[i] = L.perm[i];
+    for (int i = lane; i < A.n_slots; i += 64) A.permits[i] = perm[i];
     if (A.stats) {
-        // each lane counted its own probes; lane-uniform counters are identical in every lane
         atomicAdd(&A.stats[1], st_probe);
         if (lane == 0) {
             atomicAdd(&A.stats[0], st_iter);
@@ -651,12 +694,13 @@ extern "C" hipError_t owgs_launch_prepare(const OwgsPrepArgs* a, hipStream_t s) 
     return hipGetLastError();
 }
 
-extern "C" size_t owgs_engine_lds_bytes(int n_slots, int nm, int nb) {
-    return (size_t)(((n_slots + 3) & ~3) + ((nm + nb + 3) & ~3) + 2 * OWGS_STAMP_BUCKETS) * 4;
+extern "C" size_t owgs_engine_lds_bytes(int n_slots, int nm, int nb, int n_cursors) {
+    return (size_t)(((n_slots + 3) & ~3) + ((nm + nb + 3) & ~3) + 2 * OWGS_STAMP_BUCKETS) * 4 +
+           (size_t)((n_cursors + 3) & ~3) * 4;
 }
 
 extern "C" hipError_t owgs_launch_engine(const OwgsEngineArgs* a, hipStream_t s) {
-    const size_t lds = owgs_engine_lds_bytes(a->n_slots, a->nm, a->nb);
+    const size_t lds = owgs_engine_lds_bytes(a->n_slots, a->nm, a->nb, a->n_cursors);
     if (lds > OWGS_LDS_BYTES) return hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
