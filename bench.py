@@ -130,8 +130,9 @@ def main():
             dist.all_gather_into_tensor(gathered, health)
             b.update_health_device(len(w.inv_status), gathered[0].data_ptr(), sp)
         b.restore(sp)
-        b.replay_device(s.n_batches, d_acq.data_ptr(), d_act.data_ptr(), d_rel.data_ptr(), d_aid.data_ptr(),
-                        s.seq_base, d_out.data_ptr(), d_fl.data_ptr(), d_rf.data_ptr(), sp)
+        b.replay_device(s.n_batches, d_acq.data_ptr(), d_act.data_ptr(), len(s.act), d_rel.data_ptr(),
+                        d_aid.data_ptr(), len(s.rel_aid), s.seq_base, d_out.data_ptr(), d_fl.data_ptr(),
+                        d_rf.data_ptr(), sp)
 
     for _ in range(args.warmup):
         step()
@@ -147,8 +148,9 @@ def main():
             b.update_health_device(len(w.inv_status), gathered[0].data_ptr(), sp)
         b.restore(sp)
         evs[k][0].record(stream)
-        b.replay_device(s.n_batches, d_acq.data_ptr(), d_act.data_ptr(), d_rel.data_ptr(), d_aid.data_ptr(),
-                        s.seq_base, d_out.data_ptr(), d_fl.data_ptr(), d_rf.data_ptr(), sp)
+        b.replay_device(s.n_batches, d_acq.data_ptr(), d_act.data_ptr(), len(s.act), d_rel.data_ptr(),
+                        d_aid.data_ptr(), len(s.rel_aid), s.seq_base, d_out.data_ptr(), d_fl.data_ptr(),
+                        d_rf.data_ptr(), sp)
         evs[k][1].record(stream)
     torch.cuda.synchronize()
     if dist:

@@ -137,10 +137,11 @@ int owgs_step_sizes(owgs_ctx* ctx, int32_t pool, int32_t* out, int32_t cap, int3
 /* Stream replay with HBM-resident buffers (bench / batching thread).  Batch b first releases the activations
  * rel_aid[rel_off[b]..rel_off[b+1]) (ids into this stream; their invoker is this stream's own earlier output),
  * then publishes activations [acq_off[b], acq_off[b+1]) with action act[i] and seq = seq_base + i.
- * All pointers are device pointers; stream is a hipStream_t (NULL = default stream).  Asynchronous. */
+ * n_activations = acq_off[n_batches], n_releases = rel_off[n_batches] (given so no device read is needed).
+ * All pointers are device pointers; stream is a hipStream_t (NULL = the context's stream).  Asynchronous. */
 int owgs_replay_device(owgs_ctx* ctx, int32_t n_batches, const int64_t* acq_off, const int32_t* act,
-                       const int64_t* rel_off, const int64_t* rel_aid, uint64_t seq_base, int32_t* out_invoker,
-                       uint8_t* out_flags, uint8_t* rel_flags, void* stream);
+                       int64_t n_activations, const int64_t* rel_off, const int64_t* rel_aid, int64_t n_releases,
+                       uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, uint8_t* rel_flags, void* stream);
 /* Same with host buffers (copies in and out, synchronous). */
 int owgs_replay(owgs_ctx* ctx, int32_t n_batches, const int64_t* acq_off, const int32_t* act, const int64_t* rel_off,
                 const int64_t* rel_aid, uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags,
@@ -154,8 +155,11 @@ int owgs_restore(owgs_ctx* ctx, void* stream);
  * n bytes (InvokerState codes), e.g. the rank-0 row of an all_gather of CurrentInvokerPoolState. */
 int owgs_update_health_device(owgs_ctx* ctx, int32_t n, const uint8_t* status_dev, void* stream);
 
+/* Device self-test of the engine's wave primitives (DPP scans/reductions vs a serial computation); 0 = pass. */
+int owgs_selftest(owgs_ctx* ctx);
+
 /* Engine counters of the last replay (diagnostics): [0] chunk iterations, [1] walk probes, [2] fallbacks,
- * [3] long walks, [4] conflict groups. */
+ * [3] long walks, [4] conflict groups; [8..15] per-phase shader cycles in the diagnostic build (libowgs_prof.so). */
 int owgs_read_stats(owgs_ctx* ctx, uint64_t* out, int32_t cap);
 
 #ifdef __cplusplus

@@ -12,7 +12,7 @@ import subprocess
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
-LIB_PATH = os.path.join(PKG, "libowgs.so")
+LIB_PATH = os.environ.get("OWGS_LIB") or os.path.join(PKG, "libowgs.so")
 HEADER = os.path.join(ROOT, "include", "owgs.h")
 
 OK = 0
@@ -84,12 +84,13 @@ def lib() -> C.CDLL:
         "owgs_key_id": (C.c_int, [P, i32]),
         "owgs_state_info": (C.c_int, [P, P, P, P, P]),
         "owgs_step_sizes": (C.c_int, [P, i32, P, i32, P]),
-        "owgs_replay_device": (C.c_int, [P, i32, P, P, P, P, u64, P, P, P, P]),
+        "owgs_replay_device": (C.c_int, [P, i32, P, P, C.c_int64, P, P, C.c_int64, u64, P, P, P, P]),
         "owgs_replay": (C.c_int, [P, i32, P, P, P, P, u64, P, P, P]),
         "owgs_snapshot": (C.c_int, [P]),
         "owgs_restore": (C.c_int, [P, P]),
         "owgs_update_health_device": (C.c_int, [P, i32, P, P]),
         "owgs_read_stats": (C.c_int, [P, P, i32]),
+        "owgs_selftest": (C.c_int, [P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

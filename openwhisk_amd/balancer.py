@@ -228,12 +228,13 @@ class GpuShardingContainerPoolBalancer:
                                       np.zeros(1, np.int64)), int(stream.seq_base), _p(out), _p(fl), _p(rf)))
         return out[:n], fl[:n], rf[:nr]
 
-    def replay_device(self, n_batches, acq_off, act, rel_off, rel_aid, seq_base, out_inv, out_flags, rel_flags,
-                      stream=None):
+    def replay_device(self, n_batches, acq_off, act, n_act, rel_off, rel_aid, n_rel, seq_base, out_inv, out_flags,
+                      rel_flags, stream=None):
         """Replay with HBM-resident buffers given as device addresses (ints, e.g. torch tensor.data_ptr())."""
         vp = lambda x: C.c_void_p(int(x)) if x else None  # noqa: E731
-        self._chk(self._L.owgs_replay_device(self._h, n_batches, vp(acq_off), vp(act), vp(rel_off), vp(rel_aid),
-                                             seq_base, vp(out_inv), vp(out_flags), vp(rel_flags), vp(stream)))
+        self._chk(self._L.owgs_replay_device(self._h, n_batches, vp(acq_off), vp(act), n_act, vp(rel_off),
+                                             vp(rel_aid), n_rel, seq_base, vp(out_inv), vp(out_flags), vp(rel_flags),
+                                             vp(stream)))
 
     def snapshot(self):
         self._chk(self._L.owgs_snapshot(self._h))
@@ -245,8 +246,15 @@ class GpuShardingContainerPoolBalancer:
         self._chk(self._L.owgs_update_health_device(self._h, n, C.c_void_p(int(status_dev_ptr)),
                                                     C.c_void_p(int(stream)) if stream else None))
 
+    def selftest(self):
+        self._chk(self._L.owgs_selftest(self._h))
+
     def stats(self) -> dict:
-        out = (C.c_uint64 * 8)()
-        self._chk(self._L.owgs_read_stats(self._h, out, 8))
-        return {"iterations": out[0], "probes": out[1], "fallbacks": out[2], "long_walks": out[3],
-                "conflict_groups": out[4]}
+        out = (C.c_uint64 * 16)()
+        self._chk(self._L.owgs_read_stats(self._h, out, 16))
+        d = {"iterations": out[0], "probes": out[1], "fallbacks": out[2], "long_walks": out[3],
+             "conflict_groups": out[4]}
+        if any(out[8:16]):
+            names = ["releases", "bounds", "chunk_load", "walk", "coop_walk", "grouping", "decide_commit", "other"]
+            d["cycles"] = {k: out[8 + i] for i, k in enumerate(names)}
+        return d

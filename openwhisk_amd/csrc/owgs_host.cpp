@@ -20,6 +20,8 @@ typedef unsigned long long u64;
 
 extern "C" hipError_t owgs_launch_hash(const OwgsHashArgs* a, hipStream_t s);
 extern "C" hipError_t owgs_launch_lookup(const OwgsLookupArgs* a, hipStream_t s);
+extern "C" hipError_t owgs_launch_gather(const OwgsGatherArgs* g, hipStream_t s);
+extern "C" hipError_t owgs_launch_selftest(int* bad, int trials, hipStream_t s);
 extern "C" hipError_t owgs_launch_prepare(const OwgsPrepArgs* a, hipStream_t s);
 extern "C" hipError_t owgs_launch_engine(const OwgsEngineArgs* a, hipStream_t s);
 extern "C" size_t owgs_engine_lds_bytes(int n_slots, int nm, int nb, int n_cursors);
@@ -121,8 +123,9 @@ struct owgs_ctx {
     DevBuf<int32_t> d_a, d_b, d_out;
     DevBuf<uint8_t> d_flags, d_rflags;
     DevBuf<u64> d_seq;
-    DevBuf<int4> d_xw;
     DevBuf<int64_t> d_rel;
+    DevBuf<int4> d_info, d_rinfo;
+    DevBuf<int2> d_aux;
     // snapshot
     DevBuf<int32_t> s_permits;
     DevBuf<u64> s_ctab;
@@ -267,8 +270,33 @@ static void base_args(owgs_ctx* c, OwgsEngineArgs& A) {
 static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s) {
     int rc = lds_check(c);
     if (rc) return rc;
-    HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, 8 * sizeof(u64), s));
+    HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, 16 * sizeof(u64), s));
     HIPCHK(c, owgs_launch_engine(&A, s));
+    return OWGS_OK;
+}
+
+// dense per-activation / per-release records for the engine (owgs_gather_kernel)
+static int run_gather(owgs_ctx* c, OwgsEngineArgs& A, const int32_t* act, int64_t n_act, const int64_t* rel_aid,
+                      const int32_t* rel_inv, const int32_t* rel_act, int64_t n_rel, hipStream_t s) {
+    HIPCHK(c, c->d_info.reserve((size_t)std::max<int64_t>(n_act, 1)));
+    HIPCHK(c, c->d_aux.reserve((size_t)std::max<int64_t>(n_act, 1)));
+    HIPCHK(c, c->d_rinfo.reserve((size_t)std::max<int64_t>(n_rel, 1)));
+    OwgsGatherArgs g{};
+    g.act = act;
+    g.n_act = n_act;
+    g.act_info = c->d_act_info.p;
+    g.act_slot = c->d_act_slot.p;
+    g.info = c->d_info.p;
+    g.aux = c->d_aux.p;
+    g.rel_aid = rel_aid;
+    g.rel_inv = rel_inv;
+    g.rel_act = rel_act;
+    g.n_rel = n_rel;
+    g.rinfo = c->d_rinfo.p;
+    HIPCHK(c, owgs_launch_gather(&g, s));
+    A.info = c->d_info.p;
+    A.aux = c->d_aux.p;
+    A.rinfo = c->d_rinfo.p;
     return OWGS_OK;
 }
 
@@ -314,7 +342,7 @@ int owgs_create(const owgs_config* cfg, owgs_ctx** out) {
         return OWGS_EDEVICE;
     }
     const size_t cap = (size_t)1 << kCtabLog2;
-    if (c->d_ctab.reserve(cap) || c->d_stats.reserve(8) || c->d_err.reserve(1) ||
+    if (c->d_ctab.reserve(cap) || c->d_stats.reserve(16) || c->d_err.reserve(1) ||
         c->d_permits.reserve(1)) {
         owgs_destroy(c);
         return OWGS_ENOMEM;
@@ -354,8 +382,10 @@ void owgs_destroy(owgs_ctx* c) {
     c->d_flags.release();
     c->d_rflags.release();
     c->d_seq.release();
-    c->d_xw.release();
     c->d_rel.release();
+    c->d_info.release();
+    c->d_rinfo.release();
+    c->d_aux.release();
     c->s_ctab.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -546,7 +576,8 @@ int owgs_publish_batch(owgs_ctx* c, int32_t n, const int32_t* action, const uint
     A.seq = seq ? c->d_seq.p : nullptr;
     A.out_inv = c->d_out.p;
     A.out_flags = c->d_flags.p;
-    int rc = run_engine(c, A, c->stream);
+    int rc = run_gather(c, A, c->d_a.p, n, nullptr, nullptr, nullptr, 0, c->stream);
+    if (!rc) rc = run_engine(c, A, c->stream);
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(out_invoker, c->d_out.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(out_flags, c->d_flags.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
@@ -574,7 +605,8 @@ int owgs_release_batch(owgs_ctx* c, int32_t n, const int32_t* invoker, const int
     A.rel_inv = c->d_a.p;
     A.rel_act = c->d_b.p;
     A.rel_flags = c->d_rflags.p;
-    int rc = run_engine(c, A, c->stream);
+    int rc = run_gather(c, A, nullptr, 0, nullptr, c->d_a.p, c->d_b.p, n, c->stream);
+    if (!rc) rc = run_engine(c, A, c->stream);
     if (rc) return rc;
     if (out_flags)
         HIPCHK(c, hipMemcpyAsync(out_flags, c->d_rflags.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
@@ -589,6 +621,7 @@ int owgs_schedule_walks(owgs_ctx* c, int32_t n, const uint8_t* pool, const int32
         return OWGS_EINVAL;
     if (n == 0) return OWGS_OK;
     std::vector<int4> xw(n);
+    std::vector<int2> xa(n);
     for (int32_t i = 0; i < n; ++i) {
         if (mem_mb[i] <= 0 || max_conc[i] < 1 || max_conc[i] > OWGS_MAX_CONC || step[i] < 0 || step[i] > (1 << 30) ||
             key[i] < 0 || key[i] > OWGS_MAX_SLOTKEYS)
@@ -599,12 +632,13 @@ int owgs_schedule_walks(owgs_ctx* c, int32_t n, const uint8_t* pool, const int32
         if (np == 0) meta |= OWGS_META_EMPTY;
         else if (index[i] < 0 || index[i] >= np) meta |= OWGS_META_THROW;
         xw[i] = make_int4(index[i], step[i], mem_mb[i], (int)meta);
+        xa[i] = make_int2(key[i], -1);
     }
     (void)hipSetDevice(c->cfg.device);
     const int64_t off[2] = {0, n};
     HIPCHK(c, upload(c->d_off, off, 2, c->stream));
-    HIPCHK(c, upload(c->d_xw, xw.data(), (size_t)n, c->stream));
-    HIPCHK(c, upload(c->d_b, key, (size_t)n, c->stream));
+    HIPCHK(c, upload(c->d_info, xw.data(), (size_t)n, c->stream));
+    HIPCHK(c, upload(c->d_aux, xa.data(), (size_t)n, c->stream));
     if (seq) HIPCHK(c, upload(c->d_seq, (const u64*)seq, (size_t)n, c->stream));
     HIPCHK(c, c->d_out.reserve((size_t)n));
     HIPCHK(c, c->d_flags.reserve((size_t)n));
@@ -612,8 +646,8 @@ int owgs_schedule_walks(owgs_ctx* c, int32_t n, const uint8_t* pool, const int32
     base_args(c, A);
     A.n_batches = 1;
     A.acq_off = c->d_off.p;
-    A.xw_info = c->d_xw.p;
-    A.xw_slot = c->d_b.p;
+    A.info = c->d_info.p;
+    A.aux = c->d_aux.p;
     A.seq = seq ? c->d_seq.p : nullptr;
     A.out_inv = c->d_out.p;
     A.out_flags = c->d_flags.p;
@@ -703,11 +737,14 @@ int owgs_step_sizes(owgs_ctx* c, int32_t pool, int32_t* out, int32_t cap, int32_
 }
 
 int owgs_replay_device(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const int32_t* act,
-                       const int64_t* rel_off, const int64_t* rel_aid, uint64_t seq_base, int32_t* out_invoker,
-                       uint8_t* out_flags, uint8_t* rel_flags, void* stream) {
-    if (!c || n_batches < 0 || !acq_off || !act || !out_invoker || !out_flags) return OWGS_EINVAL;
+                       int64_t n_activations, const int64_t* rel_off, const int64_t* rel_aid, int64_t n_releases,
+                       uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, uint8_t* rel_flags, void* stream) {
+    if (!c || n_batches < 0 || !acq_off || !act || !out_invoker || !out_flags || n_activations < 0 ||
+        n_activations >= ((int64_t)1 << 31) || n_releases < 0 || (n_releases > 0 && (!rel_off || !rel_aid)))
+        return OWGS_EINVAL;
     if (n_batches == 0) return OWGS_OK;
     (void)hipSetDevice(c->cfg.device);
+    hipStream_t hs = stream ? (hipStream_t)stream : c->stream;
     OwgsEngineArgs A;
     base_args(c, A);
     A.n_batches = n_batches;
@@ -719,7 +756,9 @@ int owgs_replay_device(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, c
     A.out_inv = out_invoker;
     A.out_flags = out_flags;
     A.rel_flags = rel_flags;
-    return run_engine(c, A, stream ? (hipStream_t)stream : c->stream);
+    int rc = run_gather(c, A, act, n_activations, rel_aid, nullptr, nullptr, n_releases, hs);
+    if (rc) return rc;
+    return run_engine(c, A, hs);
 }
 
 int owgs_replay(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const int32_t* act, const int64_t* rel_off,
@@ -743,8 +782,8 @@ int owgs_replay(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const in
     HIPCHK(c, c->d_out.reserve((size_t)n_act));
     HIPCHK(c, c->d_flags.reserve((size_t)n_act));
     HIPCHK(c, c->d_rflags.reserve((size_t)n_rel));
-    int rc = owgs_replay_device(c, n_batches, c->d_off.p, c->d_a.p, c->d_off.p + n_batches + 1, c->d_rel.p, seq_base,
-                                c->d_out.p, c->d_flags.p, c->d_rflags.p, nullptr);
+    int rc = owgs_replay_device(c, n_batches, c->d_off.p, c->d_a.p, n_act, c->d_off.p + n_batches + 1, c->d_rel.p,
+                                n_rel, seq_base, c->d_out.p, c->d_flags.p, c->d_rflags.p, nullptr);
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(out_invoker, c->d_out.p, (size_t)n_act * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(out_flags, c->d_flags.p, (size_t)n_act, hipMemcpyDeviceToHost, c->stream));
@@ -791,13 +830,25 @@ int owgs_update_health_device(owgs_ctx* c, int32_t n, const uint8_t* status_dev,
     return rc;
 }
 
+int owgs_selftest(owgs_ctx* c) {
+    if (!c) return OWGS_EINVAL;
+    (void)hipSetDevice(c->cfg.device);
+    HIPCHK(c, hipMemsetAsync(c->d_err.p, 0, sizeof(int32_t), c->stream));
+    HIPCHK(c, owgs_launch_selftest(c->d_err.p, 64, c->stream));
+    int32_t bad = 0;
+    HIPCHK(c, hipMemcpyAsync(&bad, c->d_err.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_err.p, 0, sizeof(int32_t), c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return bad ? c->fail(OWGS_EDEVICE, "device self-test mismatch") : OWGS_OK;
+}
+
 int owgs_read_stats(owgs_ctx* c, uint64_t* out, int32_t cap) {
     if (!c || !out) return OWGS_EINVAL;
     (void)hipSetDevice(c->cfg.device);
-    u64 v[8];
+    u64 v[16];
     HIPCHK(c, hipDeviceSynchronize());
     HIPCHK(c, hipMemcpy(v, c->d_stats.p, sizeof(v), hipMemcpyDeviceToHost));
-    for (int32_t i = 0; i < cap && i < 8; ++i) out[i] = v[i];
+    for (int32_t i = 0; i < cap && i < 16; ++i) out[i] = v[i];
     return OWGS_OK;
 }
 

@@ -66,9 +66,10 @@ struct OwgsEngineArgs {
     const int32_t* rel_act;
     unsigned long long seq_base;
     const unsigned long long* seq; // optional explicit seq per activation
-    // explicit-walk mode (owgs_schedule_walks): per activation {home, step, mem, meta} + slot
-    const int4* xw_info;
-    const int32_t* xw_slot;
+    // dense per-activation / per-release records built by owgs_gather_kernel (or by the host for explicit walks)
+    const int4* info;   // [n_act] {home, step, mem, meta}
+    const int2* aux;    // [n_act] {slot key, action handle or -1}
+    const int4* rinfo;  // [n_rel] {aid (or invoker if rel_inv), mem, meta, slot key}
     int32_t* out_inv;
     uint8_t* out_flags;
     uint8_t* rel_flags;
@@ -87,6 +88,20 @@ struct OwgsHashArgs {
     int32_t n;
     int32_t raw;
     int32_t* out;
+};
+
+struct OwgsGatherArgs {
+    const int32_t* act;
+    int64_t n_act;
+    const int4* act_info;
+    const int32_t* act_slot;
+    int4* info;
+    int2* aux;
+    const int64_t* rel_aid;
+    const int32_t* rel_inv;
+    const int32_t* rel_act;
+    int64_t n_rel;
+    int4* rinfo;
 };
 
 struct OwgsLookupArgs {

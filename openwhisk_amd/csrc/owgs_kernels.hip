@@ -39,6 +39,22 @@ typedef unsigned long long u64;
 
 #define KPROBE 4
 
+// diagnostic build (-DOWGS_PROFILE, libowgs_prof.so): s_memtime cycle accounting per engine phase into stats[8..15]
+#ifdef OWGS_PROFILE
+#define PT_DECL                 \
+    u64 pt_acc[8] = {0};        \
+    u64 pt_t = __builtin_amdgcn_s_memtime();
+#define PT(k)                                          \
+    {                                                  \
+        const u64 _t = __builtin_amdgcn_s_memtime();   \
+        pt_acc[k] += _t - pt_t;                        \
+        pt_t = _t;                                     \
+    }
+#else
+#define PT_DECL
+#define PT(k)
+#endif
+
 // ------------------------------------------------------------------------------------------------ helpers
 __device__ __forceinline__ u64 splitmix64(u64 x) {
     x += 0x9E3779B97F4A7C15ULL;
@@ -57,9 +73,11 @@ __device__ __forceinline__ int jmod_step(int pos, int step, int n) {
     return (int)((int)((unsigned)pos + (unsigned)step) % n);  // Java (index + step) % numInvokers
 }
 
-// pool position of walk step s: (home + s*step) mod n  (home in [0,n), step >= 0)
+// pool position of walk step s: (home + s*step) mod n.  home < n, step < 2^30 and s < n <= 32767 (engine limits)
+// keep every operand below 2^32, so 32-bit unsigned arithmetic is exact.
 __device__ __forceinline__ int walk_pos(int home, int s, int step, int n) {
-    return (int)(((long long)home + (long long)s * (long long)step) % (long long)n);
+    const uint32_t un = (uint32_t)n;
+    return (int)(((uint32_t)home + (uint32_t)s * ((uint32_t)step % un)) % un);
 }
 
 __device__ __forceinline__ int ffs64(u64 m) { return __ffsll((long long)m) - 1; }
@@ -67,27 +85,45 @@ __device__ __forceinline__ int fls64(u64 m) { return 63 - __clzll((long long)m);
 
 __device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
-__device__ __forceinline__ int wave_excl_scan(int v) {
-    const int lane = __lane_id();
-    int x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        int y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
-    return x - v;
+// DPP (GFX9 row_shr / row_bcast) wave64 scans: no LDS round trip, ~6 VALU ops.
+template <int CTRL, int ROWM>
+__device__ __forceinline__ int dpp_add_src(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWM, 0xf, true);  // out-of-row / masked lanes read 0
 }
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    v += dpp_add_src<0x111, 0xf>(v);  // row_shr:1
+    v += dpp_add_src<0x112, 0xf>(v);  // row_shr:2
+    v += dpp_add_src<0x114, 0xf>(v);  // row_shr:4
+    v += dpp_add_src<0x118, 0xf>(v);  // row_shr:8
+    v += dpp_add_src<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+    v += dpp_add_src<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+__device__ __forceinline__ int wave_excl_scan(int v) { return wave_incl_scan(v) - v; }
 
+template <int CTRL, int ROWM>
+__device__ __forceinline__ int dpp_keep(int old, int v) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWM, 0xf, false);  // invalid source lanes keep `old`
+}
 __device__ __forceinline__ int wave_max(int v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d, 64));
-    return v;
+    const int I = (int)0x80000000;
+    v = max(v, dpp_keep<0x111, 0xf>(I, v));
+    v = max(v, dpp_keep<0x112, 0xf>(I, v));
+    v = max(v, dpp_keep<0x114, 0xf>(I, v));
+    v = max(v, dpp_keep<0x118, 0xf>(I, v));
+    v = max(v, dpp_keep<0x142, 0xa>(I, v));
+    v = max(v, dpp_keep<0x143, 0xc>(I, v));
+    return __builtin_amdgcn_readlane(v, 63);
 }
-
 __device__ __forceinline__ int wave_min(int v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v = min(v, __shfl_xor(v, d, 64));
-    return v;
+    const int I = 0x7FFFFFFF;
+    v = min(v, dpp_keep<0x111, 0xf>(I, v));
+    v = min(v, dpp_keep<0x112, 0xf>(I, v));
+    v = min(v, dpp_keep<0x114, 0xf>(I, v));
+    v = min(v, dpp_keep<0x118, 0xf>(I, v));
+    v = min(v, dpp_keep<0x142, 0xa>(I, v));
+    v = min(v, dpp_keep<0x143, 0xc>(I, v));
+    return __builtin_amdgcn_readlane(v, 63);
 }
 
 // ---- concurrency table: entry = key32 << 32 | val32; key32 = (inv+1) | slot << 15; val32 = c | ops << 12
@@ -186,6 +222,29 @@ __global__ __launch_bounds__(256) void owgs_lookup_kernel(OwgsLookupArgs a) {
     a.out[i] = make_int2(ct_c(e), ct_ops(e));
 }
 
+// dense per-activation / per-release records (one coalesced load each in the engine instead of dependent gathers)
+__global__ __launch_bounds__(256) void owgs_gather_kernel(OwgsGatherArgs g) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < g.n_act; i += stride) {
+        const int a = g.act[i];
+        g.info[i] = g.act_info[a];
+        g.aux[i] = make_int2(g.act_slot[a], a);
+    }
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < g.n_rel; r += stride) {
+        int x, a;
+        if (g.rel_inv) {
+            x = g.rel_inv[r];
+            a = g.rel_act[r];
+        } else {
+            const int64_t aid = g.rel_aid[r];
+            x = (int)aid;
+            a = g.act[aid];
+        }
+        const int4 ai = g.act_info[a];
+        g.rinfo[r] = make_int4(x, ai.z, ai.w, g.act_slot[a]);
+    }
+}
+
 // home/step selection (SCPB:266-268)
 __global__ __launch_bounds__(256) void owgs_prepare_kernel(OwgsPrepArgs a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -254,6 +313,7 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
     __syncthreads();
 
     u64 st_iter = 0, st_probe = 0, st_fb = 0, st_long = 0, st_grp = 0;
+    PT_DECL
     uint32_t iter = 0;
     const u64 lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
     const u64 self_bit = 1ull << lane;
@@ -264,23 +324,13 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
         for (int64_t r0 = r_beg; r0 < r_end; r0 += 64) {
             const int64_t r = r0 + lane;
             const bool valid = r < r_end;
-            int inv = -1, a = 0;
+            int inv = -1, mem = 0, maxc = 1, slot = 0;
             if (valid) {
-                if (A.rel_inv) {
-                    inv = A.rel_inv[r];
-                    a = A.rel_act[r];
-                } else {
-                    const int64_t aid = A.rel_aid[r];
-                    inv = A.out_inv[aid];
-                    a = A.act[aid];
-                }
-            }
-            int mem = 0, maxc = 1, slot = 0;
-            if (valid) {
-                const int4 info = A.act_info[a];
-                mem = info.z;
-                maxc = info.w & OWGS_META_MAXC_MASK;
-                slot = A.act_slot[a];
+                const int4 ri = A.rinfo[r];
+                inv = A.rel_inv ? ri.x : A.out_inv[ri.x];
+                mem = ri.y;
+                maxc = ri.z & OWGS_META_MAXC_MASK;
+                slot = ri.w;
             }
             uint8_t flag = 0;
             bool simple = false, conc = false;
@@ -343,6 +393,7 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
             }
             if (valid && A.rel_flags) A.rel_flags[r] = flag;
             wave_fence();
+            PT(0);
         }
 
         // ================================================================ per-batch bounds and cursors
@@ -359,6 +410,7 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
         }
         for (int i = lane; i < n_cur; i += 64) cur[i] = 0;
         wave_fence();
+        PT(1);
 
         // ================================================================ acquires (SCPB:398-436, NS:32-91)
         const int64_t a_beg = A.acq_off[b], a_end = A.acq_off[b + 1];
@@ -367,19 +419,14 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
             bool pending = i < a_end;
             int a = -1, home = 0, step = 0, mem = 0, meta = 0, slot = 0;
             if (pending) {
-                int4 info;
-                if (A.xw_info) {
-                    info = A.xw_info[i];
-                    slot = A.xw_slot[i];
-                } else {
-                    a = A.act[i];
-                    info = A.act_info[a];
-                    slot = A.act_slot[a];
-                }
+                const int4 info = A.info[i];
+                const int2 ax = A.aux[i];
                 home = info.x;
                 step = info.y;
                 mem = info.z;
                 meta = info.w;
+                slot = ax.x;
+                a = ax.y;
             }
             const u64 seq = A.seq ? A.seq[pending ? i : a_beg] : (A.seq_base + (u64)i);
             const int maxc = meta & OWGS_META_MAXC_MASK;
@@ -401,10 +448,11 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
             }
 
             int f = 0;
+            PT(2);
             while (__ballot(pending)) {
                 ++st_iter;
                 // -------------------------------------------------------- speculate targets against state at f
-                int kind = K_NONE, tgt = -1, c0 = 0, cidx = -1, ops0 = 0;
+                int kind = K_NONE, tgt = -1, c0 = 0, cidx = -1, ops0 = 0, pv = 0;
                 bool fullwalk = false;
                 const bool act = pending && lane >= f;
                 if (act) {
@@ -427,7 +475,8 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                                 break;
                             }
                             if (w >= 0) {
-                                bool feas = perm[w] >= mem;
+                                const int pw_perm = perm[w];
+                                bool feas = pw_perm >= mem;
                                 int c = 0, ix = -1, o = 0;
                                 if (maxc > 1) {
                                     c = conc_lookup(A, w, slot, &ix, &o);
@@ -439,6 +488,7 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                                     c0 = c;
                                     cidx = ix;
                                     ops0 = o;
+                                    pv = pw_perm;
                                     break;
                                 }
                             }
@@ -447,6 +497,7 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                         }
                     }
                 }
+                PT(3);
                 // -------------------------------------------------------- frontier lane with a long walk:
                 // wave-cooperative scan of 64 walk steps per round (ballot picks the first feasible one)
                 if (__builtin_amdgcn_readlane(kind, f) == K_LONG) {
@@ -459,17 +510,18 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                     const int m = __builtin_amdgcn_readlane(mem, f);
                     const int mc = __builtin_amdgcn_readlane(maxc, f);
                     const int sl = __builtin_amdgcn_readlane(slot, f);
-                    int fk = K_LONG, ft = -1, fs = s0, fc = 0, fix = -1, fo = 0;
+                    int fk = K_LONG, ft = -1, fs = s0, fc = 0, fix = -1, fo = 0, fp = 0;
                     while (s0 < nn) {
                         const int sk = s0 + lane;
                         bool feas = false;
-                        int w = -1, c = 0, ix = -1, o = 0;
+                        int w = -1, c = 0, ix = -1, o = 0, pvv = 0;
                         if (sk < nn) {
                             w = pw[pb + walk_pos(hm, sk, stp, nn)];
                             if (w == OWGS_PW_BADID) {
                                 feas = true;
                             } else if (w >= 0) {
-                                feas = perm[w] >= m;
+                                pvv = perm[w];
+                                feas = pvv >= m;
                                 if (mc > 1) {
                                     c = conc_lookup(A, w, sl, &ix, &o);
                                     feas = feas || c >= 1;
@@ -484,6 +536,7 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                             fc = __builtin_amdgcn_readlane(c, j);
                             fix = __builtin_amdgcn_readlane(ix, j);
                             fo = __builtin_amdgcn_readlane(o, j);
+                            fp = __builtin_amdgcn_readlane(pvv, j);
                             fs = s0 + j;
                             fk = (ft == OWGS_PW_BADID) ? K_THROW : K_TARGET;
                             break;
@@ -502,10 +555,12 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                             c0 = fc;
                             cidx = fix;
                             ops0 = fo;
+                            pv = fp;
                         }
                     }
                 }
                 if (act && kind == K_FALLBACK && maxc > 1) c0 = conc_lookup(A, tgt, slot, &cidx, &ops0);
+                PT(4);
 
                 // -------------------------------------------------------- group by target / by fqn (slot key)
                 const bool part = act && (kind == K_TARGET || kind == K_FALLBACK);
@@ -565,6 +620,7 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                     }
                     pend &= ~Gs;
                 }
+                PT(5);
                 // -------------------------------------------------------- decide
                 bool ok = false, rej = false;
                 if (act) {
@@ -573,7 +629,7 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                     } else if (kind == K_FALLBACK) {
                         ok = !(maxc > 1 && unc);
                     } else if (kind == K_TARGET) {
-                        const long long room = (long long)perm[tgt] - (long long)E;
+                        const long long room = (long long)pv - (long long)E;
                         if (maxc == 1) {
                             ok = room >= mem;
                             rej = !ok;
@@ -639,9 +695,11 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                 wave_fence();
                 if (commit && cok && kind == K_FALLBACK && maxc > 1) cur[a] = 0;  // forced slots may lie anywhere
                 // a failed full walk proves every usable pool member has permits < mem from now on
-                for (int p = 0; p < 2; ++p) {
-                    const bool t = commit && kind == K_FALLBACK && fullwalk && maxc == 1 && pool == p;
-                    U[p] = min(U[p], wave_min(t ? mem - 1 : 0x7FFFFFFF));
+                if (__ballot(commit && kind == K_FALLBACK && fullwalk && maxc == 1)) {
+                    for (int p = 0; p < 2; ++p) {
+                        const bool t = commit && kind == K_FALLBACK && fullwalk && maxc == 1 && pool == p;
+                        U[p] = min(U[p], wave_min(t ? mem - 1 : 0x7FFFFFFF));
+                    }
                 }
                 if (commit) pending = false;
                 // true rejection at l*: it, and every later lane of the same maxConcurrent==1 action speculated at
@@ -657,6 +715,7 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                 }
                 wave_fence();
                 f = ls;
+                PT(6);
             }
         }
         wave_fence();
@@ -670,15 +729,50 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
             atomicAdd(&A.stats[2], st_fb);
             atomicAdd(&A.stats[3], st_long);
             atomicAdd(&A.stats[4], st_grp);
+#ifdef OWGS_PROFILE
+            for (int k = 0; k < 8; ++k) atomicAdd(&A.stats[8 + k], pt_acc[k]);
+#endif
         }
     }
 }
 
+// ------------------------------------------------------------------------------------------------ self-test
+// DPP scan / reduction helpers against a serial computation (one wave per trial)
+__global__ __launch_bounds__(64) void owgs_selftest_kernel(int* bad, int trials) {
+    const int lane = threadIdx.x;
+    for (int t = 0; t < trials; ++t) {
+        const uint32_t h = ct_hash((uint32_t)(t * 64 + lane) * 2654435761u);
+        const int v = (int)(h % 2001u) - 1000;
+        const int inc = wave_incl_scan(v), exc = wave_excl_scan(v), mx = wave_max(v), mn = wave_min(v);
+        int ref_inc = 0, ref_mx = (int)0x80000000, ref_mn = 0x7FFFFFFF;
+        for (int j = 0; j < 64; ++j) {
+            const int vj = __shfl(v, j, 64);
+            if (j <= lane) ref_inc += vj;
+            ref_mx = max(ref_mx, vj);
+            ref_mn = min(ref_mn, vj);
+        }
+        if (inc != ref_inc || exc != ref_inc - v || mx != ref_mx || mn != ref_mn) atomicAdd(bad, 1);
+    }
+}
+
 // ------------------------------------------------------------------------------------------------ launchers
+extern "C" hipError_t owgs_launch_selftest(int* bad, int trials, hipStream_t s) {
+    hipLaunchKernelGGL(owgs_selftest_kernel, dim3(1), dim3(64), 0, s, bad, trials);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t owgs_launch_hash(const OwgsHashArgs* a, hipStream_t s) {
     if (a->n <= 0) return hipSuccess;
     const int blocks = (a->n * 64 + 255) / 256;
     hipLaunchKernelGGL(owgs_hash_kernel, dim3(blocks), dim3(256), 0, s, *a);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t owgs_launch_gather(const OwgsGatherArgs* g, hipStream_t s) {
+    const int64_t n = g->n_act > g->n_rel ? g->n_act : g->n_rel;
+    if (n <= 0) return hipSuccess;
+    const int64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(owgs_gather_kernel, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0, s, *g);
     return hipGetLastError();
 }
 

@@ -20,6 +20,10 @@ def gpu(**kw):
     return GpuShardingContainerPoolBalancer(**kw)
 
 
+def test_device_selftest():
+    gpu().selftest()
+
+
 # ----------------------------------------------------------------------------------------------- hashing
 def test_generate_hash_on_gpu_matches_jls():
     names = [("invocationSpace", "testspace/testname"), ("", "polygenelubricants"), ("a", "b"), ("ns", "x" * 300),

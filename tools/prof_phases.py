@@ -1,0 +1,31 @@
+"""Diagnostic: per-phase engine cycles (OWGS_LIB=openwhisk_amd/libowgs_prof.so) for several workloads."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from openwhisk_amd import GpuShardingContainerPoolBalancer  # noqa: E402
+from openwhisk_amd import workload as W  # noqa: E402
+
+configs = sys.argv[1:] or ["headline", "c2", "c3", "c4"]
+for name in configs:
+    n = None if name != "c3" else 300_000
+    w = W.config(name, n_activations=n)
+    b = GpuShardingContainerPoolBalancer(managed_fraction=w.managed_fraction, blackbox_fraction=w.blackbox_fraction,
+                                         rng_seed=w.rng_seed)
+    b.update_invokers_arrays(w.inv_ids, w.inv_mem, w.inv_status)
+    b.update_cluster(w.cluster_size)
+    b.register_actions(w.actions)
+    b.snapshot()
+    b.replay(w.stream)
+    b.restore()
+    t = time.perf_counter()
+    b.replay(w.stream)
+    dt = time.perf_counter() - t
+    st = b.stats()
+    cyc = st.pop("cycles", {})
+    tot = sum(cyc.values()) or 1
+    print(f"{name}: n={w.n_activations} batches={w.stream.n_batches} {dt*1e3:.1f} ms  {w.n_activations/dt:.3g}/s  {st}")
+    print("   cycles/activation:", {k: round(v / w.n_activations, 1) for k, v in cyc.items()},
+          "share:", {k: round(v / tot, 3) for k, v in cyc.items()})
