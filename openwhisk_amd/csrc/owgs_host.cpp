@@ -631,7 +631,7 @@ int owgs_schedule_walks(owgs_ctx* c, int32_t n, const uint8_t* pool, const int32
         uint32_t meta = (uint32_t)max_conc[i] | ((uint32_t)p << OWGS_META_POOL_SHIFT);
         if (np == 0) meta |= OWGS_META_EMPTY;
         else if (index[i] < 0 || index[i] >= np) meta |= OWGS_META_THROW;
-        xw[i] = make_int4(index[i], step[i], mem_mb[i], (int)meta);
+        xw[i] = make_int4(index[i], np > 0 ? step[i] % np : 0, mem_mb[i], (int)meta);  // same walk (Java %)
         xa[i] = make_int2(key[i], -1);
     }
     (void)hipSetDevice(c->cfg.device);

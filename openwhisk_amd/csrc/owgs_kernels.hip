@@ -69,15 +69,19 @@ __device__ __forceinline__ uint32_t rng_index(u64 seed, u64 seq, uint32_t n) {
     return (uint32_t)((u * (u64)n) >> 32);
 }
 
-__device__ __forceinline__ int jmod_step(int pos, int step, int n) {
-    return (int)((int)((unsigned)pos + (unsigned)step) % n);  // Java (index + step) % numInvokers
+// (index + step) % numInvokers (SCPB:429) for index, step in [0, n]: one conditional subtract, no division
+__device__ __forceinline__ int next_pos(int pos, int step, int n) {
+    const int p = pos + step;
+    return p >= n ? p - n : p;
 }
 
-// pool position of walk step s: (home + s*step) mod n.  home < n, step < 2^30 and s < n <= 32767 (engine limits)
-// keep every operand below 2^32, so 32-bit unsigned arithmetic is exact.
-__device__ __forceinline__ int walk_pos(int home, int s, int step, int n) {
-    const uint32_t un = (uint32_t)n;
-    return (int)(((uint32_t)home + (uint32_t)s * ((uint32_t)step % un)) % un);
+// x mod R for 0 <= x < 2^24, 1 <= R < 2^24 without an integer division (float reciprocal, one correction step)
+__device__ __forceinline__ int mod_small(int x, int R) {
+    const int q = (int)((float)x * __builtin_amdgcn_rcpf((float)R));
+    int r = x - q * R;
+    if (r < 0) r += R;
+    if (r >= R) r -= R;
+    return r;
 }
 
 __device__ __forceinline__ int ffs64(u64 m) { return __ffsll((long long)m) - 1; }
@@ -265,7 +269,7 @@ __global__ __launch_bounds__(256) void owgs_prepare_kernel(OwgsPrepArgs a) {
         home = h % n;
         const int si = h % k;
         if (si < 0 || home < 0) meta |= OWGS_META_THROW;
-        else step = steps[si];
+        else step = steps[si] % n;  // same walk; lets the engine advance with one conditional subtract
     }
     a.act_info[i] = make_int4(home, step, a.mem[i], (int)meta);
 }
@@ -291,7 +295,7 @@ __device__ __forceinline__ void fallback_target(const OwgsEngineArgs& A, int poo
 __device__ __forceinline__ int c_now_of(int c0, int q, int R) {
     const int x = q - c0;
     if (x < 0) return c0 - q;
-    const int r = x % R;
+    const int r = mod_small(x, R);
     return r == 0 ? 0 : R - r;
 }
 
@@ -374,12 +378,12 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
             bool mem_rel = false;
             if (conc) {
                 // RS.release(1, opComplete = true) applied rank+1 times to (c0, o0), reductionSize = maxConcurrent
-                if (rank < o0) mem_rel = ((c0 + rank + 1) % maxc) == 0;
+                if (rank < o0) mem_rel = mod_small(c0 + rank + 1, maxc) == 0;
                 else flag = OWGS_REL_NOSUCH_BIT;  // entry already removed by an earlier release in this group
             }
             if (conc && rank == 0) {
                 const int j = min(gsz, o0);
-                int c1 = (c0 + j) % maxc;
+                int c1 = mod_small(c0 + j, maxc);
                 const int o1 = o0 - j;
                 if (o1 == 0) c1 = 0;  // actionRelease: entry removed (NS:109-111)
                 A.ctab[idx] = ct_entry(ct_key(inv, slot), c1, o1);
@@ -434,7 +438,7 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
             const int n = pool ? A.nb : A.nm;
             const int pwb = pool ? A.nm : 0;
             const bool cok = (meta & OWGS_META_CURSOR) && a >= 0 && a < n_cur;
-            int s = 0;
+            int s = 0, pos = home;  // walk step and its pool position, kept across iterations
 
             if (pending) {
                 int ok_kind = -1;
@@ -456,12 +460,17 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                 bool fullwalk = false;
                 const bool act = pending && lane >= f;
                 if (act) {
-                    if (cok) s = max(s, cur[a]);
+                    if (cok) {  // cursor = walk step << 16 | pool position
+                        const int cv = cur[a];
+                        if ((cv >> 16) > s) {
+                            s = cv >> 16;
+                            pos = cv & 0xFFFF;
+                        }
+                    }
                     if (maxc == 1 && mem > U[pool] && ((A.shortcut_ok >> pool) & 1)) {
                         fallback_target(A, pool, seq, &kind, &tgt);  // every usable permit < mem: walk fails
                     } else {
                         kind = K_LONG;
-                        int pos = walk_pos(home, s, step, n);
                         for (int k = 0; k < KPROBE; ++k) {
                             if (s >= n) {  // every pool position probed: the n+2-probe walk fails (SCPB:417)
                                 fallback_target(A, pool, seq, &kind, &tgt);
@@ -492,7 +501,7 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                                     break;
                                 }
                             }
-                            pos = jmod_step(pos, step, n);
+                            pos = next_pos(pos, step, n);
                             ++s;
                         }
                     }
@@ -503,20 +512,23 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                 if (__builtin_amdgcn_readlane(kind, f) == K_LONG) {
                     ++st_long;
                     int s0 = __builtin_amdgcn_readlane(s, f);
-                    const int hm = __builtin_amdgcn_readlane(home, f);
+                    int p0 = __builtin_amdgcn_readlane(pos, f);
                     const int stp = __builtin_amdgcn_readlane(step, f);
                     const int nn = __builtin_amdgcn_readlane(n, f);
                     const int pb = __builtin_amdgcn_readlane(pwb, f);
                     const int m = __builtin_amdgcn_readlane(mem, f);
                     const int mc = __builtin_amdgcn_readlane(maxc, f);
                     const int sl = __builtin_amdgcn_readlane(slot, f);
-                    int fk = K_LONG, ft = -1, fs = s0, fc = 0, fix = -1, fo = 0, fp = 0;
+                    int fk = K_LONG, ft = -1, fs = s0, fc = 0, fix = -1, fo = 0, fp = 0, fpos = p0;
+                    const int loff = (int)(((uint32_t)lane * (uint32_t)stp) % (uint32_t)nn);
+                    const int boff = (int)((64u * (uint32_t)stp) % (uint32_t)nn);
                     while (s0 < nn) {
                         const int sk = s0 + lane;
+                        const int p = next_pos(p0, loff, nn);
                         bool feas = false;
                         int w = -1, c = 0, ix = -1, o = 0, pvv = 0;
                         if (sk < nn) {
-                            w = pw[pb + walk_pos(hm, sk, stp, nn)];
+                            w = pw[pb + p];
                             if (w == OWGS_PW_BADID) {
                                 feas = true;
                             } else if (w >= 0) {
@@ -537,11 +549,13 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                             fix = __builtin_amdgcn_readlane(ix, j);
                             fo = __builtin_amdgcn_readlane(o, j);
                             fp = __builtin_amdgcn_readlane(pvv, j);
+                            fpos = __builtin_amdgcn_readlane(p, j);
                             fs = s0 + j;
                             fk = (ft == OWGS_PW_BADID) ? K_THROW : K_TARGET;
                             break;
                         }
                         s0 += 64;
+                        p0 = next_pos(p0, boff, nn);
                     }
                     if (lane == f) {
                         if (fk == K_LONG) {
@@ -552,6 +566,7 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                             kind = fk;
                             tgt = ft;
                             s = fs;
+                            pos = fpos;
                             c0 = fc;
                             cidx = fix;
                             ops0 = fo;
@@ -676,7 +691,7 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                         c1 = cn - 1;  // RS.tryAcquire(1)
                     } else {        // memory (try or force) + RS.release(maxConcurrent - 1, false)
                         const int next2 = cn + (maxc - 1);
-                        c1 = (next2 % maxc == 0) ? next2 - maxc : next2;
+                        c1 = (mod_small(next2, maxc) == 0) ? next2 - maxc : next2;
                     }
                     A.ctab[cidx] = ct_entry(ct_key(tgt, slot), c1, (ops0 > 0 ? ops0 : 0) + q + 1);
                 }
@@ -691,7 +706,7 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                 }
                 // cursors (LDS, per action): steps before the committed target / after a full walk are infeasible
                 if (commit && cok && (kind == K_TARGET || (kind == K_FALLBACK && maxc == 1)))
-                    atomicMax(&cur[a], kind == K_TARGET ? s : n);
+                    atomicMax(&cur[a], kind == K_TARGET ? ((s << 16) | pos) : (n << 16));
                 wave_fence();
                 if (commit && cok && kind == K_FALLBACK && maxc > 1) cur[a] = 0;  // forced slots may lie anywhere
                 // a failed full walk proves every usable pool member has permits < mem from now on
@@ -710,8 +725,11 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                     const int ms = __builtin_amdgcn_readlane(maxc, ls);
                     bool adv = lane == ls;
                     if (as >= 0 && ms == 1) adv = adv || (act && lane > ls && a == as && kind == K_TARGET && s == ss);
-                    if (adv) ++s;
-                    if (lane == ls && cok) atomicMax(&cur[a], s);
+                    if (adv) {
+                        pos = next_pos(pos, step, n);
+                        ++s;
+                    }
+                    if (lane == ls && cok) atomicMax(&cur[a], (s << 16) | pos);
                 }
                 wave_fence();
                 f = ls;
