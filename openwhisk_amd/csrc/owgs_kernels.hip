@@ -275,22 +275,6 @@ __global__ __launch_bounds__(256) void owgs_prepare_kernel(OwgsPrepArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------ engine
-// fallback target (SCPB:417-424): H = usable pool members in pool order, r = H[rng(seq) mod |H|]
-__device__ __forceinline__ void fallback_target(const OwgsEngineArgs& A, int pool, u64 seq, int* kind, int* tgt) {
-    const int hc = pool ? A.hb : A.hm;
-    if (hc <= 0) {
-        *kind = K_NONE;
-        return;
-    }
-    const int r = A.hlist[(pool ? A.hm : 0) + (int)rng_index(A.rng_seed, seq, (uint32_t)hc)];
-    if (r < 0 || r >= A.n_slots) {
-        *kind = K_THROW;
-        return;
-    }
-    *kind = K_FALLBACK;
-    *tgt = r;
-}
-
 // concurrency slots an acquisition finds, given c0 at state f and q earlier same-fqn lanes at the same invoker
 __device__ __forceinline__ int c_now_of(int c0, int q, int R) {
     const int x = q - c0;
@@ -299,24 +283,33 @@ __device__ __forceinline__ int c_now_of(int c0, int q, int R) {
     return r == 0 ? 0 : R - r;
 }
 
+__device__ __forceinline__ uint32_t next_stamp(uint32_t& iter, uint32_t* st, int lane) {
+    ++iter;
+    if ((iter & 0x03FFFFFFu) == 0) {  // stamps are (2^26 - iter) << 6 | lane: re-arm the tables on wrap
+        for (int t = lane; t < 2 * OWGS_STAMP_BUCKETS; t += 64) st[t] = 0xFFFFFFFFu;
+        wave_fence();
+        ++iter;
+    }
+    return ((0x03FFFFFFu - (iter & 0x03FFFFFFu)) << 6) | (uint32_t)lane;
+}
+
 __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
     extern __shared__ __attribute__((aligned(16))) int32_t lds_raw[];
     const int lane = threadIdx.x;
-    const int nsl_al = (A.n_slots + 3) & ~3;
-    const int npw_al = (A.nm + A.nb + 3) & ~3;
+    const int n_slots = A.n_slots, nm = A.nm, nb = A.nb;
     int32_t* perm = lds_raw;
-    int32_t* pw = lds_raw + nsl_al;
-    uint32_t* stT = (uint32_t*)(pw + npw_al);
+    int32_t* pw = lds_raw + ((n_slots + 3) & ~3);
+    uint32_t* stT = (uint32_t*)(pw + ((nm + nb + 3) & ~3));
     uint32_t* stS = stT + OWGS_STAMP_BUCKETS;
     int32_t* cur = (int32_t*)(stS + OWGS_STAMP_BUCKETS);
     const int n_cur = A.n_cursors;
 
-    for (int i = lane; i < A.n_slots; i += 64) perm[i] = A.permits[i];
-    for (int i = lane; i < A.nm + A.nb; i += 64) pw[i] = A.pool_words[i];
+    for (int i = lane; i < n_slots; i += 64) perm[i] = A.permits[i];
+    for (int i = lane; i < nm + nb; i += 64) pw[i] = A.pool_words[i];
     for (int i = lane; i < 2 * OWGS_STAMP_BUCKETS; i += 64) stT[i] = 0xFFFFFFFFu;
     __syncthreads();
 
-    u64 st_iter = 0, st_probe = 0, st_fb = 0, st_long = 0, st_grp = 0;
+    uint32_t st_iter = 0, st_fb = 0, st_long = 0, st_grp = 0, st_probe = 0;
     PT_DECL
     uint32_t iter = 0;
     const u64 lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
@@ -326,40 +319,38 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
         // ================================================================ releases (SCPB:327-331, NS:98-113)
         const int64_t r_beg = A.rel_off ? A.rel_off[b] : 0, r_end = A.rel_off ? A.rel_off[b + 1] : 0;
         for (int64_t r0 = r_beg; r0 < r_end; r0 += 64) {
-            const int64_t r = r0 + lane;
-            const bool valid = r < r_end;
+            const bool valid = lane < r_end - r0;
             int inv = -1, mem = 0, maxc = 1, slot = 0;
             if (valid) {
-                const int4 ri = A.rinfo[r];
+                const int4 ri = A.rinfo[r0 + lane];
                 inv = A.rel_inv ? ri.x : A.out_inv[ri.x];
                 mem = ri.y;
                 maxc = ri.z & OWGS_META_MAXC_MASK;
                 slot = ri.w;
             }
             uint8_t flag = 0;
-            bool simple = false, conc = false;
+            bool conc = false, rel = false;
             if (valid) {
                 if (inv < 0) flag = OWGS_REL_NOENTRY_BIT;  // no ActivationEntry (CLB:278-279)
-                else if (inv >= A.n_slots) flag = 0;        // invokerSlots.lift -> no-op
-                else if (maxc == 1) simple = true;
+                else if (inv >= n_slots) flag = 0;          // invokerSlots.lift -> no-op
+                else if (maxc == 1) rel = true;
                 else conc = true;
             }
-            int idx = -1, c0 = 0, o0 = 0;
-            if (conc) {
-                u64 e;
-                idx = ct_find(A.ctab, A.ctab_mask, ct_key(inv, slot), &e);
-                c0 = ct_c(e);
-                o0 = ct_ops(e);
-                if (idx < 0 || o0 <= 0) {
-                    conc = false;
-                    flag = OWGS_REL_NOSUCH_BIT;  // actionConcurrentSlotsMap(actionid) throws (NS:103)
+            if (__ballot(conc)) {
+                int idx = -1, c0 = 0, o0 = 0;
+                if (conc) {
+                    u64 e;
+                    idx = ct_find(A.ctab, A.ctab_mask, ct_key(inv, slot), &e);
+                    c0 = ct_c(e);
+                    o0 = ct_ops(e);
+                    if (idx < 0 || o0 <= 0) {
+                        conc = false;
+                        flag = OWGS_REL_NOSUCH_BIT;  // actionConcurrentSlotsMap(actionid) throws (NS:103)
+                    }
                 }
-            }
-            // releases of one entry inside this group of 64: rank in stream order and group size
-            int rank = 0, gsz = 1;
-            {
-                ++iter;
-                const uint32_t stamp = ((0x03FFFFFFu - (iter & 0x03FFFFFFu)) << 6) | (uint32_t)lane;
+                // releases of one entry inside this group of 64: rank in stream order and group size
+                int rank = 0, gsz = 1;
+                const uint32_t stamp = next_stamp(iter, stT, lane);
                 if (conc) atomicMin(&stT[idx & (OWGS_STAMP_BUCKETS - 1)], stamp);
                 wave_fence();
                 const bool leader = conc && stT[idx & (OWGS_STAMP_BUCKETS - 1)] == stamp;
@@ -374,43 +365,46 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                     }
                     pend &= ~G;
                 }
+                if (conc) {
+                    // RS.release(1, opComplete = true) applied rank+1 times to (c0, o0), reductionSize = maxConc
+                    if (rank < o0) rel = mod_small(c0 + rank + 1, maxc) == 0;
+                    else flag = OWGS_REL_NOSUCH_BIT;  // entry already removed by an earlier release of this group
+                    if (rank == 0) {
+                        const int j = min(gsz, o0);
+                        int c1 = mod_small(c0 + j, maxc);
+                        const int o1 = o0 - j;
+                        if (o1 == 0) c1 = 0;  // actionRelease: entry removed (NS:109-111)
+                        A.ctab[idx] = ct_entry(ct_key(inv, slot), c1, o1);
+                    }
+                }
             }
-            bool mem_rel = false;
-            if (conc) {
-                // RS.release(1, opComplete = true) applied rank+1 times to (c0, o0), reductionSize = maxConcurrent
-                if (rank < o0) mem_rel = mod_small(c0 + rank + 1, maxc) == 0;
-                else flag = OWGS_REL_NOSUCH_BIT;  // entry already removed by an earlier release in this group
-            }
-            if (conc && rank == 0) {
-                const int j = min(gsz, o0);
-                int c1 = mod_small(c0 + j, maxc);
-                const int o1 = o0 - j;
-                if (o1 == 0) c1 = 0;  // actionRelease: entry removed (NS:109-111)
-                A.ctab[idx] = ct_entry(ct_key(inv, slot), c1, o1);
-            }
-            if (simple || mem_rel) {
+            if (rel) {
                 const int old = atomicAdd(&perm[inv], mem);
                 if (old > 0x7FFFFFFF - mem) {  // ForcibleSemaphore overflow -> Error, state unchanged (FS:48-50)
                     atomicSub(&perm[inv], mem);
                     flag |= OWGS_REL_OVERFLOW_BIT;
                 }
             }
-            if (valid && A.rel_flags) A.rel_flags[r] = flag;
+            if (valid && A.rel_flags) A.rel_flags[r0 + lane] = flag;
             wave_fence();
             PT(0);
         }
 
         // ================================================================ per-batch bounds and cursors
-        // U[p] >= max permits over usable members of pool p; permits only fall until the next batch.
-        int U[2];
-        for (int p = 0; p < 2; ++p) {
-            const int base = p ? A.nm : 0, n = p ? A.nb : A.nm;
-            int m = (int)0x80000000;
-            for (int i = lane; i < n; i += 64) {
-                const int w = pw[base + i];
-                if (w >= 0) m = max(m, perm[w]);
+        // U0/U1 >= max permits over usable members of the managed/blackbox pool; permits only fall inside a batch.
+        int U0, U1;
+        {
+            int m0 = (int)0x80000000, m1 = (int)0x80000000;
+            for (int i = lane; i < nm; i += 64) {
+                const int w = pw[i];
+                if (w >= 0) m0 = max(m0, perm[w]);
             }
-            U[p] = wave_max(m);
+            for (int i = lane; i < nb; i += 64) {
+                const int w = pw[nm + i];
+                if (w >= 0) m1 = max(m1, perm[w]);
+            }
+            U0 = wave_max(m0);
+            U1 = wave_max(m1);
         }
         for (int i = lane; i < n_cur; i += 64) cur[i] = 0;
         wave_fence();
@@ -419,8 +413,8 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
         // ================================================================ acquires (SCPB:398-436, NS:32-91)
         const int64_t a_beg = A.acq_off[b], a_end = A.acq_off[b + 1];
         for (int64_t c0i = a_beg; c0i < a_end; c0i += 64) {
-            const int64_t i = c0i + lane;
-            bool pending = i < a_end;
+            bool pending = lane < a_end - c0i;
+            const int64_t i = c0i + (pending ? lane : 0);
             int a = -1, home = 0, step = 0, mem = 0, meta = 0, slot = 0;
             if (pending) {
                 const int4 info = A.info[i];
@@ -432,23 +426,16 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                 slot = ax.x;
                 a = ax.y;
             }
-            const u64 seq = A.seq ? A.seq[pending ? i : a_beg] : (A.seq_base + (u64)i);
             const int maxc = meta & OWGS_META_MAXC_MASK;
             const int pool = (meta >> OWGS_META_POOL_SHIFT) & 1;
-            const int n = pool ? A.nb : A.nm;
-            const int pwb = pool ? A.nm : 0;
+            const int n = pool ? nb : nm;
+            const int pwb = pool ? nm : 0;
             const bool cok = (meta & OWGS_META_CURSOR) && a >= 0 && a < n_cur;
             int s = 0, pos = home;  // walk step and its pool position, kept across iterations
-
-            if (pending) {
-                int ok_kind = -1;
-                if (meta & OWGS_META_EMPTY) ok_kind = K_NONE;
-                else if ((meta & OWGS_META_THROW) || home < 0 || home >= n || step < 0) ok_kind = K_THROW;
-                if (ok_kind >= 0) {
-                    A.out_inv[i] = ok_kind == K_NONE ? OWGS_NONE_V : OWGS_THROW_V;
-                    A.out_flags[i] = 0;
-                    pending = false;
-                }
+            if (pending && ((meta & (OWGS_META_EMPTY | OWGS_META_THROW)) || home < 0 || home >= n || step < 0)) {
+                A.out_inv[i] = (meta & OWGS_META_EMPTY) ? OWGS_NONE_V : OWGS_THROW_V;  // None / schedule() throws
+                A.out_flags[i] = 0;
+                pending = false;
             }
 
             int f = 0;
@@ -456,9 +443,9 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
             while (__ballot(pending)) {
                 ++st_iter;
                 // -------------------------------------------------------- speculate targets against state at f
-                int kind = K_NONE, tgt = -1, c0 = 0, cidx = -1, ops0 = 0, pv = 0;
-                bool fullwalk = false;
                 const bool act = pending && lane >= f;
+                int kind = K_NONE, tgt = -1, pv = 0, c0 = 0, cidx = -1, ops0 = 0;
+                bool fullwalk = false;
                 if (act) {
                     if (cok) {  // cursor = walk step << 16 | pool position
                         const int cv = cur[a];
@@ -467,39 +454,65 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                             pos = cv & 0xFFFF;
                         }
                     }
-                    if (maxc == 1 && mem > U[pool] && ((A.shortcut_ok >> pool) & 1)) {
-                        fallback_target(A, pool, seq, &kind, &tgt);  // every usable permit < mem: walk fails
-                    } else {
-                        kind = K_LONG;
+                    kind = K_LONG;
+                    if (maxc == 1) {
+                        if (mem > (pool ? U1 : U0) && ((A.shortcut_ok >> pool) & 1)) {
+                            kind = K_FALLBACK;  // every usable permit < mem: the walk fails everywhere
+                        } else {
+#pragma unroll 1
+                            for (int k = 0; k < KPROBE; ++k) {
+                                if (s >= n) {  // every pool position probed: the n+2-probe walk fails (SCPB:417)
+                                    kind = K_FALLBACK;
+                                    fullwalk = true;
+                                    break;
+                                }
+                                const int w = pw[pwb + pos];
+                                ++st_probe;
+                                if (w >= 0) {
+                                    const int p = perm[w];
+                                    if (p >= mem) {
+                                        kind = K_TARGET;
+                                        tgt = w;
+                                        pv = p;
+                                        break;
+                                    }
+                                } else if (w == OWGS_PW_BADID) {
+                                    kind = K_THROW;
+                                    break;
+                                }
+                                pos = next_pos(pos, step, n);
+                                ++s;
+                            }
+                        }
+                    }
+                }
+                if (__ballot(act && maxc > 1)) {  // concurrent actions: c >= 1 also makes a probe feasible
+                    if (act && maxc > 1) {
+#pragma unroll 1
                         for (int k = 0; k < KPROBE; ++k) {
-                            if (s >= n) {  // every pool position probed: the n+2-probe walk fails (SCPB:417)
-                                fallback_target(A, pool, seq, &kind, &tgt);
+                            if (s >= n) {
+                                kind = K_FALLBACK;
                                 fullwalk = true;
                                 break;
                             }
                             const int w = pw[pwb + pos];
                             ++st_probe;
-                            if (w == OWGS_PW_BADID) {
-                                kind = K_THROW;
-                                break;
-                            }
                             if (w >= 0) {
-                                const int pw_perm = perm[w];
-                                bool feas = pw_perm >= mem;
-                                int c = 0, ix = -1, o = 0;
-                                if (maxc > 1) {
-                                    c = conc_lookup(A, w, slot, &ix, &o);
-                                    feas = feas || c >= 1;
-                                }
-                                if (feas) {
+                                const int p = perm[w];
+                                int ix, o;
+                                const int c = conc_lookup(A, w, slot, &ix, &o);
+                                if (p >= mem || c >= 1) {
                                     kind = K_TARGET;
                                     tgt = w;
+                                    pv = p;
                                     c0 = c;
                                     cidx = ix;
                                     ops0 = o;
-                                    pv = pw_perm;
                                     break;
                                 }
+                            } else if (w == OWGS_PW_BADID) {
+                                kind = K_THROW;
+                                break;
                             }
                             pos = next_pos(pos, step, n);
                             ++s;
@@ -540,7 +553,6 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                                 }
                             }
                         }
-                        st_probe += (sk < nn);
                         const u64 fm = __ballot(feas);
                         if (fm) {
                             const int j = ffs64(fm);
@@ -560,7 +572,7 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                     if (lane == f) {
                         if (fk == K_LONG) {
                             s = nn;
-                            fallback_target(A, pool, seq, &kind, &tgt);
+                            kind = K_FALLBACK;
                             fullwalk = true;
                         } else {
                             kind = fk;
@@ -574,29 +586,37 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                         }
                     }
                 }
-                if (act && kind == K_FALLBACK && maxc > 1) c0 = conc_lookup(A, tgt, slot, &cidx, &ops0);
+                // fallback target (SCPB:417-424): H = usable pool members in pool order, r = H[rng(seq) mod |H|]
+                if (__ballot(act && kind == K_FALLBACK)) {
+                    if (act && kind == K_FALLBACK) {
+                        const int hc = pool ? A.hb : A.hm;
+                        if (hc <= 0) {
+                            kind = K_NONE;
+                        } else {
+                            const u64 seq = A.seq ? A.seq[i] : (A.seq_base + (u64)i);
+                            tgt = A.hlist[(pool ? A.hm : 0) + (int)rng_index(A.rng_seed, seq, (uint32_t)hc)];
+                            if (tgt < 0 || tgt >= n_slots) kind = K_THROW;
+                            else if (maxc > 1) c0 = conc_lookup(A, tgt, slot, &cidx, &ops0);
+                        }
+                    }
+                }
                 PT(4);
 
                 // -------------------------------------------------------- group by target / by fqn (slot key)
                 const bool part = act && (kind == K_TARGET || kind == K_FALLBACK);
                 const bool cpart = part && maxc > 1;
-                ++iter;
-                if ((iter & 0x03FFFFFFu) == 0) {
-                    for (int t = lane; t < 2 * OWGS_STAMP_BUCKETS; t += 64) stT[t] = 0xFFFFFFFFu;
-                    wave_fence();
-                    ++iter;
-                }
-                const uint32_t stamp = ((0x03FFFFFFu - (iter & 0x03FFFFFFu)) << 6) | (uint32_t)lane;
+                const u64 anyc = __ballot(cpart);
+                const uint32_t stamp = next_stamp(iter, stT, lane);
                 if (part) atomicMin(&stT[tgt & (OWGS_STAMP_BUCKETS - 1)], stamp);
                 if (cpart) atomicMin(&stS[slot & (OWGS_STAMP_BUCKETS - 1)], stamp);
                 wave_fence();
                 const bool leadT = part && stT[tgt & (OWGS_STAMP_BUCKETS - 1)] == stamp;
-                const bool leadS = cpart && stS[slot & (OWGS_STAMP_BUCKETS - 1)] == stamp;
 
                 // q = earlier lanes of the same fqn at the same invoker; cons = memory this lane takes; E = memory
                 // taken by earlier lanes at the same invoker
                 int q = 0, E = 0;
-                int cons = part ? (maxc == 1 ? mem : (c_now_of(c0, 0, maxc) >= 1 ? 0 : mem)) : 0;
+                int cons = part ? mem : 0;
+                if (cpart) cons = c0 >= 1 ? 0 : mem;
                 u64 pend = __ballot(part && !leadT);
                 while (pend) {
                     ++st_grp;
@@ -604,15 +624,17 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                     const int t = __builtin_amdgcn_readlane(tgt, j);
                     const u64 G = __ballot(part && tgt == t);
                     const bool in = (G >> lane) & 1;
-                    u64 Cg = G & __ballot(cpart);
+                    u64 Cg = G & anyc;
                     while (Cg) {
                         const int j2 = ffs64(Cg);
                         const int sl = __builtin_amdgcn_readlane(slot, j2);
                         const u64 H = Cg & __ballot(slot == sl);
-                        if ((H >> lane) & 1) q = __popcll(H & lt_mask);
+                        if ((H >> lane) & 1) {
+                            q = __popcll(H & lt_mask);
+                            cons = c_now_of(c0, q, maxc) >= 1 ? 0 : mem;
+                        }
                         Cg &= ~H;
                     }
-                    if (in && maxc > 1) cons = c_now_of(c0, q, maxc) >= 1 ? 0 : mem;
                     const int ex = wave_excl_scan(in ? cons : 0);
                     if (in) E = ex;
                     pend &= ~G;
@@ -620,20 +642,23 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                 // an earlier lane of the same fqn on another walk, or an earlier forced acquire of the same fqn,
                 // may create concurrency slots this lane's speculation did not see -> uncertain
                 bool unc = false;
-                pend = __ballot(cpart && !leadS);
-                while (pend) {
-                    const int j = ffs64(pend);
-                    const int sl = __builtin_amdgcn_readlane(slot, j);
-                    const u64 Gs = __ballot(cpart && slot == sl);
-                    const int a0 = __builtin_amdgcn_readlane(a, ffs64(Gs));
-                    const u64 D = Gs & __ballot(a != a0);
-                    const u64 FB = Gs & __ballot(kind == K_FALLBACK);
-                    if ((Gs >> lane) & 1) {
-                        const bool lower = (Gs & lt_mask) != 0;
-                        if (kind == K_FALLBACK) unc = lower;
-                        else unc = lower && (((FB & lt_mask) != 0) || ((D & (lt_mask | self_bit)) != 0) || a < 0);
+                if (anyc) {
+                    const bool leadS = cpart && stS[slot & (OWGS_STAMP_BUCKETS - 1)] == stamp;
+                    pend = __ballot(cpart && !leadS);
+                    while (pend) {
+                        const int j = ffs64(pend);
+                        const int sl = __builtin_amdgcn_readlane(slot, j);
+                        const u64 Gs = __ballot(cpart && slot == sl);
+                        const int a0 = __builtin_amdgcn_readlane(a, ffs64(Gs));
+                        const u64 D = Gs & __ballot(a != a0);
+                        const u64 FB = Gs & __ballot(kind == K_FALLBACK);
+                        if ((Gs >> lane) & 1) {
+                            const bool lower = (Gs & lt_mask) != 0;
+                            if (kind == K_FALLBACK) unc = lower;
+                            else unc = lower && (((FB & lt_mask) != 0) || ((D & (lt_mask | self_bit)) != 0) || a < 0);
+                        }
+                        pend &= ~Gs;
                     }
-                    pend &= ~Gs;
                 }
                 PT(5);
                 // -------------------------------------------------------- decide
@@ -644,7 +669,7 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                     } else if (kind == K_FALLBACK) {
                         ok = !(maxc > 1 && unc);
                     } else if (kind == K_TARGET) {
-                        const long long room = (long long)pv - (long long)E;
+                        const int room = pv - E;  // |pv|, E < 2^30 for any sane permit count
                         if (maxc == 1) {
                             ok = room >= mem;
                             rej = !ok;
@@ -660,63 +685,60 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
 
                 // -------------------------------------------------------- commit lanes [f, l*)
                 if (commit && part && cons > 0) atomicSub(&perm[tgt], mem);
-                // concurrency map: the last committed lane of each (invoker, fqn) group writes the entry
-                u64 W = __ballot(commit && cpart);
-                bool writer = false;
-                while (W) {
-                    const int j = ffs64(W);
-                    const int t = __builtin_amdgcn_readlane(tgt, j);
-                    const int sl = __builtin_amdgcn_readlane(slot, j);
-                    const u64 K = W & __ballot(tgt == t && slot == sl);
-                    if (lane == fls64(K)) writer = true;
-                    W &= ~K;
-                }
-                {
+                if (anyc) {
+                    // concurrency map: the last committed lane of each (invoker, fqn) group writes the entry
+                    u64 W = __ballot(commit && cpart);
+                    bool writer = false;
+                    while (W) {
+                        const int j = ffs64(W);
+                        const int t = __builtin_amdgcn_readlane(tgt, j);
+                        const int sl = __builtin_amdgcn_readlane(slot, j);
+                        const u64 K = W & __ballot(tgt == t && slot == sl);
+                        if (lane == fls64(K)) writer = true;
+                        W &= ~K;
+                    }
                     u64 ins = __ballot(writer && cidx < 0);
                     while (ins) {
                         const int j = ffs64(ins);
                         if (lane == j) {
                             cidx = ct_insert(A.ctab, A.ctab_mask, ct_key(tgt, slot));
                             if (cidx < 0) atomicOr(A.err, 1);
-                            else A.ctab[cidx] = ct_entry(ct_key(tgt, slot), 0, 0);
                         }
                         wave_fence();
                         ins &= ins - 1;
                     }
-                }
-                if (writer && cidx >= 0) {
-                    const int cn = c_now_of(c0, q, maxc);
-                    int c1;
-                    if (cn >= 1) {
-                        c1 = cn - 1;  // RS.tryAcquire(1)
-                    } else {        // memory (try or force) + RS.release(maxConcurrent - 1, false)
-                        const int next2 = cn + (maxc - 1);
-                        c1 = (mod_small(next2, maxc) == 0) ? next2 - maxc : next2;
+                    if (writer && cidx >= 0) {
+                        const int cn = c_now_of(c0, q, maxc);
+                        int c1;
+                        if (cn >= 1) {
+                            c1 = cn - 1;  // RS.tryAcquire(1)
+                        } else {        // memory (try or force) + RS.release(maxConcurrent - 1, false)
+                            const int next2 = cn + (maxc - 1);
+                            c1 = (mod_small(next2, maxc) == 0) ? next2 - maxc : next2;
+                        }
+                        A.ctab[cidx] = ct_entry(ct_key(tgt, slot), c1, (ops0 > 0 ? ops0 : 0) + q + 1);
                     }
-                    A.ctab[cidx] = ct_entry(ct_key(tgt, slot), c1, (ops0 > 0 ? ops0 : 0) + q + 1);
                 }
                 if (commit) {
-                    int oi;
-                    if (kind == K_NONE) oi = OWGS_NONE_V;
-                    else if (kind == K_THROW) oi = OWGS_THROW_V;
-                    else oi = tgt;
-                    A.out_inv[i] = oi;
+                    A.out_inv[i] = kind == K_NONE ? OWGS_NONE_V : (kind == K_THROW ? OWGS_THROW_V : tgt);
                     A.out_flags[i] = (kind == K_FALLBACK) ? 1 : 0;
-                    if (kind == K_FALLBACK) ++st_fb;
+                    // cursors: steps before the committed target / after a full walk are infeasible from now on
+                    if (cok && (kind == K_TARGET || (kind == K_FALLBACK && maxc == 1)))
+                        atomicMax(&cur[a], kind == K_TARGET ? ((s << 16) | pos) : (n << 16));
+                    pending = false;
                 }
-                // cursors (LDS, per action): steps before the committed target / after a full walk are infeasible
-                if (commit && cok && (kind == K_TARGET || (kind == K_FALLBACK && maxc == 1)))
-                    atomicMax(&cur[a], kind == K_TARGET ? ((s << 16) | pos) : (n << 16));
-                wave_fence();
-                if (commit && cok && kind == K_FALLBACK && maxc > 1) cur[a] = 0;  // forced slots may lie anywhere
-                // a failed full walk proves every usable pool member has permits < mem from now on
-                if (__ballot(commit && kind == K_FALLBACK && fullwalk && maxc == 1)) {
-                    for (int p = 0; p < 2; ++p) {
-                        const bool t = commit && kind == K_FALLBACK && fullwalk && maxc == 1 && pool == p;
-                        U[p] = min(U[p], wave_min(t ? mem - 1 : 0x7FFFFFFF));
+                const u64 fbm = __ballot(commit && kind == K_FALLBACK);
+                if (fbm) {
+                    st_fb += __popcll(fbm);
+                    wave_fence();
+                    if (commit && cok && kind == K_FALLBACK && maxc > 1) cur[a] = 0;  // forced slots: anywhere
+                    // a failed full walk proves every usable pool member has permits < mem from now on
+                    const bool t = commit && kind == K_FALLBACK && fullwalk && maxc == 1;
+                    if (__ballot(t)) {
+                        U0 = min(U0, wave_min(t && pool == 0 ? mem - 1 : 0x7FFFFFFF));
+                        U1 = min(U1, wave_min(t && pool == 1 ? mem - 1 : 0x7FFFFFFF));
                     }
                 }
-                if (commit) pending = false;
                 // true rejection at l*: it, and every later lane of the same maxConcurrent==1 action speculated at
                 // the same walk step, continue past that step
                 if (ls < 64 && __builtin_amdgcn_readlane((int)rej, ls)) {
@@ -739,14 +761,14 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
         wave_fence();
     }
 
-    for (int i = lane; i < A.n_slots; i += 64) A.permits[i] = perm[i];
+    for (int i = lane; i < n_slots; i += 64) A.permits[i] = perm[i];
     if (A.stats) {
-        atomicAdd(&A.stats[1], st_probe);
+        atomicAdd(&A.stats[1], (u64)st_probe);
         if (lane == 0) {
-            atomicAdd(&A.stats[0], st_iter);
-            atomicAdd(&A.stats[2], st_fb);
-            atomicAdd(&A.stats[3], st_long);
-            atomicAdd(&A.stats[4], st_grp);
+            atomicAdd(&A.stats[0], (u64)st_iter);
+            atomicAdd(&A.stats[2], (u64)st_fb);
+            atomicAdd(&A.stats[3], (u64)st_long);
+            atomicAdd(&A.stats[4], (u64)st_grp);
 #ifdef OWGS_PROFILE
             for (int k = 0; k < 8; ++k) atomicAdd(&A.stats[8 + k], pt_acc[k]);
 #endif
