@@ -293,6 +293,81 @@ __device__ __forceinline__ uint32_t next_stamp(uint32_t& iter, uint32_t* st, int
     return ((0x03FFFFFFu - (iter & 0x03FFFFFFu)) << 6) | (uint32_t)lane;
 }
 
+struct CoopResult {
+    int kind, tgt, pv, s, pos, c, cidx, ops;
+};
+
+// Wave-cooperative walk for lane `who` (all lanes call it): walk steps s0.. are probed 64 at a time and ballot picks
+// the first feasible one.  kind = K_TARGET / K_THROW, or K_LONG when every remaining step fails (s = n).
+__device__ CoopResult coop_walk(const OwgsEngineArgs& A, const int32_t* perm, const int32_t* pw, int who, int s_l,
+                                int pos_l, int step_l, int n_l, int pwb_l, int mem_l, int maxc_l, int slot_l) {
+    const int lane = threadIdx.x;
+    int s0 = __builtin_amdgcn_readlane(s_l, who);
+    int p0 = __builtin_amdgcn_readlane(pos_l, who);
+    const int stp = __builtin_amdgcn_readlane(step_l, who);
+    const int nn = __builtin_amdgcn_readlane(n_l, who);
+    const int pb = __builtin_amdgcn_readlane(pwb_l, who);
+    const int m = __builtin_amdgcn_readlane(mem_l, who);
+    const int mc = __builtin_amdgcn_readlane(maxc_l, who);
+    const int sl = __builtin_amdgcn_readlane(slot_l, who);
+    CoopResult r{K_LONG, -1, 0, nn, p0, 0, -1, 0};
+    const int loff = (int)(((uint32_t)lane * (uint32_t)stp) % (uint32_t)nn);
+    const int boff = (int)((64u * (uint32_t)stp) % (uint32_t)nn);
+    while (s0 < nn) {
+        const int sk = s0 + lane;
+        const int p = next_pos(p0, loff, nn);
+        bool feas = false;
+        int w = -1, c = 0, ix = -1, o = 0, pvv = 0;
+        if (sk < nn) {
+            w = pw[pb + p];
+            if (w == OWGS_PW_BADID) {
+                feas = true;
+            } else if (w >= 0) {
+                pvv = perm[w];
+                feas = pvv >= m;
+                if (mc > 1) {
+                    c = conc_lookup(A, w, sl, &ix, &o);
+                    feas = feas || c >= 1;
+                }
+            }
+        }
+        const u64 fm = __ballot(feas);
+        if (fm) {
+            const int j = ffs64(fm);
+            r.tgt = __builtin_amdgcn_readlane(w, j);
+            r.c = __builtin_amdgcn_readlane(c, j);
+            r.cidx = __builtin_amdgcn_readlane(ix, j);
+            r.ops = __builtin_amdgcn_readlane(o, j);
+            r.pv = __builtin_amdgcn_readlane(pvv, j);
+            r.pos = __builtin_amdgcn_readlane(p, j);
+            r.s = s0 + j;
+            r.kind = (r.tgt == OWGS_PW_BADID) ? K_THROW : K_TARGET;
+            return r;
+        }
+        s0 += 64;
+        p0 = next_pos(p0, boff, nn);
+    }
+    return r;
+}
+
+// fallback target (SCPB:417-424): H = usable pool members in pool order, r = H[rng(seq) mod |H|]
+__device__ __forceinline__ void fallback_target(const OwgsEngineArgs& A, int pool, int64_t i, int n_slots, int* kind,
+                                                int* tgt) {
+    const int hc = pool ? A.hb : A.hm;
+    if (hc <= 0) {
+        *kind = K_NONE;
+        return;
+    }
+    const u64 seq = A.seq ? A.seq[i] : (A.seq_base + (u64)i);
+    const int r = A.hlist[(pool ? A.hm : 0) + (int)rng_index(A.rng_seed, seq, (uint32_t)hc)];
+    if (r < 0 || r >= n_slots) {
+        *kind = K_THROW;
+        return;
+    }
+    *kind = K_FALLBACK;
+    *tgt = r;
+}
+
 __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
     extern __shared__ __attribute__((aligned(16))) int32_t lds_raw[];
     const int lane = threadIdx.x;
@@ -309,7 +384,7 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
     for (int i = lane; i < 2 * OWGS_STAMP_BUCKETS; i += 64) stT[i] = 0xFFFFFFFFu;
     __syncthreads();
 
-    uint32_t st_iter = 0, st_fb = 0, st_long = 0, st_grp = 0, st_probe = 0;
+    uint32_t st_iter = 0, st_fb = 0, st_long = 0, st_grp = 0, st_probe = 0, st_inc = 0;
     PT_DECL
     uint32_t iter = 0;
     const u64 lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
@@ -439,29 +514,71 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
             }
 
             int f = 0;
+            bool full = true;  // lanes >= f need (re)speculation
+            // per-lane speculation, valid for lanes >= f until the next full pass
+            int kind = K_NONE, tgt = -1, room = 0, c0 = 0, cidx = -1, ops0 = 0, q = 0, cons = 0;
+            bool unc = false, fullwalk = false;
             PT(2);
             while (__ballot(pending)) {
-                ++st_iter;
-                // -------------------------------------------------------- speculate targets against state at f
                 const bool act = pending && lane >= f;
-                int kind = K_NONE, tgt = -1, pv = 0, c0 = 0, cidx = -1, ops0 = 0;
-                bool fullwalk = false;
-                if (act) {
-                    if (cok) {  // cursor = walk step << 16 | pool position
-                        const int cv = cur[a];
-                        if ((cv >> 16) > s) {
-                            s = cv >> 16;
-                            pos = cv & 0xFFFF;
+                if (full) {
+                    full = false;
+                    ++st_iter;
+                    // ---------------------------------------------------- speculate targets against state at f
+                    kind = K_NONE;
+                    tgt = -1;
+                    c0 = 0;
+                    cidx = -1;
+                    ops0 = 0;
+                    q = 0;
+                    unc = false;
+                    fullwalk = false;
+                    int pv = 0;
+                    if (act) {
+                        if (cok) {  // cursor = walk step << 16 | pool position
+                            const int cv = cur[a];
+                            if ((cv >> 16) > s) {
+                                s = cv >> 16;
+                                pos = cv & 0xFFFF;
+                            }
+                        }
+                        kind = K_LONG;
+                        if (maxc == 1) {
+                            if (mem > (pool ? U1 : U0) && ((A.shortcut_ok >> pool) & 1)) {
+                                kind = K_FALLBACK;  // every usable permit < mem: the walk fails everywhere
+                            } else {
+#pragma unroll 1
+                                for (int k = 0; k < KPROBE; ++k) {
+                                    if (s >= n) {  // every pool position probed: the n+2-probe walk fails (SCPB:417)
+                                        kind = K_FALLBACK;
+                                        fullwalk = true;
+                                        break;
+                                    }
+                                    const int w = pw[pwb + pos];
+                                    ++st_probe;
+                                    if (w >= 0) {
+                                        const int p = perm[w];
+                                        if (p >= mem) {
+                                            kind = K_TARGET;
+                                            tgt = w;
+                                            pv = p;
+                                            break;
+                                        }
+                                    } else if (w == OWGS_PW_BADID) {
+                                        kind = K_THROW;
+                                        break;
+                                    }
+                                    pos = next_pos(pos, step, n);
+                                    ++s;
+                                }
+                            }
                         }
                     }
-                    kind = K_LONG;
-                    if (maxc == 1) {
-                        if (mem > (pool ? U1 : U0) && ((A.shortcut_ok >> pool) & 1)) {
-                            kind = K_FALLBACK;  // every usable permit < mem: the walk fails everywhere
-                        } else {
+                    if (__ballot(act && maxc > 1)) {  // concurrent actions: c >= 1 also makes a probe feasible
+                        if (act && maxc > 1) {
 #pragma unroll 1
                             for (int k = 0; k < KPROBE; ++k) {
-                                if (s >= n) {  // every pool position probed: the n+2-probe walk fails (SCPB:417)
+                                if (s >= n) {
                                     kind = K_FALLBACK;
                                     fullwalk = true;
                                     break;
@@ -470,10 +587,15 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                                 ++st_probe;
                                 if (w >= 0) {
                                     const int p = perm[w];
-                                    if (p >= mem) {
+                                    int ix, o;
+                                    const int c = conc_lookup(A, w, slot, &ix, &o);
+                                    if (p >= mem || c >= 1) {
                                         kind = K_TARGET;
                                         tgt = w;
                                         pv = p;
+                                        c0 = c;
+                                        cidx = ix;
+                                        ops0 = o;
                                         break;
                                     }
                                 } else if (w == OWGS_PW_BADID) {
@@ -485,183 +607,98 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                             }
                         }
                     }
-                }
-                if (__ballot(act && maxc > 1)) {  // concurrent actions: c >= 1 also makes a probe feasible
-                    if (act && maxc > 1) {
-#pragma unroll 1
-                        for (int k = 0; k < KPROBE; ++k) {
-                            if (s >= n) {
+                    PT(3);
+                    // frontier lane with a long walk: wave-cooperative scan, 64 walk steps per round
+                    if (__builtin_amdgcn_readlane(kind, f) == K_LONG) {
+                        ++st_long;
+                        const CoopResult cr = coop_walk(A, perm, pw, f, s, pos, step, n, pwb, mem, maxc, slot);
+                        if (lane == f) {
+                            s = cr.s;
+                            pos = cr.pos;
+                            if (cr.kind == K_LONG) {
                                 kind = K_FALLBACK;
                                 fullwalk = true;
-                                break;
-                            }
-                            const int w = pw[pwb + pos];
-                            ++st_probe;
-                            if (w >= 0) {
-                                const int p = perm[w];
-                                int ix, o;
-                                const int c = conc_lookup(A, w, slot, &ix, &o);
-                                if (p >= mem || c >= 1) {
-                                    kind = K_TARGET;
-                                    tgt = w;
-                                    pv = p;
-                                    c0 = c;
-                                    cidx = ix;
-                                    ops0 = o;
-                                    break;
-                                }
-                            } else if (w == OWGS_PW_BADID) {
-                                kind = K_THROW;
-                                break;
-                            }
-                            pos = next_pos(pos, step, n);
-                            ++s;
-                        }
-                    }
-                }
-                PT(3);
-                // -------------------------------------------------------- frontier lane with a long walk:
-                // wave-cooperative scan of 64 walk steps per round (ballot picks the first feasible one)
-                if (__builtin_amdgcn_readlane(kind, f) == K_LONG) {
-                    ++st_long;
-                    int s0 = __builtin_amdgcn_readlane(s, f);
-                    int p0 = __builtin_amdgcn_readlane(pos, f);
-                    const int stp = __builtin_amdgcn_readlane(step, f);
-                    const int nn = __builtin_amdgcn_readlane(n, f);
-                    const int pb = __builtin_amdgcn_readlane(pwb, f);
-                    const int m = __builtin_amdgcn_readlane(mem, f);
-                    const int mc = __builtin_amdgcn_readlane(maxc, f);
-                    const int sl = __builtin_amdgcn_readlane(slot, f);
-                    int fk = K_LONG, ft = -1, fs = s0, fc = 0, fix = -1, fo = 0, fp = 0, fpos = p0;
-                    const int loff = (int)(((uint32_t)lane * (uint32_t)stp) % (uint32_t)nn);
-                    const int boff = (int)((64u * (uint32_t)stp) % (uint32_t)nn);
-                    while (s0 < nn) {
-                        const int sk = s0 + lane;
-                        const int p = next_pos(p0, loff, nn);
-                        bool feas = false;
-                        int w = -1, c = 0, ix = -1, o = 0, pvv = 0;
-                        if (sk < nn) {
-                            w = pw[pb + p];
-                            if (w == OWGS_PW_BADID) {
-                                feas = true;
-                            } else if (w >= 0) {
-                                pvv = perm[w];
-                                feas = pvv >= m;
-                                if (mc > 1) {
-                                    c = conc_lookup(A, w, sl, &ix, &o);
-                                    feas = feas || c >= 1;
-                                }
+                            } else {
+                                kind = cr.kind;
+                                tgt = cr.tgt;
+                                pv = cr.pv;
+                                c0 = cr.c;
+                                cidx = cr.cidx;
+                                ops0 = cr.ops;
                             }
                         }
-                        const u64 fm = __ballot(feas);
-                        if (fm) {
-                            const int j = ffs64(fm);
-                            ft = __builtin_amdgcn_readlane(w, j);
-                            fc = __builtin_amdgcn_readlane(c, j);
-                            fix = __builtin_amdgcn_readlane(ix, j);
-                            fo = __builtin_amdgcn_readlane(o, j);
-                            fp = __builtin_amdgcn_readlane(pvv, j);
-                            fpos = __builtin_amdgcn_readlane(p, j);
-                            fs = s0 + j;
-                            fk = (ft == OWGS_PW_BADID) ? K_THROW : K_TARGET;
-                            break;
-                        }
-                        s0 += 64;
-                        p0 = next_pos(p0, boff, nn);
                     }
-                    if (lane == f) {
-                        if (fk == K_LONG) {
-                            s = nn;
-                            kind = K_FALLBACK;
-                            fullwalk = true;
-                        } else {
-                            kind = fk;
-                            tgt = ft;
-                            s = fs;
-                            pos = fpos;
-                            c0 = fc;
-                            cidx = fix;
-                            ops0 = fo;
-                            pv = fp;
+                    // fallback target (SCPB:417-424): H = usable pool members in pool order, r = H[rng(seq) mod |H|]
+                    if (__ballot(act && kind == K_FALLBACK)) {
+                        if (act && kind == K_FALLBACK) {
+                            fallback_target(A, pool, i, n_slots, &kind, &tgt);
+                            if (kind == K_FALLBACK && maxc > 1) c0 = conc_lookup(A, tgt, slot, &cidx, &ops0);
                         }
                     }
-                }
-                // fallback target (SCPB:417-424): H = usable pool members in pool order, r = H[rng(seq) mod |H|]
-                if (__ballot(act && kind == K_FALLBACK)) {
-                    if (act && kind == K_FALLBACK) {
-                        const int hc = pool ? A.hb : A.hm;
-                        if (hc <= 0) {
-                            kind = K_NONE;
-                        } else {
-                            const u64 seq = A.seq ? A.seq[i] : (A.seq_base + (u64)i);
-                            tgt = A.hlist[(pool ? A.hm : 0) + (int)rng_index(A.rng_seed, seq, (uint32_t)hc)];
-                            if (tgt < 0 || tgt >= n_slots) kind = K_THROW;
-                            else if (maxc > 1) c0 = conc_lookup(A, tgt, slot, &cidx, &ops0);
-                        }
-                    }
-                }
-                PT(4);
-
-                // -------------------------------------------------------- group by target / by fqn (slot key)
-                const bool part = act && (kind == K_TARGET || kind == K_FALLBACK);
-                const bool cpart = part && maxc > 1;
-                const u64 anyc = __ballot(cpart);
-                const uint32_t stamp = next_stamp(iter, stT, lane);
-                if (part) atomicMin(&stT[tgt & (OWGS_STAMP_BUCKETS - 1)], stamp);
-                if (cpart) atomicMin(&stS[slot & (OWGS_STAMP_BUCKETS - 1)], stamp);
-                wave_fence();
-                const bool leadT = part && stT[tgt & (OWGS_STAMP_BUCKETS - 1)] == stamp;
-
-                // q = earlier lanes of the same fqn at the same invoker; cons = memory this lane takes; E = memory
-                // taken by earlier lanes at the same invoker
-                int q = 0, E = 0;
-                int cons = part ? mem : 0;
-                if (cpart) cons = c0 >= 1 ? 0 : mem;
-                u64 pend = __ballot(part && !leadT);
-                while (pend) {
-                    ++st_grp;
-                    const int j = ffs64(pend);
-                    const int t = __builtin_amdgcn_readlane(tgt, j);
-                    const u64 G = __ballot(part && tgt == t);
-                    const bool in = (G >> lane) & 1;
-                    u64 Cg = G & anyc;
-                    while (Cg) {
-                        const int j2 = ffs64(Cg);
-                        const int sl = __builtin_amdgcn_readlane(slot, j2);
-                        const u64 H = Cg & __ballot(slot == sl);
-                        if ((H >> lane) & 1) {
-                            q = __popcll(H & lt_mask);
-                            cons = c_now_of(c0, q, maxc) >= 1 ? 0 : mem;
-                        }
-                        Cg &= ~H;
-                    }
-                    const int ex = wave_excl_scan(in ? cons : 0);
-                    if (in) E = ex;
-                    pend &= ~G;
-                }
-                // an earlier lane of the same fqn on another walk, or an earlier forced acquire of the same fqn,
-                // may create concurrency slots this lane's speculation did not see -> uncertain
-                bool unc = false;
-                if (anyc) {
-                    const bool leadS = cpart && stS[slot & (OWGS_STAMP_BUCKETS - 1)] == stamp;
-                    pend = __ballot(cpart && !leadS);
+                    PT(4);
+                    // ---------------------------------------------------- group by target / by fqn (slot key)
+                    const bool part = act && (kind == K_TARGET || kind == K_FALLBACK);
+                    const bool cpart = part && maxc > 1;
+                    const u64 anyc = __ballot(cpart);
+                    const uint32_t stamp = next_stamp(iter, stT, lane);
+                    if (part) atomicMin(&stT[tgt & (OWGS_STAMP_BUCKETS - 1)], stamp);
+                    if (cpart) atomicMin(&stS[slot & (OWGS_STAMP_BUCKETS - 1)], stamp);
+                    wave_fence();
+                    const bool leadT = part && stT[tgt & (OWGS_STAMP_BUCKETS - 1)] == stamp;
+                    // q = earlier lanes of the same fqn at the same invoker; cons = memory this lane takes;
+                    // E = memory taken at this lane's invoker by earlier lanes of the chunk
+                    int E = 0;
+                    cons = part ? mem : 0;
+                    if (cpart) cons = c0 >= 1 ? 0 : mem;
+                    u64 pend = __ballot(part && !leadT);
                     while (pend) {
+                        ++st_grp;
                         const int j = ffs64(pend);
-                        const int sl = __builtin_amdgcn_readlane(slot, j);
-                        const u64 Gs = __ballot(cpart && slot == sl);
-                        const int a0 = __builtin_amdgcn_readlane(a, ffs64(Gs));
-                        const u64 D = Gs & __ballot(a != a0);
-                        const u64 FB = Gs & __ballot(kind == K_FALLBACK);
-                        if ((Gs >> lane) & 1) {
-                            const bool lower = (Gs & lt_mask) != 0;
-                            if (kind == K_FALLBACK) unc = lower;
-                            else unc = lower && (((FB & lt_mask) != 0) || ((D & (lt_mask | self_bit)) != 0) || a < 0);
+                        const int t = __builtin_amdgcn_readlane(tgt, j);
+                        const u64 G = __ballot(part && tgt == t);
+                        const bool in = (G >> lane) & 1;
+                        u64 Cg = G & anyc;
+                        while (Cg) {
+                            const int j2 = ffs64(Cg);
+                            const int sl = __builtin_amdgcn_readlane(slot, j2);
+                            const u64 H = Cg & __ballot(slot == sl);
+                            if ((H >> lane) & 1) {
+                                q = __popcll(H & lt_mask);
+                                cons = c_now_of(c0, q, maxc) >= 1 ? 0 : mem;
+                            }
+                            Cg &= ~H;
                         }
-                        pend &= ~Gs;
+                        const int ex = wave_excl_scan(in ? cons : 0);
+                        if (in) E = ex;
+                        pend &= ~G;
                     }
+                    room = pv - E;  // |pv|, E < 2^30 for any sane permit count
+                    // an earlier lane of the same fqn on another walk, or an earlier forced acquire of the same fqn,
+                    // may create concurrency slots this lane's speculation did not see -> uncertain
+                    if (anyc) {
+                        const bool leadS = cpart && stS[slot & (OWGS_STAMP_BUCKETS - 1)] == stamp;
+                        pend = __ballot(cpart && !leadS);
+                        while (pend) {
+                            const int j = ffs64(pend);
+                            const int sl = __builtin_amdgcn_readlane(slot, j);
+                            const u64 Gs = __ballot(cpart && slot == sl);
+                            const int a0 = __builtin_amdgcn_readlane(a, ffs64(Gs));
+                            const u64 D = Gs & __ballot(a != a0);
+                            const u64 FB = Gs & __ballot(kind == K_FALLBACK);
+                            if ((Gs >> lane) & 1) {
+                                const bool lower = (Gs & lt_mask) != 0;
+                                if (kind == K_FALLBACK) unc = lower;
+                                else
+                                    unc = lower &&
+                                          (((FB & lt_mask) != 0) || ((D & (lt_mask | self_bit)) != 0) || a < 0);
+                            }
+                            pend &= ~Gs;
+                        }
+                    }
+                    PT(5);
                 }
-                PT(5);
                 // -------------------------------------------------------- decide
+                const bool part = act && (kind == K_TARGET || kind == K_FALLBACK);
                 bool ok = false, rej = false;
                 if (act) {
                     if (kind == K_NONE || kind == K_THROW) {
@@ -669,7 +706,6 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                     } else if (kind == K_FALLBACK) {
                         ok = !(maxc > 1 && unc);
                     } else if (kind == K_TARGET) {
-                        const int room = pv - E;  // |pv|, E < 2^30 for any sane permit count
                         if (maxc == 1) {
                             ok = room >= mem;
                             rej = !ok;
@@ -685,8 +721,9 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
 
                 // -------------------------------------------------------- commit lanes [f, l*)
                 if (commit && part && cons > 0) atomicSub(&perm[tgt], mem);
-                if (anyc) {
+                if (__ballot(commit && part && maxc > 1)) {
                     // concurrency map: the last committed lane of each (invoker, fqn) group writes the entry
+                    const bool cpart = part && maxc > 1;
                     u64 W = __ballot(commit && cpart);
                     bool writer = false;
                     while (W) {
@@ -739,23 +776,93 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                         U1 = min(U1, wave_min(t && pool == 1 ? mem - 1 : 0x7FFFFFFF));
                     }
                 }
-                // true rejection at l*: it, and every later lane of the same maxConcurrent==1 action speculated at
-                // the same walk step, continue past that step
-                if (ls < 64 && __builtin_amdgcn_readlane((int)rej, ls)) {
-                    const int as = __builtin_amdgcn_readlane(a, ls);
-                    const int ss = __builtin_amdgcn_readlane(s, ls);
-                    const int ms = __builtin_amdgcn_readlane(maxc, ls);
-                    bool adv = lane == ls;
-                    if (as >= 0 && ms == 1) adv = adv || (act && lane > ls && a == as && kind == K_TARGET && s == ss);
-                    if (adv) {
-                        pos = next_pos(pos, step, n);
-                        ++s;
-                    }
-                    if (lane == ls && cok) atomicMax(&cur[a], (s << 16) | pos);
-                }
-                wave_fence();
-                f = ls;
                 PT(6);
+                if (ls == 64) break;
+
+                // -------------------------------------------------------- resolve l*
+                const int lk = __builtin_amdgcn_readlane(kind, ls);
+                const int lmc = __builtin_amdgcn_readlane(maxc, ls);
+                if (lmc == 1 && (lk == K_TARGET || lk == K_LONG)) {
+                    // Incremental: l* is a maxConcurrent==1 lane and every lane before it is committed, so the
+                    // state is exact at l*'s time.  Walk it to its true target, commit it, and patch the
+                    // remaining permits (room) of later lanes at its old and new invokers; nothing else changed.
+                    ++st_inc;
+                    wave_fence();
+                    const int lm = __builtin_amdgcn_readlane(mem, ls);
+                    if (lk == K_TARGET) {
+                        const int t_old = __builtin_amdgcn_readlane(tgt, ls);
+                        if (act && lane > ls && tgt == t_old && (kind == K_TARGET || kind == K_FALLBACK)) room += lm;
+                        if (lane == ls) {
+                            pos = next_pos(pos, step, n);
+                            ++s;
+                        }
+                    }
+                    if (lane == ls && cok) {
+                        const int cv = cur[a];
+                        if ((cv >> 16) > s) {
+                            s = cv >> 16;
+                            pos = cv & 0xFFFF;
+                        }
+                    }
+                    const int lpool = __builtin_amdgcn_readlane(pool, ls);
+                    int nk, nt = -1, nfull = 0;
+                    if (lm > (lpool ? U1 : U0) && ((A.shortcut_ok >> lpool) & 1)) {
+                        nk = K_LONG;  // provably no feasible step: straight to the fallback
+                    } else {
+                        ++st_long;
+                        const CoopResult cr = coop_walk(A, perm, pw, ls, s, pos, step, n, pwb, mem, 1, slot);
+                        if (lane == ls) {
+                            s = cr.s;
+                            pos = cr.pos;
+                        }
+                        nk = cr.kind;
+                        nt = cr.tgt;
+                        nfull = 1;
+                    }
+                    if (nk == K_LONG) {  // every step fails: random fallback
+                        int fk = K_NONE, ft = -1;
+                        if (lane == ls) fallback_target(A, pool, i, n_slots, &fk, &ft);
+                        nk = __builtin_amdgcn_readlane(fk, ls);
+                        nt = __builtin_amdgcn_readlane(ft, ls);
+                        if (nk == K_FALLBACK) {
+                            ++st_fb;
+                            if (nfull) {
+                                if (lpool) U1 = min(U1, lm - 1);
+                                else U0 = min(U0, lm - 1);
+                            }
+                        }
+                    }
+                    if (lane == ls) {
+                        A.out_inv[i] = nk == K_NONE ? OWGS_NONE_V : (nk == K_THROW ? OWGS_THROW_V : nt);
+                        A.out_flags[i] = (nk == K_FALLBACK) ? 1 : 0;
+                        if (nk == K_TARGET || nk == K_FALLBACK) atomicSub(&perm[nt], lm);
+                        if (cok && (nk == K_TARGET || nk == K_FALLBACK))
+                            atomicMax(&cur[a], nk == K_TARGET ? ((s << 16) | pos) : (n << 16));
+                        pending = false;
+                    }
+                    if ((nk == K_TARGET || nk == K_FALLBACK) && act && lane > ls && tgt == nt &&
+                        (kind == K_TARGET || kind == K_FALLBACK))
+                        room -= lm;
+                    wave_fence();
+                    f = ls + 1;
+                } else {
+                    // general case: l* (and every later lane of the same maxConcurrent==1 action speculated at the
+                    // same walk step, when l* is a true rejection) continue past that step; re-speculate from l*
+                    if (__builtin_amdgcn_readlane((int)rej, ls)) {
+                        const int as = __builtin_amdgcn_readlane(a, ls);
+                        const int ss = __builtin_amdgcn_readlane(s, ls);
+                        bool adv = lane == ls;
+                        if (as >= 0 && lmc == 1) adv = adv || (act && lane > ls && a == as && kind == K_TARGET && s == ss);
+                        if (adv) {
+                            pos = next_pos(pos, step, n);
+                            ++s;
+                        }
+                        if (lane == ls && cok) atomicMax(&cur[a], (s << 16) | pos);
+                    }
+                    wave_fence();
+                    f = ls;
+                    full = true;
+                }
             }
         }
         wave_fence();
@@ -769,6 +876,7 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
             atomicAdd(&A.stats[2], (u64)st_fb);
             atomicAdd(&A.stats[3], (u64)st_long);
             atomicAdd(&A.stats[4], (u64)st_grp);
+            atomicAdd(&A.stats[5], (u64)st_inc);
 #ifdef OWGS_PROFILE
             for (int k = 0; k < 8; ++k) atomicAdd(&A.stats[8 + k], pt_acc[k]);
 #endif
