@@ -1,0 +1,93 @@
+/*
+ * owgs_jni.c -- JNI binding of include/owgs.h for integration/GpuShardingContainerPoolBalancer.scala
+ * (SOURCE ONLY: this image has no JDK, so no jni.h; build on a controller host with
+ *   gcc -O2 -shared -fPIC -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -I<repo>/include owgs_jni.c \
+ *       -L<repo>/openwhisk_amd -lowgs -o libowgs_jni.so ).
+ * Arrays are pinned with Get/ReleasePrimitiveArrayCritical for the duration of one batch call; the native context is
+ * single-writer (the shim's batching thread), as owgs.h requires.
+ */
+#include <jni.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "owgs.h"
+
+#define CTX(h) ((owgs_ctx*)(intptr_t)(h))
+
+JNIEXPORT jlong JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_create(
+    JNIEnv* env, jobject self, jdouble mf, jdouble bf, jlong min_mem, jint cluster, jint device, jlong seed) {
+    owgs_config cfg = {mf, bf, (int64_t)min_mem, (int32_t)cluster, (int32_t)device, (uint64_t)seed};
+    owgs_ctx* c = NULL;
+    return owgs_create(&cfg, &c) == OWGS_OK ? (jlong)(intptr_t)c : 0;
+}
+
+JNIEXPORT void JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_destroy(JNIEnv* env, jobject self,
+                                                                                          jlong h) {
+    owgs_destroy(CTX(h));
+}
+
+JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_updateInvokers(
+    JNIEnv* env, jobject self, jlong h, jintArray ids, jlongArray mem, jbyteArray status) {
+    const jsize n = (*env)->GetArrayLength(env, ids);
+    jint* pi = (*env)->GetPrimitiveArrayCritical(env, ids, NULL);
+    jlong* pm = (*env)->GetPrimitiveArrayCritical(env, mem, NULL);
+    jbyte* ps = (*env)->GetPrimitiveArrayCritical(env, status, NULL);
+    const int rc = owgs_update_invokers(CTX(h), n, (const int32_t*)pi, (const int64_t*)pm, (const uint8_t*)ps);
+    (*env)->ReleasePrimitiveArrayCritical(env, status, ps, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, mem, pm, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, ids, pi, JNI_ABORT);
+    return rc;
+}
+
+JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_updateCluster(JNIEnv* env,
+                                                                                                jobject self, jlong h,
+                                                                                                jint size) {
+    return owgs_update_cluster(CTX(h), size);
+}
+
+JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_registerAction(
+    JNIEnv* env, jobject self, jlong h, jstring ns, jstring path, jstring key, jint mem, jint maxc, jboolean bb) {
+    const char* s0 = (*env)->GetStringUTFChars(env, ns, NULL);
+    const char* s1 = (*env)->GetStringUTFChars(env, path, NULL);
+    const char* s2 = (*env)->GetStringUTFChars(env, key, NULL);
+    const int32_t o0[2] = {0, (int32_t)strlen(s0)}, o1[2] = {0, (int32_t)strlen(s1)}, o2[2] = {0, (int32_t)strlen(s2)};
+    const int32_t m = mem, c = maxc;
+    const uint8_t b = bb ? 1 : 0;
+    int32_t action = -1;
+    const int rc = owgs_register_actions(CTX(h), 1, s0, o0, s1, o1, s2, o2, &m, &c, &b, &action, NULL);
+    (*env)->ReleaseStringUTFChars(env, key, s2);
+    (*env)->ReleaseStringUTFChars(env, path, s1);
+    (*env)->ReleaseStringUTFChars(env, ns, s0);
+    return rc == OWGS_OK ? action : rc;
+}
+
+JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_publishBatch(
+    JNIEnv* env, jobject self, jlong h, jintArray actions, jlongArray seq, jint n, jintArray out, jbyteArray flags) {
+    jint* pa = (*env)->GetPrimitiveArrayCritical(env, actions, NULL);
+    jlong* ps = (*env)->GetPrimitiveArrayCritical(env, seq, NULL);
+    jint* po = (*env)->GetPrimitiveArrayCritical(env, out, NULL);
+    jbyte* pf = (*env)->GetPrimitiveArrayCritical(env, flags, NULL);
+    const int rc = owgs_publish_batch(CTX(h), n, (const int32_t*)pa, (const uint64_t*)ps, 0, (int32_t*)po, (uint8_t*)pf);
+    (*env)->ReleasePrimitiveArrayCritical(env, flags, pf, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, out, po, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, seq, ps, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, actions, pa, JNI_ABORT);
+    return rc;
+}
+
+JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_releaseBatch(
+    JNIEnv* env, jobject self, jlong h, jintArray invokers, jintArray actions, jint n, jbyteArray flags) {
+    jint* pi = (*env)->GetPrimitiveArrayCritical(env, invokers, NULL);
+    jint* pa = (*env)->GetPrimitiveArrayCritical(env, actions, NULL);
+    jbyte* pf = (*env)->GetPrimitiveArrayCritical(env, flags, NULL);
+    const int rc = owgs_release_batch(CTX(h), n, (const int32_t*)pi, (const int32_t*)pa, (uint8_t*)pf);
+    (*env)->ReleasePrimitiveArrayCritical(env, flags, pf, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, actions, pa, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, invokers, pi, JNI_ABORT);
+    return rc;
+}
+
+JNIEXPORT jstring JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_lastError(JNIEnv* env,
+                                                                                               jobject self, jlong h) {
+    return (*env)->NewStringUTF(env, owgs_last_error(CTX(h)));
+}
