@@ -85,10 +85,11 @@ def cpu_baseline(args, world):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
+
+    from openwhisk_amd import cluster
+
+    rank, world, local = cluster.env_rank()
 
     dist = None
     if world > 1:
@@ -101,9 +102,8 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from openwhisk_amd import GpuShardingContainerPoolBalancer
-    from openwhisk_amd import workload as W
 
-    w = W.config(args.config, n_activations=args.n_activations, shard=rank, n_shards=world)
+    w = cluster.shard_workload(args.config, rank, world, n_activations=args.n_activations)
     b = GpuShardingContainerPoolBalancer(managed_fraction=w.managed_fraction, blackbox_fraction=w.blackbox_fraction,
                                          rng_seed=w.rng_seed, device=torch.cuda.current_device())
     b.update_invokers_arrays(w.inv_ids, w.inv_mem, w.inv_status)
@@ -118,8 +118,7 @@ def main():
     d_out = torch.empty(len(s.act), dtype=torch.int32, device=dev)
     d_fl = torch.empty(len(s.act), dtype=torch.uint8, device=dev)
     d_rf = torch.empty(max(len(s.rel_aid), 1), dtype=torch.uint8, device=dev)
-    health = torch.from_numpy(w.inv_status.copy()).to(dev)
-    gathered = torch.empty((world, len(w.inv_status)), dtype=torch.uint8, device=dev) if world > 1 else None
+    hx = cluster.HealthExchange(dist, torch.from_numpy(w.inv_status.copy()).to(dev), world)
     torch.cuda.synchronize()
     stream = torch.cuda.Stream()  # a real (non-null) HIP stream: the engine and the timing events share it
     torch.cuda.set_stream(stream)
@@ -127,8 +126,7 @@ def main():
 
     def step():
         if world > 1:
-            dist.all_gather_into_tensor(gathered, health)
-            b.update_health_device(len(w.inv_status), gathered[0].data_ptr(), sp)
+            b.update_health_device(len(w.inv_status), hx.exchange().data_ptr(), sp)
         b.restore(sp)
         b.replay_device(s.n_batches, d_acq.data_ptr(), d_act.data_ptr(), len(s.act), d_rel.data_ptr(),
                         d_aid.data_ptr(), len(s.rel_aid), s.seq_base, d_out.data_ptr(), d_fl.data_ptr(),
@@ -144,8 +142,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         if world > 1:
-            dist.all_gather_into_tensor(gathered, health)
-            b.update_health_device(len(w.inv_status), gathered[0].data_ptr(), sp)
+            b.update_health_device(len(w.inv_status), hx.exchange().data_ptr(), sp)
         b.restore(sp)
         evs[k][0].record(stream)
         b.replay_device(s.n_batches, d_acq.data_ptr(), d_act.data_ptr(), len(s.act), d_rel.data_ptr(),
@@ -173,12 +170,9 @@ def main():
 
     n_dec = len(s.act)
     t_step = wall / args.steps
-    if dist:
-        v = torch.tensor([t_step, 0.0 if exact else 1.0, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(v, op=dist.ReduceOp.MAX)
-        t_step, bad, kern_ms = float(v[0]), float(v[1]), float(v[2])
-        exact = bad == 0.0
-    value = world * n_dec / t_step
+    t_step, bad, kern_ms = cluster.max_over_ranks(dist, [t_step, 0.0 if exact else 1.0, kern_ms], dev)
+    exact = bad == 0.0
+    value = cluster.whole_job_rate(n_dec, world, t_step)
     algo = algorithmic_bytes(w)
     achieved = algo / (kern_ms * 1e-3) / 1e9
     if rank == 0:

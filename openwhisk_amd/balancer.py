@@ -253,7 +253,7 @@ class GpuShardingContainerPoolBalancer:
         out = (C.c_uint64 * 16)()
         self._chk(self._L.owgs_read_stats(self._h, out, 16))
         d = {"iterations": out[0], "probes": out[1], "fallbacks": out[2], "long_walks": out[3],
-             "exceptions": out[4], "resolved_in_order": out[5]}
+             "conflict_groups": out[4], "incremental": out[5]}
         if any(out[8:16]):
             names = ["releases", "bounds", "chunk_load", "walk", "coop_walk", "grouping", "decide_commit", "other"]
             d["cycles"] = {k: out[8 + i] for i, k in enumerate(names)}

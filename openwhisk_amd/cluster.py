@@ -1,0 +1,68 @@
+"""Multi-controller (multi-GPU) plumbing: one controller shard per GPU, one process per GPU.
+
+The reference runs `clusterSize` controllers side by side; each keeps its own ShardingContainerPoolBalancerState
+whose slots hold `1/clusterSize` of every invoker's memory (SCPB:485-507, updateCluster SCPB:561-584) and schedules
+only the activations it receives.  The shards never exchange scheduling state, so the data path has no collective
+(weak scaling).  What the controllers do share is invoker health: every controller consumes the same health topic
+(InvokerPool, SCPB:355-358).  Here that is one all-gather of the health vector per step; a shard adopts rank 0's
+view, which equals its own when the views agree (they do unless a health ping is in flight).
+
+Works with any torch.distributed backend: RCCL ("nccl") on the GPUs, gloo on the CPU (tests/test_distributed.py).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+
+def env_rank() -> tuple[int, int, int]:
+    """(rank, world, local_rank) from the torch.distributed.run environment (defaults: single process)."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def shard_workload(name: str, rank: int, world: int, n_activations: int | None = None, **kw):
+    """The workload of controller shard `rank` of `world` (shared cluster, own stream, clusterSize = world)."""
+    from . import workload as W
+
+    return W.config(name, n_activations=n_activations, shard=rank, n_shards=world, **kw)
+
+
+class HealthExchange:
+    """All-gathers the invoker health vector (uint8 InvokerState codes) across controller shards."""
+
+    def __init__(self, dist, health, world: int):
+        import torch
+
+        self.dist, self.health, self.world = dist, health, world
+        self.flat = torch.empty(world * health.numel(), dtype=health.dtype, device=health.device)
+        self.gathered = self.flat.view(world, health.numel())
+
+    def exchange(self):
+        """Returns the agreed health vector (rank 0's row) as a tensor on the health device."""
+        if self.world > 1:
+            self.dist.all_gather_into_tensor(self.flat, self.health)
+        else:
+            self.gathered[0].copy_(self.health)
+        return self.gathered[0]
+
+    def disagreeing_ranks(self) -> list[int]:
+        """Ranks whose last gathered view differs from rank 0's (diagnostics)."""
+        g = self.gathered.cpu().numpy()
+        return [r for r in range(self.world) if not np.array_equal(g[r], g[0])]
+
+
+def max_over_ranks(dist, values, device) -> list[float]:
+    """Element-wise max of a list of floats over all ranks (step time, error flags, kernel time)."""
+    import torch
+
+    v = torch.tensor([float(x) for x in values], dtype=torch.float64, device=device)
+    if dist is not None:
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    return [float(x) for x in v.cpu()]
+
+
+def whole_job_rate(n_per_shard: int, world: int, t_step_max: float) -> float:
+    """Weak-scaling throughput: all shards' decisions divided by the slowest shard's step time."""
+    return world * n_per_shard / t_step_max

@@ -85,7 +85,6 @@ __device__ __forceinline__ int mod_small(int x, int R) {
 }
 
 __device__ __forceinline__ int ffs64(u64 m) { return __ffsll((long long)m) - 1; }
-__device__ __forceinline__ u64 lt_mask_of(int l) { return l >= 64 ? ~0ull : ((1ull << l) - 1ull); }
 __device__ __forceinline__ int fls64(u64 m) { return 63 - __clzll((long long)m); }
 
 __device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
@@ -389,6 +388,7 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
     PT_DECL
     uint32_t iter = 0;
     const u64 lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+    const u64 self_bit = 1ull << lane;
 
     for (int b = 0; b < A.n_batches; ++b) {
         // ================================================================ releases (SCPB:327-331, NS:98-113)
@@ -513,257 +513,356 @@ __global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
                 pending = false;
             }
 
+            int f = 0;
+            bool full = true;  // lanes >= f need (re)speculation
+            // per-lane speculation, valid for lanes >= f until the next full pass
+            int kind = K_NONE, tgt = -1, room = 0, c0 = 0, cidx = -1, ops0 = 0, q = 0, cons = 0;
+            bool unc = false, fullwalk = false;
             PT(2);
-            // ---------------------------------------------------------------- 1. speculate every lane's target
-            // against the state at the chunk start (exact for lane 0; a lower bound on the walk step for the rest)
-            int kind = K_NONE, tgt = -1, c0 = 0, cidx = -1, ops0 = 0;
-            bool fullwalk = false;
-            if (pending) {
-                if (cok) {  // cursor = walk step << 16 | pool position
-                    const int cv = cur[a];
-                    if ((cv >> 16) > s) {
-                        s = cv >> 16;
-                        pos = cv & 0xFFFF;
-                    }
-                }
-                kind = K_LONG;
-                if (maxc == 1) {
-                    if (mem > (pool ? U1 : U0) && ((A.shortcut_ok >> pool) & 1)) {
-                        kind = K_FALLBACK;  // every usable permit < mem: the walk fails everywhere
-                    } else {
-#pragma unroll 1
-                        for (int k = 0; k < KPROBE; ++k) {
-                            if (s >= n) {  // every pool position probed: the n+2-probe walk fails (SCPB:417)
-                                kind = K_FALLBACK;
-                                fullwalk = true;
-                                break;
+            while (__ballot(pending)) {
+                const bool act = pending && lane >= f;
+                if (full) {
+                    full = false;
+                    ++st_iter;
+                    // ---------------------------------------------------- speculate targets against state at f
+                    kind = K_NONE;
+                    tgt = -1;
+                    c0 = 0;
+                    cidx = -1;
+                    ops0 = 0;
+                    q = 0;
+                    unc = false;
+                    fullwalk = false;
+                    int pv = 0;
+                    if (act) {
+                        if (cok) {  // cursor = walk step << 16 | pool position
+                            const int cv = cur[a];
+                            if ((cv >> 16) > s) {
+                                s = cv >> 16;
+                                pos = cv & 0xFFFF;
                             }
-                            const int w = pw[pwb + pos];
-                            ++st_probe;
-                            if (w >= 0) {
-                                const int p = perm[w];
-                                if (p >= mem) {
-                                    kind = K_TARGET;
-                                    tgt = w;
+                        }
+                        kind = K_LONG;
+                        if (maxc == 1) {
+                            if (mem > (pool ? U1 : U0) && ((A.shortcut_ok >> pool) & 1)) {
+                                kind = K_FALLBACK;  // every usable permit < mem: the walk fails everywhere
+                            } else {
+#pragma unroll 1
+                                for (int k = 0; k < KPROBE; ++k) {
+                                    if (s >= n) {  // every pool position probed: the n+2-probe walk fails (SCPB:417)
+                                        kind = K_FALLBACK;
+                                        fullwalk = true;
+                                        break;
+                                    }
+                                    const int w = pw[pwb + pos];
+                                    ++st_probe;
+                                    if (w >= 0) {
+                                        const int p = perm[w];
+                                        if (p >= mem) {
+                                            kind = K_TARGET;
+                                            tgt = w;
+                                            pv = p;
+                                            break;
+                                        }
+                                    } else if (w == OWGS_PW_BADID) {
+                                        kind = K_THROW;
+                                        break;
+                                    }
+                                    pos = next_pos(pos, step, n);
+                                    ++s;
+                                }
+                            }
+                        }
+                    }
+                    if (__ballot(act && maxc > 1)) {  // concurrent actions: c >= 1 also makes a probe feasible
+                        if (act && maxc > 1) {
+#pragma unroll 1
+                            for (int k = 0; k < KPROBE; ++k) {
+                                if (s >= n) {
+                                    kind = K_FALLBACK;
+                                    fullwalk = true;
                                     break;
                                 }
-                            } else if (w == OWGS_PW_BADID) {
-                                kind = K_THROW;
-                                break;
+                                const int w = pw[pwb + pos];
+                                ++st_probe;
+                                if (w >= 0) {
+                                    const int p = perm[w];
+                                    int ix, o;
+                                    const int c = conc_lookup(A, w, slot, &ix, &o);
+                                    if (p >= mem || c >= 1) {
+                                        kind = K_TARGET;
+                                        tgt = w;
+                                        pv = p;
+                                        c0 = c;
+                                        cidx = ix;
+                                        ops0 = o;
+                                        break;
+                                    }
+                                } else if (w == OWGS_PW_BADID) {
+                                    kind = K_THROW;
+                                    break;
+                                }
+                                pos = next_pos(pos, step, n);
+                                ++s;
                             }
+                        }
+                    }
+                    PT(3);
+                    // frontier lane with a long walk: wave-cooperative scan, 64 walk steps per round
+                    if (__builtin_amdgcn_readlane(kind, f) == K_LONG) {
+                        ++st_long;
+                        const CoopResult cr = coop_walk(A, perm, pw, f, s, pos, step, n, pwb, mem, maxc, slot);
+                        if (lane == f) {
+                            s = cr.s;
+                            pos = cr.pos;
+                            if (cr.kind == K_LONG) {
+                                kind = K_FALLBACK;
+                                fullwalk = true;
+                            } else {
+                                kind = cr.kind;
+                                tgt = cr.tgt;
+                                pv = cr.pv;
+                                c0 = cr.c;
+                                cidx = cr.cidx;
+                                ops0 = cr.ops;
+                            }
+                        }
+                    }
+                    // fallback target (SCPB:417-424): H = usable pool members in pool order, r = H[rng(seq) mod |H|]
+                    if (__ballot(act && kind == K_FALLBACK)) {
+                        if (act && kind == K_FALLBACK) {
+                            fallback_target(A, pool, i, n_slots, &kind, &tgt);
+                            if (kind == K_FALLBACK && maxc > 1) c0 = conc_lookup(A, tgt, slot, &cidx, &ops0);
+                        }
+                    }
+                    PT(4);
+                    // ---------------------------------------------------- group by target / by fqn (slot key)
+                    const bool part = act && (kind == K_TARGET || kind == K_FALLBACK);
+                    const bool cpart = part && maxc > 1;
+                    const u64 anyc = __ballot(cpart);
+                    const uint32_t stamp = next_stamp(iter, stT, lane);
+                    if (part) atomicMin(&stT[tgt & (OWGS_STAMP_BUCKETS - 1)], stamp);
+                    if (cpart) atomicMin(&stS[slot & (OWGS_STAMP_BUCKETS - 1)], stamp);
+                    wave_fence();
+                    const bool leadT = part && stT[tgt & (OWGS_STAMP_BUCKETS - 1)] == stamp;
+                    // q = earlier lanes of the same fqn at the same invoker; cons = memory this lane takes;
+                    // E = memory taken at this lane's invoker by earlier lanes of the chunk
+                    int E = 0;
+                    cons = part ? mem : 0;
+                    if (cpart) cons = c0 >= 1 ? 0 : mem;
+                    u64 pend = __ballot(part && !leadT);
+                    while (pend) {
+                        ++st_grp;
+                        const int j = ffs64(pend);
+                        const int t = __builtin_amdgcn_readlane(tgt, j);
+                        const u64 G = __ballot(part && tgt == t);
+                        const bool in = (G >> lane) & 1;
+                        u64 Cg = G & anyc;
+                        while (Cg) {
+                            const int j2 = ffs64(Cg);
+                            const int sl = __builtin_amdgcn_readlane(slot, j2);
+                            const u64 H = Cg & __ballot(slot == sl);
+                            if ((H >> lane) & 1) {
+                                q = __popcll(H & lt_mask);
+                                cons = c_now_of(c0, q, maxc) >= 1 ? 0 : mem;
+                            }
+                            Cg &= ~H;
+                        }
+                        const int ex = wave_excl_scan(in ? cons : 0);
+                        if (in) E = ex;
+                        pend &= ~G;
+                    }
+                    room = pv - E;  // |pv|, E < 2^30 for any sane permit count
+                    // an earlier lane of the same fqn on another walk, or an earlier forced acquire of the same fqn,
+                    // may create concurrency slots this lane's speculation did not see -> uncertain
+                    if (anyc) {
+                        const bool leadS = cpart && stS[slot & (OWGS_STAMP_BUCKETS - 1)] == stamp;
+                        pend = __ballot(cpart && !leadS);
+                        while (pend) {
+                            const int j = ffs64(pend);
+                            const int sl = __builtin_amdgcn_readlane(slot, j);
+                            const u64 Gs = __ballot(cpart && slot == sl);
+                            const int a0 = __builtin_amdgcn_readlane(a, ffs64(Gs));
+                            const u64 D = Gs & __ballot(a != a0);
+                            const u64 FB = Gs & __ballot(kind == K_FALLBACK);
+                            if ((Gs >> lane) & 1) {
+                                const bool lower = (Gs & lt_mask) != 0;
+                                if (kind == K_FALLBACK) unc = lower;
+                                else
+                                    unc = lower &&
+                                          (((FB & lt_mask) != 0) || ((D & (lt_mask | self_bit)) != 0) || a < 0);
+                            }
+                            pend &= ~Gs;
+                        }
+                    }
+                    PT(5);
+                }
+                // -------------------------------------------------------- decide
+                const bool part = act && (kind == K_TARGET || kind == K_FALLBACK);
+                bool ok = false, rej = false;
+                if (act) {
+                    if (kind == K_NONE || kind == K_THROW) {
+                        ok = true;
+                    } else if (kind == K_FALLBACK) {
+                        ok = !(maxc > 1 && unc);
+                    } else if (kind == K_TARGET) {
+                        if (maxc == 1) {
+                            ok = room >= mem;
+                            rej = !ok;
+                        } else if (!unc) {
+                            ok = c_now_of(c0, q, maxc) >= 1 || room >= mem;
+                            rej = !ok;
+                        }
+                    }
+                }
+                const u64 stop = __ballot(act && !ok);
+                const int ls = stop ? ffs64(stop) : 64;
+                const bool commit = act && lane < ls;
+
+                // -------------------------------------------------------- commit lanes [f, l*)
+                if (commit && part && cons > 0) atomicSub(&perm[tgt], mem);
+                if (__ballot(commit && part && maxc > 1)) {
+                    // concurrency map: the last committed lane of each (invoker, fqn) group writes the entry
+                    const bool cpart = part && maxc > 1;
+                    u64 W = __ballot(commit && cpart);
+                    bool writer = false;
+                    while (W) {
+                        const int j = ffs64(W);
+                        const int t = __builtin_amdgcn_readlane(tgt, j);
+                        const int sl = __builtin_amdgcn_readlane(slot, j);
+                        const u64 K = W & __ballot(tgt == t && slot == sl);
+                        if (lane == fls64(K)) writer = true;
+                        W &= ~K;
+                    }
+                    u64 ins = __ballot(writer && cidx < 0);
+                    while (ins) {
+                        const int j = ffs64(ins);
+                        if (lane == j) {
+                            cidx = ct_insert(A.ctab, A.ctab_mask, ct_key(tgt, slot));
+                            if (cidx < 0) atomicOr(A.err, 1);
+                        }
+                        wave_fence();
+                        ins &= ins - 1;
+                    }
+                    if (writer && cidx >= 0) {
+                        const int cn = c_now_of(c0, q, maxc);
+                        int c1;
+                        if (cn >= 1) {
+                            c1 = cn - 1;  // RS.tryAcquire(1)
+                        } else {        // memory (try or force) + RS.release(maxConcurrent - 1, false)
+                            const int next2 = cn + (maxc - 1);
+                            c1 = (mod_small(next2, maxc) == 0) ? next2 - maxc : next2;
+                        }
+                        A.ctab[cidx] = ct_entry(ct_key(tgt, slot), c1, (ops0 > 0 ? ops0 : 0) + q + 1);
+                    }
+                }
+                if (commit) {
+                    A.out_inv[i] = kind == K_NONE ? OWGS_NONE_V : (kind == K_THROW ? OWGS_THROW_V : tgt);
+                    A.out_flags[i] = (kind == K_FALLBACK) ? 1 : 0;
+                    // cursors: steps before the committed target / after a full walk are infeasible from now on
+                    if (cok && (kind == K_TARGET || (kind == K_FALLBACK && maxc == 1)))
+                        atomicMax(&cur[a], kind == K_TARGET ? ((s << 16) | pos) : (n << 16));
+                    pending = false;
+                }
+                const u64 fbm = __ballot(commit && kind == K_FALLBACK);
+                if (fbm) {
+                    st_fb += __popcll(fbm);
+                    wave_fence();
+                    if (commit && cok && kind == K_FALLBACK && maxc > 1) cur[a] = 0;  // forced slots: anywhere
+                    // a failed full walk proves every usable pool member has permits < mem from now on
+                    const bool t = commit && kind == K_FALLBACK && fullwalk && maxc == 1;
+                    if (__ballot(t)) {
+                        U0 = min(U0, wave_min(t && pool == 0 ? mem - 1 : 0x7FFFFFFF));
+                        U1 = min(U1, wave_min(t && pool == 1 ? mem - 1 : 0x7FFFFFFF));
+                    }
+                }
+                PT(6);
+                if (ls == 64) break;
+
+                // -------------------------------------------------------- resolve l*
+                const int lk = __builtin_amdgcn_readlane(kind, ls);
+                const int lmc = __builtin_amdgcn_readlane(maxc, ls);
+                if (lmc == 1 && (lk == K_TARGET || lk == K_LONG)) {
+                    // Incremental: l* is a maxConcurrent==1 lane and every lane before it is committed, so the
+                    // state is exact at l*'s time.  Walk it to its true target, commit it, and patch the
+                    // remaining permits (room) of later lanes at its old and new invokers; nothing else changed.
+                    ++st_inc;
+                    wave_fence();
+                    const int lm = __builtin_amdgcn_readlane(mem, ls);
+                    if (lk == K_TARGET) {
+                        const int t_old = __builtin_amdgcn_readlane(tgt, ls);
+                        if (act && lane > ls && tgt == t_old && (kind == K_TARGET || kind == K_FALLBACK)) room += lm;
+                        if (lane == ls) {
                             pos = next_pos(pos, step, n);
                             ++s;
                         }
                     }
-                }
-            }
-            if (__ballot(pending && maxc > 1)) {  // concurrent actions: c >= 1 also makes a probe feasible
-                if (pending && maxc > 1) {
-#pragma unroll 1
-                    for (int k = 0; k < KPROBE; ++k) {
-                        if (s >= n) {
-                            kind = K_FALLBACK;
-                            fullwalk = true;
-                            break;
-                        }
-                        const int w = pw[pwb + pos];
-                        ++st_probe;
-                        if (w >= 0) {
-                            const int p = perm[w];
-                            int ix, o;
-                            const int c = conc_lookup(A, w, slot, &ix, &o);
-                            if (p >= mem || c >= 1) {
-                                kind = K_TARGET;
-                                tgt = w;
-                                c0 = c;
-                                cidx = ix;
-                                ops0 = o;
-                                break;
-                            }
-                        } else if (w == OWGS_PW_BADID) {
-                            kind = K_THROW;
-                            break;
-                        }
-                        pos = next_pos(pos, step, n);
-                        ++s;
-                    }
-                }
-            }
-            // fallback target (SCPB:417-424): H = usable pool members in pool order, r = H[rng(seq) mod |H|]
-            if (__ballot(pending && kind == K_FALLBACK)) {
-                if (pending && kind == K_FALLBACK) {
-                    fallback_target(A, pool, i, n_slots, &kind, &tgt);
-                    if (kind == K_FALLBACK && maxc > 1) c0 = conc_lookup(A, tgt, slot, &cidx, &ops0);
-                }
-            }
-            PT(3);
-            // ---------------------------------------------------------------- 2. clean lanes
-            // A lane is clean when its speculation is exact no matter how the lanes before it resolve: no earlier
-            // lane of the chunk speculated the same invoker (stamp table: lowest lane per bucket, exact match) and,
-            // for concurrent actions, no earlier lane uses the same fqn; forced acquires of concurrent actions and
-            // unfinished walks are never clean.  Everything else is an exception, resolved exactly in stream order.
-            const bool part = pending && (kind == K_TARGET || kind == K_FALLBACK);
-            const bool cpart = part && maxc > 1;
-            const u64 anyc = __ballot(cpart);
-            const uint32_t stamp = next_stamp(iter, stT, lane);
-            if (part) atomicMin(&stT[tgt & (OWGS_STAMP_BUCKETS - 1)], stamp);
-            if (cpart) atomicMin(&stS[slot & (OWGS_STAMP_BUCKETS - 1)], stamp);
-            wave_fence();
-            bool clean = pending && (kind == K_THROW || kind == K_NONE);
-            if (part && stT[tgt & (OWGS_STAMP_BUCKETS - 1)] == stamp) {
-                if (maxc == 1) clean = true;
-                else clean = kind == K_TARGET && stS[slot & (OWGS_STAMP_BUCKETS - 1)] == stamp;
-            }
-            // bucket leaders are exact leaders; a lane sharing a bucket with a lower lane of another target is an
-            // exception it did not need to be (rare, only costs time)
-            u64 X = __ballot(pending && !clean);
-            (void)anyc;
-            st_grp += __popcll(X);
-            PT(4);
-
-            // ---------------------------------------------------------------- 3. commit runs, resolve exceptions
-            int cl = 0;
-            for (;;) {
-                const u64 rest = X & ~(lt_mask_of(cl));
-                const int x = rest ? ffs64(rest) : 64;
-                // bulk-commit the clean lanes [cl, x): their speculation is exact
-                const bool cm = pending && lane >= cl && lane < x;
-                if (__ballot(cm)) {
-                    const int cons = (maxc > 1 && kind == K_TARGET && c0 >= 1) ? 0 : mem;
-                    if (cm && part) atomicSub(&perm[tgt], cons);
-                    if (__ballot(cm && cpart)) {
-                        // concurrency map entry of (tgt, slot): unique among committed lanes of this chunk so far
-                        u64 ins = __ballot(cm && cpart && cidx < 0);
-                        while (ins) {
-                            const int j = ffs64(ins);
-                            if (lane == j) {
-                                cidx = ct_insert(A.ctab, A.ctab_mask, ct_key(tgt, slot));
-                                if (cidx < 0) atomicOr(A.err, 1);
-                            }
-                            wave_fence();
-                            ins &= ins - 1;
-                        }
-                        if (cm && cpart && cidx >= 0) {
-                            int c1;
-                            if (c0 >= 1) {
-                                c1 = c0 - 1;  // RS.tryAcquire(1)
-                            } else {        // memory + RS.release(maxConcurrent - 1, false)
-                                const int next2 = maxc - 1;
-                                c1 = (mod_small(next2, maxc) == 0) ? next2 - maxc : next2;
-                            }
-                            A.ctab[cidx] = ct_entry(ct_key(tgt, slot), c1, (ops0 > 0 ? ops0 : 0) + 1);
+                    if (lane == ls && cok) {
+                        const int cv = cur[a];
+                        if ((cv >> 16) > s) {
+                            s = cv >> 16;
+                            pos = cv & 0xFFFF;
                         }
                     }
-                    if (cm) {
-                        A.out_inv[i] = kind == K_NONE ? OWGS_NONE_V : (kind == K_THROW ? OWGS_THROW_V : tgt);
-                        A.out_flags[i] = (kind == K_FALLBACK) ? 1 : 0;
-                        // cursors: steps before the committed target / after a full walk are infeasible from now on
-                        if (cok && (kind == K_TARGET || (kind == K_FALLBACK && maxc == 1)))
-                            atomicMax(&cur[a], kind == K_TARGET ? ((s << 16) | pos) : (n << 16));
+                    const int lpool = __builtin_amdgcn_readlane(pool, ls);
+                    int nk, nt = -1, nfull = 0;
+                    if (lm > (lpool ? U1 : U0) && ((A.shortcut_ok >> lpool) & 1)) {
+                        nk = K_LONG;  // provably no feasible step: straight to the fallback
+                    } else {
+                        ++st_long;
+                        const CoopResult cr = coop_walk(A, perm, pw, ls, s, pos, step, n, pwb, mem, 1, slot);
+                        if (lane == ls) {
+                            s = cr.s;
+                            pos = cr.pos;
+                        }
+                        nk = cr.kind;
+                        nt = cr.tgt;
+                        nfull = 1;
+                    }
+                    if (nk == K_LONG) {  // every step fails: random fallback
+                        int fk = K_NONE, ft = -1;
+                        if (lane == ls) fallback_target(A, pool, i, n_slots, &fk, &ft);
+                        nk = __builtin_amdgcn_readlane(fk, ls);
+                        nt = __builtin_amdgcn_readlane(ft, ls);
+                        if (nk == K_FALLBACK) {
+                            ++st_fb;
+                            if (nfull) {
+                                if (lpool) U1 = min(U1, lm - 1);
+                                else U0 = min(U0, lm - 1);
+                            }
+                        }
+                    }
+                    if (lane == ls) {
+                        A.out_inv[i] = nk == K_NONE ? OWGS_NONE_V : (nk == K_THROW ? OWGS_THROW_V : nt);
+                        A.out_flags[i] = (nk == K_FALLBACK) ? 1 : 0;
+                        if (nk == K_TARGET || nk == K_FALLBACK) atomicSub(&perm[nt], lm);
+                        if (cok && (nk == K_TARGET || nk == K_FALLBACK))
+                            atomicMax(&cur[a], nk == K_TARGET ? ((s << 16) | pos) : (n << 16));
                         pending = false;
                     }
-                    const bool tf = cm && kind == K_FALLBACK && fullwalk && maxc == 1;
-                    const u64 fbm = __ballot(cm && kind == K_FALLBACK);
-                    if (fbm) {
-                        st_fb += __popcll(fbm);
-                        // a failed full walk proves every usable pool member has permits < mem from now on
-                        if (__ballot(tf)) {
-                            U0 = min(U0, wave_min(tf && pool == 0 ? mem - 1 : 0x7FFFFFFF));
-                            U1 = min(U1, wave_min(tf && pool == 1 ? mem - 1 : 0x7FFFFFFF));
+                    if ((nk == K_TARGET || nk == K_FALLBACK) && act && lane > ls && tgt == nt &&
+                        (kind == K_TARGET || kind == K_FALLBACK))
+                        room -= lm;
+                    wave_fence();
+                    f = ls + 1;
+                } else {
+                    // general case: l* (and every later lane of the same maxConcurrent==1 action speculated at the
+                    // same walk step, when l* is a true rejection) continue past that step; re-speculate from l*
+                    if (__builtin_amdgcn_readlane((int)rej, ls)) {
+                        const int as = __builtin_amdgcn_readlane(a, ls);
+                        const int ss = __builtin_amdgcn_readlane(s, ls);
+                        bool adv = lane == ls;
+                        if (as >= 0 && lmc == 1) adv = adv || (act && lane > ls && a == as && kind == K_TARGET && s == ss);
+                        if (adv) {
+                            pos = next_pos(pos, step, n);
+                            ++s;
                         }
+                        if (lane == ls && cok) atomicMax(&cur[a], (s << 16) | pos);
                     }
                     wave_fence();
+                    f = ls;
+                    full = true;
                 }
-                if (x == 64) break;
-                PT(5);
-
-                // exception x: every lane before it is committed, so the LDS state is exact at x's time
-                ++st_inc;
-                if (lane == x && cok) {
-                    const int cv = cur[a];
-                    if ((cv >> 16) > s) {
-                        s = cv >> 16;
-                        pos = cv & 0xFFFF;
-                    }
-                }
-                const int xm = __builtin_amdgcn_readlane(mem, x);
-                const int xmc = __builtin_amdgcn_readlane(maxc, x);
-                const int xpool = __builtin_amdgcn_readlane(pool, x);
-                CoopResult cr;
-                bool xfull = false;
-                if (xmc == 1 && xm > (xpool ? U1 : U0) && ((A.shortcut_ok >> xpool) & 1)) {
-                    cr.kind = K_LONG;  // provably no feasible step: straight to the fallback
-                    cr.tgt = -1;
-                    cr.c = 0;
-                    cr.cidx = -1;
-                    cr.ops = 0;
-                } else {
-                    ++st_long;
-                    cr = coop_walk(A, perm, pw, x, s, pos, step, n, pwb, mem, maxc, slot);
-                    xfull = true;
-                    if (lane == x) {
-                        s = cr.s;
-                        pos = cr.pos;
-                    }
-                }
-                int nk = cr.kind, nt = cr.tgt, nc = cr.c, nix = cr.cidx, nops = cr.ops;
-                if (nk == K_LONG) {  // every step fails: random fallback + forceAcquire
-                    int fk = K_NONE, ft = -1, fc = 0, fix = -1, fo = 0;
-                    if (lane == x) {
-                        fallback_target(A, pool, i, n_slots, &fk, &ft);
-                        if (fk == K_FALLBACK && maxc > 1) fc = conc_lookup(A, ft, slot, &fix, &fo);
-                    }
-                    nk = __builtin_amdgcn_readlane(fk, x);
-                    nt = __builtin_amdgcn_readlane(ft, x);
-                    nc = __builtin_amdgcn_readlane(fc, x);
-                    nix = __builtin_amdgcn_readlane(fix, x);
-                    nops = __builtin_amdgcn_readlane(fo, x);
-                    if (nk == K_FALLBACK) {
-                        ++st_fb;
-                        if (xmc == 1 && xfull) {
-                            if (xpool) U1 = min(U1, xm - 1);
-                            else U0 = min(U0, xm - 1);
-                        }
-                    }
-                }
-                if (lane == x) {
-                    A.out_inv[i] = nk == K_NONE ? OWGS_NONE_V : (nk == K_THROW ? OWGS_THROW_V : nt);
-                    A.out_flags[i] = (nk == K_FALLBACK) ? 1 : 0;
-                    if (nk == K_TARGET || nk == K_FALLBACK) {
-                        const bool slot_taken = maxc > 1 && nc >= 1;  // RS.tryAcquire(1) succeeds
-                        if (!slot_taken) atomicSub(&perm[nt], mem);
-                        if (maxc > 1) {
-                            if (nix < 0) {
-                                nix = ct_insert(A.ctab, A.ctab_mask, ct_key(nt, slot));
-                                if (nix < 0) atomicOr(A.err, 1);
-                            }
-                            if (nix >= 0) {
-                                int c1;
-                                if (slot_taken) {
-                                    c1 = nc - 1;
-                                } else {
-                                    const int next2 = nc + (maxc - 1);
-                                    c1 = (mod_small(next2, maxc) == 0) ? next2 - maxc : next2;
-                                }
-                                A.ctab[nix] = ct_entry(ct_key(nt, slot), c1, (nops > 0 ? nops : 0) + 1);
-                            }
-                        }
-                        if (cok) {
-                            if (nk == K_TARGET) atomicMax(&cur[a], (s << 16) | pos);
-                            else if (maxc == 1) atomicMax(&cur[a], n << 16);
-                            else cur[a] = 0;  // forced concurrency slots may lie anywhere on this walk
-                        }
-                    }
-                    pending = false;
-                }
-                // later lanes whose speculation read the invoker (or fqn) x just changed are no longer clean
-                if (nk == K_TARGET || nk == K_FALLBACK) {
-                    const int xs = __builtin_amdgcn_readlane(slot, x);
-                    X |= __ballot(pending && lane > x && part && (tgt == nt || (xmc > 1 && cpart && slot == xs)));
-                }
-                wave_fence();
-                cl = x + 1;
-                PT(6);
             }
         }
         wave_fence();

@@ -14,7 +14,8 @@ Configs (BASELINE.json "configs"):
   c3        10k invokers, 10 % unhealthy/offline, 10 % blackbox actions, load 1.2 x capacity (overload fallback)
   c4        c2 + 30 % concurrent actions (maxConcurrent 2..500) with completion releases
   headline  10k invokers x 16 GiB, 1M activations per shard, Zipf 1.0, 128..2048 MB, 10 % blackbox, 20 % concurrent,
-            2 % unhealthy, clusterSize = number of shards (one shard per GPU, SCPB:485-499 / 561-584)
+            2 % unhealthy, clusterSize = number of shards (one shard per GPU, SCPB:485-499 / 561-584); all shards
+            share invokers, health and actions, each has its own activation stream
 """
 from __future__ import annotations
 
@@ -92,7 +93,9 @@ def generate(name: str = "headline", n_invokers: int = 10_000, user_memory_mb: i
              shared_frac: float = 0.1, n_activations: int = 1_000_000, load: float = 0.9, delay_mean: float = 4.0,
              batch: int | None = None, managed_fraction: float = 0.9, blackbox_fraction: float = 0.1,
              cluster_size: int = 1, min_memory_mb: int = 128, seed: int = 0x0F15C005, rng_seed: int | None = None,
-             fixed_actions: list | None = None) -> Workload:
+             fixed_actions: list | None = None, shard: int | None = None) -> Workload:
+    """`seed` fixes the cluster (invokers, their health, the action universe and its popularity order), which every
+    controller shard shares; `shard` (when given) seeds that controller's own activation stream."""
     rng = np.random.Generator(np.random.PCG64(seed))
     # ---- invokers (dense ids, as InvokerPool.registerInvoker pads them: InvokerSupervision.scala:191-207)
     inv_ids = np.arange(n_invokers, dtype=np.int32)
@@ -132,8 +135,9 @@ def generate(name: str = "headline", n_invokers: int = 10_000, user_memory_mb: i
     capacity = usable * slot_mb / max(mem_per_act, 1e-9)
     if batch is None:
         batch = max(1, int(load * capacity / delay_mean))
-    keys = perm[_zipf_sample(rng, n_keys, zipf_s, n_activations)]
-    stream = make_stream(rng, n_activations, batch, delay_mean, keys=keys)
+    srng = rng if shard is None else np.random.Generator(np.random.PCG64([seed, shard]))
+    keys = perm[_zipf_sample(srng, n_keys, zipf_s, n_activations)]
+    stream = make_stream(srng, n_activations, batch, delay_mean, keys=keys)
     info = dict(batch=batch, n_batches=stream.n_batches, capacity_activations=capacity, mem_per_activation=mem_per_act,
                 slot_mb=int(slot_mb), usable=usable, n_keys=n_keys, load=load, delay_mean=delay_mean)
     return Workload(name, inv_ids, inv_mem, inv_status, managed_fraction, blackbox_fraction, actions, stream,
@@ -156,7 +160,7 @@ def config(name: str, n_activations: int | None = None, shard: int = 0, n_shards
         base = dict(n_invokers=1000, conc_frac=0.3, blackbox_frac=0.0, unhealthy_frac=0.0, seed=0x0F15C004)
     elif name in ("headline", "c5"):
         base = dict(n_invokers=10_000, conc_frac=0.2, blackbox_frac=0.1, unhealthy_frac=0.02,
-                    seed=0x0F15C005 + shard, cluster_size=n_shards)
+                    seed=0x0F15C005, shard=shard, rng_seed=0x0F15C005 + shard, cluster_size=n_shards)
     else:
         raise ValueError(name)
     base.update(kw)

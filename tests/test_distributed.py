@@ -1,0 +1,103 @@
+"""Multi-controller path on the CPU: world_size 2 over gloo (the GPU run uses RCCL with the same code).
+
+Each rank is one controller shard (clusterSize = 2, SCPB:485-507): it builds its shard workload, agrees on invoker
+health with the other rank (HealthExchange), replays its own stream through the oracle, and the ranks combine step
+times by max (bench.py's aggregation).  Checks: shards share cluster + health but not streams, each shard's slots hold
+half of every invoker (getInvokerSlot), shard replays are independent of each other (replaying rank r's stream alone
+gives the same answer as inside the 2-rank job), and the whole-job rate uses the slowest rank.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N_ACT = 20_000
+KW = dict(n_invokers=400, n_actions=800, n_namespaces=80)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, out_dir):
+    for p in (ROOT, os.path.join(ROOT, "oracle")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+    import oracle as O
+    from openwhisk_amd import cluster
+
+    w = cluster.shard_workload("headline", rank, world, n_activations=N_ACT, **KW)
+    health = torch.from_numpy(w.inv_status.copy())
+    hx = cluster.HealthExchange(dist, health, world)
+    agreed = hx.exchange().numpy()
+    st = O.state_for(w)
+    inv, fl, rf = st.replay(w.stream)
+    t_step = 0.010 * (rank + 1)  # synthetic per-rank step times: the max must win
+    t_max, = cluster.max_over_ranks(dist, [t_step], torch.device("cpu"))
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), agreed=agreed, disagree=np.array(hx.disagreeing_ranks()),
+             inv=inv, fl=fl, rf=rf, permits=st.permits(), act=w.stream.act, t_max=t_max,
+             rate=cluster.whole_job_rate(len(w.stream.act), world, t_max))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def two_ranks(tmp_path_factory):
+    out = tmp_path_factory.mktemp("dist")
+    mp.start_processes(_rank_main, args=(2, _free_port(), str(out)), nprocs=2, join=True, start_method="spawn")
+    return [dict(np.load(out / f"rank{r}.npz")) for r in range(2)]
+
+
+def test_shards_share_cluster_not_streams(two_ranks):
+    r0, r1 = two_ranks
+    assert np.array_equal(r0["agreed"], r1["agreed"])
+    assert len(r0["disagree"]) == 0 and len(r1["disagree"]) == 0
+    assert not np.array_equal(r0["act"], r1["act"])
+
+
+def test_shard_slots_hold_half_of_each_invoker(two_ranks):
+    from openwhisk_amd import cluster
+    import oracle as O
+
+    w = cluster.shard_workload("headline", 0, 2, n_activations=10, **KW)
+    st = O.state_for(w)
+    assert st.permits().tolist() == [16_384 // 2] * KW["n_invokers"]  # getInvokerSlot: 16 GiB / clusterSize 2
+
+
+def test_shard_replay_is_independent_of_the_job(two_ranks):
+    from openwhisk_amd import cluster
+    import oracle as O
+
+    for r in (0, 1):
+        w = cluster.shard_workload("headline", r, 2, n_activations=N_ACT, **KW)
+        st = O.state_for(w)
+        inv, fl, rf = st.replay(w.stream)
+        assert np.array_equal(inv, two_ranks[r]["inv"]) and np.array_equal(fl, two_ranks[r]["fl"])
+        assert np.array_equal(rf, two_ranks[r]["rf"])
+        assert np.array_equal(st.permits(), two_ranks[r]["permits"])
+
+
+def test_assignments_respect_health(two_ranks):
+    health = two_ranks[0]["agreed"]
+    for r in two_ranks:
+        inv = r["inv"]
+        placed = inv[inv >= 0]
+        assert len(placed) > 0.9 * len(inv)
+        # normal placements (no overload flag) only go to healthy invokers
+        normal = inv[(inv >= 0) & ((r["fl"] & 1) == 0)]
+        assert np.all(health[normal] == 0)
+
+
+def test_max_over_ranks_and_rate(two_ranks):
+    for r in two_ranks:
+        assert float(r["t_max"]) == pytest.approx(0.020)
+        assert float(r["rate"]) == pytest.approx(2 * N_ACT / 0.020)
