@@ -252,9 +252,9 @@ class GpuShardingContainerPoolBalancer:
     def stats(self) -> dict:
         out = (C.c_uint64 * 16)()
         self._chk(self._L.owgs_read_stats(self._h, out, 16))
-        d = {"iterations": out[0], "probes": out[1], "fallbacks": out[2], "long_walks": out[3],
-             "conflict_groups": out[4], "incremental": out[5]}
+        d = {"passes": out[0], "probes": out[1], "fallbacks": out[2], "long_walks": out[3], "chunks": out[4],
+             "stops": out[5]}
         if any(out[8:16]):
-            names = ["releases", "bounds", "chunk_load", "walk", "coop_walk", "grouping", "decide_commit", "other"]
+            names = ["batch", "chunk_load", "spec_setup", "walk_fast", "walk_general", "long_walk", "buckets", "validate_commit"]
             d["cycles"] = {k: out[8 + i] for i, k in enumerate(names)}
         return d

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -20,11 +21,20 @@ typedef unsigned long long u64;
 
 extern "C" hipError_t owgs_launch_hash(const OwgsHashArgs* a, hipStream_t s);
 extern "C" hipError_t owgs_launch_lookup(const OwgsLookupArgs* a, hipStream_t s);
-extern "C" hipError_t owgs_launch_gather(const OwgsGatherArgs* g, hipStream_t s);
 extern "C" hipError_t owgs_launch_selftest(int* bad, int trials, hipStream_t s);
 extern "C" hipError_t owgs_launch_prepare(const OwgsPrepArgs* a, hipStream_t s);
+extern "C" hipError_t owgs_launch_prepass(const OwgsPrepassArgs* a, int32_t* cstart, int64_t max_chunks,
+                                          hipStream_t s);
+extern "C" int64_t owgs_relscan_blocks(int64_t n_rel);
+extern "C" hipError_t owgs_launch_relscan(const int64_t* rel_aid, int64_t n_rel, const int32_t* act,
+                                          const uint2* act_meta, int32_t* cpos, int32_t* bsum,
+                                          const int64_t* rel_off, int32_t n_batches, int32_t* relx,
+                                          int32_t* crel_off, hipStream_t s);
+extern "C" hipError_t owgs_launch_relflags(const int64_t* rel_aid, int64_t n_rel, const int32_t* out_inv,
+                                           uint8_t* rel_flags, hipStream_t s);
+extern "C" hipError_t owgs_launch_release_seq(const OwgsReleaseArgs* a, hipStream_t s);
 extern "C" hipError_t owgs_launch_engine(const OwgsEngineArgs* a, hipStream_t s);
-extern "C" size_t owgs_engine_lds_bytes(int n_slots, int nm, int nb, int n_cursors);
+extern "C" size_t owgs_engine_lds_bytes(int n_slots, int pool_mode, int n_ids, int nm, int nb, int n_actions);
 
 namespace {
 
@@ -80,10 +90,7 @@ std::vector<int32_t> pairwise_coprime(int32_t x) {  // SCPB:379-384
     return out;
 }
 
-constexpr uint32_t kCtabLog2 = 19;  // 512k entries x 8 B = 4 MiB: one XCD L2
-
 }  // namespace
-
 struct owgs_ctx {
     owgs_config cfg{};
     double mf = 0, bf = 0;
@@ -104,6 +111,7 @@ struct owgs_ctx {
 
     // derived pools
     int32_t nm = 0, nb = 0, hm = 0, hb = 0, shortcut_ok = 3;
+    int32_t pool_mode = 0, n_ids = 0;  // 0: pool position p -> id p (managed) / N - nb + p (blackbox)
 
     // actions
     std::vector<int32_t> a_mem, a_maxc, a_slot, a_hash;
@@ -111,24 +119,24 @@ struct owgs_ctx {
     std::vector<int32_t> slot_uses, slot_maxc, slot_mem;
     std::unordered_map<std::string, int32_t> slot_ids;
 
-    // device
+    // device state
     DevBuf<int32_t> d_permits, d_pool_words, d_hlist, d_act_slot, d_act_hash, d_act_mem, d_act_maxc, d_msteps,
         d_bsteps, d_err;
+    DevBuf<uint32_t> d_usable, d_ct_keys, d_ct_vals, d_ct_tmp;
     DevBuf<uint8_t> d_act_bb, d_act_cok;
-    DevBuf<int4> d_act_info;
-    DevBuf<u64> d_ctab, d_stats;
-    uint32_t ctab_mask = 0;
-    // scratch for host-buffer entry points
+    DevBuf<uint2> d_act_meta;
+    DevBuf<u64> d_stats;
+    // per-call scratch
     DevBuf<int64_t> d_off;
-    DevBuf<int32_t> d_a, d_b, d_out;
+    DevBuf<int32_t> d_a, d_b, d_c, d_d, d_out, d_cstart, d_relx, d_cpos, d_bsum, d_crel_off, d_acc, d_xslot;
     DevBuf<uint8_t> d_flags, d_rflags;
     DevBuf<u64> d_seq;
     DevBuf<int64_t> d_rel;
-    DevBuf<int4> d_info, d_rinfo;
-    DevBuf<int2> d_aux;
+    DevBuf<uint4> d_rec;
+    DevBuf<uint2> d_rel_rec, d_xmeta;
     // snapshot
     DevBuf<int32_t> s_permits;
-    DevBuf<u64> s_ctab;
+    DevBuf<uint32_t> s_ct_keys, s_ct_vals;
     bool has_snap = false;
     int32_t snap_slots = 0;
 
@@ -162,11 +170,16 @@ static hipError_t upload(DevBuf<T>& d, const T* h, size_t n, hipStream_t s) {
     return hipMemcpyAsync(d.p, h, n * sizeof(T), hipMemcpyHostToDevice, s);
 }
 
-// managed = take(managed), blackbox = takeRight(blackboxes) (SCPB:522-523) -> pool words, healthy lists
+// managed = take(managed), blackbox = takeRight(blackboxes) (SCPB:522-523) -> pool words / usable bitmap, healthy
+// lists.  InvokerPool pads the health list so that position i holds invoker id i (InvokerSupervision.scala:191-207):
+// then pool position p is id p (managed) or N - blackboxes + p (blackbox) and the engine keeps only a usable bitmap.
 static int rebuild_pools(owgs_ctx* c) {
     std::vector<int32_t> words, hl;
     int32_t cnt[2], hcnt[2];
     c->shortcut_ok = 3;
+    const int32_t N = (int32_t)c->ids.size();
+    bool identity = !c->pool_override[0] && !c->pool_override[1] && N <= c->n_slots;
+    for (int32_t i = 0; identity && i < N; ++i) identity = c->ids[i] == i;
     for (int p = 0; p < 2; ++p) {
         const int32_t* pid;
         const uint8_t* pst;
@@ -176,7 +189,6 @@ static int rebuild_pools(owgs_ctx* c) {
             pst = c->ov_status[p].data();
             n = (int32_t)c->ov_ids[p].size();
         } else {
-            const int32_t N = (int32_t)c->ids.size();
             const int32_t k = p == 0 ? std::min(c->managed, N) : std::min(c->blackboxes, N);
             const int32_t base = p == 0 ? 0 : N - k;
             pid = c->ids.data() + base;
@@ -200,6 +212,12 @@ static int rebuild_pools(owgs_ctx* c) {
     c->nb = cnt[1];
     c->hm = hcnt[0];
     c->hb = hcnt[1];
+    c->pool_mode = identity ? 0 : 1;
+    c->n_ids = N;
+    std::vector<uint32_t> bits((size_t)(N + 31) / 32 + 1, 0u);
+    for (int32_t i = 0; i < N; ++i)
+        if (c->status[i] == OWGS_HEALTHY) bits[(size_t)i >> 5] |= 1u << (i & 31);
+    HIPCHK(c, upload(c->d_usable, bits.data(), bits.size(), c->stream));
     HIPCHK(c, upload(c->d_pool_words, words.data(), words.size(), c->stream));
     HIPCHK(c, upload(c->d_hlist, hl.data(), hl.size(), c->stream));
     return OWGS_OK;
@@ -210,7 +228,7 @@ static int prepare_actions(owgs_ctx* c) {
     if (n == 0) return OWGS_OK;
     HIPCHK(c, upload(c->d_msteps, c->msteps.data(), c->msteps.size(), c->stream));
     HIPCHK(c, upload(c->d_bsteps, c->bsteps.data(), c->bsteps.size(), c->stream));
-    HIPCHK(c, c->d_act_info.reserve(n));
+    HIPCHK(c, c->d_act_meta.reserve(n));
     OwgsPrepArgs a{};
     a.hash = c->d_act_hash.p;
     a.mem = c->d_act_mem.p;
@@ -224,25 +242,27 @@ static int prepare_actions(owgs_ctx* c) {
     a.n_msteps = (int32_t)c->msteps.size();
     a.bsteps = c->d_bsteps.p;
     a.n_bsteps = (int32_t)c->bsteps.size();
-    a.act_info = c->d_act_info.p;
+    a.act_meta = c->d_act_meta.p;
     HIPCHK(c, owgs_launch_prepare(&a, c->stream));
     return OWGS_OK;
 }
 
-static int32_t n_cursors(const owgs_ctx* c) {
-    const int32_t na = (int32_t)c->a_mem.size();
-    return owgs_engine_lds_bytes(c->n_slots, c->nm, c->nb, na) <= OWGS_LDS_BYTES ? na : 0;
+static size_t lds_need(const owgs_ctx* c, int32_t n_actions) {
+    return owgs_engine_lds_bytes(c->n_slots, c->pool_mode, c->n_ids, c->nm, c->nb, n_actions);
 }
 
 static int lds_check(owgs_ctx* c) {
     if (c->n_slots > OWGS_MAX_SLOTS_CT) return c->fail(OWGS_ERANGE, "invoker ids beyond the concurrency-map key range");
-    if (owgs_engine_lds_bytes(c->n_slots, c->nm, c->nb, 0) > OWGS_LDS_BYTES)
-        return c->fail(OWGS_ERANGE, "slot + pool state exceeds the engine's on-chip (LDS) capacity");
+    if (c->nm > (int32_t)OWGS_AM_POS_MASK || c->nb > (int32_t)OWGS_AM_POS_MASK)
+        return c->fail(OWGS_ERANGE, "pool larger than 32767 positions");
+    if (lds_need(c, (int32_t)c->a_mem.size()) > OWGS_LDS_BYTES)
+        return c->fail(OWGS_ERANGE, "slot + pool + per-action state exceeds the engine's on-chip (LDS) capacity");
     return OWGS_OK;
 }
 
 static int reset_ctab(owgs_ctx* c) {
-    HIPCHK(c, hipMemsetAsync(c->d_ctab.p, 0, c->d_ctab.n * sizeof(u64), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_ct_keys.p, 0, OWGS_CTC * sizeof(uint32_t), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_ct_vals.p, 0, OWGS_CTC * sizeof(uint32_t), c->stream));
     return OWGS_OK;
 }
 
@@ -250,6 +270,9 @@ static void base_args(owgs_ctx* c, OwgsEngineArgs& A) {
     memset(&A, 0, sizeof(A));
     A.permits = c->d_permits.p;
     A.n_slots = c->n_slots;
+    A.pool_mode = c->pool_mode;
+    A.usable = c->d_usable.p;
+    A.n_ids = c->n_ids;
     A.pool_words = c->d_pool_words.p;
     A.nm = c->nm;
     A.nb = c->nb;
@@ -257,14 +280,38 @@ static void base_args(owgs_ctx* c, OwgsEngineArgs& A) {
     A.hm = c->hm;
     A.hb = c->hb;
     A.shortcut_ok = c->shortcut_ok;
-    A.act_info = c->d_act_info.p;
-    A.act_slot = c->d_act_slot.p;
-    A.ctab = c->d_ctab.p;
-    A.ctab_mask = c->ctab_mask;
-    A.n_cursors = n_cursors(c);
+    A.ct_keys = c->d_ct_keys.p;
+    A.ct_vals = c->d_ct_vals.p;
+    A.ct_tmp = c->d_ct_tmp.p;
+    A.n_actions = (int32_t)c->a_mem.size();
     A.rng_seed = c->cfg.rng_seed;
     A.stats = c->d_stats.p;
     A.err = c->d_err.p;
+    const char* o = getenv("OWGS_OPTS");
+    A.opts = o ? atoi(o) : 0;
+}
+
+// chunk records of n_act activations (act != null: registered actions; else explicit per-activation walks)
+static int run_prepass(owgs_ctx* c, OwgsEngineArgs& A, int32_t n_batches, const int64_t* acq_off, const int32_t* act,
+                       int64_t n_act, hipStream_t s) {
+    HIPCHK(c, c->d_rec.reserve((size_t)std::max<int64_t>(n_act, 1)));
+    HIPCHK(c, c->d_cstart.reserve((size_t)n_batches + 1));
+    OwgsPrepassArgs p{};
+    p.n_batches = n_batches;
+    p.acq_off = acq_off;
+    p.act = act;
+    p.act_meta = c->d_act_meta.p;
+    p.act_slot = c->d_act_slot.p;
+    p.xmeta = c->d_xmeta.p;
+    p.xslot = c->d_xslot.p;
+    p.rec = c->d_rec.p;
+    const int64_t max_chunks = n_act / OWGS_WL + n_batches;
+    HIPCHK(c, owgs_launch_prepass(&p, c->d_cstart.p, max_chunks, s));
+    A.n_batches = n_batches;
+    A.acq_off = acq_off;
+    A.n_act = n_act;
+    A.rec = c->d_rec.p;
+    return OWGS_OK;
 }
 
 static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s) {
@@ -275,39 +322,24 @@ static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s) {
     return OWGS_OK;
 }
 
-// dense per-activation / per-release records for the engine (owgs_gather_kernel)
-static int run_gather(owgs_ctx* c, OwgsEngineArgs& A, const int32_t* act, int64_t n_act, const int64_t* rel_aid,
-                      const int32_t* rel_inv, const int32_t* rel_act, int64_t n_rel, hipStream_t s) {
-    HIPCHK(c, c->d_info.reserve((size_t)std::max<int64_t>(n_act, 1)));
-    HIPCHK(c, c->d_aux.reserve((size_t)std::max<int64_t>(n_act, 1)));
-    HIPCHK(c, c->d_rinfo.reserve((size_t)std::max<int64_t>(n_rel, 1)));
-    OwgsGatherArgs g{};
-    g.act = act;
-    g.n_act = n_act;
-    g.act_info = c->d_act_info.p;
-    g.act_slot = c->d_act_slot.p;
-    g.info = c->d_info.p;
-    g.aux = c->d_aux.p;
-    g.rel_aid = rel_aid;
-    g.rel_inv = rel_inv;
-    g.rel_act = rel_act;
-    g.n_rel = n_rel;
-    g.rinfo = c->d_rinfo.p;
-    HIPCHK(c, owgs_launch_gather(&g, s));
-    A.info = c->d_info.p;
-    A.aux = c->d_aux.p;
-    A.rinfo = c->d_rinfo.p;
-    return OWGS_OK;
-}
-
 static int check_err_word(owgs_ctx* c) {
     int32_t e = 0;
     HIPCHK(c, hipMemcpy(&e, c->d_err.p, sizeof(int32_t), hipMemcpyDeviceToHost));
     if (e) {
         HIPCHK(c, hipMemset(c->d_err.p, 0, sizeof(int32_t)));
-        return c->fail(OWGS_ENOMEM, "concurrency table full");
+        if (e & OWGS_ERR_CTAB_FULL) return c->fail(OWGS_ENOMEM, "concurrency table full");
+        if (e & OWGS_ERR_OPS) return c->fail(OWGS_ERANGE, "operationCount beyond the engine's range");
+        if (e & OWGS_ERR_INTERNAL) return c->fail(OWGS_EDEVICE, "engine invariant violated");
+        return c->fail(OWGS_EINVAL, "stream releases an activation that holds no slot (or a permit overflow)");
     }
     return OWGS_OK;
+}
+
+static bool registered(const owgs_ctx* c, int32_t n, const int32_t* action) {
+    const int32_t na = (int32_t)c->a_mem.size();
+    for (int32_t i = 0; i < n; ++i)
+        if (action[i] < 0 || action[i] >= na) return false;
+    return true;
 }
 
 extern "C" {
@@ -315,9 +347,11 @@ extern "C" {
 int owgs_abi_version(void) { return OWGS_ABI_VERSION; }
 
 int owgs_limits(int32_t* max_invokers, int32_t* max_slots) {
-    const int32_t words = OWGS_LDS_BYTES / 4 - 2 * OWGS_STAMP_BUCKETS - 8;
-    if (max_invokers) *max_invokers = words / 2;
-    if (max_slots) *max_slots = words / 2;
+    // identity pools, no registered actions: 4 B permits + 1 bit usable per invoker on top of the fixed LDS state
+    const size_t fixed = owgs_engine_lds_bytes(0, 0, 0, 0, 0, 0);
+    const int32_t n = (int32_t)std::min<size_t>((OWGS_LDS_BYTES - fixed - 64) * 8 / 33, OWGS_MAX_SLOTS_CT);
+    if (max_invokers) *max_invokers = n;
+    if (max_slots) *max_slots = n;
     return OWGS_OK;
 }
 
@@ -341,14 +375,14 @@ int owgs_create(const owgs_config* cfg, owgs_ctx** out) {
         delete c;
         return OWGS_EDEVICE;
     }
-    const size_t cap = (size_t)1 << kCtabLog2;
-    if (c->d_ctab.reserve(cap) || c->d_stats.reserve(16) || c->d_err.reserve(1) ||
-        c->d_permits.reserve(1)) {
+    if (c->d_ct_keys.reserve(OWGS_CTC) || c->d_ct_vals.reserve(OWGS_CTC) || c->d_ct_tmp.reserve(2 * OWGS_CTC) ||
+        c->d_stats.reserve(16) ||
+        c->d_err.reserve(1) || c->d_permits.reserve(1)) {
         owgs_destroy(c);
         return OWGS_ENOMEM;
     }
-    c->ctab_mask = (uint32_t)(cap - 1);
-    if (reset_ctab(c) || hipMemset(c->d_err.p, 0, sizeof(int32_t)) != hipSuccess) {
+    if (reset_ctab(c) || hipMemset(c->d_err.p, 0, sizeof(int32_t)) != hipSuccess ||
+        hipMemset(c->d_stats.p, 0, 16 * sizeof(u64)) != hipSuccess) {
         owgs_destroy(c);
         return OWGS_EDEVICE;
     }
@@ -370,23 +404,25 @@ void owgs_destroy(owgs_ctx* c) {
     (void)hipSetDevice(c->cfg.device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf<int32_t>* i32s[] = {&c->d_permits, &c->d_pool_words, &c->d_hlist, &c->d_act_slot, &c->d_act_hash,
-                               &c->d_act_mem, &c->d_act_maxc, &c->d_msteps, &c->d_bsteps, &c->d_err, &c->d_a,
-                               &c->d_b, &c->d_out, &c->s_permits};
+                               &c->d_act_mem,  &c->d_act_maxc,   &c->d_msteps, &c->d_bsteps,   &c->d_err,
+                               &c->d_a,        &c->d_b,          &c->d_c,      &c->d_d,        &c->d_out,
+                               &c->d_cstart,   &c->d_relx,       &c->d_cpos,   &c->d_bsum,     &c->d_crel_off,
+                               &c->d_acc,      &c->d_xslot,      &c->s_permits};
     for (auto* b : i32s) b->release();
+    DevBuf<uint32_t>* u32s[] = {&c->d_usable, &c->d_ct_keys, &c->d_ct_vals, &c->d_ct_tmp, &c->s_ct_keys, &c->s_ct_vals};
+    for (auto* b : u32s) b->release();
     c->d_act_bb.release();
     c->d_act_cok.release();
-    c->d_act_info.release();
-    c->d_ctab.release();
+    c->d_act_meta.release();
     c->d_stats.release();
     c->d_off.release();
     c->d_flags.release();
     c->d_rflags.release();
     c->d_seq.release();
     c->d_rel.release();
-    c->d_info.release();
-    c->d_rinfo.release();
-    c->d_aux.release();
-    c->s_ctab.release();
+    c->d_rec.release();
+    c->d_rel_rec.release();
+    c->d_xmeta.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -465,10 +501,13 @@ int owgs_register_actions(owgs_ctx* c, int32_t n, const char* ns_bytes, const in
     for (int32_t i = 0; i < n; ++i) {
         // MemoryLimit/ConcurrencyLimit guarantee positive values (MemoryLimit.scala:68-69); the reference's
         // require(...) checks (FS:96, NS:85) would throw on anything else
-        if (mem_mb[i] <= 0 || max_conc[i] < 1 || max_conc[i] > OWGS_MAX_CONC) return c->fail(OWGS_EINVAL, "mem/maxConcurrent");
+        if (mem_mb[i] <= 0 || mem_mb[i] > OWGS_MAX_MEM_MB || max_conc[i] < 1 || max_conc[i] > OWGS_MAX_CONC)
+            return c->fail(OWGS_EINVAL, "mem/maxConcurrent");
         if (ns_off[i + 1] < ns_off[i] || path_off[i + 1] < path_off[i] || key_off[i + 1] < key_off[i])
             return c->fail(OWGS_EINVAL, "offsets");
     }
+    if (c->a_mem.size() + (size_t)n > (size_t)OWGS_REC_NOACT)
+        return c->fail(OWGS_ERANGE, "too many actions");
     // validate before mutating: one fqn@version has one set of limits (the action document is versioned)
     {
         std::unordered_map<std::string, std::pair<int32_t, int32_t>> seen;
@@ -557,9 +596,7 @@ int owgs_publish_batch(owgs_ctx* c, int32_t n, const int32_t* action, const uint
                        int32_t* out_invoker, uint8_t* out_flags) {
     if (!c || n < 0 || (n > 0 && (!action || !out_invoker || !out_flags))) return OWGS_EINVAL;
     if (n == 0) return OWGS_OK;
-    const int32_t na = (int32_t)c->a_mem.size();
-    for (int32_t i = 0; i < n; ++i)
-        if (action[i] < 0 || action[i] >= na) return c->fail(OWGS_ENOENT, "unknown action");
+    if (!registered(c, n, action)) return c->fail(OWGS_ENOENT, "unknown action");
     (void)hipSetDevice(c->cfg.device);
     const int64_t off[2] = {0, n};
     HIPCHK(c, upload(c->d_off, off, 2, c->stream));
@@ -569,14 +606,11 @@ int owgs_publish_batch(owgs_ctx* c, int32_t n, const int32_t* action, const uint
     HIPCHK(c, c->d_flags.reserve((size_t)n));
     OwgsEngineArgs A;
     base_args(c, A);
-    A.n_batches = 1;
-    A.acq_off = c->d_off.p;
-    A.act = c->d_a.p;
     A.seq_base = seq_base;
     A.seq = seq ? c->d_seq.p : nullptr;
     A.out_inv = c->d_out.p;
     A.out_flags = c->d_flags.p;
-    int rc = run_gather(c, A, c->d_a.p, n, nullptr, nullptr, nullptr, 0, c->stream);
+    int rc = run_prepass(c, A, 1, c->d_off.p, c->d_a.p, n, c->stream);
     if (!rc) rc = run_engine(c, A, c->stream);
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(out_invoker, c->d_out.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
@@ -588,26 +622,32 @@ int owgs_publish_batch(owgs_ctx* c, int32_t n, const int32_t* action, const uint
 int owgs_release_batch(owgs_ctx* c, int32_t n, const int32_t* invoker, const int32_t* action, uint8_t* out_flags) {
     if (!c || n < 0 || (n > 0 && (!invoker || !action))) return OWGS_EINVAL;
     if (n == 0) return OWGS_OK;
-    const int32_t na = (int32_t)c->a_mem.size();
-    for (int32_t i = 0; i < n; ++i)
-        if (action[i] < 0 || action[i] >= na) return c->fail(OWGS_ENOENT, "unknown action");
+    if (!registered(c, n, action)) return c->fail(OWGS_ENOENT, "unknown action");
     (void)hipSetDevice(c->cfg.device);
-    const int64_t off[4] = {0, 0, 0, n};  // acq_off = {0,0}, rel_off = {0,n}
-    HIPCHK(c, upload(c->d_off, off, 4, c->stream));
+    std::vector<int32_t> mem(n), mc(n), sl(n);
+    for (int32_t i = 0; i < n; ++i) {
+        mem[i] = c->a_mem[action[i]];
+        mc[i] = c->a_maxc[action[i]];
+        sl[i] = c->a_slot[action[i]];
+    }
     HIPCHK(c, upload(c->d_a, invoker, (size_t)n, c->stream));
-    HIPCHK(c, upload(c->d_b, action, (size_t)n, c->stream));
+    HIPCHK(c, upload(c->d_b, mem.data(), (size_t)n, c->stream));
+    HIPCHK(c, upload(c->d_c, mc.data(), (size_t)n, c->stream));
+    HIPCHK(c, upload(c->d_d, sl.data(), (size_t)n, c->stream));
     HIPCHK(c, c->d_rflags.reserve((size_t)n));
-    OwgsEngineArgs A;
-    base_args(c, A);
-    A.n_batches = 1;
-    A.acq_off = c->d_off.p;
-    A.rel_off = c->d_off.p + 2;
-    A.rel_inv = c->d_a.p;
-    A.rel_act = c->d_b.p;
-    A.rel_flags = c->d_rflags.p;
-    int rc = run_gather(c, A, nullptr, 0, nullptr, c->d_a.p, c->d_b.p, n, c->stream);
-    if (!rc) rc = run_engine(c, A, c->stream);
-    if (rc) return rc;
+    OwgsReleaseArgs R{};
+    R.permits = c->d_permits.p;
+    R.n_slots = c->n_slots;
+    R.ct_keys = c->d_ct_keys.p;
+    R.ct_vals = c->d_ct_vals.p;
+    R.n = n;
+    R.inv = c->d_a.p;
+    R.mem = c->d_b.p;
+    R.maxc = c->d_c.p;
+    R.slot = c->d_d.p;
+    R.flags = c->d_rflags.p;
+    R.err = c->d_err.p;
+    HIPCHK(c, owgs_launch_release_seq(&R, c->stream));
     if (out_flags)
         HIPCHK(c, hipMemcpyAsync(out_flags, c->d_rflags.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -620,38 +660,39 @@ int owgs_schedule_walks(owgs_ctx* c, int32_t n, const uint8_t* pool, const int32
     if (!c || n < 0 || (n > 0 && (!pool || !index || !step || !mem_mb || !max_conc || !key || !out_invoker || !out_flags)))
         return OWGS_EINVAL;
     if (n == 0) return OWGS_OK;
-    std::vector<int4> xw(n);
-    std::vector<int2> xa(n);
+    std::vector<uint2> xm(n);
     for (int32_t i = 0; i < n; ++i) {
-        if (mem_mb[i] <= 0 || max_conc[i] < 1 || max_conc[i] > OWGS_MAX_CONC || step[i] < 0 || step[i] > (1 << 30) ||
-            key[i] < 0 || key[i] > OWGS_MAX_SLOTKEYS)
+        if (mem_mb[i] <= 0 || mem_mb[i] > OWGS_MAX_MEM_MB || max_conc[i] < 1 || max_conc[i] > OWGS_MAX_CONC ||
+            step[i] < 0 || step[i] > (1 << 30) || key[i] < 0 || key[i] > OWGS_MAX_SLOTKEYS)
             return c->fail(OWGS_EINVAL, "mem/maxConcurrent/step");
         const int p = pool[i] ? 1 : 0;
         const int32_t np = p ? c->nb : c->nm;
-        uint32_t meta = (uint32_t)max_conc[i] | ((uint32_t)p << OWGS_META_POOL_SHIFT);
-        if (np == 0) meta |= OWGS_META_EMPTY;
-        else if (index[i] < 0 || index[i] >= np) meta |= OWGS_META_THROW;
-        xw[i] = make_int4(index[i], np > 0 ? step[i] % np : 0, mem_mb[i], (int)meta);  // same walk (Java %)
-        xa[i] = make_int2(key[i], -1);
+        uint32_t y = (uint32_t)mem_mb[i] | ((uint32_t)max_conc[i] << OWGS_AM_MAXC_SHIFT);
+        uint32_t x = p ? OWGS_AM_POOL : 0u;
+        if (np == 0) {
+            y |= OWGS_AM_EMPTY;
+        } else if (index[i] < 0 || index[i] >= np) {
+            y |= OWGS_AM_THROW;
+        } else {
+            x |= (uint32_t)index[i] | ((uint32_t)(step[i] % np) << 15);  // same walk (Java %)
+        }
+        xm[i] = make_uint2(x, y);  // no cursor: explicit walks are independent
     }
     (void)hipSetDevice(c->cfg.device);
     const int64_t off[2] = {0, n};
     HIPCHK(c, upload(c->d_off, off, 2, c->stream));
-    HIPCHK(c, upload(c->d_info, xw.data(), (size_t)n, c->stream));
-    HIPCHK(c, upload(c->d_aux, xa.data(), (size_t)n, c->stream));
+    HIPCHK(c, upload(c->d_xmeta, xm.data(), (size_t)n, c->stream));
+    HIPCHK(c, upload(c->d_xslot, key, (size_t)n, c->stream));
     if (seq) HIPCHK(c, upload(c->d_seq, (const u64*)seq, (size_t)n, c->stream));
     HIPCHK(c, c->d_out.reserve((size_t)n));
     HIPCHK(c, c->d_flags.reserve((size_t)n));
     OwgsEngineArgs A;
     base_args(c, A);
-    A.n_batches = 1;
-    A.acq_off = c->d_off.p;
-    A.info = c->d_info.p;
-    A.aux = c->d_aux.p;
     A.seq = seq ? c->d_seq.p : nullptr;
     A.out_inv = c->d_out.p;
     A.out_flags = c->d_flags.p;
-    int rc = run_engine(c, A, c->stream);
+    int rc = run_prepass(c, A, 1, c->d_off.p, nullptr, n, c->stream);
+    if (!rc) rc = run_engine(c, A, c->stream);
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(out_invoker, c->d_out.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(out_flags, c->d_flags.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
@@ -700,7 +741,7 @@ int owgs_read_concurrent(owgs_ctx* c, int32_t invoker, int32_t key, int32_t* per
     HIPCHK(c, upload(di, &invoker, 1, c->stream));
     HIPCHK(c, upload(dk, &key, 1, c->stream));
     HIPCHK(c, dv.reserve(1));
-    OwgsLookupArgs la{c->d_ctab.p, c->ctab_mask, di.p, dk.p, 1, dv.p};
+    OwgsLookupArgs la{c->d_ct_keys.p, c->d_ct_vals.p, di.p, dk.p, 1, dv.p};
     HIPCHK(c, owgs_launch_lookup(&la, c->stream));
     int2 v;
     HIPCHK(c, hipMemcpyAsync(&v, dv.p, sizeof(int2), hipMemcpyDeviceToHost, c->stream));
@@ -743,22 +784,43 @@ int owgs_replay_device(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, c
         n_activations >= ((int64_t)1 << 31) || n_releases < 0 || (n_releases > 0 && (!rel_off || !rel_aid)))
         return OWGS_EINVAL;
     if (n_batches == 0) return OWGS_OK;
+    if (c->a_mem.empty()) return c->fail(OWGS_ENOENT, "no actions registered");
     (void)hipSetDevice(c->cfg.device);
     hipStream_t hs = stream ? (hipStream_t)stream : c->stream;
     OwgsEngineArgs A;
     base_args(c, A);
-    A.n_batches = n_batches;
-    A.acq_off = acq_off;
-    A.act = act;
-    A.rel_off = rel_off;
-    A.rel_aid = rel_aid;
     A.seq_base = seq_base;
     A.out_inv = out_invoker;
     A.out_flags = out_flags;
     A.rel_flags = rel_flags;
-    int rc = run_gather(c, A, act, n_activations, rel_aid, nullptr, nullptr, n_releases, hs);
+    int rc = run_prepass(c, A, n_batches, acq_off, act, n_activations, hs);
     if (rc) return rc;
-    return run_engine(c, A, hs);
+    if (rel_off) {
+        // release bookkeeping: relx per activation, compacted concurrent releases, per-batch aggregation rows
+        const int64_t nr = std::max<int64_t>(n_releases, 1);
+        HIPCHK(c, c->d_relx.reserve((size_t)std::max<int64_t>(n_activations, 1)));
+        HIPCHK(c, c->d_cpos.reserve((size_t)nr));
+        HIPCHK(c, c->d_bsum.reserve((size_t)std::max<int64_t>(owgs_relscan_blocks(n_releases), 1)));
+        HIPCHK(c, c->d_crel_off.reserve((size_t)n_batches + 1));
+        HIPCHK(c, c->d_rel_rec.reserve((size_t)nr));
+        const int64_t stride = ((int64_t)c->n_slots + 63) & ~(int64_t)63;  // whole 256-B lines per row
+        HIPCHK(c, c->d_acc.reserve((size_t)(stride * n_batches)));
+        HIPCHK(c, hipMemsetAsync(c->d_relx.p, 0xFF, (size_t)n_activations * 4, hs));
+        HIPCHK(c, hipMemsetAsync(c->d_acc.p, 0, (size_t)(stride * n_batches) * 4, hs));
+        if (rel_flags && n_releases) HIPCHK(c, hipMemsetAsync(rel_flags, 0, (size_t)n_releases, hs));
+        HIPCHK(c, owgs_launch_relscan(rel_aid, n_releases, act, c->d_act_meta.p, c->d_cpos.p, c->d_bsum.p, rel_off,
+                                      n_batches, c->d_relx.p, c->d_crel_off.p, hs));
+        A.rel_off = rel_off;
+        A.relpos = c->d_relx.p;
+        A.rel_rec = c->d_rel_rec.p;
+        A.crel_off = c->d_crel_off.p;
+        A.acc = c->d_acc.p;
+        A.acc_stride = stride;
+    }
+    rc = run_engine(c, A, hs);
+    if (rc) return rc;
+    if (rel_off && rel_flags) HIPCHK(c, owgs_launch_relflags(rel_aid, n_releases, out_invoker, rel_flags, hs));
+    return OWGS_OK;
 }
 
 int owgs_replay(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const int32_t* act, const int64_t* rel_off,
@@ -768,11 +830,14 @@ int owgs_replay(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const in
     if (n_batches == 0) return OWGS_OK;
     (void)hipSetDevice(c->cfg.device);
     const int64_t n_act = acq_off[n_batches], n_rel = rel_off[n_batches];
-    const int32_t na = (int32_t)c->a_mem.size();
-    for (int64_t i = 0; i < n_act; ++i)
-        if (act[i] < 0 || act[i] >= na) return c->fail(OWGS_ENOENT, "unknown action");
-    for (int64_t r = 0; r < n_rel; ++r)
-        if (rel_aid[r] < 0 || rel_aid[r] >= n_act) return c->fail(OWGS_EINVAL, "release id outside the stream");
+    for (int32_t b = 0; b < n_batches; ++b)
+        if (acq_off[b + 1] < acq_off[b] || rel_off[b + 1] < rel_off[b]) return c->fail(OWGS_EINVAL, "offsets");
+    if (acq_off[0] != 0 || rel_off[0] != 0) return c->fail(OWGS_EINVAL, "offsets must start at 0");
+    if (!registered(c, (int32_t)std::min<int64_t>(n_act, INT32_MAX), act)) return c->fail(OWGS_ENOENT, "unknown action");
+    // a release refers to an activation of an earlier batch
+    for (int32_t b = 0; b < n_batches; ++b)
+        for (int64_t r = rel_off[b]; r < rel_off[b + 1]; ++r)
+            if (rel_aid[r] < 0 || rel_aid[r] >= acq_off[b]) return c->fail(OWGS_EINVAL, "release id outside the stream");
     std::vector<int64_t> offs((size_t)2 * (n_batches + 1));
     memcpy(offs.data(), acq_off, (size_t)(n_batches + 1) * 8);
     memcpy(offs.data() + n_batches + 1, rel_off, (size_t)(n_batches + 1) * 8);
@@ -781,7 +846,7 @@ int owgs_replay(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const in
     HIPCHK(c, upload(c->d_rel, rel_aid, (size_t)n_rel, c->stream));
     HIPCHK(c, c->d_out.reserve((size_t)n_act));
     HIPCHK(c, c->d_flags.reserve((size_t)n_act));
-    HIPCHK(c, c->d_rflags.reserve((size_t)n_rel));
+    HIPCHK(c, c->d_rflags.reserve((size_t)std::max<int64_t>(n_rel, 1)));
     int rc = owgs_replay_device(c, n_batches, c->d_off.p, c->d_a.p, n_act, c->d_off.p + n_batches + 1, c->d_rel.p,
                                 n_rel, seq_base, c->d_out.p, c->d_flags.p, c->d_rflags.p, nullptr);
     if (rc) return rc;
@@ -797,10 +862,12 @@ int owgs_snapshot(owgs_ctx* c) {
     if (!c) return OWGS_EINVAL;
     (void)hipSetDevice(c->cfg.device);
     HIPCHK(c, c->s_permits.reserve((size_t)std::max(c->n_slots, 1)));
-    HIPCHK(c, c->s_ctab.reserve(c->d_ctab.n));
+    HIPCHK(c, c->s_ct_keys.reserve(OWGS_CTC));
+    HIPCHK(c, c->s_ct_vals.reserve(OWGS_CTC));
     if (c->n_slots)
         HIPCHK(c, hipMemcpyAsync(c->s_permits.p, c->d_permits.p, (size_t)c->n_slots * 4, hipMemcpyDeviceToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->s_ctab.p, c->d_ctab.p, c->d_ctab.n * 8, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->s_ct_keys.p, c->d_ct_keys.p, OWGS_CTC * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->s_ct_vals.p, c->d_ct_vals.p, OWGS_CTC * 4, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->has_snap = true;
     c->snap_slots = c->n_slots;
@@ -813,7 +880,8 @@ int owgs_restore(owgs_ctx* c, void* stream) {
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     if (c->n_slots)
         HIPCHK(c, hipMemcpyAsync(c->d_permits.p, c->s_permits.p, (size_t)c->n_slots * 4, hipMemcpyDeviceToDevice, s));
-    HIPCHK(c, hipMemcpyAsync(c->d_ctab.p, c->s_ctab.p, c->d_ctab.n * 8, hipMemcpyDeviceToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->d_ct_keys.p, c->s_ct_keys.p, OWGS_CTC * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->d_ct_vals.p, c->s_ct_vals.p, OWGS_CTC * 4, hipMemcpyDeviceToDevice, s));
     return OWGS_OK;
 }
 

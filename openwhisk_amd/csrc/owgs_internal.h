@@ -2,80 +2,132 @@
 //
 // HBM layout of one controller shard (one owgs_ctx), all struct-of-arrays:
 //   permits[n_slots]        i32  ForcibleSemaphore state of NestedSemaphore #i (indexed by invoker id, SCPB:413)
-//   pool_words[nm + nb]     i32  managed pool positions [0,nm) then blackbox [nm,nm+nb): id if usable, -1 unusable,
-//                                 -2 usable but id outside invokerSlots (the reference throws when probing it)
+//   usable[(n_ids+31)/32]   u32  bitmap: invoker id is Healthy (InvokerState.isUsable, ISUP:54-59)   [identity pools]
+//   pool_words[nm + nb]     i32  pool position -> id if usable, -1 unusable, -2 usable but id outside invokerSlots
+//                                 (the reference throws when probing it)                           [explicit pools]
 //   hlist[hm + hb]          i32  usable ids of each pool in pool order (healthyInvokers, SCPB:418)
-//   act_info[n_actions]     i4   {home, step, mem_mb, meta}; meta = maxConcurrent | pool<<24 | throw<<25 | empty<<26
-//   act_slot[n_actions]     i32  slot-key id (fullyQualifiedName(true) interned)
-//   act_hash[n_actions]     i32  generateHash(namespace, fqn(false))
-//   ctab[cap]               u64  NestedSemaphore concurrency maps of all invokers: one open-addressing table keyed by
-//                                 (invoker id, slot key), value {permits c, operationCount} packed in one 8-byte entry
-//                                 (one load per probe).  operationCount 0 means "absent" (the reference removes the
-//                                 entry, NS:109-111).
+//   act_meta[n_actions]     u32x2 per action: {home | step << 15 | pool << 30 | cursor_ok << 31,
+//                                 mem | maxConcurrent << 17 | throw << 29 | empty << 30}   (SCPB:262-268)
+//   act_slot[n_actions]     i32  slot-key id (fullyQualifiedName(true) interned, the NestedSemaphore map key)
+//   ct_keys/ct_vals[CTC]    u32  NestedSemaphore concurrency maps of all invokers: one open-addressing table keyed by
+//                                 (invoker id, slot key) = (inv + 1) | slot << 15, value c | operationCount << 12.
+//                                 Key 0 = empty, key 0xFFFFFFFF = deleted.  Loaded into LDS by every kernel that
+//                                 touches it and written back at its end.
+//
+// Per-replay scratch (built by the pre-pass kernels from the stream, consumed by the engine):
+//   rec[n_act]              u32x4 per activation (see OWGS_REC_*): static walk/limit fields of its action plus the
+//                                 chunk-local ranks (occurrence of its action among earlier lanes of its chunk, the
+//                                 next lane of the same action, the nearest earlier lane of the same slot key with a
+//                                 different action).
+//   relx[n_act]             i32  where the activation's release goes: maxConcurrent == 1 -> the batch that releases it
+//                                 (the engine adds its memory to acc[batch][invoker] when it is decided);
+//                                 maxConcurrent > 1 -> its slot in the compacted concurrent-release list; -1 never
+//   acc[n_batches][stride]  i32  memory (MB) that batch b releases per invoker (maxConcurrent == 1 activations)
+//   rel_rec[n_crel]         u32x2 written by the engine when a concurrent activation is decided: {inv | mem << 15,
+//                                 slot | maxConcurrent << 17}; inv 0x7FFF = no ActivationEntry (CLB:278-279)
 #pragma once
 #include <stdint.h>
 
-#define OWGS_META_MAXC_MASK 0x00FFFFFF
-#define OWGS_META_POOL_SHIFT 24
-#define OWGS_META_THROW (1u << 25)
-#define OWGS_META_EMPTY (1u << 26)
-#define OWGS_META_CURSOR (1u << 27)  // walk cursor valid: maxConcurrent == 1 or the fqn is invoked on one walk only
+// --------------------------------------------------------------------------------------------- engine geometry
+#ifndef OWGS_EW
+#define OWGS_EW 4                      // engine waves per workgroup (one per SIMD)
+#endif
+#define OWGS_WL (OWGS_EW * 64)         // chunk width: activations resolved together (one per engine lane)
+#define OWGS_NT (OWGS_WL + 64)         // threads: engine waves + one I/O wave
+#define OWGS_NBK 4096                  // "first lane of its invoker" buckets (hashed; collisions are conservative)
+#define OWGS_CTC 4096                  // concurrency-table capacity (entries, power of two)
+#define OWGS_LDS_BYTES (160 * 1024)
 
-// concurrency-map entry (8 bytes): key32 << 32 | val32, key32 = (invoker+1) | slot << 15, val32 = c | ops << 12
+// --------------------------------------------------------------------------------------------- action meta
+#define OWGS_AM_POS_MASK 0x7FFFu       // home / step (pool positions < 32768)
+#define OWGS_AM_POOL (1u << 30)
+#define OWGS_AM_COK (1u << 31)         // walk cursor exact: maxConcurrent == 1 or the slot key has one walk
+#define OWGS_AM_MEM_MASK 0x1FFFFu      // memory limit MB < 131072
+#define OWGS_AM_MAXC_SHIFT 17
+#define OWGS_AM_MAXC_MASK 0xFFFu       // maxConcurrent <= 4095
+#define OWGS_AM_THROW (1u << 29)       // home/step index negative (Int.MinValue hash): schedule() throws
+#define OWGS_AM_EMPTY (1u << 30)       // pool empty: None
+#define OWGS_AM_VALID (1u << 31)       // (rec only) lane holds an activation
+
+// rec.z = action (17 bits, 0x1FFFF none) | occ << 17 (10 bits) | pk1 low 5 bits << 27
+// rec.w = slot (17 bits) | next << 17 (10 bits, 0x3FF none) | pk1 high 5 bits << 27
+// (the 10-bit "ext" field split over z/w holds pk1 for maxConcurrent > 1 lanes and the hot-action slot otherwise)
+// (chunk-lane fields are 10 bits: OWGS_WL <= 512)
+#define OWGS_REC_NOACT 0x1FFFFu
+#define OWGS_RMASK 0x3FFu
+#define OWGS_REC_NONEXT OWGS_RMASK
+#define OWGS_REC_NOHOT 0x3FF           // ext field of a maxConcurrent==1 lane: hot-action slot or none
+
+// --------------------------------------------------------------------------------------------- concurrency map
 #define OWGS_CT_SLOT_SHIFT 15
 #define OWGS_CT_C_BITS 12
 #define OWGS_CT_C_MASK 0xFFFu
-#define OWGS_MAX_SLOTS_CT 32767      // invoker ids representable in key32
-#define OWGS_MAX_SLOTKEYS 131071     // fqn@version keys representable in key32
-#define OWGS_MAX_CONC 4095           // maxConcurrent representable in val32 (c < maxConcurrent)
+#define OWGS_CT_TOMB 0xFFFFFFFFu
+#define OWGS_MAX_SLOTS_CT 32767        // invoker ids representable in the key
+#define OWGS_MAX_SLOTKEYS 131070       // fqn@version keys representable in the key (131071 would alias the tombstone)
+#define OWGS_MAX_CONC 4095             // maxConcurrent representable (c < maxConcurrent)
 #define OWGS_MAX_OPS 1048575
+#define OWGS_MAX_MEM_MB 131071
 
 #define OWGS_NONE_V (-1)
 #define OWGS_THROW_V (-2)
 #define OWGS_REL_NOSUCH_BIT 1
 #define OWGS_REL_OVERFLOW_BIT 2
 #define OWGS_REL_NOENTRY_BIT 4
+#define OWGS_RR_NOINV 0x7FFFu
 
 #define OWGS_PW_UNUSABLE (-1)
 #define OWGS_PW_BADID (-2)
 
-#define OWGS_STAMP_BUCKETS 1024
-#define OWGS_LDS_BYTES (160 * 1024)
-#define OWGS_ENGINE_WAVES 1
+// device error word bits
+#define OWGS_ERR_CTAB_FULL 1
+#define OWGS_ERR_BAD_STREAM 2          // replay: a release without a matching acquire, or a permit overflow
+#define OWGS_ERR_OPS 4
+#define OWGS_ERR_INTERNAL 8             // engine invariant violated (a pass without progress)
+
+// stats slots
+#define OWGS_ST_PASSES 0
+#define OWGS_ST_PROBES 1
+#define OWGS_ST_FALLBACKS 2
+#define OWGS_ST_LONG 3
+#define OWGS_ST_CHUNKS 4
+#define OWGS_ST_STOPS 5
 
 struct OwgsEngineArgs {
     int32_t* permits;
     int32_t n_slots;
-    const int32_t* pool_words;
+    int32_t pool_mode;           // 0: identity pools (usable bitmap), 1: explicit pool words
+    const uint32_t* usable;      // identity: bitmap over ids [0, n_ids)
+    int32_t n_ids;               // identity: blackbox pool position p -> id n_ids - nb + p
+    const int32_t* pool_words;   // explicit: [nm + nb]
     int32_t nm, nb;
     const int32_t* hlist;
     int32_t hm, hb;
-    int32_t shortcut_ok; // bit0 managed, bit1 blackbox: pool has no usable out-of-range id
-    const int4* act_info;
-    const int32_t* act_slot;
-    unsigned long long* ctab;
-    uint32_t ctab_mask;
-    int32_t n_cursors;  // actions with an LDS walk cursor (0 = cursors off)
+    int32_t shortcut_ok;         // bit0 managed, bit1 blackbox: pool has no usable out-of-range id
+    uint32_t* ct_keys;           // [OWGS_CTC] HBM image of the concurrency table
+    uint32_t* ct_vals;
+    uint32_t* ct_tmp;            // [2 * OWGS_CTC] scratch for the table rebuild
+    int32_t n_actions;           // per-action LDS words (walk cursor + chunk rank base)
     // stream
     int32_t n_batches;
-    const int64_t* acq_off;
-    const int32_t* act;
-    const int64_t* rel_off;
-    const int64_t* rel_aid;
-    const int32_t* rel_inv; // explicit-release mode (owgs_release_batch): invoker per release, action in rel_act
-    const int32_t* rel_act;
+    const int64_t* acq_off;      // [n_batches + 1]
+    int64_t n_act;               // acq_off[n_batches]
+    const int64_t* rel_off;      // [n_batches + 1] or null (no releases)
+    const uint4* rec;            // [n_act] pre-pass records
+    const int32_t* relpos;       // [n_act] relx (see above), or null: no releases
+    uint2* rel_rec;              // [n_crel] concurrent release records (compacted)
+    const int32_t* crel_off;     // [n_batches + 1] first concurrent release of each batch
+    int32_t* acc;                // [n_batches][acc_stride] maxConcurrent==1 memory released at each batch, per invoker
+    int64_t acc_stride;
     unsigned long long seq_base;
     const unsigned long long* seq; // optional explicit seq per activation
-    // dense per-activation / per-release records built by owgs_gather_kernel (or by the host for explicit walks)
-    const int4* info;   // [n_act] {home, step, mem, meta}
-    const int2* aux;    // [n_act] {slot key, action handle or -1}
-    const int4* rinfo;  // [n_rel] {aid (or invoker if rel_inv), mem, meta, slot key}
     int32_t* out_inv;
     uint8_t* out_flags;
     uint8_t* rel_flags;
     unsigned long long rng_seed;
-    unsigned long long* stats; // [0] iterations [1] probes [2] fallbacks [3] long walks [4] groups
-    int32_t* err;              // device error word (table full, ...)
+    unsigned long long* stats;
+    int32_t* err;
+    int32_t opts;                // diagnostics (env OWGS_OPTS): bit0 = no hot-action rank tables
 };
 
 // generateHash(namespace, action) for n actions: out[i] = abs(h(ns_i) ^ h(path_i)), Int.MinValue kept (SCPB:370-372).
@@ -90,29 +142,6 @@ struct OwgsHashArgs {
     int32_t* out;
 };
 
-struct OwgsGatherArgs {
-    const int32_t* act;
-    int64_t n_act;
-    const int4* act_info;
-    const int32_t* act_slot;
-    int4* info;
-    int2* aux;
-    const int64_t* rel_aid;
-    const int32_t* rel_inv;
-    const int32_t* rel_act;
-    int64_t n_rel;
-    int4* rinfo;
-};
-
-struct OwgsLookupArgs {
-    const unsigned long long* ctab;
-    uint32_t ctab_mask;
-    const int32_t* inv;
-    const int32_t* slot;
-    int32_t n;
-    int2* out;
-};
-
 struct OwgsPrepArgs {
     const int32_t* hash;
     const int32_t* mem;
@@ -125,5 +154,50 @@ struct OwgsPrepArgs {
     int32_t n_msteps;
     const int32_t* bsteps;
     int32_t n_bsteps;
-    int4* act_info;
+    uint2* act_meta;
+};
+
+// chunk-local pre-pass: one workgroup of OWGS_WL threads per chunk
+struct OwgsPrepassArgs {
+    int32_t n_batches;
+    const int64_t* acq_off;
+    const int32_t* cstart;       // [n_batches + 1] first chunk of each batch (built by owgs_chunks_kernel)
+    const int32_t* act;          // [n_act] action per activation, or null: per-activation meta in xmeta/xslot
+    const uint2* act_meta;       // [n_actions]
+    const int32_t* act_slot;     // [n_actions]
+    const uint2* xmeta;          // explicit walks: [n_act]
+    const int32_t* xslot;        // explicit walks: [n_act]
+    uint4* rec;                  // out [n_act]
+};
+
+struct OwgsRelposArgs {
+    const int64_t* rel_aid;
+    int64_t n_rel;
+    int64_t n_act;
+    int32_t* relpos;
+    int32_t* err;
+};
+
+// ordered explicit releases (owgs_release_batch): one wave, releases in stream order
+struct OwgsReleaseArgs {
+    int32_t* permits;
+    int32_t n_slots;
+    uint32_t* ct_keys;
+    uint32_t* ct_vals;
+    int32_t n;
+    const int32_t* inv;
+    const int32_t* mem;
+    const int32_t* maxc;
+    const int32_t* slot;
+    uint8_t* flags;
+    int32_t* err;
+};
+
+struct OwgsLookupArgs {
+    const uint32_t* ct_keys;
+    const uint32_t* ct_vals;
+    const int32_t* inv;
+    const int32_t* slot;
+    int32_t n;
+    int2* out;
 };

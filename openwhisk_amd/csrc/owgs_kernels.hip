@@ -1,30 +1,35 @@
 // owgs_kernels.hip -- CDNA4 (gfx950) kernels of the batched invoker scheduler.
 //
 // Kernels
-//   owgs_hash_kernel     generateHash(namespace, action) (SCPB:370-372): java.lang.String.hashCode of both strings,
-//                        one wave per action; lane i sums c[i+64k] * 31^(L-1-i-64k) (mod 2^32), the wave reduces.
-//   owgs_prepare_kernel  per action: home = hash % n, step = stepSizes(hash % k), meta bits (SCPB:262-268).
-//   owgs_lookup_kernel   NestedSemaphore.concurrentState reads (introspection).
-//   owgs_engine_kernel   the hot path: releases (SCPB:327-331 -> NS:98-113) and schedule() (SCPB:398-436 with
-//                        NS:32-91) for a whole stream of batches, replaying the reference's SEQUENTIAL semantics.
+//   owgs_hash_kernel      generateHash(namespace, action) (SCPB:370-372): java.lang.String.hashCode of both strings,
+//                         one wave per action; lane i sums c[i+64k] * 31^(L-1-i-64k) (mod 2^32), the wave reduces.
+//   owgs_prepare_kernel   per action: home = hash % n, step = stepSizes(hash % k), limits -> act_meta (SCPB:262-268).
+//   owgs_chunks_kernel    first chunk of every batch (chunks = OWGS_WL consecutive publishes of one batch).
+//   owgs_prepass_kernel   one workgroup per chunk: per-activation engine record = action meta + chunk-local ranks.
+//   owgs_relscan*_kernel  release bookkeeping: maxConcurrent==1 releases are aggregated per (release batch, invoker);
+//                         concurrent releases get a compacted slot in rel_rec.
+//   owgs_engine_kernel    the hot path: releases (SCPB:327-331 -> NS:98-113) and schedule() (SCPB:398-436 with
+//                         NS:32-91) for a whole stream of batches, replaying the reference's SEQUENTIAL semantics.
+//   owgs_relflags_kernel  per-release flags after the replay (no ActivationEntry, CLB:278-279).
+//   owgs_release_seq_kernel  explicit releases in stream order (owgs_release_batch).
 //
-// Engine design (DESIGN.md "Engine").  One wavefront owns one controller shard.  Slot permits, pool vectors and a
-// per-action walk cursor live in LDS for the whole stream (HBM is read once and written once); the concurrency maps
-// live in one 8-byte-entry open-addressing table (L2-resident).  Activations are taken 64 at a time (one per lane, in
-// stream order) and resolved by speculation + exact validation:
-//   * memory permits never increase inside a batch (releases are applied at batch boundaries), so a probe that
-//     fails against the state at the chunk frontier f fails at every later time: a lane's speculated target is never
-//     EARLIER in its walk than its true target, and the per-action cursor (first walk step that may still be feasible)
-//     only moves forward inside a batch;
-//   * lanes are grouped by target invoker (LDS stamp table + ballot); inside a group an exclusive prefix sum of the
-//     memory consumed by earlier lanes gives each lane the permits left at its own time, and concurrency slots are
-//     modelled per (target, action) from the rank inside the group;
-//   * the first lane l* whose speculation does not hold is a TRUE rejection (every earlier lane was exact), lanes
-//     [f, l*) commit, l* (and the later lanes of the same maxConcurrent==1 action at the same target) step past the
-//     target, and the chunk iterates with f = l*.  The frontier lane is always exact, so every iteration commits.
-//   * cases whose speculation cannot be validated cheaply (an earlier lane of the chunk that may create concurrency
-//     slots for the same fqn on another walk, or a forced acquire) are treated as uncertain and resolved when they
-//     reach the frontier.
+// Engine.  One workgroup owns one controller shard: OWGS_EW engine waves + one I/O wave.  Slot
+// permits, pool usability, the concurrency maps and one word per action (walk cursor + chunk rank base) live in LDS
+// for the whole stream.  Activations are resolved OWGS_WL at a time (one per engine lane, in stream order) by
+// speculation + conservative validation + prefix commit:
+//   * memory permits never increase inside a batch (releases are applied at batch boundaries), so a walk step that is
+//     infeasible at the chunk frontier f stays infeasible: the per-action cursor (first step that may still be
+//     feasible) only moves forward inside a batch;
+//   * PACKING: lane i of action a with rank r (earlier uncommitted lanes of a in the chunk) speculates the step at
+//     which the capacity along a's walk (floor(permits / mem) invocations per invoker, + the concurrency slots for
+//     maxConcurrent > 1) first exceeds r, i.e. where it lands if the r earlier lanes of a land where they speculate;
+//   * every lane adds its memory consumption to a (hashed) bucket of its target invoker; a lane is KNOWN to fit when
+//     it is the first lane of its bucket or the bucket total fits the invoker's permits (a sound upper bound of the
+//     consumption by earlier lanes), or it is a forced acquire;
+//   * lanes [f, l) commit, l = first lane not known to fit; the frontier lane f is always exact, so each pass
+//     commits at least one lane; the next pass re-speculates [l, chunk end) against the updated state.
+// The I/O wave streams the next chunk's records from HBM into an LDS double buffer; the engine waves only store to
+// HBM (decisions, release records), so no engine-wave load ever waits behind its own stores.
 #include <hip/hip_runtime.h>
 
 #include "owgs_internal.h"
@@ -36,24 +41,43 @@ typedef unsigned long long u64;
 #define K_TARGET 2
 #define K_FALLBACK 3
 #define K_LONG 4
+#define K_HOT 5  // resolved from the hot-action rank table after the pass barrier
 
-#define KPROBE 4
+#define KPROBE 16  // walk steps a lane probes on its own before the wave-cooperative walk (multiple of 4)
+#define CAPMAX 1024  // capacities are clamped: a lane's rank is < OWGS_WL
 
 // diagnostic build (-DOWGS_PROFILE, libowgs_prof.so): s_memtime cycle accounting per engine phase into stats[8..15]
 #ifdef OWGS_PROFILE
 #define PT_DECL                 \
-    u64 pt_acc[8] = {0};        \
+    u64 pt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
     u64 pt_t = __builtin_amdgcn_s_memtime();
-#define PT(k)                                          \
-    {                                                  \
-        const u64 _t = __builtin_amdgcn_s_memtime();   \
-        pt_acc[k] += _t - pt_t;                        \
-        pt_t = _t;                                     \
+#define PT(k)                                        \
+    {                                                \
+        const u64 _t = __builtin_amdgcn_s_memtime(); \
+        pt_acc[k] += _t - pt_t;                      \
+        pt_t = _t;                                   \
     }
 #else
 #define PT_DECL
 #define PT(k)
 #endif
+
+// LDS scalars
+#define SC_LMIN 0   // [2] first lane not known to fit (pass parity)
+#define SC_CFB 2    // [2] first concurrent forced lane (pass parity)
+#define SC_U0 4     // upper bound of usable permits, managed pool
+#define SC_U1 5     // blackbox pool
+#define SC_USED 6   // non-empty concurrency-table entries (live + deleted)
+#define SC_NLIVE 7  // table rebuild: live entries
+#define SC_NHOT 8   // multi-lane actions of the current chunk (hot slots claimed)
+#define SC_N 16
+
+// hot actions: every maxConcurrent==1 action with >= HOT_MIN lanes in a chunk gets a slot (assigned by the pre-pass);
+// per pass one wave walks its capacity prefix once and writes the target of each rank 0..HOT_RANKS-1 into the slot's
+// table, so the action's lanes do not walk one by one
+#define NHOT 16
+#define HOT_RANKS 64
+#define HOT_MIN 6
 
 // ------------------------------------------------------------------------------------------------ helpers
 __device__ __forceinline__ u64 splitmix64(u64 x) {
@@ -69,27 +93,9 @@ __device__ __forceinline__ uint32_t rng_index(u64 seed, u64 seq, uint32_t n) {
     return (uint32_t)((u * (u64)n) >> 32);
 }
 
-// (index + step) % numInvokers (SCPB:429) for index, step in [0, n]: one conditional subtract, no division
-__device__ __forceinline__ int next_pos(int pos, int step, int n) {
-    const int p = pos + step;
-    return p >= n ? p - n : p;
-}
-
-// x mod R for 0 <= x < 2^24, 1 <= R < 2^24 without an integer division (float reciprocal, one correction step)
-__device__ __forceinline__ int mod_small(int x, int R) {
-    const int q = (int)((float)x * __builtin_amdgcn_rcpf((float)R));
-    int r = x - q * R;
-    if (r < 0) r += R;
-    if (r >= R) r -= R;
-    return r;
-}
-
 __device__ __forceinline__ int ffs64(u64 m) { return __ffsll((long long)m) - 1; }
-__device__ __forceinline__ int fls64(u64 m) { return 63 - __clzll((long long)m); }
 
-__device__ __forceinline__ void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
-
-// DPP (GFX9 row_shr / row_bcast) wave64 scans: no LDS round trip, ~6 VALU ops.
+// DPP (GFX9 row_shr / row_bcast) wave64 scans: no LDS round trip
 template <int CTRL, int ROWM>
 __device__ __forceinline__ int dpp_add_src(int v) {
     return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWM, 0xf, true);  // out-of-row / masked lanes read 0
@@ -103,11 +109,19 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
     v += dpp_add_src<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
     return v;
 }
-__device__ __forceinline__ int wave_excl_scan(int v) { return wave_incl_scan(v) - v; }
-
 template <int CTRL, int ROWM>
 __device__ __forceinline__ int dpp_keep(int old, int v) {
     return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWM, 0xf, false);  // invalid source lanes keep `old`
+}
+__device__ __forceinline__ int wave_incl_max(int v) {
+    const int I = (int)0x80000000;
+    v = max(v, dpp_keep<0x111, 0xf>(I, v));
+    v = max(v, dpp_keep<0x112, 0xf>(I, v));
+    v = max(v, dpp_keep<0x114, 0xf>(I, v));
+    v = max(v, dpp_keep<0x118, 0xf>(I, v));
+    v = max(v, dpp_keep<0x142, 0xa>(I, v));
+    v = max(v, dpp_keep<0x143, 0xc>(I, v));
+    return v;
 }
 __device__ __forceinline__ int wave_max(int v) {
     const int I = (int)0x80000000;
@@ -119,21 +133,7 @@ __device__ __forceinline__ int wave_max(int v) {
     v = max(v, dpp_keep<0x143, 0xc>(I, v));
     return __builtin_amdgcn_readlane(v, 63);
 }
-__device__ __forceinline__ int wave_min(int v) {
-    const int I = 0x7FFFFFFF;
-    v = min(v, dpp_keep<0x111, 0xf>(I, v));
-    v = min(v, dpp_keep<0x112, 0xf>(I, v));
-    v = min(v, dpp_keep<0x114, 0xf>(I, v));
-    v = min(v, dpp_keep<0x118, 0xf>(I, v));
-    v = min(v, dpp_keep<0x142, 0xa>(I, v));
-    v = min(v, dpp_keep<0x143, 0xc>(I, v));
-    return __builtin_amdgcn_readlane(v, 63);
-}
 
-// ---- concurrency table: entry = key32 << 32 | val32; key32 = (inv+1) | slot << 15; val32 = c | ops << 12
-__device__ __forceinline__ uint32_t ct_key(int inv, int slot) {
-    return (uint32_t)(inv + 1) | ((uint32_t)slot << OWGS_CT_SLOT_SHIFT);
-}
 __device__ __forceinline__ uint32_t ct_hash(uint32_t k) {
     k ^= k >> 16;
     k *= 0x7feb352dU;
@@ -142,44 +142,135 @@ __device__ __forceinline__ uint32_t ct_hash(uint32_t k) {
     k ^= k >> 16;
     return k;
 }
-__device__ __forceinline__ int ct_c(u64 e) { return (int)((uint32_t)e & OWGS_CT_C_MASK); }
-__device__ __forceinline__ int ct_ops(u64 e) { return (int)((uint32_t)e >> OWGS_CT_C_BITS); }
-__device__ __forceinline__ u64 ct_entry(uint32_t key, int c, int ops) {
-    return ((u64)key << 32) | (u64)((uint32_t)c | ((uint32_t)ops << OWGS_CT_C_BITS));
+__device__ __forceinline__ uint32_t ct_key(int inv, int slot) {
+    return (uint32_t)(inv + 1) | ((uint32_t)slot << OWGS_CT_SLOT_SHIFT);
 }
-
-// returns table index or -1; *e = entry (0 if absent)
-__device__ int ct_find(const u64* tab, uint32_t mask, uint32_t key, u64* e) {
-    uint32_t h = ct_hash(key) & mask;
-    for (uint32_t p = 0; p <= mask; ++p) {
-        const u64 v = tab[h];
-        if ((uint32_t)(v >> 32) == key) {
-            *e = v;
-            return (int)h;
+// concurrency table (LDS or HBM image): index of key or -1; deleted entries are skipped, empty ends the chain
+__device__ __forceinline__ int ct_find(const uint32_t* ctk, uint32_t key) {
+    uint32_t h = ct_hash(key) & (OWGS_CTC - 1);
+    for (int p = 0; p < OWGS_CTC; ++p) {
+        const uint32_t k = ctk[h];
+        if (k == key) return (int)h;
+        if (k == 0) return -1;
+        h = (h + 1) & (OWGS_CTC - 1);
+    }
+    return -1;
+}
+// insert a key known to be absent: claim the first empty or deleted entry of its chain (concurrent inserters of
+// different keys race by CAS)
+__device__ __forceinline__ int ct_insert(uint32_t* ctk, uint32_t key, int* fresh) {
+    uint32_t h = ct_hash(key) & (OWGS_CTC - 1);
+    for (int p = 0; p < OWGS_CTC;) {
+        const uint32_t k = ctk[h];
+        if (k == 0 || k == OWGS_CT_TOMB) {
+            if (atomicCAS(&ctk[h], k, key) == k) {
+                *fresh = k == 0;
+                return (int)h;
+            }
+            continue;  // lost the race: re-read this entry
         }
-        if (v == 0) break;
-        h = (h + 1) & mask;
-    }
-    *e = 0;
-    return -1;
-}
-
-__device__ int ct_insert(u64* tab, uint32_t mask, uint32_t key) {
-    uint32_t h = ct_hash(key) & mask;
-    for (uint32_t p = 0; p <= mask; ++p) {
-        const u64 v = tab[h];
-        if (v == 0 || (uint32_t)(v >> 32) == key) return (int)h;
-        h = (h + 1) & mask;
+        h = (h + 1) & (OWGS_CTC - 1);
+        ++p;
     }
     return -1;
 }
 
-// c of NestedSemaphore(inv).actionConcurrentSlotsMap(slot); absent entries (operationCount 0) read as c = 0
-__device__ __forceinline__ int conc_lookup(const OwgsEngineArgs& A, int inv, int slot, int* idx, int* ops) {
-    u64 e;
-    *idx = ct_find(A.ctab, A.ctab_mask, ct_key(inv, slot), &e);
-    *ops = ct_ops(e);
-    return *ops > 0 ? ct_c(e) : 0;
+// min(floor(pv / m), CAPMAX) for pv >= 0, 0 when pv < m; float reciprocal + one correction (pv / m < 2^10)
+__device__ __forceinline__ int cap_of(int pv, int m, float rm) {
+    if (pv < m) return 0;
+    if (pv >= m * CAPMAX) return CAPMAX;
+    int q = (int)((float)pv * rm);
+    const int r = pv - q * m;
+    if (r < 0) --q;
+    else if (r >= m) ++q;
+    return q;
+}
+
+// x mod n for 0 <= x < 2^31, 1 <= n < 2^15 without an integer division: float reciprocal, then exact correction
+__device__ __forceinline__ int mod_fast(int x, int n, float rn) {
+    const int q = (int)((float)x * rn);  // |q - x / n| <= 2 for x < 2^31, n < 2^15
+    int r = x - q * n;
+    r += r < 0 ? n : 0;
+    r += r < 0 ? n : 0;
+    r -= r >= n ? n : 0;
+    r -= r >= n ? n : 0;
+    return r;
+}
+
+// branch-free cap_of (float reciprocal + one correction); pv may be negative (forced acquires)
+__device__ __forceinline__ int cap_bf(int pv, int m, float rm) {
+    int q = (int)((float)max(pv, 0) * rm);
+    const int r = pv - q * m;
+    q += r >= m ? 1 : 0;
+    q -= r < 0 ? 1 : 0;
+    q = min(q, CAPMAX);
+    return pv >= m ? q : 0;
+}
+
+// LDS-DMA (global_load_lds): each lane's 16 (4) bytes land at lds_dst + 16 (4) * lane.  M0 is compiler-reserved:
+// saved and restored inside the statement (cdna_hip_programming.md section 5.7).  The issuing wave must wait
+// vmcnt before a barrier that publishes the bytes.
+__device__ __forceinline__ void lds_dma16(const void* gsrc, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+__device__ __forceinline__ void lds_dma4(const void* gsrc, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+
+// ------------------------------------------------------------------------------------------------ LDS layout
+struct OwgsLayout {
+    uint32_t P, pool, pc, cur, ctk, ctv, stgA, stgX, fst, spt, hdir, htab, hscr, rc, sc, uni, uni_bytes, total;
+};
+
+__host__ __device__ inline OwgsLayout owgs_layout(int n_slots, int pool_mode, int n_ids, int nm, int nb, int n_actions) {
+    OwgsLayout L;
+    uint32_t o = 0;
+#define OWGS_AL(x) (((uint32_t)(x) + 15u) & ~15u)
+    const uint32_t words = (uint32_t)(n_ids + 31) / 32;
+    L.P = o;
+    o += OWGS_AL(4u * (uint32_t)n_slots);
+    L.pool = o;
+    o += pool_mode ? OWGS_AL(2u * (uint32_t)(nm + nb)) : OWGS_AL(4u * words);
+    L.pc = o;  // identity pools: usable ids before each bitmap word (rank/select for the fallback)
+    o += pool_mode ? 0u : OWGS_AL(4u * (words + 1));
+    L.cur = o;
+    o += OWGS_AL(4u * (uint32_t)n_actions);
+    L.ctk = o;
+    o += 4u * OWGS_CTC;
+    L.ctv = o;
+    o += 4u * OWGS_CTC;
+    L.stgA = o;
+    o += 2u * OWGS_WL * 16u;
+    L.stgX = o;
+    o += 2u * OWGS_WL * 4u;
+    L.sc = o;
+    o += 4u * SC_N;
+    // phase union: acquire phase {fst, spt, hot directory, hot rank tables, hot scratch} / release phase {rc}
+    L.uni = o;
+    L.fst = o;
+    L.spt = o + 4u * OWGS_NBK;
+    L.hdir = L.spt + 4u * OWGS_WL;                  // NHOT x {action, meta.x, meta.y, slot}, then NHOT x max occ
+    L.htab = L.hdir + 20u * NHOT;                   // NHOT x HOT_RANKS x {id | kind << 15 | ks << 18, step}
+    L.hscr = L.htab + 8u * NHOT * HOT_RANKS;        // OWGS_EW x 64 rank marks
+    L.rc = o;
+    const uint32_t ua = (L.hscr - o) + 4u * 64 * OWGS_EW, ur = 4u * OWGS_CTC;
+    L.uni_bytes = ua > ur ? ua : ur;
+    o += L.uni_bytes;
+    L.total = o;
+#undef OWGS_AL
+    return L;
+}
+
+extern "C" size_t owgs_engine_lds_bytes(int n_slots, int pool_mode, int n_ids, int nm, int nb, int n_actions) {
+    return owgs_layout(n_slots, pool_mode, n_ids, nm, nb, n_actions).total;
 }
 
 // ------------------------------------------------------------------------------------------------ hashing
@@ -221,35 +312,12 @@ __global__ __launch_bounds__(256) void owgs_hash_kernel(OwgsHashArgs a) {
 __global__ __launch_bounds__(256) void owgs_lookup_kernel(OwgsLookupArgs a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
-    u64 e;
-    ct_find(a.ctab, a.ctab_mask, ct_key(a.inv[i], a.slot[i]), &e);
-    a.out[i] = make_int2(ct_c(e), ct_ops(e));
+    const int ix = ct_find(a.ct_keys, ct_key(a.inv[i], a.slot[i]));
+    const uint32_t v = ix >= 0 ? a.ct_vals[ix] : 0u;
+    a.out[i] = make_int2((int)(v & OWGS_CT_C_MASK), (int)(v >> OWGS_CT_C_BITS));
 }
 
-// dense per-activation / per-release records (one coalesced load each in the engine instead of dependent gathers)
-__global__ __launch_bounds__(256) void owgs_gather_kernel(OwgsGatherArgs g) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < g.n_act; i += stride) {
-        const int a = g.act[i];
-        g.info[i] = g.act_info[a];
-        g.aux[i] = make_int2(g.act_slot[a], a);
-    }
-    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < g.n_rel; r += stride) {
-        int x, a;
-        if (g.rel_inv) {
-            x = g.rel_inv[r];
-            a = g.rel_act[r];
-        } else {
-            const int64_t aid = g.rel_aid[r];
-            x = (int)aid;
-            a = g.act[aid];
-        }
-        const int4 ai = g.act_info[a];
-        g.rinfo[r] = make_int4(x, ai.z, ai.w, g.act_slot[a]);
-    }
-}
-
-// home/step selection (SCPB:266-268)
+// home/step selection (SCPB:266-268) -> packed action meta
 __global__ __launch_bounds__(256) void owgs_prepare_kernel(OwgsPrepArgs a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
@@ -257,630 +325,1191 @@ __global__ __launch_bounds__(256) void owgs_prepare_kernel(OwgsPrepArgs a) {
     const int n = pool ? a.nb : a.nm;
     const int k = pool ? a.n_bsteps : a.n_msteps;
     const int32_t* steps = pool ? a.bsteps : a.msteps;
-    uint32_t meta = (uint32_t)(a.maxc[i] & OWGS_META_MAXC_MASK) | ((uint32_t)pool << OWGS_META_POOL_SHIFT);
-    if (a.cursor_ok[i]) meta |= OWGS_META_CURSOR;
+    uint32_t y = (uint32_t)a.mem[i] | ((uint32_t)a.maxc[i] << OWGS_AM_MAXC_SHIFT);
     int home = 0, step = 0;
     if (n <= 0) {
-        meta |= OWGS_META_EMPTY;
+        y |= OWGS_AM_EMPTY;
     } else if (k <= 0) {
-        meta |= OWGS_META_THROW;
+        y |= OWGS_AM_THROW;
     } else {
         const int h = a.hash[i];
         home = h % n;
         const int si = h % k;
-        if (si < 0 || home < 0) meta |= OWGS_META_THROW;
-        else step = steps[si] % n;  // same walk; lets the engine advance with one conditional subtract
+        if (si < 0 || home < 0) y |= OWGS_AM_THROW;  // Vector.apply(negative) throws (SCPB:268 / 411)
+        else step = steps[si] % n;                    // same walk; lets the engine advance with one conditional subtract
     }
-    a.act_info[i] = make_int4(home, step, a.mem[i], (int)meta);
+    uint32_t x = (uint32_t)home | ((uint32_t)step << 15) | (pool ? OWGS_AM_POOL : 0u);
+    if (a.cursor_ok[i]) x |= OWGS_AM_COK;
+    a.act_meta[i] = make_uint2(x, y);
 }
 
-// ------------------------------------------------------------------------------------------------ engine
-// concurrency slots an acquisition finds, given c0 at state f and q earlier same-fqn lanes at the same invoker
-__device__ __forceinline__ int c_now_of(int c0, int q, int R) {
-    const int x = q - c0;
-    if (x < 0) return c0 - q;
-    const int r = mod_small(x, R);
-    return r == 0 ? 0 : R - r;
-}
-
-__device__ __forceinline__ uint32_t next_stamp(uint32_t& iter, uint32_t* st, int lane) {
-    ++iter;
-    if ((iter & 0x03FFFFFFu) == 0) {  // stamps are (2^26 - iter) << 6 | lane: re-arm the tables on wrap
-        for (int t = lane; t < 2 * OWGS_STAMP_BUCKETS; t += 64) st[t] = 0xFFFFFFFFu;
-        wave_fence();
-        ++iter;
+// ------------------------------------------------------------------------------------------------ pre-pass
+// first chunk of each batch: cstart[b] = sum over b' < b of ceil(n_b' / OWGS_WL)
+__global__ __launch_bounds__(64) void owgs_chunks_kernel(const int64_t* acq_off, int32_t n_batches, int32_t* cstart) {
+    if (threadIdx.x != 0) return;
+    int32_t c = 0;
+    for (int b = 0; b < n_batches; ++b) {
+        cstart[b] = c;
+        const int64_t n = acq_off[b + 1] - acq_off[b];
+        c += (int32_t)((n + OWGS_WL - 1) / OWGS_WL);
     }
-    return ((0x03FFFFFFu - (iter & 0x03FFFFFFu)) << 6) | (uint32_t)lane;
+    cstart[n_batches] = c;
 }
 
-struct CoopResult {
-    int kind, tgt, pv, s, pos, c, cidx, ops;
-};
-
-// Wave-cooperative walk for lane `who` (all lanes call it): walk steps s0.. are probed 64 at a time and ballot picks
-// the first feasible one.  kind = K_TARGET / K_THROW, or K_LONG when every remaining step fails (s = n).
-__device__ CoopResult coop_walk(const OwgsEngineArgs& A, const int32_t* perm, const int32_t* pw, int who, int s_l,
-                                int pos_l, int step_l, int n_l, int pwb_l, int mem_l, int maxc_l, int slot_l) {
-    const int lane = threadIdx.x;
-    int s0 = __builtin_amdgcn_readlane(s_l, who);
-    int p0 = __builtin_amdgcn_readlane(pos_l, who);
-    const int stp = __builtin_amdgcn_readlane(step_l, who);
-    const int nn = __builtin_amdgcn_readlane(n_l, who);
-    const int pb = __builtin_amdgcn_readlane(pwb_l, who);
-    const int m = __builtin_amdgcn_readlane(mem_l, who);
-    const int mc = __builtin_amdgcn_readlane(maxc_l, who);
-    const int sl = __builtin_amdgcn_readlane(slot_l, who);
-    CoopResult r{K_LONG, -1, 0, nn, p0, 0, -1, 0};
-    const int loff = (int)(((uint32_t)lane * (uint32_t)stp) % (uint32_t)nn);
-    const int boff = (int)((64u * (uint32_t)stp) % (uint32_t)nn);
-    while (s0 < nn) {
-        const int sk = s0 + lane;
-        const int p = next_pos(p0, loff, nn);
-        bool feas = false;
-        int w = -1, c = 0, ix = -1, o = 0, pvv = 0;
-        if (sk < nn) {
-            w = pw[pb + p];
-            if (w == OWGS_PW_BADID) {
-                feas = true;
-            } else if (w >= 0) {
-                pvv = perm[w];
-                feas = pvv >= m;
-                if (mc > 1) {
-                    c = conc_lookup(A, w, sl, &ix, &o);
-                    feas = feas || c >= 1;
-                }
+// one workgroup per chunk: occ (earlier lanes of the same action), next lane of the same action, nearest earlier
+// lane with the same slot key and a different action (shared fqn@version), packed with the action meta
+__global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A) {
+    __shared__ int32_t s_a[OWGS_WL], s_s[OWGS_WL];
+    const int g = blockIdx.x;
+    if (g >= A.cstart[A.n_batches]) return;
+    int lo = 0, hi = A.n_batches - 1;  // last batch with cstart[b] <= g
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (A.cstart[mid] <= g) lo = mid;
+        else hi = mid - 1;
+    }
+    const int b = lo;
+    const int64_t c0 = A.acq_off[b] + (int64_t)(g - A.cstart[b]) * OWGS_WL;
+    const int len = (int)min((int64_t)OWGS_WL, A.acq_off[b + 1] - c0);
+    const int t = threadIdx.x;
+    uint2 meta = make_uint2(0, 0);
+    int a = -1, slot = 0;
+    if (t < len) {
+        if (A.act) {
+            a = A.act[c0 + t];
+            meta = A.act_meta[a];
+            slot = A.act_slot[a];
+        } else {
+            meta = A.xmeta[c0 + t];
+            slot = A.xslot[c0 + t];
+        }
+    }
+    const int aid = (A.act && t < len) ? a : -1 - t;  // explicit walks: every lane is its own walk
+    s_a[t] = aid;
+    s_s[t] = slot;
+    __syncthreads();
+    int occ = 0, next = (int)OWGS_REC_NONEXT, pk1 = 0, cnt = 0, lead = t;
+    if (t < len) {
+        for (int j = 0; j < len; ++j) {
+            const int aj = s_a[j];
+            if (aj == aid) {
+                ++cnt;
+                if (j < lead) lead = j;
+            }
+            if (j < t) {
+                if (aj == aid) ++occ;
+                else if (s_s[j] == slot) pk1 = j + 1;
+            } else if (j > t && aj == aid && next == (int)OWGS_REC_NONEXT) {
+                next = j;
             }
         }
-        const u64 fm = __ballot(feas);
-        if (fm) {
-            const int j = ffs64(fm);
-            r.tgt = __builtin_amdgcn_readlane(w, j);
-            r.c = __builtin_amdgcn_readlane(c, j);
-            r.cidx = __builtin_amdgcn_readlane(ix, j);
-            r.ops = __builtin_amdgcn_readlane(o, j);
-            r.pv = __builtin_amdgcn_readlane(pvv, j);
-            r.pos = __builtin_amdgcn_readlane(p, j);
-            r.s = s0 + j;
-            r.kind = (r.tgt == OWGS_PW_BADID) ? K_THROW : K_TARGET;
-            return r;
-        }
-        s0 += 64;
-        p0 = next_pos(p0, boff, nn);
     }
+    // hot actions (maxConcurrent == 1, >= HOT_MIN lanes in the chunk): slots in order of their first lane
+    const bool q = t < len && A.act && cnt >= HOT_MIN && ((meta.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK) == 1 &&
+                   !(meta.y & (OWGS_AM_THROW | OWGS_AM_EMPTY));
+    __syncthreads();
+    s_s[t] = (q && occ == 0) ? 1 : 0;  // qualifying leaders
+    __syncthreads();
+    if (t >= len) return;
+    int hs = OWGS_REC_NOHOT;
+    if (q) {
+        int k = 0;
+        for (int j = 0; j < lead; ++j) k += s_s[j];
+        if (k < NHOT) hs = k;
+    }
+    const int ext = ((meta.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK) > 1 ? pk1 : hs;  // 10 bits
+    const uint32_t an = A.act ? (uint32_t)a : OWGS_REC_NOACT;
+    uint4 r;
+    r.x = meta.x;
+    r.y = meta.y | OWGS_AM_VALID;
+    r.z = an | ((uint32_t)occ << 17) | ((uint32_t)(ext & 31) << 27);
+    r.w = (uint32_t)slot | ((uint32_t)next << 17) | ((uint32_t)(ext >> 5) << 27);
+    A.rec[c0 + t] = r;
+}
+
+// Release bookkeeping.  relx[aid] = release batch (maxConcurrent == 1: aggregated into acc[batch][invoker]) or the
+// compacted position of a concurrent release in rel_rec.  Three-step exclusive scan over the concurrent flags.
+#define RS_TPB 1024
+#define RS_IPT 4
+#define RS_ELEMS (RS_TPB * RS_IPT)
+
+__device__ __forceinline__ int rel_batch(const int64_t* rel_off, int n_batches, int64_t r) {
+    int lo = 0, hi = n_batches - 1;  // last b with rel_off[b] <= r
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (rel_off[mid] <= r) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+struct OwgsRelScanArgs {
+    const int64_t* rel_aid;
+    int64_t n_rel;
+    const int32_t* act;
+    const uint2* act_meta;
+    int32_t* cpos;      // [n_rel] exclusive scan of concurrent flags (local, then global)
+    int32_t* bsum;      // [n_blocks]
+    int32_t n_blocks;
+    const int64_t* rel_off;
+    int32_t n_batches;
+    int32_t* relx;      // [n_act]
+    int32_t* crel_off;  // [n_batches + 1]
+};
+
+__device__ __forceinline__ int is_conc_rel(const OwgsRelScanArgs& A, int64_t r) {
+    const int a = A.act[A.rel_aid[r]];
+    return ((A.act_meta[a].y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK) > 1 ? 1 : 0;
+}
+
+__device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* total) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int inc = wave_incl_scan(v);
+    if (lane == 63) tmp[w] = inc;
+    __syncthreads();
+    if (t < 64) {
+        const int x = t < (int)(blockDim.x >> 6) ? tmp[t] : 0;
+        const int xi = wave_incl_scan(x);
+        tmp[64 + t] = xi - x;
+        if (t == 63) tmp[128] = xi;
+    }
+    __syncthreads();
+    const int r = tmp[64 + w] + inc - v;
+    *total = tmp[128];
+    __syncthreads();
     return r;
 }
 
-// fallback target (SCPB:417-424): H = usable pool members in pool order, r = H[rng(seq) mod |H|]
-__device__ __forceinline__ void fallback_target(const OwgsEngineArgs& A, int pool, int64_t i, int n_slots, int* kind,
-                                                int* tgt) {
-    const int hc = pool ? A.hb : A.hm;
-    if (hc <= 0) {
-        *kind = K_NONE;
-        return;
+__global__ __launch_bounds__(RS_TPB) void owgs_relscan1_kernel(OwgsRelScanArgs A) {
+    __shared__ int tmp[160];
+    const int64_t base = (int64_t)blockIdx.x * RS_ELEMS + (int64_t)threadIdx.x * RS_IPT;
+    int f[RS_IPT], s = 0;
+    for (int k = 0; k < RS_IPT; ++k) {
+        const int64_t r = base + k;
+        f[k] = r < A.n_rel ? is_conc_rel(A, r) : 0;
+        s += f[k];
     }
-    const u64 seq = A.seq ? A.seq[i] : (A.seq_base + (u64)i);
-    const int r = A.hlist[(pool ? A.hm : 0) + (int)rng_index(A.rng_seed, seq, (uint32_t)hc)];
-    if (r < 0 || r >= n_slots) {
-        *kind = K_THROW;
-        return;
+    int total;
+    int ex = block_excl_scan(s, tmp, &total);
+    for (int k = 0; k < RS_IPT; ++k) {
+        const int64_t r = base + k;
+        if (r < A.n_rel) A.cpos[r] = ex;
+        ex += f[k];
     }
-    *kind = K_FALLBACK;
-    *tgt = r;
+    if (threadIdx.x == 0) A.bsum[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(64) void owgs_engine_kernel(OwgsEngineArgs A) {
-    extern __shared__ __attribute__((aligned(16))) int32_t lds_raw[];
-    const int lane = threadIdx.x;
+__global__ __launch_bounds__(RS_TPB) void owgs_relscan2_kernel(OwgsRelScanArgs A) {
+    __shared__ int tmp[160];
+    int carry = 0;
+    for (int b0 = 0; b0 < A.n_blocks; b0 += RS_TPB) {
+        const int i = b0 + (int)threadIdx.x;
+        const int v = i < A.n_blocks ? A.bsum[i] : 0;
+        int total;
+        const int ex = block_excl_scan(v, tmp, &total);
+        if (i < A.n_blocks) A.bsum[i] = carry + ex;
+        carry += total;
+    }
+}
+
+__global__ __launch_bounds__(RS_TPB) void owgs_relscan3_kernel(OwgsRelScanArgs A) {
+    const int64_t base = (int64_t)blockIdx.x * RS_ELEMS + (int64_t)threadIdx.x * RS_IPT;
+    const int off = A.bsum[blockIdx.x];
+    for (int k = 0; k < RS_IPT; ++k) {
+        const int64_t r = base + k;
+        if (r >= A.n_rel) break;
+        const int64_t aid = A.rel_aid[r];
+        const int cp = off + A.cpos[r];
+        A.cpos[r] = cp;
+        A.relx[aid] = is_conc_rel(A, r) ? cp : rel_batch(A.rel_off, A.n_batches, r);
+    }
+}
+
+// crel_off[b] = number of concurrent releases before rel_off[b]
+__global__ __launch_bounds__(256) void owgs_relscan4_kernel(OwgsRelScanArgs A) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > A.n_batches) return;
+    const int64_t r = A.rel_off[b];
+    int v;
+    if (r < A.n_rel) {
+        v = A.cpos[r];
+    } else if (A.n_rel > 0) {
+        v = A.cpos[A.n_rel - 1] + is_conc_rel(A, A.n_rel - 1);
+    } else {
+        v = 0;
+    }
+    A.crel_off[b] = v;
+}
+
+// per-release flags after a replay: the activation was never scheduled -> no ActivationEntry (CLB:278-279)
+__global__ __launch_bounds__(256) void owgs_relflags_kernel(const int64_t* rel_aid, int64_t n_rel,
+                                                           const int32_t* out_inv, uint8_t* rel_flags) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rel) return;
+    if (out_inv[rel_aid[r]] < 0) rel_flags[r] |= (uint8_t)OWGS_REL_NOENTRY_BIT;
+}
+
+// ------------------------------------------------------------------------------------------------ engine
+struct EngineCtx {
+    const int32_t* P;
+    const uint32_t* ub;
+    const int16_t* pw;
+    const uint32_t* pc;
+    int pool_mode, n_ids, nm, nb;
+};
+
+// pool position -> invoker id (>= 0, usable), OWGS_PW_UNUSABLE or OWGS_PW_BADID
+__device__ __forceinline__ int pool_id(const EngineCtx& E, int pool, int pos) {
+    if (E.pool_mode == 0) {
+        const int id = pool ? E.n_ids - E.nb + pos : pos;
+        return ((E.ub[id >> 5] >> (id & 31)) & 1u) ? id : OWGS_PW_UNUSABLE;
+    }
+    return (int)E.pw[pool ? E.nm + pos : pos];
+}
+
+// usable ids of the identity pool [lo, lo + n) before id x
+__device__ __forceinline__ int usable_before(const EngineCtx& E, int x) {
+    const int w = x >> 5, b = x & 31;
+    const uint32_t m = b ? (E.ub[w] & ((1u << b) - 1u)) : 0u;
+    return (int)E.pc[w] + __popc(m);
+}
+
+// k-th usable id (0-based) at or after id lo (identity pools): binary search over the word prefix counts
+__device__ __forceinline__ int select_usable(const EngineCtx& E, int lo, int k) {
+    const int target = usable_before(E, lo) + k;  // global rank of the wanted id
+    int a = lo >> 5, z = (E.n_ids - 1) >> 5;       // last word w with pc[w] <= target
+    while (a < z) {
+        const int mid = (a + z + 1) >> 1;
+        if ((int)E.pc[mid] <= target) a = mid;
+        else z = mid - 1;
+    }
+    uint32_t m = E.ub[a];
+    int need = target - (int)E.pc[a];
+    while (m) {  // need < popcount(m) when the host's healthy counts match the bitmap
+        const int bit = __ffs((int)m) - 1;
+        if (need == 0) return (a << 5) + bit;
+        m &= m - 1;
+        --need;
+    }
+    return -1;
+}
+
+// Workgroup barrier that orders LDS only: a plain __syncthreads() also waits for every outstanding global store of
+// the wave (vmcnt(0)), which would drain the engine's decision stores and the I/O wave's prefetch at every pass.
+__device__ __forceinline__ void lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+__global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs A) {
+    extern __shared__ uint4 lds_raw[];
+    char* L = (char*)lds_raw;
+    const OwgsLayout Y = owgs_layout(A.n_slots, A.pool_mode, A.n_ids, A.nm, A.nb, A.n_actions);
+    int32_t* P = (int32_t*)(L + Y.P);
+    uint32_t* ub = (uint32_t*)(L + Y.pool);
+    int16_t* pw = (int16_t*)(L + Y.pool);
+    uint32_t* pc = (uint32_t*)(L + Y.pc);
+    uint32_t* cur = (uint32_t*)(L + Y.cur);
+    uint32_t* ctk = (uint32_t*)(L + Y.ctk);
+    uint32_t* ctv = (uint32_t*)(L + Y.ctv);
+    uint4* stgA = (uint4*)(L + Y.stgA);
+    int32_t* stgX = (int32_t*)(L + Y.stgX);
+    uint32_t* fst = (uint32_t*)(L + Y.fst);
+    int32_t* spt = (int32_t*)(L + Y.spt);
+    uint4* hdir = (uint4*)(L + Y.hdir);
+    int32_t* hocc = (int32_t*)(L + Y.hdir + 16u * NHOT);
+    uint2* htab = (uint2*)(L + Y.htab);
+    int32_t* hscr = (int32_t*)(L + Y.hscr);
+    uint32_t* rc = (uint32_t*)(L + Y.rc);
+    int32_t* sc = (int32_t*)(L + Y.sc);
+
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const bool io = wave >= OWGS_EW;
     const int n_slots = A.n_slots, nm = A.nm, nb = A.nb;
-    int32_t* perm = lds_raw;
-    int32_t* pw = lds_raw + ((n_slots + 3) & ~3);
-    uint32_t* stT = (uint32_t*)(pw + ((nm + nb + 3) & ~3));
-    uint32_t* stS = stT + OWGS_STAMP_BUCKETS;
-    int32_t* cur = (int32_t*)(stS + OWGS_STAMP_BUCKETS);
-    const int n_cur = A.n_cursors;
+    const int words = (A.n_ids + 31) >> 5;
 
-    for (int i = lane; i < n_slots; i += 64) perm[i] = A.permits[i];
-    for (int i = lane; i < nm + nb; i += 64) pw[i] = A.pool_words[i];
-    for (int i = lane; i < 2 * OWGS_STAMP_BUCKETS; i += 64) stT[i] = 0xFFFFFFFFu;
-    __syncthreads();
+    // ---------------------------------------------------------------- state -> LDS
+    for (int i = tid; i < n_slots; i += OWGS_NT) P[i] = A.permits[i];
+    if (A.pool_mode == 0) {
+        for (int i = tid; i < words; i += OWGS_NT) ub[i] = A.usable[i];
+    } else {
+        for (int i = tid; i < nm + nb; i += OWGS_NT) pw[i] = (int16_t)A.pool_words[i];
+    }
+    if (tid < SC_N) sc[tid] = (tid < 4) ? OWGS_WL : (tid < 6 ? (int)0x80000000 : 0);
+    lds_sync();
+    {
+        int used = 0;
+        for (int i = tid; i < OWGS_CTC; i += OWGS_NT) {
+            const uint32_t k = A.ct_keys[i];
+            ctk[i] = k;
+            ctv[i] = A.ct_vals[i];
+            used += k != 0;
+        }
+        if (used) atomicAdd(&sc[SC_USED], used);
+    }
+    for (int i = tid; i < (int)(Y.uni_bytes / 4); i += OWGS_NT) ((uint32_t*)(L + Y.uni))[i] = 0u;
+    lds_sync();
+    if (A.pool_mode == 0 && wave == 0) {  // prefix counts of the usable bitmap
+        int carry = 0;
+        for (int w0 = 0; w0 <= words; w0 += 64) {
+            const int w = w0 + lane;
+            const int c = w < words ? __popc(ub[w]) : 0;
+            const int inc = wave_incl_scan(c);
+            if (w <= words) pc[w] = (uint32_t)(carry + inc - c);
+            carry += __builtin_amdgcn_readlane(inc, 63);
+        }
+    }
+    EngineCtx E;
+    E.P = P;
+    E.ub = ub;
+    E.pw = pw;
+    E.pc = pc;
+    E.pool_mode = A.pool_mode;
+    E.n_ids = A.n_ids;
+    E.nm = nm;
+    E.nb = nb;
 
-    uint32_t st_iter = 0, st_fb = 0, st_long = 0, st_grp = 0, st_probe = 0, st_inc = 0;
+    uint32_t st_pass = 0, st_probe = 0, st_fb = 0, st_long = 0, st_chunk = 0, st_stop = 0;
+    uint32_t err = 0;
     PT_DECL
-    uint32_t iter = 0;
-    const u64 lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-    const u64 self_bit = 1ull << lane;
 
+    // ---------------------------------------------------------------- I/O wave: chunk prefetch pipeline
+    // While the engine resolves chunk g, the I/O wave streams the records of chunk g+1 from HBM straight into
+    // stgA/stgX[(g+1)&1] by LDS-DMA (global_load_lds: no registers, nothing for the engine waves to wait on) and
+    // drains them (vmcnt(0)) before the last barrier of chunk g.
+    int io_b = 0;
+    int64_t io_c0 = 0;
+    const uint32_t stgA_lds = (uint32_t)(size_t)stgA, stgX_lds = (uint32_t)(size_t)stgX;
+    // advance (io_b, io_c0) to the next chunk; returns false at the end of the stream
+    auto io_locate = [&](int& bb, int64_t& c0) -> bool {
+        while (bb < A.n_batches && c0 >= A.acq_off[bb + 1]) {
+            ++bb;
+            if (bb < A.n_batches) c0 = A.acq_off[bb];
+        }
+        return bb < A.n_batches;
+    };
+    // lanes past the end of the stream re-read its last record: the engine ignores lanes >= the chunk length
+    auto io_dma = [&](int64_t c0, int buf) {
+        const int64_t last = A.n_act - 1;
+#pragma unroll
+        for (int k = 0; k < OWGS_WL / 64; ++k) {
+            int64_t i = c0 + lane + 64 * k;
+            i = i < last ? i : last;
+            lds_dma16(&A.rec[i], __builtin_amdgcn_readfirstlane(stgA_lds + (uint32_t)(buf * OWGS_WL + 64 * k) * 16u));
+            if (A.relpos)
+                lds_dma4(&A.relpos[i], __builtin_amdgcn_readfirstlane(stgX_lds + (uint32_t)(buf * OWGS_WL + 64 * k) * 4u));
+        }
+    };
+    if (io) {
+        if (A.n_batches > 0) io_c0 = A.acq_off[0];
+        if (io_locate(io_b, io_c0)) {
+            io_dma(io_c0, 0);
+            io_c0 += OWGS_WL;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_sync();
+
+    int g = 0;    // global chunk index
+    int par = 0;  // pass parity (double-buffered LDS scalars)
     for (int b = 0; b < A.n_batches; ++b) {
-        // ================================================================ releases (SCPB:327-331, NS:98-113)
-        const int64_t r_beg = A.rel_off ? A.rel_off[b] : 0, r_end = A.rel_off ? A.rel_off[b + 1] : 0;
-        for (int64_t r0 = r_beg; r0 < r_end; r0 += 64) {
-            const bool valid = lane < r_end - r0;
-            int inv = -1, mem = 0, maxc = 1, slot = 0;
-            if (valid) {
-                const int4 ri = A.rinfo[r0 + lane];
-                inv = A.rel_inv ? ri.x : A.out_inv[ri.x];
-                mem = ri.y;
-                maxc = ri.z & OWGS_META_MAXC_MASK;
-                slot = ri.w;
-            }
-            uint8_t flag = 0;
-            bool conc = false, rel = false;
-            if (valid) {
-                if (inv < 0) flag = OWGS_REL_NOENTRY_BIT;  // no ActivationEntry (CLB:278-279)
-                else if (inv >= n_slots) flag = 0;          // invokerSlots.lift -> no-op
-                else if (maxc == 1) rel = true;
-                else conc = true;
-            }
-            if (__ballot(conc)) {
-                int idx = -1, c0 = 0, o0 = 0;
-                if (conc) {
-                    u64 e;
-                    idx = ct_find(A.ctab, A.ctab_mask, ct_key(inv, slot), &e);
-                    c0 = ct_c(e);
-                    o0 = ct_ops(e);
-                    if (idx < 0 || o0 <= 0) {
-                        conc = false;
-                        flag = OWGS_REL_NOSUCH_BIT;  // actionConcurrentSlotsMap(actionid) throws (NS:103)
-                    }
-                }
-                // releases of one entry inside this group of 64: rank in stream order and group size
-                int rank = 0, gsz = 1;
-                const uint32_t stamp = next_stamp(iter, stT, lane);
-                if (conc) atomicMin(&stT[idx & (OWGS_STAMP_BUCKETS - 1)], stamp);
-                wave_fence();
-                const bool leader = conc && stT[idx & (OWGS_STAMP_BUCKETS - 1)] == stamp;
-                u64 pend = __ballot(conc && !leader);
-                while (pend) {
-                    const int j = ffs64(pend);
-                    const int e = __builtin_amdgcn_readlane(idx, j);
-                    const u64 G = __ballot(conc && idx == e);
-                    if ((G >> lane) & 1) {
-                        rank = __popcll(G & lt_mask);
-                        gsz = __popcll(G);
-                    }
-                    pend &= ~G;
-                }
-                if (conc) {
-                    // RS.release(1, opComplete = true) applied rank+1 times to (c0, o0), reductionSize = maxConc
-                    if (rank < o0) rel = mod_small(c0 + rank + 1, maxc) == 0;
-                    else flag = OWGS_REL_NOSUCH_BIT;  // entry already removed by an earlier release of this group
-                    if (rank == 0) {
-                        const int j = min(gsz, o0);
-                        int c1 = mod_small(c0 + j, maxc);
-                        const int o1 = o0 - j;
-                        if (o1 == 0) c1 = 0;  // actionRelease: entry removed (NS:109-111)
-                        A.ctab[idx] = ct_entry(ct_key(inv, slot), c1, o1);
-                    }
-                }
-            }
-            if (rel) {
-                const int old = atomicAdd(&perm[inv], mem);
-                if (old > 0x7FFFFFFF - mem) {  // ForcibleSemaphore overflow -> Error, state unchanged (FS:48-50)
-                    atomicSub(&perm[inv], mem);
-                    flag |= OWGS_REL_OVERFLOW_BIT;
-                }
-            }
-            if (valid && A.rel_flags) A.rel_flags[r0 + lane] = flag;
-            wave_fence();
-            PT(0);
-        }
-
-        // ================================================================ per-batch bounds and cursors
-        // U0/U1 >= max permits over usable members of the managed/blackbox pool; permits only fall inside a batch.
-        int U0, U1;
-        {
-            int m0 = (int)0x80000000, m1 = (int)0x80000000;
-            for (int i = lane; i < nm; i += 64) {
-                const int w = pw[i];
-                if (w >= 0) m0 = max(m0, perm[w]);
-            }
-            for (int i = lane; i < nb; i += 64) {
-                const int w = pw[nm + i];
-                if (w >= 0) m1 = max(m1, perm[w]);
-            }
-            U0 = wave_max(m0);
-            U1 = wave_max(m1);
-        }
-        for (int i = lane; i < n_cur; i += 64) cur[i] = 0;
-        wave_fence();
-        PT(1);
-
-        // ================================================================ acquires (SCPB:398-436, NS:32-91)
         const int64_t a_beg = A.acq_off[b], a_end = A.acq_off[b + 1];
-        for (int64_t c0i = a_beg; c0i < a_end; c0i += 64) {
-            bool pending = lane < a_end - c0i;
-            const int64_t i = c0i + (pending ? lane : 0);
-            int a = -1, home = 0, step = 0, mem = 0, meta = 0, slot = 0;
-            if (pending) {
-                const int4 info = A.info[i];
-                const int2 ax = A.aux[i];
-                home = info.x;
-                step = info.y;
-                mem = info.z;
-                meta = info.w;
-                slot = ax.x;
-                a = ax.y;
+
+        // ============================================================ releases of batch b (SCPB:327-331)
+        if (A.rel_off) {
+            // the engine's own stores (decisions, aggregated releases, release records) of earlier batches land
+            if (!io) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            lds_sync();
+            if (!io) {
+                // maxConcurrent == 1: the releases of batch b were aggregated per invoker when the activations were
+                // decided (ForcibleSemaphore.release, FS:117-120; the sum of releases is order-free)
+                const int32_t* row = A.acc + (size_t)b * (size_t)A.acc_stride;
+                for (int i = tid; i < n_slots; i += OWGS_WL) {
+                    const int d = __hip_atomic_load(&row[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (d) {
+                        const long long s = (long long)P[i] + d;
+                        if (s > 0x7FFFFFFFLL) err |= OWGS_ERR_BAD_STREAM;  // FS:48-50 would throw
+                        else P[i] = (int32_t)s;
+                    }
+                }
+                // concurrent releases: RS.release(1, true) per release (NS:98-113); the count per entry decides the
+                // final state, each release's memory return depends only on its rank (c0 + q + 1) % R == 0
+                const int64_t cb = A.crel_off[b], ce = A.crel_off[b + 1];
+                for (int64_t r0 = cb + tid; r0 < ce; r0 += 8 * OWGS_WL) {
+                    u64 rr[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int64_t r = r0 + (int64_t)k * OWGS_WL;
+                        rr[k] = r < ce ? __hip_atomic_load((const u64*)&A.rel_rec[r], __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT)
+                                       : 0ull;
+                    }
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int64_t r = r0 + (int64_t)k * OWGS_WL;
+                        if (r >= ce) break;
+                        const uint32_t lo = (uint32_t)rr[k], hi = (uint32_t)(rr[k] >> 32);
+                        const int inv = (int)(lo & 0x7FFFu);
+                        if (inv == (int)OWGS_RR_NOINV || inv >= n_slots) continue;  // no entry / invokerSlots.lift
+                        const int mem = (int)(lo >> 15);
+                        const int slot = (int)(hi & 0x1FFFFu);
+                        const int R = (int)((hi >> 17) & OWGS_AM_MAXC_MASK);
+                        const int ix = ct_find(ctk, ct_key(inv, slot));
+                        const uint32_t v = ix >= 0 ? ctv[ix] : 0u;
+                        const int c0 = (int)(v & OWGS_CT_C_MASK), ops0 = (int)(v >> OWGS_CT_C_BITS);
+                        if (ix < 0 || ops0 == 0) {
+                            err |= OWGS_ERR_BAD_STREAM;  // NoSuchElementException (NS:103)
+                            continue;
+                        }
+                        const uint32_t q = atomicAdd(&rc[ix], 1u << 12) >> 12;
+                        if (q == 0) atomicOr(&rc[ix], (uint32_t)R);
+                        if ((int)q >= ops0) {
+                            err |= OWGS_ERR_BAD_STREAM;
+                            continue;
+                        }
+                        if ((c0 + (int)q + 1) % R == 0) {  // RS:50-52: reduction -> memory release
+                            const int old = atomicAdd(&P[inv], mem);
+                            if (old > 0x7FFFFFFF - mem) err |= OWGS_ERR_BAD_STREAM;
+                        }
+                    }
+                }
             }
-            const int maxc = meta & OWGS_META_MAXC_MASK;
-            const int pool = (meta >> OWGS_META_POOL_SHIFT) & 1;
+            lds_sync();
+            if (!io) {  // apply the release counts: c1 = (c0 + j) mod R, ops1 = ops0 - j, removed at 0 (NS:109-111)
+                for (int ix = tid; ix < OWGS_CTC; ix += OWGS_WL) {
+                    const uint32_t v = rc[ix];
+                    if (!v) continue;
+                    rc[ix] = 0u;
+                    const int R = (int)(v & 0xFFFu);
+                    const uint32_t cv = ctv[ix];
+                    const int c0 = (int)(cv & OWGS_CT_C_MASK), ops0 = (int)(cv >> OWGS_CT_C_BITS);
+                    const int j = min((int)(v >> 12), ops0);
+                    const int ops1 = ops0 - j;
+                    if (ops1 == 0) {
+                        ctk[ix] = OWGS_CT_TOMB;
+                        ctv[ix] = 0u;
+                    } else {
+                        ctv[ix] = (uint32_t)((c0 + j) % R) | ((uint32_t)ops1 << OWGS_CT_C_BITS);
+                    }
+                }
+            }
+        }
+
+        // ============================================================ concurrency-table cleanup
+        // Deleted entries keep probe chains long; once live + deleted exceed half the table, the live entries are
+        // parked in HBM and re-inserted (batch boundary: the engine waves' stores have drained, see above).
+        lds_sync();
+        if (sc[SC_USED] > OWGS_CTC / 2) {
+            if (!io) {
+                for (int ix = tid; ix < OWGS_CTC; ix += OWGS_WL) {
+                    const uint32_t k = ctk[ix];
+                    if (k != 0u && k != OWGS_CT_TOMB) {
+                        const int j = atomicAdd(&sc[SC_NLIVE], 1);
+                        A.ct_tmp[2 * j] = k;
+                        A.ct_tmp[2 * j + 1] = ctv[ix];
+                    }
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            lds_sync();
+            const int nlive = sc[SC_NLIVE];
+            for (int ix = tid; ix < OWGS_CTC; ix += OWGS_NT) {
+                ctk[ix] = 0u;
+                ctv[ix] = 0u;
+            }
+            lds_sync();
+            if (!io) {
+                for (int j = tid; j < nlive; j += OWGS_WL) {
+                    const uint32_t k = __hip_atomic_load(&A.ct_tmp[2 * j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t v = __hip_atomic_load(&A.ct_tmp[2 * j + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    int fresh = 0;
+                    const int ix = ct_insert(ctk, k, &fresh);
+                    ctv[ix] = v;
+                }
+            }
+            lds_sync();
+            if (tid == 0) {
+                sc[SC_USED] = nlive;
+                sc[SC_NLIVE] = 0;
+            }
+            lds_sync();
+        }
+        PT(0);
+        // ============================================================ per-batch bounds and cursors
+        if (!io) {
+            for (int i = tid; i < A.n_actions; i += OWGS_WL) cur[i] = 0u;
+            int m0 = (int)0x80000000, m1 = (int)0x80000000;
+            if (A.pool_mode == 0) {
+                for (int i = tid; i < nm; i += OWGS_WL)
+                    if ((ub[i >> 5] >> (i & 31)) & 1u) m0 = max(m0, P[i]);
+                for (int p = tid; p < nb; p += OWGS_WL) {
+                    const int i = A.n_ids - nb + p;
+                    if ((ub[i >> 5] >> (i & 31)) & 1u) m1 = max(m1, P[i]);
+                }
+            } else {
+                for (int i = tid; i < nm; i += OWGS_WL)
+                    if (pw[i] >= 0) m0 = max(m0, P[pw[i]]);
+                for (int i = tid; i < nb; i += OWGS_WL)
+                    if (pw[nm + i] >= 0) m1 = max(m1, P[pw[nm + i]]);
+            }
+            m0 = wave_max(m0);
+            m1 = wave_max(m1);
+            if (lane == 0) {
+                atomicMax(&sc[SC_U0], m0);
+                atomicMax(&sc[SC_U1], m1);
+            }
+        }
+        lds_sync();
+
+        PT(0);
+        // ============================================================ publishes (SCPB:398-436, NS:32-91)
+        int kstamp = 0;
+        for (int64_t c0 = a_beg; c0 < a_end; c0 += OWGS_WL, ++g) {
+            const int len = (int)min((int64_t)OWGS_WL, a_end - c0);
+            if (++kstamp == 128) {  // stamps wrap: clear the chunk-rank fields, keep the walk cursors
+                if (!io)
+                    for (int i = tid; i < A.n_actions; i += OWGS_WL) cur[i] &= 0x7FFFu;
+                kstamp = 1;
+                lds_sync();
+            }
+            ++st_chunk;
+            // ---- lane record
+            const int li = tid;
+            uint4 rc4 = make_uint4(0, 0, 0, 0);
+            int relx = -1;
+            if (!io) {
+                rc4 = stgA[(g & 1) * OWGS_WL + li];
+                relx = A.relpos ? stgX[(g & 1) * OWGS_WL + li] : -1;
+            }
+            const bool valid = !io && (rc4.y & OWGS_AM_VALID) && li < len;
+            const int home = (int)(rc4.x & OWGS_AM_POS_MASK);
+            const int step = (int)((rc4.x >> 15) & OWGS_AM_POS_MASK);
+            const int pool = (rc4.x & OWGS_AM_POOL) ? 1 : 0;
+            const bool cok = (rc4.x & OWGS_AM_COK) != 0;
+            const int mem = (int)(rc4.y & OWGS_AM_MEM_MASK);
+            const int maxc = (int)((rc4.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
+            const bool sthrow = (rc4.y & OWGS_AM_THROW) != 0;
+            const bool sempty = (rc4.y & OWGS_AM_EMPTY) != 0;
+            const int a = (int)(rc4.z & OWGS_REC_NOACT);
+            const int occ = (int)((rc4.z >> 17) & OWGS_RMASK);
+            const int slot = (int)(rc4.w & 0x1FFFFu);
+            const int nxt = (int)((rc4.w >> 17) & OWGS_REC_NONEXT);
+            const int ext = (int)((rc4.z >> 27) | ((rc4.w >> 27) << 5));  // pk1 (maxConc > 1) or hot slot
+            const int pk1 = maxc > 1 ? ext : 0;
             const int n = pool ? nb : nm;
-            const int pwb = pool ? nm : 0;
-            const bool cok = (meta & OWGS_META_CURSOR) && a >= 0 && a < n_cur;
-            int s = 0, pos = home;  // walk step and its pool position, kept across iterations
-            if (pending && ((meta & (OWGS_META_EMPTY | OWGS_META_THROW)) || home < 0 || home >= n || step < 0)) {
-                A.out_inv[i] = (meta & OWGS_META_EMPTY) ? OWGS_NONE_V : OWGS_THROW_V;  // None / schedule() throws
-                A.out_flags[i] = 0;
-                pending = false;
+            const float rm = __builtin_amdgcn_rcpf((float)(mem > 0 ? mem : 1));
+            const int64_t i = c0 + li;
+            bool pending = valid;
+
+            // ---- hot actions (slots assigned by the pre-pass): the first lane publishes the walk, the last lane
+            // the largest occurrence index
+            const int hs = (valid && maxc == 1 && ext < NHOT && !(A.opts & 1)) ? ext : -1;
+            if (hs >= 0) {
+                if (occ == 0) {
+                    hdir[hs] = make_uint4((uint32_t)a, rc4.x, rc4.y, (uint32_t)slot);
+                    atomicMax(&sc[SC_NHOT], hs + 1);
+                }
+                if (nxt == (int)OWGS_REC_NONEXT) hocc[hs] = occ;
+            }
+            lds_sync();
+            const int nhot = sc[SC_NHOT];
+            // ---- I/O wave: stream chunk g+1 into the other staging buffer
+            if (io && io_locate(io_b, io_c0)) {
+                io_dma(io_c0, (g + 1) & 1);
+                io_c0 += OWGS_WL;
             }
 
             int f = 0;
-            bool full = true;  // lanes >= f need (re)speculation
-            // per-lane speculation, valid for lanes >= f until the next full pass
-            int kind = K_NONE, tgt = -1, room = 0, c0 = 0, cidx = -1, ops0 = 0, q = 0, cons = 0;
-            bool unc = false, fullwalk = false;
-            PT(2);
-            while (__ballot(pending)) {
-                const bool act = pending && lane >= f;
-                if (full) {
-                    full = false;
-                    ++st_iter;
-                    // ---------------------------------------------------- speculate targets against state at f
-                    kind = K_NONE;
-                    tgt = -1;
-                    c0 = 0;
-                    cidx = -1;
-                    ops0 = 0;
-                    q = 0;
-                    unc = false;
-                    fullwalk = false;
-                    int pv = 0;
-                    if (act) {
-                        if (cok) {  // cursor = walk step << 16 | pool position
-                            const int cv = cur[a];
-                            if ((cv >> 16) > s) {
-                                s = cv >> 16;
-                                pos = cv & 0xFFFF;
-                            }
+            PT(1);
+            while (f < len) {
+                ++st_pass;
+                const bool act = pending && li >= f;
+                // ------------------------------------------------ speculate (packing) against the state at f
+                int kind = K_NONE, t = -1, ks = 0, cons = 0, s_t = 0, r = 0;
+                uint32_t cw = 0, cval = 0;
+                int cidx = -1;
+                int ws = 0, wpos = 0, wcum = 0;  // long-walk resume state
+                // ------------------------------------------------ hot actions: one wave-cooperative walk per slot
+                // 64 walk steps per round: capacities, inclusive scan, then every rank q finds the step whose
+                // capacity range holds it (first rank of each step marked in LDS, prefix max over ranks)
+                if (!io) {
+                    for (int h = wave; h < nhot; h += OWGS_EW) {
+                        const uint4 d = hdir[h];
+                        if (d.z & (OWGS_AM_THROW | OWGS_AM_EMPTY)) continue;
+                        const int ha = (int)d.x;
+                        const int hhome = (int)(d.y & OWGS_AM_POS_MASK), hstep = (int)((d.y >> 15) & OWGS_AM_POS_MASK);
+                        const int hpool = (d.y & OWGS_AM_POOL) ? 1 : 0;
+                        const bool hcok = (d.y & OWGS_AM_COK) != 0;
+                        const int hmem = (int)(d.z & OWGS_AM_MEM_MASK);
+                        const int hmc = (int)((d.z >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
+                        const int hslot = (int)d.w;
+                        const uint32_t hcw = cur[ha];
+                        const int hcc = ((int)(hcw >> 25) == kstamp) ? (int)((hcw >> 15) & OWGS_RMASK) : 0;
+                        const int need = min(hocc[h] - hcc + 1, HOT_RANKS);
+                        if (need <= 0) continue;
+                        uint2* tab = htab + h * HOT_RANKS;
+                        const int hn = hpool ? nb : nm;
+                        if (hmc == 1 && hmem > sc[hpool ? SC_U1 : SC_U0] && ((A.shortcut_ok >> hpool) & 1)) {
+                            for (int q = lane; q < need; q += 64) tab[q] = make_uint2((uint32_t)K_FALLBACK << 15, 0u);
+                            continue;
                         }
-                        kind = K_LONG;
-                        if (maxc == 1) {
-                            if (mem > (pool ? U1 : U0) && ((A.shortcut_ok >> pool) & 1)) {
-                                kind = K_FALLBACK;  // every usable permit < mem: the walk fails everywhere
-                            } else {
-#pragma unroll 1
-                                for (int k = 0; k < KPROBE; ++k) {
-                                    if (s >= n) {  // every pool position probed: the n+2-probe walk fails (SCPB:417)
-                                        kind = K_FALLBACK;
-                                        fullwalk = true;
-                                        break;
+                        int s0 = hcok ? (int)(hcw & 0x7FFFu) : 0;
+                        const float rnn = __builtin_amdgcn_rcpf((float)hn);
+                        int p0 = mod_fast(hhome + s0 * hstep, hn, rnn);
+                        const int loff = mod_fast(lane * hstep, hn, rnn), boff = mod_fast(64 * hstep, hn, rnn);
+                        const float rmh = __builtin_amdgcn_rcpf((float)hmem);
+                        int* scr = hscr + wave * 64;
+                        int cum = 0;
+                        ++st_long;
+                        for (;;) {
+                            if (s0 >= hn) {  // every position probed: the remaining ranks fall back (SCPB:417)
+                                for (int q = cum + lane; q < need; q += 64)
+                                    tab[q] = make_uint2((uint32_t)K_FALLBACK << 15, 0u);
+                                break;
+                            }
+                            const int sk = s0 + lane;
+                            int pp = p0 + loff;
+                            pp -= pp >= hn ? hn : 0;
+                            int id = OWGS_PW_UNUSABLE, cap = 0;
+                            bool bad = false;
+                            if (sk < hn) {
+                                id = pool_id(E, hpool, pp);
+                                if (id == OWGS_PW_BADID) {
+                                    bad = true;
+                                } else if (id >= 0) {
+                                    const int pv = P[id];
+                                    if (hmc == 1) {
+                                        cap = cap_bf(pv, hmem, rmh);
+                                    } else {
+                                        const int ci = ct_find(ctk, ct_key(id, hslot));
+                                        const uint32_t v = ci >= 0 ? ctv[ci] : 0u;
+                                        cap = (int)(v & OWGS_CT_C_MASK) + min(cap_bf(pv, hmem, rmh) * hmc, CAPMAX);
                                     }
-                                    const int w = pw[pwb + pos];
-                                    ++st_probe;
-                                    if (w >= 0) {
-                                        const int p = perm[w];
-                                        if (p >= mem) {
-                                            kind = K_TARGET;
-                                            tgt = w;
-                                            pv = p;
-                                            break;
-                                        }
-                                    } else if (w == OWGS_PW_BADID) {
-                                        kind = K_THROW;
-                                        break;
-                                    }
-                                    pos = next_pos(pos, step, n);
-                                    ++s;
                                 }
                             }
+                            st_probe += 1;
+                            const u64 bm = __ballot(bad);
+                            const int qb = bm ? ffs64(bm) : 64;
+                            if (lane >= qb) cap = 0;
+                            const int inc = wave_incl_scan(cap), exc = inc - cap;
+                            const int total = __builtin_amdgcn_readlane(inc, 63);
+                            // lanes exchange marks through LDS: the fences keep the compiler from forwarding this
+                            // lane's own store (the exchange is cross-lane; the wave's LDS ops execute in order)
+                            scr[lane] = -1;
+                            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                            if (cap > 0 && exc < 64) scr[exc] = lane;
+                            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                            const int mv = scr[lane];
+                            const int sj = max(wave_incl_max(mv), 0);
+                            const int tid_ = __shfl(id, sj, 64);
+                            const int ex_ = __shfl(exc, sj, 64);
+                            const int q = cum + lane;
+                            if (q < need && lane < total)
+                                tab[q] = make_uint2((uint32_t)tid_ | ((uint32_t)K_TARGET << 15) |
+                                                        ((uint32_t)(lane - ex_) << 18),
+                                                    (uint32_t)(s0 + sj));
+                            if (qb < 64) {  // the walk of every later rank reaches a throwing probe first
+                                for (int q2 = cum + total + lane; q2 < need; q2 += 64)
+                                    tab[q2] = make_uint2((uint32_t)K_THROW << 15, 0u);
+                                break;
+                            }
+                            cum += total;
+                            if (cum >= need) break;
+                            s0 += 64;
+                            p0 += boff;
+                            p0 -= p0 >= hn ? hn : 0;
                         }
                     }
-                    if (__ballot(act && maxc > 1)) {  // concurrent actions: c >= 1 also makes a probe feasible
-                        if (act && maxc > 1) {
+                }
+                if (act) {
+                    if (sempty) {
+                        kind = K_NONE;
+                    } else if (sthrow) {
+                        kind = K_THROW;
+                    } else {
+                        int s = 0;
+                        r = occ;
+                        if (a != (int)OWGS_REC_NOACT) {
+                            cw = cur[a];
+                            // cursor word: walk step (15 bits) | committed lanes of the action in this chunk (10) |
+                            // chunk stamp (7)
+                            if ((int)(cw >> 25) == kstamp) r = occ - (int)((cw >> 15) & OWGS_RMASK);
+                            if (cok) s = (int)(cw & 0x7FFFu);
+                        }
+                        const int U = sc[pool ? SC_U1 : SC_U0];
+                        if (hs >= 0 && r < HOT_RANKS) {
+                            kind = K_HOT;
+                        } else if (maxc == 1 && mem > U && ((A.shortcut_ok >> pool) & 1)) {
+                            kind = K_FALLBACK;  // every usable permit < mem: the walk fails everywhere
+                        } else {
+                            int pos = mod_fast(home + s * step, n, __builtin_amdgcn_rcpf((float)n));
+                            int cum = 0;
+                            kind = K_LONG;
+                            PT(2);
+                            if (maxc == 1 && A.pool_mode == 0) {
+                                // identity pools: pool position -> id is arithmetic, so the permit and usable-bit
+                                // reads of 4 walk steps are independent and issue together
+                                const int base = pool ? A.n_ids - nb : 0;
+                                bool done = false;
+#pragma unroll 1
+                                for (int g4 = 0; g4 < KPROBE / 4; ++g4) {
+                                    if (done) break;
+                                    int ps[4], pv[4];
+                                    uint32_t wd[4];
+                                    int pp = pos;
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k) {
+                                        ps[k] = pp;
+                                        const int id = base + pp;
+                                        pv[k] = P[id];
+                                        wd[k] = ub[id >> 5];
+                                        pp += step;
+                                        pp -= pp >= n ? n : 0;
+                                    }
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(pv[k]), "+v"(wd[k]));  // 8 reads in flight
+                                    // branch-free scan of the 4 steps: first step whose cumulative capacity exceeds
+                                    // the rank (hit), or the end of the walk (s + k == n: every position probed)
+                                    int hit = 4, kc = cum, hc = cum;
+                                    bool ended = false;
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k) {
+                                        const int id = base + ps[k];
+                                        const int cap = cap_bf(pv[k], mem, rm) & (0 - (int)((wd[k] >> (id & 31)) & 1u));
+                                        const bool open = hit == 4 && !ended;
+                                        const bool fin = open && s + k >= n;
+                                        const bool h = open && !fin && kc + cap > r;
+                                        ended = ended || fin;
+                                        hit = h ? k : hit;
+                                        hc = h ? kc : hc;
+                                        kc += (open && !fin && !h) ? cap : 0;
+                                    }
+                                    st_probe += 4;
+                                    if (hit < 4) {
+                                        kind = K_TARGET;
+                                        t = base + (hit == 0 ? ps[0] : hit == 1 ? ps[1] : hit == 2 ? ps[2] : ps[3]);
+                                        ks = r - hc;
+                                        s_t = s + hit;
+                                        done = true;
+                                    } else if (ended) {
+                                        kind = K_FALLBACK;  // every pool position probed: the walk fails (SCPB:417)
+                                        done = true;
+                                    } else {
+                                        cum = kc;
+                                        s += 4;
+                                        pos = pp;
+                                    }
+                                }
+                                PT(3);
+                            } else {
 #pragma unroll 1
                             for (int k = 0; k < KPROBE; ++k) {
-                                if (s >= n) {
+                                if (s >= n) {  // every pool position probed: the n+2-probe walk fails (SCPB:417)
                                     kind = K_FALLBACK;
-                                    fullwalk = true;
                                     break;
                                 }
-                                const int w = pw[pwb + pos];
+                                const int id = pool_id(E, pool, pos);
                                 ++st_probe;
-                                if (w >= 0) {
-                                    const int p = perm[w];
-                                    int ix, o;
-                                    const int c = conc_lookup(A, w, slot, &ix, &o);
-                                    if (p >= mem || c >= 1) {
-                                        kind = K_TARGET;
-                                        tgt = w;
-                                        pv = p;
-                                        c0 = c;
-                                        cidx = ix;
-                                        ops0 = o;
-                                        break;
-                                    }
-                                } else if (w == OWGS_PW_BADID) {
+                                if (id == OWGS_PW_BADID) {
                                     kind = K_THROW;
                                     break;
                                 }
-                                pos = next_pos(pos, step, n);
+                                if (id >= 0) {
+                                    const int pv = P[id];
+                                    int cap;
+                                    if (maxc == 1) {
+                                        cap = cap_of(pv, mem, rm);
+                                    } else {
+                                        const int ci = ct_find(ctk, ct_key(id, slot));
+                                        const uint32_t v = ci >= 0 ? ctv[ci] : 0u;
+                                        cap = (int)(v & OWGS_CT_C_MASK) + min(cap_of(pv, mem, rm) * maxc, CAPMAX);
+                                        if (cum + cap > r) {
+                                            cval = v;
+                                            cidx = ci;
+                                        }
+                                    }
+                                    if (cum + cap > r) {
+                                        kind = K_TARGET;
+                                        t = id;
+                                        ks = r - cum;
+                                        s_t = s;
+                                        break;
+                                    }
+                                    cum += cap;
+                                }
                                 ++s;
+                                pos += step;
+                                if (pos >= n) pos -= n;
                             }
+                            }
+                            ws = s;
+                            wpos = pos;
+                            wcum = cum;
                         }
                     }
-                    PT(3);
-                    // frontier lane with a long walk: wave-cooperative scan, 64 walk steps per round
-                    if (__builtin_amdgcn_readlane(kind, f) == K_LONG) {
+                }
+                PT(4);
+                // ------------------------------------------------ long walks: wave-cooperative, 64 steps per round
+                if (!io) {
+                    u64 lm = __ballot(act && kind == K_LONG);
+                    while (lm) {
+                        const int j = ffs64(lm);
+                        lm &= lm - 1;
                         ++st_long;
-                        const CoopResult cr = coop_walk(A, perm, pw, f, s, pos, step, n, pwb, mem, maxc, slot);
-                        if (lane == f) {
-                            s = cr.s;
-                            pos = cr.pos;
-                            if (cr.kind == K_LONG) {
-                                kind = K_FALLBACK;
-                                fullwalk = true;
-                            } else {
-                                kind = cr.kind;
-                                tgt = cr.tgt;
-                                pv = cr.pv;
-                                c0 = cr.c;
-                                cidx = cr.cidx;
-                                ops0 = cr.ops;
+                        int s0 = __builtin_amdgcn_readlane(ws, j);
+                        int p0 = __builtin_amdgcn_readlane(wpos, j);
+                        int cum = __builtin_amdgcn_readlane(wcum, j);
+                        const int rj = __builtin_amdgcn_readlane(r, j);
+                        const int stp = __builtin_amdgcn_readlane(step, j);
+                        const int nn = __builtin_amdgcn_readlane(n, j);
+                        const int pj = __builtin_amdgcn_readlane(pool, j);
+                        const int mj = __builtin_amdgcn_readlane(mem, j);
+                        const int cj = __builtin_amdgcn_readlane(maxc, j);
+                        const int slj = __builtin_amdgcn_readlane(slot, j);
+                        const float rmj = __builtin_amdgcn_rcpf((float)mj);
+                        const float rnn = __builtin_amdgcn_rcpf((float)nn);
+                        const int loff = mod_fast(lane * stp, nn, rnn);
+                        const int boff = mod_fast(64 * stp, nn, rnn);
+                        int rk = K_FALLBACK, rt = -1, rks = 0, rst = 0, rci = -1;
+                        uint32_t rcv = 0;
+                        while (s0 < nn) {
+                            const int sk = s0 + lane;
+                            int p = p0 + loff;
+                            if (p >= nn) p -= nn;
+                            int cap = 0, id = OWGS_PW_UNUSABLE, ci = -1;
+                            uint32_t v = 0;
+                            bool bad = false;
+                            if (sk < nn) {
+                                id = pool_id(E, pj, p);
+                                if (id == OWGS_PW_BADID) {
+                                    bad = true;
+                                } else if (id >= 0) {
+                                    const int pv = P[id];
+                                    if (cj == 1) {
+                                        cap = cap_of(pv, mj, rmj);
+                                    } else {
+                                        ci = ct_find(ctk, ct_key(id, slj));
+                                        v = ci >= 0 ? ctv[ci] : 0u;
+                                        cap = (int)(v & OWGS_CT_C_MASK) + min(cap_of(pv, mj, rmj) * cj, CAPMAX);
+                                    }
+                                }
                             }
-                        }
-                    }
-                    // fallback target (SCPB:417-424): H = usable pool members in pool order, r = H[rng(seq) mod |H|]
-                    if (__ballot(act && kind == K_FALLBACK)) {
-                        if (act && kind == K_FALLBACK) {
-                            fallback_target(A, pool, i, n_slots, &kind, &tgt);
-                            if (kind == K_FALLBACK && maxc > 1) c0 = conc_lookup(A, tgt, slot, &cidx, &ops0);
-                        }
-                    }
-                    PT(4);
-                    // ---------------------------------------------------- group by target / by fqn (slot key)
-                    const bool part = act && (kind == K_TARGET || kind == K_FALLBACK);
-                    const bool cpart = part && maxc > 1;
-                    const u64 anyc = __ballot(cpart);
-                    const uint32_t stamp = next_stamp(iter, stT, lane);
-                    if (part) atomicMin(&stT[tgt & (OWGS_STAMP_BUCKETS - 1)], stamp);
-                    if (cpart) atomicMin(&stS[slot & (OWGS_STAMP_BUCKETS - 1)], stamp);
-                    wave_fence();
-                    const bool leadT = part && stT[tgt & (OWGS_STAMP_BUCKETS - 1)] == stamp;
-                    // q = earlier lanes of the same fqn at the same invoker; cons = memory this lane takes;
-                    // E = memory taken at this lane's invoker by earlier lanes of the chunk
-                    int E = 0;
-                    cons = part ? mem : 0;
-                    if (cpart) cons = c0 >= 1 ? 0 : mem;
-                    u64 pend = __ballot(part && !leadT);
-                    while (pend) {
-                        ++st_grp;
-                        const int j = ffs64(pend);
-                        const int t = __builtin_amdgcn_readlane(tgt, j);
-                        const u64 G = __ballot(part && tgt == t);
-                        const bool in = (G >> lane) & 1;
-                        u64 Cg = G & anyc;
-                        while (Cg) {
-                            const int j2 = ffs64(Cg);
-                            const int sl = __builtin_amdgcn_readlane(slot, j2);
-                            const u64 H = Cg & __ballot(slot == sl);
-                            if ((H >> lane) & 1) {
-                                q = __popcll(H & lt_mask);
-                                cons = c_now_of(c0, q, maxc) >= 1 ? 0 : mem;
+                            const int inc = wave_incl_scan(cap);
+                            const bool hit = sk < nn && (bad || cum + inc > rj);
+                            const u64 hm = __ballot(hit);
+                            if (hm) {
+                                const int q = ffs64(hm);
+                                const int qb = __builtin_amdgcn_readlane((int)bad, q);
+                                rst = s0 + q;
+                                if (qb) {
+                                    rk = K_THROW;
+                                } else {
+                                    rk = K_TARGET;
+                                    rt = __builtin_amdgcn_readlane(id, q);
+                                    rks = rj - (cum + __builtin_amdgcn_readlane(inc - cap, q));
+                                    rci = __builtin_amdgcn_readlane(ci, q);
+                                    rcv = (uint32_t)__builtin_amdgcn_readlane((int)v, q);
+                                }
+                                break;
                             }
-                            Cg &= ~H;
+                            cum += __builtin_amdgcn_readlane(inc, 63);
+                            s0 += 64;
+                            p0 += boff;
+                            if (p0 >= nn) p0 -= nn;
                         }
-                        const int ex = wave_excl_scan(in ? cons : 0);
-                        if (in) E = ex;
-                        pend &= ~G;
-                    }
-                    room = pv - E;  // |pv|, E < 2^30 for any sane permit count
-                    // an earlier lane of the same fqn on another walk, or an earlier forced acquire of the same fqn,
-                    // may create concurrency slots this lane's speculation did not see -> uncertain
-                    if (anyc) {
-                        const bool leadS = cpart && stS[slot & (OWGS_STAMP_BUCKETS - 1)] == stamp;
-                        pend = __ballot(cpart && !leadS);
-                        while (pend) {
-                            const int j = ffs64(pend);
-                            const int sl = __builtin_amdgcn_readlane(slot, j);
-                            const u64 Gs = __ballot(cpart && slot == sl);
-                            const int a0 = __builtin_amdgcn_readlane(a, ffs64(Gs));
-                            const u64 D = Gs & __ballot(a != a0);
-                            const u64 FB = Gs & __ballot(kind == K_FALLBACK);
-                            if ((Gs >> lane) & 1) {
-                                const bool lower = (Gs & lt_mask) != 0;
-                                if (kind == K_FALLBACK) unc = lower;
-                                else
-                                    unc = lower &&
-                                          (((FB & lt_mask) != 0) || ((D & (lt_mask | self_bit)) != 0) || a < 0);
-                            }
-                            pend &= ~Gs;
-                        }
-                    }
-                    PT(5);
-                }
-                // -------------------------------------------------------- decide
-                const bool part = act && (kind == K_TARGET || kind == K_FALLBACK);
-                bool ok = false, rej = false;
-                if (act) {
-                    if (kind == K_NONE || kind == K_THROW) {
-                        ok = true;
-                    } else if (kind == K_FALLBACK) {
-                        ok = !(maxc > 1 && unc);
-                    } else if (kind == K_TARGET) {
-                        if (maxc == 1) {
-                            ok = room >= mem;
-                            rej = !ok;
-                        } else if (!unc) {
-                            ok = c_now_of(c0, q, maxc) >= 1 || room >= mem;
-                            rej = !ok;
-                        }
-                    }
-                }
-                const u64 stop = __ballot(act && !ok);
-                const int ls = stop ? ffs64(stop) : 64;
-                const bool commit = act && lane < ls;
-
-                // -------------------------------------------------------- commit lanes [f, l*)
-                if (commit && part && cons > 0) atomicSub(&perm[tgt], mem);
-                if (__ballot(commit && part && maxc > 1)) {
-                    // concurrency map: the last committed lane of each (invoker, fqn) group writes the entry
-                    const bool cpart = part && maxc > 1;
-                    u64 W = __ballot(commit && cpart);
-                    bool writer = false;
-                    while (W) {
-                        const int j = ffs64(W);
-                        const int t = __builtin_amdgcn_readlane(tgt, j);
-                        const int sl = __builtin_amdgcn_readlane(slot, j);
-                        const u64 K = W & __ballot(tgt == t && slot == sl);
-                        if (lane == fls64(K)) writer = true;
-                        W &= ~K;
-                    }
-                    u64 ins = __ballot(writer && cidx < 0);
-                    while (ins) {
-                        const int j = ffs64(ins);
+                        st_probe += (lane == 0) ? 64u : 0u;
                         if (lane == j) {
-                            cidx = ct_insert(A.ctab, A.ctab_mask, ct_key(tgt, slot));
-                            if (cidx < 0) atomicOr(A.err, 1);
+                            kind = rk;
+                            t = rt;
+                            ks = rks;
+                            s_t = rst;
+                            cidx = rci;
+                            cval = rcv;
                         }
-                        wave_fence();
-                        ins &= ins - 1;
-                    }
-                    if (writer && cidx >= 0) {
-                        const int cn = c_now_of(c0, q, maxc);
-                        int c1;
-                        if (cn >= 1) {
-                            c1 = cn - 1;  // RS.tryAcquire(1)
-                        } else {        // memory (try or force) + RS.release(maxConcurrent - 1, false)
-                            const int next2 = cn + (maxc - 1);
-                            c1 = (mod_small(next2, maxc) == 0) ? next2 - maxc : next2;
-                        }
-                        A.ctab[cidx] = ct_entry(ct_key(tgt, slot), c1, (ops0 > 0 ? ops0 : 0) + q + 1);
                     }
                 }
-                if (commit) {
-                    A.out_inv[i] = kind == K_NONE ? OWGS_NONE_V : (kind == K_THROW ? OWGS_THROW_V : tgt);
-                    A.out_flags[i] = (kind == K_FALLBACK) ? 1 : 0;
-                    // cursors: steps before the committed target / after a full walk are infeasible from now on
-                    if (cok && (kind == K_TARGET || (kind == K_FALLBACK && maxc == 1)))
-                        atomicMax(&cur[a], kind == K_TARGET ? ((s << 16) | pos) : (n << 16));
+                PT(5);
+                lds_sync();  // hot tables written; every wave has finished reading P for its speculation
+                if (act && kind == K_HOT) {
+                    const uint2 e = htab[hs * HOT_RANKS + r];
+                    kind = (int)((e.x >> 15) & 7u);
+                    if (kind == K_TARGET) {
+                        t = (int)(e.x & 0x7FFFu);
+                        ks = (int)((e.x >> 18) & OWGS_RMASK);
+                        s_t = (int)e.y;
+                        if (maxc > 1) {
+                            cidx = ct_find(ctk, ct_key(t, slot));
+                            cval = cidx >= 0 ? ctv[cidx] : 0u;
+                        }
+                    }
+                }
+                // ------------------------------------------------ forced fallback target (SCPB:417-424)
+                // (the explicit-seq and explicit-pool variants load from HBM; they are kept on their own paths so
+                // that their vmcnt waits never drain the decision stores of the common path)
+                if (act && kind == K_FALLBACK) {
+                    const int hc = pool ? A.hb : A.hm;
+#define OWGS_LAND(X)                                          \
+    {                                                         \
+        const int x_ = (X);                                   \
+        if (x_ < 0 || x_ >= n_slots) {                        \
+            kind = K_THROW;                                   \
+        } else {                                              \
+            t = x_;                                           \
+            if (maxc > 1) {                                   \
+                cidx = ct_find(ctk, ct_key(t, slot));         \
+                cval = cidx >= 0 ? ctv[cidx] : 0u;            \
+            }                                                 \
+        }                                                     \
+    }
+                    if (hc <= 0) {
+                        kind = K_NONE;
+                    } else if (A.seq == nullptr && A.pool_mode == 0) {
+                        const int k = (int)rng_index(A.rng_seed, A.seq_base + (u64)i, (uint32_t)hc);
+                        OWGS_LAND(select_usable(E, pool ? A.n_ids - nb : 0, k));
+                    } else {
+                        const u64 seq = A.seq ? A.seq[i] : (A.seq_base + (u64)i);
+                        const int k = (int)rng_index(A.rng_seed, seq, (uint32_t)hc);
+                        OWGS_LAND(A.pool_mode == 0 ? select_usable(E, pool ? A.n_ids - nb : 0, k)
+                                                   : A.hlist[(pool ? A.hm : 0) + k]);
+                    }
+#undef OWGS_LAND
+                }
+                const bool part = act && (kind == K_TARGET || kind == K_FALLBACK);
+                if (part) {
+                    const int c0v = (int)(cval & OWGS_CT_C_MASK);
+                    if (maxc == 1) cons = mem;
+                    else if (kind == K_FALLBACK) cons = c0v >= 1 ? 0 : mem;
+                    else cons = (ks < c0v) ? 0 : (((ks - c0v) % maxc) == 0 ? mem : 0);
+                }
+                // ------------------------------------------------ bucket totals
+                // every lane tentatively takes its memory from its target's permits: after the barrier P[t] is the
+                // frontier permits minus the consumption of ALL lanes of the pass at t (the commit keeps it, the
+                // lanes after l give it back).  "first" = lowest lane of the (hashed) bucket of t.
+                const int bk = part ? (int)(((uint32_t)t * 2654435761u) >> (32 - 12)) : 0;
+                static_assert(OWGS_NBK == 4096 && OWGS_WL <= 512, "bucket hash assumes 4096 buckets; lane fields 10 bits");
+                if (part) {
+                    if (cons) atomicSub(&P[t], cons);
+                    atomicMax(&fst[bk], (uint32_t)(OWGS_WL - li));
+                }
+                if (act && maxc > 1 && kind == K_FALLBACK) atomicMin(&sc[SC_CFB + par], li);
+                if (!io) spt[li] = part ? t : -1;
+                lds_sync();
+                // (fallback+buckets accrue to PT(6));
+                PT(6);
+                // ------------------------------------------------ validate: known to fit?
+                bool nf = false;
+                if (part) {
+                    const bool first = fst[bk] == (uint32_t)(OWGS_WL - li);
+                    bool kf;
+                    if (maxc == 1) {
+                        kf = first || kind == K_FALLBACK || P[t] >= 0;
+                    } else {
+                        const int cfb = sc[SC_CFB + par];
+                        if (kind == K_FALLBACK) kf = first && cfb >= li;
+                        else kf = (first || P[t] >= 0) && cfb > li;
+                        if (pk1 > f) kf = false;  // an earlier lane of this pass has the same fqn, another walk
+                    }
+                    nf = !kf;
+                }
+                if (!io) {
+                    const u64 nfm = __ballot(nf);
+                    if (nfm && lane == ffs64(nfm)) atomicMin(&sc[SC_LMIN + par], li);
+                }
+                lds_sync();
+                // (validate accrues to PT(7));
+                // ------------------------------------------------ commit lanes [f, l)
+                int l = sc[SC_LMIN + par];
+                if (l <= f) {  // the frontier lane is always exact; never loop without progress
+                    l = f + 1;
+                    err |= OWGS_ERR_INTERNAL;
+                }
+                if (act && li < l) {
+                    const int outv = kind == K_NONE ? OWGS_NONE_V : (kind == K_THROW ? OWGS_THROW_V : t);
+                    A.out_inv[i] = outv;
+                    A.out_flags[i] = kind == K_FALLBACK ? 1 : 0;
+                    if (kind == K_FALLBACK) ++st_fb;
+                    if (relx >= 0) {
+                        if (maxc == 1) {
+                            if (outv >= 0)
+                                atomicAdd(&A.acc[(size_t)relx * (size_t)A.acc_stride + outv], mem);
+                        } else {
+                            const uint32_t inv15 = outv >= 0 ? (uint32_t)outv : OWGS_RR_NOINV;
+                            A.rel_rec[relx] = make_uint2(inv15 | ((uint32_t)mem << 15),
+                                                         (uint32_t)slot | ((uint32_t)maxc << 17));
+                        }
+                    }
+                    // walk cursor + chunk rank base, written by the last committed lane of the action
+                    if (a != (int)OWGS_REC_NOACT && (nxt == (int)OWGS_REC_NONEXT || nxt >= l)) {
+                        uint32_t ns = cw & 0x7FFFu;
+                        if (cok) {
+                            if (kind == K_TARGET) ns = (uint32_t)s_t;
+                            else if (kind == K_FALLBACK) ns = maxc == 1 ? (uint32_t)n : 0u;
+                        }
+                        cur[a] = ((uint32_t)kstamp << 25) | ((uint32_t)(occ + 1) << 15) | ns;
+                    }
+                    // NestedSemaphore concurrency entry: the last committed lane of the (invoker, fqn) group
+                    if (maxc > 1 && (kind == K_TARGET || kind == K_FALLBACK)) {
+                        const bool writer = kind == K_FALLBACK || nxt == (int)OWGS_REC_NONEXT || nxt >= l ||
+                                            spt[nxt] != t;
+                        if (writer) {
+                            const int c0v = (int)(cval & OWGS_CT_C_MASK), ops0 = (int)(cval >> OWGS_CT_C_BITS);
+                            const int jn = kind == K_FALLBACK ? 1 : ks + 1;
+                            const int c1 = jn <= c0v ? c0v - jn : (maxc - 1 - ((jn - c0v - 1) % maxc));
+                            const int ops1 = ops0 + jn;
+                            if (ops1 > OWGS_MAX_OPS) err |= OWGS_ERR_OPS;
+                            int ix = cidx;
+                            if (ix < 0) {
+                                int fresh = 0;
+                                ix = ct_insert(ctk, ct_key(t, slot), &fresh);
+                                if (fresh) atomicAdd(&sc[SC_USED], 1);
+                            }
+                            if (ix < 0) err |= OWGS_ERR_CTAB_FULL;
+                            else ctv[ix] = (uint32_t)c1 | ((uint32_t)ops1 << OWGS_CT_C_BITS);
+                        }
+                    }
+                    // a failed full walk at rank 0 proves every usable permit of the pool < mem from now on
+                    if (kind == K_FALLBACK && maxc == 1 && r == 0) atomicMin(&sc[pool ? SC_U1 : SC_U0], mem - 1);
                     pending = false;
                 }
-                const u64 fbm = __ballot(commit && kind == K_FALLBACK);
-                if (fbm) {
-                    st_fb += __popcll(fbm);
-                    wave_fence();
-                    if (commit && cok && kind == K_FALLBACK && maxc > 1) cur[a] = 0;  // forced slots: anywhere
-                    // a failed full walk proves every usable pool member has permits < mem from now on
-                    const bool t = commit && kind == K_FALLBACK && fullwalk && maxc == 1;
-                    if (__ballot(t)) {
-                        U0 = min(U0, wave_min(t && pool == 0 ? mem - 1 : 0x7FFFFFFF));
-                        U1 = min(U1, wave_min(t && pool == 1 ? mem - 1 : 0x7FFFFFFF));
-                    }
+                if (part) {
+                    if (li >= l && cons) atomicAdd(&P[t], cons);  // not committed: give the memory back
+                    fst[bk] = 0u;
                 }
-                PT(6);
-                if (ls == 64) break;
+                if (io && l >= len) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk g+1 staged
+                if (tid == 0) {
+                    sc[SC_NHOT] = 0;  // read at the chunk start, before this pass's barriers
+                    sc[SC_LMIN + (par ^ 1)] = OWGS_WL;
+                    sc[SC_CFB + (par ^ 1)] = OWGS_WL;
+                    if (l < len) ++st_stop;
+                }
+                lds_sync();
+                PT(7);
+                f = l;
+                par ^= 1;
+            }
+        }
+        // U bounds are per batch (releases raise permits)
+        if (tid == 0) {
+            sc[SC_U0] = (int)0x80000000;
+            sc[SC_U1] = (int)0x80000000;
+        }
+        lds_sync();
+    }
 
-                // -------------------------------------------------------- resolve l*
-                const int lk = __builtin_amdgcn_readlane(kind, ls);
-                const int lmc = __builtin_amdgcn_readlane(maxc, ls);
-                if (lmc == 1 && (lk == K_TARGET || lk == K_LONG)) {
-                    // Incremental: l* is a maxConcurrent==1 lane and every lane before it is committed, so the
-                    // state is exact at l*'s time.  Walk it to its true target, commit it, and patch the
-                    // remaining permits (room) of later lanes at its old and new invokers; nothing else changed.
-                    ++st_inc;
-                    wave_fence();
-                    const int lm = __builtin_amdgcn_readlane(mem, ls);
-                    if (lk == K_TARGET) {
-                        const int t_old = __builtin_amdgcn_readlane(tgt, ls);
-                        if (act && lane > ls && tgt == t_old && (kind == K_TARGET || kind == K_FALLBACK)) room += lm;
-                        if (lane == ls) {
-                            pos = next_pos(pos, step, n);
-                            ++s;
-                        }
-                    }
-                    if (lane == ls && cok) {
-                        const int cv = cur[a];
-                        if ((cv >> 16) > s) {
-                            s = cv >> 16;
-                            pos = cv & 0xFFFF;
-                        }
-                    }
-                    const int lpool = __builtin_amdgcn_readlane(pool, ls);
-                    int nk, nt = -1, nfull = 0;
-                    if (lm > (lpool ? U1 : U0) && ((A.shortcut_ok >> lpool) & 1)) {
-                        nk = K_LONG;  // provably no feasible step: straight to the fallback
-                    } else {
-                        ++st_long;
-                        const CoopResult cr = coop_walk(A, perm, pw, ls, s, pos, step, n, pwb, mem, 1, slot);
-                        if (lane == ls) {
-                            s = cr.s;
-                            pos = cr.pos;
-                        }
-                        nk = cr.kind;
-                        nt = cr.tgt;
-                        nfull = 1;
-                    }
-                    if (nk == K_LONG) {  // every step fails: random fallback
-                        int fk = K_NONE, ft = -1;
-                        if (lane == ls) fallback_target(A, pool, i, n_slots, &fk, &ft);
-                        nk = __builtin_amdgcn_readlane(fk, ls);
-                        nt = __builtin_amdgcn_readlane(ft, ls);
-                        if (nk == K_FALLBACK) {
-                            ++st_fb;
-                            if (nfull) {
-                                if (lpool) U1 = min(U1, lm - 1);
-                                else U0 = min(U0, lm - 1);
-                            }
-                        }
-                    }
-                    if (lane == ls) {
-                        A.out_inv[i] = nk == K_NONE ? OWGS_NONE_V : (nk == K_THROW ? OWGS_THROW_V : nt);
-                        A.out_flags[i] = (nk == K_FALLBACK) ? 1 : 0;
-                        if (nk == K_TARGET || nk == K_FALLBACK) atomicSub(&perm[nt], lm);
-                        if (cok && (nk == K_TARGET || nk == K_FALLBACK))
-                            atomicMax(&cur[a], nk == K_TARGET ? ((s << 16) | pos) : (n << 16));
-                        pending = false;
-                    }
-                    if ((nk == K_TARGET || nk == K_FALLBACK) && act && lane > ls && tgt == nt &&
-                        (kind == K_TARGET || kind == K_FALLBACK))
-                        room -= lm;
-                    wave_fence();
-                    f = ls + 1;
+    // ---------------------------------------------------------------- LDS -> state
+    for (int i = tid; i < n_slots; i += OWGS_NT) A.permits[i] = P[i];
+    for (int i = tid; i < OWGS_CTC; i += OWGS_NT) {
+        A.ct_keys[i] = ctk[i];
+        A.ct_vals[i] = ctv[i];
+    }
+    if (err) atomicOr(A.err, (int)err);
+    if (A.stats) {
+        if (!io) {
+            atomicAdd(&A.stats[OWGS_ST_PROBES], (u64)st_probe);
+            atomicAdd(&A.stats[OWGS_ST_FALLBACKS], (u64)st_fb);
+            if (lane == 0) atomicAdd(&A.stats[OWGS_ST_LONG], (u64)st_long);
+        }
+#ifdef OWGS_PROFILE
+        if (!io && lane == 0)
+            for (int k = 0; k < 8; ++k) atomicAdd(&A.stats[8 + k], pt_acc[k]);
+#endif
+        if (tid == 0) {
+            atomicAdd(&A.stats[OWGS_ST_PASSES], (u64)st_pass);
+            atomicAdd(&A.stats[OWGS_ST_CHUNKS], (u64)st_chunk);
+            atomicAdd(&A.stats[OWGS_ST_STOPS], (u64)st_stop);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ explicit releases
+// owgs_release_batch: releases in stream order, 64 at a time.  maxConcurrent == 1: FS.release (FS:117-120) with the
+// overflow Error leaving the state unchanged; concurrent: RS.release(1, true) applied rank+1 times inside each group
+// of 64 (NS:98-113), NoSuchElementException when the entry is absent or already removed.
+__global__ __launch_bounds__(64) void owgs_release_seq_kernel(OwgsReleaseArgs R) {
+    __shared__ uint32_t ctk[OWGS_CTC], ctv[OWGS_CTC];
+    const int lane = threadIdx.x;
+    for (int i = lane; i < OWGS_CTC; i += 64) {
+        ctk[i] = R.ct_keys[i];
+        ctv[i] = R.ct_vals[i];
+    }
+    __syncthreads();
+    const u64 lt_mask = lane == 0 ? 0ull : ((~0ull) >> (64 - lane));
+    for (int r0 = 0; r0 < R.n; r0 += 64) {
+        const int r = r0 + lane;
+        const bool valid = r < R.n;
+        int inv = -1, mem = 0, maxc = 1, slot = 0;
+        if (valid) {
+            inv = R.inv[r];
+            mem = R.mem[r];
+            maxc = R.maxc[r];
+            slot = R.slot[r];
+        }
+        uint8_t flag = 0;
+        bool rel = false, conc = false;
+        if (valid) {
+            if (inv < 0) flag = OWGS_REL_NOENTRY_BIT;
+            else if (inv >= R.n_slots) flag = 0;  // invokerSlots.lift -> no-op (SCPB:329)
+            else if (maxc == 1) rel = true;
+            else conc = true;
+        }
+        int ix = -1, c0 = 0, o0 = 0;
+        if (conc) {
+            ix = ct_find(ctk, ct_key(inv, slot));
+            const uint32_t v = ix >= 0 ? ctv[ix] : 0u;
+            c0 = (int)(v & OWGS_CT_C_MASK);
+            o0 = (int)(v >> OWGS_CT_C_BITS);
+            if (ix < 0 || o0 <= 0) {
+                conc = false;
+                flag = OWGS_REL_NOSUCH_BIT;
+            }
+        }
+        // rank of each release among the group's releases of the same entry (stream order) and group size
+        int rank = 0, gsz = 1;
+        u64 pend = __ballot(conc);
+        while (pend) {
+            const int j = ffs64(pend);
+            const int e = __builtin_amdgcn_readlane(ix, j);
+            const u64 G = __ballot(conc && ix == e);
+            if ((G >> lane) & 1) {
+                rank = __popcll(G & lt_mask);
+                gsz = __popcll(G);
+            }
+            pend &= ~G;
+        }
+        if (conc) {
+            if (rank < o0) rel = ((c0 + rank + 1) % maxc) == 0;
+            else flag = OWGS_REL_NOSUCH_BIT;  // entry already removed by an earlier release of this group
+            if (rank == 0) {
+                const int j = min(gsz, o0);
+                const int o1 = o0 - j;
+                if (o1 == 0) {
+                    ctk[ix] = OWGS_CT_TOMB;
+                    ctv[ix] = 0u;
                 } else {
-                    // general case: l* (and every later lane of the same maxConcurrent==1 action speculated at the
-                    // same walk step, when l* is a true rejection) continue past that step; re-speculate from l*
-                    if (__builtin_amdgcn_readlane((int)rej, ls)) {
-                        const int as = __builtin_amdgcn_readlane(a, ls);
-                        const int ss = __builtin_amdgcn_readlane(s, ls);
-                        bool adv = lane == ls;
-                        if (as >= 0 && lmc == 1) adv = adv || (act && lane > ls && a == as && kind == K_TARGET && s == ss);
-                        if (adv) {
-                            pos = next_pos(pos, step, n);
-                            ++s;
-                        }
-                        if (lane == ls && cok) atomicMax(&cur[a], (s << 16) | pos);
-                    }
-                    wave_fence();
-                    f = ls;
-                    full = true;
+                    ctv[ix] = (uint32_t)((c0 + j) % maxc) | ((uint32_t)o1 << OWGS_CT_C_BITS);
                 }
             }
         }
-        wave_fence();
-    }
-
-    for (int i = lane; i < n_slots; i += 64) A.permits[i] = perm[i];
-    if (A.stats) {
-        atomicAdd(&A.stats[1], (u64)st_probe);
-        if (lane == 0) {
-            atomicAdd(&A.stats[0], (u64)st_iter);
-            atomicAdd(&A.stats[2], (u64)st_fb);
-            atomicAdd(&A.stats[3], (u64)st_long);
-            atomicAdd(&A.stats[4], (u64)st_grp);
-            atomicAdd(&A.stats[5], (u64)st_inc);
-#ifdef OWGS_PROFILE
-            for (int k = 0; k < 8; ++k) atomicAdd(&A.stats[8 + k], pt_acc[k]);
-#endif
+        // memory releases in stream order: lanes releasing to the same invoker are applied lane by lane so the
+        // overflow Error (FS:48-50) hits exactly the releases the reference rejects
+        u64 rm = __ballot(rel);
+        while (rm) {
+            const int j = ffs64(rm);
+            rm &= rm - 1;
+            if (lane == j) {
+                const int old = R.permits[inv];
+                if (old > 0x7FFFFFFF - mem) flag |= OWGS_REL_OVERFLOW_BIT;
+                else R.permits[inv] = old + mem;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         }
+        if (valid && R.flags) R.flags[r] = flag;
+        __syncthreads();
+    }
+    for (int i = lane; i < OWGS_CTC; i += 64) {
+        R.ct_keys[i] = ctk[i];
+        R.ct_vals[i] = ctv[i];
     }
 }
 
@@ -891,15 +1520,19 @@ __global__ __launch_bounds__(64) void owgs_selftest_kernel(int* bad, int trials)
     for (int t = 0; t < trials; ++t) {
         const uint32_t h = ct_hash((uint32_t)(t * 64 + lane) * 2654435761u);
         const int v = (int)(h % 2001u) - 1000;
-        const int inc = wave_incl_scan(v), exc = wave_excl_scan(v), mx = wave_max(v), mn = wave_min(v);
-        int ref_inc = 0, ref_mx = (int)0x80000000, ref_mn = 0x7FFFFFFF;
+        const int inc = wave_incl_scan(v), mx = wave_max(v);
+        int ref_inc = 0, ref_mx = (int)0x80000000;
         for (int j = 0; j < 64; ++j) {
             const int vj = __shfl(v, j, 64);
             if (j <= lane) ref_inc += vj;
             ref_mx = max(ref_mx, vj);
-            ref_mn = min(ref_mn, vj);
         }
-        if (inc != ref_inc || exc != ref_inc - v || mx != ref_mx || mn != ref_mn) atomicAdd(bad, 1);
+        if (inc != ref_inc || mx != ref_mx) atomicAdd(bad, 1);
+        // cap_of against integer division
+        const int m = 1 + (int)(h % 4096u), pv = (int)(ct_hash(h) % 5000000u);
+        const int cq = cap_of(pv, m, __builtin_amdgcn_rcpf((float)m));
+        const int ref = min(pv / m, CAPMAX);
+        if (cq != ref) atomicAdd(bad, 1);
     }
 }
 
@@ -916,14 +1549,6 @@ extern "C" hipError_t owgs_launch_hash(const OwgsHashArgs* a, hipStream_t s) {
     return hipGetLastError();
 }
 
-extern "C" hipError_t owgs_launch_gather(const OwgsGatherArgs* g, hipStream_t s) {
-    const int64_t n = g->n_act > g->n_rel ? g->n_act : g->n_rel;
-    if (n <= 0) return hipSuccess;
-    const int64_t blocks = (n + 255) / 256;
-    hipLaunchKernelGGL(owgs_gather_kernel, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0, s, *g);
-    return hipGetLastError();
-}
-
 extern "C" hipError_t owgs_launch_lookup(const OwgsLookupArgs* a, hipStream_t s) {
     if (a->n <= 0) return hipSuccess;
     hipLaunchKernelGGL(owgs_lookup_kernel, dim3((a->n + 255) / 256), dim3(256), 0, s, *a);
@@ -936,13 +1561,59 @@ extern "C" hipError_t owgs_launch_prepare(const OwgsPrepArgs* a, hipStream_t s) 
     return hipGetLastError();
 }
 
-extern "C" size_t owgs_engine_lds_bytes(int n_slots, int nm, int nb, int n_cursors) {
-    return (size_t)(((n_slots + 3) & ~3) + ((nm + nb + 3) & ~3) + 2 * OWGS_STAMP_BUCKETS) * 4 +
-           (size_t)((n_cursors + 3) & ~3) * 4;
+// chunk table + per-activation records; max_chunks >= sum of ceil(n_b / OWGS_WL)
+extern "C" hipError_t owgs_launch_prepass(const OwgsPrepassArgs* a, int32_t* cstart, int64_t max_chunks,
+                                          hipStream_t s) {
+    hipLaunchKernelGGL(owgs_chunks_kernel, dim3(1), dim3(64), 0, s, a->acq_off, a->n_batches, cstart);
+    if (max_chunks <= 0) return hipGetLastError();
+    OwgsPrepassArgs b = *a;
+    b.cstart = cstart;
+    hipLaunchKernelGGL(owgs_prepass_kernel, dim3((unsigned)max_chunks), dim3(OWGS_WL), 0, s, b);
+    return hipGetLastError();
+}
+
+extern "C" int64_t owgs_relscan_blocks(int64_t n_rel) { return (n_rel + RS_ELEMS - 1) / RS_ELEMS; }
+
+extern "C" hipError_t owgs_launch_relscan(const int64_t* rel_aid, int64_t n_rel, const int32_t* act,
+                                          const uint2* act_meta, int32_t* cpos, int32_t* bsum,
+                                          const int64_t* rel_off, int32_t n_batches, int32_t* relx,
+                                          int32_t* crel_off, hipStream_t s) {
+    OwgsRelScanArgs A;
+    A.rel_aid = rel_aid;
+    A.n_rel = n_rel;
+    A.act = act;
+    A.act_meta = act_meta;
+    A.cpos = cpos;
+    A.bsum = bsum;
+    A.n_blocks = (int32_t)owgs_relscan_blocks(n_rel);
+    A.rel_off = rel_off;
+    A.n_batches = n_batches;
+    A.relx = relx;
+    A.crel_off = crel_off;
+    if (n_rel > 0) {
+        hipLaunchKernelGGL(owgs_relscan1_kernel, dim3((unsigned)A.n_blocks), dim3(RS_TPB), 0, s, A);
+        hipLaunchKernelGGL(owgs_relscan2_kernel, dim3(1), dim3(RS_TPB), 0, s, A);
+        hipLaunchKernelGGL(owgs_relscan3_kernel, dim3((unsigned)A.n_blocks), dim3(RS_TPB), 0, s, A);
+    }
+    hipLaunchKernelGGL(owgs_relscan4_kernel, dim3((unsigned)((n_batches + 1 + 255) / 256)), dim3(256), 0, s, A);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t owgs_launch_relflags(const int64_t* rel_aid, int64_t n_rel, const int32_t* out_inv,
+                                           uint8_t* rel_flags, hipStream_t s) {
+    if (n_rel <= 0) return hipSuccess;
+    hipLaunchKernelGGL(owgs_relflags_kernel, dim3((unsigned)((n_rel + 255) / 256)), dim3(256), 0, s, rel_aid, n_rel,
+                       out_inv, rel_flags);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t owgs_launch_release_seq(const OwgsReleaseArgs* a, hipStream_t s) {
+    hipLaunchKernelGGL(owgs_release_seq_kernel, dim3(1), dim3(64), 0, s, *a);
+    return hipGetLastError();
 }
 
 extern "C" hipError_t owgs_launch_engine(const OwgsEngineArgs* a, hipStream_t s) {
-    const size_t lds = owgs_engine_lds_bytes(a->n_slots, a->nm, a->nb, a->n_cursors);
+    const size_t lds = owgs_engine_lds_bytes(a->n_slots, a->pool_mode, a->n_ids, a->nm, a->nb, a->n_actions);
     if (lds > OWGS_LDS_BYTES) return hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
@@ -951,6 +1622,6 @@ extern "C" hipError_t owgs_launch_engine(const OwgsEngineArgs* a, hipStream_t s)
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL(owgs_engine_kernel, dim3(1), dim3(64), lds, s, *a);
+    hipLaunchKernelGGL(owgs_engine_kernel, dim3(1), dim3(OWGS_NT), lds, s, *a);
     return hipGetLastError();
 }
