@@ -253,8 +253,8 @@ class GpuShardingContainerPoolBalancer:
         out = (C.c_uint64 * 16)()
         self._chk(self._L.owgs_read_stats(self._h, out, 16))
         d = {"passes": out[0], "probes": out[1], "fallbacks": out[2], "long_walks": out[3], "chunks": out[4],
-             "stops": out[5]}
+             "stops": out[5], "general_probes": out[6], "general_lanes": out[7]}
         if any(out[8:16]):
-            names = ["batch", "chunk_load", "spec_setup", "walk_fast", "walk_general", "long_walk", "buckets", "validate_commit"]
+            names = ["batch", "chunk_start", "speculate", "tables_buckets", "validate", "commit", "worst_hot", "worst_lane"]
             d["cycles"] = {k: out[8 + i] for i, k in enumerate(names)}
         return d

@@ -30,10 +30,14 @@
 
 // --------------------------------------------------------------------------------------------- engine geometry
 #ifndef OWGS_EW
-#define OWGS_EW 4                      // engine waves per workgroup (one per SIMD)
+#define OWGS_EW 8                      // engine waves per workgroup (two per SIMD: one issues while the other waits)
 #endif
-#define OWGS_WL (OWGS_EW * 64)         // chunk width: activations resolved together (one per engine lane)
-#define OWGS_NT (OWGS_WL + 64)         // threads: engine waves + one I/O wave
+#ifndef OWGS_LPW
+#define OWGS_LPW 32                    // activations per engine wave (the other lanes serve the wave-wide walks)
+#endif
+#define OWGS_ENT (OWGS_EW * 64)        // engine threads
+#define OWGS_WL (OWGS_EW * OWGS_LPW)   // chunk width: activations resolved together (one per engine lane)
+#define OWGS_NT (OWGS_ENT + 64)        // threads: engine waves + one I/O wave
 #define OWGS_NBK 4096                  // "first lane of its invoker" buckets (hashed; collisions are conservative)
 #define OWGS_CTC 4096                  // concurrency-table capacity (entries, power of two)
 #define OWGS_LDS_BYTES (160 * 1024)

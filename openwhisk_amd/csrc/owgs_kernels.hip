@@ -43,13 +43,19 @@ typedef unsigned long long u64;
 #define K_LONG 4
 #define K_HOT 5  // resolved from the hot-action rank table after the pass barrier
 
-#define KPROBE 16  // walk steps a lane probes on its own before the wave-cooperative walk (multiple of 4)
+#ifndef KPROBE
+#define KPROBE 16  // walk steps a maxConcurrent==1 lane probes on its own before the wave-cooperative walk (x4)
+#endif
+#ifndef KPROBE_G
+#define KPROBE_G 16  // same for the general path (concurrency lookups per step)
+#endif
 #define CAPMAX 1024  // capacities are clamped: a lane's rank is < OWGS_WL
 
 // diagnostic build (-DOWGS_PROFILE, libowgs_prof.so): s_memtime cycle accounting per engine phase into stats[8..15]
 #ifdef OWGS_PROFILE
 #define PT_DECL                 \
     u64 pt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
+    u64 pt_x[2] = {0, 0};                     \
     u64 pt_t = __builtin_amdgcn_s_memtime();
 #define PT(k)                                        \
     {                                                \
@@ -70,7 +76,7 @@ typedef unsigned long long u64;
 #define SC_USED 6   // non-empty concurrency-table entries (live + deleted)
 #define SC_NLIVE 7  // table rebuild: live entries
 #define SC_NHOT 8   // multi-lane actions of the current chunk (hot slots claimed)
-#define SC_N 16
+#define SC_N (16 + 4 * OWGS_EW)
 
 // hot actions: every maxConcurrent==1 action with >= HOT_MIN lanes in a chunk gets a slot (assigned by the pre-pass);
 // per pass one wave walks its capacity prefix once and writes the target of each rank 0..HOT_RANKS-1 into the slot's
@@ -175,6 +181,38 @@ __device__ __forceinline__ int ct_insert(uint32_t* ctk, uint32_t key, int* fresh
     return -1;
 }
 
+// interleaved {key, value} table (engine LDS): one ds_read_b64 per probe returns both
+__device__ __forceinline__ int ct_findv(const uint2* ct, uint32_t key, uint32_t* val) {
+    uint32_t h = ct_hash(key) & (OWGS_CTC - 1);
+    for (int p = 0; p < OWGS_CTC; ++p) {
+        const uint2 e = ct[h];
+        if (e.x == key) {
+            *val = e.y;
+            return (int)h;
+        }
+        if (e.x == 0) break;
+        h = (h + 1) & (OWGS_CTC - 1);
+    }
+    *val = 0u;
+    return -1;
+}
+__device__ __forceinline__ int ct_insertv(uint2* ct, uint32_t key, int* fresh) {
+    uint32_t h = ct_hash(key) & (OWGS_CTC - 1);
+    for (int p = 0; p < OWGS_CTC;) {
+        const uint32_t k = ct[h].x;
+        if (k == 0 || k == OWGS_CT_TOMB) {
+            if (atomicCAS((uint32_t*)&ct[h], k, key) == k) {
+                *fresh = k == 0;
+                return (int)h;
+            }
+            continue;  // lost the race: re-read this entry
+        }
+        h = (h + 1) & (OWGS_CTC - 1);
+        ++p;
+    }
+    return -1;
+}
+
 // min(floor(pv / m), CAPMAX) for pv >= 0, 0 when pv < m; float reciprocal + one correction (pv / m < 2^10)
 __device__ __forceinline__ int cap_of(int pv, int m, float rm) {
     if (pv < m) return 0;
@@ -227,7 +265,7 @@ __device__ __forceinline__ void lds_dma4(const void* gsrc, uint32_t lds_dst) {
 
 // ------------------------------------------------------------------------------------------------ LDS layout
 struct OwgsLayout {
-    uint32_t P, pool, pc, cur, ctk, ctv, stgA, stgX, fst, spt, hdir, htab, hscr, rc, sc, uni, uni_bytes, total;
+    uint32_t P, pool, pc, cur, ct, stgA, stgX, fst, spt, hdir, htab, hscr, rc, sc, uni, uni_bytes, total;
 };
 
 __host__ __device__ inline OwgsLayout owgs_layout(int n_slots, int pool_mode, int n_ids, int nm, int nb, int n_actions) {
@@ -243,10 +281,8 @@ __host__ __device__ inline OwgsLayout owgs_layout(int n_slots, int pool_mode, in
     o += pool_mode ? 0u : OWGS_AL(4u * (words + 1));
     L.cur = o;
     o += OWGS_AL(4u * (uint32_t)n_actions);
-    L.ctk = o;
-    o += 4u * OWGS_CTC;
-    L.ctv = o;
-    o += 4u * OWGS_CTC;
+    L.ct = o;
+    o += 8u * OWGS_CTC;
     L.stgA = o;
     o += 2u * OWGS_WL * 16u;
     L.stgX = o;
@@ -257,8 +293,8 @@ __host__ __device__ inline OwgsLayout owgs_layout(int n_slots, int pool_mode, in
     L.uni = o;
     L.fst = o;
     L.spt = o + 4u * OWGS_NBK;
-    L.hdir = L.spt + 4u * OWGS_WL;                  // NHOT x {action, meta.x, meta.y, slot}, then NHOT x max occ
-    L.htab = L.hdir + 20u * NHOT;                   // NHOT x HOT_RANKS x {id | kind << 15 | ks << 18, step}
+    L.hdir = L.spt + 4u * OWGS_WL;                  // NHOT x {action, meta.x, meta.y, slot}, NHOT x max occ, NHOT x flag
+    L.htab = L.hdir + 24u * NHOT;                   // NHOT x HOT_RANKS x {id | kind << 15 | ks << 18, step}
     L.hscr = L.htab + 8u * NHOT * HOT_RANKS;        // OWGS_EW x 64 rank marks
     L.rc = o;
     const uint32_t ua = (L.hscr - o) + 4u * 64 * OWGS_EW, ur = 4u * OWGS_CTC;
@@ -611,18 +647,21 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
     int16_t* pw = (int16_t*)(L + Y.pool);
     uint32_t* pc = (uint32_t*)(L + Y.pc);
     uint32_t* cur = (uint32_t*)(L + Y.cur);
-    uint32_t* ctk = (uint32_t*)(L + Y.ctk);
-    uint32_t* ctv = (uint32_t*)(L + Y.ctv);
+    uint2* ct = (uint2*)(L + Y.ct);  // interleaved {key, value}
     uint4* stgA = (uint4*)(L + Y.stgA);
     int32_t* stgX = (int32_t*)(L + Y.stgX);
     uint32_t* fst = (uint32_t*)(L + Y.fst);
     int32_t* spt = (int32_t*)(L + Y.spt);
     uint4* hdir = (uint4*)(L + Y.hdir);
     int32_t* hocc = (int32_t*)(L + Y.hdir + 16u * NHOT);
+    int32_t* hflag = (int32_t*)(L + Y.hdir + 20u * NHOT);
     uint2* htab = (uint2*)(L + Y.htab);
     int32_t* hscr = (int32_t*)(L + Y.hscr);
     uint32_t* rc = (uint32_t*)(L + Y.rc);
     int32_t* sc = (int32_t*)(L + Y.sc);
+#ifdef OWGS_PROFILE
+    int* spw = sc + 16;  // per-wave speculation timings (SC_N leaves room in every build)
+#endif
 
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const bool io = wave >= OWGS_EW;
@@ -642,8 +681,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
         int used = 0;
         for (int i = tid; i < OWGS_CTC; i += OWGS_NT) {
             const uint32_t k = A.ct_keys[i];
-            ctk[i] = k;
-            ctv[i] = A.ct_vals[i];
+            ct[i] = make_uint2(k, A.ct_vals[i]);
             used += k != 0;
         }
         if (used) atomicAdd(&sc[SC_USED], used);
@@ -670,7 +708,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
     E.nm = nm;
     E.nb = nb;
 
-    uint32_t st_pass = 0, st_probe = 0, st_fb = 0, st_long = 0, st_chunk = 0, st_stop = 0;
+    uint32_t st_pass = 0, st_probe = 0, st_fb = 0, st_long = 0, st_chunk = 0, st_stop = 0, st_gprobe = 0, st_glane = 0;
     uint32_t err = 0;
     PT_DECL
 
@@ -725,7 +763,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 // maxConcurrent == 1: the releases of batch b were aggregated per invoker when the activations were
                 // decided (ForcibleSemaphore.release, FS:117-120; the sum of releases is order-free)
                 const int32_t* row = A.acc + (size_t)b * (size_t)A.acc_stride;
-                for (int i = tid; i < n_slots; i += OWGS_WL) {
+                for (int i = tid; i < n_slots; i += OWGS_ENT) {
                     const int d = __hip_atomic_load(&row[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (d) {
                         const long long s = (long long)P[i] + d;
@@ -736,18 +774,18 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 // concurrent releases: RS.release(1, true) per release (NS:98-113); the count per entry decides the
                 // final state, each release's memory return depends only on its rank (c0 + q + 1) % R == 0
                 const int64_t cb = A.crel_off[b], ce = A.crel_off[b + 1];
-                for (int64_t r0 = cb + tid; r0 < ce; r0 += 8 * OWGS_WL) {
+                for (int64_t r0 = cb + tid; r0 < ce; r0 += 8 * OWGS_ENT) {
                     u64 rr[8];
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
-                        const int64_t r = r0 + (int64_t)k * OWGS_WL;
+                        const int64_t r = r0 + (int64_t)k * OWGS_ENT;
                         rr[k] = r < ce ? __hip_atomic_load((const u64*)&A.rel_rec[r], __ATOMIC_RELAXED,
                                                            __HIP_MEMORY_SCOPE_AGENT)
                                        : 0ull;
                     }
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
-                        const int64_t r = r0 + (int64_t)k * OWGS_WL;
+                        const int64_t r = r0 + (int64_t)k * OWGS_ENT;
                         if (r >= ce) break;
                         const uint32_t lo = (uint32_t)rr[k], hi = (uint32_t)(rr[k] >> 32);
                         const int inv = (int)(lo & 0x7FFFu);
@@ -755,8 +793,8 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                         const int mem = (int)(lo >> 15);
                         const int slot = (int)(hi & 0x1FFFFu);
                         const int R = (int)((hi >> 17) & OWGS_AM_MAXC_MASK);
-                        const int ix = ct_find(ctk, ct_key(inv, slot));
-                        const uint32_t v = ix >= 0 ? ctv[ix] : 0u;
+                        uint32_t v;
+                        const int ix = ct_findv(ct, ct_key(inv, slot), &v);
                         const int c0 = (int)(v & OWGS_CT_C_MASK), ops0 = (int)(v >> OWGS_CT_C_BITS);
                         if (ix < 0 || ops0 == 0) {
                             err |= OWGS_ERR_BAD_STREAM;  // NoSuchElementException (NS:103)
@@ -768,7 +806,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                             err |= OWGS_ERR_BAD_STREAM;
                             continue;
                         }
-                        if ((c0 + (int)q + 1) % R == 0) {  // RS:50-52: reduction -> memory release
+                        if (mod_fast(c0 + (int)q + 1, R, __builtin_amdgcn_rcpf((float)R)) == 0) {  // RS:50-52
                             const int old = atomicAdd(&P[inv], mem);
                             if (old > 0x7FFFFFFF - mem) err |= OWGS_ERR_BAD_STREAM;
                         }
@@ -777,20 +815,19 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
             }
             lds_sync();
             if (!io) {  // apply the release counts: c1 = (c0 + j) mod R, ops1 = ops0 - j, removed at 0 (NS:109-111)
-                for (int ix = tid; ix < OWGS_CTC; ix += OWGS_WL) {
+                for (int ix = tid; ix < OWGS_CTC; ix += OWGS_ENT) {
                     const uint32_t v = rc[ix];
                     if (!v) continue;
                     rc[ix] = 0u;
                     const int R = (int)(v & 0xFFFu);
-                    const uint32_t cv = ctv[ix];
+                    const uint32_t cv = ct[ix].y;
                     const int c0 = (int)(cv & OWGS_CT_C_MASK), ops0 = (int)(cv >> OWGS_CT_C_BITS);
                     const int j = min((int)(v >> 12), ops0);
                     const int ops1 = ops0 - j;
                     if (ops1 == 0) {
-                        ctk[ix] = OWGS_CT_TOMB;
-                        ctv[ix] = 0u;
+                        ct[ix] = make_uint2(OWGS_CT_TOMB, 0u);
                     } else {
-                        ctv[ix] = (uint32_t)((c0 + j) % R) | ((uint32_t)ops1 << OWGS_CT_C_BITS);
+                        ct[ix].y = (uint32_t)((c0 + j) % R) | ((uint32_t)ops1 << OWGS_CT_C_BITS);
                     }
                 }
             }
@@ -802,12 +839,12 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
         lds_sync();
         if (sc[SC_USED] > OWGS_CTC / 2) {
             if (!io) {
-                for (int ix = tid; ix < OWGS_CTC; ix += OWGS_WL) {
-                    const uint32_t k = ctk[ix];
+                for (int ix = tid; ix < OWGS_CTC; ix += OWGS_ENT) {
+                    const uint32_t k = ct[ix].x;
                     if (k != 0u && k != OWGS_CT_TOMB) {
                         const int j = atomicAdd(&sc[SC_NLIVE], 1);
                         A.ct_tmp[2 * j] = k;
-                        A.ct_tmp[2 * j + 1] = ctv[ix];
+                        A.ct_tmp[2 * j + 1] = ct[ix].y;
                     }
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -815,17 +852,16 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
             lds_sync();
             const int nlive = sc[SC_NLIVE];
             for (int ix = tid; ix < OWGS_CTC; ix += OWGS_NT) {
-                ctk[ix] = 0u;
-                ctv[ix] = 0u;
+                ct[ix] = make_uint2(0u, 0u);
             }
             lds_sync();
             if (!io) {
-                for (int j = tid; j < nlive; j += OWGS_WL) {
+                for (int j = tid; j < nlive; j += OWGS_ENT) {
                     const uint32_t k = __hip_atomic_load(&A.ct_tmp[2 * j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     const uint32_t v = __hip_atomic_load(&A.ct_tmp[2 * j + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     int fresh = 0;
-                    const int ix = ct_insert(ctk, k, &fresh);
-                    ctv[ix] = v;
+                    const int ix = ct_insertv(ct, k, &fresh);
+                    ct[ix].y = v;
                 }
             }
             lds_sync();
@@ -838,19 +874,19 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
         PT(0);
         // ============================================================ per-batch bounds and cursors
         if (!io) {
-            for (int i = tid; i < A.n_actions; i += OWGS_WL) cur[i] = 0u;
+            for (int i = tid; i < A.n_actions; i += OWGS_ENT) cur[i] = 0u;
             int m0 = (int)0x80000000, m1 = (int)0x80000000;
             if (A.pool_mode == 0) {
-                for (int i = tid; i < nm; i += OWGS_WL)
+                for (int i = tid; i < nm; i += OWGS_ENT)
                     if ((ub[i >> 5] >> (i & 31)) & 1u) m0 = max(m0, P[i]);
-                for (int p = tid; p < nb; p += OWGS_WL) {
+                for (int p = tid; p < nb; p += OWGS_ENT) {
                     const int i = A.n_ids - nb + p;
                     if ((ub[i >> 5] >> (i & 31)) & 1u) m1 = max(m1, P[i]);
                 }
             } else {
-                for (int i = tid; i < nm; i += OWGS_WL)
+                for (int i = tid; i < nm; i += OWGS_ENT)
                     if (pw[i] >= 0) m0 = max(m0, P[pw[i]]);
-                for (int i = tid; i < nb; i += OWGS_WL)
+                for (int i = tid; i < nb; i += OWGS_ENT)
                     if (pw[nm + i] >= 0) m1 = max(m1, P[pw[nm + i]]);
             }
             m0 = wave_max(m0);
@@ -869,20 +905,21 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
             const int len = (int)min((int64_t)OWGS_WL, a_end - c0);
             if (++kstamp == 128) {  // stamps wrap: clear the chunk-rank fields, keep the walk cursors
                 if (!io)
-                    for (int i = tid; i < A.n_actions; i += OWGS_WL) cur[i] &= 0x7FFFu;
+                    for (int i = tid; i < A.n_actions; i += OWGS_ENT) cur[i] &= 0x7FFFu;
                 kstamp = 1;
                 lds_sync();
             }
             ++st_chunk;
             // ---- lane record
-            const int li = tid;
+            const bool own = !io && lane < OWGS_LPW;  // this thread holds an activation of the chunk
+            const int li = own ? wave * OWGS_LPW + lane : OWGS_WL;
             uint4 rc4 = make_uint4(0, 0, 0, 0);
             int relx = -1;
-            if (!io) {
+            if (own) {
                 rc4 = stgA[(g & 1) * OWGS_WL + li];
                 relx = A.relpos ? stgX[(g & 1) * OWGS_WL + li] : -1;
             }
-            const bool valid = !io && (rc4.y & OWGS_AM_VALID) && li < len;
+            const bool valid = own && (rc4.y & OWGS_AM_VALID) && li < len;
             const int home = (int)(rc4.x & OWGS_AM_POS_MASK);
             const int step = (int)((rc4.x >> 15) & OWGS_AM_POS_MASK);
             const int pool = (rc4.x & OWGS_AM_POOL) ? 1 : 0;
@@ -908,6 +945,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
             if (hs >= 0) {
                 if (occ == 0) {
                     hdir[hs] = make_uint4((uint32_t)a, rc4.x, rc4.y, (uint32_t)slot);
+                    hflag[hs] = 0;  // walked in the first pass (f = 0)
                     atomicMax(&sc[SC_NHOT], hs + 1);
                 }
                 if (nxt == (int)OWGS_REC_NONEXT) hocc[hs] = occ;
@@ -922,14 +960,33 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
 
             int f = 0;
             PT(1);
+            // per-lane speculation, kept across the passes of the chunk: a maxConcurrent==1 lane that was known to
+            // fit stays exact (its earlier walk steps only lose capacity; the next validation re-checks its target
+            // against every lane before it), so only the lanes that were not known to fit speculate again
+            int kind = K_NONE, t = -1, ks = 0, cons = 0, s_t = 0, r = 0;
+            uint32_t cw = 0, cval = 0;
+            int cidx = -1;
+            bool keep = false;
             while (f < len) {
                 ++st_pass;
                 const bool act = pending && li >= f;
+                const bool spec = act && !keep;
                 // ------------------------------------------------ speculate (packing) against the state at f
-                int kind = K_NONE, t = -1, ks = 0, cons = 0, s_t = 0, r = 0;
-                uint32_t cw = 0, cval = 0;
-                int cidx = -1;
+                if (spec) {
+                    kind = K_NONE;
+                    t = -1;
+                    ks = 0;
+                    cons = 0;
+                    s_t = 0;
+                    r = 0;
+                    cw = 0;
+                    cval = 0;
+                    cidx = -1;
+                }
                 int ws = 0, wpos = 0, wcum = 0;  // long-walk resume state
+#ifdef OWGS_PROFILE
+                const u64 ts_beg = __builtin_amdgcn_s_memtime();
+#endif
                 // ------------------------------------------------ hot actions: one wave-cooperative walk per slot
                 // 64 walk steps per round: capacities, inclusive scan, then every rank q finds the step whose
                 // capacity range holds it (first rank of each step marked in LDS, prefix max over ranks)
@@ -937,6 +994,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                     for (int h = wave; h < nhot; h += OWGS_EW) {
                         const uint4 d = hdir[h];
                         if (d.z & (OWGS_AM_THROW | OWGS_AM_EMPTY)) continue;
+                        if (hflag[h] != f) continue;  // no lane of this action speculates in this pass
                         const int ha = (int)d.x;
                         const int hhome = (int)(d.y & OWGS_AM_POS_MASK), hstep = (int)((d.y >> 15) & OWGS_AM_POS_MASK);
                         const int hpool = (d.y & OWGS_AM_POOL) ? 1 : 0;
@@ -982,8 +1040,8 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                                     if (hmc == 1) {
                                         cap = cap_bf(pv, hmem, rmh);
                                     } else {
-                                        const int ci = ct_find(ctk, ct_key(id, hslot));
-                                        const uint32_t v = ci >= 0 ? ctv[ci] : 0u;
+                                        uint32_t v;
+                                        ct_findv(ct, ct_key(id, hslot), &v);
                                         cap = (int)(v & OWGS_CT_C_MASK) + min(cap_bf(pv, hmem, rmh) * hmc, CAPMAX);
                                     }
                                 }
@@ -1022,7 +1080,10 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                         }
                     }
                 }
-                if (act) {
+#ifdef OWGS_PROFILE
+                const u64 ts_hot = __builtin_amdgcn_s_memtime();
+#endif
+                if (spec) {
                     if (sempty) {
                         kind = K_NONE;
                     } else if (sthrow) {
@@ -1046,7 +1107,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                             int pos = mod_fast(home + s * step, n, __builtin_amdgcn_rcpf((float)n));
                             int cum = 0;
                             kind = K_LONG;
-                            PT(2);
+                            
                             if (maxc == 1 && A.pool_mode == 0) {
                                 // identity pools: pool position -> id is arithmetic, so the permit and usable-bit
                                 // reads of 4 walk steps are independent and issue together
@@ -1101,16 +1162,18 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                                         pos = pp;
                                     }
                                 }
-                                PT(3);
+                                
                             } else {
+                            ++st_glane;
 #pragma unroll 1
-                            for (int k = 0; k < KPROBE; ++k) {
+                            for (int k = 0; k < KPROBE_G; ++k) {
                                 if (s >= n) {  // every pool position probed: the n+2-probe walk fails (SCPB:417)
                                     kind = K_FALLBACK;
                                     break;
                                 }
                                 const int id = pool_id(E, pool, pos);
                                 ++st_probe;
+                                ++st_gprobe;
                                 if (id == OWGS_PW_BADID) {
                                     kind = K_THROW;
                                     break;
@@ -1121,8 +1184,8 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                                     if (maxc == 1) {
                                         cap = cap_of(pv, mem, rm);
                                     } else {
-                                        const int ci = ct_find(ctk, ct_key(id, slot));
-                                        const uint32_t v = ci >= 0 ? ctv[ci] : 0u;
+                                        uint32_t v;
+                                        const int ci = ct_findv(ct, ct_key(id, slot), &v);
                                         cap = (int)(v & OWGS_CT_C_MASK) + min(cap_of(pv, mem, rm) * maxc, CAPMAX);
                                         if (cum + cap > r) {
                                             cval = v;
@@ -1149,10 +1212,13 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                         }
                     }
                 }
-                PT(4);
+                
+#ifdef OWGS_PROFILE
+                const u64 ts_lane = __builtin_amdgcn_s_memtime();
+#endif
                 // ------------------------------------------------ long walks: wave-cooperative, 64 steps per round
                 if (!io) {
-                    u64 lm = __ballot(act && kind == K_LONG);
+                    u64 lm = __ballot(spec && kind == K_LONG);
                     while (lm) {
                         const int j = ffs64(lm);
                         lm &= lm - 1;
@@ -1189,8 +1255,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                                     if (cj == 1) {
                                         cap = cap_of(pv, mj, rmj);
                                     } else {
-                                        ci = ct_find(ctk, ct_key(id, slj));
-                                        v = ci >= 0 ? ctv[ci] : 0u;
+                                        ci = ct_findv(ct, ct_key(id, slj), &v);
                                         cap = (int)(v & OWGS_CT_C_MASK) + min(cap_of(pv, mj, rmj) * cj, CAPMAX);
                                     }
                                 }
@@ -1229,9 +1294,36 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                         }
                     }
                 }
-                PT(5);
-                lds_sync();  // hot tables written; every wave has finished reading P for its speculation
-                if (act && kind == K_HOT) {
+                
+#ifdef OWGS_PROFILE
+                if (!io && lane == 0) {
+                    const u64 ts_end = __builtin_amdgcn_s_memtime();
+                    spw[4 * wave] = (int)(ts_hot - ts_beg);
+                    spw[4 * wave + 1] = (int)(ts_lane - ts_hot);
+                    spw[4 * wave + 2] = (int)(ts_end - ts_lane);
+                }
+#endif
+                lds_sync();
+                PT(2);  // hot tables written; every wave has finished reading P for its speculation
+#ifdef OWGS_PROFILE
+                if (!io && lane == 0) {
+                    volatile int* wt = (volatile int*)(sc + SC_N);  // scratch after the scalars (profile build)
+                    (void)wt;
+                }
+                if (tid == 0) {
+                    int worst = 0, wsum = 0, wmax = -1;
+                    for (int w = 0; w < OWGS_EW; ++w) {
+                        const int tt = spw[4 * w] + spw[4 * w + 1] + spw[4 * w + 2];
+                        wsum += tt;
+                        if (tt > wmax) { wmax = tt; worst = w; }
+                    }
+                    pt_acc[6] += (u64)spw[4 * worst];       // worst wave: hot walks
+                    pt_acc[7] += (u64)spw[4 * worst + 1];   // worst wave: per-lane speculation
+                    pt_x[0] += (u64)spw[4 * worst + 2];     // worst wave: long walks
+                    pt_x[1] += (u64)wsum;                   // all waves: speculation total
+                }
+#endif
+                if (spec && kind == K_HOT) {
                     const uint2 e = htab[hs * HOT_RANKS + r];
                     kind = (int)((e.x >> 15) & 7u);
                     if (kind == K_TARGET) {
@@ -1239,15 +1331,14 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                         ks = (int)((e.x >> 18) & OWGS_RMASK);
                         s_t = (int)e.y;
                         if (maxc > 1) {
-                            cidx = ct_find(ctk, ct_key(t, slot));
-                            cval = cidx >= 0 ? ctv[cidx] : 0u;
+                            cidx = ct_findv(ct, ct_key(t, slot), &cval);
                         }
                     }
                 }
                 // ------------------------------------------------ forced fallback target (SCPB:417-424)
                 // (the explicit-seq and explicit-pool variants load from HBM; they are kept on their own paths so
                 // that their vmcnt waits never drain the decision stores of the common path)
-                if (act && kind == K_FALLBACK) {
+                if (spec && kind == K_FALLBACK) {
                     const int hc = pool ? A.hb : A.hm;
 #define OWGS_LAND(X)                                          \
     {                                                         \
@@ -1257,8 +1348,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
         } else {                                              \
             t = x_;                                           \
             if (maxc > 1) {                                   \
-                cidx = ct_find(ctk, ct_key(t, slot));         \
-                cval = cidx >= 0 ? ctv[cidx] : 0u;            \
+                cidx = ct_findv(ct, ct_key(t, slot), &cval); \
             }                                                 \
         }                                                     \
     }
@@ -1276,11 +1366,11 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
 #undef OWGS_LAND
                 }
                 const bool part = act && (kind == K_TARGET || kind == K_FALLBACK);
-                if (part) {
+                if (spec && part) {
                     const int c0v = (int)(cval & OWGS_CT_C_MASK);
                     if (maxc == 1) cons = mem;
                     else if (kind == K_FALLBACK) cons = c0v >= 1 ? 0 : mem;
-                    else cons = (ks < c0v) ? 0 : (((ks - c0v) % maxc) == 0 ? mem : 0);
+                    else cons = (ks < c0v) ? 0 : (mod_fast(ks - c0v, maxc, __builtin_amdgcn_rcpf((float)maxc)) == 0 ? mem : 0);
                 }
                 // ------------------------------------------------ bucket totals
                 // every lane tentatively takes its memory from its target's permits: after the barrier P[t] is the
@@ -1293,10 +1383,10 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                     atomicMax(&fst[bk], (uint32_t)(OWGS_WL - li));
                 }
                 if (act && maxc > 1 && kind == K_FALLBACK) atomicMin(&sc[SC_CFB + par], li);
-                if (!io) spt[li] = part ? t : -1;
+                if (own) spt[li] = part ? t : -1;
                 lds_sync();
                 // (fallback+buckets accrue to PT(6));
-                PT(6);
+                PT(3);
                 // ------------------------------------------------ validate: known to fit?
                 bool nf = false;
                 if (part) {
@@ -1317,7 +1407,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                     if (nfm && lane == ffs64(nfm)) atomicMin(&sc[SC_LMIN + par], li);
                 }
                 lds_sync();
-                // (validate accrues to PT(7));
+                PT(4);
                 // ------------------------------------------------ commit lanes [f, l)
                 int l = sc[SC_LMIN + par];
                 if (l <= f) {  // the frontier lane is always exact; never loop without progress
@@ -1355,17 +1445,19 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                         if (writer) {
                             const int c0v = (int)(cval & OWGS_CT_C_MASK), ops0 = (int)(cval >> OWGS_CT_C_BITS);
                             const int jn = kind == K_FALLBACK ? 1 : ks + 1;
-                            const int c1 = jn <= c0v ? c0v - jn : (maxc - 1 - ((jn - c0v - 1) % maxc));
+                            const int c1 = jn <= c0v ? c0v - jn
+                                                     : (maxc - 1 - mod_fast(jn - c0v - 1, maxc,
+                                                                            __builtin_amdgcn_rcpf((float)maxc)));
                             const int ops1 = ops0 + jn;
                             if (ops1 > OWGS_MAX_OPS) err |= OWGS_ERR_OPS;
                             int ix = cidx;
                             if (ix < 0) {
                                 int fresh = 0;
-                                ix = ct_insert(ctk, ct_key(t, slot), &fresh);
+                                ix = ct_insertv(ct, ct_key(t, slot), &fresh);
                                 if (fresh) atomicAdd(&sc[SC_USED], 1);
                             }
                             if (ix < 0) err |= OWGS_ERR_CTAB_FULL;
-                            else ctv[ix] = (uint32_t)c1 | ((uint32_t)ops1 << OWGS_CT_C_BITS);
+                            else ct[ix].y = (uint32_t)c1 | ((uint32_t)ops1 << OWGS_CT_C_BITS);
                         }
                     }
                     // a failed full walk at rank 0 proves every usable permit of the pool < mem from now on
@@ -1376,6 +1468,10 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                     if (li >= l && cons) atomicAdd(&P[t], cons);  // not committed: give the memory back
                     fst[bk] = 0u;
                 }
+                if (act && li >= l) {
+                    keep = !nf && (maxc == 1 || !part);
+                    if (!keep && hs >= 0) hflag[hs] = l;  // the action's hot table is needed in the next pass
+                }
                 if (io && l >= len) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk g+1 staged
                 if (tid == 0) {
                     sc[SC_NHOT] = 0;  // read at the chunk start, before this pass's barriers
@@ -1384,7 +1480,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                     if (l < len) ++st_stop;
                 }
                 lds_sync();
-                PT(7);
+                PT(5);
                 f = l;
                 par ^= 1;
             }
@@ -1400,19 +1496,25 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
     // ---------------------------------------------------------------- LDS -> state
     for (int i = tid; i < n_slots; i += OWGS_NT) A.permits[i] = P[i];
     for (int i = tid; i < OWGS_CTC; i += OWGS_NT) {
-        A.ct_keys[i] = ctk[i];
-        A.ct_vals[i] = ctv[i];
+        const uint2 e = ct[i];
+        A.ct_keys[i] = e.x;
+        A.ct_vals[i] = e.y;
     }
     if (err) atomicOr(A.err, (int)err);
     if (A.stats) {
         if (!io) {
             atomicAdd(&A.stats[OWGS_ST_PROBES], (u64)st_probe);
             atomicAdd(&A.stats[OWGS_ST_FALLBACKS], (u64)st_fb);
+            atomicAdd(&A.stats[6], (u64)st_gprobe);
+            atomicAdd(&A.stats[7], (u64)st_glane);
             if (lane == 0) atomicAdd(&A.stats[OWGS_ST_LONG], (u64)st_long);
         }
 #ifdef OWGS_PROFILE
-        if (!io && lane == 0)
+        if (tid == 0) {  // wave 0: marks sit right after barriers, so the intervals are the critical path
             for (int k = 0; k < 8; ++k) atomicAdd(&A.stats[8 + k], pt_acc[k]);
+            atomicAdd(&A.stats[6], pt_x[0]);
+            atomicAdd(&A.stats[7], pt_x[1]);
+        }
 #endif
         if (tid == 0) {
             atomicAdd(&A.stats[OWGS_ST_PASSES], (u64)st_pass);
