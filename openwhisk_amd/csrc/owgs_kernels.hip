@@ -756,8 +756,10 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
 
         // ============================================================ releases of batch b (SCPB:327-331)
         if (A.rel_off) {
-            // the engine's own stores (decisions, aggregated releases, release records) of earlier batches land
+            // the engine's own stores (decisions, aggregated releases, release records) of earlier batches land;
+            // the release counters share LDS with the publish-phase scratch: clear them
             if (!io) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            for (int ix = tid; ix < OWGS_CTC; ix += OWGS_NT) rc[ix] = 0u;
             lds_sync();
             if (!io) {
                 // maxConcurrent == 1: the releases of batch b were aggregated per invoker when the activations were

@@ -131,7 +131,7 @@ int main(int argc, char** argv) {
                 int64_t lim = end;
                 if (mode >= 2) {
                     // bucketed totals: lane fits if first in its bucket or bucket total <= P[t] at f
-                    int B = mode == 2 ? 4096 : 1 << 20;
+                    int B = (mode == 2 || mode == 6) ? 4096 : 1 << 20;
                     static vector<long> tot(1 << 20, 0); static vector<int64_t> firstl(1 << 20, -1);
                     vector<int> touched;
                     for (int64_t i = f; i < end; ++i) {
@@ -142,9 +142,17 @@ int main(int argc, char** argv) {
                         if (firstl[bk] < 0) { firstl[bk] = i; touched.push_back(bk); }
                         tot[bk] += cons;
                     }
+                    static vector<long> pre(1 << 20, 0);
                     for (int64_t i = f; i < end; ++i) {
                         int a = w.act[i]; int t = spec_t[i - c0]; int bk = (unsigned)(t * 2654435761u) % B; if (B == (1<<20)) bk = t;
                         bool kf = firstl[bk] == i || spec_fb[i - c0] || tot[bk] <= S.P[t];
+                        if (mode >= 5) {
+                            // exact per-invoker prefix: the lanes before i at t leave room for i
+                            long cons = w.mem[a];
+                            if (w.maxc[a] > 1) cons = spec_fb[i - c0] ? w.mem[a] : (spec_k[i - c0] == 0 ? w.mem[a] : 0);
+                            kf = spec_fb[i - c0] || pre[t] + cons <= S.P[t] || pre[t] == 0 && firstl[bk] == i;
+                            pre[t] += cons;
+                        }
                         bool ck = false;
                         if (w.maxc[a] > 1 && firstl[bk] != i && mode < 4) { if (kf) ck = true; kf = false; }
                         if (w.maxc[a] > 1 && mode >= 4) {
@@ -154,6 +162,7 @@ int main(int argc, char** argv) {
                         if (!kf) { lim = i; if (ck) ++stop_conc; else if (tot[bk] > S.P[t]) ++stop_ovf; break; }
                     }
                     for (int bk : touched) { tot[bk] = 0; firstl[bk] = -1; }
+                    if (mode >= 5) for (int64_t i = f; i < end; ++i) pre[spec_t[i - c0]] = 0;
                 }
                 // exact validation in stream order
                 int64_t i = f;
