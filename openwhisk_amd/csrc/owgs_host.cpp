@@ -133,6 +133,7 @@ struct owgs_ctx {
     DevBuf<u64> d_seq;
     DevBuf<int64_t> d_rel;
     DevBuf<uint4> d_rec;
+    DevBuf<uint16_t> d_lix;
     DevBuf<uint2> d_rel_rec, d_xmeta;
     // snapshot
     DevBuf<int32_t> s_permits;
@@ -304,13 +305,16 @@ static int run_prepass(owgs_ctx* c, OwgsEngineArgs& A, int32_t n_batches, const 
     p.act_slot = c->d_act_slot.p;
     p.xmeta = c->d_xmeta.p;
     p.xslot = c->d_xslot.p;
-    p.rec = c->d_rec.p;
     const int64_t max_chunks = n_act / OWGS_WL + n_batches;
+    HIPCHK(c, c->d_lix.reserve((size_t)std::max<int64_t>(max_chunks, 1) * OWGS_WL));
+    p.rec = c->d_rec.p;
+    p.lix = c->d_lix.p;
     HIPCHK(c, owgs_launch_prepass(&p, c->d_cstart.p, max_chunks, s));
     A.n_batches = n_batches;
     A.acq_off = acq_off;
     A.n_act = n_act;
     A.rec = c->d_rec.p;
+    A.lix = c->d_lix.p;
     return OWGS_OK;
 }
 
@@ -330,6 +334,7 @@ static int check_err_word(owgs_ctx* c) {
         if (e & OWGS_ERR_CTAB_FULL) return c->fail(OWGS_ENOMEM, "concurrency table full");
         if (e & OWGS_ERR_OPS) return c->fail(OWGS_ERANGE, "operationCount beyond the engine's range");
         if (e & OWGS_ERR_INTERNAL) return c->fail(OWGS_EDEVICE, "engine invariant violated");
+        if (e & OWGS_ERR_PERMITS) return c->fail(OWGS_ERANGE, "slot permits outside the engine's range [-2^29, 2^29) MB");
         return c->fail(OWGS_EINVAL, "stream releases an activation that holds no slot (or a permit overflow)");
     }
     return OWGS_OK;
@@ -421,6 +426,7 @@ void owgs_destroy(owgs_ctx* c) {
     c->d_seq.release();
     c->d_rel.release();
     c->d_rec.release();
+    c->d_lix.release();
     c->d_rel_rec.release();
     c->d_xmeta.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);

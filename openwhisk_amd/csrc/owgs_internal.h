@@ -18,7 +18,10 @@
 //   rec[n_act]              u32x4 per activation (see OWGS_REC_*): static walk/limit fields of its action plus the
 //                                 chunk-local ranks (occurrence of its action among earlier lanes of its chunk, the
 //                                 next lane of the same action, the nearest earlier lane of the same slot key with a
-//                                 different action).
+//                                 different action).  Inside a chunk the records are dealt by class: maxConcurrent
+//                                 == 1 lanes first, then the concurrent ones (stream order inside a class), so each
+//                                 engine wave runs one speculation path.
+//   lix[n_chunks][OWGS_WL]  u16  stream lane (index in the chunk) of each record position
 //   relx[n_act]             i32  where the activation's release goes: maxConcurrent == 1 -> the batch that releases it
 //                                 (the engine adds its memory to acc[batch][invoker] when it is decided);
 //                                 maxConcurrent > 1 -> its slot in the compacted concurrent-release list; -1 never
@@ -88,6 +91,12 @@
 #define OWGS_ERR_BAD_STREAM 2          // replay: a release without a matching acquire, or a permit overflow
 #define OWGS_ERR_OPS 4
 #define OWGS_ERR_INTERNAL 8             // engine invariant violated (a pass without progress)
+#define OWGS_ERR_PERMITS 16             // slot permits outside [-2^29, 2^29) MB (the LDS encoding's range)
+
+// LDS permits of identity pools carry the usable flag: an unusable invoker's permits are stored + OWGS_PENC, so one
+// LDS read gives both (usable permits < OWGS_PLIM <= unusable ones); HBM holds the plain values
+#define OWGS_PLIM (1 << 29)
+#define OWGS_PENC (1 << 30)
 
 // stats slots
 #define OWGS_ST_PASSES 0
@@ -117,7 +126,8 @@ struct OwgsEngineArgs {
     const int64_t* acq_off;      // [n_batches + 1]
     int64_t n_act;               // acq_off[n_batches]
     const int64_t* rel_off;      // [n_batches + 1] or null (no releases)
-    const uint4* rec;            // [n_act] pre-pass records
+    const uint4* rec;            // [n_act] pre-pass records, each chunk's lanes dealt by class (see lix)
+    const uint16_t* lix;         // [n_chunks][OWGS_WL] stream lane of each record position of the chunk
     const int32_t* relpos;       // [n_act] relx (see above), or null: no releases
     uint2* rel_rec;              // [n_crel] concurrent release records (compacted)
     const int32_t* crel_off;     // [n_batches + 1] first concurrent release of each batch
@@ -171,7 +181,8 @@ struct OwgsPrepassArgs {
     const int32_t* act_slot;     // [n_actions]
     const uint2* xmeta;          // explicit walks: [n_act]
     const int32_t* xslot;        // explicit walks: [n_act]
-    uint4* rec;                  // out [n_act]
+    uint4* rec;                  // out [n_act]: chunk lanes in class order (maxConcurrent == 1 first)
+    uint16_t* lix;               // out [n_chunks][OWGS_WL]: stream lane of each position
 };
 
 struct OwgsRelposArgs {

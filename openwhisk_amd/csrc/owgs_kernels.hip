@@ -47,7 +47,7 @@ typedef unsigned long long u64;
 #define KPROBE 16  // walk steps a maxConcurrent==1 lane probes on its own before the wave-cooperative walk (x4)
 #endif
 #ifndef KPROBE_G
-#define KPROBE_G 16  // same for the general path (concurrency lookups per step)
+#define KPROBE_G 4  // same for the general path (concurrency lookups per step)
 #endif
 #define CAPMAX 1024  // capacities are clamped: a lane's rank is < OWGS_WL
 
@@ -63,6 +63,12 @@ typedef unsigned long long u64;
         pt_acc[k] += _t - pt_t;                      \
         pt_t = _t;                                   \
     }
+// a timestamp the compiler can neither merge with another nor move out of its branch
+__device__ __forceinline__ unsigned long long memtime_pinned() {
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
 #else
 #define PT_DECL
 #define PT(k)
@@ -76,14 +82,22 @@ typedef unsigned long long u64;
 #define SC_USED 6   // non-empty concurrency-table entries (live + deleted)
 #define SC_NLIVE 7  // table rebuild: live entries
 #define SC_NHOT 8   // multi-lane actions of the current chunk (hot slots claimed)
-#define SC_N (16 + 4 * OWGS_EW)
+#define SC_N (16 + 6 * OWGS_EW)
 
-// hot actions: every maxConcurrent==1 action with >= HOT_MIN lanes in a chunk gets a slot (assigned by the pre-pass);
-// per pass one wave walks its capacity prefix once and writes the target of each rank 0..HOT_RANKS-1 into the slot's
-// table, so the action's lanes do not walk one by one
+// hot actions: every action with >= HOT_MIN lanes in a chunk gets a slot (assigned by the pre-pass; a concurrent
+// action only when no lane of the chunk shares its fqn@version with another action); per pass one wave walks its
+// capacity prefix once and writes the target of each rank 0..HOT_RANKS-1 into the slot's table, so the action's
+// lanes do not walk one by one.  The rec "ext" field holds the slot (maxConcurrent == 1: slot or OWGS_REC_NOHOT;
+// maxConcurrent > 1: pk1 + 1 <= OWGS_WL, or HOT_CONC + slot)
 #define NHOT 16
 #define HOT_RANKS 64
 #define HOT_MIN 6
+#define HOT_CONC 0x3E0
+#ifndef HOT_CONC_ON
+#define HOT_CONC_ON 0  // concurrent hot tables: measured slower (their walks re-run every pass), kept as an option
+#endif
+static_assert(OWGS_WL < HOT_CONC, "pk1 and the concurrent hot marker share the 10-bit ext field");
+static_assert(OWGS_WL % 128 == 0, "the I/O wave stages whole dwords of 2-byte lane indices");
 
 // ------------------------------------------------------------------------------------------------ helpers
 __device__ __forceinline__ u64 splitmix64(u64 x) {
@@ -151,9 +165,15 @@ __device__ __forceinline__ uint32_t ct_hash(uint32_t k) {
 __device__ __forceinline__ uint32_t ct_key(int inv, int slot) {
     return (uint32_t)(inv + 1) | ((uint32_t)slot << OWGS_CT_SLOT_SHIFT);
 }
-// concurrency table (LDS or HBM image): index of key or -1; deleted entries are skipped, empty ends the chain
+// Concurrency table (LDS or HBM image): linear probing from a 4-entry-aligned home, so the engine reads a key's
+// first 4 candidate entries with two ds_read_b128 (bucketized linear probing).  Deleted entries are skipped, an empty
+// entry ends the chain.
+#define CT_BLK 4
+__device__ __forceinline__ uint32_t ct_home(uint32_t key) {
+    return (ct_hash(key) & (OWGS_CTC / CT_BLK - 1)) * CT_BLK;
+}
 __device__ __forceinline__ int ct_find(const uint32_t* ctk, uint32_t key) {
-    uint32_t h = ct_hash(key) & (OWGS_CTC - 1);
+    uint32_t h = ct_home(key);
     for (int p = 0; p < OWGS_CTC; ++p) {
         const uint32_t k = ctk[h];
         if (k == key) return (int)h;
@@ -165,7 +185,7 @@ __device__ __forceinline__ int ct_find(const uint32_t* ctk, uint32_t key) {
 // insert a key known to be absent: claim the first empty or deleted entry of its chain (concurrent inserters of
 // different keys race by CAS)
 __device__ __forceinline__ int ct_insert(uint32_t* ctk, uint32_t key, int* fresh) {
-    uint32_t h = ct_hash(key) & (OWGS_CTC - 1);
+    uint32_t h = ct_home(key);
     for (int p = 0; p < OWGS_CTC;) {
         const uint32_t k = ctk[h];
         if (k == 0 || k == OWGS_CT_TOMB) {
@@ -181,23 +201,38 @@ __device__ __forceinline__ int ct_insert(uint32_t* ctk, uint32_t key, int* fresh
     return -1;
 }
 
-// interleaved {key, value} table (engine LDS): one ds_read_b64 per probe returns both
-__device__ __forceinline__ int ct_findv(const uint2* ct, uint32_t key, uint32_t* val) {
-    uint32_t h = ct_hash(key) & (OWGS_CTC - 1);
-    for (int p = 0; p < OWGS_CTC; ++p) {
-        const uint2 e = ct[h];
-        if (e.x == key) {
-            *val = e.y;
-            return (int)h;
-        }
-        if (e.x == 0) break;
-        h = (h + 1) & (OWGS_CTC - 1);
+// interleaved {key, value} table (engine LDS).  One aligned block of 4 entries: 1 = key found (*val, *idx),
+// 0 = an empty entry ends the chain, 2 = the chain continues in the next block.
+__device__ __forceinline__ int ct_block(uint4 e01, uint4 e23, uint32_t key, uint32_t h, uint32_t* val, int* idx) {
+    // branch-free: a key of the chain always sits before the chain's first empty entry
+    const bool h0 = e01.x == key, h1 = e01.z == key, h2 = e23.x == key, h3 = e23.z == key;
+    const bool z = e01.x == 0u || e01.z == 0u || e23.x == 0u || e23.z == 0u;
+    const bool hit = h0 || h1 || h2 || h3;
+    const uint32_t v = h0 ? e01.y : h1 ? e01.w : h2 ? e23.y : e23.w;
+    const int k = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
+    *val = hit ? v : 0u;
+    *idx = hit ? (int)h + k : -1;
+    return hit ? 1 : (z ? 0 : 2);
+}
+// lookup from block h (a home, or the block after one that did not end the chain); index or -1, *val (0 if absent)
+__device__ __forceinline__ int ct_findv_from(const uint2* ct, uint32_t key, uint32_t h, uint32_t* val) {
+    int idx = -1;
+    *val = 0u;
+    for (int p = 0; p < OWGS_CTC / CT_BLK; ++p) {
+        const uint4 e01 = *(const uint4*)&ct[h];
+        const uint4 e23 = *(const uint4*)&ct[h + 2];
+        const int st = ct_block(e01, e23, key, h, val, &idx);
+        if (st != 2) return st == 1 ? idx : -1;
+        h = (h + CT_BLK) & (OWGS_CTC - 1);
     }
     *val = 0u;
     return -1;
 }
+__device__ __forceinline__ int ct_findv(const uint2* ct, uint32_t key, uint32_t* val) {
+    return ct_findv_from(ct, key, ct_home(key), val);
+}
 __device__ __forceinline__ int ct_insertv(uint2* ct, uint32_t key, int* fresh) {
-    uint32_t h = ct_hash(key) & (OWGS_CTC - 1);
+    uint32_t h = ct_home(key);
     for (int p = 0; p < OWGS_CTC;) {
         const uint32_t k = ct[h].x;
         if (k == 0 || k == OWGS_CT_TOMB) {
@@ -265,7 +300,7 @@ __device__ __forceinline__ void lds_dma4(const void* gsrc, uint32_t lds_dst) {
 
 // ------------------------------------------------------------------------------------------------ LDS layout
 struct OwgsLayout {
-    uint32_t P, pool, pc, cur, ct, stgA, stgX, fst, spt, hdir, htab, hscr, rc, sc, uni, uni_bytes, total;
+    uint32_t P, pool, pc, cur, ct, stgA, stgX, stgL, fst, spt, hdir, htab, hscr, rc, sc, uni, uni_bytes, total;
 };
 
 __host__ __device__ inline OwgsLayout owgs_layout(int n_slots, int pool_mode, int n_ids, int nm, int nb, int n_actions) {
@@ -287,6 +322,8 @@ __host__ __device__ inline OwgsLayout owgs_layout(int n_slots, int pool_mode, in
     o += 2u * OWGS_WL * 16u;
     L.stgX = o;
     o += 2u * OWGS_WL * 4u;
+    L.stgL = o;
+    o += 2u * OWGS_WL * 2u;
     L.sc = o;
     o += 4u * SC_N;
     // phase union: acquire phase {fst, spt, hot directory, hot rank tables, hot scratch} / release phase {rc}
@@ -395,7 +432,7 @@ __global__ __launch_bounds__(64) void owgs_chunks_kernel(const int64_t* acq_off,
 // one workgroup per chunk: occ (earlier lanes of the same action), next lane of the same action, nearest earlier
 // lane with the same slot key and a different action (shared fqn@version), packed with the action meta
 __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A) {
-    __shared__ int32_t s_a[OWGS_WL], s_s[OWGS_WL];
+    __shared__ int32_t s_a[OWGS_WL], s_s[OWGS_WL], s_p[OWGS_WL];
     const int g = blockIdx.x;
     if (g >= A.cstart[A.n_batches]) return;
     int lo = 0, hi = A.n_batches - 1;  // last batch with cstart[b] <= g
@@ -440,27 +477,43 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
             }
         }
     }
-    // hot actions (maxConcurrent == 1, >= HOT_MIN lanes in the chunk): slots in order of their first lane
-    const bool q = t < len && A.act && cnt >= HOT_MIN && ((meta.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK) == 1 &&
-                   !(meta.y & (OWGS_AM_THROW | OWGS_AM_EMPTY));
+    // hot actions (>= HOT_MIN lanes in the chunk; concurrent ones only without a shared-key lane): slots in order of
+    // their first lane
+    const int mc = (int)((meta.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
+    s_p[t] = pk1;
+    __syncthreads();
+    bool shared = false;
+    if (t < len && mc > 1)
+        for (int j = 0; j < len; ++j) shared = shared || (s_a[j] == aid && s_p[j] != 0);
+    const bool q = t < len && A.act && cnt >= HOT_MIN && !shared && !(meta.y & (OWGS_AM_THROW | OWGS_AM_EMPTY)) &&
+                   (mc == 1 || HOT_CONC_ON);
     __syncthreads();
     s_s[t] = (q && occ == 0) ? 1 : 0;  // qualifying leaders
+    s_p[t] = (t < len && mc > 1) ? 1 : 0;  // class: concurrent
     __syncthreads();
     if (t >= len) return;
+    // record position: maxConcurrent == 1 lanes first, then the concurrent ones, stream order inside a class
+    int cb = 0, ctot = 0;
+    for (int j = 0; j < len; ++j) {
+        ctot += s_p[j];
+        cb += j < t ? s_p[j] : 0;
+    }
+    const int pos = mc > 1 ? (len - ctot) + cb : t - cb;
     int hs = OWGS_REC_NOHOT;
     if (q) {
         int k = 0;
         for (int j = 0; j < lead; ++j) k += s_s[j];
         if (k < NHOT) hs = k;
     }
-    const int ext = ((meta.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK) > 1 ? pk1 : hs;  // 10 bits
+    const int ext = mc > 1 ? (hs != OWGS_REC_NOHOT ? HOT_CONC + hs : pk1) : hs;  // 10 bits
     const uint32_t an = A.act ? (uint32_t)a : OWGS_REC_NOACT;
     uint4 r;
     r.x = meta.x;
     r.y = meta.y | OWGS_AM_VALID;
     r.z = an | ((uint32_t)occ << 17) | ((uint32_t)(ext & 31) << 27);
     r.w = (uint32_t)slot | ((uint32_t)next << 17) | ((uint32_t)(ext >> 5) << 27);
-    A.rec[c0 + t] = r;
+    A.rec[c0 + pos] = r;
+    A.lix[(int64_t)g * OWGS_WL + pos] = (uint16_t)t;
 }
 
 // Release bookkeeping.  relx[aid] = release batch (maxConcurrent == 1: aggregated into acc[batch][invoker]) or the
@@ -594,13 +647,18 @@ struct EngineCtx {
     int pool_mode, n_ids, nm, nb;
 };
 
-// pool position -> invoker id (>= 0, usable), OWGS_PW_UNUSABLE or OWGS_PW_BADID
-__device__ __forceinline__ int pool_id(const EngineCtx& E, int pool, int pos) {
+// pool position -> invoker id (>= 0, usable), OWGS_PW_UNUSABLE or OWGS_PW_BADID, and the id's permits (one LDS read
+// for identity pools: the usable flag is folded into the permits)
+__device__ __forceinline__ int pool_probe(const EngineCtx& E, int pool, int pos, int* pv) {
     if (E.pool_mode == 0) {
         const int id = pool ? E.n_ids - E.nb + pos : pos;
-        return ((E.ub[id >> 5] >> (id & 31)) & 1u) ? id : OWGS_PW_UNUSABLE;
+        const int v = E.P[id];
+        *pv = v;
+        return v < OWGS_PLIM ? id : OWGS_PW_UNUSABLE;
     }
-    return (int)E.pw[pool ? E.nm + pos : pos];
+    const int id = (int)E.pw[pool ? E.nm + pos : pos];
+    *pv = id >= 0 ? E.P[id] : 0;
+    return id;
 }
 
 // usable ids of the identity pool [lo, lo + n) before id x
@@ -657,10 +715,12 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
     int32_t* hflag = (int32_t*)(L + Y.hdir + 20u * NHOT);
     uint2* htab = (uint2*)(L + Y.htab);
     int32_t* hscr = (int32_t*)(L + Y.hscr);
+    const uint16_t* stgL = (const uint16_t*)(L + Y.stgL);
     uint32_t* rc = (uint32_t*)(L + Y.rc);
     int32_t* sc = (int32_t*)(L + Y.sc);
 #ifdef OWGS_PROFILE
-    int* spw = sc + 16;  // per-wave speculation timings (SC_N leaves room in every build)
+    int* spw = sc + 16;
+    int* pfw = sc + 16 + 4 * OWGS_EW;  // per-wave speculation timings (SC_N leaves room in every build)
 #endif
 
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -669,7 +729,13 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
     const int words = (A.n_ids + 31) >> 5;
 
     // ---------------------------------------------------------------- state -> LDS
-    for (int i = tid; i < n_slots; i += OWGS_NT) P[i] = A.permits[i];
+    uint32_t err = 0;
+    for (int i = tid; i < n_slots; i += OWGS_NT) {
+        const int v = A.permits[i];
+        if (v < -OWGS_PLIM || v >= OWGS_PLIM) err |= OWGS_ERR_PERMITS;
+        const bool unusable = A.pool_mode == 0 && i < A.n_ids && !((A.usable[i >> 5] >> (i & 31)) & 1u);
+        P[i] = unusable ? v + OWGS_PENC : v;
+    }
     if (A.pool_mode == 0) {
         for (int i = tid; i < words; i += OWGS_NT) ub[i] = A.usable[i];
     } else {
@@ -709,7 +775,6 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
     E.nb = nb;
 
     uint32_t st_pass = 0, st_probe = 0, st_fb = 0, st_long = 0, st_chunk = 0, st_stop = 0, st_gprobe = 0, st_glane = 0;
-    uint32_t err = 0;
     PT_DECL
 
     // ---------------------------------------------------------------- I/O wave: chunk prefetch pipeline
@@ -718,7 +783,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
     // drains them (vmcnt(0)) before the last barrier of chunk g.
     int io_b = 0;
     int64_t io_c0 = 0;
-    const uint32_t stgA_lds = (uint32_t)(size_t)stgA, stgX_lds = (uint32_t)(size_t)stgX;
+    const uint32_t stgA_lds = (uint32_t)(size_t)stgA, stgX_lds = (uint32_t)(size_t)stgX, stgL_lds = (uint32_t)(size_t)stgL;
     // advance (io_b, io_c0) to the next chunk; returns false at the end of the stream
     auto io_locate = [&](int& bb, int64_t& c0) -> bool {
         while (bb < A.n_batches && c0 >= A.acq_off[bb + 1]) {
@@ -728,8 +793,12 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
         return bb < A.n_batches;
     };
     // lanes past the end of the stream re-read its last record: the engine ignores lanes >= the chunk length
-    auto io_dma = [&](int64_t c0, int buf) {
+    auto io_dma = [&](int64_t c0, int buf, int gc) {
         const int64_t last = A.n_act - 1;
+        const uint32_t* lx = (const uint32_t*)(A.lix + (int64_t)gc * OWGS_WL);
+#pragma unroll
+        for (int k = 0; k < OWGS_WL / 128; ++k)  // 2-byte lane indices: OWGS_WL / 2 dwords
+            lds_dma4(&lx[lane + 64 * k], __builtin_amdgcn_readfirstlane(stgL_lds + (uint32_t)(buf * OWGS_WL * 2 + 256 * k)));
 #pragma unroll
         for (int k = 0; k < OWGS_WL / 64; ++k) {
             int64_t i = c0 + lane + 64 * k;
@@ -742,7 +811,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
     if (io) {
         if (A.n_batches > 0) io_c0 = A.acq_off[0];
         if (io_locate(io_b, io_c0)) {
-            io_dma(io_c0, 0);
+            io_dma(io_c0, 0, 0);
             io_c0 += OWGS_WL;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -768,9 +837,12 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 for (int i = tid; i < n_slots; i += OWGS_ENT) {
                     const int d = __hip_atomic_load(&row[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (d) {
-                        const long long s = (long long)P[i] + d;
+                        const int v = P[i];
+                        const int enc = v >= OWGS_PLIM ? OWGS_PENC : 0;
+                        const long long s = (long long)(v - enc) + d;
                         if (s > 0x7FFFFFFFLL) err |= OWGS_ERR_BAD_STREAM;  // FS:48-50 would throw
-                        else P[i] = (int32_t)s;
+                        else if (s >= OWGS_PLIM) err |= OWGS_ERR_PERMITS;
+                        else P[i] = (int32_t)s + enc;
                     }
                 }
                 // concurrent releases: RS.release(1, true) per release (NS:98-113); the count per entry decides the
@@ -809,8 +881,9 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                             continue;
                         }
                         if (mod_fast(c0 + (int)q + 1, R, __builtin_amdgcn_rcpf((float)R)) == 0) {  // RS:50-52
-                            const int old = atomicAdd(&P[inv], mem);
-                            if (old > 0x7FFFFFFF - mem) err |= OWGS_ERR_BAD_STREAM;
+                            int old = atomicAdd(&P[inv], mem);
+                            old -= old >= OWGS_PLIM ? OWGS_PENC : 0;
+                            if (old >= OWGS_PLIM - mem) err |= OWGS_ERR_PERMITS;
                         }
                     }
                 }
@@ -912,13 +985,16 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 lds_sync();
             }
             ++st_chunk;
-            // ---- lane record
+            // ---- lane record: the pre-pass dealt the chunk's records by class (maxConcurrent == 1 first), so a wave
+            // mostly runs one speculation path; li = the lane's index in the stream order of the chunk
             const bool own = !io && lane < OWGS_LPW;  // this thread holds an activation of the chunk
-            const int li = own ? wave * OWGS_LPW + lane : OWGS_WL;
+            const int sl = wave * OWGS_LPW + lane;    // record position
+            const bool held = own && sl < len;
+            const int li = held ? (int)stgL[(g & 1) * OWGS_WL + sl] : OWGS_WL;
             uint4 rc4 = make_uint4(0, 0, 0, 0);
             int relx = -1;
-            if (own) {
-                rc4 = stgA[(g & 1) * OWGS_WL + li];
+            if (held) {
+                rc4 = stgA[(g & 1) * OWGS_WL + sl];
                 relx = A.relpos ? stgX[(g & 1) * OWGS_WL + li] : -1;
             }
             const bool valid = own && (rc4.y & OWGS_AM_VALID) && li < len;
@@ -935,7 +1011,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
             const int slot = (int)(rc4.w & 0x1FFFFu);
             const int nxt = (int)((rc4.w >> 17) & OWGS_REC_NONEXT);
             const int ext = (int)((rc4.z >> 27) | ((rc4.w >> 27) << 5));  // pk1 (maxConc > 1) or hot slot
-            const int pk1 = maxc > 1 ? ext : 0;
+            const int pk1 = (maxc > 1 && ext < HOT_CONC) ? ext : 0;
             const int n = pool ? nb : nm;
             const float rm = __builtin_amdgcn_rcpf((float)(mem > 0 ? mem : 1));
             const int64_t i = c0 + li;
@@ -943,7 +1019,8 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
 
             // ---- hot actions (slots assigned by the pre-pass): the first lane publishes the walk, the last lane
             // the largest occurrence index
-            const int hs = (valid && maxc == 1 && ext < NHOT && !(A.opts & 1)) ? ext : -1;
+            const int hsx = maxc > 1 ? ext - HOT_CONC : ext;  // hot slot or out of [0, NHOT)
+            const int hs = (valid && hsx >= 0 && hsx < NHOT && !(A.opts & 1)) ? hsx : -1;
             if (hs >= 0) {
                 if (occ == 0) {
                     hdir[hs] = make_uint4((uint32_t)a, rc4.x, rc4.y, (uint32_t)slot);
@@ -956,7 +1033,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
             const int nhot = sc[SC_NHOT];
             // ---- I/O wave: stream chunk g+1 into the other staging buffer
             if (io && io_locate(io_b, io_c0)) {
-                io_dma(io_c0, (g + 1) & 1);
+                io_dma(io_c0, (g + 1) & 1, g + 1);
                 io_c0 += OWGS_WL;
             }
 
@@ -988,6 +1065,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 int ws = 0, wpos = 0, wcum = 0;  // long-walk resume state
 #ifdef OWGS_PROFILE
                 const u64 ts_beg = __builtin_amdgcn_s_memtime();
+                int pf_fast = 0, pf_gen = 0;
 #endif
                 // ------------------------------------------------ hot actions: one wave-cooperative walk per slot
                 // 64 walk steps per round: capacities, inclusive scan, then every rank q finds the step whose
@@ -1034,11 +1112,11 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                             int id = OWGS_PW_UNUSABLE, cap = 0;
                             bool bad = false;
                             if (sk < hn) {
-                                id = pool_id(E, hpool, pp);
+                                int pv;
+                                id = pool_probe(E, hpool, pp, &pv);
                                 if (id == OWGS_PW_BADID) {
                                     bad = true;
                                 } else if (id >= 0) {
-                                    const int pv = P[id];
                                     if (hmc == 1) {
                                         cap = cap_bf(pv, hmem, rmh);
                                     } else {
@@ -1111,6 +1189,9 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                             kind = K_LONG;
                             
                             if (maxc == 1 && A.pool_mode == 0) {
+#ifdef OWGS_PROFILE
+                                const u64 tf0 = memtime_pinned();
+#endif
                                 // identity pools: pool position -> id is arithmetic, so the permit and usable-bit
                                 // reads of 4 walk steps are independent and issue together
                                 const int base = pool ? A.n_ids - nb : 0;
@@ -1119,27 +1200,23 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                                 for (int g4 = 0; g4 < KPROBE / 4; ++g4) {
                                     if (done) break;
                                     int ps[4], pv[4];
-                                    uint32_t wd[4];
                                     int pp = pos;
 #pragma unroll
                                     for (int k = 0; k < 4; ++k) {
                                         ps[k] = pp;
-                                        const int id = base + pp;
-                                        pv[k] = P[id];
-                                        wd[k] = ub[id >> 5];
+                                        pv[k] = P[base + pp];  // usable flag folded in (OWGS_PENC)
                                         pp += step;
                                         pp -= pp >= n ? n : 0;
                                     }
 #pragma unroll
-                                    for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(pv[k]), "+v"(wd[k]));  // 8 reads in flight
+                                    for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(pv[k]));  // 4 reads in flight
                                     // branch-free scan of the 4 steps: first step whose cumulative capacity exceeds
                                     // the rank (hit), or the end of the walk (s + k == n: every position probed)
                                     int hit = 4, kc = cum, hc = cum;
                                     bool ended = false;
 #pragma unroll
                                     for (int k = 0; k < 4; ++k) {
-                                        const int id = base + ps[k];
-                                        const int cap = cap_bf(pv[k], mem, rm) & (0 - (int)((wd[k] >> (id & 31)) & 1u));
+                                        const int cap = pv[k] < OWGS_PLIM ? cap_bf(pv[k], mem, rm) : 0;
                                         const bool open = hit == 4 && !ended;
                                         const bool fin = open && s + k >= n;
                                         const bool h = open && !fin && kc + cap > r;
@@ -1164,16 +1241,97 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                                         pos = pp;
                                     }
                                 }
-                                
+#ifdef OWGS_PROFILE
+                                pf_fast = (int)(memtime_pinned() - tf0);
+#endif
                             } else {
+#ifdef OWGS_PROFILE
+                            const u64 tg0 = memtime_pinned();
+#endif
                             ++st_glane;
+                            if (maxc > 1 && A.pool_mode == 0) {
+                                // identity pools, concurrent action: the permits and the first concurrency-table entry
+                                // of 4 walk steps issue together; a key whose first entry holds another key follows
+                                // its chain afterwards
+                                const int base = pool ? A.n_ids - nb : 0;
+                                bool done = false;
+#pragma unroll 1
+                                for (int g4 = 0; g4 < KPROBE_G / 4; ++g4) {
+                                    if (done) break;
+                                    int ps[4], pv[4];
+                                    uint32_t hx[4];
+                                    uint4 ea[4], eb[4];
+                                    int pp = pos;
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k) {
+                                        ps[k] = pp;
+                                        pv[k] = P[base + pp];
+                                        hx[k] = ct_home(ct_key(base + pp, slot));
+                                        ea[k] = *(const uint4*)&ct[hx[k]];
+                                        eb[k] = *(const uint4*)&ct[hx[k] + 2];
+                                        pp += step;
+                                        pp -= pp >= n ? n : 0;
+                                    }
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(pv[k]), "+v"(ea[k].x), "+v"(eb[k].x));
+                                    int hit = 4, kc = cum, hc = cum, hi = -1;
+                                    uint32_t hv = 0;
+                                    bool ended = false;
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k) {
+                                        const bool open = hit == 4 && !ended;
+                                        const bool fin = open && s + k >= n;
+                                        const uint32_t key = ct_key(base + ps[k], slot);
+                                        uint32_t v = 0;
+                                        int ci = -1;
+                                        const int bst = ct_block(ea[k], eb[k], key, hx[k], &v, &ci);
+                                        if (bst == 2 && open && !fin) {
+                                            ci = ct_findv_from(ct, key, (hx[k] + CT_BLK) & (OWGS_CTC - 1), &v);
+#ifdef OWGS_COUNT_CHAINS
+                                            st_glane += 1u << 16;
+#endif
+                                        }
+                                        const int cap = pv[k] < OWGS_PLIM
+                                                            ? (int)(v & OWGS_CT_C_MASK) + min(cap_bf(pv[k], mem, rm) * maxc, CAPMAX)
+                                                            : 0;
+                                        const bool h = open && !fin && kc + cap > r;
+                                        ended = ended || fin;
+                                        if (h) {
+                                            hit = k;
+                                            hc = kc;
+                                            hv = v;
+                                            hi = ci;
+                                        }
+                                        kc += (open && !fin && !h) ? cap : 0;
+                                    }
+                                    st_probe += 4;
+                                    st_gprobe += 4;
+                                    if (hit < 4) {
+                                        kind = K_TARGET;
+                                        t = base + (hit == 0 ? ps[0] : hit == 1 ? ps[1] : hit == 2 ? ps[2] : ps[3]);
+                                        ks = r - hc;
+                                        s_t = s + hit;
+                                        cval = hv;
+                                        cidx = hi;
+                                        done = true;
+                                    } else if (ended) {
+                                        kind = K_FALLBACK;  // every pool position probed (SCPB:417)
+                                        done = true;
+                                    } else {
+                                        cum = kc;
+                                        s += 4;
+                                        pos = pp;
+                                    }
+                                }
+                            } else {
 #pragma unroll 1
                             for (int k = 0; k < KPROBE_G; ++k) {
                                 if (s >= n) {  // every pool position probed: the n+2-probe walk fails (SCPB:417)
                                     kind = K_FALLBACK;
                                     break;
                                 }
-                                const int id = pool_id(E, pool, pos);
+                                int pv;
+                                const int id = pool_probe(E, pool, pos, &pv);
                                 ++st_probe;
                                 ++st_gprobe;
                                 if (id == OWGS_PW_BADID) {
@@ -1181,7 +1339,6 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                                     break;
                                 }
                                 if (id >= 0) {
-                                    const int pv = P[id];
                                     int cap;
                                     if (maxc == 1) {
                                         cap = cap_of(pv, mem, rm);
@@ -1207,6 +1364,10 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                                 pos += step;
                                 if (pos >= n) pos -= n;
                             }
+                            }
+#ifdef OWGS_PROFILE
+                            pf_gen = (int)(memtime_pinned() - tg0);
+#endif
                             }
                             ws = s;
                             wpos = pos;
@@ -1249,11 +1410,11 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                             uint32_t v = 0;
                             bool bad = false;
                             if (sk < nn) {
-                                id = pool_id(E, pj, p);
+                                int pv;
+                                id = pool_probe(E, pj, p, &pv);
                                 if (id == OWGS_PW_BADID) {
                                     bad = true;
                                 } else if (id >= 0) {
-                                    const int pv = P[id];
                                     if (cj == 1) {
                                         cap = cap_of(pv, mj, rmj);
                                     } else {
@@ -1298,31 +1459,29 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 }
                 
 #ifdef OWGS_PROFILE
+                const int pf_fw = wave_max(pf_fast), pf_gw = wave_max(pf_gen);
                 if (!io && lane == 0) {
                     const u64 ts_end = __builtin_amdgcn_s_memtime();
                     spw[4 * wave] = (int)(ts_hot - ts_beg);
                     spw[4 * wave + 1] = (int)(ts_lane - ts_hot);
                     spw[4 * wave + 2] = (int)(ts_end - ts_lane);
+                    pfw[2 * wave] = pf_fw;
+                    pfw[2 * wave + 1] = pf_gw;
                 }
 #endif
                 lds_sync();
                 PT(2);  // hot tables written; every wave has finished reading P for its speculation
 #ifdef OWGS_PROFILE
-                if (!io && lane == 0) {
-                    volatile int* wt = (volatile int*)(sc + SC_N);  // scratch after the scalars (profile build)
-                    (void)wt;
-                }
                 if (tid == 0) {
-                    int worst = 0, wsum = 0, wmax = -1;
+                    int worst = 0, wmax = -1;
                     for (int w = 0; w < OWGS_EW; ++w) {
                         const int tt = spw[4 * w] + spw[4 * w + 1] + spw[4 * w + 2];
-                        wsum += tt;
                         if (tt > wmax) { wmax = tt; worst = w; }
                     }
                     pt_acc[6] += (u64)spw[4 * worst];       // worst wave: hot walks
                     pt_acc[7] += (u64)spw[4 * worst + 1];   // worst wave: per-lane speculation
-                    pt_x[0] += (u64)spw[4 * worst + 2];     // worst wave: long walks
-                    pt_x[1] += (u64)wsum;                   // all waves: speculation total
+                    pt_x[0] += (u64)pfw[2 * worst];         // worst wave: slowest maxConcurrent==1 per-lane walk
+                    pt_x[1] += (u64)pfw[2 * worst + 1];     // worst wave: slowest general per-lane walk
                 }
 #endif
                 if (spec && kind == K_HOT) {
@@ -1385,7 +1544,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                     atomicMax(&fst[bk], (uint32_t)(OWGS_WL - li));
                 }
                 if (act && maxc > 1 && kind == K_FALLBACK) atomicMin(&sc[SC_CFB + par], li);
-                if (own) spt[li] = part ? t : -1;
+                if (own && li < OWGS_WL) spt[li] = part ? t : -1;
                 lds_sync();
                 // (fallback+buckets accrue to PT(6));
                 PT(3);
@@ -1405,8 +1564,11 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                     nf = !kf;
                 }
                 if (!io) {
-                    const u64 nfm = __ballot(nf);
-                    if (nfm && lane == ffs64(nfm)) atomicMin(&sc[SC_LMIN + par], li);
+                    // (the lanes of a wave are not in stream order) the wave's smallest such lane
+                    if (__ballot(nf)) {
+                        const int lm = -wave_max(nf ? -li : -OWGS_WL);
+                        if (lane == 0) atomicMin(&sc[SC_LMIN + par], lm);
+                    }
                 }
                 lds_sync();
                 PT(4);
@@ -1496,7 +1658,10 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
     }
 
     // ---------------------------------------------------------------- LDS -> state
-    for (int i = tid; i < n_slots; i += OWGS_NT) A.permits[i] = P[i];
+    for (int i = tid; i < n_slots; i += OWGS_NT) {
+        const int v = P[i];
+        A.permits[i] = v >= OWGS_PLIM ? v - OWGS_PENC : v;
+    }
     for (int i = tid; i < OWGS_CTC; i += OWGS_NT) {
         const uint2 e = ct[i];
         A.ct_keys[i] = e.x;
@@ -1507,8 +1672,10 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
         if (!io) {
             atomicAdd(&A.stats[OWGS_ST_PROBES], (u64)st_probe);
             atomicAdd(&A.stats[OWGS_ST_FALLBACKS], (u64)st_fb);
+#ifndef OWGS_PROFILE
             atomicAdd(&A.stats[6], (u64)st_gprobe);
             atomicAdd(&A.stats[7], (u64)st_glane);
+#endif
             if (lane == 0) atomicAdd(&A.stats[OWGS_ST_LONG], (u64)st_long);
         }
 #ifdef OWGS_PROFILE

@@ -19,13 +19,18 @@ for name in configs:
     b.register_actions(w.actions)
     b.snapshot()
     b.replay(w.stream)
-    b.restore()
-    t = time.perf_counter()
-    b.replay(w.stream)
-    dt = time.perf_counter() - t
+    reps = int(os.environ.get("REPS", "5"))
+    ts = []
+    for _ in range(reps):  # min over repeats: single replays vary by a few percent
+        b.restore()
+        t = time.perf_counter()
+        b.replay(w.stream)
+        ts.append(time.perf_counter() - t)
+    dt = min(ts)
     st = b.stats()
     cyc = st.pop("cycles", {})
     tot = sum(cyc.values()) or 1
-    print(f"{name}: n={w.n_activations} batches={w.stream.n_batches} {dt*1e3:.1f} ms  {w.n_activations/dt:.3g}/s  {st}")
+    print(f"{name}: n={w.n_activations} batches={w.stream.n_batches} {dt*1e3:.1f} ms (min of {reps}; median "
+          f"{sorted(ts)[len(ts) // 2]*1e3:.1f})  {w.n_activations/dt:.3g}/s  {st}")
     print("   cycles/activation:", {k: round(v / w.n_activations, 1) for k, v in cyc.items()},
           "share:", {k: round(v / tot, 3) for k, v in cyc.items()})
