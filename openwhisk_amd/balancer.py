@@ -258,6 +258,6 @@ class GpuShardingContainerPoolBalancer:
             names = ["batch", "chunk_start", "speculate", "tables_buckets", "validate", "commit", "worst_hot", "worst_lane"]
             d["cycles"] = {k: out[8 + i] for i, k in enumerate(names)}
             # profile build: slots 6/7 hold the worst wave's slowest per-lane walks instead of the probe counters
-            d["cycles"]["worst_fast_walk"] = d.pop("general_probes")
+            d["cycles"]["worst_prelude"] = d.pop("general_probes")
             d["cycles"]["worst_general_walk"] = d.pop("general_lanes")
         return d

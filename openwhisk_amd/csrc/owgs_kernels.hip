@@ -53,22 +53,22 @@ typedef unsigned long long u64;
 
 // diagnostic build (-DOWGS_PROFILE, libowgs_prof.so): s_memtime cycle accounting per engine phase into stats[8..15]
 #ifdef OWGS_PROFILE
-#define PT_DECL                 \
-    u64 pt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
-    u64 pt_x[2] = {0, 0};                     \
-    u64 pt_t = __builtin_amdgcn_s_memtime();
-#define PT(k)                                        \
-    {                                                \
-        const u64 _t = __builtin_amdgcn_s_memtime(); \
-        pt_acc[k] += _t - pt_t;                      \
-        pt_t = _t;                                   \
-    }
 // a timestamp the compiler can neither merge with another nor move out of its branch
 __device__ __forceinline__ unsigned long long memtime_pinned() {
     unsigned long long t;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
     return t;
 }
+#define PT_DECL                 \
+    u64 pt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
+    u64 pt_x[2] = {0, 0};                     \
+    u64 pt_t = memtime_pinned();
+#define PT(k)                                        \
+    {                                                \
+        const u64 _t = memtime_pinned(); \
+        pt_acc[k] += _t - pt_t;                      \
+        pt_t = _t;                                   \
+    }
 #else
 #define PT_DECL
 #define PT(k)
@@ -489,22 +489,32 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
                    (mc == 1 || HOT_CONC_ON);
     __syncthreads();
     s_s[t] = (q && occ == 0) ? 1 : 0;  // qualifying leaders
-    s_p[t] = (t < len && mc > 1) ? 1 : 0;  // class: concurrent
     __syncthreads();
-    if (t >= len) return;
-    // record position: maxConcurrent == 1 lanes first, then the concurrent ones, stream order inside a class
-    int cb = 0, ctot = 0;
-    for (int j = 0; j < len; ++j) {
-        ctot += s_p[j];
-        cb += j < t ? s_p[j] : 0;
-    }
-    const int pos = mc > 1 ? (len - ctot) + cb : t - cb;
     int hs = OWGS_REC_NOHOT;
     if (q) {
         int k = 0;
         for (int j = 0; j < lead; ++j) k += s_s[j];
         if (k < NHOT) hs = k;
     }
+    // record position by class: 0 = walks of maxConcurrent == 1 actions, 1 = no walk of its own (hot-table rank,
+    // throwing index, empty pool), 2 = concurrent walks; stream order inside a class.  A wave then mostly runs one
+    // speculation path, and the class-1 lanes sit between the two walking classes.
+    const int cls = (hs != OWGS_REC_NOHOT || (meta.y & (OWGS_AM_THROW | OWGS_AM_EMPTY))) ? 1 : (mc > 1 ? 2 : 0);
+    s_p[t] = t < len ? cls : 3;
+    __syncthreads();
+    if (t >= len) return;
+    int nb0 = 0, nb1 = 0, nb2 = 0, n0 = 0, n1 = 0;
+    for (int j = 0; j < len; ++j) {
+        const int cj = s_p[j];
+        n0 += cj == 0;
+        n1 += cj == 1;
+        if (j < t) {
+            nb0 += cj == 0;
+            nb1 += cj == 1;
+            nb2 += cj == 2;
+        }
+    }
+    const int pos = cls == 0 ? nb0 : cls == 1 ? n0 + nb1 : n0 + n1 + nb2;
     const int ext = mc > 1 ? (hs != OWGS_REC_NOHOT ? HOT_CONC + hs : pk1) : hs;  // 10 bits
     const uint32_t an = A.act ? (uint32_t)a : OWGS_REC_NOACT;
     uint4 r;
@@ -1064,8 +1074,8 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 }
                 int ws = 0, wpos = 0, wcum = 0;  // long-walk resume state
 #ifdef OWGS_PROFILE
-                const u64 ts_beg = __builtin_amdgcn_s_memtime();
-                int pf_fast = 0, pf_gen = 0;
+                const u64 ts_beg = memtime_pinned();
+                int pf_fast = 0, pf_gen = 0, pf_pre = 0;
 #endif
                 // ------------------------------------------------ hot actions: one wave-cooperative walk per slot
                 // 64 walk steps per round: capacities, inclusive scan, then every rank q finds the step whose
@@ -1161,7 +1171,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                     }
                 }
 #ifdef OWGS_PROFILE
-                const u64 ts_hot = __builtin_amdgcn_s_memtime();
+                const u64 ts_hot = memtime_pinned();
 #endif
                 if (spec) {
                     if (sempty) {
@@ -1187,6 +1197,9 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                             int pos = mod_fast(home + s * step, n, __builtin_amdgcn_rcpf((float)n));
                             int cum = 0;
                             kind = K_LONG;
+#ifdef OWGS_PROFILE
+                            pf_pre = (int)(memtime_pinned() - ts_hot);
+#endif
                             
                             if (maxc == 1 && A.pool_mode == 0) {
 #ifdef OWGS_PROFILE
@@ -1377,7 +1390,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 }
                 
 #ifdef OWGS_PROFILE
-                const u64 ts_lane = __builtin_amdgcn_s_memtime();
+                const u64 ts_lane = memtime_pinned();
 #endif
                 // ------------------------------------------------ long walks: wave-cooperative, 64 steps per round
                 if (!io) {
@@ -1459,9 +1472,9 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 }
                 
 #ifdef OWGS_PROFILE
-                const int pf_fw = wave_max(pf_fast), pf_gw = wave_max(pf_gen);
+                const int pf_fw = wave_max(pf_pre), pf_gw = wave_max(pf_gen);
                 if (!io && lane == 0) {
-                    const u64 ts_end = __builtin_amdgcn_s_memtime();
+                    const u64 ts_end = memtime_pinned();
                     spw[4 * wave] = (int)(ts_hot - ts_beg);
                     spw[4 * wave + 1] = (int)(ts_lane - ts_hot);
                     spw[4 * wave + 2] = (int)(ts_end - ts_lane);
