@@ -133,7 +133,9 @@ struct owgs_ctx {
     DevBuf<u64> d_seq;
     DevBuf<int64_t> d_rel;
     DevBuf<uint4> d_rec;
-    DevBuf<uint16_t> d_lix;
+    DevBuf<uint32_t> d_lix;
+    DevBuf<uint32_t> d_gcur;  // per-action walk cursors (tagged by batch)
+    int32_t cur_tag = 0;      // tags used so far (wraps with a clear of d_gcur)
     DevBuf<uint2> d_rel_rec, d_xmeta;
     // snapshot
     DevBuf<int32_t> s_permits;
@@ -321,6 +323,17 @@ static int run_prepass(owgs_ctx* c, OwgsEngineArgs& A, int32_t n_batches, const 
 static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s) {
     int rc = lds_check(c);
     if (rc) return rc;
+    // walk cursors: one tagged word per action; the tags of this launch's batches must not repeat a stored tag
+    if (A.n_batches >= 0x1FFFF) return c->fail(OWGS_ERANGE, "more than 131070 batches in one call");
+    const size_t na = (size_t)std::max(A.n_actions, 1);
+    if (c->d_gcur.n < na || c->cur_tag + A.n_batches + 1 > 0x1FFFF) {
+        HIPCHK(c, c->d_gcur.reserve(na));
+        HIPCHK(c, hipMemsetAsync(c->d_gcur.p, 0, c->d_gcur.n * sizeof(uint32_t), s));
+        c->cur_tag = 0;
+    }
+    A.gcur = c->d_gcur.p;
+    A.cur_tag0 = c->cur_tag;
+    c->cur_tag += A.n_batches;
     HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, 16 * sizeof(u64), s));
     HIPCHK(c, owgs_launch_engine(&A, s));
     return OWGS_OK;
@@ -427,6 +440,7 @@ void owgs_destroy(owgs_ctx* c) {
     c->d_rel.release();
     c->d_rec.release();
     c->d_lix.release();
+    c->d_gcur.release();
     c->d_rel_rec.release();
     c->d_xmeta.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);

@@ -21,7 +21,10 @@
 //                                 different action).  Inside a chunk the records are dealt by class: maxConcurrent
 //                                 == 1 lanes first, then the concurrent ones (stream order inside a class), so each
 //                                 engine wave runs one speculation path.
-//   lix[n_chunks][OWGS_WL]  u16  stream lane (index in the chunk) of each record position
+//   lix[n_chunks][OWGS_WL]  u32  stream lane (index in the chunk) of each record position | the first lane of its
+//                                 action << 16 (the lane that holds the action's chunk cursor word)
+//   gcur[n_actions]         u32  walk cursor of each action (first walk step that may still fit) | batch tag << 15,
+//                                 written by the engine, gathered into LDS a chunk ahead by the I/O wave
 //   relx[n_act]             i32  where the activation's release goes: maxConcurrent == 1 -> the batch that releases it
 //                                 (the engine adds its memory to acc[batch][invoker] when it is decided);
 //                                 maxConcurrent > 1 -> its slot in the compacted concurrent-release list; -1 never
@@ -127,7 +130,9 @@ struct OwgsEngineArgs {
     int64_t n_act;               // acq_off[n_batches]
     const int64_t* rel_off;      // [n_batches + 1] or null (no releases)
     const uint4* rec;            // [n_act] pre-pass records, each chunk's lanes dealt by class (see lix)
-    const uint16_t* lix;         // [n_chunks][OWGS_WL] stream lane of each record position of the chunk
+    const uint32_t* lix;         // [n_chunks][OWGS_WL] stream lane | first lane of its action << 16, per record position
+    uint32_t* gcur;              // [max(n_actions, 1)] walk cursor of each action: batch tag << 15 | step
+    int32_t cur_tag0;            // batch b of this launch tags its cursors (cur_tag0 + b + 1) & 0x1FFFF
     const int32_t* relpos;       // [n_act] relx (see above), or null: no releases
     uint2* rel_rec;              // [n_crel] concurrent release records (compacted)
     const int32_t* crel_off;     // [n_batches + 1] first concurrent release of each batch
@@ -182,7 +187,7 @@ struct OwgsPrepassArgs {
     const uint2* xmeta;          // explicit walks: [n_act]
     const int32_t* xslot;        // explicit walks: [n_act]
     uint4* rec;                  // out [n_act]: chunk lanes in class order (maxConcurrent == 1 first)
-    uint16_t* lix;               // out [n_chunks][OWGS_WL]: stream lane of each position
+    uint32_t* lix;               // out [n_chunks][OWGS_WL]: stream lane | first lane of its action << 16
 };
 
 struct OwgsRelposArgs {

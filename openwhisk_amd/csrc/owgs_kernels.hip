@@ -97,7 +97,7 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
 #define HOT_CONC_ON 0  // concurrent hot tables: measured slower (their walks re-run every pass), kept as an option
 #endif
 static_assert(OWGS_WL < HOT_CONC, "pk1 and the concurrent hot marker share the 10-bit ext field");
-static_assert(OWGS_WL % 128 == 0, "the I/O wave stages whole dwords of 2-byte lane indices");
+static_assert(OWGS_WL % 64 == 0, "the I/O wave stages whole wave-rows");
 
 // ------------------------------------------------------------------------------------------------ helpers
 __device__ __forceinline__ u64 splitmix64(u64 x) {
@@ -298,9 +298,20 @@ __device__ __forceinline__ void lds_dma4(const void* gsrc, uint32_t lds_dst) {
                  : "memory");
 }
 
+// same, L1 bypassed (sc1): the walk cursors are re-read while this CU's engine waves store them
+__device__ __forceinline__ void lds_dma4_l2(const void* gsrc, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off sc1\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+
 // ------------------------------------------------------------------------------------------------ LDS layout
+#define OWGS_NSTG 3  // chunk staging buffers
 struct OwgsLayout {
-    uint32_t P, pool, pc, cur, ct, stgA, stgX, stgL, fst, spt, hdir, htab, hscr, rc, sc, uni, uni_bytes, total;
+    uint32_t P, pool, pc, ccw, ct, stgA, stgX, stgL, stgC, fst, spt, hdir, htab, hscr, bhead, nextl, spc, rc, sc, uni, uni_bytes,
+        total;
 };
 
 __host__ __device__ inline OwgsLayout owgs_layout(int n_slots, int pool_mode, int n_ids, int nm, int nb, int n_actions) {
@@ -314,16 +325,19 @@ __host__ __device__ inline OwgsLayout owgs_layout(int n_slots, int pool_mode, in
     o += pool_mode ? OWGS_AL(2u * (uint32_t)(nm + nb)) : OWGS_AL(4u * words);
     L.pc = o;  // identity pools: usable ids before each bitmap word (rank/select for the fallback)
     o += pool_mode ? 0u : OWGS_AL(4u * (words + 1));
-    L.cur = o;
-    o += OWGS_AL(4u * (uint32_t)n_actions);
+    (void)n_actions;  // per-action state lives in HBM (walk cursors: A.gcur)
+    L.ccw = o;        // per chunk: walk cursor + committed lanes of each action, at its first lane
+    o += 4u * OWGS_WL;
     L.ct = o;
     o += 8u * OWGS_CTC;
-    L.stgA = o;
-    o += 2u * OWGS_WL * 16u;
+    L.stgA = o;  // records, lane indices and release slots of 3 chunks (g, g+1 staged, g+2 streaming in)
+    o += OWGS_NSTG * OWGS_WL * 16u;
     L.stgX = o;
-    o += 2u * OWGS_WL * 4u;
+    o += OWGS_NSTG * OWGS_WL * 4u;
     L.stgL = o;
-    o += 2u * OWGS_WL * 2u;
+    o += OWGS_NSTG * OWGS_WL * 4u;
+    L.stgC = o;  // HBM walk cursors of chunks g and g+1, gathered by the I/O wave
+    o += 2u * OWGS_WL * 4u;
     L.sc = o;
     o += 4u * SC_N;
     // phase union: acquire phase {fst, spt, hot directory, hot rank tables, hot scratch} / release phase {rc}
@@ -333,8 +347,11 @@ __host__ __device__ inline OwgsLayout owgs_layout(int n_slots, int pool_mode, in
     L.hdir = L.spt + 4u * OWGS_WL;                  // NHOT x {action, meta.x, meta.y, slot}, NHOT x max occ, NHOT x flag
     L.htab = L.hdir + 24u * NHOT;                   // NHOT x HOT_RANKS x {id | kind << 15 | ks << 18, step}
     L.hscr = L.htab + 8u * NHOT * HOT_RANKS;        // OWGS_EW x 64 rank marks
+    L.bhead = L.hscr + 4u * 64 * OWGS_EW;           // per pass: lanes of each bucket (list head, lane + 1)
+    L.nextl = L.bhead + 4u * OWGS_NBK;              // next lane of the bucket list (lane + 1, 0 = end)
+    L.spc = L.nextl + 4u * OWGS_WL;                 // memory each lane tentatively takes at its target
     L.rc = o;
-    const uint32_t ua = (L.hscr - o) + 4u * 64 * OWGS_EW, ur = 4u * OWGS_CTC;
+    const uint32_t ua = (L.spc - o) + 4u * OWGS_WL, ur = 4u * OWGS_CTC;
     L.uni_bytes = ua > ur ? ua : ur;
     o += L.uni_bytes;
     L.total = o;
@@ -523,7 +540,7 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
     r.z = an | ((uint32_t)occ << 17) | ((uint32_t)(ext & 31) << 27);
     r.w = (uint32_t)slot | ((uint32_t)next << 17) | ((uint32_t)(ext >> 5) << 27);
     A.rec[c0 + pos] = r;
-    A.lix[(int64_t)g * OWGS_WL + pos] = (uint16_t)t;
+    A.lix[(int64_t)g * OWGS_WL + pos] = (uint32_t)t | ((uint32_t)lead << 16);
 }
 
 // Release bookkeeping.  relx[aid] = release batch (maxConcurrent == 1: aggregated into acc[batch][invoker]) or the
@@ -714,18 +731,22 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
     uint32_t* ub = (uint32_t*)(L + Y.pool);
     int16_t* pw = (int16_t*)(L + Y.pool);
     uint32_t* pc = (uint32_t*)(L + Y.pc);
-    uint32_t* cur = (uint32_t*)(L + Y.cur);
+    uint32_t* ccw = (uint32_t*)(L + Y.ccw);
+    const uint32_t* stgC = (const uint32_t*)(L + Y.stgC);
     uint2* ct = (uint2*)(L + Y.ct);  // interleaved {key, value}
     uint4* stgA = (uint4*)(L + Y.stgA);
     int32_t* stgX = (int32_t*)(L + Y.stgX);
     uint32_t* fst = (uint32_t*)(L + Y.fst);
     int32_t* spt = (int32_t*)(L + Y.spt);
+    uint32_t* bhead = (uint32_t*)(L + Y.bhead);
+    int32_t* nextl = (int32_t*)(L + Y.nextl);
+    int32_t* spc = (int32_t*)(L + Y.spc);
     uint4* hdir = (uint4*)(L + Y.hdir);
     int32_t* hocc = (int32_t*)(L + Y.hdir + 16u * NHOT);
     int32_t* hflag = (int32_t*)(L + Y.hdir + 20u * NHOT);
     uint2* htab = (uint2*)(L + Y.htab);
     int32_t* hscr = (int32_t*)(L + Y.hscr);
-    const uint16_t* stgL = (const uint16_t*)(L + Y.stgL);
+    const uint32_t* stgL = (const uint32_t*)(L + Y.stgL);
     uint32_t* rc = (uint32_t*)(L + Y.rc);
     int32_t* sc = (int32_t*)(L + Y.sc);
 #ifdef OWGS_PROFILE
@@ -788,12 +809,23 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
     PT_DECL
 
     // ---------------------------------------------------------------- I/O wave: chunk prefetch pipeline
-    // While the engine resolves chunk g, the I/O wave streams the records of chunk g+1 from HBM straight into
-    // stgA/stgX[(g+1)&1] by LDS-DMA (global_load_lds: no registers, nothing for the engine waves to wait on) and
-    // drains them (vmcnt(0)) before the last barrier of chunk g.
+    // While the engine resolves chunk g, the I/O wave streams the records of chunk g+2 from HBM straight into
+    // stgA/stgX/stgL[(g+2)%3] by LDS-DMA (global_load_lds: no registers, nothing for the engine waves to wait on),
+    // gathers the HBM walk cursors of chunk g+1's actions (staged a chunk earlier) into stgC[(g+1)&1], and drains both
+    // (vmcnt(0)) before the last barrier of chunk g.
     int io_b = 0;
     int64_t io_c0 = 0;
-    const uint32_t stgA_lds = (uint32_t)(size_t)stgA, stgX_lds = (uint32_t)(size_t)stgX, stgL_lds = (uint32_t)(size_t)stgL;
+    const uint32_t stgA_lds = (uint32_t)(size_t)stgA, stgX_lds = (uint32_t)(size_t)stgX, stgL_lds = (uint32_t)(size_t)stgL,
+                   stgC_lds = (uint32_t)(size_t)stgC;
+    // cursor words of the actions of the chunk staged in stgA[sb] (lanes past its end gather a valid dummy word)
+    auto io_gather = [&](int sb, int cb) {
+#pragma unroll
+        for (int k = 0; k < OWGS_WL / 64; ++k) {
+            const uint32_t a = stgA[sb * OWGS_WL + 64 * k + lane].z & OWGS_REC_NOACT;
+            const int ai = (int)a < A.n_actions ? (int)a : 0;
+            lds_dma4_l2(&A.gcur[ai], __builtin_amdgcn_readfirstlane(stgC_lds + (uint32_t)(cb * OWGS_WL + 64 * k) * 4u));
+        }
+    };
     // advance (io_b, io_c0) to the next chunk; returns false at the end of the stream
     auto io_locate = [&](int& bb, int64_t& c0) -> bool {
         while (bb < A.n_batches && c0 >= A.acq_off[bb + 1]) {
@@ -805,10 +837,10 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
     // lanes past the end of the stream re-read its last record: the engine ignores lanes >= the chunk length
     auto io_dma = [&](int64_t c0, int buf, int gc) {
         const int64_t last = A.n_act - 1;
-        const uint32_t* lx = (const uint32_t*)(A.lix + (int64_t)gc * OWGS_WL);
+        const uint32_t* lx = A.lix + (int64_t)gc * OWGS_WL;
 #pragma unroll
-        for (int k = 0; k < OWGS_WL / 128; ++k)  // 2-byte lane indices: OWGS_WL / 2 dwords
-            lds_dma4(&lx[lane + 64 * k], __builtin_amdgcn_readfirstlane(stgL_lds + (uint32_t)(buf * OWGS_WL * 2 + 256 * k)));
+        for (int k = 0; k < OWGS_WL / 64; ++k)
+            lds_dma4(&lx[lane + 64 * k], __builtin_amdgcn_readfirstlane(stgL_lds + (uint32_t)(buf * OWGS_WL + 64 * k) * 4u));
 #pragma unroll
         for (int k = 0; k < OWGS_WL / 64; ++k) {
             int64_t i = c0 + lane + 64 * k;
@@ -820,10 +852,13 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
     };
     if (io) {
         if (A.n_batches > 0) io_c0 = A.acq_off[0];
-        if (io_locate(io_b, io_c0)) {
-            io_dma(io_c0, 0, 0);
-            io_c0 += OWGS_WL;
-        }
+        for (int k = 0; k < 2; ++k)
+            if (io_locate(io_b, io_c0)) {
+                io_dma(io_c0, k, k);
+                io_c0 += OWGS_WL;
+            }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        io_gather(0, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     lds_sync();
@@ -957,9 +992,8 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
             lds_sync();
         }
         PT(0);
-        // ============================================================ per-batch bounds and cursors
+        // ============================================================ per-batch bounds
         if (!io) {
-            for (int i = tid; i < A.n_actions; i += OWGS_ENT) cur[i] = 0u;
             int m0 = (int)0x80000000, m1 = (int)0x80000000;
             if (A.pool_mode == 0) {
                 for (int i = tid; i < nm; i += OWGS_ENT)
@@ -985,27 +1019,26 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
 
         PT(0);
         // ============================================================ publishes (SCPB:398-436, NS:32-91)
-        int kstamp = 0;
+        const uint32_t btag = (uint32_t)(A.cur_tag0 + b + 1) & 0x1FFFFu;  // HBM cursors written in this batch
         for (int64_t c0 = a_beg; c0 < a_end; c0 += OWGS_WL, ++g) {
             const int len = (int)min((int64_t)OWGS_WL, a_end - c0);
-            if (++kstamp == 128) {  // stamps wrap: clear the chunk-rank fields, keep the walk cursors
-                if (!io)
-                    for (int i = tid; i < A.n_actions; i += OWGS_ENT) cur[i] &= 0x7FFFu;
-                kstamp = 1;
-                lds_sync();
-            }
             ++st_chunk;
             // ---- lane record: the pre-pass dealt the chunk's records by class (maxConcurrent == 1 first), so a wave
             // mostly runs one speculation path; li = the lane's index in the stream order of the chunk
             const bool own = !io && lane < OWGS_LPW;  // this thread holds an activation of the chunk
             const int sl = wave * OWGS_LPW + lane;    // record position
             const bool held = own && sl < len;
-            const int li = held ? (int)stgL[(g & 1) * OWGS_WL + sl] : OWGS_WL;
+            const int sbuf = g % OWGS_NSTG;
+            const int lx = held ? (int)stgL[sbuf * OWGS_WL + sl] : 0;
+            const int li = held ? (lx & 0xFFFF) : OWGS_WL;
+            const int lead = lx >> 16;  // first lane of the chunk with this lane's action (its walk-cursor word)
             uint4 rc4 = make_uint4(0, 0, 0, 0);
             int relx = -1;
+            uint32_t gcw = 0;
             if (held) {
-                rc4 = stgA[(g & 1) * OWGS_WL + sl];
-                relx = A.relpos ? stgX[(g & 1) * OWGS_WL + li] : -1;
+                rc4 = stgA[sbuf * OWGS_WL + sl];
+                relx = A.relpos ? stgX[sbuf * OWGS_WL + li] : -1;
+                gcw = stgC[(g & 1) * OWGS_WL + sl];
             }
             const bool valid = own && (rc4.y & OWGS_AM_VALID) && li < len;
             const int home = (int)(rc4.x & OWGS_AM_POS_MASK);
@@ -1026,6 +1059,13 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
             const float rm = __builtin_amdgcn_rcpf((float)(mem > 0 ? mem : 1));
             const int64_t i = c0 + li;
             bool pending = valid;
+            // chunk cursor word of each action, at its first lane: walk step (15 bits) | lanes committed (10 bits);
+            // the step starts from the action's HBM cursor when it was written in this batch (a lower bound: steps
+            // before it were full and permits only fall inside a batch)
+            if (held && occ == 0) {
+                const uint32_t st0 = (a != (int)OWGS_REC_NOACT && cok && (gcw >> 15) == btag) ? (gcw & 0x7FFFu) : 0u;
+                ccw[li] = st0;
+            }
 
             // ---- hot actions (slots assigned by the pre-pass): the first lane publishes the walk, the last lane
             // the largest occurrence index
@@ -1033,7 +1073,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
             const int hs = (valid && hsx >= 0 && hsx < NHOT && !(A.opts & 1)) ? hsx : -1;
             if (hs >= 0) {
                 if (occ == 0) {
-                    hdir[hs] = make_uint4((uint32_t)a, rc4.x, rc4.y, (uint32_t)slot);
+                    hdir[hs] = make_uint4((uint32_t)li, rc4.x, rc4.y, (uint32_t)slot);  // .x = cursor word
                     hflag[hs] = 0;  // walked in the first pass (f = 0)
                     atomicMax(&sc[SC_NHOT], hs + 1);
                 }
@@ -1041,10 +1081,13 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
             }
             lds_sync();
             const int nhot = sc[SC_NHOT];
-            // ---- I/O wave: stream chunk g+1 into the other staging buffer
-            if (io && io_locate(io_b, io_c0)) {
-                io_dma(io_c0, (g + 1) & 1, g + 1);
-                io_c0 += OWGS_WL;
+            // ---- I/O wave: cursors of chunk g+1, records of chunk g+2
+            if (io) {
+                io_gather((g + 1) % OWGS_NSTG, (g + 1) & 1);
+                if (io_locate(io_b, io_c0)) {
+                    io_dma(io_c0, (g + 2) % OWGS_NSTG, g + 2);
+                    io_c0 += OWGS_WL;
+                }
             }
 
             int f = 0;
@@ -1085,15 +1128,14 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                         const uint4 d = hdir[h];
                         if (d.z & (OWGS_AM_THROW | OWGS_AM_EMPTY)) continue;
                         if (hflag[h] != f) continue;  // no lane of this action speculates in this pass
-                        const int ha = (int)d.x;
                         const int hhome = (int)(d.y & OWGS_AM_POS_MASK), hstep = (int)((d.y >> 15) & OWGS_AM_POS_MASK);
                         const int hpool = (d.y & OWGS_AM_POOL) ? 1 : 0;
                         const bool hcok = (d.y & OWGS_AM_COK) != 0;
                         const int hmem = (int)(d.z & OWGS_AM_MEM_MASK);
                         const int hmc = (int)((d.z >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
                         const int hslot = (int)d.w;
-                        const uint32_t hcw = cur[ha];
-                        const int hcc = ((int)(hcw >> 25) == kstamp) ? (int)((hcw >> 15) & OWGS_RMASK) : 0;
+                        const uint32_t hcw = ccw[d.x];
+                        const int hcc = (int)((hcw >> 15) & OWGS_RMASK);
                         const int need = min(hocc[h] - hcc + 1, HOT_RANKS);
                         if (need <= 0) continue;
                         uint2* tab = htab + h * HOT_RANKS;
@@ -1181,13 +1223,9 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                     } else {
                         int s = 0;
                         r = occ;
-                        if (a != (int)OWGS_REC_NOACT) {
-                            cw = cur[a];
-                            // cursor word: walk step (15 bits) | committed lanes of the action in this chunk (10) |
-                            // chunk stamp (7)
-                            if ((int)(cw >> 25) == kstamp) r = occ - (int)((cw >> 15) & OWGS_RMASK);
-                            if (cok) s = (int)(cw & 0x7FFFu);
-                        }
+                        cw = ccw[lead];  // walk step (15 bits) | committed lanes of the action in this chunk (10)
+                        r = occ - (int)((cw >> 15) & OWGS_RMASK);
+                        if (cok) s = (int)(cw & 0x7FFFu);
                         const int U = sc[pool ? SC_U1 : SC_U0];
                         if (hs >= 0 && r < HOT_RANKS) {
                             kind = K_HOT;
@@ -1555,6 +1593,8 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 if (part) {
                     if (cons) atomicSub(&P[t], cons);
                     atomicMax(&fst[bk], (uint32_t)(OWGS_WL - li));
+                    nextl[li] = (int)atomicExch(&bhead[bk], (uint32_t)(li + 1));
+                    spc[li] = cons;
                 }
                 if (act && maxc > 1 && kind == K_FALLBACK) atomicMin(&sc[SC_CFB + par], li);
                 if (own && li < OWGS_WL) spt[li] = part ? t : -1;
@@ -1563,18 +1603,40 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 PT(3);
                 // ------------------------------------------------ validate: known to fit?
                 bool nf = false;
+#ifdef OWGS_STOP_REASONS
+                int why = 0;
+#endif
                 if (part) {
                     const bool first = fst[bk] == (uint32_t)(OWGS_WL - li);
+                    // fits at t: the lowest lane of its bucket, or every lane of the pass at t fits, or (walking the
+                    // bucket's lanes) the lanes before this one at t leave room for it
+                    bool fit = first || P[t] >= 0;
+                    if (!fit && kind != K_FALLBACK) {
+                        int pf = 0, tot = 0;
+                        for (int j = (int)bhead[bk] - 1; j >= 0; j = nextl[j] - 1)
+                            if (spt[j] == t) {
+                                const int cj = spc[j];
+                                tot += cj;
+                                pf += j < li ? cj : 0;
+                            }
+                        fit = P[t] + tot - pf - cons >= 0;
+                    }
                     bool kf;
                     if (maxc == 1) {
-                        kf = first || kind == K_FALLBACK || P[t] >= 0;
+                        kf = fit || kind == K_FALLBACK;
                     } else {
                         const int cfb = sc[SC_CFB + par];
                         if (kind == K_FALLBACK) kf = first && cfb >= li;
-                        else kf = (first || P[t] >= 0) && cfb > li;
+                        else kf = fit && cfb > li;
                         if (pk1 > f) kf = false;  // an earlier lane of this pass has the same fqn, another walk
                     }
                     nf = !kf;
+#ifdef OWGS_STOP_REASONS
+                    if (nf) {
+                        const int cfb = sc[SC_CFB + par];
+                        why = maxc == 1 ? 1 : pk1 > f ? 5 : kind == K_FALLBACK ? (!first ? 2 : 4) : (cfb <= li ? 4 : 3);
+                    }
+#endif
                 }
                 if (!io) {
                     // (the lanes of a wave are not in stream order) the wave's smallest such lane
@@ -1591,6 +1653,9 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                     l = f + 1;
                     err |= OWGS_ERR_INTERNAL;
                 }
+#ifdef OWGS_STOP_REASONS
+                if (li == l && why) atomicAdd(&A.stats[6], 1ull << (12 * (why - 1)));
+#endif
                 if (act && li < l) {
                     const int outv = kind == K_NONE ? OWGS_NONE_V : (kind == K_THROW ? OWGS_THROW_V : t);
                     A.out_inv[i] = outv;
@@ -1613,7 +1678,9 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                             if (kind == K_TARGET) ns = (uint32_t)s_t;
                             else if (kind == K_FALLBACK) ns = maxc == 1 ? (uint32_t)n : 0u;
                         }
-                        cur[a] = ((uint32_t)kstamp << 25) | ((uint32_t)(occ + 1) << 15) | ns;
+                        ccw[lead] = ((uint32_t)(occ + 1) << 15) | ns;
+                        if (cok && a != (int)OWGS_REC_NOACT && ns != (cw & 0x7FFFu))
+                            A.gcur[a] = (btag << 15) | ns;  // for the later chunks of this batch
                     }
                     // NestedSemaphore concurrency entry: the last committed lane of the (invoker, fqn) group
                     if (maxc > 1 && (kind == K_TARGET || kind == K_FALLBACK)) {
@@ -1644,6 +1711,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 if (part) {
                     if (li >= l && cons) atomicAdd(&P[t], cons);  // not committed: give the memory back
                     fst[bk] = 0u;
+                    bhead[bk] = 0u;
                 }
                 if (act && li >= l) {
                     keep = !nf && (maxc == 1 || !part);
@@ -1685,7 +1753,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
         if (!io) {
             atomicAdd(&A.stats[OWGS_ST_PROBES], (u64)st_probe);
             atomicAdd(&A.stats[OWGS_ST_FALLBACKS], (u64)st_fb);
-#ifndef OWGS_PROFILE
+#if !defined(OWGS_PROFILE) && !defined(OWGS_STOP_REASONS)
             atomicAdd(&A.stats[6], (u64)st_gprobe);
             atomicAdd(&A.stats[7], (u64)st_glane);
 #endif
