@@ -44,7 +44,10 @@
 #define OWGS_ENT (OWGS_EW * 64)        // engine threads
 #define OWGS_WL (OWGS_EW * OWGS_LPW)   // chunk width: activations resolved together (one per engine lane)
 #define OWGS_NT (OWGS_ENT + 64)        // threads: engine waves + one I/O wave
-#define OWGS_NBK 4096                  // "first lane of its invoker" buckets (hashed; collisions are conservative)
+#ifndef OWGS_NBK_LOG2
+#define OWGS_NBK_LOG2 11
+#endif
+#define OWGS_NBK (1 << OWGS_NBK_LOG2)  // "first lane of its invoker" buckets (hashed; collisions are conservative)
 #define OWGS_CTC 4096                  // concurrency-table capacity (entries, power of two)
 #define OWGS_LDS_BYTES (160 * 1024)
 

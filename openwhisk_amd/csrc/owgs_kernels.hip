@@ -519,19 +519,61 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
     const int cls = (hs != OWGS_REC_NOHOT || (meta.y & (OWGS_AM_THROW | OWGS_AM_EMPTY))) ? 1 : (mc > 1 ? 2 : 0);
     s_p[t] = t < len ? cls : 3;
     __syncthreads();
-    if (t >= len) return;
-    int nb0 = 0, nb1 = 0, nb2 = 0, n0 = 0, n1 = 0;
-    for (int j = 0; j < len; ++j) {
-        const int cj = s_p[j];
-        n0 += cj == 0;
-        n1 += cj == 1;
-        if (j < t) {
-            nb0 += cj == 0;
-            nb1 += cj == 1;
-            nb2 += cj == 2;
+    if (len == OWGS_WL && t == 0) {
+        // full chunk: the concurrent lanes are spread round-robin over the waves left after the maxConcurrent == 1
+        // walkers, and the lanes without a walk fill the gaps (from the last wave down), so the waves that run the
+        // concurrent path hold fewer of them (a wave takes as long as its slowest lane)
+        int cnt[OWGS_EW];
+        int n0 = 0, n2 = 0;
+        for (int w = 0; w < OWGS_EW; ++w) cnt[w] = 0;
+        for (int j = 0; j < len; ++j) {
+            n0 += s_p[j] == 0;
+            n2 += s_p[j] == 2;
         }
+        const int f0 = (n0 + OWGS_LPW - 1) / OWGS_LPW, R = OWGS_EW - f0;
+        int w0 = 0, rr = 0;
+        for (int j = 0; j < len; ++j)
+            if (s_p[j] == 0) {
+                while (cnt[w0] == OWGS_LPW) ++w0;
+                s_s[j] = w0 * OWGS_LPW + cnt[w0]++;
+            }
+        for (int j = 0; j < len; ++j)
+            if (s_p[j] == 2) {
+                int w = -1;
+                for (int k = 0; k < R && w < 0; ++k, ++rr) {
+                    const int c = OWGS_EW - 1 - (rr % R);
+                    if (cnt[c] < OWGS_LPW) w = c;
+                }
+                for (int c = OWGS_EW - 1; c >= 0 && w < 0; --c)
+                    if (cnt[c] < OWGS_LPW) w = c;
+                s_s[j] = w * OWGS_LPW + cnt[w]++;
+            }
+        for (int j = 0; j < len; ++j)
+            if (s_p[j] == 1) {
+                int w = OWGS_EW - 1;
+                while (cnt[w] == OWGS_LPW) --w;
+                s_s[j] = w * OWGS_LPW + cnt[w]++;
+            }
     }
-    const int pos = cls == 0 ? nb0 : cls == 1 ? n0 + nb1 : n0 + n1 + nb2;
+    __syncthreads();
+    if (t >= len) return;
+    int pos;
+    if (len == OWGS_WL) {
+        pos = s_s[t];
+    } else {  // short chunk (positions must stay below len): classes in order
+        int nb0 = 0, nb1 = 0, nb2 = 0, n0 = 0, n1 = 0;
+        for (int j = 0; j < len; ++j) {
+            const int cj = s_p[j];
+            n0 += cj == 0;
+            n1 += cj == 1;
+            if (j < t) {
+                nb0 += cj == 0;
+                nb1 += cj == 1;
+                nb2 += cj == 2;
+            }
+        }
+        pos = cls == 0 ? nb0 : cls == 1 ? n0 + nb1 : n0 + n1 + nb2;
+    }
     const int ext = mc > 1 ? (hs != OWGS_REC_NOHOT ? HOT_CONC + hs : pk1) : hs;  // 10 bits
     const uint32_t an = A.act ? (uint32_t)a : OWGS_REC_NOACT;
     uint4 r;
@@ -1588,8 +1630,8 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 // every lane tentatively takes its memory from its target's permits: after the barrier P[t] is the
                 // frontier permits minus the consumption of ALL lanes of the pass at t (the commit keeps it, the
                 // lanes after l give it back).  "first" = lowest lane of the (hashed) bucket of t.
-                const int bk = part ? (int)(((uint32_t)t * 2654435761u) >> (32 - 12)) : 0;
-                static_assert(OWGS_NBK == 4096 && OWGS_WL <= 512, "bucket hash assumes 4096 buckets; lane fields 10 bits");
+                const int bk = part ? (int)(((uint32_t)t * 2654435761u) >> (32 - OWGS_NBK_LOG2)) : 0;
+                static_assert(OWGS_NBK == (1 << OWGS_NBK_LOG2) && OWGS_WL <= 512, "power-of-two buckets; lane fields 10 bits");
                 if (part) {
                     if (cons) atomicSub(&P[t], cons);
                     atomicMax(&fst[bk], (uint32_t)(OWGS_WL - li));
