@@ -257,7 +257,7 @@ class GpuShardingContainerPoolBalancer:
         if any(out[8:16]):
             names = ["batch", "chunk_start", "speculate", "tables_buckets", "validate", "commit", "worst_hot", "worst_lane"]
             d["cycles"] = {k: out[8 + i] for i, k in enumerate(names)}
-            # profile build: slots 6/7 hold the worst wave's slowest per-lane walks instead of the probe counters
-            d["cycles"]["worst_prelude"] = d.pop("general_probes")
-            d["cycles"]["worst_general_walk"] = d.pop("general_lanes")
+            # profile build: slots 6/7 hold the cycles of the first and of the later passes of the chunks
+            d["cycles"]["first_passes"] = d.pop("general_probes")
+            d["cycles"]["later_passes"] = d.pop("general_lanes")
         return d

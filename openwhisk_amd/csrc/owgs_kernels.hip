@@ -1101,6 +1101,29 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
             const float rm = __builtin_amdgcn_rcpf((float)(mem > 0 ? mem : 1));
             const int64_t i = c0 + li;
             bool pending = valid;
+            // walk cursor after a forced acquire of a concurrent action at invoker x: the walk had failed everywhere,
+            // and the new container at x (maxConcurrent - 1 free slots) is the only step that became feasible, so the
+            // next lanes start at x's step j = (pos(x) - home) * step^-1 mod n (identity pools; else from 0)
+            auto fallback_cursor = [&](int x) -> uint32_t {
+                if (A.pool_mode != 0 || n <= 1) return 0u;
+                const int xp = x - (pool ? A.n_ids - nb : 0);
+                if (xp < 0 || xp >= n) return 0u;
+                int t0 = 0, t1 = 1, r0 = n, r1 = step % n;  // extended Euclid: step^-1 mod n (gcd(step, n) = 1)
+                while (r1 != 0) {
+                    const int q = r0 / r1;
+                    const int tt = t0 - q * t1;
+                    t0 = t1;
+                    t1 = tt;
+                    const int rr = r0 - q * r1;
+                    r0 = r1;
+                    r1 = rr;
+                }
+                if (r0 != 1) return 0u;
+                const int inv = t0 < 0 ? t0 + n : t0;
+                const int d = xp - home;
+                const int dd = d < 0 ? d + n : d;
+                return (uint32_t)(int)(((long long)dd * inv) % n);
+            };
             // chunk cursor word of each action, at its first lane: walk step (15 bits) | lanes committed (10 bits);
             // the step starts from the action's HBM cursor when it was written in this batch (a lower bound: steps
             // before it were full and permits only fall inside a batch)
@@ -1143,6 +1166,9 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
             bool keep = false;
             while (f < len) {
                 ++st_pass;
+#ifdef OWGS_PROFILE
+                const u64 tpass0 = memtime_pinned();
+#endif
                 const bool act = pending && li >= f;
                 const bool spec = act && !keep;
                 // ------------------------------------------------ speculate (packing) against the state at f
@@ -1573,8 +1599,6 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                     }
                     pt_acc[6] += (u64)spw[4 * worst];       // worst wave: hot walks
                     pt_acc[7] += (u64)spw[4 * worst + 1];   // worst wave: per-lane speculation
-                    pt_x[0] += (u64)pfw[2 * worst];         // worst wave: slowest maxConcurrent==1 per-lane walk
-                    pt_x[1] += (u64)pfw[2 * worst + 1];     // worst wave: slowest general per-lane walk
                 }
 #endif
                 if (spec && kind == K_HOT) {
@@ -1718,7 +1742,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                         uint32_t ns = cw & 0x7FFFu;
                         if (cok) {
                             if (kind == K_TARGET) ns = (uint32_t)s_t;
-                            else if (kind == K_FALLBACK) ns = maxc == 1 ? (uint32_t)n : 0u;
+                            else if (kind == K_FALLBACK) ns = maxc == 1 ? (uint32_t)n : fallback_cursor(t);
                         }
                         ccw[lead] = ((uint32_t)(occ + 1) << 15) | ns;
                         if (cok && a != (int)OWGS_REC_NOACT && ns != (cw & 0x7FFFu))
@@ -1768,6 +1792,9 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 }
                 lds_sync();
                 PT(5);
+#ifdef OWGS_PROFILE
+                if (tid == 0) pt_x[f == 0 ? 0 : 1] += memtime_pinned() - tpass0;  // first vs repeated passes
+#endif
                 f = l;
                 par ^= 1;
             }
