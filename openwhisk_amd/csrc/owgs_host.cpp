@@ -365,11 +365,16 @@ extern "C" {
 int owgs_abi_version(void) { return OWGS_ABI_VERSION; }
 
 int owgs_limits(int32_t* max_invokers, int32_t* max_slots) {
-    // identity pools, no registered actions: 4 B permits + 1 bit usable per invoker on top of the fixed LDS state
-    const size_t fixed = owgs_engine_lds_bytes(0, 0, 0, 0, 0, 0);
-    const int32_t n = (int32_t)std::min<size_t>((OWGS_LDS_BYTES - fixed - 64) * 8 / 33, OWGS_MAX_SLOTS_CT);
-    if (max_invokers) *max_invokers = n;
-    if (max_slots) *max_slots = n;
+    // identity pools (the largest on-chip state per invoker: permits + usable bit + prefix counts): the largest
+    // invoker count whose LDS image fits, found by bisection over the layout itself
+    int32_t lo = 0, hi = OWGS_MAX_SLOTS_CT;
+    while (lo < hi) {
+        const int32_t mid = lo + (hi - lo + 1) / 2;
+        if (owgs_engine_lds_bytes(mid, 0, mid, mid, mid, 0) <= OWGS_LDS_BYTES) lo = mid;
+        else hi = mid - 1;
+    }
+    if (max_invokers) *max_invokers = lo;
+    if (max_slots) *max_slots = lo;
     return OWGS_OK;
 }
 
