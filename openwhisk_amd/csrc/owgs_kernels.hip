@@ -62,11 +62,12 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
 #define PT_DECL                 \
     u64 pt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
     u64 pt_x[2] = {0, 0};                     \
-    u64 pt_t = memtime_pinned();
+    u64 pt_t = memtime_pinned(); \
+    int pt_on = 1;
 #define PT(k)                                        \
     {                                                \
-        const u64 _t = memtime_pinned(); \
-        pt_acc[k] += _t - pt_t;                      \
+        const u64 _t = memtime_pinned();             \
+        if (pt_on) pt_acc[k] += _t - pt_t;           \
         pt_t = _t;                                   \
     }
 #else
@@ -310,8 +311,8 @@ __device__ __forceinline__ void lds_dma4_l2(const void* gsrc, uint32_t lds_dst) 
 // ------------------------------------------------------------------------------------------------ LDS layout
 #define OWGS_NSTG 3  // chunk staging buffers
 struct OwgsLayout {
-    uint32_t P, pool, pc, ccw, ct, stgA, stgX, stgL, stgC, fst, spt, hdir, htab, hscr, bhead, nextl, spc, rc, sc, uni, uni_bytes,
-        total;
+    uint32_t P, pool, pc, ccw, ct, stgA, stgX, stgL, stgC, fst, spt, hdir, htab, hscr, bhead, nextl, spc, cdirty, rc, sc, uni,
+        uni_bytes, total;
 };
 
 __host__ __device__ inline OwgsLayout owgs_layout(int n_slots, int pool_mode, int n_ids, int nm, int nb, int n_actions) {
@@ -350,8 +351,9 @@ __host__ __device__ inline OwgsLayout owgs_layout(int n_slots, int pool_mode, in
     L.bhead = L.hscr + 4u * 64 * OWGS_EW;           // per pass: lanes of each bucket (list head, lane + 1)
     L.nextl = L.bhead + 4u * OWGS_NBK;              // next lane of the bucket list (lane + 1, 0 = end)
     L.spc = L.nextl + 4u * OWGS_WL;                 // memory each lane tentatively takes at its target
+    L.cdirty = L.spc + 4u * OWGS_WL;                // [2][OWGS_WL] pass parity x first lane of an action: re-speculated
     L.rc = o;
-    const uint32_t ua = (L.spc - o) + 4u * OWGS_WL, ur = 4u * OWGS_CTC;
+    const uint32_t ua = (L.cdirty - o) + 8u * OWGS_WL, ur = 4u * OWGS_CTC;
     L.uni_bytes = ua > ur ? ua : ur;
     o += L.uni_bytes;
     L.total = o;
@@ -783,6 +785,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
     uint32_t* bhead = (uint32_t*)(L + Y.bhead);
     int32_t* nextl = (int32_t*)(L + Y.nextl);
     int32_t* spc = (int32_t*)(L + Y.spc);
+    int32_t* cdirty = (int32_t*)(L + Y.cdirty);
     uint4* hdir = (uint4*)(L + Y.hdir);
     int32_t* hocc = (int32_t*)(L + Y.hdir + 16u * NHOT);
     int32_t* hflag = (int32_t*)(L + Y.hdir + 20u * NHOT);
@@ -1168,8 +1171,14 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 ++st_pass;
 #ifdef OWGS_PROFILE
                 const u64 tpass0 = memtime_pinned();
+#ifdef OWGS_PROF_LATER
+                pt_on = f > 0;  // phase cycles of the later passes only
+#endif
 #endif
                 const bool act = pending && li >= f;
+                // a kept concurrent lane's unit index at its target (and so its memory take) assumed every earlier
+                // lane of its action lands as speculated: it speculates again when one of them did
+                if (keep && maxc > 1 && cdirty[par * OWGS_WL + lead]) keep = false;
                 const bool spec = act && !keep;
                 // ------------------------------------------------ speculate (packing) against the state at f
                 if (spec) {
@@ -1561,6 +1570,9 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                                 break;
                             }
                             cum += __builtin_amdgcn_readlane(inc, 63);
+#ifdef OWGS_COUNT_ROUNDS
+                            st_glane += lane == 0 ? 1u : 0u;
+#endif
                             s0 += 64;
                             p0 += boff;
                             if (p0 >= nn) p0 -= nn;
@@ -1590,6 +1602,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
 #endif
                 lds_sync();
                 PT(2);  // hot tables written; every wave has finished reading P for its speculation
+                if (own) cdirty[par * OWGS_WL + sl] = 0;  // read above; the commit of this pass fills the other half
 #ifdef OWGS_PROFILE
                 if (tid == 0) {
                     int worst = 0, wmax = -1;
@@ -1761,6 +1774,10 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                             const int ops1 = ops0 + jn;
                             if (ops1 > OWGS_MAX_OPS) err |= OWGS_ERR_OPS;
                             int ix = cidx;
+                            if (ix < 0) {  // absent when speculated; a kept lane's group may have created it since
+                                uint32_t v0;
+                                ix = ct_findv(ct, ct_key(t, slot), &v0);
+                            }
                             if (ix < 0) {
                                 int fresh = 0;
                                 ix = ct_insertv(ct, ct_key(t, slot), &fresh);
@@ -1780,8 +1797,9 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                     bhead[bk] = 0u;
                 }
                 if (act && li >= l) {
-                    keep = !nf && (maxc == 1 || !part);
+                    keep = !nf;
                     if (!keep && hs >= 0) hflag[hs] = l;  // the action's hot table is needed in the next pass
+                    if (!keep && maxc > 1) cdirty[(par ^ 1) * OWGS_WL + lead] = 1;
                 }
                 if (io && l >= len) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk g+1 staged
                 if (tid == 0) {
