@@ -98,7 +98,7 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
 #define HOT_CONC_ON 0  // concurrent hot tables: measured slower (their walks re-run every pass), kept as an option
 #endif
 static_assert(OWGS_WL < HOT_CONC, "pk1 and the concurrent hot marker share the 10-bit ext field");
-static_assert(OWGS_WL % 64 == 0, "the I/O wave stages whole wave-rows");
+#define OWGS_WROWS ((OWGS_WL + 63) / 64)  // wave rows the I/O wave stages per chunk
 
 // ------------------------------------------------------------------------------------------------ helpers
 __device__ __forceinline__ u64 splitmix64(u64 x) {
@@ -311,8 +311,8 @@ __device__ __forceinline__ void lds_dma4_l2(const void* gsrc, uint32_t lds_dst) 
 // ------------------------------------------------------------------------------------------------ LDS layout
 #define OWGS_NSTG 3  // chunk staging buffers
 struct OwgsLayout {
-    uint32_t P, pool, pc, ccw, ct, stgA, stgX, stgL, stgC, fst, spt, hdir, htab, hscr, bhead, nextl, spc, cdirty, rc, sc, uni,
-        uni_bytes, total;
+    uint32_t P, pool, pc, ccw, ct, stgA, stgX, stgL, stgC, fst, spt, hdir, htab, hscr, bhead, nextl, spc, cdirty, skey, rc, sc,
+        uni, uni_bytes, total;
 };
 
 __host__ __device__ inline OwgsLayout owgs_layout(int n_slots, int pool_mode, int n_ids, int nm, int nb, int n_actions) {
@@ -352,8 +352,9 @@ __host__ __device__ inline OwgsLayout owgs_layout(int n_slots, int pool_mode, in
     L.nextl = L.bhead + 4u * OWGS_NBK;              // next lane of the bucket list (lane + 1, 0 = end)
     L.spc = L.nextl + 4u * OWGS_WL;                 // memory each lane tentatively takes at its target
     L.cdirty = L.spc + 4u * OWGS_WL;                // [2][OWGS_WL] pass parity x first lane of an action: re-speculated
+    L.skey = L.cdirty + 8u * OWGS_WL;               // per lane {slot key, action} (shared-key check)
     L.rc = o;
-    const uint32_t ua = (L.cdirty - o) + 8u * OWGS_WL, ur = 4u * OWGS_CTC;
+    const uint32_t ua = (L.skey - o) + 8u * OWGS_WL, ur = 4u * OWGS_CTC;
     L.uni_bytes = ua > ur ? ua : ur;
     o += L.uni_bytes;
     L.total = o;
@@ -786,6 +787,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
     int32_t* nextl = (int32_t*)(L + Y.nextl);
     int32_t* spc = (int32_t*)(L + Y.spc);
     int32_t* cdirty = (int32_t*)(L + Y.cdirty);
+    uint2* skey = (uint2*)(L + Y.skey);
     uint4* hdir = (uint4*)(L + Y.hdir);
     int32_t* hocc = (int32_t*)(L + Y.hdir + 16u * NHOT);
     int32_t* hflag = (int32_t*)(L + Y.hdir + 20u * NHOT);
@@ -865,10 +867,13 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
     // cursor words of the actions of the chunk staged in stgA[sb] (lanes past its end gather a valid dummy word)
     auto io_gather = [&](int sb, int cb) {
 #pragma unroll
-        for (int k = 0; k < OWGS_WL / 64; ++k) {
-            const uint32_t a = stgA[sb * OWGS_WL + 64 * k + lane].z & OWGS_REC_NOACT;
-            const int ai = (int)a < A.n_actions ? (int)a : 0;
-            lds_dma4_l2(&A.gcur[ai], __builtin_amdgcn_readfirstlane(stgC_lds + (uint32_t)(cb * OWGS_WL + 64 * k) * 4u));
+        for (int k = 0; k < OWGS_WROWS; ++k) {
+            const uint32_t m0 = __builtin_amdgcn_readfirstlane(stgC_lds + (uint32_t)(cb * OWGS_WL + 64 * k) * 4u);
+            if (64 * k + lane < OWGS_WL) {
+                const uint32_t a = stgA[sb * OWGS_WL + 64 * k + lane].z & OWGS_REC_NOACT;
+                const int ai = (int)a < A.n_actions ? (int)a : 0;
+                lds_dma4_l2(&A.gcur[ai], m0);
+            }
         }
     };
     // advance (io_b, io_c0) to the next chunk; returns false at the end of the stream
@@ -884,15 +889,17 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
         const int64_t last = A.n_act - 1;
         const uint32_t* lx = A.lix + (int64_t)gc * OWGS_WL;
 #pragma unroll
-        for (int k = 0; k < OWGS_WL / 64; ++k)
-            lds_dma4(&lx[lane + 64 * k], __builtin_amdgcn_readfirstlane(stgL_lds + (uint32_t)(buf * OWGS_WL + 64 * k) * 4u));
-#pragma unroll
-        for (int k = 0; k < OWGS_WL / 64; ++k) {
-            int64_t i = c0 + lane + 64 * k;
-            i = i < last ? i : last;
-            lds_dma16(&A.rec[i], __builtin_amdgcn_readfirstlane(stgA_lds + (uint32_t)(buf * OWGS_WL + 64 * k) * 16u));
-            if (A.relpos)
-                lds_dma4(&A.relpos[i], __builtin_amdgcn_readfirstlane(stgX_lds + (uint32_t)(buf * OWGS_WL + 64 * k) * 4u));
+        for (int k = 0; k < OWGS_WROWS; ++k) {  // (a partial last row: its lanes past OWGS_WL stay idle)
+            const uint32_t mL = __builtin_amdgcn_readfirstlane(stgL_lds + (uint32_t)(buf * OWGS_WL + 64 * k) * 4u);
+            const uint32_t mA = __builtin_amdgcn_readfirstlane(stgA_lds + (uint32_t)(buf * OWGS_WL + 64 * k) * 16u);
+            const uint32_t mX = __builtin_amdgcn_readfirstlane(stgX_lds + (uint32_t)(buf * OWGS_WL + 64 * k) * 4u);
+            if (64 * k + lane < OWGS_WL) {
+                lds_dma4(&lx[lane + 64 * k], mL);
+                int64_t i = c0 + lane + 64 * k;
+                i = i < last ? i : last;
+                lds_dma16(&A.rec[i], mA);
+                if (A.relpos) lds_dma4(&A.relpos[i], mX);
+            }
         }
     };
     if (io) {
@@ -1674,6 +1681,8 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                     atomicMax(&fst[bk], (uint32_t)(OWGS_WL - li));
                     nextl[li] = (int)atomicExch(&bhead[bk], (uint32_t)(li + 1));
                     spc[li] = cons;
+                    // walk identity: the action, or the lane itself for explicit per-activation walks
+                    if (maxc > 1) skey[li] = make_uint2((uint32_t)slot, a != (int)OWGS_REC_NOACT ? (uint32_t)a : 0x80000000u | li);
                 }
                 if (act && maxc > 1 && kind == K_FALLBACK) atomicMin(&sc[SC_CFB + par], li);
                 if (own && li < OWGS_WL) spt[li] = part ? t : -1;
@@ -1707,7 +1716,17 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                         const int cfb = sc[SC_CFB + par];
                         if (kind == K_FALLBACK) kf = first && cfb >= li;
                         else kf = fit && cfb > li;
-                        if (pk1 > f) kf = false;  // an earlier lane of this pass has the same fqn, another walk
+                        // an earlier lane of this pass has the same fqn under another action (another walk): its
+                        // unit at t shifts this lane's unit index (and memory take) -- uncertain when one of them
+                        // shares the target (a shared earlier walk step is caught at that lane)
+                        if (kf && pk1 > f) {
+                            for (int j = (int)bhead[bk] - 1; j >= 0; j = nextl[j] - 1)
+                                if (j >= f && j < li && spt[j] == t) {
+                                    const uint2 kj = skey[j];
+                                    const uint32_t wid = a != (int)OWGS_REC_NOACT ? (uint32_t)a : 0x80000000u | li;
+                                    if (kj.x == (uint32_t)slot && kj.y != wid) kf = false;
+                                }
+                        }
                     }
                     nf = !kf;
 #ifdef OWGS_STOP_REASONS

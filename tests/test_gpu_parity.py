@@ -181,6 +181,17 @@ def test_stream_parity(name, n):
     check_stream(w)
 
 
+@pytest.mark.parametrize("kw", [dict(shared_frac=0.6, conc_frac=0.6, n_actions=2000, n_invokers=2000),
+                                dict(shared_frac=0.5, conc_frac=0.4, n_actions=500, n_invokers=300, conc_range=(2, 8)),
+                                dict(shared_frac=0.3, conc_frac=1.0, n_actions=300, n_invokers=1000,
+                                     unhealthy_frac=0.2, load=1.3)])
+def test_stream_parity_shared_keys(kw):
+    # many fqn@version keys shared by several actions (different walks, one NestedSemaphore entry per invoker):
+    # stresses the shared-key validation rule, the kept concurrent speculation and concurrent forced acquires
+    w = W.config("headline", n_activations=120_000, **kw)
+    check_stream(w)
+
+
 def test_stream_parity_literal_zombie_oracle():
     # the literal oracle (entries created on failed tries, NS:61-62) gives the same answers on valid streams
     w = W.config("c4", n_activations=50_000)
