@@ -36,10 +36,10 @@
 
 // --------------------------------------------------------------------------------------------- engine geometry
 #ifndef OWGS_EW
-#define OWGS_EW 8                      // engine waves per workgroup (two per SIMD: one issues while the other waits)
+#define OWGS_EW 7                      // engine waves (+ the I/O wave: two waves per SIMD, 256 VGPRs each)
 #endif
 #ifndef OWGS_LPW
-#define OWGS_LPW 32                    // activations per engine wave (the other lanes serve the wave-wide walks)
+#define OWGS_LPW 48                    // activations per engine wave (all 64 lanes serve the wave-wide walks)
 #endif
 #define OWGS_ENT (OWGS_EW * 64)        // engine threads
 #define OWGS_WL (OWGS_EW * OWGS_LPW)   // chunk width: activations resolved together (one per engine lane)
@@ -150,6 +150,7 @@ struct OwgsEngineArgs {
     unsigned long long* stats;
     int32_t* err;
     int32_t opts;                // diagnostics (env OWGS_OPTS): bit0 = no hot-action rank tables
+    int32_t cw;                  // chunk width of this replay (<= OWGS_WL)
 };
 
 // generateHash(namespace, action) for n actions: out[i] = abs(h(ns_i) ^ h(path_i)), Int.MinValue kept (SCPB:370-372).
@@ -191,6 +192,7 @@ struct OwgsPrepassArgs {
     const int32_t* xslot;        // explicit walks: [n_act]
     uint4* rec;                  // out [n_act]: chunk lanes in class order (maxConcurrent == 1 first)
     uint32_t* lix;               // out [n_chunks][OWGS_WL]: stream lane | first lane of its action << 16
+    int32_t cw;                  // chunk width (<= OWGS_WL)
 };
 
 struct OwgsRelposArgs {

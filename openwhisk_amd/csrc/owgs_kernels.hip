@@ -99,6 +99,16 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
 #endif
 static_assert(OWGS_WL < HOT_CONC, "pk1 and the concurrent hot marker share the 10-bit ext field");
 #define OWGS_WROWS ((OWGS_WL + 63) / 64)  // wave rows the I/O wave stages per chunk
+// a chunk of len lanes is spread evenly over the engine waves: wave w holds record positions
+// [wave_off(len, w), wave_off(len, w) + wave_cap(len, w)) in its lanes 0.. (positions stay dense below len)
+__host__ __device__ inline int wave_cap(int len, int w) {
+    const int b = len / OWGS_EW, r = len % OWGS_EW;
+    return min(OWGS_LPW, b + (w < r ? 1 : 0));
+}
+__host__ __device__ inline int wave_off(int len, int w) {
+    const int b = len / OWGS_EW, r = len % OWGS_EW;
+    return w * b + min(w, r);
+}
 
 // ------------------------------------------------------------------------------------------------ helpers
 __device__ __forceinline__ u64 splitmix64(u64 x) {
@@ -437,14 +447,15 @@ __global__ __launch_bounds__(256) void owgs_prepare_kernel(OwgsPrepArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------ pre-pass
-// first chunk of each batch: cstart[b] = sum over b' < b of ceil(n_b' / OWGS_WL)
-__global__ __launch_bounds__(64) void owgs_chunks_kernel(const int64_t* acq_off, int32_t n_batches, int32_t* cstart) {
+// first chunk of each batch: cstart[b] = sum over b' < b of ceil(n_b' / cw), cw = the replay's chunk width
+__global__ __launch_bounds__(64) void owgs_chunks_kernel(const int64_t* acq_off, int32_t n_batches, int32_t cw,
+                                                         int32_t* cstart) {
     if (threadIdx.x != 0) return;
     int32_t c = 0;
     for (int b = 0; b < n_batches; ++b) {
         cstart[b] = c;
         const int64_t n = acq_off[b + 1] - acq_off[b];
-        c += (int32_t)((n + OWGS_WL - 1) / OWGS_WL);
+        c += (int32_t)((n + cw - 1) / cw);
     }
     cstart[n_batches] = c;
 }
@@ -462,8 +473,8 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
         else hi = mid - 1;
     }
     const int b = lo;
-    const int64_t c0 = A.acq_off[b] + (int64_t)(g - A.cstart[b]) * OWGS_WL;
-    const int len = (int)min((int64_t)OWGS_WL, A.acq_off[b + 1] - c0);
+    const int64_t c0 = A.acq_off[b] + (int64_t)(g - A.cstart[b]) * A.cw;
+    const int len = (int)min((int64_t)A.cw, A.acq_off[b + 1] - c0);
     const int t = threadIdx.x;
     uint2 meta = make_uint2(0, 0);
     int a = -1, slot = 0;
@@ -522,61 +533,49 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
     const int cls = (hs != OWGS_REC_NOHOT || (meta.y & (OWGS_AM_THROW | OWGS_AM_EMPTY))) ? 1 : (mc > 1 ? 2 : 0);
     s_p[t] = t < len ? cls : 3;
     __syncthreads();
-    if (len == OWGS_WL && t == 0) {
-        // full chunk: the concurrent lanes are spread round-robin over the waves left after the maxConcurrent == 1
-        // walkers, and the lanes without a walk fill the gaps (from the last wave down), so the waves that run the
-        // concurrent path hold fewer of them (a wave takes as long as its slowest lane)
-        int cnt[OWGS_EW];
-        int n0 = 0, n2 = 0;
-        for (int w = 0; w < OWGS_EW; ++w) cnt[w] = 0;
-        for (int j = 0; j < len; ++j) {
-            n0 += s_p[j] == 0;
-            n2 += s_p[j] == 2;
+    if (t == 0) {
+        // the maxConcurrent == 1 walkers fill the first waves; the concurrent lanes are spread round-robin over the
+        // remaining waves and the lanes without a walk fill the gaps (from the last wave down), so the waves that
+        // run the concurrent path hold fewer of them (a wave takes as long as its slowest lane).  Wave w holds
+        // positions [wave_off(len, w), + wave_cap(len, w)): the chunk spread evenly, positions dense below len.
+        int cnt[OWGS_EW], cap[OWGS_EW];
+        int n0 = 0, nwv = 0;
+        for (int w = 0; w < OWGS_EW; ++w) {
+            cnt[w] = 0;
+            cap[w] = wave_cap(len, w);
+            nwv += cap[w] > 0;
         }
-        const int f0 = (n0 + OWGS_LPW - 1) / OWGS_LPW, R = OWGS_EW - f0;
+        for (int j = 0; j < len; ++j) n0 += s_p[j] == 0;
+        int f0 = 0, acc0 = 0;  // waves the maxConcurrent == 1 walkers fill
+        while (f0 < nwv && acc0 < n0) acc0 += cap[f0++];
+        const int R = max(nwv - f0, 1);
         int w0 = 0, rr = 0;
         for (int j = 0; j < len; ++j)
             if (s_p[j] == 0) {
-                while (cnt[w0] == OWGS_LPW) ++w0;
-                s_s[j] = w0 * OWGS_LPW + cnt[w0]++;
+                while (cnt[w0] == cap[w0]) ++w0;
+                s_s[j] = wave_off(len, w0) + cnt[w0]++;
             }
         for (int j = 0; j < len; ++j)
             if (s_p[j] == 2) {
                 int w = -1;
                 for (int k = 0; k < R && w < 0; ++k, ++rr) {
-                    const int c = OWGS_EW - 1 - (rr % R);
-                    if (cnt[c] < OWGS_LPW) w = c;
+                    const int c = nwv - 1 - (rr % R);
+                    if (cnt[c] < cap[c]) w = c;
                 }
-                for (int c = OWGS_EW - 1; c >= 0 && w < 0; --c)
-                    if (cnt[c] < OWGS_LPW) w = c;
-                s_s[j] = w * OWGS_LPW + cnt[w]++;
+                for (int c = nwv - 1; c >= 0 && w < 0; --c)
+                    if (cnt[c] < cap[c]) w = c;
+                s_s[j] = wave_off(len, w) + cnt[w]++;
             }
         for (int j = 0; j < len; ++j)
             if (s_p[j] == 1) {
-                int w = OWGS_EW - 1;
-                while (cnt[w] == OWGS_LPW) --w;
-                s_s[j] = w * OWGS_LPW + cnt[w]++;
+                int w = nwv - 1;
+                while (cnt[w] == cap[w]) --w;
+                s_s[j] = wave_off(len, w) + cnt[w]++;
             }
     }
     __syncthreads();
     if (t >= len) return;
-    int pos;
-    if (len == OWGS_WL) {
-        pos = s_s[t];
-    } else {  // short chunk (positions must stay below len): classes in order
-        int nb0 = 0, nb1 = 0, nb2 = 0, n0 = 0, n1 = 0;
-        for (int j = 0; j < len; ++j) {
-            const int cj = s_p[j];
-            n0 += cj == 0;
-            n1 += cj == 1;
-            if (j < t) {
-                nb0 += cj == 0;
-                nb1 += cj == 1;
-                nb2 += cj == 2;
-            }
-        }
-        pos = cls == 0 ? nb0 : cls == 1 ? n0 + nb1 : n0 + n1 + nb2;
-    }
+    const int pos = s_s[t];
     const int ext = mc > 1 ? (hs != OWGS_REC_NOHOT ? HOT_CONC + hs : pk1) : hs;  // 10 bits
     const uint32_t an = A.act ? (uint32_t)a : OWGS_REC_NOACT;
     uint4 r;
@@ -907,7 +906,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
         for (int k = 0; k < 2; ++k)
             if (io_locate(io_b, io_c0)) {
                 io_dma(io_c0, k, k);
-                io_c0 += OWGS_WL;
+                io_c0 += A.cw;
             }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         io_gather(0, 0);
@@ -1072,14 +1071,14 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
         PT(0);
         // ============================================================ publishes (SCPB:398-436, NS:32-91)
         const uint32_t btag = (uint32_t)(A.cur_tag0 + b + 1) & 0x1FFFFu;  // HBM cursors written in this batch
-        for (int64_t c0 = a_beg; c0 < a_end; c0 += OWGS_WL, ++g) {
-            const int len = (int)min((int64_t)OWGS_WL, a_end - c0);
+        for (int64_t c0 = a_beg; c0 < a_end; c0 += A.cw, ++g) {
+            const int len = (int)min((int64_t)A.cw, a_end - c0);
             ++st_chunk;
             // ---- lane record: the pre-pass dealt the chunk's records by class (maxConcurrent == 1 first), so a wave
             // mostly runs one speculation path; li = the lane's index in the stream order of the chunk
-            const bool own = !io && lane < OWGS_LPW;  // this thread holds an activation of the chunk
-            const int sl = wave * OWGS_LPW + lane;    // record position
-            const bool held = own && sl < len;
+            const bool own = !io && lane < OWGS_LPW;  // this thread may hold an activation of the chunk
+            const bool held = !io && lane < wave_cap(len, wave);
+            const int sl = held ? wave_off(len, wave) + lane : 0;  // record position
             const int sbuf = g % OWGS_NSTG;
             const int lx = held ? (int)stgL[sbuf * OWGS_WL + sl] : 0;
             const int li = held ? (lx & 0xFFFF) : OWGS_WL;
@@ -1161,7 +1160,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 io_gather((g + 1) % OWGS_NSTG, (g + 1) & 1);
                 if (io_locate(io_b, io_c0)) {
                     io_dma(io_c0, (g + 2) % OWGS_NSTG, g + 2);
-                    io_c0 += OWGS_WL;
+                    io_c0 += A.cw;
                 }
             }
 
@@ -1609,7 +1608,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
 #endif
                 lds_sync();
                 PT(2);  // hot tables written; every wave has finished reading P for its speculation
-                if (own) cdirty[par * OWGS_WL + sl] = 0;  // read above; the commit of this pass fills the other half
+                if (tid < OWGS_WL) cdirty[par * OWGS_WL + tid] = 0;  // read above; this pass's commit fills the other half
 #ifdef OWGS_PROFILE
                 if (tid == 0) {
                     int worst = 0, wmax = -1;
@@ -2022,7 +2021,7 @@ extern "C" hipError_t owgs_launch_prepare(const OwgsPrepArgs* a, hipStream_t s) 
 // chunk table + per-activation records; max_chunks >= sum of ceil(n_b / OWGS_WL)
 extern "C" hipError_t owgs_launch_prepass(const OwgsPrepassArgs* a, int32_t* cstart, int64_t max_chunks,
                                           hipStream_t s) {
-    hipLaunchKernelGGL(owgs_chunks_kernel, dim3(1), dim3(64), 0, s, a->acq_off, a->n_batches, cstart);
+    hipLaunchKernelGGL(owgs_chunks_kernel, dim3(1), dim3(64), 0, s, a->acq_off, a->n_batches, a->cw, cstart);
     if (max_chunks <= 0) return hipGetLastError();
     OwgsPrepassArgs b = *a;
     b.cstart = cstart;
