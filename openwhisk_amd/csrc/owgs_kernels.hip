@@ -90,9 +90,13 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
 // capacity prefix once and writes the target of each rank 0..HOT_RANKS-1 into the slot's table, so the action's
 // lanes do not walk one by one.  The rec "ext" field holds the slot (maxConcurrent == 1: slot or OWGS_REC_NOHOT;
 // maxConcurrent > 1: pk1 + 1 <= OWGS_WL, or HOT_CONC + slot)
+#ifndef NHOT
 #define NHOT 16
+#endif
 #define HOT_RANKS 64
+#ifndef HOT_MIN
 #define HOT_MIN 6
+#endif
 #define HOT_CONC 0x3E0
 #ifndef HOT_CONC_ON
 #define HOT_CONC_ON 0  // concurrent hot tables: measured slower (their walks re-run every pass), kept as an option
@@ -1746,6 +1750,9 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 PT(4);
                 // ------------------------------------------------ commit lanes [f, l)
                 int l = sc[SC_LMIN + par];
+#ifdef OWGS_PROF_COMMIT
+                const u64 tc0 = memtime_pinned();
+#endif
                 if (l <= f) {  // the frontier lane is always exact; never loop without progress
                     l = f + 1;
                     err |= OWGS_ERR_INTERNAL;
@@ -1755,9 +1762,12 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
 #endif
                 if (act && li < l) {
                     const int outv = kind == K_NONE ? OWGS_NONE_V : (kind == K_THROW ? OWGS_THROW_V : t);
+#ifndef OWGS_EXP_NOSTORE
                     A.out_inv[i] = outv;
                     A.out_flags[i] = kind == K_FALLBACK ? 1 : 0;
+#endif
                     if (kind == K_FALLBACK) ++st_fb;
+#ifndef OWGS_EXP_NOSTORE
                     if (relx >= 0) {
                         if (maxc == 1) {
                             if (outv >= 0)
@@ -1768,6 +1778,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                                                          (uint32_t)slot | ((uint32_t)maxc << 17));
                         }
                     }
+#endif
                     // walk cursor + chunk rank base, written by the last committed lane of the action
                     if (a != (int)OWGS_REC_NOACT && (nxt == (int)OWGS_REC_NONEXT || nxt >= l)) {
                         uint32_t ns = cw & 0x7FFFu;
@@ -1809,6 +1820,9 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                     if (kind == K_FALLBACK && maxc == 1 && r == 0) atomicMin(&sc[pool ? SC_U1 : SC_U0], mem - 1);
                     pending = false;
                 }
+#ifdef OWGS_PROF_COMMIT
+                const u64 tc1 = memtime_pinned();
+#endif
                 if (part) {
                     if (li >= l && cons) atomicAdd(&P[t], cons);  // not committed: give the memory back
                     fst[bk] = 0u;
@@ -1820,6 +1834,13 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                     if (!keep && maxc > 1) cdirty[(par ^ 1) * OWGS_WL + lead] = 1;
                 }
                 if (io && l >= len) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk g+1 staged
+#ifdef OWGS_PROF_COMMIT
+                if (!io && lane == 0) {
+                    const u64 tc2 = memtime_pinned();
+                    atomicMax(&pfw[0], (int)(tc1 - tc0));
+                    atomicMax(&pfw[1], (int)(tc2 - tc1));
+                }
+#endif
                 if (tid == 0) {
                     sc[SC_NHOT] = 0;  // read at the chunk start, before this pass's barriers
                     sc[SC_LMIN + (par ^ 1)] = OWGS_WL;
@@ -1829,7 +1850,16 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 lds_sync();
                 PT(5);
 #ifdef OWGS_PROFILE
+#ifdef OWGS_PROF_COMMIT
+                if (tid == 0) {  // slowest wave: committing lanes, giving back and resetting
+                    pt_x[0] += (u64)pfw[0];
+                    pt_x[1] += (u64)pfw[1];
+                    pfw[0] = 0;
+                    pfw[1] = 0;
+                }
+#else
                 if (tid == 0) pt_x[f == 0 ? 0 : 1] += memtime_pinned() - tpass0;  // first vs repeated passes
+#endif
 #endif
                 f = l;
                 par ^= 1;
