@@ -151,6 +151,7 @@ struct OwgsEngineArgs {
     int32_t* err;
     int32_t opts;                // diagnostics (env OWGS_OPTS): bit0 = no hot-action rank tables
     int32_t cw;                  // chunk width of this replay (<= OWGS_WL)
+    unsigned long long* trace;   // diagnostic build only (-DOWGS_TRACE): [waves][OWGS_TRACE_CAP] barrier timeline
 };
 
 // generateHash(namespace, action) for n actions: out[i] = abs(h(ns_i) ^ h(path_i)), Int.MinValue kept (SCPB:370-372).
@@ -193,6 +194,7 @@ struct OwgsPrepassArgs {
     uint4* rec;                  // out [n_act]: chunk lanes in class order (maxConcurrent == 1 first)
     uint32_t* lix;               // out [n_chunks][OWGS_WL]: stream lane | first lane of its action << 16
     int32_t cw;                  // chunk width (<= OWGS_WL)
+    int32_t deal;                // lane dealing strategy (diagnostics, env OWGS_DEAL; 0 = default)
 };
 
 struct OwgsRelposArgs {

@@ -52,13 +52,15 @@ typedef unsigned long long u64;
 #define CAPMAX 1024  // capacities are clamped: a lane's rank is < OWGS_WL
 
 // diagnostic build (-DOWGS_PROFILE, libowgs_prof.so): s_memtime cycle accounting per engine phase into stats[8..15]
-#ifdef OWGS_PROFILE
+#if defined(OWGS_PROFILE) || defined(OWGS_TRACE)
 // a timestamp the compiler can neither merge with another nor move out of its branch
 __device__ __forceinline__ unsigned long long memtime_pinned() {
     unsigned long long t;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
     return t;
 }
+#endif
+#ifdef OWGS_PROFILE
 #define PT_DECL                 \
     u64 pt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
     u64 pt_x[2] = {0, 0};                     \
@@ -550,32 +552,67 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
             nwv += cap[w] > 0;
         }
         for (int j = 0; j < len; ++j) n0 += s_p[j] == 0;
+        // place the class-c lanes round-robin over waves [wlo, whi) (skipping full ones), spilling anywhere
+        auto deal = [&](int c, int wlo, int whi) {
+            int rr = 0;
+            const int span = max(whi - wlo, 1);
+            for (int j = 0; j < len; ++j)
+                if (s_p[j] == c) {
+                    int w = -1;
+                    for (int k = 0; k < span && w < 0; ++k, ++rr) {
+                        const int cw_ = wlo + (rr % span);
+                        if (cw_ < nwv && cnt[cw_] < cap[cw_]) w = cw_;
+                    }
+                    for (int q = nwv - 1; q >= 0 && w < 0; --q)
+                        if (cnt[q] < cap[q]) w = q;
+                    s_s[j] = wave_off(len, w) + cnt[w]++;
+                }
+        };
+        auto fill = [&](int c, bool from_back) {  // contiguous, first free slot
+            for (int j = 0; j < len; ++j)
+                if (s_p[j] == c) {
+                    int w = from_back ? nwv - 1 : 0;
+                    if (from_back) while (cnt[w] == cap[w]) --w;
+                    else while (cnt[w] == cap[w]) ++w;
+                    s_s[j] = wave_off(len, w) + cnt[w]++;
+                }
+        };
+        int n1 = 0, n2 = 0;
+        for (int j = 0; j < len; ++j) {
+            n1 += s_p[j] == 1;
+            n2 += s_p[j] == 2;
+        }
         int f0 = 0, acc0 = 0;  // waves the maxConcurrent == 1 walkers fill
         while (f0 < nwv && acc0 < n0) acc0 += cap[f0++];
-        const int R = max(nwv - f0, 1);
-        int w0 = 0, rr = 0;
-        for (int j = 0; j < len; ++j)
-            if (s_p[j] == 0) {
-                while (cnt[w0] == cap[w0]) ++w0;
-                s_s[j] = wave_off(len, w0) + cnt[w0]++;
-            }
-        for (int j = 0; j < len; ++j)
-            if (s_p[j] == 2) {
-                int w = -1;
-                for (int k = 0; k < R && w < 0; ++k, ++rr) {
-                    const int c = nwv - 1 - (rr % R);
-                    if (cnt[c] < cap[c]) w = c;
-                }
-                for (int c = nwv - 1; c >= 0 && w < 0; --c)
-                    if (cnt[c] < cap[c]) w = c;
-                s_s[j] = wave_off(len, w) + cnt[w]++;
-            }
-        for (int j = 0; j < len; ++j)
-            if (s_p[j] == 1) {
-                int w = nwv - 1;
-                while (cnt[w] == cap[w]) --w;
-                s_s[j] = wave_off(len, w) + cnt[w]++;
-            }
+        // the host picks the strategy per replay (owgs_host.cpp, chunk_width): 1 for large pools, 2 for small ones
+        const int mode = A.deal;
+        if (mode == 1) {  // walkers and walk-free lanes share the front waves; concurrent lanes packed at the back
+            int f2 = 0, acc2 = 0;
+            while (f2 < nwv && acc2 < n2) acc2 += cap[nwv - 1 - f2++];
+            deal(2, nwv - f2, nwv);
+            deal(0, 0, max(nwv - f2, 1));
+            fill(1, false);
+        } else if (mode == 2) {  // every class spread over every wave
+            deal(2, 0, nwv);
+            deal(0, 0, nwv);
+            fill(1, false);
+        } else if (mode == 4 || mode == 5) {  // concurrent lanes over (2|3) x the waves they need, then walkers
+            int f2 = 0, acc2 = 0;
+            while (f2 < nwv && acc2 < n2) acc2 += cap[nwv - 1 - f2++];
+            const int k2 = min(nwv, (mode == 4 ? 2 : 3) * f2);
+            deal(2, nwv - k2, nwv);
+            deal(0, 0, nwv);
+            fill(1, false);
+        } else if (mode == 3) {  // concurrent lanes spread over every wave, walkers from the front
+            deal(2, 0, nwv);
+            fill(0, false);
+            fill(1, false);
+        } else {
+            fill(0, false);
+            deal(2, f0, nwv);
+            fill(1, true);
+        }
+        (void)n1;
     }
     __syncthreads();
     if (t >= len) return;
@@ -771,6 +808,27 @@ __device__ __forceinline__ void lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// diagnostic build (-DOWGS_TRACE): every wave logs {barrier id, arrival, departure} of the pass-loop barriers into
+// A.trace[wave][OWGS_TRACE_CAP] (u64 pairs), for a timeline of which wave arrives last at each barrier
+#ifndef OWGS_TRACE_CAP
+#define OWGS_TRACE_CAP 16384
+#endif
+#ifdef OWGS_TRACE
+#define LDS_SYNC_T(id)                                                                               \
+    {                                                                                                \
+        const u64 ta_ = memtime_pinned();                                                            \
+        lds_sync();                                                                                  \
+        const u64 td_ = memtime_pinned();                                                            \
+        if (lane == 0 && tr_n < OWGS_TRACE_CAP) {                                                    \
+            A.trace[2 * ((size_t)wave * OWGS_TRACE_CAP + tr_n)] = ((u64)(id) << 56) | (ta_ & ((1ull << 56) - 1)); \
+            A.trace[2 * ((size_t)wave * OWGS_TRACE_CAP + tr_n) + 1] = td_;                           \
+        }                                                                                            \
+        ++tr_n;                                                                                      \
+    }
+#else
+#define LDS_SYNC_T(id) lds_sync()
+#endif
+
 __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs A) {
     extern __shared__ uint4 lds_raw[];
     char* L = (char*)lds_raw;
@@ -856,6 +914,9 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
     E.nb = nb;
 
     uint32_t st_pass = 0, st_probe = 0, st_fb = 0, st_long = 0, st_chunk = 0, st_stop = 0, st_gprobe = 0, st_glane = 0;
+#ifdef OWGS_TRACE
+    int tr_n = 0;
+#endif
     PT_DECL
 
     // ---------------------------------------------------------------- I/O wave: chunk prefetch pipeline
@@ -1157,7 +1218,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 }
                 if (nxt == (int)OWGS_REC_NONEXT) hocc[hs] = occ;
             }
-            lds_sync();
+            LDS_SYNC_T(1);
             const int nhot = sc[SC_NHOT];
             // ---- I/O wave: cursors of chunk g+1, records of chunk g+2
             if (io) {
@@ -1610,7 +1671,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                     pfw[2 * wave + 1] = pf_gw;
                 }
 #endif
-                lds_sync();
+                LDS_SYNC_T(2);
                 PT(2);  // hot tables written; every wave has finished reading P for its speculation
                 if (tid < OWGS_WL) cdirty[par * OWGS_WL + tid] = 0;  // read above; this pass's commit fills the other half
 #ifdef OWGS_PROFILE
@@ -1689,7 +1750,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                 }
                 if (act && maxc > 1 && kind == K_FALLBACK) atomicMin(&sc[SC_CFB + par], li);
                 if (own && li < OWGS_WL) spt[li] = part ? t : -1;
-                lds_sync();
+                LDS_SYNC_T(3);
                 // (fallback+buckets accrue to PT(6));
                 PT(3);
                 // ------------------------------------------------ validate: known to fit?
@@ -1746,7 +1807,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                         if (lane == 0) atomicMin(&sc[SC_LMIN + par], lm);
                     }
                 }
-                lds_sync();
+                LDS_SYNC_T(4);
                 PT(4);
                 // ------------------------------------------------ commit lanes [f, l)
                 int l = sc[SC_LMIN + par];
@@ -1847,7 +1908,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                     sc[SC_CFB + (par ^ 1)] = OWGS_WL;
                     if (l < len) ++st_stop;
                 }
-                lds_sync();
+                LDS_SYNC_T(5);
                 PT(5);
 #ifdef OWGS_PROFILE
 #ifdef OWGS_PROF_COMMIT
