@@ -248,6 +248,43 @@ __device__ __forceinline__ int ct_findv_from(const uint2* ct, uint32_t key, uint
 __device__ __forceinline__ int ct_findv(const uint2* ct, uint32_t key, uint32_t* val) {
     return ct_findv_from(ct, key, ct_home(key), val);
 }
+// find-or-insert with block reads: the key's index, inserting it into the first deleted or empty entry of its chain
+// when absent (concurrent inserters of different keys race by CAS and rescan); *fresh = a new entry took an empty one
+__device__ __forceinline__ int ct_upsertv(uint2* ct, uint32_t key, int* fresh) {
+    *fresh = 0;
+    for (int attempt = 0; attempt < OWGS_CTC; ++attempt) {
+        uint32_t h = ct_home(key);
+        int freei = -1;
+        uint32_t freek = 0;
+        bool ended = false;
+        for (int p = 0; p < OWGS_CTC / CT_BLK && !ended; ++p) {
+            const uint4 e01 = *(const uint4*)&ct[h];
+            const uint4 e23 = *(const uint4*)&ct[h + 2];
+            const uint32_t ks[4] = {e01.x, e01.z, e23.x, e23.z};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (ended) break;
+                if (ks[q] == key) return (int)h + q;
+                if (ks[q] == 0u || ks[q] == OWGS_CT_TOMB) {
+                    if (freei < 0) {
+                        freei = (int)h + q;
+                        freek = ks[q];
+                    }
+                    if (ks[q] == 0u) ended = true;  // the key is absent
+                }
+            }
+            h = (h + CT_BLK) & (OWGS_CTC - 1);
+        }
+        if (freei < 0) return -1;  // full
+        if (atomicCAS((uint32_t*)&ct[freei], freek, key) == freek) {
+            *fresh = freek == 0u;
+            return freei;
+        }
+        // lost the entry to another inserter: rescan (the key may have been inserted by nobody else: it is this
+        // lane's group)
+    }
+    return -1;
+}
 __device__ __forceinline__ int ct_insertv(uint2* ct, uint32_t key, int* fresh) {
     uint32_t h = ct_home(key);
     for (int p = 0; p < OWGS_CTC;) {
@@ -1864,13 +1901,9 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                             const int ops1 = ops0 + jn;
                             if (ops1 > OWGS_MAX_OPS) err |= OWGS_ERR_OPS;
                             int ix = cidx;
-                            if (ix < 0) {  // absent when speculated; a kept lane's group may have created it since
-                                uint32_t v0;
-                                ix = ct_findv(ct, ct_key(t, slot), &v0);
-                            }
-                            if (ix < 0) {
+                            if (ix < 0) {  // absent when speculated (a kept lane's group may have created it since)
                                 int fresh = 0;
-                                ix = ct_insertv(ct, ct_key(t, slot), &fresh);
+                                ix = ct_upsertv(ct, ct_key(t, slot), &fresh);
                                 if (fresh) atomicAdd(&sc[SC_USED], 1);
                             }
                             if (ix < 0) err |= OWGS_ERR_CTAB_FULL;
