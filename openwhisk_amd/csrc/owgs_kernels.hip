@@ -49,6 +49,9 @@ typedef unsigned long long u64;
 #ifndef KPROBE_G
 #define KPROBE_G 4  // same for the general path (concurrency lookups per step)
 #endif
+#ifndef FGRP
+#define FGRP 4  // walk steps per group of the maxConcurrent == 1 fast path (their reads issue together)
+#endif
 #define CAPMAX 1024  // capacities are clamped: a lane's rank is < OWGS_WL
 
 // diagnostic build (-DOWGS_PROFILE, libowgs_prof.so): s_memtime cycle accounting per engine phase into stats[8..15]
@@ -1433,38 +1436,39 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                                 const int base = pool ? A.n_ids - nb : 0;
                                 bool done = false;
 #pragma unroll 1
-                                for (int g4 = 0; g4 < KPROBE / 4; ++g4) {
+                                for (int g4 = 0; g4 < KPROBE / FGRP; ++g4) {
                                     if (done) break;
-                                    int ps[4], pv[4];
+                                    int ps[FGRP], pv[FGRP];
                                     int pp = pos;
 #pragma unroll
-                                    for (int k = 0; k < 4; ++k) {
+                                    for (int k = 0; k < FGRP; ++k) {
                                         ps[k] = pp;
                                         pv[k] = P[base + pp];  // usable flag folded in (OWGS_PENC)
                                         pp += step;
                                         pp -= pp >= n ? n : 0;
                                     }
 #pragma unroll
-                                    for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(pv[k]));  // 4 reads in flight
-                                    // branch-free scan of the 4 steps: first step whose cumulative capacity exceeds
-                                    // the rank (hit), or the end of the walk (s + k == n: every position probed)
-                                    int hit = 4, kc = cum, hc = cum;
+                                    for (int k = 0; k < FGRP; ++k) asm volatile("" : "+v"(pv[k]));  // reads in flight
+                                    // branch-free scan of the group's steps: first step whose cumulative capacity
+                                    // exceeds the rank (hit), or the end of the walk (s + k == n: every position probed)
+                                    int hit = FGRP, kc = cum, hc = cum, tsel = ps[0];
                                     bool ended = false;
 #pragma unroll
-                                    for (int k = 0; k < 4; ++k) {
+                                    for (int k = 0; k < FGRP; ++k) {
                                         const int cap = pv[k] < OWGS_PLIM ? cap_bf(pv[k], mem, rm) : 0;
-                                        const bool open = hit == 4 && !ended;
+                                        const bool open = hit == FGRP && !ended;
                                         const bool fin = open && s + k >= n;
                                         const bool h = open && !fin && kc + cap > r;
                                         ended = ended || fin;
                                         hit = h ? k : hit;
                                         hc = h ? kc : hc;
+                                        tsel = h ? ps[k] : tsel;
                                         kc += (open && !fin && !h) ? cap : 0;
                                     }
-                                    st_probe += 4;
-                                    if (hit < 4) {
+                                    st_probe += FGRP;
+                                    if (hit < FGRP) {
                                         kind = K_TARGET;
-                                        t = base + (hit == 0 ? ps[0] : hit == 1 ? ps[1] : hit == 2 ? ps[2] : ps[3]);
+                                        t = base + tsel;
                                         ks = r - hc;
                                         s_t = s + hit;
                                         done = true;
@@ -1473,7 +1477,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                                         done = true;
                                     } else {
                                         cum = kc;
-                                        s += 4;
+                                        s += FGRP;
                                         pos = pp;
                                     }
                                 }
@@ -1720,6 +1724,13 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                     }
                     pt_acc[6] += (u64)spw[4 * worst];       // worst wave: hot walks
                     pt_acc[7] += (u64)spw[4 * worst + 1];   // worst wave: per-lane speculation
+#ifdef OWGS_PROF_SPLIT
+                    if (f == 0)  // first passes, summed over the engine waves: hot walks | per-lane | long walks
+                        for (int w = 0; w < OWGS_EW; ++w) {
+                            pt_x[0] += (u64)spw[4 * w] | ((u64)spw[4 * w + 2] << 32);
+                            pt_x[1] += (u64)spw[4 * w + 1];
+                        }
+#endif
                 }
 #endif
                 if (spec && kind == K_HOT) {
@@ -1951,7 +1962,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                     pfw[0] = 0;
                     pfw[1] = 0;
                 }
-#else
+#elif !defined(OWGS_PROF_SPLIT)
                 if (tid == 0) pt_x[f == 0 ? 0 : 1] += memtime_pinned() - tpass0;  // first vs repeated passes
 #endif
 #endif
