@@ -865,8 +865,18 @@ __device__ __forceinline__ void lds_sync() {
         }                                                                                            \
         ++tr_n;                                                                                      \
     }
+#define TRACE_MARK(id)                                                                               \
+    {                                                                                                \
+        const u64 tm_ = memtime_pinned();                                                            \
+        if (lane == 0 && tr_n < OWGS_TRACE_CAP) {                                                    \
+            A.trace[2 * ((size_t)wave * OWGS_TRACE_CAP + tr_n)] = ((u64)(id) << 56) | (tm_ & ((1ull << 56) - 1)); \
+            A.trace[2 * ((size_t)wave * OWGS_TRACE_CAP + tr_n) + 1] = tm_;                           \
+        }                                                                                            \
+        ++tr_n;                                                                                      \
+    }
 #else
 #define LDS_SYNC_T(id) lds_sync()
+#define TRACE_MARK(id)
 #endif
 
 __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs A) {
@@ -1179,6 +1189,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
         for (int64_t c0 = a_beg; c0 < a_end; c0 += A.cw, ++g) {
             const int len = (int)min((int64_t)A.cw, a_end - c0);
             ++st_chunk;
+            TRACE_MARK(6);
             // ---- lane record: the pre-pass dealt the chunk's records by class (maxConcurrent == 1 first), so a wave
             // mostly runs one speculation path; li = the lane's index in the stream order of the chunk
             const bool own = !io && lane < OWGS_LPW;  // this thread may hold an activation of the chunk
@@ -1215,6 +1226,7 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
             const float rm = __builtin_amdgcn_rcpf((float)(mem > 0 ? mem : 1));
             const int64_t i = c0 + li;
             bool pending = valid;
+            TRACE_MARK(7);
             // walk cursor after a forced acquire of a concurrent action at invoker x: the walk had failed everywhere,
             // and the new container at x (maxConcurrent - 1 free slots) is the only step that became feasible, so the
             // next lanes start at x's step j = (pos(x) - home) * step^-1 mod n (identity pools; else from 0)
