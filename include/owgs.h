@@ -134,6 +134,12 @@ int owgs_key_id(owgs_ctx* ctx, int32_t action);
 int owgs_state_info(owgs_ctx* ctx, int32_t* n_invokers, int32_t* managed, int32_t* blackbox, int32_t* cluster_size);
 int owgs_step_sizes(owgs_ctx* ctx, int32_t pool, int32_t* out, int32_t cap, int32_t* n);
 
+/* Replaces: ShardingContainerPoolBalancer.pairwiseCoprimeNumbersUntil(x) (SCPB:379-384), the step-size table that
+ * updateInvokers (SCPB:525-527) rebuilds on the device; exposed for the reference's unit test
+ * (ShardingContainerPoolBalancerTests.scala:371-384).  Writes min(cap, n) values to out (may be NULL), n = list length.
+ * x > owgs_limits' pool range returns OWGS_ERANGE. */
+int owgs_pairwise_coprime(owgs_ctx* ctx, int32_t x, int32_t* out, int32_t cap, int32_t* n);
+
 /* Stream replay with HBM-resident buffers (bench / batching thread).  Batch b first releases the activations
  * rel_aid[rel_off[b]..rel_off[b+1]) (ids into this stream; their invoker is this stream's own earlier output),
  * then publishes activations [acq_off[b], acq_off[b+1]) with action act[i] and seq = seq_base + i.

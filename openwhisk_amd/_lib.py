@@ -84,6 +84,7 @@ def lib() -> C.CDLL:
         "owgs_key_id": (C.c_int, [P, i32]),
         "owgs_state_info": (C.c_int, [P, P, P, P, P]),
         "owgs_step_sizes": (C.c_int, [P, i32, P, i32, P]),
+        "owgs_pairwise_coprime": (C.c_int, [P, i32, P, i32, P]),
         "owgs_replay_device": (C.c_int, [P, i32, P, P, C.c_int64, P, P, C.c_int64, u64, P, P, P, P]),
         "owgs_replay": (C.c_int, [P, i32, P, P, P, P, u64, P, P, P]),
         "owgs_snapshot": (C.c_int, [P]),

@@ -126,6 +126,14 @@ class GpuShardingContainerPoolBalancer:
         self._chk(self._L.owgs_step_sizes(self._h, pool, _p(out), n.value, None))
         return out[: n.value].tolist()
 
+    def pairwise_coprime_numbers_until(self, x: int) -> list:
+        """ShardingContainerPoolBalancer.pairwiseCoprimeNumbersUntil (SCPB:379-384), computed by owgs_coprime_kernel."""
+        n = C.c_int32()
+        self._chk(self._L.owgs_pairwise_coprime(self._h, x, None, 0, C.byref(n)))
+        out = np.zeros(max(n.value, 1), dtype=np.int32)
+        self._chk(self._L.owgs_pairwise_coprime(self._h, x, _p(out), n.value, None))
+        return out[: n.value].tolist()
+
     @property
     def managed_step_sizes(self):
         return self._steps(0)

@@ -6,6 +6,7 @@
 // (owgs_kernels.hip).  No CPU fallback exists: without a HIP device every compute entry point fails.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -34,6 +35,13 @@ extern "C" hipError_t owgs_launch_relflags(const int64_t* rel_aid, int64_t n_rel
                                            uint8_t* rel_flags, hipStream_t s);
 extern "C" hipError_t owgs_launch_release_seq(const OwgsReleaseArgs* a, hipStream_t s);
 extern "C" hipError_t owgs_launch_engine(const OwgsEngineArgs* a, hipStream_t s);
+extern "C" int32_t owgs_coprime_max(void);
+extern "C" hipError_t owgs_launch_coprime(const int32_t* xs, int32_t n_pools, int32_t* out, int32_t out_stride,
+                                          int32_t* counts, hipStream_t s);
+extern "C" hipError_t owgs_launch_slots(const int64_t* mem_bytes, int32_t from, int32_t n, int32_t cluster,
+                                       int64_t min_bytes, int32_t* permits, hipStream_t s);
+extern "C" hipError_t owgs_launch_usable(const uint8_t* status, int32_t n, uint32_t* bits, int32_t n_words,
+                                        hipStream_t s);
 extern "C" size_t owgs_engine_lds_bytes(int n_slots, int pool_mode, int n_ids, int nm, int nb, int n_actions);
 
 namespace {
@@ -66,30 +74,6 @@ int32_t d2i(double d) {  // Scala Double.toInt
     return (int32_t)d;
 }
 
-int32_t gcd(int32_t a, int32_t b) {  // SCPB:375-376
-    while (b != 0) {
-        int32_t t = (b == -1) ? 0 : a % b;
-        a = b;
-        b = t;
-    }
-    return a;
-}
-
-std::vector<int32_t> pairwise_coprime(int32_t x) {  // SCPB:379-384
-    std::vector<int32_t> out;
-    for (int32_t cur = 1; cur <= x && cur > 0; ++cur) {
-        if (gcd(cur, x) != 1) continue;
-        bool ok = true;
-        for (int32_t v : out)
-            if (gcd(v, cur) != 1) {
-                ok = false;
-                break;
-            }
-        if (ok) out.push_back(cur);
-    }
-    return out;
-}
-
 }  // namespace
 struct owgs_ctx {
     owgs_config cfg{};
@@ -120,8 +104,11 @@ struct owgs_ctx {
     std::unordered_map<std::string, int32_t> slot_ids;
 
     // device state
-    DevBuf<int32_t> d_permits, d_pool_words, d_hlist, d_act_slot, d_act_hash, d_act_mem, d_act_maxc, d_msteps,
-        d_bsteps, d_err;
+    DevBuf<int32_t> d_permits, d_pool_words, d_hlist, d_act_slot, d_act_hash, d_act_mem, d_act_maxc, d_steps,
+        d_cpx, d_err;
+    int32_t steps_stride = 0;  // d_steps = [managed list | blackbox list], each steps_stride entries
+    DevBuf<int64_t> d_mem_bytes;  // userMemory of every invoker (updateCluster recomputes all slots from it)
+    DevBuf<uint8_t> d_status;
     DevBuf<uint32_t> d_usable, d_ct_keys, d_ct_vals, d_ct_tmp;
     DevBuf<uint8_t> d_act_bb, d_act_cok;
     DevBuf<uint2> d_act_meta;
@@ -159,12 +146,6 @@ struct owgs_ctx {
         hipError_t _e = (call);                                               \
         if (_e != hipSuccess) return (ctx)->fail(OWGS_EDEVICE, #call, _e);    \
     } while (0)
-
-static int32_t invoker_slot_mb(const owgs_ctx* c, int64_t mem_bytes) {  // SCPB:485-499, Size.scala:70,97-99
-    int64_t shard = mem_bytes / c->cluster;
-    if (shard < c->cfg.min_memory_bytes) shard = c->cfg.min_memory_bytes;
-    return (int32_t)(shard / 1024 / 1024);
-}
 
 template <class T>
 static hipError_t upload(DevBuf<T>& d, const T* h, size_t n, hipStream_t s) {
@@ -218,10 +199,11 @@ static int rebuild_pools(owgs_ctx* c) {
     c->hb = hcnt[1];
     c->pool_mode = identity ? 0 : 1;
     c->n_ids = N;
-    std::vector<uint32_t> bits((size_t)(N + 31) / 32 + 1, 0u);
-    for (int32_t i = 0; i < N; ++i)
-        if (c->status[i] == OWGS_HEALTHY) bits[(size_t)i >> 5] |= 1u << (i & 31);
-    HIPCHK(c, upload(c->d_usable, bits.data(), bits.size(), c->stream));
+    // usable bitmap built on the device from the status bytes (d_status mirrors c->status)
+    const int32_t n_words = (N + 31) / 32 + 1;
+    HIPCHK(c, c->d_usable.reserve((size_t)n_words));
+    HIPCHK(c, c->d_status.reserve((size_t)N));
+    HIPCHK(c, owgs_launch_usable(c->d_status.p, N, c->d_usable.p, n_words, c->stream));
     HIPCHK(c, upload(c->d_pool_words, words.data(), words.size(), c->stream));
     HIPCHK(c, upload(c->d_hlist, hl.data(), hl.size(), c->stream));
     return OWGS_OK;
@@ -230,8 +212,7 @@ static int rebuild_pools(owgs_ctx* c) {
 static int prepare_actions(owgs_ctx* c) {
     const int32_t n = (int32_t)c->a_mem.size();
     if (n == 0) return OWGS_OK;
-    HIPCHK(c, upload(c->d_msteps, c->msteps.data(), c->msteps.size(), c->stream));
-    HIPCHK(c, upload(c->d_bsteps, c->bsteps.data(), c->bsteps.size(), c->stream));
+    if (!c->d_steps.p) HIPCHK(c, c->d_steps.reserve(2));
     HIPCHK(c, c->d_act_meta.reserve(n));
     OwgsPrepArgs a{};
     a.hash = c->d_act_hash.p;
@@ -242,9 +223,9 @@ static int prepare_actions(owgs_ctx* c) {
     a.n = n;
     a.nm = c->nm;
     a.nb = c->nb;
-    a.msteps = c->d_msteps.p;
+    a.msteps = c->d_steps.p;
     a.n_msteps = (int32_t)c->msteps.size();
-    a.bsteps = c->d_bsteps.p;
+    a.bsteps = c->d_steps.p + c->steps_stride;
     a.n_bsteps = (int32_t)c->bsteps.size();
     a.act_meta = c->d_act_meta.p;
     HIPCHK(c, owgs_launch_prepare(&a, c->stream));
@@ -444,8 +425,6 @@ int owgs_create(const owgs_config* cfg, owgs_ctx** out) {
         owgs_destroy(c);
         return OWGS_EDEVICE;
     }
-    c->msteps = pairwise_coprime(0);
-    c->bsteps = pairwise_coprime(0);
     int rc = rebuild_pools(c);
     if (rc) {
         owgs_destroy(c);
@@ -462,7 +441,7 @@ void owgs_destroy(owgs_ctx* c) {
     (void)hipSetDevice(c->cfg.device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf<int32_t>* i32s[] = {&c->d_permits, &c->d_pool_words, &c->d_hlist, &c->d_act_slot, &c->d_act_hash,
-                               &c->d_act_mem,  &c->d_act_maxc,   &c->d_msteps, &c->d_bsteps,   &c->d_err,
+                               &c->d_act_mem,  &c->d_act_maxc,   &c->d_steps,  &c->d_cpx,     &c->d_err,
                                &c->d_a,        &c->d_b,          &c->d_c,      &c->d_d,        &c->d_out,
                                &c->d_cstart,   &c->d_relx,       &c->d_cpos,   &c->d_bsum,     &c->d_crel_off,
                                &c->d_acc,      &c->d_xslot,      &c->s_permits};
@@ -501,24 +480,44 @@ int owgs_update_invokers(owgs_ctx* c, int32_t n, const int32_t* ids, const int64
     if (managed < 1) managed = 1;
     int32_t blackboxes = d2i(std::floor((double)new_size * c->bf));
     if (blackboxes < 1) blackboxes = 1;
+    if (managed > owgs_coprime_max() || blackboxes > owgs_coprime_max())
+        return c->fail(OWGS_ERANGE, "pool larger than the step-size kernel's range");
     c->ids.assign(ids, ids + n);
     c->mem.assign(user_memory_bytes, user_memory_bytes + n);
     c->status.assign(status, status + n);
     c->managed = managed;
     c->blackboxes = blackboxes;
     c->pool_override[0] = c->pool_override[1] = false;
+    HIPCHK(c, upload(c->d_mem_bytes, user_memory_bytes, (size_t)n, c->stream));
+    HIPCHK(c, upload(c->d_status, status, (size_t)n, c->stream));
     if (old_size != new_size) {
-        c->msteps = pairwise_coprime(managed);
-        c->bsteps = pairwise_coprime(blackboxes);
+        // pairwiseCoprimeNumbersUntil(managed / blackboxes) on the device (owgs_state.hip), both pools in one launch
+        const int32_t stride = std::max(managed, blackboxes);
+        HIPCHK(c, c->d_steps.reserve((size_t)2 * stride));
+        HIPCHK(c, c->d_cpx.reserve(4));
+        int32_t xs[2] = {managed, blackboxes};
+        HIPCHK(c, hipMemcpyAsync(c->d_cpx.p, xs, sizeof(xs), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, owgs_launch_coprime(c->d_cpx.p, 2, c->d_steps.p, stride, c->d_cpx.p + 2, c->stream));
+        int32_t cnt[2];
+        HIPCHK(c, hipMemcpyAsync(cnt, c->d_cpx.p + 2, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        c->steps_stride = stride;
+        // host copies of the lists: introspection only (owgs_step_sizes); the prepare kernel reads d_steps
+        c->msteps.resize((size_t)cnt[0]);
+        c->bsteps.resize((size_t)cnt[1]);
+        if (cnt[0]) HIPCHK(c, hipMemcpyAsync(c->msteps.data(), c->d_steps.p, (size_t)cnt[0] * 4, hipMemcpyDeviceToHost, c->stream));
+        if (cnt[1])
+            HIPCHK(c, hipMemcpyAsync(c->bsteps.data(), c->d_steps.p + stride, (size_t)cnt[1] * 4, hipMemcpyDeviceToHost,
+                                     c->stream));
         if (old_size < new_size && n > c->n_slots) {
-            // keep existing semaphores; append NestedSemaphore(getInvokerSlot(userMemory).toMB) for new ones
-            std::vector<int32_t> tail;
-            for (int32_t i = c->n_slots; i < n; ++i) tail.push_back(invoker_slot_mb(c, c->mem[i]));
+            // keep existing semaphores; append NestedSemaphore(getInvokerSlot(userMemory).toMB) for the new ones
+            // (owgs_slots_kernel computes the tail in place)
             DevBuf<int32_t> nb;
             HIPCHK(c, nb.reserve((size_t)n));
             if (c->n_slots > 0)
                 HIPCHK(c, hipMemcpyAsync(nb.p, c->d_permits.p, (size_t)c->n_slots * 4, hipMemcpyDeviceToDevice, c->stream));
-            HIPCHK(c, hipMemcpyAsync(nb.p + c->n_slots, tail.data(), tail.size() * 4, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(c, owgs_launch_slots(c->d_mem_bytes.p, c->n_slots, n, c->cluster, c->cfg.min_memory_bytes, nb.p,
+                                        c->stream));
             HIPCHK(c, hipStreamSynchronize(c->stream));
             c->d_permits.release();
             c->d_permits = nb;
@@ -541,9 +540,9 @@ int owgs_update_cluster(owgs_ctx* c, int32_t new_size) {
     if (c->cluster == actual) return OWGS_OK;
     c->cluster = actual;
     const int32_t n = (int32_t)c->ids.size();
-    std::vector<int32_t> p(n);
-    for (int32_t i = 0; i < n; ++i) p[i] = invoker_slot_mb(c, c->mem[i]);
-    HIPCHK(c, upload(c->d_permits, p.data(), p.size(), c->stream));
+    HIPCHK(c, c->d_permits.reserve((size_t)n));
+    HIPCHK(c, owgs_launch_slots(c->d_mem_bytes.p, 0, n, c->cluster, c->cfg.min_memory_bytes, c->d_permits.p,
+                                c->stream));
     c->n_slots = n;
     int rc = reset_ctab(c);
     if (!rc) rc = rebuild_pools(c);
@@ -838,6 +837,24 @@ int owgs_step_sizes(owgs_ctx* c, int32_t pool, int32_t* out, int32_t cap, int32_
     return OWGS_OK;
 }
 
+int owgs_pairwise_coprime(owgs_ctx* c, int32_t x, int32_t* out, int32_t cap, int32_t* n) {
+    if (!c || cap < 0) return OWGS_EINVAL;
+    if (x > owgs_coprime_max()) return c->fail(OWGS_ERANGE, "x beyond the step-size kernel's range");
+    (void)hipSetDevice(c->cfg.device);
+    DevBuf<int32_t> d;
+    HIPCHK(c, d.reserve((size_t)std::max(x, 0) + 2));
+    HIPCHK(c, hipMemcpyAsync(d.p, &x, 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, owgs_launch_coprime(d.p, 1, d.p + 2, std::max(x, 1), d.p + 1, c->stream));
+    int32_t cnt = 0;
+    HIPCHK(c, hipMemcpyAsync(&cnt, d.p + 1, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (out && cap > 0 && cnt > 0)
+        HIPCHK(c, hipMemcpy(out, d.p + 2, (size_t)std::min(cap, cnt) * 4, hipMemcpyDeviceToHost));
+    if (n) *n = cnt;
+    d.release();
+    return OWGS_OK;
+}
+
 int owgs_replay_device(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const int32_t* act,
                        int64_t n_activations, const int64_t* rel_off, const int64_t* rel_aid, int64_t n_releases,
                        uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, uint8_t* rel_flags, void* stream) {
@@ -951,6 +968,8 @@ int owgs_update_health_device(owgs_ctx* c, int32_t n, const uint8_t* status_dev,
     (void)hipSetDevice(c->cfg.device);
     if (n) {
         HIPCHK(c, hipMemcpyAsync(c->status.data(), status_dev, (size_t)n, hipMemcpyDeviceToHost,
+                                 stream ? (hipStream_t)stream : c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->d_status.p, status_dev, (size_t)n, hipMemcpyDeviceToDevice,
                                  stream ? (hipStream_t)stream : c->stream));
         HIPCHK(c, hipStreamSynchronize(stream ? (hipStream_t)stream : c->stream));
     }

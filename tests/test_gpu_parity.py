@@ -261,3 +261,42 @@ def test_release_after_cluster_change_is_nosuchelement():
     rf = b.release_invoker(inv, [a])
     assert rf.tolist() == [1]
     assert b.permits().tolist() == [512, 512]
+
+
+# ----------------------------------------------------------------------------------------------- state updates (§8f-2)
+def test_pairwise_coprime_golden_on_gpu(golden):
+    b = gpu()
+    for x, exp in golden["pairwise_coprime_numbers_until"]["expect"].items():
+        assert b.pairwise_coprime_numbers_until(int(x)) == exp
+
+
+def test_pairwise_coprime_sweep_matches_oracle_fold():
+    """owgs_coprime_kernel (sieve + ordered compaction) == the literal greedy fold (SCPB:379-384) for every x."""
+    b = gpu()
+    xs = list(range(-2, 1300)) + [2310, 4096, 9000, 9001, 10000, 30030, 32767]
+    for x in xs:
+        assert b.pairwise_coprime_numbers_until(x) == O.pairwise_coprime_numbers_until(x), x
+    with pytest.raises(Exception):
+        b.pairwise_coprime_numbers_until(1 << 20)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_update_invokers_and_cluster_on_device_match_oracle(seed):
+    """Step sizes, grown slots (old ones kept) and updateCluster's re-created slots, 10k invokers (SCPB:512-584)."""
+    rng = np.random.default_rng(seed)
+    b = gpu(managed_fraction=0.9, blackbox_fraction=0.1)
+    o = O.BalancerState(managed_fraction=0.9, blackbox_fraction=0.1)
+    n_steps = [3000, 3000, 10000, 9999, 10000]
+    for n in n_steps:
+        ids = np.arange(n, dtype=np.int32)
+        mem = rng.choice([128, 256, 1000, 2048, 16384, 65536], size=n).astype(np.int64) * MB + rng.integers(0, MB, n)
+        st = rng.choice([HEALTHY, UNHEALTHY, OFFLINE], p=[0.9, 0.05, 0.05], size=n).astype(np.uint8)
+        b.update_invokers_arrays(ids, mem, st)
+        o.update_invokers(ids, mem, st)
+        assert b.managed_step_sizes == o.managed_step_sizes
+        assert b.blackbox_step_sizes == o.blackbox_step_sizes
+        assert np.array_equal(b.permits(), o.permits())
+        for size in (3, 8, 64, 1):
+            b.update_cluster(size)
+            o.update_cluster(size)
+            assert np.array_equal(b.permits(), o.permits()), (n, size)
