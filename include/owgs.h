@@ -153,6 +153,53 @@ int owgs_replay(owgs_ctx* ctx, int32_t n_batches, const int64_t* acq_off, const 
                 const int64_t* rel_aid, uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags,
                 uint8_t* rel_flags);
 
+/* ---- completion path (CommonLoadBalancer.processAcknowledgement / processCompletion, CLB:205-346) ----------------
+ * activationSlots (CLB:60) lives on the device: an activation is tracked when it is published and removed by its
+ * completion ack.  Per-message outcome codes (out_kind): */
+#define OWGS_ACK_FAIL 0           /* AcknowledegmentMessage.parse fails (CLB:226-228): the shim logs the raw message */
+#define OWGS_ACK_JVM 1            /* the message has a "response" member (ResultMessage / Combined...): its
+                                     WhiskActivation is deserialised by the JVM, which completes the slot with
+                                     owgs_complete_activations */
+#define OWGS_ACK_UNSUPPORTED 2    /* outside the device parser's limits (container depth > 64, an exponent of more
+                                     than 9 digits, a non-ASCII or numeric activation id, U+FFFF, a number of more
+                                     than 34 significant digits in instance / transid): the JVM parses it */
+#define OWGS_ACK_RELEASED 3       /* processCompletion found the entry: releaseInvoker ran (CLB:286-319) */
+#define OWGS_ACK_HEALTH 4         /* no entry, transid == TransactionId.invokerHealth (CLB:320-328) */
+#define OWGS_ACK_NOENTRY 5        /* no entry, regular ack after a forced one (CLB:329-337) */
+#define OWGS_ACK_FORCED_NOENTRY 6 /* no entry, forced (timeout) after a regular ack (CLB:338-345) */
+
+/* TransactionId.invokerHealth's start (TransactionId.scala:225) of this controller: health acks echo it. */
+int owgs_set_health_tid(owgs_ctx* ctx, int64_t start_ms);
+
+/* Replaces: activationSlots.getOrElseUpdate(msg.activationId, ActivationEntry(...)) in setupActivation (CLB:148-166),
+ * in array order.  aid32 = n activation ids of 32 chars [0-9a-f] (ActivationId.asString, no terminator); action =
+ * the action handle (its limits and fqn@version are the entry's); ticket = the caller's handle for its own per-
+ * activation state (promise, timeout handler).  out_ticket = the ticket of the entry now in the map (the existing
+ * one when out_existed = 1). */
+int owgs_track_activations(owgs_ctx* ctx, int32_t n, const char* aid32, const int32_t* action, const int32_t* ticket,
+                           int32_t* out_ticket, uint8_t* out_existed);
+
+/* Replaces: processAcknowledgement (CLB:205-232) for n raw ack messages (UTF-8 bytes, offsets off[0..n]) processed
+ * in array order: AcknowledegmentMessage.parse (Message.scala:237-256) on the device, then for every
+ * CompletionMessage processCompletion(aid, tid, forced = false, isSystemError, invoker) (CLB:260-346): the entry is
+ * removed and releaseInvoker(invoker, entry) (SCPB:327-331) applied.  out_invoker = the message's invoker instance,
+ * out_ticket = the removed entry's ticket (-1 otherwise), out_flags bit0 = isSystemError, bits1-2 = the release
+ * flags (OWGS_REL_NOSUCHELEMENT, OWGS_REL_OVERFLOW) of releaseInvoker.  The shim sends InvocationFinishedMessage
+ * for RELEASED / HEALTH outcomes and completes promises for OWGS_ACK_JVM messages. */
+int owgs_process_acks(owgs_ctx* ctx, int32_t n, const char* bytes, const int64_t* off, uint8_t* out_kind,
+                      int32_t* out_invoker, int32_t* out_ticket, uint8_t* out_flags);
+/* Same with device buffers (bytes padded by 16 readable bytes past off[n]); stream as in owgs_replay_device. */
+int owgs_process_acks_device(owgs_ctx* ctx, int32_t n, const uint8_t* bytes, const int64_t* off, uint8_t* out_kind,
+                             int32_t* out_invoker, int32_t* out_ticket, uint8_t* out_flags, void* stream);
+
+/* Replaces: processCompletion (CLB:260-346) called directly -- the completion-ack timeout (forced, CLB:150-152) and
+ * the completion half of messages the JVM parsed itself (OWGS_ACK_JVM).  flags bit0 forced, bit1 isSystemError,
+ * bit2 transid == invokerHealth.  Outcomes and out_flags as in owgs_process_acks. */
+int owgs_complete_activations(owgs_ctx* ctx, int32_t n, const char* aid32, const int32_t* invoker,
+                              const uint8_t* flags, uint8_t* out_kind, int32_t* out_ticket, uint8_t* out_flags);
+/* activationSlots.size */
+int owgs_activations_live(owgs_ctx* ctx, int64_t* live);
+
 /* Restore the slot state captured by owgs_snapshot (bench: every timed step starts from the same state). */
 int owgs_snapshot(owgs_ctx* ctx);
 int owgs_restore(owgs_ctx* ctx, void* stream);

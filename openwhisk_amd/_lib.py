@@ -20,6 +20,7 @@ EINVAL, ENOMEM, EDEVICE, ERANGE, ENOENT = -22, -12, -5, -34, -2
 NONE, THROW_INDEX = -1, -2
 FLAG_OVERLOAD = 1
 REL_NOSUCHELEMENT, REL_OVERFLOW, REL_NOENTRY = 1, 2, 4
+ACK_FAIL, ACK_JVM, ACK_UNSUPPORTED, ACK_RELEASED, ACK_HEALTH, ACK_NOENTRY, ACK_FORCED_NOENTRY = range(7)
 HEALTHY, UNHEALTHY, UNRESPONSIVE, OFFLINE = 0, 1, 2, 3
 
 
@@ -85,6 +86,12 @@ def lib() -> C.CDLL:
         "owgs_state_info": (C.c_int, [P, P, P, P, P]),
         "owgs_step_sizes": (C.c_int, [P, i32, P, i32, P]),
         "owgs_pairwise_coprime": (C.c_int, [P, i32, P, i32, P]),
+        "owgs_set_health_tid": (C.c_int, [P, C.c_int64]),
+        "owgs_track_activations": (C.c_int, [P, i32, P, P, P, P, P]),
+        "owgs_process_acks": (C.c_int, [P, i32, P, P, P, P, P, P]),
+        "owgs_process_acks_device": (C.c_int, [P, i32, P, P, P, P, P, P, P]),
+        "owgs_complete_activations": (C.c_int, [P, i32, P, P, P, P, P, P]),
+        "owgs_activations_live": (C.c_int, [P, P]),
         "owgs_replay_device": (C.c_int, [P, i32, P, P, C.c_int64, P, P, C.c_int64, u64, P, P, P, P]),
         "owgs_replay": (C.c_int, [P, i32, P, P, P, P, u64, P, P, P]),
         "owgs_snapshot": (C.c_int, [P]),

@@ -126,6 +126,56 @@ class GpuShardingContainerPoolBalancer:
         self._chk(self._L.owgs_step_sizes(self._h, pool, _p(out), n.value, None))
         return out[: n.value].tolist()
 
+    # ------------------------------------------------------------------ completion path (CLB:148-166, 205-346)
+    def set_health_tid(self, start_ms: int):
+        """TransactionId.invokerHealth's start time (TransactionId.scala:225): health acks echo it."""
+        self._chk(self._L.owgs_set_health_tid(self._h, start_ms))
+
+    def track_activations(self, aids, actions, tickets):
+        """setupActivation's activationSlots.getOrElseUpdate (CLB:148-166) for a batch: (ticket, existed)."""
+        n = len(aids)
+        buf = np.frombuffer(b"".join(a.encode("ascii") for a in aids) or b"\0", dtype=np.uint8)
+        act = np.ascontiguousarray(actions, dtype=np.int32)
+        tk = np.ascontiguousarray(tickets, dtype=np.int32)
+        out = np.zeros(max(n, 1), dtype=np.int32)
+        ex = np.zeros(max(n, 1), dtype=np.uint8)
+        self._chk(self._L.owgs_track_activations(self._h, n, _p(buf), _p(act), _p(tk), _p(out), _p(ex)))
+        return out[:n], ex[:n]
+
+    def process_acks(self, msgs):
+        """processAcknowledgement (CLB:205-232) for raw ack messages (bytes): (kind, invoker, ticket, flags)."""
+        n = len(msgs)
+        off = np.zeros(n + 1, dtype=np.int64)
+        off[1:] = np.cumsum([len(m) for m in msgs])
+        buf = np.frombuffer(b"".join(msgs) + b"\0", dtype=np.uint8)
+        kind = np.zeros(max(n, 1), dtype=np.uint8)
+        inv = np.zeros(max(n, 1), dtype=np.int32)
+        tk = np.zeros(max(n, 1), dtype=np.int32)
+        fl = np.zeros(max(n, 1), dtype=np.uint8)
+        self._chk(self._L.owgs_process_acks(self._h, n, _p(buf), _p(off), _p(kind), _p(inv), _p(tk), _p(fl)))
+        return kind[:n], inv[:n], tk[:n], fl[:n]
+
+    def complete_activations(self, aids, invokers, forced=None, system_error=None, health=None):
+        """processCompletion (CLB:260-346) called directly (timeouts, JVM-parsed acks): (kind, ticket, flags)."""
+        n = len(aids)
+        buf = np.frombuffer(b"".join(a.encode("ascii") for a in aids) or b"\0", dtype=np.uint8)
+        inv = np.ascontiguousarray(invokers, dtype=np.int32)
+        z = np.zeros(n, dtype=np.uint8)
+        f = ((np.asarray(forced if forced is not None else z, dtype=np.uint8) & 1)
+             | (np.asarray(system_error if system_error is not None else z, dtype=np.uint8) & 1) << 1
+             | (np.asarray(health if health is not None else z, dtype=np.uint8) & 1) << 2).astype(np.uint8)
+        f = np.ascontiguousarray(f if n else np.zeros(1, np.uint8))
+        kind = np.zeros(max(n, 1), dtype=np.uint8)
+        tk = np.zeros(max(n, 1), dtype=np.int32)
+        fl = np.zeros(max(n, 1), dtype=np.uint8)
+        self._chk(self._L.owgs_complete_activations(self._h, n, _p(buf), _p(inv), _p(f), _p(kind), _p(tk), _p(fl)))
+        return kind[:n], tk[:n], fl[:n]
+
+    def activations_live(self) -> int:
+        v = C.c_int64()
+        self._chk(self._L.owgs_activations_live(self._h, C.byref(v)))
+        return v.value
+
     def pairwise_coprime_numbers_until(self, x: int) -> list:
         """ShardingContainerPoolBalancer.pairwiseCoprimeNumbersUntil (SCPB:379-384), computed by owgs_coprime_kernel."""
         n = C.c_int32()

@@ -42,6 +42,18 @@ extern "C" hipError_t owgs_launch_slots(const int64_t* mem_bytes, int32_t from, 
                                        int64_t min_bytes, int32_t* permits, hipStream_t s);
 extern "C" hipError_t owgs_launch_usable(const uint8_t* status, int32_t n, uint32_t* bits, int32_t n_words,
                                         hipStream_t s);
+extern "C" hipError_t owgs_launch_ack_parse(const OwgsAckParseArgs* a, hipStream_t st);
+extern "C" hipError_t owgs_launch_aid_decode(const char* aid32, int32_t n, const uint8_t* cflags, ulonglong2* key,
+                                             uint8_t* info, int32_t* inst, const int32_t* inv, hipStream_t st);
+extern "C" hipError_t owgs_launch_act_init(const OwgsActTable* T, hipStream_t st);
+extern "C" hipError_t owgs_launch_act_rehash(const OwgsActTable* O, const OwgsActTable* T, hipStream_t st);
+extern "C" hipError_t owgs_launch_act_track(const OwgsActTable* T, const ulonglong2* key, int32_t n,
+                                            const int32_t* action, const int32_t* ticket, int32_t* slot,
+                                            uint8_t* state, int32_t* out_ticket, uint8_t* out_existed,
+                                            unsigned long long* counters, hipStream_t st);
+extern "C" hipError_t owgs_launch_ack_complete(const OwgsActTable* T, const OwgsAckCompleteArgs* a, hipStream_t st);
+extern "C" hipError_t owgs_launch_ack_flags(int32_t n, const uint8_t* info, const uint8_t* rflags,
+                                            const uint8_t* out_kind, uint8_t* out_flags, hipStream_t st);
 extern "C" size_t owgs_engine_lds_bytes(int n_slots, int pool_mode, int n_ids, int nm, int nb, int n_actions);
 
 namespace {
@@ -125,6 +137,19 @@ struct owgs_ctx {
     DevBuf<unsigned long long> d_trace;  // barrier timeline (diagnostic builds, env OWGS_TRACE_FILE)
     int32_t cur_tag = 0;      // tags used so far (wraps with a clear of d_gcur)
     DevBuf<uint2> d_rel_rec, d_xmeta;
+    // activationSlots (owgs_acks.hip)
+    DevBuf<unsigned long long> t_tw;
+    DevBuf<ulonglong2> t_tk;
+    DevBuf<int2> t_tv;
+    DevBuf<int32_t> t_owner;
+    long long t_cap = 0, t_used = 0, t_live = 0;
+    long long health_ms = 0;
+    DevBuf<ulonglong2> k_key;
+    DevBuf<uint8_t> k_info, k_state, k_kind, k_oflags, k_bytes, k_cfl;
+    DevBuf<int32_t> k_inst, k_slot, k_tick, k_r0, k_r1, k_r2, k_r3, k_act;
+    DevBuf<int64_t> k_off;
+    DevBuf<char> k_aid;
+    DevBuf<unsigned long long> k_cnt;
     // snapshot
     DevBuf<int32_t> s_permits;
     DevBuf<uint32_t> s_ct_keys, s_ct_vals;
@@ -463,6 +488,22 @@ void owgs_destroy(owgs_ctx* c) {
     c->d_trace.release();
     c->d_rel_rec.release();
     c->d_xmeta.release();
+    c->t_tw.release();
+    c->t_tk.release();
+    c->t_tv.release();
+    c->t_owner.release();
+    c->k_key.release();
+    c->k_info.release();
+    c->k_state.release();
+    c->k_kind.release();
+    c->k_oflags.release();
+    c->k_bytes.release();
+    c->k_cfl.release();
+    DevBuf<int32_t>* ks[] = {&c->k_inst, &c->k_slot, &c->k_tick, &c->k_r0, &c->k_r1, &c->k_r2, &c->k_r3, &c->k_act};
+    for (auto* b : ks) b->release();
+    c->k_off.release();
+    c->k_aid.release();
+    c->k_cnt.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1001,3 +1042,240 @@ int owgs_read_stats(owgs_ctx* c, uint64_t* out, int32_t cap) {
 }
 
 }  // extern "C"
+
+// ============================================================================================== completion acks
+// activationSlots (CLB:60) on the device; see owgs_acks.hip.
+
+static OwgsActTable act_table(owgs_ctx* c) {
+    OwgsActTable T;
+    T.tw = c->t_tw.p;
+    T.tk = c->t_tk.p;
+    T.tv = c->t_tv.p;
+    T.owner = c->t_owner.p;
+    T.cap = c->t_cap;
+    return T;
+}
+
+// keep used slots (live + deleted) under half the capacity: rehash the live entries into a table of
+// max(cap, 4 * (live + n)) slots when n more inserts could cross it
+static int act_reserve(owgs_ctx* c, long long n) {
+    if (c->t_cap > 0 && c->t_used + n <= c->t_cap / 2) return OWGS_OK;
+    long long cap = 1 << 16;
+    while (cap < 4 * (c->t_live + n)) cap <<= 1;
+    if (cap < c->t_cap) cap = c->t_cap;
+    DevBuf<unsigned long long> tw;
+    DevBuf<ulonglong2> tk;
+    DevBuf<int2> tv;
+    DevBuf<int32_t> ow;
+    HIPCHK(c, tw.reserve((size_t)cap));
+    HIPCHK(c, tk.reserve((size_t)cap));
+    HIPCHK(c, tv.reserve((size_t)cap));
+    HIPCHK(c, ow.reserve((size_t)cap));
+    OwgsActTable T{tw.p, tk.p, tv.p, ow.p, cap};
+    HIPCHK(c, owgs_launch_act_init(&T, c->stream));
+    if (c->t_cap > 0) {
+        OwgsActTable O = act_table(c);
+        HIPCHK(c, owgs_launch_act_rehash(&O, &T, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->t_tw.release();
+    c->t_tk.release();
+    c->t_tv.release();
+    c->t_owner.release();
+    c->t_tw = tw;
+    c->t_tk = tk;
+    c->t_tv = tv;
+    c->t_owner = ow;
+    tw.p = nullptr;
+    tk.p = nullptr;
+    tv.p = nullptr;
+    ow.p = nullptr;
+    c->t_cap = cap;
+    c->t_used = c->t_live;
+    return OWGS_OK;
+}
+
+int owgs_set_health_tid(owgs_ctx* c, int64_t start_ms) {
+    if (!c) return OWGS_EINVAL;
+    c->health_ms = start_ms;
+    return OWGS_OK;
+}
+
+int owgs_activations_live(owgs_ctx* c, int64_t* live) {
+    if (!c || !live) return OWGS_EINVAL;
+    *live = c->t_live;
+    return OWGS_OK;
+}
+
+int owgs_track_activations(owgs_ctx* c, int32_t n, const char* aid32, const int32_t* action, const int32_t* ticket,
+                           int32_t* out_ticket, uint8_t* out_existed) {
+    if (!c || n < 0 || (n > 0 && (!aid32 || !action || !ticket || !out_ticket || !out_existed))) return OWGS_EINVAL;
+    if (n == 0) return OWGS_OK;
+    if (!registered(c, n, action)) return c->fail(OWGS_ENOENT, "unknown action");
+    (void)hipSetDevice(c->cfg.device);
+    int rc = act_reserve(c, n);
+    if (rc) return rc;
+    HIPCHK(c, upload(c->k_aid, aid32, (size_t)n * 32, c->stream));
+    HIPCHK(c, upload(c->k_act, action, (size_t)n, c->stream));
+    HIPCHK(c, upload(c->k_r0, ticket, (size_t)n, c->stream));
+    HIPCHK(c, c->k_key.reserve((size_t)n));
+    HIPCHK(c, c->k_slot.reserve((size_t)n));
+    HIPCHK(c, c->k_state.reserve((size_t)n));
+    HIPCHK(c, c->k_tick.reserve((size_t)n));
+    HIPCHK(c, c->k_oflags.reserve((size_t)n));
+    HIPCHK(c, c->k_cnt.reserve(2));
+    HIPCHK(c, hipMemsetAsync(c->k_cnt.p, 0, 16, c->stream));
+    HIPCHK(c, owgs_launch_aid_decode(c->k_aid.p, n, nullptr, c->k_key.p, nullptr, nullptr, nullptr, c->stream));
+    OwgsActTable T = act_table(c);
+    HIPCHK(c, owgs_launch_act_track(&T, c->k_key.p, n, c->k_act.p, c->k_r0.p, c->k_slot.p, c->k_state.p, c->k_tick.p,
+                                    c->k_oflags.p, c->k_cnt.p, c->stream));
+    unsigned long long cnt[2];
+    HIPCHK(c, hipMemcpyAsync(out_ticket, c->k_tick.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out_existed, c->k_oflags.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(cnt, c->k_cnt.p, 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->t_used += (long long)cnt[0];
+    c->t_live += (long long)cnt[0];
+    for (int32_t i = 0; i < n; ++i)
+        if (out_existed[i] == 2) return c->fail(OWGS_EINVAL, "activation id is not 32 characters of [0-9a-f]");
+    return OWGS_OK;
+}
+
+// shared tail: info/key/inst of n messages are in k_info/k_key/k_inst; resolve, release in order, flags
+static int ack_complete(owgs_ctx* c, int32_t n, uint8_t* d_kind, int32_t* d_ticket, uint8_t* d_flags,
+                        hipStream_t st) {
+    if (c->t_cap == 0) {
+        int rc = act_reserve(c, 0);
+        if (rc) return rc;
+    }
+    HIPCHK(c, c->k_slot.reserve((size_t)n));
+    HIPCHK(c, c->k_r0.reserve((size_t)n));
+    HIPCHK(c, c->k_r1.reserve((size_t)n));
+    HIPCHK(c, c->k_r2.reserve((size_t)n));
+    HIPCHK(c, c->k_r3.reserve((size_t)n));
+    HIPCHK(c, c->d_rflags.reserve((size_t)n));
+    HIPCHK(c, c->k_cnt.reserve(2));
+    HIPCHK(c, hipMemsetAsync(c->k_cnt.p, 0, 16, st));
+    if (!c->d_act_mem.p) {  // no actions registered: every lookup misses, the records are never read
+        HIPCHK(c, c->d_act_mem.reserve(1));
+        HIPCHK(c, c->d_act_maxc.reserve(1));
+        HIPCHK(c, c->d_act_slot.reserve(1));
+    }
+    OwgsActTable T = act_table(c);
+    OwgsAckCompleteArgs a{};
+    a.key = c->k_key.p;
+    a.info = c->k_info.p;
+    a.inst = c->k_inst.p;
+    a.n = n;
+    a.slot = c->k_slot.p;
+    a.act_mem = c->d_act_mem.p;
+    a.act_maxc = c->d_act_maxc.p;
+    a.act_slot = c->d_act_slot.p;
+    a.n_slots = c->n_slots;
+    a.r_inv = c->k_r0.p;
+    a.r_mem = c->k_r1.p;
+    a.r_maxc = c->k_r2.p;
+    a.r_slot = c->k_r3.p;
+    a.out_kind = d_kind;
+    a.out_ticket = d_ticket;
+    a.counters = c->k_cnt.p;
+    HIPCHK(c, owgs_launch_ack_complete(&T, &a, st));
+    OwgsReleaseArgs R{};
+    R.permits = c->d_permits.p;
+    R.n_slots = c->n_slots;
+    R.ct_keys = c->d_ct_keys.p;
+    R.ct_vals = c->d_ct_vals.p;
+    R.n = n;
+    R.inv = c->k_r0.p;
+    R.mem = c->k_r1.p;
+    R.maxc = c->k_r2.p;
+    R.slot = c->k_r3.p;
+    R.flags = c->d_rflags.p;
+    R.err = c->d_err.p;
+    HIPCHK(c, owgs_launch_release_seq(&R, st));
+    HIPCHK(c, owgs_launch_ack_flags(n, c->k_info.p, c->d_rflags.p, d_kind, d_flags, st));
+    unsigned long long cnt[2];
+    HIPCHK(c, hipMemcpyAsync(cnt, c->k_cnt.p, 16, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    c->t_live -= (long long)cnt[1];
+    return check_err_word(c);
+}
+
+int owgs_process_acks_device(owgs_ctx* c, int32_t n, const uint8_t* bytes, const int64_t* off, uint8_t* out_kind,
+                             int32_t* out_invoker, int32_t* out_ticket, uint8_t* out_flags, void* stream) {
+    if (!c || n < 0 || (n > 0 && (!bytes || !off || !out_kind || !out_invoker || !out_ticket || !out_flags)))
+        return OWGS_EINVAL;
+    if (n == 0) return OWGS_OK;
+    (void)hipSetDevice(c->cfg.device);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(c, c->k_key.reserve((size_t)n));
+    HIPCHK(c, c->k_info.reserve((size_t)n));
+    OwgsAckParseArgs p{};
+    p.bytes = bytes;
+    p.off = off;
+    p.n = n;
+    p.health_start_ms = c->health_ms;
+    p.forced = nullptr;
+    p.key = c->k_key.p;
+    p.inst = out_invoker;
+    p.info = c->k_info.p;
+    HIPCHK(c, owgs_launch_ack_parse(&p, st));
+    // the resolve step reads the instance from k_inst
+    HIPCHK(c, c->k_inst.reserve((size_t)n));
+    HIPCHK(c, hipMemcpyAsync(c->k_inst.p, out_invoker, (size_t)n * 4, hipMemcpyDeviceToDevice, st));
+    return ack_complete(c, n, out_kind, out_ticket, out_flags, st);
+}
+
+int owgs_process_acks(owgs_ctx* c, int32_t n, const char* bytes, const int64_t* off, uint8_t* out_kind,
+                      int32_t* out_invoker, int32_t* out_ticket, uint8_t* out_flags) {
+    if (!c || n < 0 || (n > 0 && (!bytes || !off || !out_kind || !out_invoker || !out_ticket || !out_flags)))
+        return OWGS_EINVAL;
+    if (n == 0) return OWGS_OK;
+    for (int32_t i = 0; i < n; ++i)
+        if (off[i + 1] < off[i] || off[i] < 0) return c->fail(OWGS_EINVAL, "offsets");
+    (void)hipSetDevice(c->cfg.device);
+    const size_t nb = (size_t)(off[n] - off[0]);
+    std::vector<int64_t> o((size_t)n + 1);
+    for (int32_t i = 0; i <= n; ++i) o[i] = off[i] - off[0];
+    HIPCHK(c, c->k_bytes.reserve(nb + 32));
+    HIPCHK(c, hipMemsetAsync(c->k_bytes.p + nb, 0, 32, c->stream));
+    if (nb) HIPCHK(c, hipMemcpyAsync(c->k_bytes.p, bytes + off[0], nb, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, upload(c->k_off, o.data(), o.size(), c->stream));
+    HIPCHK(c, c->k_kind.reserve((size_t)n));
+    HIPCHK(c, c->k_tick.reserve((size_t)n));
+    HIPCHK(c, c->k_oflags.reserve((size_t)n));
+    HIPCHK(c, c->k_act.reserve((size_t)n));
+    int rc = owgs_process_acks_device(c, n, c->k_bytes.p, c->k_off.p, c->k_kind.p, c->k_act.p, c->k_tick.p,
+                                      c->k_oflags.p, nullptr);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpy(out_kind, c->k_kind.p, (size_t)n, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(out_invoker, c->k_act.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(out_ticket, c->k_tick.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(out_flags, c->k_oflags.p, (size_t)n, hipMemcpyDeviceToHost));
+    return OWGS_OK;
+}
+
+int owgs_complete_activations(owgs_ctx* c, int32_t n, const char* aid32, const int32_t* invoker, const uint8_t* flags,
+                              uint8_t* out_kind, int32_t* out_ticket, uint8_t* out_flags) {
+    if (!c || n < 0 || (n > 0 && (!aid32 || !invoker || !flags || !out_kind || !out_ticket || !out_flags)))
+        return OWGS_EINVAL;
+    if (n == 0) return OWGS_OK;
+    (void)hipSetDevice(c->cfg.device);
+    HIPCHK(c, upload(c->k_aid, aid32, (size_t)n * 32, c->stream));
+    HIPCHK(c, upload(c->k_cfl, flags, (size_t)n, c->stream));
+    HIPCHK(c, upload(c->k_act, invoker, (size_t)n, c->stream));
+    HIPCHK(c, c->k_key.reserve((size_t)n));
+    HIPCHK(c, c->k_info.reserve((size_t)n));
+    HIPCHK(c, c->k_inst.reserve((size_t)n));
+    HIPCHK(c, c->k_kind.reserve((size_t)n));
+    HIPCHK(c, c->k_tick.reserve((size_t)n));
+    HIPCHK(c, c->k_oflags.reserve((size_t)n));
+    HIPCHK(c, owgs_launch_aid_decode(c->k_aid.p, n, c->k_cfl.p, c->k_key.p, c->k_info.p, c->k_inst.p, c->k_act.p,
+                                     c->stream));
+    int rc = ack_complete(c, n, c->k_kind.p, c->k_tick.p, c->k_oflags.p, c->stream);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpy(out_kind, c->k_kind.p, (size_t)n, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(out_ticket, c->k_tick.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(out_flags, c->k_oflags.p, (size_t)n, hipMemcpyDeviceToHost));
+    return OWGS_OK;
+}

@@ -228,3 +228,52 @@ struct OwgsLookupArgs {
     int32_t n;
     int2* out;
 };
+
+// --------------------------------------------------------------------------------------------- completion acks
+// (owgs_acks.hip; outcome codes = OWGS_ACK_* in include/owgs.h)
+#ifndef OWGS_ACK_FAIL
+#define OWGS_ACK_FAIL 0
+#define OWGS_ACK_JVM 1
+#define OWGS_ACK_UNSUPPORTED 2
+#define OWGS_ACK_RELEASED 3
+#define OWGS_ACK_HEALTH 4
+#define OWGS_ACK_NOENTRY 5
+#define OWGS_ACK_FORCED_NOENTRY 6
+#endif
+#define OWGS_ACK_COMPLETION 3       // parsed CompletionMessage (before resolution into RELEASED / HEALTH / NOENTRY)
+
+struct OwgsAckParseArgs {
+    const uint8_t* bytes;        // messages, padded by >= 16 readable bytes
+    const int64_t* off;          // [n + 1]
+    int32_t n;
+    long long health_start_ms;   // TransactionId.invokerHealth's start (TransactionId.scala:225)
+    const uint8_t* forced;       // null for raw acks
+    ulonglong2* key;             // out: activation id (128 bits)
+    int32_t* inst;               // out: invoker instance (BigDecimal.intValue)
+    uint8_t* info;               // out: kind | isSystemError << 4 | health tid << 5 | forced << 6
+};
+
+// activationSlots (CLB:60): open addressing over cap (power of two) slots
+struct OwgsActTable {
+    unsigned long long* tw;      // 0 empty, 1 ready, 2 deleted, 1 << 63 | batch index = claimed by an insert batch
+    ulonglong2* tk;              // activation id
+    int2* tv;                    // {action handle, caller ticket}
+    int32_t* owner;              // lowest batch index of a slot's inserts / removals (INT_MAX between calls)
+    long long cap;
+};
+
+struct OwgsAckCompleteArgs {
+    const ulonglong2* key;
+    const uint8_t* info;
+    const int32_t* inst;
+    int32_t n;
+    int32_t* slot;               // scratch [n]
+    const int32_t* act_mem;
+    const int32_t* act_maxc;
+    const int32_t* act_slot;
+    int32_t n_slots;
+    int32_t *r_inv, *r_mem, *r_maxc, *r_slot;   // release records (owgs_release_seq_kernel input)
+    uint8_t* out_kind;
+    int32_t* out_ticket;
+    unsigned long long* counters;               // [0] entries inserted, [1] entries removed
+};

@@ -167,3 +167,75 @@ def config(name: str, n_activations: int | None = None, shard: int = 0, n_shards
     if n_activations is not None:
         base["n_activations"] = n_activations
     return generate(name=name, **base)
+
+
+# ------------------------------------------------------------------------------------------- completion acks
+# Ack messages as the invoker's serializer writes them: CompletionMessage(...).serialize = jsonFormat4 compactPrint
+# with fields transid, activationId, isSystemError, invoker (Message.scala:85-100, 204-216); InvokerInstanceId with
+# its None options omitted and userMemory as ByteSize.toString "<n> MB" (InstanceId.scala:31-49, Size.scala:107-114);
+# transid as [id, start] (TransactionId.scala:236-241).
+TESTING_TID = ("sid_testing", 1700000000456)
+
+
+def activation_ids(rng, n: int) -> list[str]:
+    """ActivationId.generate(): a random UUID without dashes (32 lowercase hex chars, ActivationId.scala:77)."""
+    hi = rng.integers(0, 2**63, size=n, dtype=np.int64).astype(np.uint64) * np.uint64(2) + rng.integers(0, 2, n).astype(np.uint64)
+    lo = rng.integers(0, 2**63, size=n, dtype=np.int64).astype(np.uint64) * np.uint64(2) + rng.integers(0, 2, n).astype(np.uint64)
+    return [f"{int(h):016x}{int(l):016x}" for h, l in zip(hi, lo)]
+
+
+def completion_message(aid: str, instance: int, system_error: bool = False, tid=TESTING_TID,
+                       user_memory_mb: int = 16384, unique_name: str | None = None) -> bytes:
+    inv = '{"instance":%d%s,"userMemory":"%d MB"}' % (
+        instance, (',"uniqueName":"%s"' % unique_name) if unique_name else "", user_memory_mb)
+    return ('{"transid":["%s",%d],"activationId":"%s","isSystemError":%s,"invoker":%s}' % (
+        tid[0], tid[1], aid, "true" if system_error else "false", inv)).encode("ascii")
+
+
+def combined_message(aid: str, instance: int, user_memory_mb: int = 16384) -> bytes:
+    """CombinedCompletionAndResultMessage after shrink (response = Left(activationId))."""
+    return ('{"transid":["%s",%d],"response":"%s","isSystemError":false,"invoker":{"instance":%d,'
+            '"userMemory":"%d MB"}}' % (TESTING_TID[0], TESTING_TID[1], aid, instance, user_memory_mb)).encode("ascii")
+
+
+def ack_batch(rng, aids: list[str], invokers, health_start_ms: int, dup=0.05, unknown=0.03, health=0.02,
+              out_of_range=0.02, combined=0.02, garbage=0.01, syserr=0.1):
+    """Ack messages completing each (aid, invoker) once in a random order, mixed with the cases processCompletion
+    distinguishes: duplicates (the second sees no entry), unknown ids, health acks, invoker ids outside the slots,
+    combined messages (left to the JVM) and unparsable ones."""
+    order = rng.permutation(len(aids))
+    msgs = []
+    for i in order:
+        r = rng.random()
+        if r < garbage:
+            msgs.append(completion_message(aids[i], int(invokers[i]))[:-3])
+            continue
+        if r < garbage + combined:
+            msgs.append(combined_message(aids[i], int(invokers[i])))
+            continue
+        inst = int(invokers[i]) if rng.random() >= out_of_range else int(rng.choice([-1, 99999, 2**31 - 1]))
+        m = completion_message(aids[i], inst, bool(rng.random() < syserr))
+        msgs.append(m)
+        if rng.random() < dup:
+            msgs.append(m)
+        if rng.random() < unknown:
+            msgs.append(completion_message(activation_ids(rng, 1)[0], inst))
+        if rng.random() < health:
+            msgs.append(completion_message(activation_ids(rng, 1)[0], inst, tid=("sid_invokerHealth", health_start_ms)))
+    return msgs
+
+
+def mutate(rng, m: bytes, k: int = 2) -> bytes:
+    """Random byte-level edits of a message (parser fuzzing)."""
+    b = bytearray(m)
+    alphabet = b'{}[]",:\\ 0123456789-+.eEtrufalsn\t\nabcdefu\x01\xc3\xa9'
+    for _ in range(k):
+        op = rng.integers(0, 3)
+        p = int(rng.integers(0, len(b) + 1))
+        if op == 0 and b:
+            del b[min(p, len(b) - 1)]
+        elif op == 1:
+            b.insert(p, alphabet[int(rng.integers(0, len(alphabet)))])
+        elif b:
+            b[min(p, len(b) - 1)] = alphabet[int(rng.integers(0, len(alphabet)))]
+    return bytes(b)

@@ -82,6 +82,13 @@ def lib() -> C.CDLL:
             "owo_release": (C.c_int, [P, i32, i32]),
             "owo_replay": (C.c_int, [P, i32, P, P, P, P, u64, P, P, P]),
             "owo_replay_parallel": (C.c_int, [P, i32, i32, P, P, P, P, u64, P, P, P]),
+            "owa_parse_batch": (C.c_int, [i32, P, P, i64, P, P, P, P, P]),
+            "owa_table_new": (P, [i64]),
+            "owa_table_free": (None, [P]),
+            "owa_track": (C.c_int, [P, u64, u64, i32, i32, P]),
+            "owa_remove": (C.c_int, [P, u64, u64, P, P]),
+            "owa_live": (i64, [P]),
+            "owa_process_acks": (C.c_int, [P, P, i32, P, P, i64, P, P, P, P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -348,3 +355,79 @@ def state_for(workload, zombies: bool = True, slot_keys: dict | None = None) -> 
         k = keys.setdefault(a.key, len(keys))
         st.register_action(a.namespace, a.path, k, a.mem_mb, a.max_concurrent, a.blackbox)
     return st
+
+
+# ------------------------------------------------------------------------------------------- completion acks
+# (owack_oracle.c: processAcknowledgement / processCompletion, CommonLoadBalancer.scala:205-346)
+ACK_FAIL, ACK_JVM, ACK_UNSUPPORTED, ACK_COMPLETION = 0, 1, 2, 3
+# processCompletion outcomes (CLB:286-345), as the device path reports them
+OUT_RELEASED, OUT_HEALTH, OUT_NOENTRY, OUT_FORCED_NOENTRY = 3, 4, 5, 6
+
+
+def parse_acks(msgs: list[bytes], health_start_ms: int):
+    """owa_parse over a batch: (kind, instance, syserr, health, aid u64[n,2])."""
+    n = len(msgs)
+    off = np.zeros(n + 1, dtype=np.int64)
+    off[1:] = np.cumsum([len(m) for m in msgs])
+    buf = np.frombuffer(b"".join(msgs) + b"\0" * 8, dtype=np.uint8)
+    kind, inst, sy, he = (np.zeros(max(n, 1), dtype=np.int32) for _ in range(4))
+    aid = np.zeros((max(n, 1), 2), dtype=np.uint64)
+    lib().owa_parse_batch(n, _ptr(buf), _ptr(off), health_start_ms, _ptr(kind), _ptr(inst), _ptr(sy), _ptr(he),
+                          _ptr(aid))
+    return kind[:n], inst[:n], sy[:n], he[:n], aid[:n]
+
+
+def aid_words(aid: str) -> tuple[int, int]:
+    return int(aid[:16], 16), int(aid[16:], 16)
+
+
+class AckFlow:
+    """activationSlots + processCompletion over an oracle BalancerState (CLB:148-166, 260-346)."""
+
+    def __init__(self, state: "BalancerState", health_start_ms: int, cap: int = 1 << 22):
+        self.st = state
+        self.h = health_start_ms
+        self.t = lib().owa_table_new(cap)
+
+    def __del__(self):
+        if getattr(self, "t", None):
+            lib().owa_table_free(self.t)
+            self.t = None
+
+    def track(self, aid: str, action: int, ticket: int):
+        hi, lo = aid_words(aid)
+        out = C.c_int32()
+        ex = lib().owa_track(self.t, hi, lo, action, ticket, C.byref(out))
+        return out.value, ex
+
+    def complete(self, hi: int, lo: int, invoker: int, forced: bool, health: bool):
+        """processCompletion: (outcome, ticket, action, release_flag)."""
+        a, t = C.c_int32(), C.c_int32()
+        if lib().owa_remove(self.t, hi, lo, C.byref(a), C.byref(t)):
+            # releaseInvoker(invoker, entry): invokerSlots.lift(invoker.toInt) (SCPB:327-331)
+            n_slots = len(self.st.permits())
+            rf = self.st.release(invoker, a.value) if 0 <= invoker < n_slots else 0
+            return OUT_RELEASED, t.value, a.value, rf
+        if health:
+            return OUT_HEALTH, -1, -1, 0
+        return (OUT_NOENTRY if not forced else OUT_FORCED_NOENTRY), -1, -1, 0
+
+    def process_acks(self, msgs: list[bytes]):
+        """processAcknowledgement for each message in order: (kind/outcome, instance, ticket, flags)."""
+        n = len(msgs)
+        off = np.zeros(n + 1, dtype=np.int64)
+        off[1:] = np.cumsum([len(m) for m in msgs])
+        buf = np.frombuffer(b"".join(msgs) + b"\0" * 8, dtype=np.uint8)
+        kind, inst, tick = (np.zeros(max(n, 1), dtype=np.int32) for _ in range(3))
+        fl = np.zeros(max(n, 1), dtype=np.uint8)
+        lib().owa_process_acks(self.t, self.st.h, n, _ptr(buf), _ptr(off), self.h, _ptr(kind), _ptr(inst),
+                               _ptr(tick), _ptr(fl))
+        return kind[:n], inst[:n], tick[:n], fl[:n]
+
+    def live(self) -> int:
+        return lib().owa_live(self.t)
+
+
+def _rel_bits(rf: int) -> int:
+    """owo_release result -> OWGS_REL_* bits (NoSuchElement 1, overflow 2)."""
+    return {0: 0, THROW_NOSUCHELEMENT: 1, THROW_OVERFLOW: 2}.get(rf, 0)
