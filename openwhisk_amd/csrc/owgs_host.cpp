@@ -1112,6 +1112,12 @@ int owgs_track_activations(owgs_ctx* c, int32_t n, const char* aid32, const int3
     if (!c || n < 0 || (n > 0 && (!aid32 || !action || !ticket || !out_ticket || !out_existed))) return OWGS_EINVAL;
     if (n == 0) return OWGS_OK;
     if (!registered(c, n, action)) return c->fail(OWGS_ENOENT, "unknown action");
+    // ActivationId.asString is 32 chars of [0-9a-f]; reject a malformed batch before any entry is created
+    for (size_t k = 0; k < (size_t)n * 32; ++k) {
+        const char ch = aid32[k];
+        if (!((ch >= '0' && ch <= '9') || (ch >= 'a' && ch <= 'f')))
+            return c->fail(OWGS_EINVAL, "activation id is not 32 characters of [0-9a-f]");
+    }
     (void)hipSetDevice(c->cfg.device);
     int rc = act_reserve(c, n);
     if (rc) return rc;

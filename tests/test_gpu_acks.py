@@ -148,6 +148,7 @@ def test_track_duplicates_in_one_batch_keep_the_first():
     assert b.activations_live() == 2
     with pytest.raises(Exception):
         b.track_activations(["XYZ" * 10 + "ab"], [a], [0])
+    assert b.activations_live() == 2  # a malformed batch creates no entry
 
 
 def test_table_grows_and_rehashes():
