@@ -200,6 +200,31 @@ int owgs_complete_activations(owgs_ctx* ctx, int32_t n, const char* aid32, const
 /* activationSlots.size */
 int owgs_activations_live(owgs_ctx* ctx, int64_t* live);
 
+/* ---- invoker health supervision ----
+ * Replaces: InvokerPool (InvokerSupervision.scala:95-210: registerInvoker on the first ping, padToIndexed with Offline
+ * entries, InvocationFinishedMessage forwarding) and one InvokerActor FSM per invoker (InvokerSupervision.scala:
+ * 285-440: Offline / Unhealthy / Unresponsive / Healthy, 10 s state timeout, 1-minute Tick sending test actions
+ * while Unhealthy or Unresponsive, a ring buffer of the last 10 results with tolerance 3).
+ * Events are in mailbox order with non-decreasing times (ms, in [0, 2^60)) that never go back before the previous
+ * batch's now_ms;
+ * timers due at or before an event's time fire before it, and all timers due at or before now_ms fire at the end.
+ * user_memory_bytes = the pinging InvokerInstanceId's userMemory (ignored for other kinds).  apply != 0 hands the
+ * resulting status vector to owgs_update_invokers (the monitor's CurrentInvokerPoolState -> updateInvokers,
+ * SCPB:226-227).  Bad kinds, negative ids or times out of order: OWGS_EINVAL with no state change. */
+#define OWGS_EV_PING 0          /* PingMessage (InvokerSupervision.scala:120-131) */
+#define OWGS_EV_SUCCESS 1       /* InvocationFinishedMessage(InvocationFinishedResult.Success) */
+#define OWGS_EV_SYSTEM_ERROR 2  /* ... SystemError */
+#define OWGS_EV_TIMEOUT 3       /* ... Timeout */
+#define OWGS_EV_STATE_TIMEOUT 4 /* an FSM.StateTimeout message to the invoker's actor */
+int owgs_health_events(owgs_ctx* ctx, int32_t n, const int32_t* invoker, const uint8_t* kind, const int64_t* t_ms,
+                       const int64_t* user_memory_bytes, int64_t now_ms, int32_t apply);
+/* Replaces: InvokerPool's GetStatus (status vector, InvokerSupervision.scala:132) plus per-invoker detail: userMemory
+ * of the instance in the status vector, test actions sent during the last batch (invokeTestAction,
+ * InvokerSupervision.scala:416-434), the ring buffer (2 bits per result oldest first: 1 Success, 2 SystemError,
+ * 3 Timeout; count << 20) and the next Tick (-1: none).  *n = the status vector's length; any output may be NULL. */
+int owgs_health_read(owgs_ctx* ctx, int32_t cap, int32_t* n, uint8_t* status, int64_t* user_memory_bytes,
+                     int32_t* test_actions, uint32_t* ring, int64_t* next_tick);
+
 /* Restore the slot state captured by owgs_snapshot (bench: every timed step starts from the same state). */
 int owgs_snapshot(owgs_ctx* ctx);
 int owgs_restore(owgs_ctx* ctx, void* stream);

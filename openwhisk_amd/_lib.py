@@ -74,6 +74,8 @@ def lib() -> C.CDLL:
         "owgs_last_error": (C.c_char_p, [P]),
         "owgs_update_invokers": (C.c_int, [P, i32, P, P, P]),
         "owgs_update_cluster": (C.c_int, [P, i32]),
+        "owgs_health_events": (C.c_int, [P, i32, P, P, P, P, C.c_int64, i32]),
+        "owgs_health_read": (C.c_int, [P, i32, P, P, P, P, P, P]),
         "owgs_register_actions": (C.c_int, [P, i32, P, P, P, P, P, P, P, P, P, P, P]),
         "owgs_publish_batch": (C.c_int, [P, i32, P, P, u64, P, P]),
         "owgs_release_batch": (C.c_int, [P, i32, P, P, P]),

@@ -127,6 +127,32 @@ class GpuShardingContainerPoolBalancer:
         return out[: n.value].tolist()
 
     # ------------------------------------------------------------------ completion path (CLB:148-166, 205-346)
+    def health_events(self, invoker, kind, t_ms, user_memory, now_ms: int, apply: bool = False) -> None:
+        """InvokerPool + InvokerActor FSMs (InvokerSupervision.scala:95-440) for a batch of supervision events in
+        mailbox order; apply=True hands the status vector to updateInvokers (SCPB:226-227)."""
+        inv = np.ascontiguousarray(invoker, dtype=np.int32)
+        k = np.ascontiguousarray(kind, dtype=np.uint8)
+        t = np.ascontiguousarray(t_ms, dtype=np.int64)
+        m = np.ascontiguousarray(user_memory, dtype=np.int64)
+        n = len(inv)
+        if not (len(k) == len(t) == len(m) == n):
+            raise ValueError("health_events: arrays of different lengths")
+        self._chk(self._L.owgs_health_events(self._h, n, _p(inv) if n else None, _p(k) if n else None,
+                                             _p(t) if n else None, _p(m) if n else None, int(now_ms), int(apply)))
+
+    def health_read(self):
+        """GetStatus (InvokerSupervision.scala:132): (status, userMemory, test actions of the last batch, ring, tick)."""
+        n = C.c_int32(0)
+        self._chk(self._L.owgs_health_read(self._h, 0, C.byref(n), None, None, None, None, None))
+        m = n.value
+        st = np.zeros(max(m, 1), np.uint8)
+        mem = np.zeros(max(m, 1), np.int64)
+        te = np.zeros(max(m, 1), np.int32)
+        ring = np.zeros(max(m, 1), np.uint32)
+        tick = np.zeros(max(m, 1), np.int64)
+        self._chk(self._L.owgs_health_read(self._h, m, None, _p(st), _p(mem), _p(te), _p(ring), _p(tick)))
+        return st[:m], mem[:m], te[:m], ring[:m], tick[:m]
+
     def set_health_tid(self, start_ms: int):
         """TransactionId.invokerHealth's start time (TransactionId.scala:225): health acks echo it."""
         self._chk(self._L.owgs_set_health_tid(self._h, start_ms))

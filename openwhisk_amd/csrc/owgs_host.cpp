@@ -54,6 +54,16 @@ extern "C" hipError_t owgs_launch_act_track(const OwgsActTable* T, const ulonglo
 extern "C" hipError_t owgs_launch_ack_complete(const OwgsActTable* T, const OwgsAckCompleteArgs* a, hipStream_t st);
 extern "C" hipError_t owgs_launch_ack_flags(int32_t n, const uint8_t* info, const uint8_t* rflags,
                                             const uint8_t* out_kind, uint8_t* out_flags, hipStream_t st);
+extern "C" hipError_t owgs_launch_health_init(uint8_t* s, uint32_t* ring, int64_t* last, int64_t* tick, int64_t* mem,
+                                              int32_t* tests, int32_t from, int32_t to, hipStream_t st);
+extern "C" size_t owgs_health_sort_bytes(int32_t n, int32_t bits);
+extern "C" hipError_t owgs_launch_health_batch(const int32_t* ev_inv, const uint8_t* ev_kind, const int64_t* ev_t,
+                                               const int64_t* ev_mem, int32_t n, int32_t bits, void* temp,
+                                               size_t temp_bytes, int32_t* key_out, int32_t* idx_in,
+                                               int32_t* idx_out, int64_t* packed, int32_t* seg_beg, int32_t* seg_end,
+                                               int32_t* reg_first, int32_t* pad_src, uint8_t* s, uint32_t* ring,
+                                               int64_t* last, int64_t* tick, int64_t* mem, int32_t* tests,
+                                               int32_t old_size, int32_t new_size, int64_t now, hipStream_t st);
 extern "C" size_t owgs_engine_lds_bytes(int n_slots, int pool_mode, int n_ids, int nm, int nb, int n_actions);
 
 namespace {
@@ -150,6 +160,13 @@ struct owgs_ctx {
     DevBuf<int64_t> k_off;
     DevBuf<char> k_aid;
     DevBuf<unsigned long long> k_cnt;
+    // invoker health supervision (owgs_health.hip): persistent SoA by invoker id + per-batch scratch
+    DevBuf<uint8_t> h_st, he_kind, he_temp;
+    DevBuf<uint32_t> h_ring;
+    DevBuf<int64_t> h_last, h_tick, h_mem, he_t, he_mem, he_packed;
+    DevBuf<int32_t> h_tests, he_inv, he_key, he_idx0, he_idx1, he_beg, he_end, he_reg, he_pad;
+    int32_t h_cap = 0, h_size = 0;
+    int64_t h_now = INT64_MIN;
     // snapshot
     DevBuf<int32_t> s_permits;
     DevBuf<uint32_t> s_ct_keys, s_ct_vals;
@@ -504,6 +521,15 @@ void owgs_destroy(owgs_ctx* c) {
     c->k_off.release();
     c->k_aid.release();
     c->k_cnt.release();
+    c->h_st.release();
+    c->he_kind.release();
+    c->he_temp.release();
+    c->h_ring.release();
+    DevBuf<int64_t>* h64[] = {&c->h_last, &c->h_tick, &c->h_mem, &c->he_t, &c->he_mem, &c->he_packed};
+    for (auto* b : h64) b->release();
+    DevBuf<int32_t>* h32[] = {&c->h_tests, &c->he_inv, &c->he_key, &c->he_idx0, &c->he_idx1,
+                              &c->he_beg,  &c->he_end, &c->he_reg, &c->he_pad};
+    for (auto* b : h32) b->release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1283,5 +1309,127 @@ int owgs_complete_activations(owgs_ctx* c, int32_t n, const char* aid32, const i
     HIPCHK(c, hipMemcpy(out_kind, c->k_kind.p, (size_t)n, hipMemcpyDeviceToHost));
     HIPCHK(c, hipMemcpy(out_ticket, c->k_tick.p, (size_t)n * 4, hipMemcpyDeviceToHost));
     HIPCHK(c, hipMemcpy(out_flags, c->k_oflags.p, (size_t)n, hipMemcpyDeviceToHost));
+    return OWGS_OK;
+}
+
+// ------------------------------------------------------------------------------------------ health supervision
+// grow a persistent per-invoker array to cap entries, keeping the first `keep`
+template <class T>
+static hipError_t grow_keep(DevBuf<T>& d, size_t cap, size_t keep, hipStream_t st) {
+    DevBuf<T> nb;
+    hipError_t e = nb.reserve(cap);
+    if (e != hipSuccess) return e;
+    if (keep && d.p) {
+        e = hipMemcpyAsync(nb.p, d.p, keep * sizeof(T), hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) {
+            nb.release();
+            return e;
+        }
+        e = hipStreamSynchronize(st);
+        if (e != hipSuccess) {
+            nb.release();
+            return e;
+        }
+    }
+    d.release();
+    d = nb;
+    nb.p = nullptr;
+    nb.n = 0;
+    return hipSuccess;
+}
+
+int owgs_health_events(owgs_ctx* c, int32_t n, const int32_t* invoker, const uint8_t* kind, const int64_t* t_ms,
+                       const int64_t* user_memory_bytes, int64_t now_ms, int32_t apply) {
+    if (!c || n < 0 || (n > 0 && (!invoker || !kind || !t_ms || !user_memory_bytes))) return OWGS_EINVAL;
+    // argument contract (mailbox order with a clock): validated before any state changes
+    int64_t prev = c->h_now;
+    int32_t max_id = -1, max_ping = -1;
+    for (int32_t e = 0; e < n; ++e) {
+        if (kind[e] > OWGS_EV_STATE_TIMEOUT || invoker[e] < 0 || t_ms[e] < prev || t_ms[e] >= (1LL << 60))
+            return c->fail(OWGS_EINVAL, "health event: kind > 4, negative invoker, time before the previous one or "
+                                        "outside [0, 2^60)");
+        prev = t_ms[e];
+        max_id = std::max(max_id, invoker[e]);
+        if (kind[e] == OWGS_EV_PING) max_ping = std::max(max_ping, invoker[e]);
+    }
+    if (now_ms < prev || now_ms < 0 || now_ms >= (1LL << 60))
+        return c->fail(OWGS_EINVAL, "health batch: now before its last event or outside [0, 2^60)");
+    (void)hipSetDevice(c->cfg.device);
+    hipStream_t st = c->stream;
+    const int32_t old_size = c->h_size;
+    const int32_t new_size = std::max(old_size, max_ping + 1);
+    if (new_size > c->h_cap) {
+        int32_t cap = c->h_cap ? c->h_cap : 1024;
+        while (cap < new_size) cap *= 2;
+        const size_t keep = (size_t)c->h_cap;
+        HIPCHK(c, grow_keep(c->h_st, cap, keep, st));
+        HIPCHK(c, grow_keep(c->h_ring, cap, keep, st));
+        HIPCHK(c, grow_keep(c->h_last, cap, keep, st));
+        HIPCHK(c, grow_keep(c->h_tick, cap, keep, st));
+        HIPCHK(c, grow_keep(c->h_mem, cap, keep, st));
+        HIPCHK(c, grow_keep(c->h_tests, cap, keep, st));
+        HIPCHK(c, owgs_launch_health_init(c->h_st.p, c->h_ring.p, c->h_last.p, c->h_tick.p, c->h_mem.p, c->h_tests.p,
+                                          c->h_cap, cap, st));
+        c->h_cap = cap;
+    }
+    HIPCHK(c, upload(c->he_inv, invoker, (size_t)n, st));
+    HIPCHK(c, upload(c->he_kind, kind, (size_t)n, st));
+    HIPCHK(c, upload(c->he_t, t_ms, (size_t)n, st));
+    HIPCHK(c, upload(c->he_mem, user_memory_bytes, (size_t)n, st));
+    int32_t bits = 1;
+    while (bits < 31 && (max_id >> bits) != 0) ++bits;
+    const size_t tb = n ? owgs_health_sort_bytes(n, bits) : 0;
+    HIPCHK(c, c->he_temp.reserve(tb));
+    HIPCHK(c, c->he_key.reserve((size_t)n));
+    HIPCHK(c, c->he_idx0.reserve((size_t)n));
+    HIPCHK(c, c->he_idx1.reserve((size_t)n));
+    HIPCHK(c, c->he_packed.reserve((size_t)n));
+    HIPCHK(c, c->he_beg.reserve((size_t)new_size));
+    HIPCHK(c, c->he_end.reserve((size_t)new_size));
+    HIPCHK(c, c->he_reg.reserve((size_t)new_size));
+    HIPCHK(c, c->he_pad.reserve((size_t)new_size));
+    HIPCHK(c, owgs_launch_health_batch(c->he_inv.p, c->he_kind.p, c->he_t.p, c->he_mem.p, n, bits, c->he_temp.p, tb,
+                                       c->he_key.p, c->he_idx0.p, c->he_idx1.p, c->he_packed.p, c->he_beg.p,
+                                       c->he_end.p, c->he_reg.p,
+                                       c->he_pad.p, c->h_st.p, c->h_ring.p, c->h_last.p, c->h_tick.p, c->h_mem.p,
+                                       c->h_tests.p, old_size, new_size, now_ms, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    c->h_size = new_size;
+    c->h_now = now_ms;
+    if (!apply) return OWGS_OK;
+    // CurrentInvokerPoolState -> monitor -> updateInvokers (SCPB:226-227): ids are the positions (InvokerPool keeps
+    // status(i).id.toInt == i, ISUP:186-191)
+    std::vector<int32_t> ids(new_size);
+    std::vector<int64_t> mem(new_size);
+    std::vector<uint8_t> sts(new_size);
+    int rc = owgs_health_read(c, new_size, nullptr, sts.data(), mem.data(), nullptr, nullptr, nullptr);
+    if (rc) return rc;
+    for (int32_t i = 0; i < new_size; ++i) ids[i] = i;
+    return owgs_update_invokers(c, new_size, ids.data(), mem.data(), sts.data());
+}
+
+int owgs_health_read(owgs_ctx* c, int32_t cap, int32_t* n, uint8_t* status, int64_t* user_memory_bytes,
+                     int32_t* test_actions, uint32_t* ring, int64_t* next_tick) {
+    if (!c || cap < 0) return OWGS_EINVAL;
+    if (n) *n = c->h_size;
+    const int32_t m = c->h_size;
+    if (m == 0) return OWGS_OK;
+    if (!status && !user_memory_bytes && !test_actions && !ring && !next_tick) return OWGS_OK;  // size query
+    if (cap < m) return c->fail(OWGS_ERANGE, "health read: capacity below the status vector size");
+    (void)hipSetDevice(c->cfg.device);
+    hipStream_t st = c->stream;
+    if (status) HIPCHK(c, hipMemcpyAsync(status, c->h_st.p, (size_t)m, hipMemcpyDeviceToHost, st));
+    if (user_memory_bytes)
+        HIPCHK(c, hipMemcpyAsync(user_memory_bytes, c->h_mem.p, (size_t)m * 8, hipMemcpyDeviceToHost, st));
+    if (test_actions) HIPCHK(c, hipMemcpyAsync(test_actions, c->h_tests.p, (size_t)m * 4, hipMemcpyDeviceToHost, st));
+    if (ring) HIPCHK(c, hipMemcpyAsync(ring, c->h_ring.p, (size_t)m * 4, hipMemcpyDeviceToHost, st));
+    if (next_tick) HIPCHK(c, hipMemcpyAsync(next_tick, c->h_tick.p, (size_t)m * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    if (status)  // an entry without an actor (padToIndexed) is Offline
+        for (int32_t i = 0; i < m; ++i)
+            if (status[i] > OWGS_OFFLINE) status[i] = OWGS_OFFLINE;
+    if (next_tick)
+        for (int32_t i = 0; i < m; ++i)
+            if (next_tick[i] == INT64_MAX) next_tick[i] = -1;
     return OWGS_OK;
 }

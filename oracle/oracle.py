@@ -431,3 +431,49 @@ class AckFlow:
 def _rel_bits(rf: int) -> int:
     """owo_release result -> OWGS_REL_* bits (NoSuchElement 1, overflow 2)."""
     return {0: 0, THROW_NOSUCHELEMENT: 1, THROW_OVERFLOW: 2}.get(rf, 0)
+
+
+# ------------------------------------------------------------------------------------------------ health supervision
+EV_PING, EV_SUCCESS, EV_SYSTEM_ERROR, EV_TIMEOUT, EV_STATE_TIMEOUT = 0, 1, 2, 3, 4
+
+
+class HealthPool:
+    """InvokerPool + InvokerActor FSMs (InvokerSupervision.scala:95-440) restated in oracle/owhealth_oracle.c."""
+
+    def __init__(self, start_ms: int = 0):
+        L = lib()
+        L.owh_new.restype = C.c_void_p
+        L.owh_new.argtypes = [C.c_int64]
+        L.owh_free.argtypes = [C.c_void_p]
+        L.owh_events.restype = C.c_int
+        L.owh_events.argtypes = [C.c_void_p, C.c_int32] + [C.c_void_p] * 4 + [C.c_int64]
+        L.owh_size.restype = C.c_int32
+        L.owh_size.argtypes = [C.c_void_p]
+        L.owh_read.argtypes = [C.c_void_p] + [C.c_void_p] * 5
+        self._L = L
+        self.h = L.owh_new(start_ms)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self._L.owh_free(self.h)
+            self.h = None
+
+    def events(self, invoker, kind, t_ms, user_memory, now_ms: int) -> None:
+        inv = np.ascontiguousarray(invoker, dtype=np.int32)
+        k = np.ascontiguousarray(kind, dtype=np.uint8)
+        t = np.ascontiguousarray(t_ms, dtype=np.int64)
+        m = np.ascontiguousarray(user_memory, dtype=np.int64)
+        rc = self._L.owh_events(self.h, len(inv), _ptr(inv), _ptr(k), _ptr(t), _ptr(m), int(now_ms))
+        if rc:
+            raise ValueError(f"owh_events rc={rc}")
+
+    def read(self):
+        """(status u8, userMemory i64, test actions of the last batch i32, ring u32, next tick i64 (-1 none))"""
+        n = self._L.owh_size(self.h)
+        st = np.zeros(max(n, 1), np.uint8)
+        mem = np.zeros(max(n, 1), np.int64)
+        te = np.zeros(max(n, 1), np.int32)
+        ring = np.zeros(max(n, 1), np.uint32)
+        tick = np.zeros(max(n, 1), np.int64)
+        self._L.owh_read(self.h, _ptr(st), _ptr(mem), _ptr(te), _ptr(ring), _ptr(tick))
+        return st[:n], mem[:n], te[:n], ring[:n], tick[:n]
