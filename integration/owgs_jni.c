@@ -87,6 +87,97 @@ JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00
     return rc;
 }
 
+/* ---- completion path (CommonLoadBalancer.setupActivation / processAcknowledgement / processCompletion) ---- */
+JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_trackActivations(
+    JNIEnv* env, jobject self, jlong h, jbyteArray aid32, jintArray actions, jintArray tickets, jint n,
+    jintArray outTicket, jbyteArray outExisted) {
+    jbyte* pa = (*env)->GetPrimitiveArrayCritical(env, aid32, NULL);
+    jint* pc = (*env)->GetPrimitiveArrayCritical(env, actions, NULL);
+    jint* pt = (*env)->GetPrimitiveArrayCritical(env, tickets, NULL);
+    jint* po = (*env)->GetPrimitiveArrayCritical(env, outTicket, NULL);
+    jbyte* pe = (*env)->GetPrimitiveArrayCritical(env, outExisted, NULL);
+    const int rc = owgs_track_activations(CTX(h), n, (const char*)pa, (const int32_t*)pc, (const int32_t*)pt,
+                                          (int32_t*)po, (uint8_t*)pe);
+    (*env)->ReleasePrimitiveArrayCritical(env, outExisted, pe, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, outTicket, po, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, tickets, pt, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, actions, pc, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, aid32, pa, JNI_ABORT);
+    return rc;
+}
+
+/* raw ack bytes of one feed batch (MessageFeed hands the consumer's records over as Array[Byte], LB:94-108) */
+JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_processAcks(
+    JNIEnv* env, jobject self, jlong h, jbyteArray bytes, jlongArray off, jint n, jbyteArray outKind,
+    jintArray outInvoker, jintArray outTicket, jbyteArray outFlags) {
+    jbyte* pb = (*env)->GetPrimitiveArrayCritical(env, bytes, NULL);
+    jlong* po = (*env)->GetPrimitiveArrayCritical(env, off, NULL);
+    jbyte* pk = (*env)->GetPrimitiveArrayCritical(env, outKind, NULL);
+    jint* pi = (*env)->GetPrimitiveArrayCritical(env, outInvoker, NULL);
+    jint* pt = (*env)->GetPrimitiveArrayCritical(env, outTicket, NULL);
+    jbyte* pf = (*env)->GetPrimitiveArrayCritical(env, outFlags, NULL);
+    const int rc = owgs_process_acks(CTX(h), n, (const char*)pb, (const int64_t*)po, (uint8_t*)pk, (int32_t*)pi,
+                                     (int32_t*)pt, (uint8_t*)pf);
+    (*env)->ReleasePrimitiveArrayCritical(env, outFlags, pf, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, outTicket, pt, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, outInvoker, pi, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, outKind, pk, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, off, po, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, bytes, pb, JNI_ABORT);
+    return rc;
+}
+
+JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_completeActivations(
+    JNIEnv* env, jobject self, jlong h, jbyteArray aid32, jintArray invokers, jbyteArray flags, jint n,
+    jbyteArray outKind, jintArray outTicket, jbyteArray outFlags) {
+    jbyte* pa = (*env)->GetPrimitiveArrayCritical(env, aid32, NULL);
+    jint* pi = (*env)->GetPrimitiveArrayCritical(env, invokers, NULL);
+    jbyte* pc = (*env)->GetPrimitiveArrayCritical(env, flags, NULL);
+    jbyte* pk = (*env)->GetPrimitiveArrayCritical(env, outKind, NULL);
+    jint* pt = (*env)->GetPrimitiveArrayCritical(env, outTicket, NULL);
+    jbyte* pf = (*env)->GetPrimitiveArrayCritical(env, outFlags, NULL);
+    const int rc = owgs_complete_activations(CTX(h), n, (const char*)pa, (const int32_t*)pi, (const uint8_t*)pc,
+                                             (uint8_t*)pk, (int32_t*)pt, (uint8_t*)pf);
+    (*env)->ReleasePrimitiveArrayCritical(env, outFlags, pf, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, outTicket, pt, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, outKind, pk, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, flags, pc, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, invokers, pi, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, aid32, pa, JNI_ABORT);
+    return rc;
+}
+
+/* ---- invoker health supervision (InvokerPool + InvokerActor) ---- */
+JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_healthEvents(
+    JNIEnv* env, jobject self, jlong h, jintArray invokers, jbyteArray kinds, jlongArray tMs, jlongArray userMemory,
+    jint n, jlong nowMs, jboolean apply) {
+    jint* pi = (*env)->GetPrimitiveArrayCritical(env, invokers, NULL);
+    jbyte* pk = (*env)->GetPrimitiveArrayCritical(env, kinds, NULL);
+    jlong* pt = (*env)->GetPrimitiveArrayCritical(env, tMs, NULL);
+    jlong* pm = (*env)->GetPrimitiveArrayCritical(env, userMemory, NULL);
+    const int rc = owgs_health_events(CTX(h), n, (const int32_t*)pi, (const uint8_t*)pk, (const int64_t*)pt,
+                                      (const int64_t*)pm, nowMs, apply ? 1 : 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, userMemory, pm, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, tMs, pt, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, kinds, pk, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, invokers, pi, JNI_ABORT);
+    return rc;
+}
+
+/* status vector + test actions to send (the shim sends one health test action per count, InvokerPool.ActivationRequest) */
+JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_healthRead(
+    JNIEnv* env, jobject self, jlong h, jint cap, jbyteArray status, jlongArray userMemory, jintArray tests) {
+    int32_t n = 0;
+    jbyte* ps = (*env)->GetPrimitiveArrayCritical(env, status, NULL);
+    jlong* pm = (*env)->GetPrimitiveArrayCritical(env, userMemory, NULL);
+    jint* pt = (*env)->GetPrimitiveArrayCritical(env, tests, NULL);
+    const int rc = owgs_health_read(CTX(h), cap, &n, (uint8_t*)ps, (int64_t*)pm, (int32_t*)pt, NULL, NULL);
+    (*env)->ReleasePrimitiveArrayCritical(env, tests, pt, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, userMemory, pm, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, status, ps, 0);
+    return rc == OWGS_OK ? n : rc;
+}
+
 JNIEXPORT jstring JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_lastError(JNIEnv* env,
                                                                                                jobject self, jlong h) {
     return (*env)->NewStringUTF(env, owgs_last_error(CTX(h)));
