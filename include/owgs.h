@@ -225,6 +225,51 @@ int owgs_health_events(owgs_ctx* ctx, int32_t n, const int32_t* invoker, const u
 int owgs_health_read(owgs_ctx* ctx, int32_t cap, int32_t* n, uint8_t* status, int64_t* user_memory_bytes,
                      int32_t* test_actions, uint32_t* ring, int64_t* next_tick);
 
+/* ---- ActivationMessage serialisation + per-invoker topic fan-out ----
+ * Replaces: ActivationMessage.serialize (jsonFormat11 + spray-json compactPrint, Message.scala:51-70, 170-175) and
+ * the per-activation producer.send to topic "invoker<N>" (sendActivationToInvoker, CommonLoadBalancer.scala:175-198)
+ * for a batch of publishes.  The invariant members are templates printed once per (action, identity) by the caller:
+ * part A = the three members `"action":<fqn>,"revision":<rev>,"user":<identity>` (no surrounding commas), part B =
+ * the initArgs array value; rootControllerIndex is one JSON value per context.  Templates append; returns the id
+ * of the first new one. */
+int owgs_register_templates(owgs_ctx* ctx, int32_t n, const char* a_bytes, const int64_t* a_off, const char* b_bytes,
+                            const int64_t* b_off, int32_t* out_first_id);
+int owgs_set_root_controller(owgs_ctx* ctx, const char* json, int32_t len);
+
+#define OWGS_MSG_BLOCKING 1       /* ActivationMessage.blocking */
+#define OWGS_MSG_EXTRA_LOGGING 2  /* transid.meta.extraLogging: ["id", start, true] */
+#define OWGS_MSG_HAS_CONTENT 4    /* content = Some(JsObject) (printed, in content/content_off) */
+#define OWGS_MSG_HAS_CAUSE 8      /* cause = Some(ActivationId) */
+#define OWGS_MSG_HAS_TRACE 16     /* traceContext = Some(Map) (printed, in trace/trace_off) */
+typedef struct owgs_msg_batch {
+    int32_t n;
+    const int32_t* invoker;      /* the publish decisions (owgs_publish_batch out_invoker); < 0: no message */
+    const int32_t* tmpl;         /* template id per activation */
+    const uint64_t* aid;         /* 2 per activation: the 32 hex digits of ActivationId as (hi, lo) */
+    const char* tid;             /* TransactionId.meta.id strings, UTF-8, offsets tid_off[0..n] */
+    const int64_t* tid_off;
+    const int64_t* tid_start;    /* TransactionId.meta.start, epoch ms */
+    const uint8_t* flags;        /* OWGS_MSG_* */
+    const char* content;         /* may be NULL when no flag asks for it */
+    const int64_t* content_off;
+    const uint64_t* cause;       /* 2 per activation */
+    const char* trace;
+    const int64_t* trace_off;
+} owgs_msg_batch;
+/* Host buffers.  Output: the m messages (activations with invoker >= 0) grouped by invoker id ascending, publish order
+ * within a topic: bytes out[out_off[j] .. out_off[j+1]), out_order[j] = activation index, topic_start[k] ..
+ * topic_start[k+1] = the messages of topic "invoker<k>" for k < n_topics.  out_off has n + 1 entries, out_order n,
+ * topic_start n_topics + 1.  *total = bytes needed; OWGS_ERANGE (nothing written) when it exceeds cap; OWGS_EINVAL
+ * for an invoker >= n_topics, an unknown template or a malformed UTF-8 transaction id. */
+int owgs_serialize_activations(owgs_ctx* ctx, const owgs_msg_batch* batch, int32_t n_topics, char* out, int64_t cap,
+                               int64_t* out_off, int32_t* out_order, int32_t* topic_start, int64_t* total,
+                               int32_t* m);
+/* Same with every pointer of batch and the outputs in device memory (e.g. invoker = owgs_replay_device's out_invoker),
+ * on `stream`; *total and *m are host values (the call synchronises once). */
+int owgs_serialize_activations_device(owgs_ctx* ctx, const owgs_msg_batch* batch, int32_t n_topics, char* out,
+                                      int64_t cap, int64_t* out_off, int32_t* out_order, int32_t* topic_start,
+                                      int64_t* total, int32_t* m, void* stream);
+
 /* Restore the slot state captured by owgs_snapshot (bench: every timed step starts from the same state). */
 int owgs_snapshot(owgs_ctx* ctx);
 int owgs_restore(owgs_ctx* ctx, void* stream);

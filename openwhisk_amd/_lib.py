@@ -41,6 +41,12 @@ class owgs_config(C.Structure):
     ]
 
 
+class owgs_msg_batch(C.Structure):
+    _fields_ = [("n", C.c_int32)] + [(k, C.c_void_p) for k in (
+        "invoker", "tmpl", "aid", "tid", "tid_off", "tid_start", "flags", "content", "content_off", "cause", "trace",
+        "trace_off")]
+
+
 def build(verbose: bool = False) -> str:
     """Compile libowgs.so for gfx950 in-tree."""
     out = subprocess.run(["make", "-s", "-C", PKG], capture_output=not verbose, text=True)
@@ -64,6 +70,12 @@ def lib() -> C.CDLL:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise OwgsError(EDEVICE, f"{LIB_PATH} is missing: run openwhisk_amd._lib.build() (hipcc, gfx950)")
+    # PyTorch-ROCm ships its own HIP runtime: when both are used in one process, torch's must be the one loaded
+    # (libowgs.so then binds to it by soname); loading libowgs first leaves torch without a visible device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     i32, u64, P = C.c_int32, C.c_uint64, C.c_void_p
     sig = {
@@ -75,6 +87,10 @@ def lib() -> C.CDLL:
         "owgs_update_invokers": (C.c_int, [P, i32, P, P, P]),
         "owgs_update_cluster": (C.c_int, [P, i32]),
         "owgs_health_events": (C.c_int, [P, i32, P, P, P, P, C.c_int64, i32]),
+        "owgs_register_templates": (C.c_int, [P, i32, P, P, P, P, P]),
+        "owgs_set_root_controller": (C.c_int, [P, C.c_char_p, i32]),
+        "owgs_serialize_activations": (C.c_int, [P, P, i32, P, C.c_int64, P, P, P, P, P]),
+        "owgs_serialize_activations_device": (C.c_int, [P, P, i32, P, C.c_int64, P, P, P, P, P, P]),
         "owgs_health_read": (C.c_int, [P, i32, P, P, P, P, P, P]),
         "owgs_register_actions": (C.c_int, [P, i32, P, P, P, P, P, P, P, P, P, P, P]),
         "owgs_publish_batch": (C.c_int, [P, i32, P, P, u64, P, P]),

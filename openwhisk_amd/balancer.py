@@ -14,7 +14,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from ._lib import (FLAG_OVERLOAD, HEALTHY, NONE, OFFLINE, THROW_INDEX, UNHEALTHY, UNRESPONSIVE, OwgsError,
+from ._lib import (ERANGE, FLAG_OVERLOAD, HEALTHY, NONE, OFFLINE, THROW_INDEX, UNHEALTHY, UNRESPONSIVE, OwgsError,
                    owgs_config)
 
 __all__ = ["GpuShardingContainerPoolBalancer", "InvokerHealth", "Action", "NONE", "THROW_INDEX", "FLAG_OVERLOAD",
@@ -57,6 +57,14 @@ def _pack(strings: list[str]) -> tuple[bytes, np.ndarray]:
     off = np.zeros(len(enc) + 1, dtype=np.int32)
     off[1:] = np.cumsum([len(b) for b in enc])
     return b"".join(enc), off
+
+
+def _blob(items) -> tuple[np.ndarray, np.ndarray]:
+    """str (UTF-8) or bytes items -> (byte buffer, int64 offsets[n + 1])."""
+    enc = [x.encode("utf-8") if isinstance(x, str) else bytes(x) for x in items]
+    off = np.zeros(len(enc) + 1, dtype=np.int64)
+    off[1:] = np.cumsum([len(b) for b in enc])
+    return np.frombuffer(b"".join(enc) + b"\0", dtype=np.uint8), off
 
 
 class GpuShardingContainerPoolBalancer:
@@ -152,6 +160,63 @@ class GpuShardingContainerPoolBalancer:
         tick = np.zeros(max(m, 1), np.int64)
         self._chk(self._L.owgs_health_read(self._h, m, None, _p(st), _p(mem), _p(te), _p(ring), _p(tick)))
         return st[:m], mem[:m], te[:m], ring[:m], tick[:m]
+
+    def register_templates(self, part_a: list[str], part_b: list[str]) -> int:
+        """ActivationMessage invariant members per (action, identity): part A = '"action":..,"revision":..,"user":..',
+        part B = the initArgs array.  Returns the first new template id."""
+        ab, ao = _blob(part_a)
+        bb, bo = _blob(part_b)
+        first = C.c_int32(0)
+        self._chk(self._L.owgs_register_templates(self._h, len(part_a), _p(ab), _p(ao), _p(bb), _p(bo),
+                                                  C.byref(first)))
+        return first.value
+
+    def set_root_controller(self, json_value: str):
+        b = json_value.encode()
+        self._chk(self._L.owgs_set_root_controller(self._h, b, len(b)))
+
+    def serialize_activations(self, invoker, tmpl, aid_words, tids: list[str], tid_start, flags, contents=None,
+                              causes=None, traces=None, n_topics: int | None = None, cap: int | None = None):
+        """ActivationMessage.serialize + the per-invoker fan-out of sendActivationToInvoker (Message.scala:51-70,
+        CLB:175-198): (bytes, out_off, out_order, topic_start)."""
+        from ._lib import owgs_msg_batch
+        n = len(invoker)
+        inv = np.ascontiguousarray(invoker, dtype=np.int32)
+        tm = np.ascontiguousarray(tmpl, dtype=np.int32)
+        aid = np.ascontiguousarray(aid_words, dtype=np.uint64).reshape(-1)
+        tb, to = _blob(tids)
+        ts = np.ascontiguousarray(tid_start, dtype=np.int64)
+        fl = np.ascontiguousarray(flags, dtype=np.uint8)
+        keep = [inv, tm, aid, tb, to, ts, fl]
+        B = owgs_msg_batch(n, _p(inv), _p(tm), _p(aid), _p(tb), _p(to), _p(ts), _p(fl))
+        if contents is not None:
+            cb, co = _blob(contents)
+            keep += [cb, co]
+            B.content, B.content_off = _p(cb), _p(co)
+        if causes is not None:
+            cz = np.ascontiguousarray(causes, dtype=np.uint64).reshape(-1)
+            keep.append(cz)
+            B.cause = _p(cz)
+        if traces is not None:
+            rb, ro = _blob(traces)
+            keep += [rb, ro]
+            B.trace, B.trace_off = _p(rb), _p(ro)
+        nt = int(n_topics if n_topics is not None else (inv.max() + 1 if n and inv.max() >= 0 else 0))
+        off = np.zeros(n + 1, np.int64)
+        order = np.zeros(max(n, 1), np.int32)
+        topic = np.zeros(nt + 1, np.int32)
+        total, m = C.c_int64(0), C.c_int32(0)
+        if cap is None:  # size query first
+            rc = self._L.owgs_serialize_activations(self._h, C.byref(B), nt, None, 0, _p(off), _p(order), _p(topic),
+                                                    C.byref(total), C.byref(m))
+            if rc not in (0, ERANGE):
+                self._chk(rc)
+            cap = total.value
+        out = C.create_string_buffer(max(cap, 1))
+        self._chk(self._L.owgs_serialize_activations(self._h, C.byref(B), nt, out, cap, _p(off), _p(order),
+                                                     _p(topic), C.byref(total), C.byref(m)))
+        mm = m.value
+        return out.raw[:total.value], off[:mm + 1], order[:mm], topic
 
     def set_health_tid(self, start_ms: int):
         """TransactionId.invokerHealth's start time (TransactionId.scala:225): health acks echo it."""

@@ -64,6 +64,11 @@ extern "C" hipError_t owgs_launch_health_batch(const int32_t* ev_inv, const uint
                                                int32_t* reg_first, int32_t* pad_src, uint8_t* s, uint32_t* ring,
                                                int64_t* last, int64_t* tick, int64_t* mem, int32_t* tests,
                                                int32_t old_size, int32_t new_size, int64_t now, hipStream_t st);
+extern "C" size_t owgs_msg_scratch_bytes(int32_t n, int32_t n_topics, int32_t bits);
+extern "C" hipError_t owgs_launch_msg_plan(const OwgsMsgArgs* a, int32_t bits, void* temp, size_t temp_bytes,
+                                           uint32_t* key_sorted, int32_t* iota, int64_t* len_sorted, int32_t* cnt,
+                                           hipStream_t st);
+extern "C" hipError_t owgs_launch_msg_write(const OwgsMsgArgs* a, hipStream_t st);
 extern "C" size_t owgs_engine_lds_bytes(int n_slots, int pool_mode, int n_ids, int nm, int nb, int n_actions);
 
 namespace {
@@ -166,6 +171,18 @@ struct owgs_ctx {
     DevBuf<int64_t> h_last, h_tick, h_mem, he_t, he_mem, he_packed;
     DevBuf<int32_t> h_tests, he_inv, he_key, he_idx0, he_idx1, he_beg, he_end, he_reg, he_pad;
     int32_t h_cap = 0, h_size = 0;
+    // ActivationMessage templates + serialisation scratch (owgs_msgs.hip)
+    std::vector<char> ta, tb;
+    std::vector<int64_t> ta_off{0}, tb_off{0};
+    std::string rci = "{\"asString\":\"0\"}";  // ControllerInstanceId("0"), jsonFormat1 (InstanceId.scala:40, 59)
+    bool tmpl_dirty = true;
+    DevBuf<char> m_ta, m_tb, m_rci, m_tid, m_content, m_trace, m_out;
+    DevBuf<int64_t> m_ta_off, m_tb_off, m_tid_off, m_tid_start, m_content_off, m_trace_off, m_len, m_len_sorted,
+        m_out_off;
+    DevBuf<int32_t> m_inv, m_tmpl, m_bad, m_order, m_iota, m_cnt, m_topic;
+    DevBuf<uint32_t> m_key, m_key_sorted;
+    DevBuf<ulonglong2> m_aid, m_cause;
+    DevBuf<uint8_t> m_flags, m_temp;
     int64_t h_now = INT64_MIN;
     // snapshot
     DevBuf<int32_t> s_permits;
@@ -521,6 +538,19 @@ void owgs_destroy(owgs_ctx* c) {
     c->k_off.release();
     c->k_aid.release();
     c->k_cnt.release();
+    DevBuf<char>* mc[] = {&c->m_ta, &c->m_tb, &c->m_rci, &c->m_tid, &c->m_content, &c->m_trace, &c->m_out};
+    for (auto* b : mc) b->release();
+    DevBuf<int64_t>* m64[] = {&c->m_ta_off, &c->m_tb_off, &c->m_tid_off, &c->m_tid_start, &c->m_content_off,
+                              &c->m_trace_off, &c->m_len, &c->m_len_sorted, &c->m_out_off};
+    for (auto* b : m64) b->release();
+    DevBuf<int32_t>* m32[] = {&c->m_inv, &c->m_tmpl, &c->m_bad, &c->m_order, &c->m_iota, &c->m_cnt, &c->m_topic};
+    for (auto* b : m32) b->release();
+    c->m_key.release();
+    c->m_key_sorted.release();
+    c->m_aid.release();
+    c->m_cause.release();
+    c->m_flags.release();
+    c->m_temp.release();
     c->h_st.release();
     c->he_kind.release();
     c->he_temp.release();
@@ -1432,4 +1462,209 @@ int owgs_health_read(owgs_ctx* c, int32_t cap, int32_t* n, uint8_t* status, int6
         for (int32_t i = 0; i < m; ++i)
             if (next_tick[i] == INT64_MAX) next_tick[i] = -1;
     return OWGS_OK;
+}
+
+// ------------------------------------------------------------------------------------------ ActivationMessage output
+int owgs_register_templates(owgs_ctx* c, int32_t n, const char* a_bytes, const int64_t* a_off, const char* b_bytes,
+                            const int64_t* b_off, int32_t* out_first_id) {
+    if (!c || n < 0 || (n > 0 && (!a_bytes || !a_off || !b_bytes || !b_off))) return OWGS_EINVAL;
+    for (int32_t i = 0; i < n; ++i)
+        if (a_off[i + 1] < a_off[i] || b_off[i + 1] < b_off[i] || a_off[0] < 0 || b_off[0] < 0)
+            return c->fail(OWGS_EINVAL, "template offsets must be non-decreasing");
+    if ((int64_t)c->ta_off.size() - 1 + n > INT32_MAX) return c->fail(OWGS_ERANGE, "too many templates");
+    if (out_first_id) *out_first_id = (int32_t)c->ta_off.size() - 1;
+    for (int32_t i = 0; i < n; ++i) {
+        c->ta.insert(c->ta.end(), a_bytes + a_off[i], a_bytes + a_off[i + 1]);
+        c->ta_off.push_back((int64_t)c->ta.size());
+        c->tb.insert(c->tb.end(), b_bytes + b_off[i], b_bytes + b_off[i + 1]);
+        c->tb_off.push_back((int64_t)c->tb.size());
+    }
+    c->tmpl_dirty = true;
+    return OWGS_OK;
+}
+
+int owgs_set_root_controller(owgs_ctx* c, const char* json, int32_t len) {
+    if (!c || len < 0 || (len > 0 && !json)) return OWGS_EINVAL;
+    c->rci.assign(json, json + len);
+    c->tmpl_dirty = true;
+    return OWGS_OK;
+}
+
+static int msg_templates_upload(owgs_ctx* c, hipStream_t st) {
+    if (!c->tmpl_dirty) return OWGS_OK;
+    HIPCHK(c, upload(c->m_ta, c->ta.data(), c->ta.size(), st));
+    HIPCHK(c, upload(c->m_tb, c->tb.data(), c->tb.size(), st));
+    HIPCHK(c, upload(c->m_ta_off, c->ta_off.data(), c->ta_off.size(), st));
+    HIPCHK(c, upload(c->m_tb_off, c->tb_off.data(), c->tb_off.size(), st));
+    HIPCHK(c, upload(c->m_rci, c->rci.data(), c->rci.size(), st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    c->tmpl_dirty = false;
+    return OWGS_OK;
+}
+
+// plan + write with device pointers; host-visible *total / *m
+static int msg_run(owgs_ctx* c, OwgsMsgArgs& A, int32_t n_topics, hipStream_t st, int64_t* total, int32_t* m) {
+    int rc = msg_templates_upload(c, st);
+    if (rc) return rc;
+    const int32_t n = A.n;
+    A.ta = c->m_ta.p;
+    A.ta_off = c->m_ta_off.p;
+    A.tb = c->m_tb.p;
+    A.tb_off = c->m_tb_off.p;
+    A.n_templates = (int32_t)c->ta_off.size() - 1;
+    A.rci = c->m_rci.p;
+    A.rci_len = (int32_t)c->rci.size();
+    A.n_topics = n_topics;
+    int32_t bits = 1;
+    while (bits < 31 && ((int64_t)n_topics >> bits) != 0) ++bits;
+    HIPCHK(c, c->m_key.reserve((size_t)n));
+    HIPCHK(c, c->m_key_sorted.reserve((size_t)n));
+    HIPCHK(c, c->m_len.reserve((size_t)n));
+    HIPCHK(c, c->m_len_sorted.reserve((size_t)n + 1));
+    HIPCHK(c, c->m_iota.reserve((size_t)n));
+    HIPCHK(c, c->m_cnt.reserve((size_t)n_topics + 1));
+    HIPCHK(c, c->m_bad.reserve(1));
+    const size_t tb = owgs_msg_scratch_bytes(n, n_topics, bits);
+    HIPCHK(c, c->m_temp.reserve(tb));
+    A.key = c->m_key.p;
+    A.len = c->m_len.p;
+    A.bad = c->m_bad.p;
+    HIPCHK(c, hipMemsetAsync(c->m_bad.p, 0, 4, st));
+    HIPCHK(c, owgs_launch_msg_plan(&A, bits, c->m_temp.p, tb, c->m_key_sorted.p, c->m_iota.p, c->m_len_sorted.p,
+                                   c->m_cnt.p, st));
+    HIPCHK(c, owgs_launch_msg_write(&A, st));
+    int32_t bad = 0, mm = 0;
+    int64_t tot = 0;
+    HIPCHK(c, hipMemcpyAsync(&bad, c->m_bad.p, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(&mm, A.topic_start + n_topics, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(&tot, A.out_off + n, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    if (total) *total = tot;
+    if (m) *m = mm;
+    if (bad & 1) return c->fail(OWGS_EINVAL, "serialize: invoker >= n_topics or unknown template");
+    if (bad & 2) return c->fail(OWGS_EINVAL, "serialize: transaction id is not valid UTF-8");
+    if (bad & 4) return c->fail(OWGS_ERANGE, "serialize: output capacity below the batch's bytes (see *total)");
+    return OWGS_OK;
+}
+
+static bool msg_batch_ok(const owgs_msg_batch* b, int32_t n_topics) {
+    if (!b || b->n < 0 || n_topics < 0 || n_topics >= INT32_MAX) return false;
+    if (b->n == 0) return true;
+    return b->invoker && b->tmpl && b->aid && b->tid_off && b->tid_start && b->flags;
+}
+
+int owgs_serialize_activations(owgs_ctx* c, const owgs_msg_batch* b, int32_t n_topics, char* out, int64_t cap,
+                               int64_t* out_off, int32_t* out_order, int32_t* topic_start, int64_t* total,
+                               int32_t* m) {
+    if (!c || !msg_batch_ok(b, n_topics) || cap < 0 || !out_off || !topic_start || (b->n > 0 && !out_order) ||
+        (cap > 0 && !out))
+        return OWGS_EINVAL;
+    const int32_t n = b->n;
+    bool need_c = false, need_r = false, need_x = false;
+    for (int32_t i = 0; i < n; ++i) {
+        need_c |= (b->flags[i] & OWGS_MSG_HAS_CONTENT) != 0;
+        need_x |= (b->flags[i] & OWGS_MSG_HAS_CAUSE) != 0;
+        need_r |= (b->flags[i] & OWGS_MSG_HAS_TRACE) != 0;
+    }
+    if ((need_c && (!b->content || !b->content_off)) || (need_x && !b->cause) || (need_r && (!b->trace || !b->trace_off)))
+        return c->fail(OWGS_EINVAL, "serialize: a flag asks for content / cause / traceContext that is missing");
+    for (int32_t i = 0; i < n; ++i)
+        if (b->tid_off[i + 1] < b->tid_off[i] || (need_c && b->content_off[i + 1] < b->content_off[i]) ||
+            (need_r && b->trace_off[i + 1] < b->trace_off[i]))
+            return c->fail(OWGS_EINVAL, "serialize: offsets must be non-decreasing");
+    (void)hipSetDevice(c->cfg.device);
+    hipStream_t st = c->stream;
+    const int64_t tid0 = n ? b->tid_off[0] : 0, tidn = n ? b->tid_off[n] : 0;
+    HIPCHK(c, upload(c->m_inv, b->invoker, (size_t)n, st));
+    HIPCHK(c, upload(c->m_tmpl, b->tmpl, (size_t)n, st));
+    HIPCHK(c, upload(c->m_aid, (const ulonglong2*)b->aid, (size_t)n, st));
+    HIPCHK(c, upload(c->m_tid, b->tid + tid0, (size_t)(tidn - tid0), st));
+    std::vector<int64_t> off((size_t)n + 1);
+    for (int32_t i = 0; i <= n; ++i) off[i] = n ? b->tid_off[i] - tid0 : 0;
+    HIPCHK(c, upload(c->m_tid_off, off.data(), off.size(), st));
+    HIPCHK(c, upload(c->m_tid_start, b->tid_start, (size_t)n, st));
+    HIPCHK(c, upload(c->m_flags, b->flags, (size_t)n, st));
+    std::vector<int64_t> coff((size_t)n + 1, 0), roff((size_t)n + 1, 0);
+    if (need_c) {
+        for (int32_t i = 0; i <= n; ++i) coff[i] = b->content_off[i] - b->content_off[0];
+        HIPCHK(c, upload(c->m_content, b->content + b->content_off[0], (size_t)coff[n], st));
+    }
+    if (need_r) {
+        for (int32_t i = 0; i <= n; ++i) roff[i] = b->trace_off[i] - b->trace_off[0];
+        HIPCHK(c, upload(c->m_trace, b->trace + b->trace_off[0], (size_t)roff[n], st));
+    }
+    HIPCHK(c, upload(c->m_content_off, coff.data(), coff.size(), st));
+    HIPCHK(c, upload(c->m_trace_off, roff.data(), roff.size(), st));
+    if (need_x) HIPCHK(c, upload(c->m_cause, (const ulonglong2*)b->cause, (size_t)n, st));
+    else HIPCHK(c, c->m_cause.reserve(1));
+    HIPCHK(c, c->m_content.reserve(1));
+    HIPCHK(c, c->m_trace.reserve(1));
+    HIPCHK(c, c->m_order.reserve((size_t)n));
+    HIPCHK(c, c->m_out_off.reserve((size_t)n + 1));
+    HIPCHK(c, c->m_topic.reserve((size_t)n_topics + 1));
+    HIPCHK(c, c->m_out.reserve((size_t)std::max<int64_t>(cap, 1)));
+    OwgsMsgArgs A{};
+    A.n = n;
+    A.invoker = c->m_inv.p;
+    A.tmpl = c->m_tmpl.p;
+    A.aid = c->m_aid.p;
+    A.tid = c->m_tid.p;
+    A.tid_off = c->m_tid_off.p;
+    A.tid_start = c->m_tid_start.p;
+    A.flags = c->m_flags.p;
+    A.content = c->m_content.p;
+    A.content_off = c->m_content_off.p;
+    A.cause = c->m_cause.p;
+    A.trace = c->m_trace.p;
+    A.trace_off = c->m_trace_off.p;
+    A.order = c->m_order.p;
+    A.out_off = c->m_out_off.p;
+    A.topic_start = c->m_topic.p;
+    A.out = c->m_out.p;
+    A.cap = cap;
+    int64_t tot = 0;
+    int32_t mm = 0;
+    int rc = msg_run(c, A, n_topics, st, &tot, &mm);
+    if (total) *total = tot;
+    if (m) *m = mm;
+    if (rc) return rc;
+    if (tot) HIPCHK(c, hipMemcpyAsync(out, c->m_out.p, (size_t)tot, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(out_off, c->m_out_off.p, (size_t)(mm + 1) * 8, hipMemcpyDeviceToHost, st));
+    if (mm) HIPCHK(c, hipMemcpyAsync(out_order, c->m_order.p, (size_t)mm * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(topic_start, c->m_topic.p, (size_t)(n_topics + 1) * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    return OWGS_OK;
+}
+
+int owgs_serialize_activations_device(owgs_ctx* c, const owgs_msg_batch* b, int32_t n_topics, char* out,
+                                      int64_t cap, int64_t* out_off, int32_t* out_order, int32_t* topic_start,
+                                      int64_t* total, int32_t* m, void* stream) {
+    if (!c || !msg_batch_ok(b, n_topics) || cap < 0 || !out_off || !topic_start || (b->n > 0 && !out_order) ||
+        (cap > 0 && !out) || (b->n > 0 && (!b->content_off || !b->trace_off)))
+        return OWGS_EINVAL;
+    (void)hipSetDevice(c->cfg.device);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(c, c->m_content.reserve(1));
+    HIPCHK(c, c->m_trace.reserve(1));
+    HIPCHK(c, c->m_cause.reserve(1));
+    OwgsMsgArgs A{};
+    A.n = b->n;
+    A.invoker = b->invoker;
+    A.tmpl = b->tmpl;
+    A.aid = (const ulonglong2*)b->aid;
+    A.tid = b->tid;
+    A.tid_off = b->tid_off;
+    A.tid_start = b->tid_start;
+    A.flags = b->flags;
+    A.content = b->content ? b->content : c->m_content.p;
+    A.content_off = b->content_off;
+    A.cause = b->cause ? (const ulonglong2*)b->cause : c->m_cause.p;
+    A.trace = b->trace ? b->trace : c->m_trace.p;
+    A.trace_off = b->trace_off;
+    A.order = out_order;
+    A.out_off = out_off;
+    A.topic_start = topic_start;
+    A.out = out;
+    A.cap = cap;
+    return msg_run(c, A, n_topics, st, total, m);
 }

@@ -277,3 +277,37 @@ struct OwgsAckCompleteArgs {
     int32_t* out_ticket;
     unsigned long long* counters;               // [0] entries inserted, [1] entries removed
 };
+
+// ActivationMessage serialisation + topic fan-out (owgs_msgs.hip); every pointer is device memory
+struct OwgsMsgArgs {
+    int32_t n;
+    const int32_t* invoker;
+    const int32_t* tmpl;
+    const char* ta;
+    const int64_t* ta_off;
+    const char* tb;
+    const int64_t* tb_off;
+    int32_t n_templates;
+    const char* rci;
+    int32_t rci_len;
+    const ulonglong2* aid;
+    const char* tid;
+    const int64_t* tid_off;
+    const int64_t* tid_start;
+    const uint8_t* flags;
+    const char* content;
+    const int64_t* content_off;
+    const ulonglong2* cause;
+    const char* trace;
+    const int64_t* trace_off;
+    int32_t n_topics;
+    // scratch and outputs
+    uint32_t* key;
+    int64_t* len;
+    int32_t* bad;          // bit0 invoker/template out of range, bit1 malformed UTF-8 transaction id, bit2 overflow
+    int32_t* order;        // [n] activation index of each output message (first m valid)
+    int64_t* out_off;      // [n + 1] byte offsets (out_off[m] = out_off[n] = total)
+    int32_t* topic_start;  // [n_topics + 1]
+    char* out;
+    int64_t cap;
+};

@@ -477,3 +477,61 @@ class HealthPool:
         tick = np.zeros(max(n, 1), np.int64)
         self._L.owh_read(self.h, _ptr(st), _ptr(mem), _ptr(te), _ptr(ring), _ptr(tick))
         return st[:n], mem[:n], te[:n], ring[:n], tick[:n]
+
+
+# ------------------------------------------------------------------------------ ActivationMessage serialisation
+# (owmsg_oracle.c: ActivationMessage.serialize + sendActivationToInvoker fan-out, Message.scala:51-70, CLB:175-198)
+MSG_BLOCKING, MSG_EXTRA_LOGGING, MSG_HAS_CONTENT, MSG_HAS_CAUSE, MSG_HAS_TRACE = 1, 2, 4, 8, 16
+
+
+class _owm_batch(C.Structure):
+    _fields_ = [("n", C.c_int32), ("invoker", C.c_void_p), ("tmpl", C.c_void_p), ("ta", C.c_void_p),
+                ("ta_off", C.c_void_p), ("tb", C.c_void_p), ("tb_off", C.c_void_p), ("n_templates", C.c_int32),
+                ("rci", C.c_void_p), ("rci_len", C.c_int32), ("aid", C.c_void_p), ("tid", C.c_void_p),
+                ("tid_off", C.c_void_p), ("tid_start", C.c_void_p), ("flags", C.c_void_p), ("content", C.c_void_p),
+                ("content_off", C.c_void_p), ("cause", C.c_void_p), ("trace", C.c_void_p), ("trace_off", C.c_void_p),
+                ("n_topics", C.c_int32)]
+
+
+def _blob(items):
+    enc = [x.encode("utf-8") if isinstance(x, str) else bytes(x) for x in items]
+    off = np.zeros(len(enc) + 1, dtype=np.int64)
+    off[1:] = np.cumsum([len(b) for b in enc])
+    return np.frombuffer(b"".join(enc) + b"\0", dtype=np.uint8), off
+
+
+def serialize_activations(part_a, part_b, rci, invoker, tmpl, aid_words, tids, tid_start, flags, contents=None,
+                          causes=None, traces=None, n_topics=None):
+    """(bytes, out_off, out_order, topic_start) -- the CPU restatement (owm_serialize)."""
+    L = lib()
+    L.owm_serialize.restype = C.c_int64
+    L.owm_serialize.argtypes = [C.c_void_p] * 7
+    n = len(invoker)
+    inv = np.ascontiguousarray(invoker, dtype=np.int32)
+    tm = np.ascontiguousarray(tmpl, dtype=np.int32)
+    ta, tao = _blob(part_a)
+    tb, tbo = _blob(part_b)
+    rc = rci.encode()
+    aid = np.ascontiguousarray(aid_words, dtype=np.uint64).reshape(-1)
+    tid, tido = _blob(tids)
+    ts = np.ascontiguousarray(tid_start, dtype=np.int64)
+    fl = np.ascontiguousarray(flags, dtype=np.uint8)
+    cb, co = _blob(contents if contents is not None else [""] * n)
+    cz = np.ascontiguousarray(causes if causes is not None else np.zeros((n, 2)), dtype=np.uint64).reshape(-1)
+    rb, ro = _blob(traces if traces is not None else [""] * n)
+    nt = int(n_topics if n_topics is not None else (inv.max() + 1 if n and inv.max() >= 0 else 0))
+    rcb = np.frombuffer(rc + b"\0", dtype=np.uint8)
+    B = _owm_batch(n, _ptr(inv), _ptr(tm), _ptr(ta), _ptr(tao), _ptr(tb), _ptr(tbo), len(part_a), _ptr(rcb), len(rc),
+                   _ptr(aid), _ptr(tid), _ptr(tido), _ptr(ts), _ptr(fl), _ptr(cb), _ptr(co), _ptr(cz), _ptr(rb),
+                   _ptr(ro), nt)
+    off = np.zeros(n + 1, np.int64)
+    order = np.zeros(max(n, 1), np.int32)
+    topic = np.zeros(nt + 1, np.int32)
+    total = C.c_int64(0)
+    m = L.owm_serialize(C.byref(B), None, 0, _ptr(off), _ptr(order), _ptr(topic), C.byref(total))
+    if m == -1:
+        raise ValueError("owm_serialize: bad argument")
+    out = C.create_string_buffer(max(total.value, 1))
+    m = L.owm_serialize(C.byref(B), out, total.value, _ptr(off), _ptr(order), _ptr(topic), C.byref(total))
+    assert m >= 0
+    return out.raw[:total.value], off[:m + 1], order[:m], topic

@@ -7,4 +7,4 @@ mkdir -p variants build/variants
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $2"
 /opt/rocm/bin/hipcc $F -c -o build/variants/k_$1.o csrc/owgs_kernels.hip
 /opt/rocm/bin/hipcc $F -x hip -c -o build/variants/h_$1.o csrc/owgs_host.cpp
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o variants/libowgs_$1.so build/variants/k_$1.o build/owgs_state.o build/owgs_acks.o build/owgs_health.o build/variants/h_$1.o
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o variants/libowgs_$1.so build/variants/k_$1.o build/owgs_state.o build/owgs_acks.o build/owgs_health.o build/owgs_msgs.o build/variants/h_$1.o
