@@ -23,6 +23,12 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# HBM bytes of one owgs_engine_kernel launch on the headline config (1M activations), from separate rocprofv3 --pmc
+# passes over `bench.py --steps 5` (tools/pmc_run.sh; summary committed as profiles/r01_v8_pmc.txt): FETCH_SIZE
+# 12,920 KiB doubled for gfx950's half-counted 16 B/lane streaming reads (the engine reads by LDS-DMA dwordx4) +
+# WRITE_SIZE 26,210 KiB.  Counters cannot be read live inside the timed run, so this is the profiled value of the
+# same engine build; other configs report null.
+ENGINE_PMC_TRAFFIC = {"bytes": (2 * 12920 + 26210) * 1024, "source": "profiles/r01_v8_pmc.txt (FETCH_SIZE x2 + WRITE_SIZE)"}
 
 
 def parse():
@@ -193,6 +199,9 @@ def main():
     value = cluster.whole_job_rate(n_dec, world, t_step)
     algo = algorithmic_bytes(w)
     achieved = algo / (kern_ms * 1e-3) / 1e9
+    headline = args.config == "headline" and args.n_activations == 1_000_000
+    traffic = ENGINE_PMC_TRAFFIC["bytes"] if headline else None
+    traffic_src = ENGINE_PMC_TRAFFIC["source"] if headline else None
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -215,7 +224,7 @@ def main():
                        "batches": s.n_batches, "batch": w.info["batch"], "releases": int(len(s.rel_aid)),
                        "cluster_size": w.cluster_size, "parallelism": f"{world} controller shard(s), 1 per GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "owgs_engine_kernel", "kernel_ms": kern_ms, "algorithmic_bytes": algo},
             "engine_stats": stats,
             "cpu_baseline": cpu,

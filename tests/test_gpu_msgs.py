@@ -47,7 +47,9 @@ def random_batch(rng, n, n_topics, n_templates):
     start = rng.integers(-10 ** 15, 10 ** 15, size=n)
     start[: n // 2] = rng.integers(1_600_000_000_000, 1_800_000_000_000, size=n // 2)
     flags = rng.integers(0, 32, size=n).astype(np.uint8)
-    contents = ['{"p":"' + "x" * int(rng.integers(0, 3000)) + '"}' for _ in range(n)]
+    # most messages fit the writer's 4 KB LDS staging buffer; some do not (direct path)
+    contents = ['{"p":"' + "x" * int(rng.integers(0, 3000) if rng.random() > 0.05 else rng.integers(4000, 9000))
+                + '"}' for _ in range(n)]
     causes = rng.integers(0, 2 ** 63, size=(n, 2), dtype=np.int64).astype(np.uint64)
     traces = ['{"t":"%d"}' % k for k in range(n)]
     return dict(invoker=inv, tmpl=tmpl, aid_words=aid, tids=tids, tid_start=start, flags=flags, contents=contents,
