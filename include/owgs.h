@@ -211,6 +211,7 @@ int owgs_activations_live(owgs_ctx* ctx, int64_t* live);
  * user_memory_bytes = the pinging InvokerInstanceId's userMemory (ignored for other kinds).  apply != 0 hands the
  * resulting status vector to owgs_update_invokers (the monitor's CurrentInvokerPoolState -> updateInvokers,
  * SCPB:226-227).  Bad kinds, negative ids or times out of order: OWGS_EINVAL with no state change. */
+#define OWGS_HEALTH_MAX_ID (1 << 24) /* invoker ids accepted by owgs_health_events (the status vector is dense) */
 #define OWGS_EV_PING 0          /* PingMessage (InvokerSupervision.scala:120-131) */
 #define OWGS_EV_SUCCESS 1       /* InvocationFinishedMessage(InvocationFinishedResult.Success) */
 #define OWGS_EV_SYSTEM_ERROR 2  /* ... SystemError */
@@ -265,7 +266,9 @@ int owgs_serialize_activations(owgs_ctx* ctx, const owgs_msg_batch* batch, int32
                                int64_t* out_off, int32_t* out_order, int32_t* topic_start, int64_t* total,
                                int32_t* m);
 /* Same with every pointer of batch and the outputs in device memory (e.g. invoker = owgs_replay_device's out_invoker),
- * on `stream`; *total and *m are host values (the call synchronises once). */
+ * on `stream`; content_off and trace_off are required (n + 1 zeros when unused); no host-side argument check beyond
+ * NULLs (the device flags bad templates / invokers / UTF-8 as above); *total and *m are host values (the call
+ * synchronises once). */
 int owgs_serialize_activations_device(owgs_ctx* ctx, const owgs_msg_batch* batch, int32_t n_topics, char* out,
                                       int64_t cap, int64_t* out_off, int32_t* out_order, int32_t* topic_start,
                                       int64_t* total, int32_t* m, void* stream);

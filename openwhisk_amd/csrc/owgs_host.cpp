@@ -1375,9 +1375,10 @@ int owgs_health_events(owgs_ctx* c, int32_t n, const int32_t* invoker, const uin
     int64_t prev = c->h_now;
     int32_t max_id = -1, max_ping = -1;
     for (int32_t e = 0; e < n; ++e) {
-        if (kind[e] > OWGS_EV_STATE_TIMEOUT || invoker[e] < 0 || t_ms[e] < prev || t_ms[e] >= (1LL << 60))
-            return c->fail(OWGS_EINVAL, "health event: kind > 4, negative invoker, time before the previous one or "
-                                        "outside [0, 2^60)");
+        if (kind[e] > OWGS_EV_STATE_TIMEOUT || invoker[e] < 0 || invoker[e] >= OWGS_HEALTH_MAX_ID || t_ms[e] < prev ||
+            t_ms[e] >= (1LL << 60))
+            return c->fail(OWGS_EINVAL, "health event: kind > 4, invoker outside [0, 2^24), time before the previous "
+                                        "one or outside [0, 2^60)");
         prev = t_ms[e];
         max_id = std::max(max_id, invoker[e]);
         if (kind[e] == OWGS_EV_PING) max_ping = std::max(max_ping, invoker[e]);
@@ -1560,6 +1561,8 @@ int owgs_serialize_activations(owgs_ctx* c, const owgs_msg_batch* b, int32_t n_t
         (cap > 0 && !out))
         return OWGS_EINVAL;
     const int32_t n = b->n;
+    if (n > 0 && b->tid_off[n] > b->tid_off[0] && !b->tid)
+        return c->fail(OWGS_EINVAL, "serialize: transaction id bytes missing");
     bool need_c = false, need_r = false, need_x = false;
     for (int32_t i = 0; i < n; ++i) {
         need_c |= (b->flags[i] & OWGS_MSG_HAS_CONTENT) != 0;

@@ -92,7 +92,7 @@ def test_gpu_health_rejects_bad_batches_without_state_change():
     g.events([3], [0], [100], [MB], 100)
     before = g.read()
     for args in (([0], [0], [99], [MB], 200), ([0, 1], [0, 0], [300, 200], [MB, MB], 400), ([0], [9], [200], [MB], 300),
-                 ([-1], [0], [200], [MB], 300), ([0], [0], [200], [MB], 150)):
+                 ([-1], [0], [200], [MB], 300), ([0], [0], [200], [MB], 150), ([1 << 24], [0], [200], [MB], 300)):
         with pytest.raises(OwgsError):
             g.events(*args)
         compare(g.read(), before)
