@@ -59,11 +59,30 @@ __device__ __forceinline__ int utf8_at(const uint8_t* s, int64_t i, int64_t n, i
 // printed length of a code point (one or two UTF-16 units)
 __device__ __forceinline__ int cp_len(int cp) { return cp >= 0x10000 ? 12 : unit_len((unsigned)cp); }
 
+__constant__ unsigned long long POW10[20] = {1ull, 10ull, 100ull, 1000ull, 10000ull, 100000ull, 1000000ull,
+    10000000ull, 100000000ull, 1000000000ull, 10000000000ull, 100000000000ull, 1000000000000ull, 10000000000000ull,
+    100000000000000ull, 1000000000000000ull, 10000000000000000ull, 100000000000000000ull, 1000000000000000000ull,
+    10000000000000000000ull};
+
+__device__ __forceinline__ uint64_t magnitude(int64_t v) { return v < 0 ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v; }
+
+// decimal digits of |v| (+1 for the sign): t = floor(bit length * log10(2)) is the digit count or one less
 __device__ __forceinline__ int digits(int64_t v) {
-    uint64_t u = v < 0 ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
-    int d = 1;
-    while (u >= 10) { u /= 10; ++d; }
-    return d + (v < 0);
+    const uint64_t u = magnitude(v);
+    const int t = ((64 - __clzll(u | 1)) * 1233) >> 12;
+    return max(t + (u >= POW10[t] ? 1 : 0), 1) + (v < 0);
+}
+
+// decimal digit of u at power r (0 = units): u split into three base-1e9 limbs by two constant divisions, then one
+// 32-bit division
+__device__ __forceinline__ int digit_at(uint64_t u, int r) {
+    const uint64_t q = u / 1000000000ull;
+    const uint32_t lo = (uint32_t)(u - q * 1000000000ull);
+    const uint64_t q2 = q / 1000000000ull;
+    const uint32_t mid = (uint32_t)(q - q2 * 1000000000ull), top = (uint32_t)q2;
+    const uint32_t x = r < 9 ? lo : r < 18 ? mid : top;
+    const uint32_t p = (uint32_t)POW10[r < 9 ? r : r < 18 ? r - 9 : r - 18];
+    return (int)((x / p) % 10u);
 }
 
 #define LIT(s) (int64_t)(sizeof(s) - 1)
@@ -134,7 +153,8 @@ __global__ __launch_bounds__(256) void owgs_msg_gather_kernel(const int32_t* ord
 
 // wave-cooperative copy of len bytes
 __device__ __forceinline__ void wcopy(char* dst, const char* src, int64_t len, int lane) {
-    for (int64_t j = lane; j < len; j += 64) dst[j] = src[j];
+    const int n = (int)len;  // a piece of one message: < 2^31 bytes
+    for (int j = lane; j < n; j += 64) dst[j] = src[j];
 }
 __device__ __forceinline__ void wlit(char* dst, const char* lit, int len, int lane) {
     if (lane < len) dst[lane] = lit[lane];
@@ -228,15 +248,9 @@ __global__ __launch_bounds__(256) void owgs_msg_write_kernel(OwgsMsgArgs A) {
     {
         const int64_t v = A.tid_start[i];
         const int nd = digits(v);
-        uint64_t u = v < 0 ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
-        if (lane < nd) {
-            // lane k writes digit k from the left
-            const int from_right = nd - 1 - lane;
+        if (lane < nd) {  // lane k writes character k from the left
             if (v < 0 && lane == 0) d[o] = '-';
-            else {
-                for (int r = 0; r < from_right; ++r) u /= 10;
-                d[o + lane] = (char)('0' + u % 10);
-            }
+            else d[o + lane] = (char)('0' + digit_at(magnitude(v), nd - 1 - lane));
         }
         o += nd;
     }
