@@ -273,6 +273,10 @@ int owgs_serialize_activations_device(owgs_ctx* ctx, const owgs_msg_batch* batch
                                       int64_t cap, int64_t* out_off, int32_t* out_order, int32_t* topic_start,
                                       int64_t* total, int32_t* m, void* stream);
 
+/* Duration of the last owgs_engine_kernel launch (HIP events recorded on its stream right before and after it);
+ * waits for it to finish.  Measurement hook for bench.py's roofline. */
+int owgs_engine_ms(owgs_ctx* ctx, float* ms);
+
 /* Restore the slot state captured by owgs_snapshot (bench: every timed step starts from the same state). */
 int owgs_snapshot(owgs_ctx* ctx);
 int owgs_restore(owgs_ctx* ctx, void* stream);

@@ -218,6 +218,12 @@ class GpuShardingContainerPoolBalancer:
         mm = m.value
         return out.raw[:total.value], off[:mm + 1], order[:mm], topic
 
+    def engine_ms(self) -> float:
+        """Duration of the last engine kernel launch (HIP events on its stream)."""
+        v = C.c_float(0)
+        self._chk(self._L.owgs_engine_ms(self._h, C.byref(v)))
+        return float(v.value)
+
     def set_health_tid(self, start_ms: int):
         """TransactionId.invokerHealth's start time (TransactionId.scala:225): health acks echo it."""
         self._chk(self._L.owgs_set_health_tid(self._h, start_ms))

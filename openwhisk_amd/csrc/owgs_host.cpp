@@ -171,6 +171,8 @@ struct owgs_ctx {
     DevBuf<int64_t> h_last, h_tick, h_mem, he_t, he_mem, he_packed;
     DevBuf<int32_t> h_tests, he_inv, he_key, he_idx0, he_idx1, he_beg, he_end, he_reg, he_pad;
     int32_t h_cap = 0, h_size = 0;
+    hipEvent_t ev_engine[2] = {nullptr, nullptr};  // around the last owgs_engine_kernel launch
+    bool ev_engine_valid = false;
     // ActivationMessage templates + serialisation scratch (owgs_msgs.hip)
     std::vector<char> ta, tb;
     std::vector<int64_t> ta_off{0}, tb_off{0};
@@ -401,7 +403,14 @@ static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s) {
     A.cur_tag0 = c->cur_tag;
     c->cur_tag += A.n_batches;
     HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, 16 * sizeof(u64), s));
+    if (!c->ev_engine[0]) {
+        HIPCHK(c, hipEventCreate(&c->ev_engine[0]));
+        HIPCHK(c, hipEventCreate(&c->ev_engine[1]));
+    }
+    HIPCHK(c, hipEventRecord(c->ev_engine[0], s));  // brackets exactly the engine launch (owgs_engine_ms)
     HIPCHK(c, owgs_launch_engine(&A, s));
+    HIPCHK(c, hipEventRecord(c->ev_engine[1], s));
+    c->ev_engine_valid = true;
     if (A.trace) {  // diagnostic timeline: raw u64 pairs, [waves][16384][2]
         HIPCHK(c, hipStreamSynchronize(s));
         std::vector<unsigned long long> h(c->d_trace.n);
@@ -560,6 +569,8 @@ void owgs_destroy(owgs_ctx* c) {
     DevBuf<int32_t>* h32[] = {&c->h_tests, &c->he_inv, &c->he_key, &c->he_idx0, &c->he_idx1,
                               &c->he_beg,  &c->he_end, &c->he_reg, &c->he_pad};
     for (auto* b : h32) b->release();
+    if (c->ev_engine[0]) (void)hipEventDestroy(c->ev_engine[0]);
+    if (c->ev_engine[1]) (void)hipEventDestroy(c->ev_engine[1]);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1670,4 +1681,13 @@ int owgs_serialize_activations_device(owgs_ctx* c, const owgs_msg_batch* b, int3
     A.out = out;
     A.cap = cap;
     return msg_run(c, A, n_topics, st, total, m);
+}
+
+int owgs_engine_ms(owgs_ctx* c, float* ms) {
+    if (!c || !ms) return OWGS_EINVAL;
+    if (!c->ev_engine_valid) return c->fail(OWGS_ENOENT, "no engine launch yet");
+    (void)hipSetDevice(c->cfg.device);
+    HIPCHK(c, hipEventSynchronize(c->ev_engine[1]));
+    HIPCHK(c, hipEventElapsedTime(ms, c->ev_engine[0], c->ev_engine[1]));
+    return OWGS_OK;
 }
