@@ -578,8 +578,29 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
     // speculation path, and the class-1 lanes sit between the two walking classes.
     const int cls = (hs != OWGS_REC_NOHOT || (meta.y & (OWGS_AM_THROW | OWGS_AM_EMPTY))) ? 1 : (mc > 1 ? 2 : 0);
     s_p[t] = t < len ? cls : 3;
+    // class masks (one ballot per wave and class): thread 0's dealing below walks set bits in registers instead of
+    // re-reading every lane's class from LDS in each of its loops
+    __shared__ unsigned long long s_m[3][(OWGS_WL + 63) / 64];
+    {
+        const unsigned long long m0 = __ballot(t < len && cls == 0), m1 = __ballot(t < len && cls == 1),
+                                 m2 = __ballot(t < len && cls == 2);
+        if ((t & 63) == 0) {
+            s_m[0][t >> 6] = m0;
+            s_m[1][t >> 6] = m1;
+            s_m[2][t >> 6] = m2;
+        }
+    }
     __syncthreads();
     if (t == 0) {
+        constexpr int NWR = (OWGS_WL + 63) / 64;
+        unsigned long long mk[3][NWR];
+        for (int c = 0; c < 3; ++c)
+            for (int r = 0; r < NWR; ++r) mk[c][r] = s_m[c][r];
+        // f(j) for every lane j of class c, in stream order
+        auto each = [&](int c, auto&& f) {
+            for (int r = 0; r < NWR; ++r)
+                for (unsigned long long m = mk[c][r]; m; m &= m - 1) f(r * 64 + __builtin_ctzll(m));
+        };
         // the maxConcurrent == 1 walkers fill the first waves; the concurrent lanes are spread round-robin over the
         // remaining waves and the lanes without a walk fill the gaps (from the last wave down), so the waves that
         // run the concurrent path hold fewer of them (a wave takes as long as its slowest lane).  Wave w holds
@@ -591,37 +612,35 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
             cap[w] = wave_cap(len, w);
             nwv += cap[w] > 0;
         }
-        for (int j = 0; j < len; ++j) n0 += s_p[j] == 0;
+        int n1 = 0, n2 = 0;
+        for (int r = 0; r < NWR; ++r) {
+            n0 += __popcll(mk[0][r]);
+            n1 += __popcll(mk[1][r]);
+            n2 += __popcll(mk[2][r]);
+        }
         // place the class-c lanes round-robin over waves [wlo, whi) (skipping full ones), spilling anywhere
         auto deal = [&](int c, int wlo, int whi) {
             int rr = 0;
             const int span = max(whi - wlo, 1);
-            for (int j = 0; j < len; ++j)
-                if (s_p[j] == c) {
-                    int w = -1;
-                    for (int k = 0; k < span && w < 0; ++k, ++rr) {
-                        const int cw_ = wlo + (rr % span);
-                        if (cw_ < nwv && cnt[cw_] < cap[cw_]) w = cw_;
-                    }
-                    for (int q = nwv - 1; q >= 0 && w < 0; --q)
-                        if (cnt[q] < cap[q]) w = q;
-                    s_s[j] = wave_off(len, w) + cnt[w]++;
+            each(c, [&](int j) {
+                int w = -1;
+                for (int k = 0; k < span && w < 0; ++k, ++rr) {
+                    const int cw_ = wlo + (rr % span);
+                    if (cw_ < nwv && cnt[cw_] < cap[cw_]) w = cw_;
                 }
+                for (int q = nwv - 1; q >= 0 && w < 0; --q)
+                    if (cnt[q] < cap[q]) w = q;
+                s_s[j] = wave_off(len, w) + cnt[w]++;
+            });
         };
         auto fill = [&](int c, bool from_back) {  // contiguous, first free slot
-            for (int j = 0; j < len; ++j)
-                if (s_p[j] == c) {
-                    int w = from_back ? nwv - 1 : 0;
-                    if (from_back) while (cnt[w] == cap[w]) --w;
-                    else while (cnt[w] == cap[w]) ++w;
-                    s_s[j] = wave_off(len, w) + cnt[w]++;
-                }
+            each(c, [&](int j) {
+                int w = from_back ? nwv - 1 : 0;
+                if (from_back) while (cnt[w] == cap[w]) --w;
+                else while (cnt[w] == cap[w]) ++w;
+                s_s[j] = wave_off(len, w) + cnt[w]++;
+            });
         };
-        int n1 = 0, n2 = 0;
-        for (int j = 0; j < len; ++j) {
-            n1 += s_p[j] == 1;
-            n2 += s_p[j] == 2;
-        }
         int f0 = 0, acc0 = 0;  // waves the maxConcurrent == 1 walkers fill
         while (f0 < nwv && acc0 < n0) acc0 += cap[f0++];
         // the host picks the strategy per replay (owgs_host.cpp, chunk_width): 1 for large pools, 2 for small ones
