@@ -178,6 +178,65 @@ JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00
     return rc == OWGS_OK ? n : rc;
 }
 
+/* ---- ActivationMessage serialisation + topic fan-out ---- */
+JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_registerTemplates(
+    JNIEnv* env, jobject self, jlong h, jbyteArray a, jlongArray aOff, jbyteArray b, jlongArray bOff, jint n) {
+    int32_t first = 0;
+    jbyte* pa = (*env)->GetPrimitiveArrayCritical(env, a, NULL);
+    jlong* pao = (*env)->GetPrimitiveArrayCritical(env, aOff, NULL);
+    jbyte* pb = (*env)->GetPrimitiveArrayCritical(env, b, NULL);
+    jlong* pbo = (*env)->GetPrimitiveArrayCritical(env, bOff, NULL);
+    const int rc = owgs_register_templates(CTX(h), n, (const char*)pa, (const int64_t*)pao, (const char*)pb,
+                                           (const int64_t*)pbo, &first);
+    (*env)->ReleasePrimitiveArrayCritical(env, bOff, pbo, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, b, pb, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, aOff, pao, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, a, pa, JNI_ABORT);
+    return rc == OWGS_OK ? first : rc;
+}
+
+/* returns the number of messages (>= 0) or an OWGS_E* code; out must hold the batch's bytes (size query: out = null) */
+JNIEXPORT jlong JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_serializeActivations(
+    JNIEnv* env, jobject self, jlong h, jintArray invoker, jintArray tmpl, jlongArray aid, jbyteArray tid,
+    jlongArray tidOff, jlongArray tidStart, jbyteArray flags, jbyteArray content, jlongArray contentOff, jint n,
+    jint nTopics, jbyteArray out, jlongArray outOff, jintArray outOrder, jintArray topicStart) {
+    owgs_msg_batch b;
+    memset(&b, 0, sizeof b);
+    b.n = n;
+    b.invoker = (*env)->GetPrimitiveArrayCritical(env, invoker, NULL);
+    b.tmpl = (*env)->GetPrimitiveArrayCritical(env, tmpl, NULL);
+    b.aid = (*env)->GetPrimitiveArrayCritical(env, aid, NULL);
+    b.tid = (*env)->GetPrimitiveArrayCritical(env, tid, NULL);
+    b.tid_off = (*env)->GetPrimitiveArrayCritical(env, tidOff, NULL);
+    b.tid_start = (*env)->GetPrimitiveArrayCritical(env, tidStart, NULL);
+    b.flags = (*env)->GetPrimitiveArrayCritical(env, flags, NULL);
+    b.content = content ? (*env)->GetPrimitiveArrayCritical(env, content, NULL) : NULL;
+    b.content_off = contentOff ? (*env)->GetPrimitiveArrayCritical(env, contentOff, NULL) : NULL;
+    const jsize cap = out ? (*env)->GetArrayLength(env, out) : 0;
+    jbyte* po = out ? (*env)->GetPrimitiveArrayCritical(env, out, NULL) : NULL;
+    jlong* poff = (*env)->GetPrimitiveArrayCritical(env, outOff, NULL);
+    jint* pord = (*env)->GetPrimitiveArrayCritical(env, outOrder, NULL);
+    jint* pts = (*env)->GetPrimitiveArrayCritical(env, topicStart, NULL);
+    int64_t total = 0;
+    int32_t m = 0;
+    const int rc = owgs_serialize_activations(CTX(h), &b, nTopics, (char*)po, cap, (int64_t*)poff, (int32_t*)pord,
+                                              (int32_t*)pts, &total, &m);
+    (*env)->ReleasePrimitiveArrayCritical(env, topicStart, pts, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, outOrder, pord, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, outOff, poff, 0);
+    if (po) (*env)->ReleasePrimitiveArrayCritical(env, out, po, 0);
+    if (b.content_off) (*env)->ReleasePrimitiveArrayCritical(env, contentOff, (void*)b.content_off, JNI_ABORT);
+    if (b.content) (*env)->ReleasePrimitiveArrayCritical(env, content, (void*)b.content, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, flags, (void*)b.flags, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, tidStart, (void*)b.tid_start, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, tidOff, (void*)b.tid_off, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, tid, (void*)b.tid, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, aid, (void*)b.aid, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, tmpl, (void*)b.tmpl, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, invoker, (void*)b.invoker, JNI_ABORT);
+    return rc == OWGS_OK ? (jlong)m : (jlong)rc;
+}
+
 JNIEXPORT jstring JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_lastError(JNIEnv* env,
                                                                                                jobject self, jlong h) {
     return (*env)->NewStringUTF(env, owgs_last_error(CTX(h)));
