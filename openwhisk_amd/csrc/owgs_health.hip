@@ -217,30 +217,41 @@ __global__ __launch_bounds__(256) void owgs_health_fsm_kernel(HealthArgs A) {
         }
     }
     const int32_t e0 = A.seg_beg[k], e1 = A.seg_end[k];
-    for (int32_t p = e0; p < e1; ++p) {
-        const int64_t w = A.ev_packed[p];
-        const int kind = (int)(w & 7);
-        const int64_t t = w >> 3;
-        if (a.st < H_PADDED) fire_due(a, t);
-        if (kind == EV_PING) {
-            if (a.st >= H_PADDED) {  // registerInvoker: new actor, startWith(Unhealthy) + initialize() handlers
-                a.ring = 0;
-                a.st = H_UNHEALTHY;
-                a.tests++;
-                a.tick = t + TICK_MS;
-            }
-            mem = A.ev_mem[A.ev_idx[p]];
-            if (a.st == H_OFFLINE) go(a, H_UNHEALTHY, t);
-            else arm(a, t);
-        } else if (a.st < H_PADDED) {
-            if (kind == EV_STATE_TIMEOUT) {
-                if (has_timeout(a.st)) go(a, H_OFFLINE, t);
+    // the invoker's events in blocks of 8: the block's loads issue together, then the FSM steps through them (the
+    // userMemory of the status entry is the last ping's, read once at the end)
+    int32_t last_ping = -1;
+    for (int32_t p0 = e0; p0 < e1; p0 += 8) {
+        int64_t wv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) wv[u] = p0 + u < e1 ? A.ev_packed[p0 + u] : -1;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t w = wv[u];
+            if (w < 0) break;
+            const int kind = (int)(w & 7);
+            const int64_t t = w >> 3;
+            if (a.st < H_PADDED) fire_due(a, t);
+            if (kind == EV_PING) {
+                if (a.st >= H_PADDED) {  // registerInvoker: new actor, startWith(Unhealthy) + initialize() handlers
+                    a.ring = 0;
+                    a.st = H_UNHEALTHY;
+                    a.tests++;
+                    a.tick = t + TICK_MS;
+                }
+                last_ping = p0 + u;
+                if (a.st == H_OFFLINE) go(a, H_UNHEALTHY, t);
                 else arm(a, t);
-            } else {
-                completion(a, kind, t);
+            } else if (a.st < H_PADDED) {
+                if (kind == EV_STATE_TIMEOUT) {
+                    if (has_timeout(a.st)) go(a, H_OFFLINE, t);
+                    else arm(a, t);
+                } else {
+                    completion(a, kind, t);
+                }
             }
         }
     }
+    if (last_ping >= 0) mem = A.ev_mem[A.ev_idx[last_ping]];
     if (a.st < H_PADDED) fire_due(a, A.now);
     A.st[k] = (uint8_t)a.st;
     A.ring[k] = a.ring;
