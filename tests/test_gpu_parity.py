@@ -206,6 +206,17 @@ def test_headline_full_size_parity_and_determinism():
     assert np.array_equal(g1, g2) and np.array_equal(f1, f2)
 
 
+@pytest.mark.parametrize("name", ["c2", "c3", "c4"])
+def test_baseline_configs_full_size_parity(name):
+    # BASELINE.json configs[1..3] at their full sizes (1M activations each), bit-exact with the oracle
+    check_stream(W.config(name))
+
+
+def test_c5_shard_full_size_parity():
+    # configs[4]: one of 8 controller shards (clusterSize 8) with its full 1M-activation stream
+    check_stream(W.config("headline", shard=3, n_shards=8))
+
+
 def test_multi_shard_cluster_parity():
     # C5-style shards: clusterSize 8, each shard its own stream; shard state = 1/8 of every invoker
     for g in (0, 7):
