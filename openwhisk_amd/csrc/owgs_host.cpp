@@ -34,6 +34,7 @@ extern "C" hipError_t owgs_launch_relscan(const int64_t* rel_aid, int64_t n_rel,
 extern "C" hipError_t owgs_launch_relflags(const int64_t* rel_aid, int64_t n_rel, const int32_t* out_inv,
                                            uint8_t* rel_flags, hipStream_t s);
 extern "C" hipError_t owgs_launch_release_seq(const OwgsReleaseArgs* a, hipStream_t s);
+extern "C" size_t owgs_release_scratch_bytes(int32_t n);
 extern "C" hipError_t owgs_launch_engine(const OwgsEngineArgs* a, hipStream_t s);
 extern "C" int32_t owgs_coprime_max(void);
 extern "C" hipError_t owgs_launch_coprime(const int32_t* xs, int32_t n_pools, int32_t* out, int32_t out_stride,
@@ -172,6 +173,9 @@ struct owgs_ctx {
     DevBuf<int32_t> h_tests, he_inv, he_key, he_idx0, he_idx1, he_beg, he_end, he_reg, he_pad;
     int32_t h_cap = 0, h_size = 0;
     hipEvent_t ev_engine[2] = {nullptr, nullptr};  // around the last owgs_engine_kernel launch
+    DevBuf<unsigned long long> r_bound;  // release front end scratch (owgs_launch_release_seq)
+    DevBuf<int32_t> r_idx, r_cnt;
+    DevBuf<uint8_t> r_sel, r_temp;
     bool ev_engine_valid = false;
     // ActivationMessage templates + serialisation scratch (owgs_msgs.hip)
     std::vector<char> ta, tb;
@@ -560,6 +564,11 @@ void owgs_destroy(owgs_ctx* c) {
     c->m_cause.release();
     c->m_flags.release();
     c->m_temp.release();
+    c->r_bound.release();
+    c->r_idx.release();
+    c->r_cnt.release();
+    c->r_sel.release();
+    c->r_temp.release();
     c->h_st.release();
     c->he_kind.release();
     c->he_temp.release();
@@ -787,6 +796,24 @@ int owgs_publish_batch(owgs_ctx* c, int32_t n, const int32_t* action, const uint
     return check_err_word(c);
 }
 
+// scratch of the release front end for n releases
+static int release_scratch(owgs_ctx* c, OwgsReleaseArgs& R, int32_t n) {
+    HIPCHK(c, c->r_bound.reserve((size_t)std::max(c->n_slots, 1)));
+    HIPCHK(c, c->r_idx.reserve((size_t)std::max(n, 1)));
+    HIPCHK(c, c->r_sel.reserve((size_t)std::max(n, 1)));
+    HIPCHK(c, c->r_cnt.reserve(2));
+    const size_t tb = owgs_release_scratch_bytes(std::max(n, 1));
+    HIPCHK(c, c->r_temp.reserve(tb));
+    R.bound = c->r_bound.p;
+    R.risk = c->r_cnt.p + 1;
+    R.sel_flag = c->r_sel.p;
+    R.sel_idx = c->r_idx.p;
+    R.sel_cnt = c->r_cnt.p;
+    R.temp = c->r_temp.p;
+    R.temp_bytes = tb;
+    return OWGS_OK;
+}
+
 int owgs_release_batch(owgs_ctx* c, int32_t n, const int32_t* invoker, const int32_t* action, uint8_t* out_flags) {
     if (!c || n < 0 || (n > 0 && (!invoker || !action))) return OWGS_EINVAL;
     if (n == 0) return OWGS_OK;
@@ -815,6 +842,8 @@ int owgs_release_batch(owgs_ctx* c, int32_t n, const int32_t* invoker, const int
     R.slot = c->d_d.p;
     R.flags = c->d_rflags.p;
     R.err = c->d_err.p;
+    int rs = release_scratch(c, R, n);
+    if (rs) return rs;
     HIPCHK(c, owgs_launch_release_seq(&R, c->stream));
     if (out_flags)
         HIPCHK(c, hipMemcpyAsync(out_flags, c->d_rflags.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
@@ -1265,6 +1294,8 @@ static int ack_complete(owgs_ctx* c, int32_t n, uint8_t* d_kind, int32_t* d_tick
     R.slot = c->k_r3.p;
     R.flags = c->d_rflags.p;
     R.err = c->d_err.p;
+    int rs = release_scratch(c, R, n);
+    if (rs) return rs;
     HIPCHK(c, owgs_launch_release_seq(&R, st));
     HIPCHK(c, owgs_launch_ack_flags(n, c->k_info.p, c->d_rflags.p, d_kind, d_flags, st));
     unsigned long long cnt[2];

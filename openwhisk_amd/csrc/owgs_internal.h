@@ -218,6 +218,15 @@ struct OwgsReleaseArgs {
     const int32_t* slot;
     uint8_t* flags;
     int32_t* err;
+    // scratch of the parallel front end (owgs_launch_release_seq): per-invoker upper bound of the memory returned,
+    // overflow-risk word, selection of the releases the ordered kernel still has to apply
+    unsigned long long* bound;  // [n_slots]
+    int32_t* risk;
+    uint8_t* sel_flag;          // [n]
+    int32_t* sel_idx;           // [n]
+    int32_t* sel_cnt;
+    void* temp;
+    size_t temp_bytes;
 };
 
 struct OwgsLookupArgs {

@@ -31,6 +31,7 @@
 // The I/O wave streams the next chunk's records from HBM into an LDS double buffer; the engine waves only store to
 // HBM (decisions, release records), so no engine-wave load ever waits behind its own stores.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include "owgs_internal.h"
 
@@ -2049,6 +2050,46 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
 // owgs_release_batch: releases in stream order, 64 at a time.  maxConcurrent == 1: FS.release (FS:117-120) with the
 // overflow Error leaving the state unchanged; concurrent: RS.release(1, true) applied rank+1 times inside each group
 // of 64 (NS:98-113), NoSuchElementException when the entry is absent or already removed.
+// Parallel front end.  Every memory release only adds to a permit count, so releases commute unless one of them would
+// overflow (FS:48-50).  owgs_rel_bound_kernel sums, per invoker, an upper bound of what the batch can return (every
+// release's memory); if no invoker can overflow, the maxConcurrent == 1 releases are applied in parallel with atomics
+// and only the concurrent ones (whose NestedSemaphore entries are order-dependent) go through the ordered kernel;
+// otherwise every release does (the exact sequential path).
+__global__ __launch_bounds__(256) void owgs_rel_bound_kernel(OwgsReleaseArgs R) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= R.n) return;
+    const int inv = R.inv[r];
+    const bool in = inv >= 0 && inv < R.n_slots;
+    if (in) atomicAdd(&R.bound[inv], (unsigned long long)R.mem[r]);
+    if (!in && R.flags) R.flags[r] = inv < 0 ? OWGS_REL_NOENTRY_BIT : 0;  // invokerSlots.lift -> no-op (SCPB:329)
+}
+__global__ __launch_bounds__(256) void owgs_rel_check_kernel(OwgsReleaseArgs R) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= R.n_slots) return;
+    if ((long long)R.permits[i] + (long long)R.bound[i] > 0x7FFFFFFFll) atomicOr(R.risk, 1);
+}
+__global__ __launch_bounds__(256) void owgs_rel_apply_kernel(OwgsReleaseArgs R) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= R.n) return;
+    const int inv = R.inv[r];
+    const bool in = inv >= 0 && inv < R.n_slots;
+    const bool risk = *R.risk != 0;
+    uint8_t sel = 0;
+    if (in) {
+        if (risk || R.maxc[r] > 1) {
+            sel = 1;
+        } else {
+            atomicAdd(&R.permits[inv], R.mem[r]);
+            if (R.flags) R.flags[r] = 0;
+        }
+    }
+    R.sel_flag[r] = sel;
+}
+
+// the ordered part: the selected releases (all concurrent ones, or every in-range release when an overflow is
+// possible) in stream order, 64 at a time.  maxConcurrent == 1: FS.release (FS:117-120) with the overflow Error
+// leaving the state unchanged; concurrent: RS.release(1, true) applied rank+1 times inside each group of 64
+// (NS:98-113), NoSuchElementException when the entry is absent or already removed.
 __global__ __launch_bounds__(64) void owgs_release_seq_kernel(OwgsReleaseArgs R) {
     __shared__ uint32_t ctk[OWGS_CTC], ctv[OWGS_CTC];
     const int lane = threadIdx.x;
@@ -2058,9 +2099,10 @@ __global__ __launch_bounds__(64) void owgs_release_seq_kernel(OwgsReleaseArgs R)
     }
     __syncthreads();
     const u64 lt_mask = lane == 0 ? 0ull : ((~0ull) >> (64 - lane));
-    for (int r0 = 0; r0 < R.n; r0 += 64) {
-        const int r = r0 + lane;
-        const bool valid = r < R.n;
+    const int n_sel = *R.sel_cnt;
+    for (int k0 = 0; k0 < n_sel; k0 += 64) {
+        const bool valid = k0 + lane < n_sel;
+        const int r = valid ? R.sel_idx[k0 + lane] : 0;
         int inv = -1, mem = 0, maxc = 1, slot = 0;
         if (valid) {
             inv = R.inv[r];
@@ -2230,7 +2272,29 @@ extern "C" hipError_t owgs_launch_relflags(const int64_t* rel_aid, int64_t n_rel
     return hipGetLastError();
 }
 
+extern "C" size_t owgs_release_scratch_bytes(int32_t n) {
+    size_t b = 0;
+    (void)hipcub::DeviceSelect::Flagged(nullptr, b, hipcub::CountingInputIterator<int32_t>(0), (const uint8_t*)nullptr,
+                                        (int32_t*)nullptr, (int32_t*)nullptr, n);
+    return b;
+}
+
 extern "C" hipError_t owgs_launch_release_seq(const OwgsReleaseArgs* a, hipStream_t s) {
+    const OwgsReleaseArgs& R = *a;
+    hipError_t e = hipMemsetAsync(R.bound, 0, (size_t)std::max(R.n_slots, 1) * 8, s);
+    if (e == hipSuccess) e = hipMemsetAsync(R.risk, 0, 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(R.sel_cnt, 0, 4, s);
+    if (e != hipSuccess) return e;
+    if (R.n > 0) {
+        const unsigned gn = (unsigned)((R.n + 255) / 256), gs = (unsigned)((std::max(R.n_slots, 1) + 255) / 256);
+        hipLaunchKernelGGL(owgs_rel_bound_kernel, dim3(gn), dim3(256), 0, s, R);
+        hipLaunchKernelGGL(owgs_rel_check_kernel, dim3(gs), dim3(256), 0, s, R);
+        hipLaunchKernelGGL(owgs_rel_apply_kernel, dim3(gn), dim3(256), 0, s, R);
+        size_t tb = R.temp_bytes;
+        e = hipcub::DeviceSelect::Flagged(R.temp, tb, hipcub::CountingInputIterator<int32_t>(0), R.sel_flag, R.sel_idx,
+                                          R.sel_cnt, R.n, s);
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(owgs_release_seq_kernel, dim3(1), dim3(64), 0, s, *a);
     return hipGetLastError();
 }
