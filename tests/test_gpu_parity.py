@@ -263,6 +263,24 @@ def test_release_flags():
     assert b.permits().tolist() == [1024] * 4
 
 
+def test_release_overflow_takes_the_ordered_path():
+    # a batch where a release can overflow an invoker's permits (FS:48-50) is applied in stream order: exactly the
+    # overflowing releases are rejected (flag 2, state unchanged), the others of the batch still apply
+    b = gpu()
+    b.update_invokers([InvokerHealth(i, 1024 * MB) for i in range(3)])
+    acts, _ = b.register_actions([Action("ns", "ns/a", "0.0.1", 256, 1)])
+    top = 2**31 - 1
+    b.set_slots([top - 300, 1000, top - 256])
+    rf = b.release_invoker([0, 1, 0, 2, 2], [acts[0]] * 5)
+    assert rf.tolist() == [0, 0, 2, 0, 2]
+    assert b.permits().tolist() == [top - 44, 1256, top]
+    # without overflow risk the same releases take the parallel path
+    b.set_slots([1000, 1000, 1000])
+    rf = b.release_invoker([0, 1, 0, 2, 2, 7, -1], [acts[0]] * 7)
+    assert rf.tolist() == [0, 0, 0, 0, 0, 0, 4]
+    assert b.permits().tolist() == [1512, 1256, 1512]
+
+
 def test_release_after_cluster_change_is_nosuchelement():
     b = gpu()
     b.update_invokers([InvokerHealth(i, 1024 * MB) for i in range(2)])
