@@ -174,7 +174,8 @@ struct owgs_ctx {
     int32_t h_cap = 0, h_size = 0;
     hipEvent_t ev_engine[2] = {nullptr, nullptr};  // around the last owgs_engine_kernel launch
     DevBuf<unsigned long long> r_bound;  // release front end scratch (owgs_launch_release_seq)
-    DevBuf<int32_t> r_idx, r_cnt;
+    DevBuf<int32_t> r_idx, r_cnt, r_cval, r_cval_s, r_cbeg;
+    DevBuf<uint32_t> r_ckey, r_ckey_s;
     DevBuf<uint8_t> r_sel, r_temp;
     bool ev_engine_valid = false;
     // ActivationMessage templates + serialisation scratch (owgs_msgs.hip)
@@ -569,6 +570,11 @@ void owgs_destroy(owgs_ctx* c) {
     c->r_cnt.release();
     c->r_sel.release();
     c->r_temp.release();
+    c->r_cval.release();
+    c->r_cval_s.release();
+    c->r_cbeg.release();
+    c->r_ckey.release();
+    c->r_ckey_s.release();
     c->h_st.release();
     c->he_kind.release();
     c->he_temp.release();
@@ -811,6 +817,18 @@ static int release_scratch(owgs_ctx* c, OwgsReleaseArgs& R, int32_t n) {
     R.sel_cnt = c->r_cnt.p;
     R.temp = c->r_temp.p;
     R.temp_bytes = tb;
+    const size_t m = (size_t)std::max(n, 1);
+    HIPCHK(c, c->r_ckey.reserve(m));
+    HIPCHK(c, c->r_ckey_s.reserve(m));
+    HIPCHK(c, c->r_cval.reserve(m));
+    HIPCHK(c, c->r_cval_s.reserve(m));
+    HIPCHK(c, c->r_cbeg.reserve(2 * OWGS_CTC));
+    R.ckey = c->r_ckey.p;
+    R.ckey_s = c->r_ckey_s.p;
+    R.cval = c->r_cval.p;
+    R.cval_s = c->r_cval_s.p;
+    R.cbeg = c->r_cbeg.p;
+    R.cend = c->r_cbeg.p + OWGS_CTC;
     return OWGS_OK;
 }
 

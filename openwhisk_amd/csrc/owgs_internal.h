@@ -227,6 +227,14 @@ struct OwgsReleaseArgs {
     int32_t* sel_cnt;
     void* temp;
     size_t temp_bytes;
+    // concurrent releases grouped by NestedSemaphore entry (no-risk path): entry key and release index per release,
+    // sorted copies, and each entry's [begin, end) in the sorted order
+    uint32_t* ckey;      // [n]
+    int32_t* cval;       // [n]
+    uint32_t* ckey_s;    // [n]
+    int32_t* cval_s;     // [n]
+    int32_t* cbeg;       // [OWGS_CTC]
+    int32_t* cend;       // [OWGS_CTC]
 };
 
 struct OwgsLookupArgs {

@@ -2053,8 +2053,8 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
 // Parallel front end.  Every memory release only adds to a permit count, so releases commute unless one of them would
 // overflow (FS:48-50).  owgs_rel_bound_kernel sums, per invoker, an upper bound of what the batch can return (every
 // release's memory); if no invoker can overflow, the maxConcurrent == 1 releases are applied in parallel with atomics
-// and only the concurrent ones (whose NestedSemaphore entries are order-dependent) go through the ordered kernel;
-// otherwise every release does (the exact sequential path).
+// and the concurrent ones grouped by NestedSemaphore entry (stable sort) and applied in closed form per entry;
+// otherwise every release goes through the ordered kernel (the exact sequential path).
 __global__ __launch_bounds__(256) void owgs_rel_bound_kernel(OwgsReleaseArgs R) {
     const int r = blockIdx.x * 256 + threadIdx.x;
     if (r >= R.n) return;
@@ -2075,15 +2075,68 @@ __global__ __launch_bounds__(256) void owgs_rel_apply_kernel(OwgsReleaseArgs R) 
     const bool in = inv >= 0 && inv < R.n_slots;
     const bool risk = *R.risk != 0;
     uint8_t sel = 0;
+    uint32_t key = OWGS_CTC;  // no concurrent entry: sorts after every entry
     if (in) {
-        if (risk || R.maxc[r] > 1) {
+        if (risk) {
             sel = 1;
-        } else {
+        } else if (R.maxc[r] == 1) {
             atomicAdd(&R.permits[inv], R.mem[r]);
             if (R.flags) R.flags[r] = 0;
+        } else {
+            const int ix = ct_find(R.ct_keys, ct_key(inv, R.slot[r]));
+            const uint32_t v = ix >= 0 ? R.ct_vals[ix] : 0u;
+            if (ix < 0 || (int)(v >> OWGS_CT_C_BITS) <= 0) {
+                if (R.flags) R.flags[r] = OWGS_REL_NOSUCH_BIT;  // NoSuchElementException (NS:103)
+            } else {
+                key = (uint32_t)ix;
+            }
         }
     }
     R.sel_flag[r] = sel;
+    R.ckey[r] = key;
+    R.cval[r] = r;
+}
+
+// concurrent releases of one entry, in stream order (sorted by entry, stable): RS.release(1, true) (RS:99-108,
+// NS:98-113) in closed form -- release q of the entry (0-based) finds the entry when q < opCount and returns the
+// memory iff (c0 + q + 1) % maxConcurrent == 0; the entry ends at c = (c0 + j) % maxConcurrent, opCount - j
+__global__ __launch_bounds__(256) void owgs_rel_cseg_kernel(OwgsReleaseArgs R) {
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= R.n) return;
+    const uint32_t k = R.ckey_s[p];
+    if (k >= OWGS_CTC) return;
+    if (p == 0 || R.ckey_s[p - 1] != k) R.cbeg[k] = p;
+    if (p == R.n - 1 || R.ckey_s[p + 1] != k) R.cend[k] = p + 1;
+}
+__global__ __launch_bounds__(256) void owgs_rel_capply_kernel(OwgsReleaseArgs R) {
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= R.n) return;
+    const uint32_t k = R.ckey_s[p];
+    if (k >= OWGS_CTC) return;
+    const int r = R.cval_s[p], q = p - R.cbeg[k];
+    const uint32_t v = R.ct_vals[k];
+    const int c0 = (int)(v & OWGS_CT_C_MASK), o0 = (int)(v >> OWGS_CT_C_BITS), maxc = R.maxc[r];
+    uint8_t flag = 0;
+    if (q < o0) {
+        if ((c0 + q + 1) % maxc == 0) atomicAdd(&R.permits[R.inv[r]], R.mem[r]);
+    } else {
+        flag = OWGS_REL_NOSUCH_BIT;  // the entry was removed by an earlier release of this batch
+    }
+    if (R.flags) R.flags[r] = flag;
+}
+__global__ __launch_bounds__(256) void owgs_rel_cupdate_kernel(OwgsReleaseArgs R) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= OWGS_CTC || R.cend[k] <= R.cbeg[k]) return;
+    const int r = R.cval_s[R.cbeg[k]];
+    const uint32_t v = R.ct_vals[k];
+    const int c0 = (int)(v & OWGS_CT_C_MASK), o0 = (int)(v >> OWGS_CT_C_BITS), maxc = R.maxc[r];
+    const int j = min(R.cend[k] - R.cbeg[k], o0), o1 = o0 - j;
+    if (o1 == 0) {
+        R.ct_keys[k] = OWGS_CT_TOMB;
+        R.ct_vals[k] = 0u;
+    } else {
+        R.ct_vals[k] = (uint32_t)((c0 + j) % maxc) | ((uint32_t)o1 << OWGS_CT_C_BITS);
+    }
 }
 
 // the ordered part: the selected releases (all concurrent ones, or every in-range release when an overflow is
@@ -2272,11 +2325,15 @@ extern "C" hipError_t owgs_launch_relflags(const int64_t* rel_aid, int64_t n_rel
     return hipGetLastError();
 }
 
+#define REL_KEY_BITS 13  // entry keys 0..OWGS_CTC (4096 = no entry)
+
 extern "C" size_t owgs_release_scratch_bytes(int32_t n) {
-    size_t b = 0;
+    size_t b = 0, c = 0;
     (void)hipcub::DeviceSelect::Flagged(nullptr, b, hipcub::CountingInputIterator<int32_t>(0), (const uint8_t*)nullptr,
                                         (int32_t*)nullptr, (int32_t*)nullptr, n);
-    return b;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, c, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                             (const int32_t*)nullptr, (int32_t*)nullptr, n, 0, REL_KEY_BITS);
+    return b > c ? b : c;
 }
 
 extern "C" hipError_t owgs_launch_release_seq(const OwgsReleaseArgs* a, hipStream_t s) {
@@ -2290,7 +2347,16 @@ extern "C" hipError_t owgs_launch_release_seq(const OwgsReleaseArgs* a, hipStrea
         hipLaunchKernelGGL(owgs_rel_bound_kernel, dim3(gn), dim3(256), 0, s, R);
         hipLaunchKernelGGL(owgs_rel_check_kernel, dim3(gs), dim3(256), 0, s, R);
         hipLaunchKernelGGL(owgs_rel_apply_kernel, dim3(gn), dim3(256), 0, s, R);
+        // concurrent releases by entry (nothing to do after an overflow-risk verdict: every key is OWGS_CTC)
         size_t tb = R.temp_bytes;
+        e = hipcub::DeviceRadixSort::SortPairs(R.temp, tb, R.ckey, R.ckey_s, R.cval, R.cval_s, R.n, 0, REL_KEY_BITS, s);
+        if (e == hipSuccess) e = hipMemsetAsync(R.cbeg, 0, OWGS_CTC * 4, s);
+        if (e == hipSuccess) e = hipMemsetAsync(R.cend, 0, OWGS_CTC * 4, s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(owgs_rel_cseg_kernel, dim3(gn), dim3(256), 0, s, R);
+        hipLaunchKernelGGL(owgs_rel_capply_kernel, dim3(gn), dim3(256), 0, s, R);
+        hipLaunchKernelGGL(owgs_rel_cupdate_kernel, dim3(OWGS_CTC / 256), dim3(256), 0, s, R);
+        tb = R.temp_bytes;
         e = hipcub::DeviceSelect::Flagged(R.temp, tb, hipcub::CountingInputIterator<int32_t>(0), R.sel_flag, R.sel_idx,
                                           R.sel_cnt, R.n, s);
         if (e != hipSuccess) return e;
