@@ -91,7 +91,7 @@ __constant__ char k_names[9][16] = {"activationId", "invoker", "isSystemError", 
 __constant__ int k_len[9] = {12, 7, 13, 8, 7, 8, 10, 13, 10};
 
 // bitmask of the candidate names (lo..hi) the decoded key equals
-__device__ int key_match(Win& W, int64_t k, int lo, int hi) {
+__device__ __forceinline__ int key_match(Win& W, int64_t k, int lo, int hi) {
     int64_t i = k + 1;
     uint32_t alive = ((1u << (hi + 1)) - 1u) & ~((1u << lo) - 1u);
     int n = 0;
@@ -112,7 +112,7 @@ __device__ int key_match(Win& W, int64_t k, int lo, int hi) {
 #define EV_UNSUP 2
 
 // string starting at i (the opening quote); returns the index after the closing quote, or -1 on a grammar error
-__device__ int64_t scan_string(Win& W, int64_t i) {
+__device__ __forceinline__ int64_t scan_string(Win& W, int64_t i) {
     ++i;
     for (;;) {
         const int c = W.at(i);
@@ -137,7 +137,7 @@ __device__ int64_t scan_string(Win& W, int64_t i) {
 }
 
 // number at i; returns the index after it, -1 on a grammar error, -2 for an exponent of more than 9 digits
-__device__ int64_t scan_number(Win& W, int64_t i) {
+__device__ __forceinline__ int64_t scan_number(Win& W, int64_t i) {
     if (W.at(i) == '-') ++i;
     int c = W.at(i);
     if (c == '0') ++i;
@@ -165,7 +165,7 @@ __device__ int64_t scan_number(Win& W, int64_t i) {
 
 // low 64 bits of the integer part of a validated number literal (BigDecimal -> BigInteger.longValue), significant
 // digit count in *sig
-__device__ u64 number_bits(Win& W, int64_t i, int* sig) {
+__device__ __forceinline__ u64 number_bits(Win& W, int64_t i, int* sig) {
     bool neg = false;
     if (W.at(i) == '-') neg = true, ++i;
     const int64_t ib = i;
@@ -208,7 +208,7 @@ __device__ u64 number_bits(Win& W, int64_t i, int* sig) {
 }
 
 // skip one validated value at i (containers by depth counting, strings by scan_string)
-__device__ int64_t skip_value(Win& W, int64_t i) {
+__device__ __forceinline__ int64_t skip_value(Win& W, int64_t i) {
     int depth = 0;
     for (;;) {
         const int c = W.at(i);
@@ -224,7 +224,7 @@ __device__ int64_t skip_value(Win& W, int64_t i) {
 }
 
 // ByteSize.fromString over the decoded string at a (Size.scala:119-138)
-__device__ bool bytesize_ok(Win& W, int64_t a) {
+__device__ __forceinline__ bool bytesize_ok(Win& W, int64_t a) {
     int64_t i = a + 1;
     int st = 0;
     u64 val = 0;
@@ -315,7 +315,9 @@ __global__ __launch_bounds__(256) void owgs_ack_parse_kernel(OwgsAckParseArgs A)
                 while (is_ws(W.at(i))) ++i;
                 if (d == 1) {
                     const int id = key_match(W, k, K_AID, K_TID);
-                    if (id >= 0) v[id] = i;
+#pragma unroll
+                    for (int q = 0; q < 5; ++q)  // constant indices: v stays in registers (no scratch)
+                        if (id == q) v[q] = i;
                 }
                 st = VALUE;
             } else {  // AFTER a value
@@ -392,7 +394,9 @@ __global__ __launch_bounds__(256) void owgs_ack_parse_kernel(OwgsAckParseArgs A)
                             ++j;  // ':'
                             while (is_ws(W.at(j))) ++j;
                             const int id = key_match(W, k, K_INSTANCE, K_USERMEM);
-                            if (id >= 0) w[id - K_INSTANCE] = j;
+#pragma unroll
+                            for (int q = 0; q < 4; ++q)  // constant indices: w stays in registers
+                                if (id - K_INSTANCE == q) w[q] = j;
                             j = skip_value(W, j);
                             while (is_ws(W.at(j))) ++j;
                             if (W.at(j) != ',') break;
@@ -418,7 +422,9 @@ __global__ __launch_bounds__(256) void owgs_ack_parse_kernel(OwgsAckParseArgs A)
                 if (W.at(j) != ']') {
                     for (;;) {
                         while (is_ws(W.at(j))) ++j;
-                        if (ne < 3) el[ne] = j;
+#pragma unroll
+                        for (int q = 0; q < 3; ++q)  // constant indices: el stays in registers
+                            if (ne == q) el[q] = j;
                         ++ne;
                         j = skip_value(W, j);
                         while (is_ws(W.at(j))) ++j;
