@@ -582,6 +582,7 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
     // class masks (one ballot per wave and class): thread 0's dealing below walks set bits in registers instead of
     // re-reading every lane's class from LDS in each of its loops
     __shared__ unsigned long long s_m[3][(OWGS_WL + 63) / 64];
+    __shared__ int s_cnt[OWGS_EW], s_cap[OWGS_EW];
     {
         const unsigned long long m0 = __ballot(t < len && cls == 0), m1 = __ballot(t < len && cls == 1),
                                  m2 = __ballot(t < len && cls == 2);
@@ -594,19 +595,18 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
     __syncthreads();
     if (t == 0) {
         constexpr int NWR = (OWGS_WL + 63) / 64;
-        unsigned long long mk[3][NWR];
-        for (int c = 0; c < 3; ++c)
-            for (int r = 0; r < NWR; ++r) mk[c][r] = s_m[c][r];
-        // f(j) for every lane j of class c, in stream order
+        // f(j) for every lane j of class c, in stream order (masks and the per-wave counters below live in LDS:
+        // indexed by runtime values, a thread-private array would sit in scratch memory)
         auto each = [&](int c, auto&& f) {
             for (int r = 0; r < NWR; ++r)
-                for (unsigned long long m = mk[c][r]; m; m &= m - 1) f(r * 64 + __builtin_ctzll(m));
+                for (unsigned long long m = s_m[c][r]; m; m &= m - 1) f(r * 64 + __builtin_ctzll(m));
         };
         // the maxConcurrent == 1 walkers fill the first waves; the concurrent lanes are spread round-robin over the
         // remaining waves and the lanes without a walk fill the gaps (from the last wave down), so the waves that
         // run the concurrent path hold fewer of them (a wave takes as long as its slowest lane).  Wave w holds
         // positions [wave_off(len, w), + wave_cap(len, w)): the chunk spread evenly, positions dense below len.
-        int cnt[OWGS_EW], cap[OWGS_EW];
+        int* cnt = s_cnt;
+        int* cap = s_cap;
         int n0 = 0, nwv = 0;
         for (int w = 0; w < OWGS_EW; ++w) {
             cnt[w] = 0;
@@ -615,9 +615,9 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
         }
         int n1 = 0, n2 = 0;
         for (int r = 0; r < NWR; ++r) {
-            n0 += __popcll(mk[0][r]);
-            n1 += __popcll(mk[1][r]);
-            n2 += __popcll(mk[2][r]);
+            n0 += __popcll(s_m[0][r]);
+            n1 += __popcll(s_m[1][r]);
+            n2 += __popcll(s_m[2][r]);
         }
         // place the class-c lanes round-robin over waves [wlo, whi) (skipping full ones), spilling anywhere
         auto deal = [&](int c, int wlo, int whi) {
