@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--shards-per-gpu", type=int, default=1,
+                    help="controller shards hosted per GPU (clusterSize = gpus x this), one HIP stream and one engine "
+                         "workgroup each, replayed concurrently")
     return ap.parse_args()
 
 
@@ -127,37 +130,61 @@ def main():
 
     from openwhisk_amd import GpuShardingContainerPoolBalancer
 
-    w = cluster.shard_workload(args.config, rank, world, n_activations=args.n_activations)
-    b = GpuShardingContainerPoolBalancer(managed_fraction=w.managed_fraction, blackbox_fraction=w.blackbox_fraction,
-                                         rng_seed=w.rng_seed, device=torch.cuda.current_device())
-    b.update_invokers_arrays(w.inv_ids, w.inv_mem, w.inv_status)
-    b.update_cluster(w.cluster_size)
-    b.register_actions(w.actions)
-    b.snapshot()
-
-    s = w.stream
+    K = max(1, args.shards_per_gpu)
+    n_ctl = world * K  # controllers in the cluster: rank r hosts shards r*K .. r*K+K-1
     t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
-    d_acq, d_rel = t(s.acq_off, np.int64), t(s.rel_off, np.int64)
-    d_act, d_aid = t(s.act, np.int32), t(s.rel_aid if len(s.rel_aid) else np.zeros(1), np.int64)
-    d_out = torch.empty(len(s.act), dtype=torch.int32, device=dev)
-    d_fl = torch.empty(len(s.act), dtype=torch.uint8, device=dev)
-    d_rf = torch.empty(max(len(s.rel_aid), 1), dtype=torch.uint8, device=dev)
+
+    class Shard:
+        """One controller shard: its own balancer context, stream buffers in HBM and HIP stream."""
+
+        def __init__(self, idx):
+            self.w = w = cluster.shard_workload(args.config, idx, n_ctl, n_activations=args.n_activations)
+            self.b = b = GpuShardingContainerPoolBalancer(
+                managed_fraction=w.managed_fraction, blackbox_fraction=w.blackbox_fraction, rng_seed=w.rng_seed,
+                device=torch.cuda.current_device())
+            b.update_invokers_arrays(w.inv_ids, w.inv_mem, w.inv_status)
+            b.update_cluster(w.cluster_size)
+            b.register_actions(w.actions)
+            b.snapshot()
+            s = self.s = w.stream
+            self.d_acq, self.d_rel = t(s.acq_off, np.int64), t(s.rel_off, np.int64)
+            self.d_act = t(s.act, np.int32)
+            self.d_aid = t(s.rel_aid if len(s.rel_aid) else np.zeros(1), np.int64)
+            self.d_out = torch.empty(len(s.act), dtype=torch.int32, device=dev)
+            self.d_fl = torch.empty(len(s.act), dtype=torch.uint8, device=dev)
+            self.d_rf = torch.empty(max(len(s.rel_aid), 1), dtype=torch.uint8, device=dev)
+            self.stream = torch.cuda.Stream()  # a real (non-null) HIP stream: engine and timing events share it
+            self.sp = self.stream.cuda_stream
+
+        def replay(self):
+            s = self.s
+            self.b.restore(self.sp)
+            self.b.replay_device(s.n_batches, self.d_acq.data_ptr(), self.d_act.data_ptr(), len(s.act),
+                                 self.d_rel.data_ptr(), self.d_aid.data_ptr(), len(s.rel_aid), s.seq_base,
+                                 self.d_out.data_ptr(), self.d_fl.data_ptr(), self.d_rf.data_ptr(), self.sp)
+
+    shards = [Shard(rank * K + k) for k in range(K)]
+    w, s, b = shards[0].w, shards[0].s, shards[0].b
     hx = cluster.HealthExchange(dist, torch.from_numpy(w.inv_status.copy()).to(dev), world)
     torch.cuda.synchronize()
-    stream = torch.cuda.Stream()  # a real (non-null) HIP stream: the engine and the timing events share it
+    stream = shards[0].stream
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
 
-    def step():
+    def launch_all():
         if world > 1:
-            b.update_health_device(len(w.inv_status), hx.exchange().data_ptr(), sp)
-        b.restore(sp)
-        b.replay_device(s.n_batches, d_acq.data_ptr(), d_act.data_ptr(), len(s.act), d_rel.data_ptr(),
-                        d_aid.data_ptr(), len(s.rel_aid), s.seq_base, d_out.data_ptr(), d_fl.data_ptr(),
-                        d_rf.data_ptr(), sp)
+            h = hx.exchange()  # on shards[0]'s stream; the other shards' streams wait for it
+            for sh in shards:
+                if sh is not shards[0]:
+                    sh.stream.wait_stream(stream)
+                sh.b.update_health_device(len(w.inv_status), h.data_ptr(), sh.sp)
+        for sh in shards:
+            sh.replay()
+        for sh in shards[1:]:
+            stream.wait_stream(sh.stream)  # the step ends when every shard's replay has ended
 
     for _ in range(args.warmup):
-        step()
+        launch_all()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -165,13 +192,8 @@ def main():
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for k in range(args.steps):
-        if world > 1:
-            b.update_health_device(len(w.inv_status), hx.exchange().data_ptr(), sp)
-        b.restore(sp)
         evs[k][0].record(stream)
-        b.replay_device(s.n_batches, d_acq.data_ptr(), d_act.data_ptr(), len(s.act), d_rel.data_ptr(),
-                        d_aid.data_ptr(), len(s.rel_aid), s.seq_base, d_out.data_ptr(), d_fl.data_ptr(),
-                        d_rf.data_ptr(), sp)
+        launch_all()
         evs[k][1].record(stream)
     torch.cuda.synchronize()
     if dist:
@@ -184,8 +206,8 @@ def main():
     # read after instrumented replays outside the timed region (reading them inside would add a sync per step)
     eng = []
     for _ in range(max(3, min(args.steps, 5))):
-        step()
-        eng.append(b.engine_ms())
+        launch_all()
+        eng.append(float(np.mean([sh.b.engine_ms() for sh in shards])))
     kern_ms = float(np.mean(eng))
 
     exact = True
@@ -193,13 +215,15 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O
 
-        st = O.state_for(w)
-        o_inv, o_fl, o_rf = st.replay(s)
-        exact = (np.array_equal(o_inv, d_out.cpu().numpy()) and np.array_equal(o_fl, d_fl.cpu().numpy())
-                 and np.array_equal(o_rf, d_rf.cpu().numpy()[: len(o_rf)])
-                 and np.array_equal(st.permits(), b.permits()))
+        for sh in shards:
+            st = O.state_for(sh.w)
+            o_inv, o_fl, o_rf = st.replay(sh.s)
+            exact = exact and (np.array_equal(o_inv, sh.d_out.cpu().numpy())
+                               and np.array_equal(o_fl, sh.d_fl.cpu().numpy())
+                               and np.array_equal(o_rf, sh.d_rf.cpu().numpy()[: len(o_rf)])
+                               and np.array_equal(st.permits(), sh.b.permits()))
 
-    n_dec = len(s.act)
+    n_dec = sum(len(sh.s.act) for sh in shards)  # this rank's decisions per step
     t_step = wall / args.steps
     t_step, bad, kern_ms, replay_ms = cluster.max_over_ranks(dist, [t_step, 0.0 if exact else 1.0, kern_ms, replay_ms],
                                                              dev)
@@ -228,9 +252,9 @@ def main():
             "dtype": "int32",
             "data": "synthetic (workload.py, seeded Zipf stream)",
             "bit_exact": exact,
-            "config": {"workload": args.config, "invokers": int(len(w.inv_ids)), "activations_per_shard": n_dec,
+            "config": {"workload": args.config, "invokers": int(len(w.inv_ids)), "activations_per_shard": len(s.act),
                        "batches": s.n_batches, "batch": w.info["batch"], "releases": int(len(s.rel_aid)),
-                       "cluster_size": w.cluster_size, "parallelism": f"{world} controller shard(s), 1 per GPU"},
+                       "cluster_size": w.cluster_size, "parallelism": f"{n_ctl} controller shard(s), {K} per GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "owgs_engine_kernel", "kernel_ms": kern_ms, "replay_ms": replay_ms,

@@ -89,6 +89,7 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
 #define SC_USED 6   // non-empty concurrency-table entries (live + deleted)
 #define SC_NLIVE 7  // table rebuild: live entries
 #define SC_NHOT 8   // multi-lane actions of the current chunk (hot slots claimed)
+#define SC_CBWD 9   // 1 + the chunk that moved a concurrent action's HBM walk cursor backward (forced acquire)
 #define SC_N (16 + 6 * OWGS_EW)
 
 // hot actions: every action with >= HOT_MIN lanes in a chunk gets a slot (assigned by the pre-pass; a concurrent
@@ -1274,7 +1275,12 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
             // the step starts from the action's HBM cursor when it was written in this batch (a lower bound: steps
             // before it were full and permits only fall inside a batch)
             if (held && occ == 0) {
-                const uint32_t st0 = (a != (int)OWGS_REC_NOACT && cok && (gcw >> 15) == btag) ? (gcw & 0x7FFFu) : 0u;
+                // the I/O wave gathered this chunk's cursors while the previous chunk ran: a concurrent forced
+                // acquire there moved its action's cursor BACK (fallback_cursor), so the gathered word may be past
+                // the new container; concurrent lanes then walk from step 0 (always a valid lower bound)
+                const bool stale = maxc > 1 && sc[SC_CBWD] == g;
+                const uint32_t st0 =
+                    (a != (int)OWGS_REC_NOACT && cok && !stale && (gcw >> 15) == btag) ? (gcw & 0x7FFFu) : 0u;
                 ccw[li] = st0;
             }
 
@@ -1928,8 +1934,15 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
                             else if (kind == K_FALLBACK) ns = maxc == 1 ? (uint32_t)n : fallback_cursor(t);
                         }
                         ccw[lead] = ((uint32_t)(occ + 1) << 15) | ns;
-                        if (cok && a != (int)OWGS_REC_NOACT && ns != (cw & 0x7FFFu))
+                        if (cok && a != (int)OWGS_REC_NOACT && ns != (cw & 0x7FFFu)) {
                             A.gcur[a] = (btag << 15) | ns;  // for the later chunks of this batch
+                            if (kind == K_FALLBACK && maxc > 1) {
+                                // backward move: the next chunk's gathered cursors predate it (see `stale`), and
+                                // the store must reach L2 before the chunk after that gathers again
+                                sc[SC_CBWD] = g + 1;
+                                __threadfence();
+                            }
+                        }
                     }
                     // NestedSemaphore concurrency entry: the last committed lane of the (invoker, fqn) group
                     if (maxc > 1 && (kind == K_TARGET || kind == K_FALLBACK)) {

@@ -217,6 +217,14 @@ def test_c5_shard_full_size_parity():
     check_stream(W.config("headline", shard=3, n_shards=8))
 
 
+@pytest.mark.parametrize("shard,n_shards", [(1, 8), (6, 8), (1, 4)])
+def test_cluster_shard_forced_concurrent_cursor(shard, n_shards):
+    # regression: a concurrent action forced onto invoker x (fallback) in one chunk, then scheduled again in the next
+    # chunk, whose walk cursors were gathered before the forced acquire moved the cursor back to x's step (these
+    # shards hit it at activations 670829 / 938326 / 288323 of their full 1M streams)
+    check_stream(W.config("headline", shard=shard, n_shards=n_shards), zombies=True)
+
+
 def test_multi_shard_cluster_parity():
     # C5-style shards: clusterSize 8, each shard its own stream; shard state = 1/8 of every invoker
     for g in (0, 7):

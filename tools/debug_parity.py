@@ -13,8 +13,10 @@ from openwhisk_amd import workload as W  # noqa: E402
 
 name = sys.argv[1] if len(sys.argv) > 1 else "c1"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else None
-w = W.config(name, n_activations=n)
-st = O.state_for(w, zombies=False)
+shard = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+n_shards = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+w = W.config(name, n_activations=n, shard=shard, n_shards=n_shards) if n_shards > 1 else W.config(name, n_activations=n)
+st = O.state_for(w, zombies=os.environ.get("ZOMBIES", "1") == "1")
 o_inv, o_fl, o_rf = st.replay(w.stream)
 b = GpuShardingContainerPoolBalancer(managed_fraction=w.managed_fraction, blackbox_fraction=w.blackbox_fraction,
                                      rng_seed=w.rng_seed)
@@ -31,4 +33,10 @@ print(name, "n", len(o_inv), "mismatches", len(bad), "stats", b.stats())
 acq = w.stream.acq_off
 for i in bad[:12]:
     bt = int(np.searchsorted(acq, i, side="right") - 1)
-    print(f"  i={i} batch={bt} chunk_lane={(i - acq[bt]) % 256} act={w.stream.act[i]} oracle={o_inv[i]} gpu={g_inv[i]}")
+    a = w.actions[w.stream.act[i]]
+    print(f"  i={i} batch={bt} lane={i - acq[bt]} act={w.stream.act[i]} {a} oracle={o_inv[i]}/{o_fl[i]} "
+          f"gpu={g_inv[i]}/{g_fl[i]}")
+bad_rf = np.nonzero(o_rf != g_rf[: len(o_rf)])[0]
+print("release flag mismatches", len(bad_rf), bad_rf[:5], "first release batch",
+      None if not len(bad_rf) else int(np.searchsorted(w.stream.rel_off, bad_rf[0], side="right") - 1))
+print("permit mismatches", int(np.sum(st.permits() != b.permits())))
