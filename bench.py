@@ -5,7 +5,8 @@ One step = one replay of a controller shard's activation stream (1M activations 
 each batch = completion releases then publishes; workload.py "headline": 10k invokers, Zipf actions, 128..2048 MB,
 concurrent + blackbox actions, 2 % unhealthy).  Inputs are resident in HBM before the timed region; the slot state is
 restored before every step (included in the timed region).  N GPUs = N controller shards (clusterSize = N, one stream
-each, weak scaling, no data-path collective); for N > 1 the invoker health vector is all-gathered over RCCL once per
+each, weak scaling, no data-path collective; by default invoker memory is 16 GiB x N so each shard's 1/N slot stays
+16 GiB -- `--slots split` keeps 16 GiB invokers split N ways); for N > 1 the invoker health vector is all-gathered over RCCL once per
 step (the reference's controllers all consume the same health topic, SCPB:355).
 
 Prints ONE JSON line on rank 0.  The value counts only when every rank's assignment vector is bit-exact with the
@@ -41,6 +42,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--slots", choices=("weak", "split"), default="weak",
+                    help="headline invoker memory: 'weak' = 16 GiB x clusterSize, so every controller shard's 1/N slot "
+                         "(SCPB:485-499) is 16 GiB at every N; 'split' = 16 GiB invokers split N ways")
     ap.add_argument("--shards-per-gpu", type=int, default=1,
                     help="controller shards hosted per GPU (clusterSize = gpus x this), one HIP stream and one engine "
                          "workgroup each, replayed concurrently")
@@ -138,7 +142,10 @@ def main():
         """One controller shard: its own balancer context, stream buffers in HBM and HIP stream."""
 
         def __init__(self, idx):
-            self.w = w = cluster.shard_workload(args.config, idx, n_ctl, n_activations=args.n_activations)
+            kw = {}
+            if args.slots == "weak" and args.config == "headline" and n_ctl > 1:
+                kw["user_memory_mb"] = 16_384 * n_ctl
+            self.w = w = cluster.shard_workload(args.config, idx, n_ctl, n_activations=args.n_activations, **kw)
             self.b = b = GpuShardingContainerPoolBalancer(
                 managed_fraction=w.managed_fraction, blackbox_fraction=w.blackbox_fraction, rng_seed=w.rng_seed,
                 device=torch.cuda.current_device())
@@ -254,7 +261,8 @@ def main():
             "bit_exact": exact,
             "config": {"workload": args.config, "invokers": int(len(w.inv_ids)), "activations_per_shard": len(s.act),
                        "batches": s.n_batches, "batch": w.info["batch"], "releases": int(len(s.rel_aid)),
-                       "cluster_size": w.cluster_size, "parallelism": f"{n_ctl} controller shard(s), {K} per GPU"},
+                       "cluster_size": w.cluster_size,
+                       "invoker_memory_mb": int(w.inv_mem[0] // (1 << 20)), "slot_mb": int(w.info["slot_mb"]), "parallelism": f"{n_ctl} controller shard(s), {K} per GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "owgs_engine_kernel", "kernel_ms": kern_ms, "replay_ms": replay_ms,
