@@ -46,8 +46,8 @@ def parse():
                     help="headline invoker memory: 'weak' = 16 GiB x clusterSize, so every controller shard's 1/N slot "
                          "(SCPB:485-499) is 16 GiB at every N; 'split' = 16 GiB invokers split N ways")
     ap.add_argument("--shards-per-gpu", type=int, default=1,
-                    help="controller shards hosted per GPU (clusterSize = gpus x this), one HIP stream and one engine "
-                         "workgroup each, replayed concurrently")
+                    help="controller shards hosted per GPU (clusterSize = gpus x this, at most 8), replayed by one "
+                         "engine launch with one workgroup per shard")
     return ap.parse_args()
 
 
@@ -163,6 +163,12 @@ def main():
             self.stream = torch.cuda.Stream()  # a real (non-null) HIP stream: engine and timing events share it
             self.sp = self.stream.cuda_stream
 
+        def io(self):
+            s = self.s
+            return (s.n_batches, self.d_acq.data_ptr(), self.d_act.data_ptr(), len(s.act), self.d_rel.data_ptr(),
+                    self.d_aid.data_ptr(), len(s.rel_aid), s.seq_base, self.d_out.data_ptr(), self.d_fl.data_ptr(),
+                    self.d_rf.data_ptr())
+
         def replay(self):
             s = self.s
             self.b.restore(self.sp)
@@ -179,6 +185,14 @@ def main():
     sp = stream.cuda_stream
 
     def launch_all():
+        if K > 1:  # every shard of this GPU in ONE engine launch (one workgroup each) on one stream
+            h = hx.exchange() if world > 1 else None
+            for sh in shards:
+                if h is not None:
+                    sh.b.update_health_device(len(w.inv_status), h.data_ptr(), sp)
+                sh.b.restore(sp)
+            GpuShardingContainerPoolBalancer.replay_device_multi([(sh.b, sh.io()) for sh in shards], sp)
+            return
         if world > 1:
             h = hx.exchange()  # on shards[0]'s stream; the other shards' streams wait for it
             for sh in shards:

@@ -148,6 +148,24 @@ int owgs_pairwise_coprime(owgs_ctx* ctx, int32_t x, int32_t* out, int32_t cap, i
 int owgs_replay_device(owgs_ctx* ctx, int32_t n_batches, const int64_t* acq_off, const int32_t* act,
                        int64_t n_activations, const int64_t* rel_off, const int64_t* rel_aid, int64_t n_releases,
                        uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, uint8_t* rel_flags, void* stream);
+/* Several controller shards (clusterSize > 1, one context each, same device) replayed by ONE engine launch, one
+ * workgroup per shard: the reference runs one ShardingContainerPoolBalancer per controller (SCPB:126-133,
+ * 485-499); this hosts up to 8 of them on one GPU.  io[i] holds owgs_replay_device's arguments for ctxs[i]; every
+ * shard needs n_batches > 0.  Same results as k separate owgs_replay_device calls.  Asynchronous on `stream`. */
+typedef struct owgs_replay_io {
+    int32_t n_batches;
+    const int64_t* acq_off;
+    const int32_t* act;
+    int64_t n_activations;
+    const int64_t* rel_off;
+    const int64_t* rel_aid;
+    int64_t n_releases;
+    uint64_t seq_base;
+    int32_t* out_invoker;
+    uint8_t* out_flags;
+    uint8_t* rel_flags;
+} owgs_replay_io;
+int owgs_replay_device_multi(owgs_ctx** ctxs, int32_t k, const owgs_replay_io* io, void* stream);
 /* Same with host buffers (copies in and out, synchronous). */
 int owgs_replay(owgs_ctx* ctx, int32_t n_batches, const int64_t* acq_off, const int32_t* act, const int64_t* rel_off,
                 const int64_t* rel_aid, uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags,

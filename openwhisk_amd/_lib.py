@@ -41,6 +41,14 @@ class owgs_config(C.Structure):
     ]
 
 
+class owgs_replay_io(C.Structure):
+    """include/owgs.h: owgs_replay_io (one controller shard of owgs_replay_device_multi)."""
+    _fields_ = [("n_batches", C.c_int32), ("acq_off", C.c_void_p), ("act", C.c_void_p),
+                ("n_activations", C.c_int64), ("rel_off", C.c_void_p), ("rel_aid", C.c_void_p),
+                ("n_releases", C.c_int64), ("seq_base", C.c_uint64), ("out_invoker", C.c_void_p),
+                ("out_flags", C.c_void_p), ("rel_flags", C.c_void_p)]
+
+
 class owgs_msg_batch(C.Structure):
     _fields_ = [("n", C.c_int32)] + [(k, C.c_void_p) for k in (
         "invoker", "tmpl", "aid", "tid", "tid_off", "tid_start", "flags", "content", "content_off", "cause", "trace",
@@ -112,6 +120,7 @@ def lib() -> C.CDLL:
         "owgs_complete_activations": (C.c_int, [P, i32, P, P, P, P, P, P]),
         "owgs_activations_live": (C.c_int, [P, P]),
         "owgs_replay_device": (C.c_int, [P, i32, P, P, C.c_int64, P, P, C.c_int64, u64, P, P, P, P]),
+        "owgs_replay_device_multi": (C.c_int, [P, i32, P, P]),
         "owgs_replay": (C.c_int, [P, i32, P, P, P, P, u64, P, P, P]),
         "owgs_snapshot": (C.c_int, [P]),
         "owgs_restore": (C.c_int, [P, P]),

@@ -391,6 +391,21 @@ class GpuShardingContainerPoolBalancer:
                                              vp(rel_aid), n_rel, seq_base, vp(out_inv), vp(out_flags), vp(rel_flags),
                                              vp(stream)))
 
+    @staticmethod
+    def replay_device_multi(shards, stream=None):
+        """Several controller shards in ONE engine launch (owgs_replay_device_multi, one workgroup per shard).
+        `shards` = [(balancer, (n_batches, acq_off, act, n_act, rel_off, rel_aid, n_rel, seq_base, out_inv,
+        out_flags, rel_flags)), ...] with device addresses as in replay_device."""
+        from ._lib import owgs_replay_io
+
+        k = len(shards)
+        ios = (owgs_replay_io * k)()
+        for j, (_, a) in enumerate(shards):
+            ios[j] = owgs_replay_io(*[int(x) if x else 0 for x in a])
+        hs = (C.c_void_p * k)(*[b._h for b, _ in shards])
+        b0 = shards[0][0]
+        b0._chk(b0._L.owgs_replay_device_multi(hs, k, ios, C.c_void_p(int(stream)) if stream else None))
+
     def snapshot(self):
         self._chk(self._L.owgs_snapshot(self._h))
 

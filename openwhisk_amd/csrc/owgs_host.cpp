@@ -36,6 +36,7 @@ extern "C" hipError_t owgs_launch_relflags(const int64_t* rel_aid, int64_t n_rel
 extern "C" hipError_t owgs_launch_release_seq(const OwgsReleaseArgs* a, hipStream_t s);
 extern "C" size_t owgs_release_scratch_bytes(int32_t n);
 extern "C" hipError_t owgs_launch_engine(const OwgsEngineArgs* a, hipStream_t s);
+extern "C" hipError_t owgs_launch_engine_multi(const OwgsEngineArgs* a, int k, hipStream_t s);
 extern "C" int32_t owgs_coprime_max(void);
 extern "C" hipError_t owgs_launch_coprime(const int32_t* xs, int32_t n_pools, int32_t* out, int32_t out_stride,
                                           int32_t* counts, hipStream_t s);
@@ -393,7 +394,7 @@ static int run_prepass(owgs_ctx* c, OwgsEngineArgs& A, int32_t n_batches, const 
     return OWGS_OK;
 }
 
-static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s) {
+static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s, bool launch = true) {
     int rc = lds_check(c);
     if (rc) return rc;
     // walk cursors: one tagged word per action; the tags of this launch's batches must not repeat a stored tag
@@ -412,6 +413,7 @@ static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s) {
         HIPCHK(c, hipEventCreate(&c->ev_engine[0]));
         HIPCHK(c, hipEventCreate(&c->ev_engine[1]));
     }
+    if (!launch) return OWGS_OK;  // owgs_replay_device_multi launches every shard's engine at once
     HIPCHK(c, hipEventRecord(c->ev_engine[0], s));  // brackets exactly the engine launch (owgs_engine_ms)
     HIPCHK(c, owgs_launch_engine(&A, s));
     HIPCHK(c, hipEventRecord(c->ev_engine[1], s));
@@ -1010,17 +1012,63 @@ int owgs_pairwise_coprime(owgs_ctx* c, int32_t x, int32_t* out, int32_t cap, int
     return OWGS_OK;
 }
 
+static int replay_begin(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const int32_t* act,
+                        int64_t n_activations, const int64_t* rel_off, const int64_t* rel_aid, int64_t n_releases,
+                        uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, uint8_t* rel_flags,
+                        hipStream_t hs, OwgsEngineArgs& A, bool launch);
+
 int owgs_replay_device(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const int32_t* act,
                        int64_t n_activations, const int64_t* rel_off, const int64_t* rel_aid, int64_t n_releases,
                        uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, uint8_t* rel_flags, void* stream) {
+    if (!c) return OWGS_EINVAL;
+    hipStream_t hs = stream ? (hipStream_t)stream : c->stream;
+    OwgsEngineArgs A;
+    int rc = replay_begin(c, n_batches, acq_off, act, n_activations, rel_off, rel_aid, n_releases, seq_base,
+                          out_invoker, out_flags, rel_flags, hs, A, true);
+    if (rc || n_batches == 0) return rc;
+    if (rel_off && rel_flags) HIPCHK(c, owgs_launch_relflags(rel_aid, n_releases, out_invoker, rel_flags, hs));
+    return OWGS_OK;
+}
+
+int owgs_replay_device_multi(owgs_ctx** cs, int32_t k, const owgs_replay_io* io, void* stream) {
+    if (!cs || !io || k < 1 || k > OWGS_MULTI_MAX) return OWGS_EINVAL;
+    for (int32_t i = 0; i < k; ++i) {
+        if (!cs[i]) return OWGS_EINVAL;
+        if (cs[i]->cfg.device != cs[0]->cfg.device) return cs[0]->fail(OWGS_EINVAL, "shards on different devices");
+        for (int32_t j = 0; j < i; ++j)
+            if (cs[j] == cs[i]) return cs[0]->fail(OWGS_EINVAL, "one context twice in a multi-shard replay");
+        if (io[i].n_batches <= 0) return cs[i]->fail(OWGS_EINVAL, "multi-shard replay needs batches in every shard");
+    }
+    hipStream_t hs = stream ? (hipStream_t)stream : cs[0]->stream;
+    OwgsEngineArgs A[OWGS_MULTI_MAX];
+    for (int32_t i = 0; i < k; ++i) {
+        const owgs_replay_io& x = io[i];
+        int rc = replay_begin(cs[i], x.n_batches, x.acq_off, x.act, x.n_activations, x.rel_off, x.rel_aid,
+                              x.n_releases, x.seq_base, x.out_invoker, x.out_flags, x.rel_flags, hs, A[i], false);
+        if (rc) return rc;
+    }
+    for (int32_t i = 0; i < k; ++i) HIPCHK(cs[i], hipEventRecord(cs[i]->ev_engine[0], hs));
+    HIPCHK(cs[0], owgs_launch_engine_multi(A, k, hs));
+    for (int32_t i = 0; i < k; ++i) {
+        HIPCHK(cs[i], hipEventRecord(cs[i]->ev_engine[1], hs));
+        cs[i]->ev_engine_valid = true;
+        const owgs_replay_io& x = io[i];
+        if (x.rel_off && x.rel_flags)
+            HIPCHK(cs[i], owgs_launch_relflags(x.rel_aid, x.n_releases, x.out_invoker, x.rel_flags, hs));
+    }
+    return OWGS_OK;
+}
+
+static int replay_begin(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const int32_t* act,
+                        int64_t n_activations, const int64_t* rel_off, const int64_t* rel_aid, int64_t n_releases,
+                        uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, uint8_t* rel_flags,
+                        hipStream_t hs, OwgsEngineArgs& A, bool launch) {
     if (!c || n_batches < 0 || !acq_off || !act || !out_invoker || !out_flags || n_activations < 0 ||
         n_activations >= ((int64_t)1 << 31) || n_releases < 0 || (n_releases > 0 && (!rel_off || !rel_aid)))
         return OWGS_EINVAL;
     if (n_batches == 0) return OWGS_OK;
     if (c->a_mem.empty()) return c->fail(OWGS_ENOENT, "no actions registered");
     (void)hipSetDevice(c->cfg.device);
-    hipStream_t hs = stream ? (hipStream_t)stream : c->stream;
-    OwgsEngineArgs A;
     base_args(c, A);
     A.seq_base = seq_base;
     A.out_inv = out_invoker;
@@ -1050,10 +1098,7 @@ int owgs_replay_device(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, c
         A.acc = c->d_acc.p;
         A.acc_stride = stride;
     }
-    rc = run_engine(c, A, hs);
-    if (rc) return rc;
-    if (rel_off && rel_flags) HIPCHK(c, owgs_launch_relflags(rel_aid, n_releases, out_invoker, rel_flags, hs));
-    return OWGS_OK;
+    return run_engine(c, A, hs, launch);
 }
 
 int owgs_replay(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const int32_t* act, const int64_t* rel_off,

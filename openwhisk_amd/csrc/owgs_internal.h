@@ -112,6 +112,8 @@
 #define OWGS_ST_CHUNKS 4
 #define OWGS_ST_STOPS 5
 
+#define OWGS_MULTI_MAX 8  // controller shards per owgs_engine_multi_kernel launch (kernarg: 8 x args)
+
 struct OwgsEngineArgs {
     int32_t* permits;
     int32_t n_slots;

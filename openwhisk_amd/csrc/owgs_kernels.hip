@@ -900,7 +900,7 @@ __device__ __forceinline__ void lds_sync() {
 #define TRACE_MARK(id)
 #endif
 
-__global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs A) {
+__device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     extern __shared__ uint4 lds_raw[];
     char* L = (char*)lds_raw;
     const OwgsLayout Y = owgs_layout(A.n_slots, A.pool_mode, A.n_ids, A.nm, A.nb, A.n_actions);
@@ -2059,6 +2059,17 @@ __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs 
     }
 }
 
+__global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs A) { owgs_engine_body(A); }
+
+// several controller shards in one launch: workgroup k replays shard k (its own LDS image, state and stream); the
+// arguments stay in the kernarg segment, so every field is still a scalar load
+struct OwgsEngineMulti {
+    OwgsEngineArgs a[OWGS_MULTI_MAX];
+};
+__global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_multi_kernel(OwgsEngineMulti M) {
+    owgs_engine_body(M.a[blockIdx.x]);
+}
+
 // ------------------------------------------------------------------------------------------------ explicit releases
 // owgs_release_batch: releases in stream order, 64 at a time.  maxConcurrent == 1: FS.release (FS:117-120) with the
 // overflow Error leaving the state unchanged; concurrent: RS.release(1, true) applied rank+1 times inside each group
@@ -2375,6 +2386,27 @@ extern "C" hipError_t owgs_launch_release_seq(const OwgsReleaseArgs* a, hipStrea
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(owgs_release_seq_kernel, dim3(1), dim3(64), 0, s, *a);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t owgs_launch_engine_multi(const OwgsEngineArgs* a, int k, hipStream_t s) {
+    if (k < 1 || k > OWGS_MULTI_MAX) return hipErrorInvalidValue;
+    size_t lds = 0;
+    OwgsEngineMulti M;
+    for (int i = 0; i < k; ++i) {
+        lds = std::max(lds, owgs_engine_lds_bytes(a[i].n_slots, a[i].pool_mode, a[i].n_ids, a[i].nm, a[i].nb,
+                                                  a[i].n_actions));
+        M.a[i] = a[i];
+    }
+    if (lds > OWGS_LDS_BYTES) return hipErrorInvalidValue;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)owgs_engine_multi_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, OWGS_LDS_BYTES);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(owgs_engine_multi_kernel, dim3(k), dim3(OWGS_NT), lds, s, M);
     return hipGetLastError();
 }
 

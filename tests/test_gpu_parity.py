@@ -337,3 +337,39 @@ def test_update_invokers_and_cluster_on_device_match_oracle(seed):
             b.update_cluster(size)
             o.update_cluster(size)
             assert np.array_equal(b.permits(), o.permits()), (n, size)
+
+
+def test_multi_shard_single_launch_parity():
+    # owgs_replay_device_multi: 3 controller shards of a 4-controller cluster in ONE engine launch (one workgroup
+    # each), every shard bit-exact with its own oracle replay; a second launch after restore repeats the results
+    import torch
+
+    dev = torch.device("cuda", 0)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
+    shards = []
+    for g in (0, 1, 3):
+        w = W.config("headline", shard=g, n_shards=4, n_activations=150_000)
+        b = gpu_for(w)
+        b.snapshot()
+        s = w.stream
+        d = [t(s.acq_off, np.int64), t(s.act, np.int32), t(s.rel_off, np.int64),
+             t(s.rel_aid if len(s.rel_aid) else np.zeros(1), np.int64),
+             torch.empty(len(s.act), dtype=torch.int32, device=dev),
+             torch.empty(len(s.act), dtype=torch.uint8, device=dev),
+             torch.empty(max(len(s.rel_aid), 1), dtype=torch.uint8, device=dev)]
+        io = (s.n_batches, d[0].data_ptr(), d[1].data_ptr(), len(s.act), d[2].data_ptr(), d[3].data_ptr(),
+              len(s.rel_aid), s.seq_base, d[4].data_ptr(), d[5].data_ptr(), d[6].data_ptr())
+        shards.append((w, b, d, io))
+    for rep in range(2):
+        for _, b, _, _ in shards:
+            b.restore()
+        torch.cuda.synchronize()
+        GpuShardingContainerPoolBalancer.replay_device_multi([(b, io) for _, b, _, io in shards])
+        torch.cuda.synchronize()
+        for w, b, d, _ in shards:
+            st = O.state_for(w)
+            o_inv, o_fl, o_rf = st.replay(w.stream)
+            assert np.array_equal(o_inv, d[4].cpu().numpy()), (rep, w.name)
+            assert np.array_equal(o_fl, d[5].cpu().numpy())
+            assert np.array_equal(o_rf, d[6].cpu().numpy()[: len(o_rf)])
+            assert np.array_equal(st.permits(), b.permits())
