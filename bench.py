@@ -23,6 +23,7 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
+MULTI_MAX = 8  # controller shards per owgs_replay_device_multi launch (OWGS_MULTI_MAX)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # HBM bytes of one owgs_engine_kernel launch on the headline config (1M activations), from separate rocprofv3 --pmc
 # passes over `bench.py --steps 5` (tools/pmc_run.sh; summary committed as profiles/r01_v8_pmc.txt): FETCH_SIZE
@@ -46,8 +47,8 @@ def parse():
                     help="headline invoker memory: 'weak' = 16 GiB x clusterSize, so every controller shard's 1/N slot "
                          "(SCPB:485-499) is 16 GiB at every N; 'split' = 16 GiB invokers split N ways")
     ap.add_argument("--shards-per-gpu", type=int, default=1,
-                    help="controller shards hosted per GPU (clusterSize = gpus x this, at most 8), replayed by one "
-                         "engine launch with one workgroup per shard")
+                    help="controller shards hosted per GPU (clusterSize = gpus x this), replayed by engine launches of "
+                         "up to 8 shards (one workgroup each), one HIP stream per launch")
     return ap.parse_args()
 
 
@@ -141,7 +142,7 @@ def main():
     class Shard:
         """One controller shard: its own balancer context, stream buffers in HBM and HIP stream."""
 
-        def __init__(self, idx):
+        def __init__(self, idx, own_stream):
             kw = {}
             if args.slots == "weak" and args.config == "headline" and n_ctl > 1:
                 kw["user_memory_mb"] = 16_384 * n_ctl
@@ -160,8 +161,11 @@ def main():
             self.d_out = torch.empty(len(s.act), dtype=torch.int32, device=dev)
             self.d_fl = torch.empty(len(s.act), dtype=torch.uint8, device=dev)
             self.d_rf = torch.empty(max(len(s.rel_aid), 1), dtype=torch.uint8, device=dev)
-            self.stream = torch.cuda.Stream()  # a real (non-null) HIP stream: engine and timing events share it
-            self.sp = self.stream.cuda_stream
+            # a real (non-null) HIP stream: engine and timing events share it.  Only the first shard of each
+            # launch group gets one: HIP maps streams round-robin onto few hardware queues, and two group streams
+            # on one queue would serialise their launches
+            self.stream = torch.cuda.Stream() if own_stream else None
+            self.sp = self.stream.cuda_stream if own_stream else None
 
         def io(self):
             s = self.s
@@ -176,7 +180,7 @@ def main():
                                  self.d_rel.data_ptr(), self.d_aid.data_ptr(), len(s.rel_aid), s.seq_base,
                                  self.d_out.data_ptr(), self.d_fl.data_ptr(), self.d_rf.data_ptr(), self.sp)
 
-    shards = [Shard(rank * K + k) for k in range(K)]
+    shards = [Shard(rank * K + k, k % MULTI_MAX == 0) for k in range(K)]
     w, s, b = shards[0].w, shards[0].s, shards[0].b
     hx = cluster.HealthExchange(dist, torch.from_numpy(w.inv_status.copy()).to(dev), world)
     torch.cuda.synchronize()
@@ -185,13 +189,20 @@ def main():
     sp = stream.cuda_stream
 
     def launch_all():
-        if K > 1:  # every shard of this GPU in ONE engine launch (one workgroup each) on one stream
+        if K > 1:  # groups of up to 8 shards, each group ONE engine launch (one workgroup per shard) on its stream
             h = hx.exchange() if world > 1 else None
-            for sh in shards:
-                if h is not None:
-                    sh.b.update_health_device(len(w.inv_status), h.data_ptr(), sp)
-                sh.b.restore(sp)
-            GpuShardingContainerPoolBalancer.replay_device_multi([(sh.b, sh.io()) for sh in shards], sp)
+            groups = [shards[j:j + MULTI_MAX] for j in range(0, K, MULTI_MAX)]
+            for grp in groups:
+                gs = grp[0].stream
+                if gs is not stream:
+                    gs.wait_stream(stream)
+                for sh in grp:
+                    if h is not None:
+                        sh.b.update_health_device(len(w.inv_status), h.data_ptr(), gs.cuda_stream)
+                    sh.b.restore(gs.cuda_stream)
+                GpuShardingContainerPoolBalancer.replay_device_multi([(sh.b, sh.io()) for sh in grp], gs.cuda_stream)
+            for grp in groups[1:]:
+                stream.wait_stream(grp[0].stream)
             return
         if world > 1:
             h = hx.exchange()  # on shards[0]'s stream; the other shards' streams wait for it

@@ -5,7 +5,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -1 gpurun_out/pytest_gpu3.log
 timeout -k 10 300 python bench.py > gpurun_out/b1.log 2>&1 || { tail gpurun_out/b1.log; exit 1; }
 tail -1 gpurun_out/b1.log | cut -c1-300
-for k in 2 4 8; do
+for k in ${KS:-2 4 8}; do
 timeout -k 10 200 python bench.py --no-cpu-baseline --shards-per-gpu $k > gpurun_out/bk$k.log 2>&1 || { tail gpurun_out/bk$k.log; exit 1; }
 tail -1 gpurun_out/bk$k.log | cut -c1-300; done
 rm -rf gpurun_out/prof
