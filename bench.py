@@ -23,7 +23,7 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
-MULTI_MAX = 8  # controller shards per owgs_replay_device_multi launch (OWGS_MULTI_MAX)
+MULTI_MAX = 64  # controller shards per owgs_replay_device_multi launch (OWGS_MULTI_DEV_MAX)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # HBM bytes of one owgs_engine_kernel launch on the headline config (1M activations), from separate rocprofv3 --pmc
 # passes over `bench.py --steps 5` (tools/pmc_run.sh; summary committed as profiles/r01_v8_pmc.txt): FETCH_SIZE

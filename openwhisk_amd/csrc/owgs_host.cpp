@@ -37,6 +37,8 @@ extern "C" hipError_t owgs_launch_release_seq(const OwgsReleaseArgs* a, hipStrea
 extern "C" size_t owgs_release_scratch_bytes(int32_t n);
 extern "C" hipError_t owgs_launch_engine(const OwgsEngineArgs* a, hipStream_t s);
 extern "C" hipError_t owgs_launch_engine_multi(const OwgsEngineArgs* a, int k, hipStream_t s);
+extern "C" hipError_t owgs_launch_engine_multi_dev(const OwgsEngineArgs* a_host, const OwgsEngineArgs* a_dev, int k,
+                                                   hipStream_t s);
 extern "C" int32_t owgs_coprime_max(void);
 extern "C" hipError_t owgs_launch_coprime(const int32_t* xs, int32_t n_pools, int32_t* out, int32_t out_stride,
                                           int32_t* counts, hipStream_t s);
@@ -142,6 +144,7 @@ struct owgs_ctx {
     DevBuf<uint8_t> d_act_bb, d_act_cok;
     DevBuf<uint2> d_act_meta;
     DevBuf<u64> d_stats;
+    DevBuf<uint32_t> d_margs;  // owgs_replay_device_multi: shard argument blocks beyond the kernarg segment
     // per-call scratch
     DevBuf<int64_t> d_off;
     DevBuf<int32_t> d_a, d_b, d_c, d_d, d_out, d_cstart, d_relx, d_cpos, d_bsum, d_crel_off, d_acc, d_xslot;
@@ -527,6 +530,7 @@ void owgs_destroy(owgs_ctx* c) {
     c->d_act_cok.release();
     c->d_act_meta.release();
     c->d_stats.release();
+    c->d_margs.release();
     c->d_off.release();
     c->d_flags.release();
     c->d_rflags.release();
@@ -1031,7 +1035,7 @@ int owgs_replay_device(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, c
 }
 
 int owgs_replay_device_multi(owgs_ctx** cs, int32_t k, const owgs_replay_io* io, void* stream) {
-    if (!cs || !io || k < 1 || k > OWGS_MULTI_MAX) return OWGS_EINVAL;
+    if (!cs || !io || k < 1 || k > OWGS_MULTI_DEV_MAX) return OWGS_EINVAL;
     for (int32_t i = 0; i < k; ++i) {
         if (!cs[i]) return OWGS_EINVAL;
         if (cs[i]->cfg.device != cs[0]->cfg.device) return cs[0]->fail(OWGS_EINVAL, "shards on different devices");
@@ -1040,15 +1044,23 @@ int owgs_replay_device_multi(owgs_ctx** cs, int32_t k, const owgs_replay_io* io,
         if (io[i].n_batches <= 0) return cs[i]->fail(OWGS_EINVAL, "multi-shard replay needs batches in every shard");
     }
     hipStream_t hs = stream ? (hipStream_t)stream : cs[0]->stream;
-    OwgsEngineArgs A[OWGS_MULTI_MAX];
+    std::vector<OwgsEngineArgs> A((size_t)k);
     for (int32_t i = 0; i < k; ++i) {
         const owgs_replay_io& x = io[i];
         int rc = replay_begin(cs[i], x.n_batches, x.acq_off, x.act, x.n_activations, x.rel_off, x.rel_aid,
-                              x.n_releases, x.seq_base, x.out_invoker, x.out_flags, x.rel_flags, hs, A[i], false);
+                              x.n_releases, x.seq_base, x.out_invoker, x.out_flags, x.rel_flags, hs, A[(size_t)i], false);
         if (rc) return rc;
     }
     for (int32_t i = 0; i < k; ++i) HIPCHK(cs[i], hipEventRecord(cs[i]->ev_engine[0], hs));
-    HIPCHK(cs[0], owgs_launch_engine_multi(A, k, hs));
+    if (k <= OWGS_MULTI_MAX) {
+        HIPCHK(cs[0], owgs_launch_engine_multi(A.data(), k, hs));
+    } else {  // argument blocks through HBM (the context's buffer; ordered on hs before the launch)
+        owgs_ctx* c0 = cs[0];
+        const size_t words = ((size_t)k * sizeof(OwgsEngineArgs) + 3) / 4;
+        HIPCHK(c0, c0->d_margs.reserve(words));
+        HIPCHK(c0, hipMemcpyAsync(c0->d_margs.p, A.data(), (size_t)k * sizeof(OwgsEngineArgs), hipMemcpyHostToDevice, hs));
+        HIPCHK(c0, owgs_launch_engine_multi_dev(A.data(), (const OwgsEngineArgs*)c0->d_margs.p, k, hs));
+    }
     for (int32_t i = 0; i < k; ++i) {
         HIPCHK(cs[i], hipEventRecord(cs[i]->ev_engine[1], hs));
         cs[i]->ev_engine_valid = true;

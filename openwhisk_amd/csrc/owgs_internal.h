@@ -113,6 +113,7 @@
 #define OWGS_ST_STOPS 5
 
 #define OWGS_MULTI_MAX 8  // controller shards per owgs_engine_multi_kernel launch (kernarg: 8 x args)
+#define OWGS_MULTI_DEV_MAX 64  // owgs_engine_multi_dev_kernel: argument blocks in HBM
 
 struct OwgsEngineArgs {
     int32_t* permits;

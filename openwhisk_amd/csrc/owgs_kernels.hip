@@ -2069,6 +2069,10 @@ struct OwgsEngineMulti {
 __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_multi_kernel(OwgsEngineMulti M) {
     owgs_engine_body(M.a[blockIdx.x]);
 }
+// more shards than the kernarg segment holds: the argument blocks in HBM (uniform per workgroup, read-only)
+__global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_multi_dev_kernel(const OwgsEngineArgs* __restrict__ As) {
+    owgs_engine_body(As[blockIdx.x]);
+}
 
 // ------------------------------------------------------------------------------------------------ explicit releases
 // owgs_release_batch: releases in stream order, 64 at a time.  maxConcurrent == 1: FS.release (FS:117-120) with the
@@ -2386,6 +2390,25 @@ extern "C" hipError_t owgs_launch_release_seq(const OwgsReleaseArgs* a, hipStrea
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(owgs_release_seq_kernel, dim3(1), dim3(64), 0, s, *a);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t owgs_launch_engine_multi_dev(const OwgsEngineArgs* a_host, const OwgsEngineArgs* a_dev, int k,
+                                                   hipStream_t s) {
+    if (k < 1 || k > OWGS_MULTI_DEV_MAX) return hipErrorInvalidValue;
+    size_t lds = 0;
+    for (int i = 0; i < k; ++i)
+        lds = std::max(lds, owgs_engine_lds_bytes(a_host[i].n_slots, a_host[i].pool_mode, a_host[i].n_ids,
+                                                  a_host[i].nm, a_host[i].nb, a_host[i].n_actions));
+    if (lds > OWGS_LDS_BYTES) return hipErrorInvalidValue;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)owgs_engine_multi_dev_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, OWGS_LDS_BYTES);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(owgs_engine_multi_dev_kernel, dim3(k), dim3(OWGS_NT), lds, s, a_dev);
     return hipGetLastError();
 }
 
