@@ -1,20 +1,29 @@
 #!/usr/bin/env python3
 """Benchmark: bit-exact scheduling decisions/s of ShardingContainerPoolBalancer.schedule() semantics on MI355X.
 
-One step = one replay of a controller shard's activation stream (1M activations in capacity-calibrated batches,
-each batch = completion releases then publishes; workload.py "headline": 10k invokers, Zipf actions, 128..2048 MB,
-concurrent + blackbox actions, 2 % unhealthy).  Inputs are resident in HBM before the timed region; the slot state is
-restored before every step (included in the timed region).  N GPUs = N controller shards (clusterSize = N, one stream
-each, weak scaling, no data-path collective; by default invoker memory is 16 GiB x N so each shard's 1/N slot stays
-16 GiB -- `--slots split` keeps 16 GiB invokers split N ways); for N > 1 the invoker health vector is all-gathered over RCCL once per
-step (the reference's controllers all consume the same health topic, SCPB:355).
+One step = one replay of every controller shard's activation stream on its GPU (1M activations per shard in
+capacity-calibrated batches; each batch = completion releases then publishes; workload.py).  Inputs are resident in
+HBM before the timed region; the slot state is restored before every step (inside the timed region).
 
-Prints ONE JSON line on rank 0.  The value counts only when every rank's assignment vector is bit-exact with the
-CPU oracle (checked after timing).
+Multi-GPU (BASELINE configs[4]): N GPUs = N controllers of one cluster (clusterSize = N x shards-per-GPU), one
+process per GPU, each shard its own stream.  Slots are split: every invoker keeps 16 GiB of user memory and each
+controller's slot holds 1/clusterSize of it (getInvokerSlot, SCPB:485-499) -- "10k invokers' slots split 1/8 per GPU".
+The controllers exchange no scheduling state (SCPB:126-133), so the data path has no collective ("scaling": "weak":
+each shard's stream is fixed at 1M activations); the invoker health vector is all-gathered over RCCL once per step
+(every controller consumes the same health topic, SCPB:355).
+
+`python bench.py --gpus N` with no torch.distributed environment starts the N ranks itself (torch.distributed.run as
+a child process, before this process touches any GPU); the driver may also launch it under torch.distributed.run.
+
+Prints ONE JSON line on rank 0.  The value counts only when every rank's assignment vector, flags and final permits
+are bit-exact with the CPU oracle (checked after timing).
 """
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -24,104 +33,212 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 MULTI_MAX = 64  # controller shards per owgs_replay_device_multi launch (OWGS_MULTI_DEV_MAX)
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-# HBM bytes of one owgs_engine_kernel launch on the headline config (1M activations), from separate rocprofv3 --pmc
-# passes over `bench.py --steps 5` (tools/pmc_run.sh; summary committed as profiles/r01_v8_pmc.txt): FETCH_SIZE
-# 12,920 KiB doubled for gfx950's half-counted 16 B/lane streaming reads (the engine reads by LDS-DMA dwordx4) +
-# WRITE_SIZE 26,210 KiB.  Counters cannot be read live inside the timed run, so this is the profiled value of the
-# same engine build; other configs report null.
-ENGINE_PMC_TRAFFIC = {"bytes": (2 * 12920 + 26210) * 1024, "source": "profiles/r01_v8_pmc.txt (FETCH_SIZE x2 + WRITE_SIZE)"}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md, chip-level parameters)
+# algorithmic HBM bytes of the path
+B_DECISION = 28  # activation record 8 + hash 4 + step 4 + permit read 4 + permit write 4 + decision 4
+B_RELEASE = 20   # release record 8 + invoker 4 + permit read-modify-write 8
+PMC_FILE = os.path.join(ROOT, "pmc_traffic.json")  # tools/pmc_traffic.py (rocprofv3 --pmc), per libowgs.so build
+LIB = os.path.join(ROOT, "openwhisk_amd", "libowgs.so")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="headline")
-    ap.add_argument("--n-activations", type=int, default=1_000_000)
+    ap.add_argument("--config", default="headline", help="headline (= c5 shards for N > 1) | c1 | c2 | c3 | c4")
+    ap.add_argument("--n-activations", type=int, default=None, help="per shard (default: the config's, 1M)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--no-h2d", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--slots", choices=("weak", "split"), default="weak",
-                    help="headline invoker memory: 'weak' = 16 GiB x clusterSize, so every controller shard's 1/N slot "
-                         "(SCPB:485-499) is 16 GiB at every N; 'split' = 16 GiB invokers split N ways")
+    ap.add_argument("--slots", choices=("split", "weak"), default="split",
+                    help="'split' (default): 16 GiB invokers, each controller's slot = 1/clusterSize of them "
+                         "(configs[4]); 'weak': invoker memory 16 GiB x clusterSize so every slot stays 16 GiB")
     ap.add_argument("--shards-per-gpu", type=int, default=1,
-                    help="controller shards hosted per GPU (clusterSize = gpus x this), replayed by engine launches of "
-                         "up to 8 shards (one workgroup each), one HIP stream per launch")
-    return ap.parse_args()
+                    help="controller shards hosted per GPU (clusterSize = gpus x this), replayed by engine launches "
+                         "of up to 64 shards (one workgroup each; 8 argument blocks in the kernarg segment, more in HBM)")
+    ap.add_argument("--cluster-size", type=int, default=0,
+                    help="single-GPU measurement of one shard of a larger cluster: clusterSize (default gpus x "
+                         "shards-per-gpu)")
+    ap.add_argument("--shard", type=int, default=0, help="with --cluster-size: which controller shard this GPU runs")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher/collective plumbing only (gloo, CPU): no replay, value null (tests)")
+    return ap.parse_args(argv)
 
 
-def algorithmic_bytes(w) -> int:
-    """Minimum HBM bytes one replay must move: stream in/out once, action table and slot state once."""
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """`--gpus N` without a torch.distributed environment: run N ranks under torch.distributed.run as a CHILD
+    process (this process has not touched a GPU) and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4"))
+    return subprocess.call(cmd, env=env)
+
+
+def cluster_geometry(args, rank: int, world: int):
+    """(clusterSize, controller shard indices this rank replays)."""
+    K = max(1, args.shards_per_gpu)
+    n_ctl = args.cluster_size if args.cluster_size > 0 else world * K
+    base = args.shard if (args.cluster_size > 0 and world == 1) else rank * K
+    if base + K > n_ctl:
+        raise SystemExit(f"shards {base}..{base + K - 1} outside a {n_ctl}-controller cluster")
+    return n_ctl, [base + k for k in range(K)]
+
+
+def shard_workload(args, idx: int, n_ctl: int):
+    """The stream and cluster of controller shard `idx` of `n_ctl` (workload.py; configs[4] for N > 1)."""
+    from openwhisk_amd import cluster
+
+    kw = {}
+    if args.slots == "weak" and n_ctl > 1:
+        kw["user_memory_mb"] = 16_384 * n_ctl
+    return cluster.shard_workload(args.config, idx, n_ctl, n_activations=args.n_activations, **kw)
+
+
+def algorithmic_bytes(w) -> dict:
+    """Algorithmic HBM bytes of one shard's replay: SURVEY 8(d) (28 B per decision + 20 B per release) and the
+    narrower stream-only count (decision in/out, release in/out, action table and slot state once)."""
     s = w.stream
     n, r = len(s.act), len(s.rel_aid)
     n_slots = len(w.inv_ids)
-    per_act = 4 + 4 + 1             # action id in, invoker out, flags out
-    per_rel = 8 + 4 + 4 + 1         # release id in, its invoker and action (gathered), release flag out
-    table = len(w.actions) * (16 + 4)  # {home, step, mem, meta} + slot key
-    state = n_slots * 4 * 2 + (w.inv_ids.size + 64) * 4  # permits load + store, pool words
-    offs = (s.n_batches + 1) * 16
-    return n * per_act + r * per_rel + table + state + offs
+    stream = (n * (4 + 4 + 1) + r * (8 + 4 + 4 + 1) + len(w.actions) * (16 + 4) + n_slots * 4 * 2
+              + (w.inv_ids.size + 64) * 4 + (s.n_batches + 1) * 16)
+    return {"survey": n * B_DECISION + r * B_RELEASE, "stream": stream}
 
 
-def _oracle_replay(args, world, shards, reps=1):
-    """Replay `shards` independent shard streams of the bench config on len(shards) host threads, `reps` times;
-    returns (decisions, seconds)."""
+def lib_sha() -> str:
+    try:
+        with open(LIB, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return "missing"
+
+
+def pmc_traffic(key: str):
+    """HBM bytes per engine launch from a rocprofv3 --pmc pass of THIS build (same libowgs.so sha) on this workload,
+    or None.  Counters cannot be read inside the timed run; tools/pmc_traffic.py records them per build."""
+    try:
+        d = json.load(open(PMC_FILE))
+    except (OSError, ValueError):
+        return None
+    e = d.get(key)
+    return e if e and e.get("lib_sha") == lib_sha() else None
+
+
+def _oracle_replay(ws, reps=1):
+    """Replay the shards `ws` on len(ws) host threads (one shard each), `reps` times; returns (decisions, s)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ctypes as C
 
     import oracle as O
-    from openwhisk_amd import workload as W
 
-    ws = [W.config(args.config, n_activations=args.n_activations, shard=t, n_shards=world) for t in shards]
-    s0 = ws[0].stream  # owo_replay_parallel needs one batch structure: shard 0's offsets for every thread
     acts = [np.ascontiguousarray(w.stream.act, dtype=np.int32) for w in ws]
-    acq = np.ascontiguousarray(s0.acq_off, dtype=np.int64)
-    rel = np.ascontiguousarray(s0.rel_off, dtype=np.int64)
-    aid = np.ascontiguousarray(s0.rel_aid, dtype=np.int64)
+    acqs = [np.ascontiguousarray(w.stream.acq_off, dtype=np.int64) for w in ws]
+    rels = [np.ascontiguousarray(w.stream.rel_off, dtype=np.int64) for w in ws]
+    aids = [np.ascontiguousarray(w.stream.rel_aid, dtype=np.int64) for w in ws]
     P = C.c_void_p
-    arr = lambda xs: (P * len(xs))(*[x.ctypes.data_as(P) for x in xs])  # noqa: E731
     total, dt = 0, 0.0
     for _ in range(reps):
         sts = [O.state_for(w) for w in ws]  # fresh slot state each repeat (outside the timed region)
         outs = [np.zeros(len(a), dtype=np.int32) for a in acts]
         fls = [np.zeros(len(a), dtype=np.uint8) for a in acts]
-        sarr = (P * len(sts))(*[st.h for st in sts])
         t0 = time.perf_counter()
-        O.lib().owo_replay_parallel(sarr, len(sts), len(acq) - 1, acq.ctypes.data_as(P), arr(acts),
-                                    rel.ctypes.data_as(P), aid.ctypes.data_as(P), 0, arr(outs), arr(fls), None)
+        if len(ws) == 1:
+            s = ws[0].stream
+            O.lib().owo_replay(sts[0].h, s.n_batches, acqs[0].ctypes.data_as(P), acts[0].ctypes.data_as(P),
+                               rels[0].ctypes.data_as(P), aids[0].ctypes.data_as(P), C.c_uint64(s.seq_base),
+                               outs[0].ctypes.data_as(P), fls[0].ctypes.data_as(P), None)
+        else:
+            import threading
+
+            def run(k):
+                s = ws[k].stream
+                O.lib().owo_replay(sts[k].h, s.n_batches, acqs[k].ctypes.data_as(P), acts[k].ctypes.data_as(P),
+                                   rels[k].ctypes.data_as(P), aids[k].ctypes.data_as(P), C.c_uint64(s.seq_base),
+                                   outs[k].ctypes.data_as(P), fls[k].ctypes.data_as(P), None)
+
+            th = [threading.Thread(target=run, args=(k,)) for k in range(len(ws))]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
         dt += time.perf_counter() - t0
         total += sum(len(a) for a in acts)
     return total, dt
 
 
-def cpu_baseline(args, world):
+def cpu_baseline(args, w0, n_ctl, shard0):
     """The oracle (a literal C port of the reference schedule()/release path) replaying the bench's own shard stream
-    on ONE host core -- one controller's schedule() is single-threaded in the reference (SCPB:257-317 runs on the
-    balancer's actor) and the stream is sequential, so this is the same workload on the CPU.  Repeated to ~5 s.
-    `parallel` adds the aggregate of T cores replaying T independent shard streams (T controllers on one host)."""
-    n1, t1 = _oracle_replay(args, world, [0], reps=1)
-    reps = max(1, min(12, int(5.0 / max(t1, 1e-3))))
-    n, dt = _oracle_replay(args, world, [0], reps=reps)
+    on ONE host core -- one controller's schedule() runs on one thread in the reference (the balancer actor) and the
+    stream is sequential -- repeated to ~10 s.  `parallel` adds T cores replaying T independent shards of the same
+    cluster (T controllers on one host)."""
+    n1, t1 = _oracle_replay([w0], reps=1)
+    reps = max(1, min(20, int(10.0 / max(t1, 1e-3))))
+    n, dt = _oracle_replay([w0], reps=reps)
     out = {"value": n / dt, "unit": "decisions/s", "cores": 1, "kind": "port",
-           "sample": f"the bench's {args.config} shard stream ({args.n_activations} activations) replayed "
-                     f"{reps}x on 1 core (oracle/owsched_oracle.c, -O3), {dt:.2f} s"}
+           "sample": f"shard {shard0} of {n_ctl} of the bench's {args.config} workload ({len(w0.stream.act)} "
+                     f"activations) replayed {reps}x on 1 core (oracle/owsched_oracle.c, -O3), {dt:.2f} s"}
     T = max(1, min(args.cpu_threads, os.cpu_count() or 1))
     if T > 1:
-        nt, dtt = _oracle_replay(args, world, list(range(T)), reps=1)
+        ws = [shard_workload(args, t % max(n_ctl, 1), max(n_ctl, 1)) if n_ctl > 1 else
+              shard_workload(args, 0, 1) for t in range(T)]
+        nt, dtt = _oracle_replay(ws, reps=1)
         out["parallel"] = {"value": nt / dtt, "unit": "decisions/s", "cores": T,
-                           "sample": f"{T} threads x an independent {args.config} shard stream each, {dtt:.2f} s wall"}
+                           "sample": f"{T} threads, one shard stream each, {dtt:.2f} s wall"}
     return out
+
+
+def dry_run(args):
+    """Launcher + collective plumbing on the CPU (gloo): every rank builds its shard, the ranks all-gather health and
+    reduce step times exactly as the GPU path does; no replay, value null."""
+    import torch
+    import torch.distributed as dist
+
+    from openwhisk_amd import cluster
+
+    rank, world, _ = cluster.env_rank()
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+    else:
+        dist = None
+    n_ctl, shards = cluster_geometry(args, rank, world)
+    ws = [shard_workload(args, g, n_ctl) for g in shards]
+    hx = cluster.HealthExchange(dist, torch.from_numpy(ws[0].inv_status.copy()), world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        hx.exchange()
+    t_step = (time.perf_counter() - t0) / max(args.steps, 1)
+    t_step, = cluster.max_over_ranks(dist, [t_step], torch.device("cpu"))
+    if rank == 0:
+        print(json.dumps({"metric": "dry run", "value": None, "n_gpus": world, "dry_run": True,
+                          "config": {"workload": args.config, "cluster_size": n_ctl, "slots": args.slots,
+                                     "slot_mb": int(ws[0].info["slot_mb"]), "shards": shards,
+                                     "health_disagree": hx.disagreeing_ranks(), "ms_per_step": t_step * 1e3}}),
+              flush=True)
+    if dist:
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))  # before anything touches a GPU
+    if args.dry_run:
+        return dry_run(args)
     import torch
 
     from openwhisk_amd import cluster
 
     rank, world, local = cluster.env_rank()
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
     dist = None
     if world > 1:
@@ -135,18 +252,16 @@ def main():
 
     from openwhisk_amd import GpuShardingContainerPoolBalancer
 
-    K = max(1, args.shards_per_gpu)
-    n_ctl = world * K  # controllers in the cluster: rank r hosts shards r*K .. r*K+K-1
+    n_ctl, shard_ids = cluster_geometry(args, rank, world)
+    K = len(shard_ids)
     t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
 
     class Shard:
         """One controller shard: its own balancer context, stream buffers in HBM and HIP stream."""
 
         def __init__(self, idx, own_stream):
-            kw = {}
-            if args.slots == "weak" and args.config == "headline" and n_ctl > 1:
-                kw["user_memory_mb"] = 16_384 * n_ctl
-            self.w = w = cluster.shard_workload(args.config, idx, n_ctl, n_activations=args.n_activations, **kw)
+            self.idx = idx
+            self.w = w = shard_workload(args, idx, n_ctl)
             self.b = b = GpuShardingContainerPoolBalancer(
                 managed_fraction=w.managed_fraction, blackbox_fraction=w.blackbox_fraction, rng_seed=w.rng_seed,
                 device=torch.cuda.current_device())
@@ -162,8 +277,7 @@ def main():
             self.d_fl = torch.empty(len(s.act), dtype=torch.uint8, device=dev)
             self.d_rf = torch.empty(max(len(s.rel_aid), 1), dtype=torch.uint8, device=dev)
             # a real (non-null) HIP stream: engine and timing events share it.  Only the first shard of each
-            # launch group gets one: HIP maps streams round-robin onto few hardware queues, and two group streams
-            # on one queue would serialise their launches
+            # launch group gets one (HIP maps streams round-robin onto few hardware queues)
             self.stream = torch.cuda.Stream() if own_stream else None
             self.sp = self.stream.cuda_stream if own_stream else None
 
@@ -180,17 +294,20 @@ def main():
                                  self.d_rel.data_ptr(), self.d_aid.data_ptr(), len(s.rel_aid), s.seq_base,
                                  self.d_out.data_ptr(), self.d_fl.data_ptr(), self.d_rf.data_ptr(), self.sp)
 
-    shards = [Shard(rank * K + k, k % MULTI_MAX == 0) for k in range(K)]
+    shards = [Shard(g, k % MULTI_MAX == 0) for k, g in enumerate(shard_ids)]
     w, s, b = shards[0].w, shards[0].s, shards[0].b
     hx = cluster.HealthExchange(dist, torch.from_numpy(w.inv_status.copy()).to(dev), world)
     torch.cuda.synchronize()
     stream = shards[0].stream
     torch.cuda.set_stream(stream)
-    sp = stream.cuda_stream
+    n_gathers = [0]
 
     def launch_all():
-        if K > 1:  # groups of up to 8 shards, each group ONE engine launch (one workgroup per shard) on its stream
-            h = hx.exchange() if world > 1 else None
+        h = None
+        if world > 1:  # the health topic every controller consumes (SCPB:355): one all-gather per step
+            h = hx.exchange()
+            n_gathers[0] += 1
+        if K > 1:  # groups of up to 64 shards, each group ONE engine launch (one workgroup per shard) on its stream
             groups = [shards[j:j + MULTI_MAX] for j in range(0, K, MULTI_MAX)]
             for grp in groups:
                 gs = grp[0].stream
@@ -204,16 +321,9 @@ def main():
             for grp in groups[1:]:
                 stream.wait_stream(grp[0].stream)
             return
-        if world > 1:
-            h = hx.exchange()  # on shards[0]'s stream; the other shards' streams wait for it
-            for sh in shards:
-                if sh is not shards[0]:
-                    sh.stream.wait_stream(stream)
-                sh.b.update_health_device(len(w.inv_status), h.data_ptr(), sh.sp)
-        for sh in shards:
-            sh.replay()
-        for sh in shards[1:]:
-            stream.wait_stream(sh.stream)  # the step ends when every shard's replay has ended
+        if h is not None:
+            shards[0].b.update_health_device(len(w.inv_status), h.data_ptr(), shards[0].sp)
+        shards[0].replay()
 
     for _ in range(args.warmup):
         launch_all()
@@ -221,6 +331,7 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    n_gathers[0] = 0
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -232,6 +343,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    gathers_per_step = n_gathers[0] / max(args.steps, 1)
     replay_ms = float(np.mean([a.elapsed_time(c) for a, c in evs]))
     stats = b.stats()
     # the dominant kernel alone: HIP events the library records around each engine launch on the replay stream,
@@ -239,7 +351,7 @@ def main():
     eng = []
     for _ in range(max(3, min(args.steps, 5))):
         launch_all()
-        eng.append(float(np.mean([sh.b.engine_ms() for sh in shards])))
+        eng.append(float(np.mean([sh.b.engine_ms() for sh in shards[::MULTI_MAX]])))
     kern_ms = float(np.mean(eng))
 
     exact = True
@@ -255,21 +367,34 @@ def main():
                                and np.array_equal(o_rf, sh.d_rf.cpu().numpy()[: len(o_rf)])
                                and np.array_equal(st.permits(), sh.b.permits()))
 
+    # host buffers through the C ABI (owgs_replay: argument checks, H2D of the stream, replay, D2H of the decisions):
+    # the rate a JVM caller handing over host arrays would see; never the bench value
+    h2d_ms = 0.0
+    if not args.no_h2d:
+        reps = 3
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            for sh in shards:
+                sh.b.restore()
+                sh.b.replay(sh.s)
+        h2d_ms = (time.perf_counter() - t1) / reps * 1e3
+
     n_dec = sum(len(sh.s.act) for sh in shards)  # this rank's decisions per step
     t_step = wall / args.steps
-    t_step, bad, kern_ms, replay_ms = cluster.max_over_ranks(dist, [t_step, 0.0 if exact else 1.0, kern_ms, replay_ms],
-                                                             dev)
+    t_step, bad, kern_ms, replay_ms, h2d_ms = cluster.max_over_ranks(
+        dist, [t_step, 0.0 if exact else 1.0, kern_ms, replay_ms, h2d_ms], dev)
     exact = bad == 0.0
     value = cluster.whole_job_rate(n_dec, world, t_step)
     algo = algorithmic_bytes(w)
-    achieved = algo / (kern_ms * 1e-3) / 1e9
-    headline = args.config == "headline" and args.n_activations == 1_000_000
-    traffic = ENGINE_PMC_TRAFFIC["bytes"] if headline else None
-    traffic_src = ENGINE_PMC_TRAFFIC["source"] if headline else None
+    per_launch = min(K, MULTI_MAX)  # shards one engine launch replays
+    achieved = algo["survey"] * per_launch / (kern_ms * 1e-3) / 1e9
+    key = f"{args.config}|n{len(s.act)}|c{n_ctl}|s{args.slots}|k{per_launch}"
+    pmc = pmc_traffic(key)
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args, world)
+            cpu = cpu_baseline(args, w, n_ctl, shard_ids[0])
         line = {
             "metric": "scheduling decisions/sec (whole node) at 10k invokers, 1M-activation batch",
             "value": value if exact else 0.0,
@@ -286,12 +411,22 @@ def main():
             "bit_exact": exact,
             "config": {"workload": args.config, "invokers": int(len(w.inv_ids)), "activations_per_shard": len(s.act),
                        "batches": s.n_batches, "batch": w.info["batch"], "releases": int(len(s.rel_aid)),
-                       "cluster_size": w.cluster_size,
-                       "invoker_memory_mb": int(w.inv_mem[0] // (1 << 20)), "slot_mb": int(w.info["slot_mb"]), "parallelism": f"{n_ctl} controller shard(s), {K} per GPU"},
+                       "cluster_size": n_ctl, "slots": args.slots, "shards": shard_ids if world == 1 else None,
+                       "invoker_memory_mb": int(w.inv_mem[0] // (1 << 20)), "slot_mb": int(w.info["slot_mb"]),
+                       "health_allgathers_per_step": gathers_per_step,
+                       "parallelism": f"{n_ctl} controller shard(s), {K} per GPU, {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "owgs_engine_kernel", "kernel_ms": kern_ms, "replay_ms": replay_ms,
-                         "algorithmic_bytes": algo},
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": pmc["bytes"] if pmc else None,
+                         "traffic_source": pmc["source"] if pmc else f"no --pmc pass recorded for this build ({key})",
+                         "kernel": "owgs_engine_kernel" if K == 1 else "owgs_engine_multi_kernel",
+                         "kernel_ms": kern_ms, "replay_ms": replay_ms, "shards_per_launch": per_launch,
+                         "algorithmic_bytes": algo["survey"] * per_launch,
+                         "algorithmic_def": f"SURVEY 8(d): {B_DECISION} B/decision + {B_RELEASE} B/release",
+                         "achieved_stream_bytes": algo["stream"] * per_launch / (kern_ms * 1e-3) / 1e9},
+            "h2d_inclusive": None if args.no_h2d else {
+                "value": world * n_dec / (h2d_ms * 1e-3), "unit": "decisions/s", "ms_per_step": h2d_ms,
+                "path": "owgs_replay host ABI: host checks + H2D stream + replay + D2H decisions"},
             "engine_stats": stats,
             "cpu_baseline": cpu,
         }

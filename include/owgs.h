@@ -150,8 +150,9 @@ int owgs_replay_device(owgs_ctx* ctx, int32_t n_batches, const int64_t* acq_off,
                        uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, uint8_t* rel_flags, void* stream);
 /* Several controller shards (clusterSize > 1, one context each, same device) replayed by ONE engine launch, one
  * workgroup per shard: the reference runs one ShardingContainerPoolBalancer per controller (SCPB:126-133,
- * 485-499); this hosts up to 8 of them on one GPU.  io[i] holds owgs_replay_device's arguments for ctxs[i]; every
- * shard needs n_batches > 0.  Same results as k separate owgs_replay_device calls.  Asynchronous on `stream`. */
+ * 485-499); this hosts up to 64 of them on one GPU (up to 8 argument blocks travel in the kernarg segment, more
+ * through a pinned host buffer and HBM owned by ctxs[0]).  io[i] holds owgs_replay_device's arguments for ctxs[i];
+ * every shard needs n_batches > 0.  Same results as k separate owgs_replay_device calls.  Asynchronous on `stream`. */
 typedef struct owgs_replay_io {
     int32_t n_batches;
     const int64_t* acq_off;

@@ -29,6 +29,7 @@ JNIEXPORT void JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00
 JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_updateInvokers(
     JNIEnv* env, jobject self, jlong h, jintArray ids, jlongArray mem, jbyteArray status) {
     const jsize n = (*env)->GetArrayLength(env, ids);
+    if (!n_fits(env, n, mem, status, NULL, NULL)) return OWGS_EINVAL;
     jint* pi = (*env)->GetPrimitiveArrayCritical(env, ids, NULL);
     jlong* pm = (*env)->GetPrimitiveArrayCritical(env, mem, NULL);
     jbyte* ps = (*env)->GetPrimitiveArrayCritical(env, status, NULL);
@@ -61,8 +62,18 @@ JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00
     return rc == OWGS_OK ? action : rc;
 }
 
+/* n must not exceed any array: bound it by every length (a short array would be read / written past its end) */
+static int n_fits(JNIEnv* env, jint n, jarray a, jarray b, jarray c, jarray d) {
+    jarray xs[4] = {a, b, c, d};
+    if (n < 0) return 0;
+    for (int i = 0; i < 4; ++i)
+        if (xs[i] && (*env)->GetArrayLength(env, xs[i]) < n) return 0;
+    return 1;
+}
+
 JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_publishBatch(
     JNIEnv* env, jobject self, jlong h, jintArray actions, jlongArray seq, jint n, jintArray out, jbyteArray flags) {
+    if (!n_fits(env, n, actions, seq, out, flags)) return OWGS_EINVAL;
     jint* pa = (*env)->GetPrimitiveArrayCritical(env, actions, NULL);
     jlong* ps = (*env)->GetPrimitiveArrayCritical(env, seq, NULL);
     jint* po = (*env)->GetPrimitiveArrayCritical(env, out, NULL);
@@ -77,6 +88,7 @@ JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00
 
 JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_releaseBatch(
     JNIEnv* env, jobject self, jlong h, jintArray invokers, jintArray actions, jint n, jbyteArray flags) {
+    if (!n_fits(env, n, invokers, actions, flags, NULL)) return OWGS_EINVAL;
     jint* pi = (*env)->GetPrimitiveArrayCritical(env, invokers, NULL);
     jint* pa = (*env)->GetPrimitiveArrayCritical(env, actions, NULL);
     jbyte* pf = (*env)->GetPrimitiveArrayCritical(env, flags, NULL);
@@ -91,6 +103,8 @@ JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00
 JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_trackActivations(
     JNIEnv* env, jobject self, jlong h, jbyteArray aid32, jintArray actions, jintArray tickets, jint n,
     jintArray outTicket, jbyteArray outExisted) {
+    if (!n_fits(env, n, actions, tickets, outTicket, outExisted) || (*env)->GetArrayLength(env, aid32) < 32LL * n)
+        return OWGS_EINVAL;
     jbyte* pa = (*env)->GetPrimitiveArrayCritical(env, aid32, NULL);
     jint* pc = (*env)->GetPrimitiveArrayCritical(env, actions, NULL);
     jint* pt = (*env)->GetPrimitiveArrayCritical(env, tickets, NULL);
@@ -110,6 +124,8 @@ JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00
 JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_processAcks(
     JNIEnv* env, jobject self, jlong h, jbyteArray bytes, jlongArray off, jint n, jbyteArray outKind,
     jintArray outInvoker, jintArray outTicket, jbyteArray outFlags) {
+    if (!n_fits(env, n, outKind, outInvoker, outTicket, outFlags) || (*env)->GetArrayLength(env, off) < n + 1)
+        return OWGS_EINVAL;
     jbyte* pb = (*env)->GetPrimitiveArrayCritical(env, bytes, NULL);
     jlong* po = (*env)->GetPrimitiveArrayCritical(env, off, NULL);
     jbyte* pk = (*env)->GetPrimitiveArrayCritical(env, outKind, NULL);
@@ -130,6 +146,9 @@ JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00
 JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_completeActivations(
     JNIEnv* env, jobject self, jlong h, jbyteArray aid32, jintArray invokers, jbyteArray flags, jint n,
     jbyteArray outKind, jintArray outTicket, jbyteArray outFlags) {
+    if (!n_fits(env, n, invokers, flags, outKind, outTicket) || !n_fits(env, n, outFlags, NULL, NULL, NULL) ||
+        (*env)->GetArrayLength(env, aid32) < 32LL * n)
+        return OWGS_EINVAL;
     jbyte* pa = (*env)->GetPrimitiveArrayCritical(env, aid32, NULL);
     jint* pi = (*env)->GetPrimitiveArrayCritical(env, invokers, NULL);
     jbyte* pc = (*env)->GetPrimitiveArrayCritical(env, flags, NULL);
@@ -151,6 +170,7 @@ JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00
 JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_healthEvents(
     JNIEnv* env, jobject self, jlong h, jintArray invokers, jbyteArray kinds, jlongArray tMs, jlongArray userMemory,
     jint n, jlong nowMs, jboolean apply) {
+    if (!n_fits(env, n, invokers, kinds, tMs, userMemory)) return OWGS_EINVAL;
     jint* pi = (*env)->GetPrimitiveArrayCritical(env, invokers, NULL);
     jbyte* pk = (*env)->GetPrimitiveArrayCritical(env, kinds, NULL);
     jlong* pt = (*env)->GetPrimitiveArrayCritical(env, tMs, NULL);

@@ -145,6 +145,10 @@ struct owgs_ctx {
     DevBuf<uint2> d_act_meta;
     DevBuf<u64> d_stats;
     DevBuf<uint32_t> d_margs;  // owgs_replay_device_multi: shard argument blocks beyond the kernarg segment
+    void* h_margs = nullptr;   // pinned staging of d_margs (hipHostMalloc), h_margs_bytes long
+    size_t h_margs_bytes = 0;
+    hipEvent_t ev_margs = nullptr;  // recorded after the last engine launch that reads d_margs / h_margs
+    bool ev_margs_valid = false;
     // per-call scratch
     DevBuf<int64_t> d_off;
     DevBuf<int32_t> d_a, d_b, d_c, d_d, d_out, d_cstart, d_relx, d_cpos, d_bsum, d_crel_off, d_acc, d_xslot;
@@ -531,6 +535,10 @@ void owgs_destroy(owgs_ctx* c) {
     c->d_act_meta.release();
     c->d_stats.release();
     c->d_margs.release();
+    if (c->h_margs) (void)hipHostFree(c->h_margs);
+    c->h_margs = nullptr;
+    if (c->ev_margs) (void)hipEventDestroy(c->ev_margs);
+    c->ev_margs = nullptr;
     c->d_off.release();
     c->d_flags.release();
     c->d_rflags.release();
@@ -1054,12 +1062,25 @@ int owgs_replay_device_multi(owgs_ctx** cs, int32_t k, const owgs_replay_io* io,
     for (int32_t i = 0; i < k; ++i) HIPCHK(cs[i], hipEventRecord(cs[i]->ev_engine[0], hs));
     if (k <= OWGS_MULTI_MAX) {
         HIPCHK(cs[0], owgs_launch_engine_multi(A.data(), k, hs));
-    } else {  // argument blocks through HBM (the context's buffer; ordered on hs before the launch)
+    } else {  // argument blocks through HBM: the leader context's buffer, staged from its pinned host copy
         owgs_ctx* c0 = cs[0];
-        const size_t words = ((size_t)k * sizeof(OwgsEngineArgs) + 3) / 4;
-        HIPCHK(c0, c0->d_margs.reserve(words));
-        HIPCHK(c0, hipMemcpyAsync(c0->d_margs.p, A.data(), (size_t)k * sizeof(OwgsEngineArgs), hipMemcpyHostToDevice, hs));
+        const size_t bytes = (size_t)k * sizeof(OwgsEngineArgs);
+        // the previous multi launch of this leader (maybe on another stream) may still read both buffers
+        if (c0->ev_margs_valid) HIPCHK(c0, hipEventSynchronize(c0->ev_margs));
+        if (c0->h_margs_bytes < bytes) {
+            if (c0->h_margs) (void)hipHostFree(c0->h_margs);
+            c0->h_margs = nullptr;
+            c0->h_margs_bytes = 0;
+            HIPCHK(c0, hipHostMalloc(&c0->h_margs, bytes, hipHostMallocDefault));
+            c0->h_margs_bytes = bytes;
+        }
+        if (!c0->ev_margs) HIPCHK(c0, hipEventCreateWithFlags(&c0->ev_margs, hipEventDisableTiming));
+        memcpy(c0->h_margs, A.data(), bytes);
+        HIPCHK(c0, c0->d_margs.reserve((bytes + 3) / 4));
+        HIPCHK(c0, hipMemcpyAsync(c0->d_margs.p, c0->h_margs, bytes, hipMemcpyHostToDevice, hs));
         HIPCHK(c0, owgs_launch_engine_multi_dev(A.data(), (const OwgsEngineArgs*)c0->d_margs.p, k, hs));
+        HIPCHK(c0, hipEventRecord(c0->ev_margs, hs));
+        c0->ev_margs_valid = true;
     }
     for (int32_t i = 0; i < k; ++i) {
         HIPCHK(cs[i], hipEventRecord(cs[i]->ev_engine[1], hs));

@@ -2401,13 +2401,10 @@ extern "C" hipError_t owgs_launch_engine_multi_dev(const OwgsEngineArgs* a_host,
         lds = std::max(lds, owgs_engine_lds_bytes(a_host[i].n_slots, a_host[i].pool_mode, a_host[i].n_ids,
                                                   a_host[i].nm, a_host[i].nb, a_host[i].n_actions));
     if (lds > OWGS_LDS_BYTES) return hipErrorInvalidValue;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)owgs_engine_multi_dev_kernel,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, OWGS_LDS_BYTES);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    // per launch (cheap): the attribute is per device, and a process may drive contexts on several devices
+    const hipError_t ea = hipFuncSetAttribute((const void*)owgs_engine_multi_dev_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              OWGS_LDS_BYTES);
+    if (ea != hipSuccess) return ea;
     hipLaunchKernelGGL(owgs_engine_multi_dev_kernel, dim3(k), dim3(OWGS_NT), lds, s, a_dev);
     return hipGetLastError();
 }
@@ -2422,13 +2419,10 @@ extern "C" hipError_t owgs_launch_engine_multi(const OwgsEngineArgs* a, int k, h
         M.a[i] = a[i];
     }
     if (lds > OWGS_LDS_BYTES) return hipErrorInvalidValue;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)owgs_engine_multi_kernel,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, OWGS_LDS_BYTES);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    // per launch (cheap): the attribute is per device, and a process may drive contexts on several devices
+    const hipError_t ea = hipFuncSetAttribute((const void*)owgs_engine_multi_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              OWGS_LDS_BYTES);
+    if (ea != hipSuccess) return ea;
     hipLaunchKernelGGL(owgs_engine_multi_kernel, dim3(k), dim3(OWGS_NT), lds, s, M);
     return hipGetLastError();
 }
@@ -2436,13 +2430,10 @@ extern "C" hipError_t owgs_launch_engine_multi(const OwgsEngineArgs* a, int k, h
 extern "C" hipError_t owgs_launch_engine(const OwgsEngineArgs* a, hipStream_t s) {
     const size_t lds = owgs_engine_lds_bytes(a->n_slots, a->pool_mode, a->n_ids, a->nm, a->nb, a->n_actions);
     if (lds > OWGS_LDS_BYTES) return hipErrorInvalidValue;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)owgs_engine_kernel,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, OWGS_LDS_BYTES);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    // per launch (cheap): the attribute is per device, and a process may drive contexts on several devices
+    const hipError_t ea = hipFuncSetAttribute((const void*)owgs_engine_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              OWGS_LDS_BYTES);
+    if (ea != hipSuccess) return ea;
     hipLaunchKernelGGL(owgs_engine_kernel, dim3(1), dim3(OWGS_NT), lds, s, *a);
     return hipGetLastError();
 }

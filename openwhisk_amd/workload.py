@@ -145,7 +145,11 @@ def generate(name: str = "headline", n_invokers: int = 10_000, user_memory_mb: i
 
 
 def config(name: str, n_activations: int | None = None, shard: int = 0, n_shards: int = 1, **kw) -> Workload:
-    """Named BASELINE.json configs.  `n_activations` shrinks a config for fast parity tests."""
+    """Named BASELINE.json configs.  `n_activations` shrinks a config for fast parity tests.
+
+    `n_shards` > 1 makes the workload controller shard `shard` of an `n_shards`-controller cluster for every config:
+    clusterSize = n_shards (each slot holds 1/n_shards of every invoker, SCPB:485-499), the cluster (invokers, health,
+    actions) shared, the activation stream and the overload RNG seed the shard's own."""
     if name == "c1":
         act = Action("invocationSpace", "testspace/testname", "0.0.1", 256, 1, False)
         base = dict(n_invokers=10, user_memory_mb=2000, unhealthy_frac=0.0, managed_fraction=1.0,
@@ -163,6 +167,8 @@ def config(name: str, n_activations: int | None = None, shard: int = 0, n_shards
                     seed=0x0F15C005, shard=shard, rng_seed=0x0F15C005 + shard, cluster_size=n_shards)
     else:
         raise ValueError(name)
+    if name not in ("headline", "c5") and (n_shards > 1 or shard):
+        base.update(shard=shard, rng_seed=base["seed"] + shard, cluster_size=n_shards)
     base.update(kw)
     if n_activations is not None:
         base["n_activations"] = n_activations

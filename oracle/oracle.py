@@ -13,7 +13,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "libowsched_oracle.so")
+# OWO_LIB selects another build of the same sources (e.g. the ASan/UBSan one: make -C oracle sanitize)
+LIB_PATH = os.environ.get("OWO_LIB") or os.path.join(HERE, "build", "libowsched_oracle.so")
 
 NONE = -1
 THROW_INDEX = -2

@@ -97,6 +97,26 @@ def test_assignments_respect_health(two_ranks):
         assert np.all(health[normal] == 0)
 
 
+def test_bench_launches_its_own_ranks():
+    """`bench.py --gpus 2` without a torch.distributed environment starts 2 ranks itself (torch.distributed.run as a
+    child), each rank takes its controller shard of a 2-controller cluster with split slots (configs[4]), the ranks
+    all-gather health once per step and rank 0 prints one line.  --dry-run swaps RCCL for gloo and skips the replay."""
+    import json
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "3",
+                          "--n-activations", "5000"], capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["dry_run"] and d["value"] is None
+    assert d["config"]["cluster_size"] == 2 and d["config"]["slots"] == "split"
+    assert d["config"]["slot_mb"] == 16_384 // 2  # getInvokerSlot: 16 GiB / clusterSize 2
+    assert d["config"]["health_disagree"] == []
+
+
 def test_max_over_ranks_and_rate(two_ranks):
     for r in two_ranks:
         assert float(r["t_max"]) == pytest.approx(0.020)

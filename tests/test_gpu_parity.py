@@ -339,16 +339,19 @@ def test_update_invokers_and_cluster_on_device_match_oracle(seed):
             assert np.array_equal(b.permits(), o.permits()), (n, size)
 
 
-def test_multi_shard_single_launch_parity():
-    # owgs_replay_device_multi: 3 controller shards of a 4-controller cluster in ONE engine launch (one workgroup
-    # each), every shard bit-exact with its own oracle replay; a second launch after restore repeats the results
+@pytest.mark.parametrize("shard_ids,n_shards,n_act", [((0, 1, 3), 4, 150_000),
+                                                      (tuple(range(12)), 16, 20_000)])
+def test_multi_shard_single_launch_parity(shard_ids, n_shards, n_act):
+    # owgs_replay_device_multi: several controller shards in ONE engine launch (one workgroup each), every shard
+    # bit-exact with its own oracle replay; a second launch after restore repeats the results.  3 shards take the
+    # kernarg path (owgs_engine_multi_kernel), 12 the argument blocks in HBM (owgs_engine_multi_dev_kernel)
     import torch
 
     dev = torch.device("cuda", 0)
     t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
     shards = []
-    for g in (0, 1, 3):
-        w = W.config("headline", shard=g, n_shards=4, n_activations=150_000)
+    for g in shard_ids:
+        w = W.config("headline", shard=g, n_shards=n_shards, n_activations=n_act)
         b = gpu_for(w)
         b.snapshot()
         s = w.stream
