@@ -420,8 +420,8 @@ class GpuShardingContainerPoolBalancer:
         self._chk(self._L.owgs_selftest(self._h))
 
     def stats(self) -> dict:
-        out = (C.c_uint64 * 16)()
-        self._chk(self._L.owgs_read_stats(self._h, out, 16))
+        out = (C.c_uint64 * 32)()
+        self._chk(self._L.owgs_read_stats(self._h, out, 32))
         d = {"passes": out[0], "probes": out[1], "fallbacks": out[2], "long_walks": out[3], "chunks": out[4],
              "stops": out[5], "general_probes": out[6], "general_lanes": out[7]}
         if any(out[8:16]):
@@ -430,4 +430,7 @@ class GpuShardingContainerPoolBalancer:
             # profile build: slots 6/7 hold the cycles of the first and of the later passes of the chunks
             d["cycles"]["first_passes"] = d.pop("general_probes")
             d["cycles"]["later_passes"] = d.pop("general_lanes")
+            walk = ["worst_long", "long_walks_worst_wave", "long_rounds", "conc_long", "conc_long_rounds",
+                    "full_walks", "full_walk_rounds", "hot_rounds", "cyc_rounds_c1", "cyc_rounds_conc"]
+            d["walks"] = {k: out[16 + i] for i, k in enumerate(walk)}
         return d

@@ -26,11 +26,8 @@ extern "C" hipError_t owgs_launch_selftest(int* bad, int trials, hipStream_t s);
 extern "C" hipError_t owgs_launch_prepare(const OwgsPrepArgs* a, hipStream_t s);
 extern "C" hipError_t owgs_launch_prepass(const OwgsPrepassArgs* a, int32_t* cstart, int64_t max_chunks,
                                           hipStream_t s);
-extern "C" int64_t owgs_relscan_blocks(int64_t n_rel);
-extern "C" hipError_t owgs_launch_relscan(const int64_t* rel_aid, int64_t n_rel, const int32_t* act,
-                                          const uint2* act_meta, int32_t* cpos, int32_t* bsum,
-                                          const int64_t* rel_off, int32_t n_batches, int32_t* relx,
-                                          int32_t* crel_off, hipStream_t s);
+extern "C" hipError_t owgs_launch_relpos(const int64_t* rel_aid, int64_t n_rel, int64_t n_act, int32_t* relx,
+                                         int32_t* err, hipStream_t s);
 extern "C" hipError_t owgs_launch_relflags(const int64_t* rel_aid, int64_t n_rel, const int32_t* out_inv,
                                            uint8_t* rel_flags, hipStream_t s);
 extern "C" hipError_t owgs_launch_release_seq(const OwgsReleaseArgs* a, hipStream_t s);
@@ -151,7 +148,7 @@ struct owgs_ctx {
     bool ev_margs_valid = false;
     // per-call scratch
     DevBuf<int64_t> d_off;
-    DevBuf<int32_t> d_a, d_b, d_c, d_d, d_out, d_cstart, d_relx, d_cpos, d_bsum, d_crel_off, d_acc, d_xslot;
+    DevBuf<int32_t> d_a, d_b, d_c, d_d, d_out, d_cstart, d_relx, d_xslot;
     DevBuf<uint8_t> d_flags, d_rflags;
     DevBuf<u64> d_seq;
     DevBuf<int64_t> d_rel;
@@ -415,7 +412,7 @@ static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s, bool launch
     A.gcur = c->d_gcur.p;
     A.cur_tag0 = c->cur_tag;
     c->cur_tag += A.n_batches;
-    HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, 16 * sizeof(u64), s));
+    HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, OWGS_NSTATS * sizeof(u64), s));
     if (!c->ev_engine[0]) {
         HIPCHK(c, hipEventCreate(&c->ev_engine[0]));
         HIPCHK(c, hipEventCreate(&c->ev_engine[1]));
@@ -497,13 +494,13 @@ int owgs_create(const owgs_config* cfg, owgs_ctx** out) {
         return OWGS_EDEVICE;
     }
     if (c->d_ct_keys.reserve(OWGS_CTC) || c->d_ct_vals.reserve(OWGS_CTC) || c->d_ct_tmp.reserve(2 * OWGS_CTC) ||
-        c->d_stats.reserve(16) ||
+        c->d_stats.reserve(OWGS_NSTATS) ||
         c->d_err.reserve(1) || c->d_permits.reserve(1)) {
         owgs_destroy(c);
         return OWGS_ENOMEM;
     }
     if (reset_ctab(c) || hipMemset(c->d_err.p, 0, sizeof(int32_t)) != hipSuccess ||
-        hipMemset(c->d_stats.p, 0, 16 * sizeof(u64)) != hipSuccess) {
+        hipMemset(c->d_stats.p, 0, OWGS_NSTATS * sizeof(u64)) != hipSuccess) {
         owgs_destroy(c);
         return OWGS_EDEVICE;
     }
@@ -525,8 +522,7 @@ void owgs_destroy(owgs_ctx* c) {
     DevBuf<int32_t>* i32s[] = {&c->d_permits, &c->d_pool_words, &c->d_hlist, &c->d_act_slot, &c->d_act_hash,
                                &c->d_act_mem,  &c->d_act_maxc,   &c->d_steps,  &c->d_cpx,     &c->d_err,
                                &c->d_a,        &c->d_b,          &c->d_c,      &c->d_d,        &c->d_out,
-                               &c->d_cstart,   &c->d_relx,       &c->d_cpos,   &c->d_bsum,     &c->d_crel_off,
-                               &c->d_acc,      &c->d_xslot,      &c->s_permits};
+                               &c->d_cstart,   &c->d_relx,       &c->d_xslot,  &c->s_permits};
     for (auto* b : i32s) b->release();
     DevBuf<uint32_t>* u32s[] = {&c->d_usable, &c->d_ct_keys, &c->d_ct_vals, &c->d_ct_tmp, &c->s_ct_keys, &c->s_ct_vals};
     for (auto* b : u32s) b->release();
@@ -1110,26 +1106,19 @@ static int replay_begin(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, 
     int rc = run_prepass(c, A, n_batches, acq_off, act, n_activations, hs);
     if (rc) return rc;
     if (rel_off) {
-        // release bookkeeping: relx per activation, compacted concurrent releases, per-batch aggregation rows
+        // release bookkeeping: each released activation's release position; the engine writes the records
         const int64_t nr = std::max<int64_t>(n_releases, 1);
         HIPCHK(c, c->d_relx.reserve((size_t)std::max<int64_t>(n_activations, 1)));
-        HIPCHK(c, c->d_cpos.reserve((size_t)nr));
-        HIPCHK(c, c->d_bsum.reserve((size_t)std::max<int64_t>(owgs_relscan_blocks(n_releases), 1)));
-        HIPCHK(c, c->d_crel_off.reserve((size_t)n_batches + 1));
         HIPCHK(c, c->d_rel_rec.reserve((size_t)nr));
-        const int64_t stride = ((int64_t)c->n_slots + 63) & ~(int64_t)63;  // whole 256-B lines per row
-        HIPCHK(c, c->d_acc.reserve((size_t)(stride * n_batches)));
         HIPCHK(c, hipMemsetAsync(c->d_relx.p, 0xFF, (size_t)n_activations * 4, hs));
-        HIPCHK(c, hipMemsetAsync(c->d_acc.p, 0, (size_t)(stride * n_batches) * 4, hs));
+        // a record no decision writes (device streams are not checked on the host: a release of a later activation)
+        // reads as "no ActivationEntry"
+        HIPCHK(c, hipMemsetAsync(c->d_rel_rec.p, 0xFF, (size_t)nr * sizeof(uint2), hs));
         if (rel_flags && n_releases) HIPCHK(c, hipMemsetAsync(rel_flags, 0, (size_t)n_releases, hs));
-        HIPCHK(c, owgs_launch_relscan(rel_aid, n_releases, act, c->d_act_meta.p, c->d_cpos.p, c->d_bsum.p, rel_off,
-                                      n_batches, c->d_relx.p, c->d_crel_off.p, hs));
+        HIPCHK(c, owgs_launch_relpos(rel_aid, n_releases, n_activations, c->d_relx.p, c->d_err.p, hs));
         A.rel_off = rel_off;
         A.relpos = c->d_relx.p;
         A.rel_rec = c->d_rel_rec.p;
-        A.crel_off = c->d_crel_off.p;
-        A.acc = c->d_acc.p;
-        A.acc_stride = stride;
     }
     return run_engine(c, A, hs, launch);
 }
@@ -1226,10 +1215,10 @@ int owgs_selftest(owgs_ctx* c) {
 int owgs_read_stats(owgs_ctx* c, uint64_t* out, int32_t cap) {
     if (!c || !out) return OWGS_EINVAL;
     (void)hipSetDevice(c->cfg.device);
-    u64 v[16];
+    u64 v[OWGS_NSTATS];
     HIPCHK(c, hipDeviceSynchronize());
     HIPCHK(c, hipMemcpy(v, c->d_stats.p, sizeof(v), hipMemcpyDeviceToHost));
-    for (int32_t i = 0; i < cap && i < 16; ++i) out[i] = v[i];
+    for (int32_t i = 0; i < cap && i < OWGS_NSTATS; ++i) out[i] = v[i];
     return OWGS_OK;
 }
 

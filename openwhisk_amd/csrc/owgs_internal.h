@@ -25,12 +25,10 @@
 //                                 action << 16 (the lane that holds the action's chunk cursor word)
 //   gcur[n_actions]         u32  walk cursor of each action (first walk step that may still fit) | batch tag << 15,
 //                                 written by the engine, gathered into LDS a chunk ahead by the I/O wave
-//   relx[n_act]             i32  where the activation's release goes: maxConcurrent == 1 -> the batch that releases it
-//                                 (the engine adds its memory to acc[batch][invoker] when it is decided);
-//                                 maxConcurrent > 1 -> its slot in the compacted concurrent-release list; -1 never
-//   acc[n_batches][stride]  i32  memory (MB) that batch b releases per invoker (maxConcurrent == 1 activations)
-//   rel_rec[n_crel]         u32x2 written by the engine when a concurrent activation is decided: {inv | mem << 15,
-//                                 slot | maxConcurrent << 17}; inv 0x7FFF = no ActivationEntry (CLB:278-279)
+//   relx[n_act]             i32  position r of the activation's release in rel_aid, -1 never released
+//   rel_rec[n_rel]          u32x2 written by the engine when the released activation is decided: {inv | mem << 15,
+//                                 slot | maxConcurrent << 17}; inv 0x7FFF = no ActivationEntry (CLB:278-279).  Batch b
+//                                 applies rel_rec[rel_off[b] .. rel_off[b+1]) before its publishes.
 #pragma once
 #include <stdint.h>
 
@@ -111,6 +109,7 @@
 #define OWGS_ST_LONG 3
 #define OWGS_ST_CHUNKS 4
 #define OWGS_ST_STOPS 5
+#define OWGS_NSTATS 32  // 0-7 counters, 8-15 profile-build phase cycles, 16-31 profile-build walk counters
 
 #define OWGS_MULTI_MAX 8  // controller shards per owgs_engine_multi_kernel launch (kernarg: 8 x args)
 #define OWGS_MULTI_DEV_MAX 64  // owgs_engine_multi_dev_kernel: argument blocks in HBM
@@ -140,10 +139,7 @@ struct OwgsEngineArgs {
     uint32_t* gcur;              // [max(n_actions, 1)] walk cursor of each action: batch tag << 15 | step
     int32_t cur_tag0;            // batch b of this launch tags its cursors (cur_tag0 + b + 1) & 0x1FFFF
     const int32_t* relpos;       // [n_act] relx (see above), or null: no releases
-    uint2* rel_rec;              // [n_crel] concurrent release records (compacted)
-    const int32_t* crel_off;     // [n_batches + 1] first concurrent release of each batch
-    int32_t* acc;                // [n_batches][acc_stride] maxConcurrent==1 memory released at each batch, per invoker
-    int64_t acc_stride;
+    uint2* rel_rec;              // [n_rel] release records, in rel_aid order (written when the activation is decided)
     unsigned long long seq_base;
     const unsigned long long* seq; // optional explicit seq per activation
     int32_t* out_inv;
@@ -198,14 +194,6 @@ struct OwgsPrepassArgs {
     uint32_t* lix;               // out [n_chunks][OWGS_WL]: stream lane | first lane of its action << 16
     int32_t cw;                  // chunk width (<= OWGS_WL)
     int32_t deal;                // lane dealing strategy (diagnostics, env OWGS_DEAL; 0 = default)
-};
-
-struct OwgsRelposArgs {
-    const int64_t* rel_aid;
-    int64_t n_rel;
-    int64_t n_act;
-    int32_t* relpos;
-    int32_t* err;
 };
 
 // ordered explicit releases (owgs_release_batch): one wave, releases in stream order

@@ -6,8 +6,7 @@
 //   owgs_prepare_kernel   per action: home = hash % n, step = stepSizes(hash % k), limits -> act_meta (SCPB:262-268).
 //   owgs_chunks_kernel    first chunk of every batch (chunks = OWGS_WL consecutive publishes of one batch).
 //   owgs_prepass_kernel   one workgroup per chunk: per-activation engine record = action meta + chunk-local ranks.
-//   owgs_relscan*_kernel  release bookkeeping: maxConcurrent==1 releases are aggregated per (release batch, invoker);
-//                         concurrent releases get a compacted slot in rel_rec.
+//   owgs_relpos_kernel    release bookkeeping: each released activation learns the position of its release record.
 //   owgs_engine_kernel    the hot path: releases (SCPB:327-331 -> NS:98-113) and schedule() (SCPB:398-436 with
 //                         NS:32-91) for a whole stream of batches, replaying the reference's SEQUENTIAL semantics.
 //   owgs_relflags_kernel  per-release flags after the replay (no ActivationEntry, CLB:278-279).
@@ -54,6 +53,9 @@ typedef unsigned long long u64;
 #define FGRP 4  // walk steps per group of the maxConcurrent == 1 fast path (their reads issue together)
 #endif
 #define CAPMAX 1024  // capacities are clamped: a lane's rank is < OWGS_WL
+#ifndef LW_Q
+#define LW_Q 4  // walk steps each lane probes per round of a wave-cooperative long walk
+#endif
 
 // diagnostic build (-DOWGS_PROFILE, libowgs_prof.so): s_memtime cycle accounting per engine phase into stats[8..15]
 #if defined(OWGS_PROFILE) || defined(OWGS_TRACE)
@@ -67,7 +69,8 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
 #ifdef OWGS_PROFILE
 #define PT_DECL                 \
     u64 pt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
-    u64 pt_x[2] = {0, 0};                     \
+    u64 pw_c[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
+    u64 pt_x[3] = {0, 0, 0};                  \
     u64 pt_t = memtime_pinned(); \
     int pt_on = 1;
 #define PT(k)                                        \
@@ -90,7 +93,7 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
 #define SC_NLIVE 7  // table rebuild: live entries
 #define SC_NHOT 8   // multi-lane actions of the current chunk (hot slots claimed)
 #define SC_CBWD 9   // 1 + the chunk that moved a concurrent action's HBM walk cursor backward (forced acquire)
-#define SC_N (16 + 6 * OWGS_EW)
+#define SC_N (16 + 7 * OWGS_EW)
 
 // hot actions: every action with >= HOT_MIN lanes in a chunk gets a slot (assigned by the pre-pass; a concurrent
 // action only when no lane of the chunk shares its fqn@version with another action); per pass one wave walks its
@@ -689,118 +692,16 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
     A.lix[(int64_t)g * OWGS_WL + pos] = (uint32_t)t | ((uint32_t)lead << 16);
 }
 
-// Release bookkeeping.  relx[aid] = release batch (maxConcurrent == 1: aggregated into acc[batch][invoker]) or the
-// compacted position of a concurrent release in rel_rec.  Three-step exclusive scan over the concurrent flags.
-#define RS_TPB 1024
-#define RS_IPT 4
-#define RS_ELEMS (RS_TPB * RS_IPT)
-
-__device__ __forceinline__ int rel_batch(const int64_t* rel_off, int n_batches, int64_t r) {
-    int lo = 0, hi = n_batches - 1;  // last b with rel_off[b] <= r
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (rel_off[mid] <= r) lo = mid;
-        else hi = mid - 1;
-    }
-    return lo;
-}
-
-struct OwgsRelScanArgs {
-    const int64_t* rel_aid;
-    int64_t n_rel;
-    const int32_t* act;
-    const uint2* act_meta;
-    int32_t* cpos;      // [n_rel] exclusive scan of concurrent flags (local, then global)
-    int32_t* bsum;      // [n_blocks]
-    int32_t n_blocks;
-    const int64_t* rel_off;
-    int32_t n_batches;
-    int32_t* relx;      // [n_act]
-    int32_t* crel_off;  // [n_batches + 1]
-};
-
-__device__ __forceinline__ int is_conc_rel(const OwgsRelScanArgs& A, int64_t r) {
-    const int a = A.act[A.rel_aid[r]];
-    return ((A.act_meta[a].y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK) > 1 ? 1 : 0;
-}
-
-__device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* total) {
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int inc = wave_incl_scan(v);
-    if (lane == 63) tmp[w] = inc;
-    __syncthreads();
-    if (t < 64) {
-        const int x = t < (int)(blockDim.x >> 6) ? tmp[t] : 0;
-        const int xi = wave_incl_scan(x);
-        tmp[64 + t] = xi - x;
-        if (t == 63) tmp[128] = xi;
-    }
-    __syncthreads();
-    const int r = tmp[64 + w] + inc - v;
-    *total = tmp[128];
-    __syncthreads();
-    return r;
-}
-
-__global__ __launch_bounds__(RS_TPB) void owgs_relscan1_kernel(OwgsRelScanArgs A) {
-    __shared__ int tmp[160];
-    const int64_t base = (int64_t)blockIdx.x * RS_ELEMS + (int64_t)threadIdx.x * RS_IPT;
-    int f[RS_IPT], s = 0;
-    for (int k = 0; k < RS_IPT; ++k) {
-        const int64_t r = base + k;
-        f[k] = r < A.n_rel ? is_conc_rel(A, r) : 0;
-        s += f[k];
-    }
-    int total;
-    int ex = block_excl_scan(s, tmp, &total);
-    for (int k = 0; k < RS_IPT; ++k) {
-        const int64_t r = base + k;
-        if (r < A.n_rel) A.cpos[r] = ex;
-        ex += f[k];
-    }
-    if (threadIdx.x == 0) A.bsum[blockIdx.x] = total;
-}
-
-__global__ __launch_bounds__(RS_TPB) void owgs_relscan2_kernel(OwgsRelScanArgs A) {
-    __shared__ int tmp[160];
-    int carry = 0;
-    for (int b0 = 0; b0 < A.n_blocks; b0 += RS_TPB) {
-        const int i = b0 + (int)threadIdx.x;
-        const int v = i < A.n_blocks ? A.bsum[i] : 0;
-        int total;
-        const int ex = block_excl_scan(v, tmp, &total);
-        if (i < A.n_blocks) A.bsum[i] = carry + ex;
-        carry += total;
-    }
-}
-
-__global__ __launch_bounds__(RS_TPB) void owgs_relscan3_kernel(OwgsRelScanArgs A) {
-    const int64_t base = (int64_t)blockIdx.x * RS_ELEMS + (int64_t)threadIdx.x * RS_IPT;
-    const int off = A.bsum[blockIdx.x];
-    for (int k = 0; k < RS_IPT; ++k) {
-        const int64_t r = base + k;
-        if (r >= A.n_rel) break;
-        const int64_t aid = A.rel_aid[r];
-        const int cp = off + A.cpos[r];
-        A.cpos[r] = cp;
-        A.relx[aid] = is_conc_rel(A, r) ? cp : rel_batch(A.rel_off, A.n_batches, r);
-    }
-}
-
-// crel_off[b] = number of concurrent releases before rel_off[b]
-__global__ __launch_bounds__(256) void owgs_relscan4_kernel(OwgsRelScanArgs A) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b > A.n_batches) return;
-    const int64_t r = A.rel_off[b];
-    int v;
-    if (r < A.n_rel) {
-        v = A.cpos[r];
-    } else if (A.n_rel > 0) {
-        v = A.cpos[A.n_rel - 1] + is_conc_rel(A, A.n_rel - 1);
-    } else {
-        v = 0;
-    }
-    A.crel_off[b] = v;
+// Release bookkeeping: relx[aid] = r, the position of the activation's release in rel_aid (rel_aid is grouped by
+// release batch, so the engine reads batch b's records rel_rec[rel_off[b] .. rel_off[b+1]) contiguously).  An
+// activation released twice, or a release id outside the stream, is a malformed stream (the reference's
+// activationSlots.remove would find no entry the second time, CLB:278-279; replays take CommonLoadBalancer's streams).
+__global__ __launch_bounds__(256) void owgs_relpos_kernel(const int64_t* rel_aid, int64_t n_rel, int64_t n_act,
+                                                          int32_t* relx, int32_t* err) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rel) return;
+    const int64_t aid = rel_aid[r];
+    if (aid < 0 || aid >= n_act || atomicCAS(&relx[aid], -1, (int32_t)r) != -1) atomicOr(err, OWGS_ERR_BAD_STREAM);
 }
 
 // per-release flags after a replay: the activation was never scheduled -> no ActivationEntry (CLB:278-279)
@@ -1063,23 +964,12 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
             for (int ix = tid; ix < OWGS_CTC; ix += OWGS_NT) rc[ix] = 0u;
             lds_sync();
             if (!io) {
-                // maxConcurrent == 1: the releases of batch b were aggregated per invoker when the activations were
-                // decided (ForcibleSemaphore.release, FS:117-120; the sum of releases is order-free)
-                const int32_t* row = A.acc + (size_t)b * (size_t)A.acc_stride;
-                for (int i = tid; i < n_slots; i += OWGS_ENT) {
-                    const int d = __hip_atomic_load(&row[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (d) {
-                        const int v = P[i];
-                        const int enc = v >= OWGS_PLIM ? OWGS_PENC : 0;
-                        const long long s = (long long)(v - enc) + d;
-                        if (s > 0x7FFFFFFFLL) err |= OWGS_ERR_BAD_STREAM;  // FS:48-50 would throw
-                        else if (s >= OWGS_PLIM) err |= OWGS_ERR_PERMITS;
-                        else P[i] = (int32_t)s + enc;
-                    }
-                }
-                // concurrent releases: RS.release(1, true) per release (NS:98-113); the count per entry decides the
-                // final state, each release's memory return depends only on its rank (c0 + q + 1) % R == 0
-                const int64_t cb = A.crel_off[b], ce = A.crel_off[b + 1];
+                // the release records of batch b (rel_rec[rel_off[b] .. rel_off[b+1]), written when the released
+                // activations were decided): maxConcurrent == 1 -> ForcibleSemaphore.release (FS:117-120), summed
+                // per invoker with LDS atomics (the sum of releases is order-free); concurrent ->
+                // RS.release(1, true) per release (NS:98-113): the count per entry decides the final state, each
+                // release's memory return depends only on its rank (c0 + q + 1) % R == 0
+                const int64_t cb = A.rel_off[b], ce = A.rel_off[b + 1];
                 for (int64_t r0 = cb + tid; r0 < ce; r0 += 8 * OWGS_ENT) {
                     u64 rr[8];
 #pragma unroll
@@ -1099,6 +989,12 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         const int mem = (int)(lo >> 15);
                         const int slot = (int)(hi & 0x1FFFFu);
                         const int R = (int)((hi >> 17) & OWGS_AM_MAXC_MASK);
+                        if (R <= 1) {  // FS:117-120 (beyond the LDS encoding's range: error, FS:48-50 past 2^31)
+                            int old = atomicAdd(&P[inv], mem);
+                            old -= old >= OWGS_PLIM ? OWGS_PENC : 0;
+                            if (old >= OWGS_PLIM - mem) err |= OWGS_ERR_PERMITS;
+                            continue;
+                        }
                         uint32_t v;
                         const int ix = ct_findv(ct, ct_key(inv, slot), &v);
                         const int c0 = (int)(v & OWGS_CT_C_MASK), ops0 = (int)(v >> OWGS_CT_C_BITS);
@@ -1379,6 +1275,9 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         int cum = 0;
                         ++st_long;
                         for (;;) {
+#ifdef OWGS_PROFILE
+                            ++pw_c[7];
+#endif
                             if (s0 >= hn) {  // every position probed: the remaining ranks fall back (SCPB:417)
                                 for (int q = cum + lane; q < need; q += 64)
                                     tab[q] = make_uint2((uint32_t)K_FALLBACK << 15, 0u);
@@ -1657,7 +1556,8 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
 #ifdef OWGS_PROFILE
                 const u64 ts_lane = memtime_pinned();
 #endif
-                // ------------------------------------------------ long walks: wave-cooperative, 64 steps per round
+                // ------------------------------------------------ long walks: wave-cooperative, LW_Q x 64 steps
+                // per round (lane l probes steps 4l .. 4l+3 of the round, its LW_Q reads issue together)
                 if (!io) {
                     u64 lm = __ballot(spec && kind == K_LONG);
                     while (lm) {
@@ -1676,58 +1576,94 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         const int slj = __builtin_amdgcn_readlane(slot, j);
                         const float rmj = __builtin_amdgcn_rcpf((float)mj);
                         const float rnn = __builtin_amdgcn_rcpf((float)nn);
+                        // lane l probes steps l, 64 + l, .. of the round: each of its LW_Q reads is a stride-step
+                        // gather over the wave (step sizes are odd: conflict-free over the LDS banks)
                         const int loff = mod_fast(lane * stp, nn, rnn);
                         const int boff = mod_fast(64 * stp, nn, rnn);
+                        const int roff = mod_fast(64 * LW_Q * stp, nn, rnn);
                         int rk = K_FALLBACK, rt = -1, rks = 0, rst = 0, rci = -1;
                         uint32_t rcv = 0;
-                        while (s0 < nn) {
-                            const int sk = s0 + lane;
+#ifdef OWGS_PROFILE
+                        int nr_ = 0;
+                        ++pw_c[1];
+#endif
+                        bool found = false;
+                        while (s0 < nn && !found) {
+#ifdef OWGS_PROFILE
+                            ++nr_;
+                            const u64 tr0_ = memtime_pinned();
+#endif
+                            int pv[LW_Q], id[LW_Q];
                             int p = p0 + loff;
                             if (p >= nn) p -= nn;
-                            int cap = 0, id = OWGS_PW_UNUSABLE, ci = -1;
-                            uint32_t v = 0;
-                            bool bad = false;
-                            if (sk < nn) {
-                                int pv;
-                                id = pool_probe(E, pj, p, &pv);
-                                if (id == OWGS_PW_BADID) {
-                                    bad = true;
-                                } else if (id >= 0) {
+#pragma unroll
+                            for (int q = 0; q < LW_Q; ++q) {  // positions < nn: the reads are in bounds
+                                id[q] = pool_probe(E, pj, p, &pv[q]);
+                                p += boff;
+                                if (p >= nn) p -= nn;
+                            }
+#pragma unroll
+                            for (int q = 0; q < LW_Q; ++q) asm volatile("" : "+v"(pv[q]), "+v"(id[q]));
+#ifdef OWGS_PROFILE
+                            u64 tr1_ = 0;
+#endif
+#pragma unroll
+                            for (int q = 0; q < LW_Q; ++q) {
+                                const int sk = s0 + 64 * q + lane;
+                                const bool in = sk < nn;
+                                int cap = 0, ci = -1;
+                                uint32_t v = 0;
+                                const bool bad = in && id[q] == OWGS_PW_BADID;
+                                if (in && id[q] >= 0) {
                                     if (cj == 1) {
-                                        cap = cap_of(pv, mj, rmj);
+                                        cap = cap_of(pv[q], mj, rmj);
                                     } else {
-                                        ci = ct_findv(ct, ct_key(id, slj), &v);
-                                        cap = (int)(v & OWGS_CT_C_MASK) + min(cap_of(pv, mj, rmj) * cj, CAPMAX);
+                                        ci = ct_findv(ct, ct_key(id[q], slj), &v);
+                                        cap = (int)(v & OWGS_CT_C_MASK) + min(cap_of(pv[q], mj, rmj) * cj, CAPMAX);
                                     }
                                 }
-                            }
-                            const int inc = wave_incl_scan(cap);
-                            const bool hit = sk < nn && (bad || cum + inc > rj);
-                            const u64 hm = __ballot(hit);
-                            if (hm) {
-                                const int q = ffs64(hm);
-                                const int qb = __builtin_amdgcn_readlane((int)bad, q);
-                                rst = s0 + q;
-                                if (qb) {
-                                    rk = K_THROW;
-                                } else {
-                                    rk = K_TARGET;
-                                    rt = __builtin_amdgcn_readlane(id, q);
-                                    rks = rj - (cum + __builtin_amdgcn_readlane(inc - cap, q));
-                                    rci = __builtin_amdgcn_readlane(ci, q);
-                                    rcv = (uint32_t)__builtin_amdgcn_readlane((int)v, q);
+                                const int inc = wave_incl_scan(cap);
+                                const u64 hm = __ballot(in && (bad || cum + inc > rj));
+                                if (hm) {
+                                    const int L = ffs64(hm);
+                                    rst = s0 + 64 * q + L;
+                                    if (__builtin_amdgcn_readlane((int)bad, L)) {
+                                        rk = K_THROW;
+                                    } else {
+                                        rk = K_TARGET;
+                                        rt = __builtin_amdgcn_readlane(id[q], L);
+                                        rks = rj - (cum + __builtin_amdgcn_readlane(inc - cap, L));
+                                        rci = __builtin_amdgcn_readlane(ci, L);
+                                        rcv = (uint32_t)__builtin_amdgcn_readlane((int)v, L);
+                                    }
+                                    found = true;
+                                    break;
                                 }
-                                break;
+                                cum += __builtin_amdgcn_readlane(inc, 63);
                             }
-                            cum += __builtin_amdgcn_readlane(inc, 63);
+#ifdef OWGS_PROFILE
+                            pw_c[cj > 1 ? 9 : 8] += memtime_pinned() - tr0_;
+                            (void)tr1_;
+#endif
 #ifdef OWGS_COUNT_ROUNDS
                             st_glane += lane == 0 ? 1u : 0u;
 #endif
-                            s0 += 64;
-                            p0 += boff;
+                            s0 += 64 * LW_Q;
+                            p0 += roff;
                             if (p0 >= nn) p0 -= nn;
                         }
-                        st_probe += (lane == 0) ? 64u : 0u;
+                        st_probe += (lane == 0) ? 64u * LW_Q : 0u;
+#ifdef OWGS_PROFILE
+                        pw_c[2] += nr_;
+                        if (cj > 1) {
+                            ++pw_c[3];
+                            pw_c[4] += nr_;
+                        }
+                        if (rk == K_FALLBACK) {
+                            ++pw_c[5];
+                            pw_c[6] += nr_;
+                        }
+#endif
                         if (lane == j) {
                             kind = rk;
                             t = rt;
@@ -1746,6 +1682,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                     spw[4 * wave] = (int)(ts_hot - ts_beg);
                     spw[4 * wave + 1] = (int)(ts_lane - ts_hot);
                     spw[4 * wave + 2] = (int)(ts_end - ts_lane);
+                    spw[4 * wave + 3] = (int)pw_c[1];
                     pfw[2 * wave] = pf_fw;
                     pfw[2 * wave + 1] = pf_gw;
                 }
@@ -1762,6 +1699,13 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                     }
                     pt_acc[6] += (u64)spw[4 * worst];       // worst wave: hot walks
                     pt_acc[7] += (u64)spw[4 * worst + 1];   // worst wave: per-lane speculation
+                    pw_c[0] += (u64)spw[4 * worst + 2];     // worst wave: long walks (and imbalance)
+                    int lwmax = 0;  // long walks of the wave with the most of them in this pass (counters cumulative)
+                    for (int w = 0; w < OWGS_EW; ++w) {
+                        lwmax = max(lwmax, spw[4 * w + 3] - pfw[2 * OWGS_EW + w]);
+                        pfw[2 * OWGS_EW + w] = spw[4 * w + 3];
+                    }
+                    pt_x[2] += (u64)lwmax;
 #ifdef OWGS_PROF_SPLIT
                     if (f == 0)  // first passes, summed over the engine waves: hot walks | per-lane | long walks
                         for (int w = 0; w < OWGS_EW; ++w) {
@@ -1915,15 +1859,10 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
 #endif
                     if (kind == K_FALLBACK) ++st_fb;
 #ifndef OWGS_EXP_NOSTORE
-                    if (relx >= 0) {
-                        if (maxc == 1) {
-                            if (outv >= 0)
-                                atomicAdd(&A.acc[(size_t)relx * (size_t)A.acc_stride + outv], mem);
-                        } else {
-                            const uint32_t inv15 = outv >= 0 ? (uint32_t)outv : OWGS_RR_NOINV;
-                            A.rel_rec[relx] = make_uint2(inv15 | ((uint32_t)mem << 15),
-                                                         (uint32_t)slot | ((uint32_t)maxc << 17));
-                        }
+                    if (relx >= 0) {  // the release record its completion reads (a plain store, no atomics)
+                        const uint32_t inv15 = outv >= 0 ? (uint32_t)outv : OWGS_RR_NOINV;
+                        A.rel_rec[relx] = make_uint2(inv15 | ((uint32_t)mem << 15),
+                                                     (uint32_t)slot | ((uint32_t)maxc << 17));
                     }
 #endif
                     // walk cursor + chunk rank base, written by the last committed lane of the action
@@ -2045,7 +1984,11 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
             if (lane == 0) atomicAdd(&A.stats[OWGS_ST_LONG], (u64)st_long);
         }
 #ifdef OWGS_PROFILE
+        if (!io && lane == 0)
+            for (int k = 2; k < 12; ++k) atomicAdd(&A.stats[16 + k], pw_c[k]);
         if (tid == 0) {  // wave 0: marks sit right after barriers, so the intervals are the critical path
+            atomicAdd(&A.stats[16], pw_c[0]);
+            atomicAdd(&A.stats[17], pt_x[2]);
             for (int k = 0; k < 8; ++k) atomicAdd(&A.stats[8 + k], pt_acc[k]);
             atomicAdd(&A.stats[6], pt_x[0]);
             atomicAdd(&A.stats[7], pt_x[1]);
@@ -2318,30 +2261,11 @@ extern "C" hipError_t owgs_launch_prepass(const OwgsPrepassArgs* a, int32_t* cst
     return hipGetLastError();
 }
 
-extern "C" int64_t owgs_relscan_blocks(int64_t n_rel) { return (n_rel + RS_ELEMS - 1) / RS_ELEMS; }
-
-extern "C" hipError_t owgs_launch_relscan(const int64_t* rel_aid, int64_t n_rel, const int32_t* act,
-                                          const uint2* act_meta, int32_t* cpos, int32_t* bsum,
-                                          const int64_t* rel_off, int32_t n_batches, int32_t* relx,
-                                          int32_t* crel_off, hipStream_t s) {
-    OwgsRelScanArgs A;
-    A.rel_aid = rel_aid;
-    A.n_rel = n_rel;
-    A.act = act;
-    A.act_meta = act_meta;
-    A.cpos = cpos;
-    A.bsum = bsum;
-    A.n_blocks = (int32_t)owgs_relscan_blocks(n_rel);
-    A.rel_off = rel_off;
-    A.n_batches = n_batches;
-    A.relx = relx;
-    A.crel_off = crel_off;
-    if (n_rel > 0) {
-        hipLaunchKernelGGL(owgs_relscan1_kernel, dim3((unsigned)A.n_blocks), dim3(RS_TPB), 0, s, A);
-        hipLaunchKernelGGL(owgs_relscan2_kernel, dim3(1), dim3(RS_TPB), 0, s, A);
-        hipLaunchKernelGGL(owgs_relscan3_kernel, dim3((unsigned)A.n_blocks), dim3(RS_TPB), 0, s, A);
-    }
-    hipLaunchKernelGGL(owgs_relscan4_kernel, dim3((unsigned)((n_batches + 1 + 255) / 256)), dim3(256), 0, s, A);
+extern "C" hipError_t owgs_launch_relpos(const int64_t* rel_aid, int64_t n_rel, int64_t n_act, int32_t* relx,
+                                         int32_t* err, hipStream_t s) {
+    if (n_rel > 0)
+        hipLaunchKernelGGL(owgs_relpos_kernel, dim3((unsigned)((n_rel + 255) / 256)), dim3(256), 0, s, rel_aid, n_rel,
+                           n_act, relx, err);
     return hipGetLastError();
 }
 
