@@ -352,11 +352,23 @@ static void base_args(owgs_ctx* c, OwgsEngineArgs& A) {
     }
 }
 
-// Chunk width of a replay: the full engine width for large pools; 256 lanes when the managed pool is small, where
-// lanes of different actions meet at the few invokers with room and a wide chunk stops more often (measured: 1k
-// invokers 135 ms at 256 vs 155 ms at 336; 10k invokers 35.6 vs 32.9 ms).  Env OWGS_CW overrides (diagnostics).
+// Chunk width of a replay.  Wide chunks amortise a pass over more activations, but lanes of different actions that
+// meet at an invoker without room for both stop the pass.  How often that happens follows the capacity units the
+// managed pool offers (slot MB x invokers / mean action MB): with few units (small pools, or slots split over many
+// controllers) a narrow chunk wins (measured, round 2: C5 shard of 8, 23k units: 244 ms at 128 lanes vs 349 at 336;
+// configs[1], 19k units: 129 vs 139 ms at 256; headline, 187k units: 34 ms at 336 vs 37 at 256).  Env OWGS_CW
+// overrides (diagnostics).
+#ifndef OWGS_WIDE_UNITS
+#define OWGS_WIDE_UNITS 60000.0
+#endif
 static int32_t chunk_width(const owgs_ctx* c) {
-    int32_t cw = c->nm >= 4096 ? OWGS_WL : std::min(256, OWGS_WL);
+    double slot_mb = 0, act_mb = 0;
+    const int32_t nm = std::min<int32_t>(c->nm, (int32_t)c->mem.size());
+    for (int32_t i = 0; i < nm; ++i)
+        slot_mb += (double)std::max<int64_t>(c->cfg.min_memory_bytes, c->mem[i] / std::max(c->cluster, 1)) / 1048576.0;
+    for (int32_t m : c->a_mem) act_mb += m;
+    const double units = c->a_mem.empty() || act_mb <= 0 ? 1e9 : slot_mb / (act_mb / (double)c->a_mem.size());
+    int32_t cw = units >= OWGS_WIDE_UNITS ? OWGS_WL : std::min(128, OWGS_WL);
     if (const char* e = getenv("OWGS_CW")) {
         const int v = atoi(e);
         if (v >= 64 && v <= OWGS_WL) cw = v;

@@ -42,6 +42,7 @@ typedef unsigned long long u64;
 #define K_FALLBACK 3
 #define K_LONG 4
 #define K_HOT 5  // resolved from the hot-action rank table after the pass barrier
+#define K_CSCAN 6  // concurrent action, mem > every usable permit count: resolved from the key's open containers
 
 #ifndef KPROBE
 #define KPROBE 16  // walk steps a maxConcurrent==1 lane probes on its own before the wave-cooperative walk (x4)
@@ -93,6 +94,8 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
 #define SC_NLIVE 7  // table rebuild: live entries
 #define SC_NHOT 8   // multi-lane actions of the current chunk (hot slots claimed)
 #define SC_CBWD 9   // 1 + the chunk that moved a concurrent action's HBM walk cursor backward (forced acquire)
+#define SC_LQN 10   // long walks queued in this pass
+#define SC_LQH 11   // next queued long walk to take
 #define SC_N (16 + 7 * OWGS_EW)
 
 // hot actions: every action with >= HOT_MIN lanes in a chunk gets a slot (assigned by the pre-pass; a concurrent
@@ -372,7 +375,7 @@ __device__ __forceinline__ void lds_dma4_l2(const void* gsrc, uint32_t lds_dst) 
 // ------------------------------------------------------------------------------------------------ LDS layout
 #define OWGS_NSTG 3  // chunk staging buffers
 struct OwgsLayout {
-    uint32_t P, pool, pc, ccw, ct, stgA, stgX, stgL, stgC, fst, spt, hdir, htab, hscr, bhead, nextl, spc, cdirty, skey, rc, sc,
+    uint32_t P, pool, pc, ccw, ct, stgA, stgX, stgL, stgC, fst, spt, hdir, htab, hscr, bhead, nextl, spc, cdirty, skey, lq, rc, sc,
         uni, uni_bytes, total;
 };
 
@@ -414,8 +417,9 @@ __host__ __device__ inline OwgsLayout owgs_layout(int n_slots, int pool_mode, in
     L.spc = L.nextl + 4u * OWGS_WL;                 // memory each lane tentatively takes at its target
     L.cdirty = L.spc + 4u * OWGS_WL;                // [2][OWGS_WL] pass parity x first lane of an action: re-speculated
     L.skey = L.cdirty + 8u * OWGS_WL;               // per lane {slot key, action} (shared-key check)
+    L.lq = L.skey + 8u * OWGS_WL;                   // long-walk queue: {record | rank, step, position, cum} / result
     L.rc = o;
-    const uint32_t ua = (L.skey - o) + 8u * OWGS_WL, ur = 4u * OWGS_CTC;
+    const uint32_t ua = (L.lq - o) + 16u * OWGS_WL, ur = 4u * OWGS_CTC;
     L.uni_bytes = ua > ur ? ua : ur;
     o += L.uni_bytes;
     L.total = o;
@@ -821,6 +825,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     int32_t* spc = (int32_t*)(L + Y.spc);
     int32_t* cdirty = (int32_t*)(L + Y.cdirty);
     uint2* skey = (uint2*)(L + Y.skey);
+    uint4* lq = (uint4*)(L + Y.lq);
     uint4* hdir = (uint4*)(L + Y.hdir);
     int32_t* hocc = (int32_t*)(L + Y.hdir + 16u * NHOT);
     int32_t* hflag = (int32_t*)(L + Y.hdir + 20u * NHOT);
@@ -1225,6 +1230,9 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                 // lane of its action lands as speculated: it speculates again when one of them did
                 if (keep && maxc > 1 && cdirty[par * OWGS_WL + lead]) keep = false;
                 const bool spec = act && !keep;
+                // a maxConcurrent == 1 lane that speculated rank 0 at walk step s_t saw zero capacity at every step
+                // before s_t; permits only fall inside a batch, so its next walk resumes there (rank 0 stays 0)
+                const int resume = (spec && kind == K_TARGET && maxc == 1 && r == 0 && cok) ? s_t : 0;
                 // ------------------------------------------------ speculate (packing) against the state at f
                 if (spec) {
                     kind = K_NONE;
@@ -1351,11 +1359,17 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         cw = ccw[lead];  // walk step (15 bits) | committed lanes of the action in this chunk (10)
                         r = occ - (int)((cw >> 15) & OWGS_RMASK);
                         if (cok) s = (int)(cw & 0x7FFFu);
+                        if (r == 0 && resume > s) s = resume;
                         const int U = sc[pool ? SC_U1 : SC_U0];
                         if (hs >= 0 && r < HOT_RANKS) {
                             kind = K_HOT;
                         } else if (maxc == 1 && mem > U && ((A.shortcut_ok >> pool) & 1)) {
                             kind = K_FALLBACK;  // every usable permit < mem: the walk fails everywhere
+                        } else if (maxc > 1 && mem > U && A.pool_mode == 0 && n > OWGS_CTC / 2) {
+                            kind = K_CSCAN;  // no invoker can open a container: capacity = the key's open ones
+                            ws = s;          // (the ordinary walk's start, should the key have > 64 of them)
+                            wpos = mod_fast(home + s * step, n, __builtin_amdgcn_rcpf((float)n));
+                            wcum = 0;
                         } else {
                             int pos = mod_fast(home + s * step, n, __builtin_amdgcn_rcpf((float)n));
                             int cum = 0;
@@ -1556,24 +1570,140 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
 #ifdef OWGS_PROFILE
                 const u64 ts_lane = memtime_pinned();
 #endif
-                // ------------------------------------------------ long walks: wave-cooperative, LW_Q x 64 steps
-                // per round (lane l probes steps 4l .. 4l+3 of the round, its LW_Q reads issue together)
+                // ------------------------------------------------ concurrent lanes with mem > U (K_CSCAN)
+                // Every usable permit count is below mem, so along the walk only the key's existing containers have
+                // capacity (their free slots c >= 1, NS:57-82 without a new container).  The wave collects the key's
+                // open entries from the concurrency table (64 per read), orders them by walk step
+                // k(x) = (pos(x) - home) * step^-1 mod n, and finds the container holding rank r (cumulative free
+                // slots in walk order); none -> the walk fails everywhere (SCPB:417).  More than 64 open containers:
+                // the ordinary walk.  Only for pools larger than half the table: a smaller pool is walked faster.
                 if (!io) {
-                    u64 lm = __ballot(spec && kind == K_LONG);
-                    while (lm) {
-                        const int j = ffs64(lm);
-                        lm &= lm - 1;
-                        ++st_long;
-                        int s0 = __builtin_amdgcn_readlane(ws, j);
-                        int p0 = __builtin_amdgcn_readlane(wpos, j);
-                        int cum = __builtin_amdgcn_readlane(wcum, j);
-                        const int rj = __builtin_amdgcn_readlane(r, j);
-                        const int stp = __builtin_amdgcn_readlane(step, j);
-                        const int nn = __builtin_amdgcn_readlane(n, j);
-                        const int pj = __builtin_amdgcn_readlane(pool, j);
-                        const int mj = __builtin_amdgcn_readlane(mem, j);
-                        const int cj = __builtin_amdgcn_readlane(maxc, j);
+                    u64 cm = __ballot(spec && kind == K_CSCAN);
+                    int* cand = hscr + wave * 64;
+                    while (cm) {
+                        const int j = ffs64(cm);
+                        cm &= cm - 1;
                         const int slj = __builtin_amdgcn_readlane(slot, j);
+                        const int rj = __builtin_amdgcn_readlane(r, j);
+                        const int pj = __builtin_amdgcn_readlane(pool, j);
+                        const int nn = __builtin_amdgcn_readlane(n, j);
+                        const int hj = __builtin_amdgcn_readlane(home, j);
+                        const int stp = __builtin_amdgcn_readlane(step, j);
+                        const int base = pj ? A.n_ids - nb : 0;
+                        int nc = 0;
+                        for (int e0 = 0; e0 < OWGS_CTC && nc <= 64; e0 += 64) {
+                            const uint2 ev = ct[e0 + lane];
+                            const int inv = (int)(ev.x & 0x7FFFu) - 1;
+                            const int ps = inv - base;
+                            const bool m = (int)(ev.x >> OWGS_CT_SLOT_SHIFT) == slj && inv >= 0 && ps >= 0 && ps < nn &&
+                                           (ev.y & OWGS_CT_C_MASK) != 0u && P[inv] < OWGS_PLIM;
+                            const u64 bm = __ballot(m);
+                            const int at = nc + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+                            if (m && at < 64) cand[at] = e0 + lane;
+                            nc += __popcll(bm);
+                        }
+                        int rk = K_FALLBACK, rt = -1, rks = 0, rst = 0, rci = -1;
+                        uint32_t rcv = 0;
+                        if (nc > 64) {
+                            rk = K_LONG;  // too many containers: walk
+                        } else if (nc > 0) {
+                            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                            // step^-1 mod n (gcd(step, n) = 1: pairwiseCoprimeNumbersUntil, SCPB:379-384)
+                            int t0 = 0, t1 = 1, r0 = nn, r1 = stp % nn;
+                            while (r1 != 0) {
+                                const int q = r0 / r1;
+                                const int tt = t0 - q * t1;
+                                t0 = t1;
+                                t1 = tt;
+                                const int rr = r0 - q * r1;
+                                r0 = r1;
+                                r1 = rr;
+                            }
+                            const int sinv = t0 < 0 ? t0 + nn : t0;
+                            const float rnn = __builtin_amdgcn_rcpf((float)nn);
+                            int ix = -1, kx = 0x7FFFFFFF, cx = 0, idv = 0;
+                            uint32_t vx = 0;
+                            if (lane < nc) {
+                                ix = cand[lane];
+                                const uint2 ev = ct[ix];
+                                idv = (int)(ev.x & 0x7FFFu) - 1;
+                                vx = ev.y;
+                                cx = (int)(vx & OWGS_CT_C_MASK);
+                                int d = idv - base - hj;
+                                d += d < 0 ? nn : 0;
+                                kx = mod_fast(d * sinv, nn, rnn);  // d, sinv < n < 2^15
+                            }
+                            // free slots of the containers before this one in walk order (distinct steps)
+                            int before = 0;
+                            for (int m2 = 0; m2 < nc; ++m2) {
+                                const int km = __builtin_amdgcn_readlane(kx, m2);
+                                const int cmv = __builtin_amdgcn_readlane(cx, m2);
+                                before += km < kx ? cmv : 0;
+                            }
+                            const u64 hm = __ballot(lane < nc && before <= rj && rj < before + cx);
+                            if (hm) {
+                                const int L = ffs64(hm);
+                                rk = K_TARGET;
+                                rt = __builtin_amdgcn_readlane(idv, L);
+                                rks = rj - __builtin_amdgcn_readlane(before, L);
+                                rst = __builtin_amdgcn_readlane(kx, L);
+                                rci = __builtin_amdgcn_readlane(ix, L);
+                                rcv = (uint32_t)__builtin_amdgcn_readlane((int)vx, L);
+                            }
+                            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                        }
+                        if (lane == j) {
+                            kind = rk;
+                            t = rt;
+                            ks = rks;
+                            s_t = rst;
+                            cidx = rci;
+                            cval = rcv;
+                        }
+                    }
+                }
+                // ------------------------------------------------ long walks: a work queue over the engine waves
+                // Lanes whose walk outlasted their own probes queue it (record position, rank, walk state) and, after
+                // a barrier, every engine wave takes queued walks one at a time until the queue is empty, so the
+                // walks of one wave no longer serialise behind each other.  Each walk is wave-cooperative: LW_Q x 64
+                // steps per round; the result goes back through the queue entry.
+                int lq_i = -1;
+                if (!io) {
+                    const u64 lm = __ballot(spec && kind == K_LONG);
+                    if (lm) {
+                        int qb = 0;
+                        if (lane == 0) qb = atomicAdd(&sc[SC_LQN], __popcll(lm));
+                        qb = __builtin_amdgcn_readfirstlane(qb);
+                        if (spec && kind == K_LONG) {
+                            lq_i = qb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
+                            lq[lq_i] = make_uint4((uint32_t)sl | ((uint32_t)r << 16), (uint32_t)ws, (uint32_t)wpos,
+                                                  (uint32_t)wcum);
+                        }
+                    }
+                }
+                LDS_SYNC_T(8);
+                if (!io) {
+                    const int nq = sc[SC_LQN];
+                    for (;;) {
+                        int item = 0;
+                        if (lane == 0) item = atomicAdd(&sc[SC_LQH], 1);
+                        item = __builtin_amdgcn_readfirstlane(item);
+                        if (item >= nq) break;
+                        ++st_long;
+                        const uint4 qe = lq[item];
+                        const uint4 qr = stgA[sbuf * OWGS_WL + (int)(qe.x & 0xFFFFu)];
+                        int s0 = (int)qe.y;
+                        int p0 = (int)qe.z;
+                        int cum = (int)qe.w;
+                        const int rj = (int)(qe.x >> 16);
+                        const int stp = (int)((qr.x >> 15) & OWGS_AM_POS_MASK);
+                        const int pj = (qr.x & OWGS_AM_POOL) ? 1 : 0;
+                        const int nn = pj ? nb : nm;
+                        const int mj = (int)(qr.y & OWGS_AM_MEM_MASK);
+                        const int cj = (int)((qr.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
+                        const int slj = (int)(qr.w & 0x1FFFFu);
                         const float rmj = __builtin_amdgcn_rcpf((float)mj);
                         const float rnn = __builtin_amdgcn_rcpf((float)nn);
                         // lane l probes steps l, 64 + l, .. of the round: each of its LW_Q reads is a stride-step
@@ -1596,14 +1726,43 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             int pv[LW_Q], id[LW_Q];
                             int p = p0 + loff;
                             if (p >= nn) p -= nn;
+                            if (A.pool_mode == 0) {
+                                // identity pools: the id is arithmetic, the usable flag folded into the permits: the
+                                // LW_Q reads of the round issue back to back, no branch between them
+                                const int base = pj ? A.n_ids - nb : 0;
 #pragma unroll
-                            for (int q = 0; q < LW_Q; ++q) {  // positions < nn: the reads are in bounds
-                                id[q] = pool_probe(E, pj, p, &pv[q]);
-                                p += boff;
-                                if (p >= nn) p -= nn;
+                                for (int q = 0; q < LW_Q; ++q) {
+                                    id[q] = base + p;
+                                    pv[q] = P[base + p];
+                                    p += boff;
+                                    if (p >= nn) p -= nn;
+                                }
+#pragma unroll
+                                for (int q = 0; q < LW_Q; ++q) {
+                                    asm volatile("" : "+v"(pv[q]));
+                                    id[q] = pv[q] < OWGS_PLIM ? id[q] : OWGS_PW_UNUSABLE;
+                                }
+                            } else {
+#pragma unroll
+                                for (int q = 0; q < LW_Q; ++q) {  // positions < nn: the reads are in bounds
+                                    id[q] = pool_probe(E, pj, p, &pv[q]);
+                                    p += boff;
+                                    if (p >= nn) p -= nn;
+                                }
                             }
+                            // concurrent: the first 4-entry block of every probe's (invoker, fqn) key, read together
+                            uint32_t hx[LW_Q];
+                            uint4 ea[LW_Q], eb[LW_Q];
+                            if (cj > 1) {
 #pragma unroll
-                            for (int q = 0; q < LW_Q; ++q) asm volatile("" : "+v"(pv[q]), "+v"(id[q]));
+                                for (int q = 0; q < LW_Q; ++q) {
+                                    hx[q] = ct_home(ct_key(id[q] >= 0 ? id[q] : 0, slj));
+                                    ea[q] = *(const uint4*)&ct[hx[q]];
+                                    eb[q] = *(const uint4*)&ct[hx[q] + 2];
+                                }
+#pragma unroll
+                                for (int q = 0; q < LW_Q; ++q) asm volatile("" : "+v"(ea[q].x), "+v"(eb[q].x));
+                            }
 #ifdef OWGS_PROFILE
                             u64 tr1_ = 0;
 #endif
@@ -1614,13 +1773,13 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                 int cap = 0, ci = -1;
                                 uint32_t v = 0;
                                 const bool bad = in && id[q] == OWGS_PW_BADID;
-                                if (in && id[q] >= 0) {
-                                    if (cj == 1) {
-                                        cap = cap_of(pv[q], mj, rmj);
-                                    } else {
-                                        ci = ct_findv(ct, ct_key(id[q], slj), &v);
-                                        cap = (int)(v & OWGS_CT_C_MASK) + min(cap_of(pv[q], mj, rmj) * cj, CAPMAX);
-                                    }
+                                if (cj == 1) {
+                                    cap = (in && id[q] >= 0) ? cap_bf(pv[q], mj, rmj) : 0;
+                                } else if (in && id[q] >= 0) {
+                                    const uint32_t key = ct_key(id[q], slj);
+                                    if (ct_block(ea[q], eb[q], key, hx[q], &v, &ci) == 2)
+                                        ci = ct_findv_from(ct, key, (hx[q] + CT_BLK) & (OWGS_CTC - 1), &v);
+                                    cap = (int)(v & OWGS_CT_C_MASK) + min(cap_bf(pv[q], mj, rmj) * cj, CAPMAX);
                                 }
                                 const int inc = wave_incl_scan(cap);
                                 const u64 hm = __ballot(in && (bad || cum + inc > rj));
@@ -1664,14 +1823,9 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             pw_c[6] += nr_;
                         }
 #endif
-                        if (lane == j) {
-                            kind = rk;
-                            t = rt;
-                            ks = rks;
-                            s_t = rst;
-                            cidx = rci;
-                            cval = rcv;
-                        }
+                        if (lane == 0)  // kind | (t + 1) << 3 | ks << 19, s_t | (cidx + 1) << 15, cval
+                            lq[item] = make_uint4((uint32_t)rk | ((uint32_t)(rt + 1) << 3) | ((uint32_t)rks << 19),
+                                                  (uint32_t)rst | ((uint32_t)(rci + 1) << 15), rcv, 0u);
                     }
                 }
                 
@@ -1715,6 +1869,15 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
 #endif
                 }
 #endif
+                if (lq_i >= 0) {  // a queued long walk: its result
+                    const uint4 qe = lq[lq_i];
+                    kind = (int)(qe.x & 7u);
+                    t = (int)((qe.x >> 3) & 0xFFFFu) - 1;
+                    ks = (int)(qe.x >> 19);
+                    s_t = (int)(qe.y & 0x7FFFu);
+                    cidx = (int)(qe.y >> 15) - 1;
+                    cval = qe.z;
+                }
                 if (spec && kind == K_HOT) {
                     const uint2 e = htab[hs * HOT_RANKS + r];
                     kind = (int)((e.x >> 15) & 7u);
@@ -1931,6 +2094,8 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                 }
 #endif
                 if (tid == 0) {
+                    sc[SC_LQN] = 0;  // the queue of this pass was drained before barrier 2
+                    sc[SC_LQH] = 0;
                     sc[SC_NHOT] = 0;  // read at the chunk start, before this pass's barriers
                     sc[SC_LMIN + (par ^ 1)] = OWGS_WL;
                     sc[SC_CFB + (par ^ 1)] = OWGS_WL;
