@@ -431,6 +431,8 @@ class GpuShardingContainerPoolBalancer:
             d["cycles"]["first_passes"] = d.pop("general_probes")
             d["cycles"]["later_passes"] = d.pop("general_lanes")
             walk = ["worst_long", "long_walks_worst_wave", "long_rounds", "conc_long", "conc_long_rounds",
-                    "full_walks", "full_walk_rounds", "hot_rounds", "cyc_rounds_c1", "cyc_rounds_conc"]
-            d["walks"] = {k: out[16 + i] for i, k in enumerate(walk)}
+                    "full_walks", "full_walk_rounds", "hot_rounds", "cyc_rounds_c1", "cyc_rounds_conc",
+                    "worst_scan_push", "worst_barrier8", "worst_queue"]
+            d["walks"] = {k: out[16 + i] for i, k in enumerate(walk[:10])}
+            d["walks"].update({k: out[28 + i] for i, k in enumerate(walk[10:])})
         return d

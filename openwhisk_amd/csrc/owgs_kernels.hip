@@ -72,6 +72,7 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
     u64 pt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
     u64 pw_c[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
     u64 pt_x[3] = {0, 0, 0};                  \
+    u64 sc_prof_q = 0;                        \
     u64 pt_t = memtime_pinned(); \
     int pt_on = 1;
 #define PT(k)                                        \
@@ -96,7 +97,7 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
 #define SC_CBWD 9   // 1 + the chunk that moved a concurrent action's HBM walk cursor backward (forced acquire)
 #define SC_LQN 10   // long walks queued in this pass
 #define SC_LQH 11   // next queued long walk to take
-#define SC_N (16 + 7 * OWGS_EW)
+#define SC_N (16 + 10 * OWGS_EW)
 
 // hot actions: every action with >= HOT_MIN lanes in a chunk gets a slot (assigned by the pre-pass; a concurrent
 // action only when no lane of the chunk shares its fqn@version with another action); per pass one wave walks its
@@ -1581,33 +1582,47 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                     u64 cm = __ballot(spec && kind == K_CSCAN);
                     int* cand = hscr + wave * 64;
                     while (cm) {
+                        // one scan serves every lane of the wave with the same action (same key and walk)
                         const int j = ffs64(cm);
-                        cm &= cm - 1;
+                        const int aj = __builtin_amdgcn_readlane(a, j);
+                        const u64 same = aj == (int)OWGS_REC_NOACT ? (1ull << j)  // explicit walks: one lane each
+                                                                   : (__ballot(spec && kind == K_CSCAN && a == aj) & cm);
+                        cm &= ~same;
                         const int slj = __builtin_amdgcn_readlane(slot, j);
-                        const int rj = __builtin_amdgcn_readlane(r, j);
                         const int pj = __builtin_amdgcn_readlane(pool, j);
                         const int nn = __builtin_amdgcn_readlane(n, j);
                         const int hj = __builtin_amdgcn_readlane(home, j);
                         const int stp = __builtin_amdgcn_readlane(step, j);
                         const int base = pj ? A.n_ids - nb : 0;
                         int nc = 0;
-                        for (int e0 = 0; e0 < OWGS_CTC && nc <= 64; e0 += 64) {
-                            const uint2 ev = ct[e0 + lane];
-                            const int inv = (int)(ev.x & 0x7FFFu) - 1;
-                            const int ps = inv - base;
-                            const bool m = (int)(ev.x >> OWGS_CT_SLOT_SHIFT) == slj && inv >= 0 && ps >= 0 && ps < nn &&
-                                           (ev.y & OWGS_CT_C_MASK) != 0u && P[inv] < OWGS_PLIM;
-                            const u64 bm = __ballot(m);
-                            const int at = nc + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
-                                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
-                            if (m && at < 64) cand[at] = e0 + lane;
-                            nc += __popcll(bm);
+                        constexpr int SCU = 8;  // table reads in flight per lane
+                        for (int e0 = 0; e0 < OWGS_CTC && nc <= 64; e0 += 64 * SCU) {
+                            uint2 ev[SCU];
+#pragma unroll
+                            for (int u = 0; u < SCU; ++u) ev[u] = ct[e0 + 64 * u + lane];
+#pragma unroll
+                            for (int u = 0; u < SCU; ++u) {
+                                const int inv = (int)(ev[u].x & 0x7FFFu) - 1;
+                                const int ps = inv - base;
+                                const bool m = (int)(ev[u].x >> OWGS_CT_SLOT_SHIFT) == slj && inv >= 0 && ps >= 0 &&
+                                               ps < nn && (ev[u].y & OWGS_CT_C_MASK) != 0u;
+                                const u64 bm0 = __ballot(m);
+                                if (bm0) {  // (rare) usable check only for the key's entries
+                                    const bool mu = m && P[inv] < OWGS_PLIM;
+                                    const u64 bm = __ballot(mu);
+                                    const int at = nc + (int)__builtin_amdgcn_mbcnt_hi(
+                                                            (uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+                                    if (mu && at < 64) cand[at] = e0 + 64 * u + lane;
+                                    nc += __popcll(bm);
+                                }
+                            }
                         }
-                        int rk = K_FALLBACK, rt = -1, rks = 0, rst = 0, rci = -1;
-                        uint32_t rcv = 0;
+                        int rk0 = K_FALLBACK, ix = -1, kx = 0x7FFFFFFF, cx = 0, idv = 0, before = 0;
+                        uint32_t vx = 0;
                         if (nc > 64) {
-                            rk = K_LONG;  // too many containers: walk
+                            rk0 = K_LONG;  // too many containers: walk
                         } else if (nc > 0) {
+                            rk0 = K_TARGET;
                             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                             // step^-1 mod n (gcd(step, n) = 1: pairwiseCoprimeNumbersUntil, SCPB:379-384)
                             int t0 = 0, t1 = 1, r0 = nn, r1 = stp % nn;
@@ -1622,8 +1637,6 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             }
                             const int sinv = t0 < 0 ? t0 + nn : t0;
                             const float rnn = __builtin_amdgcn_rcpf((float)nn);
-                            int ix = -1, kx = 0x7FFFFFFF, cx = 0, idv = 0;
-                            uint32_t vx = 0;
                             if (lane < nc) {
                                 ix = cand[lane];
                                 const uint2 ev = ct[ix];
@@ -1635,31 +1648,41 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                 kx = mod_fast(d * sinv, nn, rnn);  // d, sinv < n < 2^15
                             }
                             // free slots of the containers before this one in walk order (distinct steps)
-                            int before = 0;
                             for (int m2 = 0; m2 < nc; ++m2) {
                                 const int km = __builtin_amdgcn_readlane(kx, m2);
                                 const int cmv = __builtin_amdgcn_readlane(cx, m2);
                                 before += km < kx ? cmv : 0;
                             }
-                            const u64 hm = __ballot(lane < nc && before <= rj && rj < before + cx);
-                            if (hm) {
-                                const int L = ffs64(hm);
-                                rk = K_TARGET;
-                                rt = __builtin_amdgcn_readlane(idv, L);
-                                rks = rj - __builtin_amdgcn_readlane(before, L);
-                                rst = __builtin_amdgcn_readlane(kx, L);
-                                rci = __builtin_amdgcn_readlane(ix, L);
-                                rcv = (uint32_t)__builtin_amdgcn_readlane((int)vx, L);
-                            }
                             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                         }
-                        if (lane == j) {
-                            kind = rk;
-                            t = rt;
-                            ks = rks;
-                            s_t = rst;
-                            cidx = rci;
-                            cval = rcv;
+                        // each lane of the action: the container holding its rank
+                        for (u64 sm = same; sm;) {
+                            const int jj = ffs64(sm);
+                            sm &= sm - 1;
+                            const int rj = __builtin_amdgcn_readlane(r, jj);
+                            int rk = rk0, rt = -1, rks = 0, rst = 0, rci = -1;
+                            uint32_t rcv = 0;
+                            if (rk0 == K_TARGET) {
+                                const u64 hm = __ballot(lane < nc && before <= rj && rj < before + cx);
+                                if (hm) {
+                                    const int L = ffs64(hm);
+                                    rt = __builtin_amdgcn_readlane(idv, L);
+                                    rks = rj - __builtin_amdgcn_readlane(before, L);
+                                    rst = __builtin_amdgcn_readlane(kx, L);
+                                    rci = __builtin_amdgcn_readlane(ix, L);
+                                    rcv = (uint32_t)__builtin_amdgcn_readlane((int)vx, L);
+                                } else {
+                                    rk = K_FALLBACK;  // fewer free slots than ranks: the walk fails (SCPB:417)
+                                }
+                            }
+                            if (lane == jj) {
+                                kind = rk;
+                                t = rt;
+                                ks = rks;
+                                s_t = rst;
+                                cidx = rci;
+                                cval = rcv;
+                            }
                         }
                     }
                 }
@@ -1683,7 +1706,13 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         }
                     }
                 }
+#ifdef OWGS_PROFILE
+                const u64 ts_b8a = memtime_pinned();
+#endif
                 LDS_SYNC_T(8);
+#ifdef OWGS_PROFILE
+                const u64 ts_b8b = memtime_pinned();
+#endif
                 if (!io) {
                     const int nq = sc[SC_LQN];
                     for (;;) {
@@ -1837,6 +1866,9 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                     spw[4 * wave + 1] = (int)(ts_lane - ts_hot);
                     spw[4 * wave + 2] = (int)(ts_end - ts_lane);
                     spw[4 * wave + 3] = (int)pw_c[1];
+                    pfw[3 * OWGS_EW + 3 * wave] = (int)(ts_b8a - ts_lane);   // container scans + queue push
+                    pfw[3 * OWGS_EW + 3 * wave + 1] = (int)(ts_b8b - ts_b8a);  // barrier 8
+                    pfw[3 * OWGS_EW + 3 * wave + 2] = (int)(ts_end - ts_b8b);  // queued long walks
                     pfw[2 * wave] = pf_fw;
                     pfw[2 * wave + 1] = pf_gw;
                 }
@@ -1854,6 +1886,15 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                     pt_acc[6] += (u64)spw[4 * worst];       // worst wave: hot walks
                     pt_acc[7] += (u64)spw[4 * worst + 1];   // worst wave: per-lane speculation
                     pw_c[0] += (u64)spw[4 * worst + 2];     // worst wave: long walks (and imbalance)
+                    int mx0 = 0, mx1 = 0, mx2 = 0;
+                    for (int w = 0; w < OWGS_EW; ++w) {
+                        mx0 = max(mx0, pfw[3 * OWGS_EW + 3 * w]);
+                        mx1 = max(mx1, pfw[3 * OWGS_EW + 3 * w + 1]);
+                        mx2 = max(mx2, pfw[3 * OWGS_EW + 3 * w + 2]);
+                    }
+                    pw_c[10] += (u64)mx0;
+                    pw_c[11] += (u64)mx1;
+                    sc_prof_q += (u64)mx2;
                     int lwmax = 0;  // long walks of the wave with the most of them in this pass (counters cumulative)
                     for (int w = 0; w < OWGS_EW; ++w) {
                         lwmax = max(lwmax, spw[4 * w + 3] - pfw[2 * OWGS_EW + w]);
@@ -2150,8 +2191,11 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
         }
 #ifdef OWGS_PROFILE
         if (!io && lane == 0)
-            for (int k = 2; k < 12; ++k) atomicAdd(&A.stats[16 + k], pw_c[k]);
+            for (int k = 2; k < 10; ++k) atomicAdd(&A.stats[16 + k], pw_c[k]);
         if (tid == 0) {  // wave 0: marks sit right after barriers, so the intervals are the critical path
+            atomicAdd(&A.stats[28], pw_c[10]);
+            atomicAdd(&A.stats[29], pw_c[11]);
+            atomicAdd(&A.stats[30], sc_prof_q);
             atomicAdd(&A.stats[16], pw_c[0]);
             atomicAdd(&A.stats[17], pt_x[2]);
             for (int k = 0; k < 8; ++k) atomicAdd(&A.stats[8 + k], pt_acc[k]);
