@@ -26,6 +26,9 @@ extern "C" hipError_t owgs_launch_selftest(int* bad, int trials, hipStream_t s);
 extern "C" hipError_t owgs_launch_prepare(const OwgsPrepArgs* a, hipStream_t s);
 extern "C" hipError_t owgs_launch_prepass(const OwgsPrepassArgs* a, int32_t* cstart, int64_t max_chunks,
                                           hipStream_t s);
+extern "C" hipError_t owgs_launch_ovf_clear(const OwgsOvf* O, hipStream_t s);
+extern "C" hipError_t owgs_launch_ovf_rehash(const uint2* old_t, int32_t old_cap, const OwgsOvf* O, int32_t* err,
+                                            hipStream_t s);
 extern "C" hipError_t owgs_launch_relpos(const int64_t* rel_aid, int64_t n_rel, int64_t n_act, int32_t* relx,
                                          int32_t* err, hipStream_t s);
 extern "C" hipError_t owgs_launch_relflags(const int64_t* rel_aid, int64_t n_rel, const int32_t* out_inv,
@@ -141,6 +144,14 @@ struct owgs_ctx {
     DevBuf<uint8_t> d_act_bb, d_act_cok;
     DevBuf<uint2> d_act_meta;
     DevBuf<u64> d_stats;
+    // NestedSemaphore map overflow (keys beyond the LDS-sized primary table, owgs_internal.h OwgsOvf)
+    DevBuf<uint2> d_ovf, s_ovf;
+    DevBuf<uint32_t> d_ovf_rc;
+    DevBuf<int32_t> d_ovf_touched, d_ovf_cnt;  // d_ovf_cnt = {entries (live + deleted), touched count}
+    int32_t ovf_cap = 0;
+    int64_t ovf_used_ub = 0;  // host upper bound of the overflow's entries (exact after a read-back)
+    int32_t s_ovf_cnt = 0;    // snapshot: overflow entries (0: the snapshot had none)
+    int32_t s_ovf_cap = 0;
     DevBuf<uint32_t> d_margs;  // owgs_replay_device_multi: shard argument blocks beyond the kernarg segment
     void* h_margs = nullptr;   // pinned staging of d_margs (hipHostMalloc), h_margs_bytes long
     size_t h_margs_bytes = 0;
@@ -316,9 +327,68 @@ static int lds_check(owgs_ctx* c) {
     return OWGS_OK;
 }
 
+static OwgsOvf ovf_args(const owgs_ctx* c) {
+    OwgsOvf O{};
+    O.t = c->d_ovf.p;
+    O.cap = c->ovf_cap;
+    O.cnt = c->d_ovf_cnt.p;
+    O.rc = c->d_ovf_rc.p;
+    O.touched = c->d_ovf_touched.p;
+    O.n_touched = c->d_ovf_cnt.p ? c->d_ovf_cnt.p + 1 : nullptr;
+    return O;
+}
+
+// The overflow holds every key the primary cannot: at most the entries it has plus one per activation of the call
+// (an activation creates at most one (invoker, fqn) entry).  Keep it at least twice that (load <= 1/2); grow (and
+// rehash) when the bound says so -- after reading the exact entry count back once.
+static int ensure_ovf(owgs_ctx* c, int64_t n_new, hipStream_t s) {
+    auto need = [&](int64_t used) {
+        int64_t want = 2 * (used + n_new + OWGS_CTC), cap = 16384;
+        while (cap < want && cap < ((int64_t)1 << 30)) cap <<= 1;
+        return cap;
+    };
+    if (c->ovf_cap >= need(c->ovf_used_ub)) return OWGS_OK;
+    if (c->ovf_cap > 0) {  // exact entry count
+        int32_t cnt = 0;
+        HIPCHK(c, hipStreamSynchronize(s));
+        HIPCHK(c, hipMemcpy(&cnt, c->d_ovf_cnt.p, sizeof(cnt), hipMemcpyDeviceToHost));
+        c->ovf_used_ub = cnt;
+        if (c->ovf_cap >= need(cnt)) return OWGS_OK;
+    }
+    const int64_t cap = need(c->ovf_used_ub);
+    if (cap > ((int64_t)1 << 26)) return c->fail(OWGS_ENOMEM, "concurrency map overflow beyond 2^26 entries");
+    DevBuf<uint2> nt;
+    HIPCHK(c, nt.reserve((size_t)cap));
+    HIPCHK(c, hipMemsetAsync(nt.p, 0, (size_t)cap * sizeof(uint2), s));
+    HIPCHK(c, c->d_ovf_cnt.reserve(2));
+    if (c->ovf_cap == 0) HIPCHK(c, hipMemsetAsync(c->d_ovf_cnt.p, 0, 2 * sizeof(int32_t), s));
+    HIPCHK(c, c->d_ovf_rc.reserve((size_t)cap));
+    HIPCHK(c, hipMemsetAsync(c->d_ovf_rc.p, 0, (size_t)cap * sizeof(uint32_t), s));
+    HIPCHK(c, c->d_ovf_touched.reserve((size_t)cap));
+    HIPCHK(c, c->d_ct_tmp.reserve((size_t)2 * (OWGS_CTC + cap)));
+    if (c->ovf_cap > 0 && c->ovf_used_ub > 0) {  // live entries move to the larger table
+        OwgsOvf O = ovf_args(c);
+        O.t = nt.p;
+        O.cap = (int32_t)cap;
+        HIPCHK(c, hipMemsetAsync(c->d_ovf_cnt.p, 0, sizeof(int32_t), s));
+        HIPCHK(c, owgs_launch_ovf_rehash(c->d_ovf.p, c->ovf_cap, &O, c->d_err.p, s));
+    }
+    HIPCHK(c, hipStreamSynchronize(s));
+    c->d_ovf.release();
+    c->d_ovf = nt;
+    nt.p = nullptr;
+    c->ovf_cap = (int32_t)cap;
+    return OWGS_OK;
+}
+
 static int reset_ctab(owgs_ctx* c) {
     HIPCHK(c, hipMemsetAsync(c->d_ct_keys.p, 0, OWGS_CTC * sizeof(uint32_t), c->stream));
     HIPCHK(c, hipMemsetAsync(c->d_ct_vals.p, 0, OWGS_CTC * sizeof(uint32_t), c->stream));
+    if (c->ovf_cap > 0) {
+        const OwgsOvf O = ovf_args(c);
+        HIPCHK(c, owgs_launch_ovf_clear(&O, c->stream));
+    }
+    c->ovf_used_ub = 0;
     return OWGS_OK;
 }
 
@@ -339,6 +409,7 @@ static void base_args(owgs_ctx* c, OwgsEngineArgs& A) {
     A.ct_keys = c->d_ct_keys.p;
     A.ct_vals = c->d_ct_vals.p;
     A.ct_tmp = c->d_ct_tmp.p;
+    A.ovf = ovf_args(c);
     A.n_actions = (int32_t)c->a_mem.size();
     A.rng_seed = c->cfg.rng_seed;
     A.stats = c->d_stats.p;
@@ -413,6 +484,11 @@ static int run_prepass(owgs_ctx* c, OwgsEngineArgs& A, int32_t n_batches, const 
 static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s, bool launch = true) {
     int rc = lds_check(c);
     if (rc) return rc;
+    rc = ensure_ovf(c, A.n_act, s);
+    if (rc) return rc;
+    A.ovf = ovf_args(c);
+    A.ct_tmp = c->d_ct_tmp.p;
+    c->ovf_used_ub += A.n_act;
     // walk cursors: one tagged word per action; the tags of this launch's batches must not repeat a stored tag
     if (A.n_batches >= 0x1FFFF) return c->fail(OWGS_ERANGE, "more than 131070 batches in one call");
     const size_t na = (size_t)std::max(A.n_actions, 1);
@@ -543,6 +619,11 @@ void owgs_destroy(owgs_ctx* c) {
     c->d_act_meta.release();
     c->d_stats.release();
     c->d_margs.release();
+    c->d_ovf.release();
+    c->s_ovf.release();
+    c->d_ovf_rc.release();
+    c->d_ovf_touched.release();
+    c->d_ovf_cnt.release();
     if (c->h_margs) (void)hipHostFree(c->h_margs);
     c->h_margs = nullptr;
     if (c->ev_margs) (void)hipEventDestroy(c->ev_margs);
@@ -875,6 +956,7 @@ int owgs_release_batch(owgs_ctx* c, int32_t n, const int32_t* invoker, const int
     R.n_slots = c->n_slots;
     R.ct_keys = c->d_ct_keys.p;
     R.ct_vals = c->d_ct_vals.p;
+    R.ovf = ovf_args(c);
     R.n = n;
     R.inv = c->d_a.p;
     R.mem = c->d_b.p;
@@ -978,7 +1060,7 @@ int owgs_read_concurrent(owgs_ctx* c, int32_t invoker, int32_t key, int32_t* per
     HIPCHK(c, upload(di, &invoker, 1, c->stream));
     HIPCHK(c, upload(dk, &key, 1, c->stream));
     HIPCHK(c, dv.reserve(1));
-    OwgsLookupArgs la{c->d_ct_keys.p, c->d_ct_vals.p, di.p, dk.p, 1, dv.p};
+    OwgsLookupArgs la{c->d_ct_keys.p, c->d_ct_vals.p, ovf_args(c), di.p, dk.p, 1, dv.p};
     HIPCHK(c, owgs_launch_lookup(&la, c->stream));
     int2 v;
     HIPCHK(c, hipMemcpyAsync(&v, dv.p, sizeof(int2), hipMemcpyDeviceToHost, c->stream));
@@ -1181,6 +1263,15 @@ int owgs_snapshot(owgs_ctx* c) {
     HIPCHK(c, hipMemcpyAsync(c->s_ct_keys.p, c->d_ct_keys.p, OWGS_CTC * 4, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->s_ct_vals.p, c->d_ct_vals.p, OWGS_CTC * 4, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->s_ovf_cnt = 0;
+    if (c->ovf_cap > 0) {  // the overflow part of the map, when it holds entries
+        HIPCHK(c, hipMemcpy(&c->s_ovf_cnt, c->d_ovf_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost));
+        if (c->s_ovf_cnt > 0) {
+            HIPCHK(c, c->s_ovf.reserve((size_t)c->ovf_cap));
+            HIPCHK(c, hipMemcpy(c->s_ovf.p, c->d_ovf.p, (size_t)c->ovf_cap * sizeof(uint2), hipMemcpyDeviceToDevice));
+            c->s_ovf_cap = c->ovf_cap;
+        }
+    }
     c->has_snap = true;
     c->snap_slots = c->n_slots;
     return OWGS_OK;
@@ -1194,6 +1285,18 @@ int owgs_restore(owgs_ctx* c, void* stream) {
         HIPCHK(c, hipMemcpyAsync(c->d_permits.p, c->s_permits.p, (size_t)c->n_slots * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(c, hipMemcpyAsync(c->d_ct_keys.p, c->s_ct_keys.p, OWGS_CTC * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(c, hipMemcpyAsync(c->d_ct_vals.p, c->s_ct_vals.p, OWGS_CTC * 4, hipMemcpyDeviceToDevice, s));
+    if (c->ovf_cap > 0) {
+        const OwgsOvf O = ovf_args(c);
+        if (c->s_ovf_cnt > 0 && c->s_ovf_cap == c->ovf_cap) {
+            HIPCHK(c, hipMemcpyAsync(c->d_ovf.p, c->s_ovf.p, (size_t)c->ovf_cap * sizeof(uint2), hipMemcpyDeviceToDevice, s));
+            HIPCHK(c, hipMemcpyAsync(c->d_ovf_cnt.p, &c->s_ovf_cnt, sizeof(int32_t), hipMemcpyHostToDevice, s));
+        } else {
+            HIPCHK(c, owgs_launch_ovf_clear(&O, s));  // (a no-op kernel while the overflow is empty)
+            if (c->s_ovf_cnt > 0)  // the table grew since the snapshot: its entries are rehashed
+                HIPCHK(c, owgs_launch_ovf_rehash(c->s_ovf.p, c->s_ovf_cap, &O, c->d_err.p, s));
+        }
+    }
+    c->ovf_used_ub = c->s_ovf_cnt;
     return OWGS_OK;
 }
 
@@ -1384,6 +1487,7 @@ static int ack_complete(owgs_ctx* c, int32_t n, uint8_t* d_kind, int32_t* d_tick
     R.n_slots = c->n_slots;
     R.ct_keys = c->d_ct_keys.p;
     R.ct_vals = c->d_ct_vals.p;
+    R.ovf = ovf_args(c);
     R.n = n;
     R.inv = c->k_r0.p;
     R.mem = c->k_r1.p;

@@ -114,6 +114,21 @@
 #define OWGS_MULTI_MAX 8  // controller shards per owgs_engine_multi_kernel launch (kernarg: 8 x args)
 #define OWGS_MULTI_DEV_MAX 64  // owgs_engine_multi_dev_kernel: argument blocks in HBM
 
+// HBM overflow of the concurrency table: (invoker, fqn) keys that do not fit in the LDS-sized primary table (the
+// reference map is an unbounded TrieMap, NestedSemaphore.scala:30).  Open addressing over cap entries (power of two),
+// {key, value} as in the primary; key 0 = empty, OWGS_CT_TOMB = deleted.  A key lives in at most one of the two
+// tables; lookups fall through to the overflow only while it holds entries (cnt[0] > 0).  Every access goes through
+// L2 (device-scope atomics or L1-bypassing loads).
+#define OWGS_CT_LDS_FILL (OWGS_CTC - 256)  // primary entries (live + deleted) beyond which new keys go to the overflow
+struct OwgsOvf {
+    uint2* t;            // [cap]
+    int32_t cap;         // 0: no overflow table
+    int32_t* cnt;        // [0] non-empty entries (live + deleted)
+    uint32_t* rc;        // [cap] engine release phase: release count << 12 | maxConcurrent (zero between batches)
+    int32_t* touched;    // [cap] engine release phase: overflow entries released in the current batch
+    int32_t* n_touched;  // [1]
+};
+
 struct OwgsEngineArgs {
     int32_t* permits;
     int32_t n_slots;
@@ -127,7 +142,8 @@ struct OwgsEngineArgs {
     int32_t shortcut_ok;         // bit0 managed, bit1 blackbox: pool has no usable out-of-range id
     uint32_t* ct_keys;           // [OWGS_CTC] HBM image of the concurrency table
     uint32_t* ct_vals;
-    uint32_t* ct_tmp;            // [2 * OWGS_CTC] scratch for the table rebuild
+    uint32_t* ct_tmp;            // [2 * max(OWGS_CTC, ovf.cap)] scratch for the table rebuild
+    OwgsOvf ovf;
     int32_t n_actions;           // per-action LDS words (walk cursor + chunk rank base)
     // stream
     int32_t n_batches;
@@ -209,6 +225,7 @@ struct OwgsReleaseArgs {
     const int32_t* slot;
     uint8_t* flags;
     int32_t* err;
+    OwgsOvf ovf;
     // scratch of the parallel front end (owgs_launch_release_seq): per-invoker upper bound of the memory returned,
     // overflow-risk word, selection of the releases the ordered kernel still has to apply
     unsigned long long* bound;  // [n_slots]
@@ -231,6 +248,7 @@ struct OwgsReleaseArgs {
 struct OwgsLookupArgs {
     const uint32_t* ct_keys;
     const uint32_t* ct_vals;
+    OwgsOvf ovf;
     const int32_t* inv;
     const int32_t* slot;
     int32_t n;

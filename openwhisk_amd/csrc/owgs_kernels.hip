@@ -95,6 +95,7 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
 #define SC_NLIVE 7  // table rebuild: live entries
 #define SC_NHOT 8   // multi-lane actions of the current chunk (hot slots claimed)
 #define SC_CBWD 9   // 1 + the chunk that moved a concurrent action's HBM walk cursor backward (forced acquire)
+#define SC_OVF 13   // overflow-table entries (live + deleted), mirror of A.ovf.cnt[0]
 #define SC_LQN 10   // long walks queued in this pass
 #define SC_LQH 11   // next queued long walk to take
 #define SC_N (16 + 10 * OWGS_EW)
@@ -314,6 +315,77 @@ __device__ __forceinline__ int ct_insertv(uint2* ct, uint32_t key, int* fresh) {
     return -1;
 }
 
+// ------------------------------------------------------------------------------------------------ overflow table
+__device__ __forceinline__ uint2 ovf_ld(const uint2* t, int i) {
+    const u64 v = __hip_atomic_load((const u64*)&t[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+}
+__device__ __forceinline__ void ovf_st(uint2* t, int i, uint32_t k, uint32_t v) {
+    __hip_atomic_store((u64*)&t[i], (u64)k | ((u64)v << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ovf_st_val(uint2* t, int i, uint32_t v) {
+    __hip_atomic_store(&t[i].y, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// index of key in the overflow (or -1), *val its value (0 if absent); linear probing from its hash, an empty entry
+// ends the chain
+__device__ __forceinline__ int ovf_find(const OwgsOvf& O, uint32_t key, uint32_t* val) {
+    *val = 0u;
+    if (O.cap <= 0) return -1;
+    const uint32_t m = (uint32_t)O.cap - 1u;
+    uint32_t h = ct_hash(key) & m;
+    for (int p = 0; p < O.cap; ++p) {
+        const uint2 e = ovf_ld(O.t, (int)h);
+        if (e.x == key) {
+            *val = e.y;
+            return (int)h;
+        }
+        if (e.x == 0u) return -1;
+        h = (h + 1u) & m;
+    }
+    return -1;
+}
+// insert a key absent from both tables into the first empty or deleted entry of its chain (CAS on the key word)
+__device__ __forceinline__ int ovf_insert(const OwgsOvf& O, uint32_t key, uint32_t val) {
+    if (O.cap <= 0) return -1;
+    const uint32_t m = (uint32_t)O.cap - 1u;
+    uint32_t h = ct_hash(key) & m;
+    for (int p = 0; p < O.cap;) {
+        const uint32_t k = ovf_ld(O.t, (int)h).x;
+        if (k == 0u || k == OWGS_CT_TOMB) {
+            if (atomicCAS(&O.t[h].x, k, key) == k) {
+                ovf_st_val(O.t, (int)h, val);
+                return (int)h;
+            }
+            continue;  // lost the entry: re-read it
+        }
+        h = (h + 1u) & m;
+        ++p;
+    }
+    return -1;
+}
+
+// engine lookups over both tables: index < OWGS_CTC = primary (LDS), OWGS_CTC + j = overflow entry j
+__device__ __forceinline__ int ct_find2(const uint2* ct, const OwgsOvf& O, bool ovf_on, uint32_t key,
+                                        uint32_t* val) {
+    int i = ct_findv(ct, key, val);
+    if (i < 0 && ovf_on) {
+        const int j = ovf_find(O, key, val);
+        i = j >= 0 ? OWGS_CTC + j : -1;
+    }
+    return i;
+}
+// resolve a lookup whose first primary block was read already: st = ct_block's result (1 hit, 0 absent from the
+// primary, 2 chain continues)
+__device__ __forceinline__ int ct_resolve2(const uint2* ct, const OwgsOvf& O, bool ovf_on, int st, uint32_t key,
+                                           uint32_t h, uint32_t* val, int ci) {
+    if (st == 2) ci = ct_findv_from(ct, key, (h + CT_BLK) & (OWGS_CTC - 1), val);
+    if (ci < 0 && ovf_on) {
+        const int j = ovf_find(O, key, val);
+        ci = j >= 0 ? OWGS_CTC + j : -1;
+    }
+    return ci;
+}
+
 // min(floor(pv / m), CAPMAX) for pv >= 0, 0 when pv < m; float reciprocal + one correction (pv / m < 2^10)
 __device__ __forceinline__ int cap_of(int pv, int m, float rm) {
     if (pv < m) return 0;
@@ -471,8 +543,10 @@ __global__ __launch_bounds__(256) void owgs_hash_kernel(OwgsHashArgs a) {
 __global__ __launch_bounds__(256) void owgs_lookup_kernel(OwgsLookupArgs a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
-    const int ix = ct_find(a.ct_keys, ct_key(a.inv[i], a.slot[i]));
-    const uint32_t v = ix >= 0 ? a.ct_vals[ix] : 0u;
+    const uint32_t key = ct_key(a.inv[i], a.slot[i]);
+    const int ix = ct_find(a.ct_keys, key);
+    uint32_t v = ix >= 0 ? a.ct_vals[ix] : 0u;
+    if (ix < 0 && a.ovf.cap > 0 && *a.ovf.cnt > 0) ovf_find(a.ovf, key, &v);
     a.out[i] = make_int2((int)(v & OWGS_CT_C_MASK), (int)(v >> OWGS_CT_C_BITS));
 }
 
@@ -868,6 +942,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
             used += k != 0;
         }
         if (used) atomicAdd(&sc[SC_USED], used);
+        if (tid == 0 && A.ovf.cap > 0) sc[SC_OVF] = __hip_atomic_load(A.ovf.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     for (int i = tid; i < (int)(Y.uni_bytes / 4); i += OWGS_NT) ((uint32_t*)(L + Y.uni))[i] = 0u;
     lds_sync();
@@ -969,6 +1044,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
             if (!io) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             for (int ix = tid; ix < OWGS_CTC; ix += OWGS_NT) rc[ix] = 0u;
             lds_sync();
+            const bool rel_ovf = sc[SC_OVF] > 0;  // overflow table in use (uniform)
             if (!io) {
                 // the release records of batch b (rel_rec[rel_off[b] .. rel_off[b+1]), written when the released
                 // activations were decided): maxConcurrent == 1 -> ForcibleSemaphore.release (FS:117-120), summed
@@ -1002,14 +1078,24 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             continue;
                         }
                         uint32_t v;
-                        const int ix = ct_findv(ct, ct_key(inv, slot), &v);
+                        const int ix = ct_find2(ct, A.ovf, rel_ovf, ct_key(inv, slot), &v);
                         const int c0 = (int)(v & OWGS_CT_C_MASK), ops0 = (int)(v >> OWGS_CT_C_BITS);
                         if (ix < 0 || ops0 == 0) {
                             err |= OWGS_ERR_BAD_STREAM;  // NoSuchElementException (NS:103)
                             continue;
                         }
-                        const uint32_t q = atomicAdd(&rc[ix], 1u << 12) >> 12;
-                        if (q == 0) atomicOr(&rc[ix], (uint32_t)R);
+                        uint32_t q;
+                        if (ix < OWGS_CTC) {
+                            q = atomicAdd(&rc[ix], 1u << 12) >> 12;
+                            if (q == 0) atomicOr(&rc[ix], (uint32_t)R);
+                        } else {  // overflow entry: its counter in HBM, first release lists it for the apply step
+                            const int oj = ix - OWGS_CTC;
+                            q = atomicAdd(&A.ovf.rc[oj], 1u << 12) >> 12;
+                            if (q == 0) {
+                                atomicOr(&A.ovf.rc[oj], (uint32_t)R);
+                                A.ovf.touched[atomicAdd(A.ovf.n_touched, 1)] = oj;
+                            }
+                        }
                         if ((int)q >= ops0) {
                             err |= OWGS_ERR_BAD_STREAM;
                             continue;
@@ -1022,6 +1108,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                     }
                 }
             }
+            if (rel_ovf && !io) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // HBM counters landed
             lds_sync();
             if (!io) {  // apply the release counts: c1 = (c0 + j) mod R, ops1 = ops0 - j, removed at 0 (NS:109-111)
                 for (int ix = tid; ix < OWGS_CTC; ix += OWGS_ENT) {
@@ -1039,14 +1126,39 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         ct[ix].y = (uint32_t)((c0 + j) % R) | ((uint32_t)ops1 << OWGS_CT_C_BITS);
                     }
                 }
+                if (rel_ovf) {  // the overflow entries this batch released
+                    const int nt = __hip_atomic_load(A.ovf.n_touched, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    for (int i2 = tid; i2 < nt; i2 += OWGS_ENT) {
+                        const int oj = __hip_atomic_load(&A.ovf.touched[i2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const uint32_t v = __hip_atomic_load(&A.ovf.rc[oj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&A.ovf.rc[oj], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const int R = (int)(v & 0xFFFu);
+                        const uint32_t cv = ovf_ld(A.ovf.t, oj).y;
+                        const int c0 = (int)(cv & OWGS_CT_C_MASK), ops0 = (int)(cv >> OWGS_CT_C_BITS);
+                        const int j = min((int)(v >> 12), ops0);
+                        const int ops1 = ops0 - j;
+                        if (ops1 == 0) ovf_st(A.ovf.t, oj, OWGS_CT_TOMB, 0u);
+                        else ovf_st_val(A.ovf.t, oj, (uint32_t)((c0 + j) % R) | ((uint32_t)ops1 << OWGS_CT_C_BITS));
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                }
+            }
+            if (rel_ovf) {
+                lds_sync();
+                if (tid == 0) {
+                    __hip_atomic_store(A.ovf.n_touched, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                }
             }
         }
 
         // ============================================================ concurrency-table cleanup
-        // Deleted entries keep probe chains long; once live + deleted exceed half the table, the live entries are
-        // parked in HBM and re-inserted (batch boundary: the engine waves' stores have drained, see above).
+        // Deleted entries keep probe chains long; once live + deleted exceed half the primary (or half the overflow),
+        // the live entries of both tables are parked in HBM scratch and re-inserted: the primary takes up to 3/4 of its
+        // capacity, the rest goes to the overflow (batch boundary: the engine waves' stores have drained, see above).
         lds_sync();
-        if (sc[SC_USED] > OWGS_CTC / 2) {
+        if (sc[SC_USED] > OWGS_CTC / 2 || (A.ovf.cap > 0 && sc[SC_OVF] > A.ovf.cap / 2)) {
+            const bool had_ovf = sc[SC_OVF] > 0;
             if (!io) {
                 for (int ix = tid; ix < OWGS_CTC; ix += OWGS_ENT) {
                     const uint32_t k = ct[ix].x;
@@ -1056,6 +1168,16 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         A.ct_tmp[2 * j + 1] = ct[ix].y;
                     }
                 }
+                if (had_ovf)
+                    for (int ix = tid; ix < A.ovf.cap; ix += OWGS_ENT) {
+                        const uint2 e = ovf_ld(A.ovf.t, ix);
+                        if (e.x != 0u) ovf_st(A.ovf.t, ix, 0u, 0u);
+                        if (e.x != 0u && e.x != OWGS_CT_TOMB) {
+                            const int j = atomicAdd(&sc[SC_NLIVE], 1);
+                            A.ct_tmp[2 * j] = e.x;
+                            A.ct_tmp[2 * j + 1] = e.y;
+                        }
+                    }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             lds_sync();
@@ -1064,18 +1186,25 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                 ct[ix] = make_uint2(0u, 0u);
             }
             lds_sync();
+            const int nprim = min(nlive, 3 * OWGS_CTC / 4);  // the rest (a map beyond the primary) to the overflow
             if (!io) {
                 for (int j = tid; j < nlive; j += OWGS_ENT) {
                     const uint32_t k = __hip_atomic_load(&A.ct_tmp[2 * j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     const uint32_t v = __hip_atomic_load(&A.ct_tmp[2 * j + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    int fresh = 0;
-                    const int ix = ct_insertv(ct, k, &fresh);
-                    ct[ix].y = v;
+                    if (j < nprim) {
+                        int fresh = 0;
+                        const int ix = ct_insertv(ct, k, &fresh);
+                        ct[ix].y = v;
+                    } else if (ovf_insert(A.ovf, k, v) < 0) {
+                        err |= OWGS_ERR_CTAB_FULL;
+                    }
                 }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             }
             lds_sync();
             if (tid == 0) {
-                sc[SC_USED] = nlive;
+                sc[SC_USED] = nprim;
+                sc[SC_OVF] = nlive - nprim;
                 sc[SC_NLIVE] = 0;
             }
             lds_sync();
@@ -1220,6 +1349,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
             bool keep = false;
             while (f < len) {
                 ++st_pass;
+                const bool ovf_on = sc[SC_OVF] > 0;  // overflow keys exist: lookups fall through (uniform)
 #ifdef OWGS_PROFILE
                 const u64 tpass0 = memtime_pinned();
 #ifdef OWGS_PROF_LATER
@@ -1307,7 +1437,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                         cap = cap_bf(pv, hmem, rmh);
                                     } else {
                                         uint32_t v;
-                                        ct_findv(ct, ct_key(id, hslot), &v);
+                                        ct_find2(ct, A.ovf, ovf_on, ct_key(id, hslot), &v);
                                         cap = (int)(v & OWGS_CT_C_MASK) + min(cap_bf(pv, hmem, rmh) * hmc, CAPMAX);
                                     }
                                 }
@@ -1366,7 +1496,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             kind = K_HOT;
                         } else if (maxc == 1 && mem > U && ((A.shortcut_ok >> pool) & 1)) {
                             kind = K_FALLBACK;  // every usable permit < mem: the walk fails everywhere
-                        } else if (maxc > 1 && mem > U && A.pool_mode == 0 && n > OWGS_CTC / 2) {
+                        } else if (maxc > 1 && mem > U && A.pool_mode == 0 && n > OWGS_CTC / 2 && !ovf_on) {
                             kind = K_CSCAN;  // no invoker can open a container: capacity = the key's open ones
                             ws = s;          // (the ordinary walk's start, should the key have > 64 of them)
                             wpos = mod_fast(home + s * step, n, __builtin_amdgcn_rcpf((float)n));
@@ -1477,8 +1607,8 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                         uint32_t v = 0;
                                         int ci = -1;
                                         const int bst = ct_block(ea[k], eb[k], key, hx[k], &v, &ci);
-                                        if (bst == 2 && open && !fin) {
-                                            ci = ct_findv_from(ct, key, (hx[k] + CT_BLK) & (OWGS_CTC - 1), &v);
+                                        if ((bst == 2 || (bst == 0 && ovf_on)) && open && !fin) {
+                                            ci = ct_resolve2(ct, A.ovf, ovf_on, bst, key, hx[k], &v, ci);
 #ifdef OWGS_COUNT_CHAINS
                                             st_glane += 1u << 16;
 #endif
@@ -1536,7 +1666,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                         cap = cap_of(pv, mem, rm);
                                     } else {
                                         uint32_t v;
-                                        const int ci = ct_findv(ct, ct_key(id, slot), &v);
+                                        const int ci = ct_find2(ct, A.ovf, ovf_on, ct_key(id, slot), &v);
                                         cap = (int)(v & OWGS_CT_C_MASK) + min(cap_of(pv, mem, rm) * maxc, CAPMAX);
                                         if (cum + cap > r) {
                                             cval = v;
@@ -1806,8 +1936,9 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                     cap = (in && id[q] >= 0) ? cap_bf(pv[q], mj, rmj) : 0;
                                 } else if (in && id[q] >= 0) {
                                     const uint32_t key = ct_key(id[q], slj);
-                                    if (ct_block(ea[q], eb[q], key, hx[q], &v, &ci) == 2)
-                                        ci = ct_findv_from(ct, key, (hx[q] + CT_BLK) & (OWGS_CTC - 1), &v);
+                                    const int bst = ct_block(ea[q], eb[q], key, hx[q], &v, &ci);
+                                    if (bst == 2 || (bst == 0 && ovf_on))
+                                        ci = ct_resolve2(ct, A.ovf, ovf_on, bst, key, hx[q], &v, ci);
                                     cap = (int)(v & OWGS_CT_C_MASK) + min(cap_bf(pv[q], mj, rmj) * cj, CAPMAX);
                                 }
                                 const int inc = wave_incl_scan(cap);
@@ -1852,9 +1983,9 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             pw_c[6] += nr_;
                         }
 #endif
-                        if (lane == 0)  // kind | (t + 1) << 3 | ks << 19, s_t | (cidx + 1) << 15, cval
+                        if (lane == 0)  // kind | (t + 1) << 3 | ks << 19, s_t, cval, cidx + 1 (overflow indices: 32 bits)
                             lq[item] = make_uint4((uint32_t)rk | ((uint32_t)(rt + 1) << 3) | ((uint32_t)rks << 19),
-                                                  (uint32_t)rst | ((uint32_t)(rci + 1) << 15), rcv, 0u);
+                                                  (uint32_t)rst, rcv, (uint32_t)(rci + 1));
                     }
                 }
                 
@@ -1915,8 +2046,8 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                     kind = (int)(qe.x & 7u);
                     t = (int)((qe.x >> 3) & 0xFFFFu) - 1;
                     ks = (int)(qe.x >> 19);
-                    s_t = (int)(qe.y & 0x7FFFu);
-                    cidx = (int)(qe.y >> 15) - 1;
+                    s_t = (int)qe.y;
+                    cidx = (int)qe.w - 1;
                     cval = qe.z;
                 }
                 if (spec && kind == K_HOT) {
@@ -1927,7 +2058,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         ks = (int)((e.x >> 18) & OWGS_RMASK);
                         s_t = (int)e.y;
                         if (maxc > 1) {
-                            cidx = ct_findv(ct, ct_key(t, slot), &cval);
+                            cidx = ct_find2(ct, A.ovf, ovf_on, ct_key(t, slot), &cval);
                         }
                     }
                 }
@@ -1944,7 +2075,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
         } else {                                              \
             t = x_;                                           \
             if (maxc > 1) {                                   \
-                cidx = ct_findv(ct, ct_key(t, slot), &cval); \
+                cidx = ct_find2(ct, A.ovf, ovf_on, ct_key(t, slot), &cval); \
             }                                                 \
         }                                                     \
     }
@@ -2045,6 +2176,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                 PT(4);
                 // ------------------------------------------------ commit lanes [f, l)
                 int l = sc[SC_LMIN + par];
+                bool ovf_w = false;  // this lane wrote an overflow entry
 #ifdef OWGS_PROF_COMMIT
                 const u64 tc0 = memtime_pinned();
 #endif
@@ -2100,13 +2232,36 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             const int ops1 = ops0 + jn;
                             if (ops1 > OWGS_MAX_OPS) err |= OWGS_ERR_OPS;
                             int ix = cidx;
+                            const uint32_t key = ct_key(t, slot), nv = (uint32_t)c1 | ((uint32_t)ops1 << OWGS_CT_C_BITS);
                             if (ix < 0) {  // absent when speculated (a kept lane's group may have created it since)
-                                int fresh = 0;
-                                ix = ct_upsertv(ct, ct_key(t, slot), &fresh);
-                                if (fresh) atomicAdd(&sc[SC_USED], 1);
+                                uint32_t vv;
+                                if (ovf_on) {
+                                    const int oj = ovf_find(A.ovf, key, &vv);
+                                    if (oj >= 0) ix = OWGS_CTC + oj;
+                                }
+                                if (ix < 0) {
+                                    if (sc[SC_USED] < OWGS_CT_LDS_FILL || A.ovf.cap <= 0) {  // find or insert
+                                        int fresh = 0;
+                                        ix = ct_upsertv(ct, key, &fresh);
+                                        if (fresh) atomicAdd(&sc[SC_USED], 1);
+                                    } else {
+                                        ix = ct_findv(ct, key, &vv);  // the nearly full primary may hold it
+                                    }
+                                }
+                                if (ix < 0 && A.ovf.cap > 0) {  // the primary is full: the key goes to the overflow
+                                    const int oj = ovf_insert(A.ovf, key, nv);
+                                    if (oj >= 0) {
+                                        ix = OWGS_CTC + oj;
+                                        atomicAdd(&sc[SC_OVF], 1);
+                                    }
+                                }
                             }
                             if (ix < 0) err |= OWGS_ERR_CTAB_FULL;
-                            else ct[ix].y = (uint32_t)c1 | ((uint32_t)ops1 << OWGS_CT_C_BITS);
+                            else if (ix < OWGS_CTC) ct[ix].y = nv;
+                            else {
+                                ovf_st_val(A.ovf.t, ix - OWGS_CTC, nv);
+                                ovf_w = true;
+                            }
                         }
                     }
                     // a failed full walk at rank 0 proves every usable permit of the pool < mem from now on
@@ -2142,6 +2297,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                     sc[SC_CFB + (par ^ 1)] = OWGS_WL;
                     if (l < len) ++st_stop;
                 }
+                if (!io && __ballot(ovf_w)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // visible next pass
                 LDS_SYNC_T(5);
                 PT(5);
 #ifdef OWGS_PROFILE
@@ -2173,6 +2329,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
         const int v = P[i];
         A.permits[i] = v >= OWGS_PLIM ? v - OWGS_PENC : v;
     }
+    if (tid == 0 && A.ovf.cap > 0) __hip_atomic_store(A.ovf.cnt, sc[SC_OVF], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int i = tid; i < OWGS_CTC; i += OWGS_NT) {
         const uint2 e = ct[i];
         A.ct_keys[i] = e.x;
@@ -2247,6 +2404,8 @@ __global__ __launch_bounds__(256) void owgs_rel_check_kernel(OwgsReleaseArgs R) 
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= R.n_slots) return;
     if ((long long)R.permits[i] + (long long)R.bound[i] > 0x7FFFFFFFll) atomicOr(R.risk, 1);
+    // keys in the overflow table: every release takes the ordered kernel (the grouped front end indexes the primary)
+    if (i == 0 && R.ovf.cap > 0 && *R.ovf.cnt > 0) atomicOr(R.risk, 1);
 }
 __global__ __launch_bounds__(256) void owgs_rel_apply_kernel(OwgsReleaseArgs R) {
     const int r = blockIdx.x * 256 + threadIdx.x;
@@ -2333,6 +2492,7 @@ __global__ __launch_bounds__(64) void owgs_release_seq_kernel(OwgsReleaseArgs R)
     __syncthreads();
     const u64 lt_mask = lane == 0 ? 0ull : ((~0ull) >> (64 - lane));
     const int n_sel = *R.sel_cnt;
+    const bool ovf_on = R.ovf.cap > 0 && *R.ovf.cnt > 0;
     for (int k0 = 0; k0 < n_sel; k0 += 64) {
         const bool valid = k0 + lane < n_sel;
         const int r = valid ? R.sel_idx[k0 + lane] : 0;
@@ -2353,8 +2513,13 @@ __global__ __launch_bounds__(64) void owgs_release_seq_kernel(OwgsReleaseArgs R)
         }
         int ix = -1, c0 = 0, o0 = 0;
         if (conc) {
-            ix = ct_find(ctk, ct_key(inv, slot));
-            const uint32_t v = ix >= 0 ? ctv[ix] : 0u;
+            const uint32_t key = ct_key(inv, slot);
+            ix = ct_find(ctk, key);
+            uint32_t v = ix >= 0 ? ctv[ix] : 0u;
+            if (ix < 0 && ovf_on) {  // overflow entries are indexed past the primary
+                const int oj = ovf_find(R.ovf, key, &v);
+                ix = oj >= 0 ? OWGS_CTC + oj : -1;
+            }
             c0 = (int)(v & OWGS_CT_C_MASK);
             o0 = (int)(v >> OWGS_CT_C_BITS);
             if (ix < 0 || o0 <= 0) {
@@ -2381,11 +2546,15 @@ __global__ __launch_bounds__(64) void owgs_release_seq_kernel(OwgsReleaseArgs R)
             if (rank == 0) {
                 const int j = min(gsz, o0);
                 const int o1 = o0 - j;
-                if (o1 == 0) {
+                const uint32_t nv = (uint32_t)((c0 + j) % maxc) | ((uint32_t)o1 << OWGS_CT_C_BITS);
+                if (ix >= OWGS_CTC) {
+                    if (o1 == 0) ovf_st(R.ovf.t, ix - OWGS_CTC, OWGS_CT_TOMB, 0u);
+                    else ovf_st_val(R.ovf.t, ix - OWGS_CTC, nv);
+                } else if (o1 == 0) {
                     ctk[ix] = OWGS_CT_TOMB;
                     ctv[ix] = 0u;
                 } else {
-                    ctv[ix] = (uint32_t)((c0 + j) % maxc) | ((uint32_t)o1 << OWGS_CT_C_BITS);
+                    ctv[ix] = nv;
                 }
             }
         }
@@ -2467,6 +2636,37 @@ extern "C" hipError_t owgs_launch_prepass(const OwgsPrepassArgs* a, int32_t* cst
     OwgsPrepassArgs b = *a;
     b.cstart = cstart;
     hipLaunchKernelGGL(owgs_prepass_kernel, dim3((unsigned)max_chunks), dim3(OWGS_WL), 0, s, b);
+    return hipGetLastError();
+}
+
+// overflow table maintenance (host-driven): clear it when it holds entries; rehash its live entries into a larger one
+__global__ __launch_bounds__(256) void owgs_ovf_clear_kernel(OwgsOvf O) {
+    if (__hip_atomic_load(O.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < O.cap; i += (int64_t)gridDim.x * 256)
+        O.t[i] = make_uint2(0u, 0u);
+}
+__global__ __launch_bounds__(256) void owgs_ovf_rehash_kernel(const uint2* old_t, int32_t old_cap, OwgsOvf O,
+                                                              int32_t* err) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= old_cap) return;
+    const uint2 e = old_t[i];
+    if (e.x == 0u || e.x == OWGS_CT_TOMB) return;
+    if (ovf_insert(O, e.x, e.y) < 0) atomicOr(err, OWGS_ERR_CTAB_FULL);
+    else atomicAdd(O.cnt, 1);
+}
+extern "C" hipError_t owgs_launch_ovf_clear(const OwgsOvf* O, hipStream_t s) {
+    if (O->cap <= 0) return hipSuccess;
+    hipLaunchKernelGGL(owgs_ovf_clear_kernel, dim3((unsigned)std::min<int64_t>(1024, (O->cap + 255) / 256)), dim3(256),
+                       0, s, *O);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemsetAsync(O->cnt, 0, sizeof(int32_t), s);
+    return e;
+}
+extern "C" hipError_t owgs_launch_ovf_rehash(const uint2* old_t, int32_t old_cap, const OwgsOvf* O, int32_t* err,
+                                            hipStream_t s) {
+    if (old_cap > 0)
+        hipLaunchKernelGGL(owgs_ovf_rehash_kernel, dim3((unsigned)((old_cap + 255) / 256)), dim3(256), 0, s, old_t,
+                           old_cap, *O, err);
     return hipGetLastError();
 }
 

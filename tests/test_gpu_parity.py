@@ -376,3 +376,46 @@ def test_multi_shard_single_launch_parity(shard_ids, n_shards, n_act):
             assert np.array_equal(o_fl, d[5].cpu().numpy())
             assert np.array_equal(o_rf, d[6].cpu().numpy()[: len(o_rf)])
             assert np.array_equal(st.permits(), b.permits())
+
+
+# ----------------------------------------------------------------------------------------------- unbounded map
+@pytest.mark.parametrize("kw", [
+    # up to 19.5k live (invoker, fqn) entries: most of the map lives in the HBM overflow
+    dict(n_activations=150_000, n_invokers=3000, n_actions=12_000, n_namespaces=1200, conc_frac=1.0, conc_range=(2, 2),
+         delay_mean=6.0, unhealthy_frac=0.0, blackbox_frac=0.0, zipf_s=0.6),
+    # ~6.7k live entries: the primary table fills and spills mid-batch
+    dict(n_activations=60_000, n_invokers=3000, n_actions=6000, n_namespaces=600, conc_frac=1.0, conc_range=(2, 3),
+         delay_mean=6.0, unhealthy_frac=0.0, blackbox_frac=0.0),
+])
+def test_concurrency_map_beyond_the_primary_table(kw):
+    """The reference keeps one TrieMap entry per (invoker, fqn@version) with no cap (NestedSemaphore.scala:30, 61-62).
+    Streams whose live entries exceed the engine's 4096-entry on-chip table continue in the HBM overflow: decisions,
+    flags and final permits bit-exact with the oracle, the surviving entries readable (concurrentState), and a
+    restore() + second replay repeats everything (the overflow is part of the snapshot)."""
+    w = W.config("headline", **kw)
+    st = O.state_for(w, zombies=False)
+    o_inv, o_fl, o_rf = st.replay(w.stream)
+    b = gpu_for(w)
+    b.snapshot()
+    for rep in range(2):
+        if rep:
+            b.restore()
+        g_inv, g_fl, g_rf = b.replay(w.stream)
+        bad = np.nonzero(o_inv != g_inv)[0]
+        assert len(bad) == 0, f"rep {rep}: first mismatch at {bad[:5]}"
+        assert np.array_equal(o_fl, g_fl) and np.array_equal(o_rf, g_rf)
+        assert np.array_equal(st.permits(), b.permits())
+    # NestedSemaphore.concurrentState of a sample of the keys that remain
+    keys = {}
+    for a in w.actions:
+        keys.setdefault(a.key, len(keys))
+    sl = st.invoker_slots
+    rng = np.random.default_rng(0)
+    checked = 0
+    for inv in rng.choice(len(sl), size=200, replace=False):
+        for k in rng.choice(len(keys), size=40, replace=False):
+            o = sl[int(inv)].concurrent_state(int(k))
+            g = b.concurrent_state(int(inv), int(k))
+            assert o == g, (inv, k, o, g)
+            checked += o is not None
+    assert checked > 0
