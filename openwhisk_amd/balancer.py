@@ -435,4 +435,6 @@ class GpuShardingContainerPoolBalancer:
                     "worst_scan_push", "worst_barrier8", "worst_queue"]
             d["walks"] = {k: out[16 + i] for i, k in enumerate(walk[:10])}
             d["walks"].update({k: out[28 + i] for i, k in enumerate(walk[10:])})
+            d["cycles"]["rel_sweep"] = out[26]
+            d["cycles"]["ct_rebuild"] = out[27]
         return d

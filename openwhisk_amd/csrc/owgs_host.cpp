@@ -29,8 +29,7 @@ extern "C" hipError_t owgs_launch_prepass(const OwgsPrepassArgs* a, int32_t* cst
 extern "C" hipError_t owgs_launch_ovf_clear(const OwgsOvf* O, hipStream_t s);
 extern "C" hipError_t owgs_launch_ovf_rehash(const uint2* old_t, int32_t old_cap, const OwgsOvf* O, int32_t* err,
                                             hipStream_t s);
-extern "C" hipError_t owgs_launch_relpos(const int64_t* rel_aid, int64_t n_rel, int64_t n_act, int32_t* relx,
-                                         int32_t* err, hipStream_t s);
+extern "C" hipError_t owgs_launch_relpos(const OwgsRelposArgs* a, hipStream_t s);
 extern "C" hipError_t owgs_launch_relflags(const int64_t* rel_aid, int64_t n_rel, const int32_t* out_inv,
                                            uint8_t* rel_flags, hipStream_t s);
 extern "C" hipError_t owgs_launch_release_seq(const OwgsReleaseArgs* a, hipStream_t s);
@@ -159,7 +158,7 @@ struct owgs_ctx {
     bool ev_margs_valid = false;
     // per-call scratch
     DevBuf<int64_t> d_off;
-    DevBuf<int32_t> d_a, d_b, d_c, d_d, d_out, d_cstart, d_relx, d_xslot;
+    DevBuf<int32_t> d_a, d_b, d_c, d_d, d_out, d_cstart, d_relx, d_relcnt, d_xslot;
     DevBuf<uint8_t> d_flags, d_rflags;
     DevBuf<u64> d_seq;
     DevBuf<int64_t> d_rel;
@@ -610,7 +609,7 @@ void owgs_destroy(owgs_ctx* c) {
     DevBuf<int32_t>* i32s[] = {&c->d_permits, &c->d_pool_words, &c->d_hlist, &c->d_act_slot, &c->d_act_hash,
                                &c->d_act_mem,  &c->d_act_maxc,   &c->d_steps,  &c->d_cpx,     &c->d_err,
                                &c->d_a,        &c->d_b,          &c->d_c,      &c->d_d,        &c->d_out,
-                               &c->d_cstart,   &c->d_relx,       &c->d_xslot,  &c->s_permits};
+                               &c->d_cstart,   &c->d_relx,       &c->d_relcnt, &c->d_xslot,  &c->s_permits};
     for (auto* b : i32s) b->release();
     DevBuf<uint32_t>* u32s[] = {&c->d_usable, &c->d_ct_keys, &c->d_ct_vals, &c->d_ct_tmp, &c->s_ct_keys, &c->s_ct_vals};
     for (auto* b : u32s) b->release();
@@ -1209,9 +1208,23 @@ static int replay_begin(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, 
         // reads as "no ActivationEntry"
         HIPCHK(c, hipMemsetAsync(c->d_rel_rec.p, 0xFF, (size_t)nr * sizeof(uint2), hs));
         if (rel_flags && n_releases) HIPCHK(c, hipMemsetAsync(rel_flags, 0, (size_t)n_releases, hs));
-        HIPCHK(c, owgs_launch_relpos(rel_aid, n_releases, n_activations, c->d_relx.p, c->d_err.p, hs));
+        HIPCHK(c, c->d_relcnt.reserve((size_t)2 * n_batches));
+        HIPCHK(c, hipMemsetAsync(c->d_relcnt.p, 0, (size_t)2 * n_batches * 4, hs));
+        OwgsRelposArgs ra{};
+        ra.rel_aid = rel_aid;
+        ra.n_rel = n_releases;
+        ra.n_act = n_activations;
+        ra.rel_off = rel_off;
+        ra.n_batches = n_batches;
+        ra.act = act;
+        ra.act_meta = c->d_act_meta.p;
+        ra.relx = c->d_relx.p;
+        ra.relcnt = c->d_relcnt.p;
+        ra.err = c->d_err.p;
+        HIPCHK(c, owgs_launch_relpos(&ra, hs));
         A.rel_off = rel_off;
         A.relpos = c->d_relx.p;
+        A.relcnt = c->d_relcnt.p;
         A.rel_rec = c->d_rel_rec.p;
     }
     return run_engine(c, A, hs, launch);

@@ -25,7 +25,9 @@
 //                                 action << 16 (the lane that holds the action's chunk cursor word)
 //   gcur[n_actions]         u32  walk cursor of each action (first walk step that may still fit) | batch tag << 15,
 //                                 written by the engine, gathered into LDS a chunk ahead by the I/O wave
-//   relx[n_act]             i32  position r of the activation's release in rel_aid, -1 never released
+//   relx[n_act]             i32  position of the activation's release record, -1 never released: inside its batch's
+//                                 range rel_off[b] .. rel_off[b+1], maxConcurrent == 1 releases first (relcnt[2b]
+//                                 of them), concurrent ones after (order inside a class is free)
 //   rel_rec[n_rel]          u32x2 written by the engine when the released activation is decided: {inv | mem << 15,
 //                                 slot | maxConcurrent << 17}; inv 0x7FFF = no ActivationEntry (CLB:278-279).  Batch b
 //                                 applies rel_rec[rel_off[b] .. rel_off[b+1]) before its publishes.
@@ -155,6 +157,7 @@ struct OwgsEngineArgs {
     uint32_t* gcur;              // [max(n_actions, 1)] walk cursor of each action: batch tag << 15 | step
     int32_t cur_tag0;            // batch b of this launch tags its cursors (cur_tag0 + b + 1) & 0x1FFFF
     const int32_t* relpos;       // [n_act] relx (see above), or null: no releases
+    const int32_t* relcnt;       // [2 * n_batches] per batch: maxConcurrent == 1 records, concurrent records
     uint2* rel_rec;              // [n_rel] release records, in rel_aid order (written when the activation is decided)
     unsigned long long seq_base;
     const unsigned long long* seq; // optional explicit seq per activation
@@ -197,6 +200,18 @@ struct OwgsPrepArgs {
 };
 
 // chunk-local pre-pass: one workgroup of OWGS_WL threads per chunk
+struct OwgsRelposArgs {
+    const int64_t* rel_aid;      // [n_rel]
+    int64_t n_rel, n_act;
+    const int64_t* rel_off;      // [n_batches + 1]
+    int32_t n_batches;
+    const int32_t* act;          // [n_act] action per activation
+    const uint2* act_meta;       // [n_actions]
+    int32_t* relx;               // out [n_act] (memset -1)
+    int32_t* relcnt;             // out [2 * n_batches] (memset 0)
+    int32_t* err;
+};
+
 struct OwgsPrepassArgs {
     int32_t n_batches;
     const int64_t* acq_off;

@@ -43,6 +43,18 @@ typedef unsigned long long u64;
 #define K_LONG 4
 #define K_HOT 5  // resolved from the hot-action rank table after the pass barrier
 #define K_CSCAN 6  // concurrent action, mem > every usable permit count: resolved from the key's open containers
+#ifndef OWGS_REL_RQ
+#define OWGS_REL_RQ 4  // release sweep: 16-byte reads in flight per thread, concurrent records
+#endif
+#ifndef OWGS_REL_RQ1
+#define OWGS_REL_RQ1 8  // maxConcurrent == 1 records
+#endif
+#ifndef OWGS_OVF
+#define OWGS_OVF 1  // 0: measurement variant without the overflow table's fall-through paths
+#endif
+#ifndef OWGS_CSCAN_ON
+#define OWGS_CSCAN_ON 1
+#endif
 
 #ifndef KPROBE
 #define KPROBE 16  // walk steps a maxConcurrent==1 lane probes on its own before the wave-cooperative walk (x4)
@@ -72,6 +84,7 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
     u64 pt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
     u64 pw_c[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
     u64 pt_x[3] = {0, 0, 0};                  \
+    u64 pt_y[2] = {0, 0};                     \
     u64 sc_prof_q = 0;                        \
     u64 pt_t = memtime_pinned(); \
     int pt_on = 1;
@@ -96,6 +109,7 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
 #define SC_NHOT 8   // multi-lane actions of the current chunk (hot slots claimed)
 #define SC_CBWD 9   // 1 + the chunk that moved a concurrent action's HBM walk cursor backward (forced acquire)
 #define SC_OVF 13   // overflow-table entries (live + deleted), mirror of A.ovf.cnt[0]
+#define SC_CLAST 12  // primary entries (live) right after the last table rebuild
 #define SC_LQN 10   // long walks queued in this pass
 #define SC_LQH 11   // next queued long walk to take
 #define SC_N (16 + 10 * OWGS_EW)
@@ -775,12 +789,53 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
 // release batch, so the engine reads batch b's records rel_rec[rel_off[b] .. rel_off[b+1]) contiguously).  An
 // activation released twice, or a release id outside the stream, is a malformed stream (the reference's
 // activationSlots.remove would find no entry the second time, CLB:278-279; replays take CommonLoadBalancer's streams).
-__global__ __launch_bounds__(256) void owgs_relpos_kernel(const int64_t* rel_aid, int64_t n_rel, int64_t n_act,
-                                                          int32_t* relx, int32_t* err) {
+// Inside batch b's range the records are placed by class: releases of maxConcurrent == 1 actions from the front
+// (relcnt[b] of them), concurrent ones from the back, so the engine's sweep runs the plain permit return over the first
+// part without the concurrency-map path (order inside a batch is free: permit sums commute, and a concurrent release's
+// effect depends only on its rank among the releases of its entry).  One atomic per wave and (batch, class).
+__global__ __launch_bounds__(256) void owgs_relpos_kernel(OwgsRelposArgs R) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n_rel) return;
-    const int64_t aid = rel_aid[r];
-    if (aid < 0 || aid >= n_act || atomicCAS(&relx[aid], -1, (int32_t)r) != -1) atomicOr(err, OWGS_ERR_BAD_STREAM);
+    const int lane = threadIdx.x & 63;
+    bool live = r < R.n_rel;
+    int64_t aid = -1;
+    int b = 0, cls = 0;
+    if (live) {
+        aid = R.rel_aid[r];
+        if (aid < 0 || aid >= R.n_act) {
+            atomicOr(R.err, OWGS_ERR_BAD_STREAM);
+            live = false;
+        } else {
+            int lo = 0, hi = R.n_batches - 1;  // last batch with rel_off[b] <= r
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (R.rel_off[mid] <= r) lo = mid;
+                else hi = mid - 1;
+            }
+            b = lo;
+            const uint2 m = R.act_meta[R.act[aid]];
+            cls = ((m.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK) > 1 ? 1 : 0;
+        }
+    }
+    int64_t pos = -1;
+    for (u64 todo = __ballot(live); todo;) {
+        const int b0 = __builtin_amdgcn_readlane(b, (int)__builtin_ctzll(todo));
+        const bool sel = live && b == b0;
+        const u64 m0 = __ballot(sel && cls == 0), m1 = __ballot(sel && cls == 1);
+        int base0 = 0, base1 = 0;
+        if (lane == (int)__builtin_ctzll(todo)) {
+            if (m0) base0 = atomicAdd(&R.relcnt[2 * b0], __popcll(m0));
+            if (m1) base1 = atomicAdd(&R.relcnt[2 * b0 + 1], __popcll(m1));
+        }
+        base0 = __shfl(base0, (int)__builtin_ctzll(todo), 64);
+        base1 = __shfl(base1, (int)__builtin_ctzll(todo), 64);
+        if (sel) {
+            const u64 mm = cls ? m1 : m0;
+            const int rk = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+            pos = cls ? R.rel_off[b0 + 1] - 1 - (base1 + rk) : R.rel_off[b0] + base0 + rk;
+        }
+        todo &= ~(m0 | m1);
+    }
+    if (live && atomicCAS(&R.relx[aid], -1, (int32_t)pos) != -1) atomicOr(R.err, OWGS_ERR_BAD_STREAM);
 }
 
 // per-release flags after a replay: the activation was never scheduled -> no ActivationEntry (CLB:278-279)
@@ -1038,43 +1093,78 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
         const int64_t a_beg = A.acq_off[b], a_end = A.acq_off[b + 1];
 
         // ============================================================ releases of batch b (SCPB:327-331)
+#ifdef OWGS_PROFILE
+        const u64 tb0 = memtime_pinned();
+#endif
         if (A.rel_off) {
             // the engine's own stores (decisions, aggregated releases, release records) of earlier batches land;
             // the release counters share LDS with the publish-phase scratch: clear them
             if (!io) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             for (int ix = tid; ix < OWGS_CTC; ix += OWGS_NT) rc[ix] = 0u;
             lds_sync();
-            const bool rel_ovf = sc[SC_OVF] > 0;  // overflow table in use (uniform)
+            const bool rel_ovf = OWGS_OVF && sc[SC_OVF] > 0;  // overflow table in use (uniform)
             if (!io) {
                 // the release records of batch b (rel_rec[rel_off[b] .. rel_off[b+1]), written when the released
                 // activations were decided): maxConcurrent == 1 -> ForcibleSemaphore.release (FS:117-120), summed
                 // per invoker with LDS atomics (the sum of releases is order-free); concurrent ->
                 // RS.release(1, true) per release (NS:98-113): the count per entry decides the final state, each
                 // release's memory return depends only on its rank (c0 + q + 1) % R == 0
+                // (this CU may hold lines of these records in its L1 from an earlier batch's read of the
+                // neighbouring records: invalidate it once, then the records stream through it)
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 const int64_t cb = A.rel_off[b], ce = A.rel_off[b + 1];
-                for (int64_t r0 = cb + tid; r0 < ce; r0 += 8 * OWGS_ENT) {
-                    u64 rr[8];
+                const int64_t cm = cb + A.relcnt[2 * b];  // [cb, cm): maxConcurrent == 1, [cm, ce): concurrent
+                // maxConcurrent == 1: 16-byte reads (two records), OWGS_REL_RQ1 of them in flight per thread (the
+                // sweep is latency-bound), a permit add per record
+                {
+                    constexpr int RQ = OWGS_REL_RQ1;
+                    const int64_t pb = cb >> 1, pe = (cm + 1) >> 1;
+                    for (int64_t p0 = pb + tid; p0 < pe; p0 += RQ * OWGS_ENT) {
+                        uint4 rp[RQ];
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const int64_t r = r0 + (int64_t)k * OWGS_ENT;
-                        rr[k] = r < ce ? __hip_atomic_load((const u64*)&A.rel_rec[r], __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT)
-                                       : 0ull;
+                        for (int k = 0; k < RQ; ++k) {
+                            const int64_t pp = p0 + (int64_t)k * OWGS_ENT;
+                            rp[k] = pp < pe ? ((const uint4*)A.rel_rec)[pp] : make_uint4(~0u, ~0u, ~0u, ~0u);
+                        }
+#pragma unroll
+                        for (int k = 0; k < 2 * RQ; ++k) {
+                            const int64_t r = 2 * (p0 + (int64_t)(k >> 1) * OWGS_ENT) + (k & 1);
+                            const uint32_t lo = (k & 1) ? rp[k >> 1].z : rp[k >> 1].x;
+                            const uint32_t hi = (k & 1) ? rp[k >> 1].w : rp[k >> 1].y;
+                            const int inv = (int)(lo & 0x7FFFu);
+                            if (r < cb || r >= cm || inv == (int)OWGS_RR_NOINV || inv >= n_slots) continue;
+                            if (((hi >> 17) & OWGS_AM_MAXC_MASK) > 1u) err |= OWGS_ERR_BAD_STREAM;  // (not its class)
+                            else atomicAdd(&P[inv], (int)(lo >> 15));  // FS:117-120 (range check: per-batch bounds)
+                        }
+                    }
+                }
+                // concurrent: RS.release(1, true) per release through the concurrency map
+                constexpr int RQ = OWGS_REL_RQ;
+                const int64_t pb = cm >> 1, pe = (ce + 1) >> 1;
+                for (int64_t p0 = pb + tid; p0 < pe; p0 += RQ * OWGS_ENT) {
+                    uint4 rp[RQ];
+#pragma unroll
+                    for (int k = 0; k < RQ; ++k) {
+                        const int64_t pp = p0 + (int64_t)k * OWGS_ENT;
+                        rp[k] = pp < pe ? ((const uint4*)A.rel_rec)[pp] : make_uint4(0u, 0u, 0u, 0u);
+                    }
+                    u64 rr[2 * RQ];
+#pragma unroll
+                    for (int k = 0; k < RQ; ++k) {
+                        const int64_t r = 2 * (p0 + (int64_t)k * OWGS_ENT);
+                        rr[2 * k] = (r >= cm && r < ce) ? ((u64)rp[k].y << 32 | rp[k].x) : ~0ull;
+                        rr[2 * k + 1] = (r + 1 >= cm && r + 1 < ce) ? ((u64)rp[k].w << 32 | rp[k].z) : ~0ull;
                     }
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const int64_t r = r0 + (int64_t)k * OWGS_ENT;
-                        if (r >= ce) break;
+                    for (int k = 0; k < 2 * RQ; ++k) {  // (out-of-range halves read as ~0: no entry)
                         const uint32_t lo = (uint32_t)rr[k], hi = (uint32_t)(rr[k] >> 32);
                         const int inv = (int)(lo & 0x7FFFu);
                         if (inv == (int)OWGS_RR_NOINV || inv >= n_slots) continue;  // no entry / invokerSlots.lift
                         const int mem = (int)(lo >> 15);
                         const int slot = (int)(hi & 0x1FFFFu);
                         const int R = (int)((hi >> 17) & OWGS_AM_MAXC_MASK);
-                        if (R <= 1) {  // FS:117-120 (beyond the LDS encoding's range: error, FS:48-50 past 2^31)
-                            int old = atomicAdd(&P[inv], mem);
-                            old -= old >= OWGS_PLIM ? OWGS_PENC : 0;
-                            if (old >= OWGS_PLIM - mem) err |= OWGS_ERR_PERMITS;
+                        if (R <= 1) {  // (not its class)
+                            err |= OWGS_ERR_BAD_STREAM;
                             continue;
                         }
                         uint32_t v;
@@ -1100,16 +1190,16 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             err |= OWGS_ERR_BAD_STREAM;
                             continue;
                         }
-                        if (mod_fast(c0 + (int)q + 1, R, __builtin_amdgcn_rcpf((float)R)) == 0) {  // RS:50-52
-                            int old = atomicAdd(&P[inv], mem);
-                            old -= old >= OWGS_PLIM ? OWGS_PENC : 0;
-                            if (old >= OWGS_PLIM - mem) err |= OWGS_ERR_PERMITS;
-                        }
+                        if (mod_fast(c0 + (int)q + 1, R, __builtin_amdgcn_rcpf((float)R)) == 0)  // RS:50-52
+                            atomicAdd(&P[inv], mem);
                     }
                 }
             }
             if (rel_ovf && !io) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // HBM counters landed
             lds_sync();
+#ifdef OWGS_PROFILE
+            pt_y[0] += memtime_pinned() - tb0;
+#endif
             if (!io) {  // apply the release counts: c1 = (c0 + j) mod R, ops1 = ops0 - j, removed at 0 (NS:109-111)
                 for (int ix = tid; ix < OWGS_CTC; ix += OWGS_ENT) {
                     const uint32_t v = rc[ix];
@@ -1157,7 +1247,13 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
         // the live entries of both tables are parked in HBM scratch and re-inserted: the primary takes up to 3/4 of its
         // capacity, the rest goes to the overflow (batch boundary: the engine waves' stores have drained, see above).
         lds_sync();
-        if (sc[SC_USED] > OWGS_CTC / 2 || (A.ovf.cap > 0 && sc[SC_OVF] > A.ovf.cap / 2)) {
+#ifdef OWGS_PROFILE
+        const u64 tb1 = memtime_pinned();
+#endif
+        // (a rebuild costs an HBM round trip of every live entry: at least CTC/8 new entries since the last one, so a
+        // shard whose live entries stay above half the primary does not rebuild in every batch)
+        if ((sc[SC_USED] > OWGS_CTC / 2 && sc[SC_USED] >= sc[SC_CLAST] + OWGS_CTC / 8) ||
+            (A.ovf.cap > 0 && sc[SC_OVF] > A.ovf.cap / 2)) {
             const bool had_ovf = sc[SC_OVF] > 0;
             if (!io) {
                 for (int ix = tid; ix < OWGS_CTC; ix += OWGS_ENT) {
@@ -1204,14 +1300,25 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
             lds_sync();
             if (tid == 0) {
                 sc[SC_USED] = nprim;
+                sc[SC_CLAST] = nprim;
                 sc[SC_OVF] = nlive - nprim;
                 sc[SC_NLIVE] = 0;
             }
             lds_sync();
         }
+#ifdef OWGS_PROFILE
+        pt_y[1] += memtime_pinned() - tb1;
+#endif
         PT(0);
         // ============================================================ per-batch bounds
         if (!io) {
+            // permits after the releases stay inside the LDS encoding's range (beyond it: error; the reference's
+            // own limit, FS:48-50, is 2^31)
+            for (int i = tid; i < n_slots; i += OWGS_ENT) {
+                const int v = P[i];
+                const bool unusable = A.pool_mode == 0 && i < A.n_ids && !((ub[i >> 5] >> (i & 31)) & 1u);
+                if ((unusable ? v - OWGS_PENC : v) >= OWGS_PLIM) err |= OWGS_ERR_PERMITS;
+            }
             int m0 = (int)0x80000000, m1 = (int)0x80000000;
             if (A.pool_mode == 0) {
                 for (int i = tid; i < nm; i += OWGS_ENT)
@@ -1349,7 +1456,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
             bool keep = false;
             while (f < len) {
                 ++st_pass;
-                const bool ovf_on = sc[SC_OVF] > 0;  // overflow keys exist: lookups fall through (uniform)
+                const bool ovf_on = OWGS_OVF && sc[SC_OVF] > 0;  // overflow keys exist: lookups fall through (uniform)
 #ifdef OWGS_PROFILE
                 const u64 tpass0 = memtime_pinned();
 #ifdef OWGS_PROF_LATER
@@ -1496,7 +1603,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             kind = K_HOT;
                         } else if (maxc == 1 && mem > U && ((A.shortcut_ok >> pool) & 1)) {
                             kind = K_FALLBACK;  // every usable permit < mem: the walk fails everywhere
-                        } else if (maxc > 1 && mem > U && A.pool_mode == 0 && n > OWGS_CTC / 2 && !ovf_on) {
+                        } else if (OWGS_CSCAN_ON && maxc > 1 && mem > U && A.pool_mode == 0 && n > OWGS_CTC / 2 && !ovf_on) {
                             kind = K_CSCAN;  // no invoker can open a container: capacity = the key's open ones
                             ws = s;          // (the ordinary walk's start, should the key have > 64 of them)
                             wpos = mod_fast(home + s * step, n, __builtin_amdgcn_rcpf((float)n));
@@ -1821,13 +1928,19 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                 // a barrier, every engine wave takes queued walks one at a time until the queue is empty, so the
                 // walks of one wave no longer serialise behind each other.  Each walk is wave-cooperative: LW_Q x 64
                 // steps per round; the result goes back through the queue entry.
-                int lq_i = -1;
+                // narrow chunks (fragmented slots: long walks are many and uneven) share the queue over the waves;
+                // wide chunks walk their own queued entries, without the extra barrier
+                const bool lqs = A.cw < OWGS_WL;
+                int lq_i = -1, nown = 0;
                 if (!io) {
                     const u64 lm = __ballot(spec && kind == K_LONG);
                     if (lm) {
-                        int qb = 0;
-                        if (lane == 0) qb = atomicAdd(&sc[SC_LQN], __popcll(lm));
-                        qb = __builtin_amdgcn_readfirstlane(qb);
+                        int qb = wave * OWGS_LPW;
+                        nown = __popcll(lm);
+                        if (lqs) {
+                            if (lane == 0) qb = atomicAdd(&sc[SC_LQN], nown);
+                            qb = __builtin_amdgcn_readfirstlane(qb);
+                        }
                         if (spec && kind == K_LONG) {
                             lq_i = qb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32),
                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
@@ -1839,16 +1952,23 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
 #ifdef OWGS_PROFILE
                 const u64 ts_b8a = memtime_pinned();
 #endif
-                LDS_SYNC_T(8);
+                if (lqs) {
+                    LDS_SYNC_T(8);
+                } else {
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // own entries: same wave
+                }
 #ifdef OWGS_PROFILE
                 const u64 ts_b8b = memtime_pinned();
 #endif
                 if (!io) {
-                    const int nq = sc[SC_LQN];
+                    const int nq = lqs ? sc[SC_LQN] : wave * OWGS_LPW + nown;
+                    int own = wave * OWGS_LPW;
                     for (;;) {
-                        int item = 0;
-                        if (lane == 0) item = atomicAdd(&sc[SC_LQH], 1);
-                        item = __builtin_amdgcn_readfirstlane(item);
+                        int item = own++;
+                        if (lqs) {
+                            if (lane == 0) item = atomicAdd(&sc[SC_LQH], 1);
+                            item = __builtin_amdgcn_readfirstlane(item);
+                        }
                         if (item >= nq) break;
                         ++st_long;
                         const uint4 qe = lq[item];
@@ -2240,7 +2360,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                     if (oj >= 0) ix = OWGS_CTC + oj;
                                 }
                                 if (ix < 0) {
-                                    if (sc[SC_USED] < OWGS_CT_LDS_FILL || A.ovf.cap <= 0) {  // find or insert
+                                    if (sc[SC_USED] < OWGS_CT_LDS_FILL || !OWGS_OVF || A.ovf.cap <= 0) {  // find or insert
                                         int fresh = 0;
                                         ix = ct_upsertv(ct, key, &fresh);
                                         if (fresh) atomicAdd(&sc[SC_USED], 1);
@@ -2248,7 +2368,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                         ix = ct_findv(ct, key, &vv);  // the nearly full primary may hold it
                                     }
                                 }
-                                if (ix < 0 && A.ovf.cap > 0) {  // the primary is full: the key goes to the overflow
+                                if (ix < 0 && OWGS_OVF && A.ovf.cap > 0) {  // the primary is full: the key goes to the overflow
                                     const int oj = ovf_insert(A.ovf, key, nv);
                                     if (oj >= 0) {
                                         ix = OWGS_CTC + oj;
@@ -2353,6 +2473,8 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
             atomicAdd(&A.stats[28], pw_c[10]);
             atomicAdd(&A.stats[29], pw_c[11]);
             atomicAdd(&A.stats[30], sc_prof_q);
+            atomicAdd(&A.stats[26], pt_y[0]);
+            atomicAdd(&A.stats[27], pt_y[1]);
             atomicAdd(&A.stats[16], pw_c[0]);
             atomicAdd(&A.stats[17], pt_x[2]);
             for (int k = 0; k < 8; ++k) atomicAdd(&A.stats[8 + k], pt_acc[k]);
@@ -2368,7 +2490,13 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     }
 }
 
-__global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineArgs A) { owgs_engine_body(A); }
+// one shard: the argument block behind a (uniform) workgroup index, like the multi-shard kernel -- read from the
+// kernarg segment where each phase needs it instead of held in registers across the whole body (a by-value block
+// is hoisted: 256 VGPRs with scratch spills against 233 without)
+struct OwgsEngineOne {
+    OwgsEngineArgs a[1];
+};
+__global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineOne M) { owgs_engine_body(M.a[blockIdx.x]); }
 
 // several controller shards in one launch: workgroup k replays shard k (its own LDS image, state and stream); the
 // arguments stay in the kernarg segment, so every field is still a scalar load
@@ -2670,11 +2798,9 @@ extern "C" hipError_t owgs_launch_ovf_rehash(const uint2* old_t, int32_t old_cap
     return hipGetLastError();
 }
 
-extern "C" hipError_t owgs_launch_relpos(const int64_t* rel_aid, int64_t n_rel, int64_t n_act, int32_t* relx,
-                                         int32_t* err, hipStream_t s) {
-    if (n_rel > 0)
-        hipLaunchKernelGGL(owgs_relpos_kernel, dim3((unsigned)((n_rel + 255) / 256)), dim3(256), 0, s, rel_aid, n_rel,
-                           n_act, relx, err);
+extern "C" hipError_t owgs_launch_relpos(const OwgsRelposArgs* a, hipStream_t s) {
+    if (a->n_rel > 0 && a->n_batches > 0)
+        hipLaunchKernelGGL(owgs_relpos_kernel, dim3((unsigned)((a->n_rel + 255) / 256)), dim3(256), 0, s, *a);
     return hipGetLastError();
 }
 
@@ -2767,6 +2893,8 @@ extern "C" hipError_t owgs_launch_engine(const OwgsEngineArgs* a, hipStream_t s)
     const hipError_t ea = hipFuncSetAttribute((const void*)owgs_engine_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                               OWGS_LDS_BYTES);
     if (ea != hipSuccess) return ea;
-    hipLaunchKernelGGL(owgs_engine_kernel, dim3(1), dim3(OWGS_NT), lds, s, *a);
+    OwgsEngineOne M;
+    M.a[0] = *a;
+    hipLaunchKernelGGL(owgs_engine_kernel, dim3(1), dim3(OWGS_NT), lds, s, M);
     return hipGetLastError();
 }
