@@ -67,7 +67,8 @@ typedef unsigned long long u64;
 #endif
 #define CAPMAX 1024  // capacities are clamped: a lane's rank is < OWGS_WL
 #ifndef LW_Q
-#define LW_Q 4  // walk steps each lane probes per round of a wave-cooperative long walk
+#define LW_Q 2  // walk steps each lane probes per round of a wave-cooperative long walk (2 vs 4: 35.4 vs 36.1 ms
+                // headline, 130 vs 137 ms configs[1], 222 vs 229 ms C5 shard 0 of 8; round 2)
 #endif
 
 // diagnostic build (-DOWGS_PROFILE, libowgs_prof.so): s_memtime cycle accounting per engine phase into stats[8..15]
@@ -785,8 +786,9 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
     A.lix[(int64_t)g * OWGS_WL + pos] = (uint32_t)t | ((uint32_t)lead << 16);
 }
 
-// Release bookkeeping: relx[aid] = r, the position of the activation's release in rel_aid (rel_aid is grouped by
-// release batch, so the engine reads batch b's records rel_rec[rel_off[b] .. rel_off[b+1]) contiguously).  An
+// Release bookkeeping: relx[aid] = the position of the activation's release record, inside its release batch's range
+// (rel_aid is grouped by release batch, so the engine reads batch b's records rel_rec[rel_off[b] .. rel_off[b+1])
+// contiguously).  An
 // activation released twice, or a release id outside the stream, is a malformed stream (the reference's
 // activationSlots.remove would find no entry the second time, CLB:278-279; replays take CommonLoadBalancer's streams).
 // Inside batch b's range the records are placed by class: releases of maxConcurrent == 1 actions from the front
