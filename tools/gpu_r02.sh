@@ -33,6 +33,11 @@ for s in ${STEPS:-tests bench cfgs phases}; do
     pmc)
       timeout -k 10 600 python3 tools/pmc_traffic.py ${BENCH_ARGS:-} > $O/pmc.log 2>&1
       rc=$?; tail -2 $O/pmc.log | cut -c1-400; [ $rc -eq 0 ] || stop pmc $rc ;;
+    pmccfg)  # HBM traffic entries for the per-config bench lines (configs[1..3])
+      for c in c2 c3 c4; do
+        timeout -k 10 600 python3 tools/pmc_traffic.py --config $c > $O/pmc_$c.log 2>&1
+        rc=$?; tail -1 $O/pmc_$c.log | cut -c1-200; [ $rc -eq 0 ] || stop "pmc $c" $rc
+      done ;;
   esac
 done
 echo "gpu_r02 done"
