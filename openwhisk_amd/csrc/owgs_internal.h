@@ -45,7 +45,7 @@
 #define OWGS_WL (OWGS_EW * OWGS_LPW)   // chunk width: activations resolved together (one per engine lane)
 #define OWGS_NT (OWGS_ENT + 64)        // threads: engine waves + one I/O wave
 #ifndef OWGS_NBK_LOG2
-#define OWGS_NBK_LOG2 11
+#define OWGS_NBK_LOG2 10  // (11: no faster on the BASELINE configs, 8 KB more LDS, ~1.9k fewer invokers)
 #endif
 #define OWGS_NBK (1 << OWGS_NBK_LOG2)  // "first lane of its invoker" buckets (hashed; collisions are conservative)
 #define OWGS_CTC 4096                  // concurrency-table capacity (entries, power of two)

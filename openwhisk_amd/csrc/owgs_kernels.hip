@@ -798,6 +798,20 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
 __global__ __launch_bounds__(256) void owgs_relpos_kernel(OwgsRelposArgs R) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63;
+    // the batch of each release: one search per workgroup (last batch with rel_off[b] <= first release), then a short
+    // forward scan per thread (a search again past 16 steps: runs of empty batches)
+    __shared__ int s_b0;
+    auto last_le = [&](int64_t x) {
+        int lo = 0, hi = R.n_batches - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (R.rel_off[mid] <= x) lo = mid;
+            else hi = mid - 1;
+        }
+        return lo;
+    };
+    if (threadIdx.x == 0) s_b0 = last_le(min((int64_t)blockIdx.x * blockDim.x, R.n_rel - 1));
+    __syncthreads();
     bool live = r < R.n_rel;
     int64_t aid = -1;
     int b = 0, cls = 0;
@@ -807,13 +821,13 @@ __global__ __launch_bounds__(256) void owgs_relpos_kernel(OwgsRelposArgs R) {
             atomicOr(R.err, OWGS_ERR_BAD_STREAM);
             live = false;
         } else {
-            int lo = 0, hi = R.n_batches - 1;  // last batch with rel_off[b] <= r
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (R.rel_off[mid] <= r) lo = mid;
-                else hi = mid - 1;
+            b = s_b0;
+            int k = 0;
+            while (k < 16 && b + 1 < R.n_batches && R.rel_off[b + 1] <= r) {
+                ++b;
+                ++k;
             }
-            b = lo;
+            if (k == 16) b = last_le(r);
             const uint2 m = R.act_meta[R.act[aid]];
             cls = ((m.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK) > 1 ? 1 : 0;
         }
