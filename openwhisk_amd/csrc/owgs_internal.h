@@ -48,7 +48,9 @@
 #define OWGS_NBK_LOG2 10  // (11: no faster on the BASELINE configs, 8 KB more LDS, ~1.9k fewer invokers)
 #endif
 #define OWGS_NBK (1 << OWGS_NBK_LOG2)  // "first lane of its invoker" buckets (hashed; collisions are conservative)
+#ifndef OWGS_CTC
 #define OWGS_CTC 4096                  // concurrency-table capacity (entries, power of two)
+#endif
 #define OWGS_LDS_BYTES (160 * 1024)
 
 // --------------------------------------------------------------------------------------------- action meta

@@ -52,6 +52,9 @@ typedef unsigned long long u64;
 #ifndef OWGS_OVF
 #define OWGS_OVF 1  // 0: measurement variant without the overflow table's fall-through paths
 #endif
+#ifndef OWGS_CSCAN_MIN_N
+#define OWGS_CSCAN_MIN_N (OWGS_CTC / 2)  // pools at most this large walk instead of scanning the table
+#endif
 #ifndef OWGS_CSCAN_ON
 #define OWGS_CSCAN_ON 1
 #endif
@@ -1619,7 +1622,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             kind = K_HOT;
                         } else if (maxc == 1 && mem > U && ((A.shortcut_ok >> pool) & 1)) {
                             kind = K_FALLBACK;  // every usable permit < mem: the walk fails everywhere
-                        } else if (OWGS_CSCAN_ON && maxc > 1 && mem > U && A.pool_mode == 0 && n > OWGS_CTC / 2 && !ovf_on) {
+                        } else if (OWGS_CSCAN_ON && maxc > 1 && mem > U && A.pool_mode == 0 && n > OWGS_CSCAN_MIN_N && !ovf_on) {
                             kind = K_CSCAN;  // no invoker can open a container: capacity = the key's open ones
                             ws = s;          // (the ordinary walk's start, should the key have > 64 of them)
                             wpos = mod_fast(home + s * step, n, __builtin_amdgcn_rcpf((float)n));
