@@ -192,6 +192,32 @@ def test_stream_parity_shared_keys(kw):
     check_stream(w)
 
 
+def test_malformed_release_stream_fails_loudly():
+    # a stream that releases one activation twice (CommonLoadBalancer never does: activationSlots.remove finds no
+    # entry the second time, CLB:278-279) is rejected by the release front end (owgs_relpos_kernel's claim of the
+    # activation's record) with OWGS_EINVAL; restore() then gives back a balancer that replays a valid stream exactly
+    from openwhisk_amd._lib import OwgsError
+    w = W.config("c4", n_activations=30_000)
+    s = w.stream
+    b = gpu_for(w)
+    b.snapshot()
+    last = s.n_batches - 1
+    dup = int(s.rel_aid[s.rel_off[1]])  # released in batch 1, released again in the last batch
+    rel_aid = np.insert(s.rel_aid, s.rel_off[last], dup)
+    rel_off = s.rel_off.copy()
+    rel_off[last + 1:] += 1
+    bad = W.Stream(act=s.act, acq_off=s.acq_off, rel_off=rel_off, rel_aid=rel_aid, seq_base=s.seq_base)
+    with pytest.raises(OwgsError) as e:
+        b.replay(bad)
+    assert e.value.code == -22  # OWGS_EINVAL
+    b.restore()
+    st = O.state_for(w, zombies=False)
+    o_inv, o_fl, o_rf = st.replay(s)
+    g_inv, g_fl, g_rf = b.replay(s)
+    assert np.array_equal(o_inv, g_inv) and np.array_equal(o_fl, g_fl) and np.array_equal(o_rf, g_rf)
+    assert np.array_equal(st.permits(), b.permits())
+
+
 def test_stream_parity_literal_zombie_oracle():
     # the literal oracle (entries created on failed tries, NS:61-62) gives the same answers on valid streams
     w = W.config("c4", n_activations=50_000)
