@@ -52,6 +52,12 @@ typedef unsigned long long u64;
 #ifndef OWGS_OVF
 #define OWGS_OVF 1  // 0: measurement variant without the overflow table's fall-through paths
 #endif
+#ifndef OWGS_HOT_IO
+#define OWGS_HOT_IO 1  // the I/O wave takes a share of the hot-action walks
+#endif
+#ifndef OWGS_QUEUE_IO
+#define OWGS_QUEUE_IO 1  // ... and pops queued long walks when the queue is shared
+#endif
 #ifndef OWGS_CSCAN_MIN_N
 #define OWGS_CSCAN_MIN_N (OWGS_CTC / 2)  // pools at most this large walk instead of scanning the table
 #endif
@@ -502,8 +508,8 @@ __host__ __device__ inline OwgsLayout owgs_layout(int n_slots, int pool_mode, in
     L.spt = o + 4u * OWGS_NBK;
     L.hdir = L.spt + 4u * OWGS_WL;                  // NHOT x {action, meta.x, meta.y, slot}, NHOT x max occ, NHOT x flag
     L.htab = L.hdir + 24u * NHOT;                   // NHOT x HOT_RANKS x {id | kind << 15 | ks << 18, step}
-    L.hscr = L.htab + 8u * NHOT * HOT_RANKS;        // OWGS_EW x 64 rank marks
-    L.bhead = L.hscr + 4u * 64 * OWGS_EW;           // per pass: lanes of each bucket (list head, lane + 1)
+    L.hscr = L.htab + 8u * NHOT * HOT_RANKS;        // (OWGS_EW + 1) x 64 rank marks (the I/O wave walks hot slots too)
+    L.bhead = L.hscr + 4u * 64 * (OWGS_EW + 1);     // per pass: lanes of each bucket (list head, lane + 1)
     L.nextl = L.bhead + 4u * OWGS_NBK;              // next lane of the bucket list (lane + 1, 0 = end)
     L.spc = L.nextl + 4u * OWGS_WL;                 // memory each lane tentatively takes at its target
     L.cdirty = L.spc + 4u * OWGS_WL;                // [2][OWGS_WL] pass parity x first lane of an action: re-speculated
@@ -1510,8 +1516,11 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                 // ------------------------------------------------ hot actions: one wave-cooperative walk per slot
                 // 64 walk steps per round: capacities, inclusive scan, then every rank q finds the step whose
                 // capacity range holds it (first rank of each step marked in LDS, prefix max over ranks)
-                if (!io) {
-                    for (int h = wave; h < nhot; h += OWGS_EW) {
+                // slot h goes to the I/O wave when h % (OWGS_EW + 1) == 0 (it holds no lanes: its speculation is
+                // otherwise idle), else to engine wave h % (OWGS_EW + 1) - 1
+                {
+                    const int hw = OWGS_HOT_IO ? (io ? 0 : wave + 1) : (io ? NHOT : wave);
+                    for (int h = hw; h < nhot; h += OWGS_HOT_IO ? OWGS_EW + 1 : OWGS_EW) {
                         const uint4 d = hdir[h];
                         if (d.z & (OWGS_AM_THROW | OWGS_AM_EMPTY)) continue;
                         if (hflag[h] != f) continue;  // no lane of this action speculates in this pass
@@ -1979,7 +1988,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
 #ifdef OWGS_PROFILE
                 const u64 ts_b8b = memtime_pinned();
 #endif
-                if (!io) {
+                if (!io || (OWGS_QUEUE_IO && lqs)) {  // (the I/O wave takes shared-queue walks too: it holds no lanes)
                     const int nq = lqs ? sc[SC_LQN] : wave * OWGS_LPW + nown;
                     int own = wave * OWGS_LPW;
                     for (;;) {
@@ -2476,14 +2485,14 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     }
     if (err) atomicOr(A.err, (int)err);
     if (A.stats) {
+        atomicAdd(&A.stats[OWGS_ST_PROBES], (u64)st_probe);  // (the I/O wave's: its share of the hot walks)
+        if (lane == 0) atomicAdd(&A.stats[OWGS_ST_LONG], (u64)st_long);
         if (!io) {
-            atomicAdd(&A.stats[OWGS_ST_PROBES], (u64)st_probe);
             atomicAdd(&A.stats[OWGS_ST_FALLBACKS], (u64)st_fb);
 #if !defined(OWGS_PROFILE) && !defined(OWGS_STOP_REASONS)
             atomicAdd(&A.stats[6], (u64)st_gprobe);
             atomicAdd(&A.stats[7], (u64)st_glane);
 #endif
-            if (lane == 0) atomicAdd(&A.stats[OWGS_ST_LONG], (u64)st_long);
         }
 #ifdef OWGS_PROFILE
         if (!io && lane == 0)
