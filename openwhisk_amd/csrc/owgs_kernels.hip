@@ -617,7 +617,9 @@ __global__ __launch_bounds__(64) void owgs_chunks_kernel(const int64_t* acq_off,
 // one workgroup per chunk: occ (earlier lanes of the same action), next lane of the same action, nearest earlier
 // lane with the same slot key and a different action (shared fqn@version), packed with the action meta
 __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A) {
-    __shared__ int32_t s_a[OWGS_WL], s_s[OWGS_WL], s_p[OWGS_WL];
+    // (16-byte aligned: the all-pairs scans below read 4 lanes per LDS access; OWGS_WL is a multiple of 4)
+    __shared__ __align__(16) int32_t s_a[OWGS_WL], s_s[OWGS_WL], s_p[OWGS_WL];
+    static_assert(OWGS_WL % 4 == 0, "4-lane reads");
     const int g = blockIdx.x;
     if (g >= A.cstart[A.n_batches]) return;
     int lo = 0, hi = A.n_batches - 1;  // last batch with cstart[b] <= g
@@ -648,17 +650,24 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
     __syncthreads();
     int occ = 0, next = (int)OWGS_REC_NONEXT, pk1 = 0, cnt = 0, lead = t;
     if (t < len) {
-        for (int j = 0; j < len; ++j) {
-            const int aj = s_a[j];
-            if (aj == aid) {
-                ++cnt;
-                if (j < lead) lead = j;
-            }
-            if (j < t) {
-                if (aj == aid) ++occ;
-                else if (s_s[j] == slot) pk1 = j + 1;
-            } else if (j > t && aj == aid && next == (int)OWGS_REC_NONEXT) {
-                next = j;
+        // lanes past len hold unique negative ids and slot 0: they match nothing below (j < t < len for pk1)
+        for (int j0 = 0; j0 < len; j0 += 4) {
+            const int4 a4 = *(const int4*)&s_a[j0];
+            const int4 s4 = *(const int4*)&s_s[j0];
+            const int av[4] = {a4.x, a4.y, a4.z, a4.w}, sv[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int j = j0 + u, aj = av[u];
+                if (aj == aid) {
+                    ++cnt;
+                    if (j < lead) lead = j;
+                }
+                if (j < t) {
+                    if (aj == aid) ++occ;
+                    else if (sv[u] == slot) pk1 = j + 1;
+                } else if (j > t && aj == aid && next == (int)OWGS_REC_NONEXT) {
+                    next = j;
+                }
             }
         }
     }
@@ -669,7 +678,12 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
     __syncthreads();
     bool shared = false;
     if (t < len && mc > 1)
-        for (int j = 0; j < len; ++j) shared = shared || (s_a[j] == aid && s_p[j] != 0);
+        for (int j0 = 0; j0 < len; j0 += 4) {
+            const int4 a4 = *(const int4*)&s_a[j0];
+            const int4 p4 = *(const int4*)&s_p[j0];
+            shared = shared || (a4.x == aid && p4.x != 0) || (a4.y == aid && p4.y != 0) || (a4.z == aid && p4.z != 0) ||
+                     (a4.w == aid && p4.w != 0);
+        }
     const bool q = t < len && A.act && cnt >= HOT_MIN && !shared && !(meta.y & (OWGS_AM_THROW | OWGS_AM_EMPTY)) &&
                    (mc == 1 || HOT_CONC_ON);
     __syncthreads();
@@ -678,7 +692,12 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
     int hs = OWGS_REC_NOHOT;
     if (q) {
         int k = 0;
-        for (int j = 0; j < lead; ++j) k += s_s[j];
+        int j0 = 0;
+        for (; j0 + 4 <= lead; j0 += 4) {
+            const int4 v = *(const int4*)&s_s[j0];
+            k += v.x + v.y + v.z + v.w;
+        }
+        for (; j0 < lead; ++j0) k += s_s[j0];
         if (k < NHOT) hs = k;
     }
     // record position by class: 0 = walks of maxConcurrent == 1 actions, 1 = no walk of its own (hot-table rank,
@@ -700,7 +719,64 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
         }
     }
     __syncthreads();
-    if (t == 0) {
+    // Mode 1 (large pools) in parallel: concurrent lanes round-robin over the fewest back waves that hold them,
+    // walkers round-robin over the front waves, walk-free lanes into the free slots from wave 0 up.  Every thread
+    // places its own lane from its class rank; this is exactly what the serial dealing below does whenever no wave
+    // fills up before its last round-robin turn (checked here; otherwise, and for the other modes, thread 0 deals).
+    bool dealt = false;
+    if (A.deal == 1) {
+        constexpr int NWR = (OWGS_WL + 63) / 64;
+        int nc[3] = {0, 0, 0};
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            for (int r = 0; r < NWR; ++r) nc[c] += __popcll(s_m[c][r]);
+        int nwv = 0;
+        for (int w = 0; w < OWGS_EW; ++w) nwv += wave_cap(len, w) > 0;
+        int f2 = 0, acc2 = 0;
+        while (f2 < nwv && acc2 < nc[2]) acc2 += wave_cap(len, nwv - 1 - f2++);
+        const int sp0 = nwv - f2, lo2 = nwv - f2;
+        // lanes of a class dealt round-robin from wave lo over span waves: wave lo + i gets ceil((n - i) / span)
+        auto rr_count = [](int n, int i, int span) { return (span > 0 && n > i) ? (n - i - 1) / span + 1 : 0; };
+        bool ok = sp0 >= 1;
+        int used[OWGS_EW];
+#pragma unroll
+        for (int w = 0; w < OWGS_EW; ++w) {
+            used[w] = w < sp0 ? rr_count(nc[0], w, sp0) : (w < nwv ? rr_count(nc[2], w - lo2, f2) : 0);
+            ok = ok && used[w] <= wave_cap(len, w);
+        }
+        if (ok) {
+            dealt = true;
+            if (t < len) {
+                const int c = cls;
+                const int row = t >> 6;
+                int k = 0;  // class rank: lanes of class c before t
+                for (int r = 0; r < row; ++r) k += __popcll(s_m[c][r]);
+                const unsigned long long below = s_m[c][row] & ((1ull << (t & 63)) - 1ull);
+                k += __popcll(below);
+                int w = 0, slot = 0;
+                if (c == 0) {
+                    w = k % sp0;
+                    slot = k / sp0;
+                } else if (c == 2) {
+                    w = lo2 + k % f2;
+                    slot = k / f2;
+                } else {  // the k-th free slot in wave order
+                    int pre = 0;
+#pragma unroll
+                    for (int v = 0; v < OWGS_EW; ++v) {
+                        const int fr = wave_cap(len, v) - used[v];
+                        if (k >= pre && k < pre + fr) {
+                            w = v;
+                            slot = used[v] + (k - pre);
+                        }
+                        pre += fr;
+                    }
+                }
+                s_s[t] = wave_off(len, w) + slot;
+            }
+        }
+    }
+    if (t == 0 && !dealt) {
         constexpr int NWR = (OWGS_WL + 63) / 64;
         // f(j) for every lane j of class c, in stream order (masks and the per-wave counters below live in LDS:
         // indexed by runtime values, a thread-private array would sit in scratch memory)
@@ -804,12 +880,15 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
 // (relcnt[b] of them), concurrent ones from the back, so the engine's sweep runs the plain permit return over the first
 // part without the concurrency-map path (order inside a batch is free: permit sums commute, and a concurrent release's
 // effect depends only on its rank among the releases of its entry).  One atomic per wave and (batch, class).
-__global__ __launch_bounds__(256) void owgs_relpos_kernel(OwgsRelposArgs R) {
+#define RP_T 1024  // releases per workgroup
+#define RP_W 8     // batches from the workgroup's first whose counts are aggregated in LDS (later ones: per wave)
+__global__ __launch_bounds__(RP_T) void owgs_relpos_kernel(OwgsRelposArgs R) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63;
     // the batch of each release: one search per workgroup (last batch with rel_off[b] <= first release), then a short
     // forward scan per thread (a search again past 16 steps: runs of empty batches)
     __shared__ int s_b0;
+    __shared__ int s_cnt[RP_W][2], s_base[RP_W][2];
     auto last_le = [&](int64_t x) {
         int lo = 0, hi = R.n_batches - 1;
         while (lo < hi) {
@@ -820,7 +899,9 @@ __global__ __launch_bounds__(256) void owgs_relpos_kernel(OwgsRelposArgs R) {
         return lo;
     };
     if (threadIdx.x == 0) s_b0 = last_le(min((int64_t)blockIdx.x * blockDim.x, R.n_rel - 1));
+    if (threadIdx.x < 2 * RP_W) (&s_cnt[0][0])[threadIdx.x] = 0;
     __syncthreads();
+    const int bw = s_b0;
     bool live = r < R.n_rel;
     int64_t aid = -1;
     int b = 0, cls = 0;
@@ -830,7 +911,7 @@ __global__ __launch_bounds__(256) void owgs_relpos_kernel(OwgsRelposArgs R) {
             atomicOr(R.err, OWGS_ERR_BAD_STREAM);
             live = false;
         } else {
-            b = s_b0;
+            b = bw;
             int k = 0;
             while (k < 16 && b + 1 < R.n_batches && R.rel_off[b + 1] <= r) {
                 ++b;
@@ -841,24 +922,50 @@ __global__ __launch_bounds__(256) void owgs_relpos_kernel(OwgsRelposArgs R) {
             cls = ((m.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK) > 1 ? 1 : 0;
         }
     }
+    // ranks per (batch, class): a wave's group takes its offset from an LDS counter (batches bw .. bw + RP_W - 1), then
+    // one global atomic per workgroup and (batch, class) gives the group's base; later batches: a global atomic per wave
     int64_t pos = -1;
+    int off = 0;
+    bool local = false;
     for (u64 todo = __ballot(live); todo;) {
-        const int b0 = __builtin_amdgcn_readlane(b, (int)__builtin_ctzll(todo));
+        const int ld = (int)__builtin_ctzll(todo);
+        const int b0 = __builtin_amdgcn_readlane(b, ld);
+        const bool win = b0 - bw < RP_W;
         const bool sel = live && b == b0;
         const u64 m0 = __ballot(sel && cls == 0), m1 = __ballot(sel && cls == 1);
         int base0 = 0, base1 = 0;
-        if (lane == (int)__builtin_ctzll(todo)) {
-            if (m0) base0 = atomicAdd(&R.relcnt[2 * b0], __popcll(m0));
-            if (m1) base1 = atomicAdd(&R.relcnt[2 * b0 + 1], __popcll(m1));
+        if (lane == ld) {
+            if (win) {
+                if (m0) base0 = atomicAdd(&s_cnt[b0 - bw][0], __popcll(m0));
+                if (m1) base1 = atomicAdd(&s_cnt[b0 - bw][1], __popcll(m1));
+            } else {
+                if (m0) base0 = atomicAdd(&R.relcnt[2 * b0], __popcll(m0));
+                if (m1) base1 = atomicAdd(&R.relcnt[2 * b0 + 1], __popcll(m1));
+            }
         }
-        base0 = __shfl(base0, (int)__builtin_ctzll(todo), 64);
-        base1 = __shfl(base1, (int)__builtin_ctzll(todo), 64);
+        base0 = __shfl(base0, ld, 64);
+        base1 = __shfl(base1, ld, 64);
         if (sel) {
             const u64 mm = cls ? m1 : m0;
             const int rk = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
-            pos = cls ? R.rel_off[b0 + 1] - 1 - (base1 + rk) : R.rel_off[b0] + base0 + rk;
+            if (win) {
+                local = true;
+                off = (cls ? base1 : base0) + rk;
+            } else {
+                pos = cls ? R.rel_off[b0 + 1] - 1 - (base1 + rk) : R.rel_off[b0] + base0 + rk;
+            }
         }
         todo &= ~(m0 | m1);
+    }
+    __syncthreads();
+    if (threadIdx.x < 2 * RP_W) {
+        const int i = threadIdx.x >> 1, c = threadIdx.x & 1, n = s_cnt[i][c];
+        s_base[i][c] = n ? atomicAdd(&R.relcnt[2 * (bw + i) + c], n) : 0;
+    }
+    __syncthreads();
+    if (local) {
+        const int base = s_base[b - bw][cls] + off;
+        pos = cls ? R.rel_off[b + 1] - 1 - base : R.rel_off[b] + base;
     }
     if (live && atomicCAS(&R.relx[aid], -1, (int32_t)pos) != -1) atomicOr(R.err, OWGS_ERR_BAD_STREAM);
 }
@@ -2828,7 +2935,7 @@ extern "C" hipError_t owgs_launch_ovf_rehash(const uint2* old_t, int32_t old_cap
 
 extern "C" hipError_t owgs_launch_relpos(const OwgsRelposArgs* a, hipStream_t s) {
     if (a->n_rel > 0 && a->n_batches > 0)
-        hipLaunchKernelGGL(owgs_relpos_kernel, dim3((unsigned)((a->n_rel + 255) / 256)), dim3(256), 0, s, *a);
+        hipLaunchKernelGGL(owgs_relpos_kernel, dim3((unsigned)((a->n_rel + RP_T - 1) / RP_T)), dim3(RP_T), 0, s, *a);
     return hipGetLastError();
 }
 
