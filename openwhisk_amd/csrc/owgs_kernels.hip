@@ -111,7 +111,7 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
 
 // LDS scalars
 #define SC_LMIN 0   // [2] first lane not known to fit (pass parity)
-#define SC_CFB 2    // [2] first concurrent forced lane (pass parity)
+#define SC_CFB 2    // [2] (unused: see SC_CFT)
 #define SC_U0 4     // upper bound of usable permits, managed pool
 #define SC_U1 5     // blackbox pool
 #define SC_USED 6   // non-empty concurrency-table entries (live + deleted)
@@ -122,7 +122,14 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
 #define SC_CLAST 12  // primary entries (live) right after the last table rebuild
 #define SC_LQN 10   // long walks queued in this pass
 #define SC_LQH 11   // next queued long walk to take
-#define SC_N (16 + 10 * OWGS_EW)
+// [2][CFT_N] per pass parity and hashed fqn@version key: the first lane of the pass with a concurrent forced acquire
+// of that key (its new container's free slots can only change the walks of lanes with the same key, NS:57-82)
+#define SC_CFT (16 + 10 * OWGS_EW)
+#ifndef CFT_LOG2
+#define CFT_LOG2 6
+#endif
+#define CFT_N (1 << CFT_LOG2)
+#define SC_N (SC_CFT + 2 * CFT_N)
 
 // hot actions: every action with >= HOT_MIN lanes in a chunk gets a slot (assigned by the pre-pass; a concurrent
 // action only when no lane of the chunk shares its fqn@version with another action); per pass one wave walks its
@@ -1119,7 +1126,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     } else {
         for (int i = tid; i < nm + nb; i += OWGS_NT) pw[i] = (int16_t)A.pool_words[i];
     }
-    if (tid < SC_N) sc[tid] = (tid < 4) ? OWGS_WL : (tid < 6 ? (int)0x80000000 : 0);
+    if (tid < SC_N) sc[tid] = (tid < 4 || tid >= SC_CFT) ? OWGS_WL : (tid < 6 ? (int)0x80000000 : 0);
     lds_sync();
     {
         int used = 0;
@@ -2368,7 +2375,8 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                     // walk identity: the action, or the lane itself for explicit per-activation walks
                     if (maxc > 1) skey[li] = make_uint2((uint32_t)slot, a != (int)OWGS_REC_NOACT ? (uint32_t)a : 0x80000000u | li);
                 }
-                if (act && maxc > 1 && kind == K_FALLBACK) atomicMin(&sc[SC_CFB + par], li);
+                const int cft = SC_CFT + par * CFT_N + (int)(((uint32_t)slot * 2654435761u) >> (32 - CFT_LOG2));
+                if (act && maxc > 1 && kind == K_FALLBACK) atomicMin(&sc[cft], li);
                 if (own && li < OWGS_WL) spt[li] = part ? t : -1;
                 LDS_SYNC_T(3);
                 // (fallback+buckets accrue to PT(6));
@@ -2397,7 +2405,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                     if (maxc == 1) {
                         kf = fit || kind == K_FALLBACK;
                     } else {
-                        const int cfb = sc[SC_CFB + par];
+                        const int cfb = sc[cft];  // first forced acquire of this key in the pass
                         if (kind == K_FALLBACK) kf = first && cfb >= li;
                         else kf = fit && cfb > li;
                         // an earlier lane of this pass has the same fqn under another action (another walk): its
@@ -2415,7 +2423,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                     nf = !kf;
 #ifdef OWGS_STOP_REASONS
                     if (nf) {
-                        const int cfb = sc[SC_CFB + par];
+                        const int cfb = sc[cft];
                         why = maxc == 1 ? 1 : pk1 > f ? 5 : kind == K_FALLBACK ? (!first ? 2 : 4) : (cfb <= li ? 4 : 3);
                     }
 #endif
@@ -2544,12 +2552,12 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                     atomicMax(&pfw[1], (int)(tc2 - tc1));
                 }
 #endif
+                if (tid < CFT_N) sc[SC_CFT + (par ^ 1) * CFT_N + tid] = OWGS_WL;  // read in this pass's other half
                 if (tid == 0) {
                     sc[SC_LQN] = 0;  // the queue of this pass was drained before barrier 2
                     sc[SC_LQH] = 0;
                     sc[SC_NHOT] = 0;  // read at the chunk start, before this pass's barriers
                     sc[SC_LMIN + (par ^ 1)] = OWGS_WL;
-                    sc[SC_CFB + (par ^ 1)] = OWGS_WL;
                     if (l < len) ++st_stop;
                 }
                 if (!io && __ballot(ovf_w)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // visible next pass

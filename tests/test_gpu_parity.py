@@ -192,6 +192,20 @@ def test_stream_parity_shared_keys(kw):
     check_stream(w)
 
 
+@pytest.mark.parametrize("kw", [
+    # overloaded pools of odd sizes (the blackbox pool starts at an id that is not a multiple of 4): ranks beyond the
+    # pool's remaining capacity fail through the capacity scan / cached bound instead of a full walk
+    dict(n_invokers=5003, load=1.5, conc_frac=0.0, unhealthy_frac=0.1, blackbox_frac=0.2, n_activations=150_000),
+    dict(n_invokers=2999, load=2.0, conc_frac=0.2, unhealthy_frac=0.05, blackbox_frac=0.3, n_activations=100_000,
+         cluster_size=3),
+    # a slot smaller than most actions (clusterSize 64: 256 MB): rank-0 failures and hot actions running dry
+    dict(n_invokers=4001, load=1.1, n_activations=100_000, cluster_size=64),
+])
+def test_stream_parity_pool_capacity_bounds(kw):
+    w = W.config("headline", **kw)
+    check_stream(w)
+
+
 def test_malformed_release_stream_fails_loudly():
     # a stream that releases one activation twice (CommonLoadBalancer never does: activationSlots.remove finds no
     # entry the second time, CLB:278-279) is rejected by the release front end (owgs_relpos_kernel's claim of the
