@@ -2390,7 +2390,10 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                     const bool first = fst[bk] == (uint32_t)(OWGS_WL - li);
                     // fits at t: the lowest lane of its bucket, or every lane of the pass at t fits, or (walking the
                     // bucket's lanes) the lanes before this one at t leave room for it
-                    bool fit = first || P[t] >= 0;
+                    // (a concurrent lane that takes a free slot of a container needs no memory (NS:57-82): the
+                    // container is an earlier commit, or an earlier lane of the pass opens it -- if that lane does
+                    // not fit, it stops the pass before this one)
+                    bool fit = first || P[t] >= 0 || (maxc > 1 && kind == K_TARGET && cons == 0);
                     if (!fit && kind != K_FALLBACK) {
                         int pf = 0, tot = 0;
                         for (int j = (int)bhead[bk] - 1; j >= 0; j = nextl[j] - 1)
