@@ -423,7 +423,10 @@ class GpuShardingContainerPoolBalancer:
         out = (C.c_uint64 * 32)()
         self._chk(self._L.owgs_read_stats(self._h, out, 32))
         d = {"passes": out[0], "probes": out[1], "fallbacks": out[2], "long_walks": out[3], "chunks": out[4],
-             "stops": out[5], "general_probes": out[6], "general_lanes": out[7]}
+             "stops": out[5], "general_probes": out[6], "general_lanes": out[7], "redecided": out[31]}
+        if any(out[28:31]) and not any(out[8:16]):  # -DOWGS_EXT_PROF build: in-pass re-decision costs
+            d["redecide"] = {"cycles": out[28], "walk_rounds": out[29], "scans": out[30], "setup": out[20], "walk": out[21],
+                             "apply": out[22], "scan": out[23]}
         if any(out[8:16]):
             names = ["batch", "chunk_start", "speculate", "tables_buckets", "validate", "commit", "worst_hot", "worst_lane"]
             d["cycles"] = {k: out[8 + i] for i, k in enumerate(names)}

@@ -61,6 +61,22 @@ typedef unsigned long long u64;
 #ifndef OWGS_CSCAN_MIN_N
 #define OWGS_CSCAN_MIN_N (OWGS_CTC / 2)  // pools at most this large walk instead of scanning the table
 #endif
+#ifndef OWGS_EXT
+#define OWGS_EXT 1  // stopping maxConcurrent == 1 lanes are re-decided exactly inside the pass (see the commit phase)
+#endif
+#ifndef EXT_MAX
+#define EXT_MAX 48  // re-decisions per pass
+#endif
+#ifndef EXT_ROUNDS
+#define EXT_ROUNDS 8  // walk rounds (128 steps each) a re-decision may take; a longer walk waits for the next pass
+#endif
+// fxa[li] (per lane of the pass, stream order): x = action | not known to fit << 24 | exempt << 25 | re-decidable << 26
+// | re-decided << 27 | kind << 28; y = record position | walk step << 16, after a re-decision target | step << 16
+#define FX_NF (1u << 24)
+#define FX_EXEMPT (1u << 25)
+#define FX_OK (1u << 26)
+#define FX_DONE (1u << 27)
+#define FX_CLASH (1u << 30)  // a lane after the pass limit that targets a re-decided lane's invoker or shares its action
 #ifndef OWGS_CSCAN_ON
 #define OWGS_CSCAN_ON 1
 #endif
@@ -81,7 +97,7 @@ typedef unsigned long long u64;
 #endif
 
 // diagnostic build (-DOWGS_PROFILE, libowgs_prof.so): s_memtime cycle accounting per engine phase into stats[8..15]
-#if defined(OWGS_PROFILE) || defined(OWGS_TRACE)
+#if defined(OWGS_PROFILE) || defined(OWGS_TRACE) || defined(OWGS_EXT_PROF)
 // a timestamp the compiler can neither merge with another nor move out of its branch
 __device__ __forceinline__ unsigned long long memtime_pinned() {
     unsigned long long t;
@@ -122,6 +138,8 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
 #define SC_CLAST 12  // primary entries (live) right after the last table rebuild
 #define SC_LQN 10   // long walks queued in this pass
 #define SC_LQH 11   // next queued long walk to take
+#define SC_LFIN 14  // pass limit after the in-pass re-decisions (OWGS_EXT)
+#define SC_NEXT 15  // re-decisions in this pass
 // [2][CFT_N] per pass parity and hashed fqn@version key: the first lane of the pass with a concurrent forced acquire
 // of that key (its new container's free slots can only change the walks of lanes with the same key, NS:57-82)
 #define SC_CFT (16 + 10 * OWGS_EW)
@@ -479,7 +497,7 @@ __device__ __forceinline__ void lds_dma4_l2(const void* gsrc, uint32_t lds_dst) 
 // ------------------------------------------------------------------------------------------------ LDS layout
 #define OWGS_NSTG 3  // chunk staging buffers
 struct OwgsLayout {
-    uint32_t P, pool, pc, ccw, ct, stgA, stgX, stgL, stgC, fst, spt, hdir, htab, hscr, bhead, nextl, spc, cdirty, skey, lq, rc, sc,
+    uint32_t P, pool, pc, ccw, ct, stgA, stgX, stgL, stgC, fst, spt, hdir, htab, hscr, bhead, nextl, spc, cdirty, skey, lq, fxa, rc, sc,
         uni, uni_bytes, total;
 };
 
@@ -522,8 +540,9 @@ __host__ __device__ inline OwgsLayout owgs_layout(int n_slots, int pool_mode, in
     L.cdirty = L.spc + 4u * OWGS_WL;                // [2][OWGS_WL] pass parity x first lane of an action: re-speculated
     L.skey = L.cdirty + 8u * OWGS_WL;               // per lane {slot key, action} (shared-key check)
     L.lq = L.skey + 8u * OWGS_WL;                   // long-walk queue: {record | rank, step, position, cum} / result
+    L.fxa = L.lq + 16u * OWGS_WL;                  // per lane: validation summary / in-pass re-decision (OWGS_EXT)
     L.rc = o;
-    const uint32_t ua = (L.lq - o) + 16u * OWGS_WL, ur = 4u * OWGS_CTC;
+    const uint32_t ua = (L.fxa - o) + 8u * OWGS_WL, ur = 4u * OWGS_CTC;
     L.uni_bytes = ua > ur ? ua : ur;
     o += L.uni_bytes;
     L.total = o;
@@ -1095,6 +1114,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     int32_t* cdirty = (int32_t*)(L + Y.cdirty);
     uint2* skey = (uint2*)(L + Y.skey);
     uint4* lq = (uint4*)(L + Y.lq);
+    uint2* fxa = (uint2*)(L + Y.fxa);
     uint4* hdir = (uint4*)(L + Y.hdir);
     int32_t* hocc = (int32_t*)(L + Y.hdir + 16u * NHOT);
     int32_t* hflag = (int32_t*)(L + Y.hdir + 20u * NHOT);
@@ -1161,6 +1181,10 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     E.nb = nb;
 
     uint32_t st_pass = 0, st_probe = 0, st_fb = 0, st_long = 0, st_chunk = 0, st_stop = 0, st_gprobe = 0, st_glane = 0;
+    uint32_t st_ext = 0;  // in-pass re-decisions (I/O wave)
+#ifdef OWGS_EXT_PROF
+    u64 xp_cyc = 0, xp_rounds = 0, xp_scans = 0, xp_ph[4] = {0, 0, 0, 0};
+#endif
 #ifdef OWGS_TRACE
     int tr_n = 0;
 #endif
@@ -2431,6 +2455,15 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                     }
 #endif
                 }
+#if OWGS_EXT
+                if (act) {  // the summary the in-pass re-decisions read (commit phase)
+                    const bool exempt = !part || kind == K_FALLBACK;
+                    const bool rd = maxc == 1 && A.pool_mode == 0 && kind == K_TARGET && a != (int)OWGS_REC_NOACT;
+                    fxa[li] = make_uint2(((uint32_t)a & OWGS_REC_NOACT) | (nf ? FX_NF : 0u) | (exempt ? FX_EXEMPT : 0u) |
+                                             (rd ? FX_OK : 0u),
+                                         (uint32_t)sl | ((uint32_t)s_t << 16));
+                }
+#endif
                 if (!io) {
                     // (the lanes of a wave are not in stream order) the wave's smallest such lane
                     if (__ballot(nf)) {
@@ -2450,6 +2483,198 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                     l = f + 1;
                     err |= OWGS_ERR_INTERNAL;
                 }
+#if OWGS_EXT
+                // ---- in-pass re-decisions.  Every lane before l is exact.  Lane l (maxConcurrent == 1, identity pool,
+                // a walk target) is decided exactly here instead of in another pass: the state it sees is the
+                // frontier minus the lanes before it = the tentative permits plus what the lanes from l on took
+                // (bucket lists), and its walk resumes at its speculated step (every earlier step of its walk had no
+                // capacity left for it: its earlier lanes of the same action took those units, others only take
+                // more).  Moving l from its speculated target t to its true target t' only adds room at t and takes
+                // room at t', so a later lane that was known to fit stays exact unless it targets t' or belongs to
+                // l's action (its rank assumed l at t); forced acquires of the pass do not depend on either.  The
+                // next lane that is not known to fit, or hits t' / l's action, is the next stop: re-decided the same
+                // way, up to EXT_MAX per pass (the I/O wave does this; it holds no lanes).
+                const int l0 = l;
+                // (the first stop must be re-decidable, else the pass ends as before)
+                const bool fixup = l < len && (fxa[l].x & FX_OK);
+                if (fixup) {
+                    if (io) {
+#ifdef OWGS_EXT_PROF
+                        const u64 tx0 = memtime_pinned();
+                        u64 tq_prev = tx0;
+#endif
+                        // every lane from l on gives its tentative take back: the permits are then exactly what lane l
+                        // sees (the frontier minus the lanes before it); the lanes that commit add theirs again below
+                        for (int k0 = l; k0 < len; k0 += 64) {
+                            const int k = k0 + lane;
+                            if (k < len) {
+                                const int tk = spt[k];
+                                if (tk >= 0) {
+                                    const int ck = spc[k];
+                                    if (ck) atomicAdd(&P[tk], ck);
+                                }
+                            }
+                        }
+                        int L = l, nE = 0;
+                        // the re-decided lanes' targets and actions as hashed 2048-bit sets over the wave's lanes
+                        uint32_t set_t = 0u, set_a = 0u;
+                        auto hsh = [](uint32_t v) { return (v * 2654435761u) >> 21; };
+                        auto inset = [&](uint32_t bits, uint32_t h) {  // (whole wave: ds_bpermute)
+                            return ((uint32_t)__shfl((int)bits, (int)(h >> 5), 64) >> (h & 31u)) & 1u;
+                        };
+                        while (L < len && nE < EXT_MAX) {
+                            const uint2 fx = fxa[L];
+                            // a re-decided action's next lane waits for the next pass (its rank, and the hot table of
+                            // its action, no longer hold: it re-speculates with its action's other lanes)
+                            const bool a_hit = inset(set_a, hsh(fx.x & OWGS_REC_NOACT)) != 0u;
+                            if (!(fx.x & FX_OK) || a_hit) break;
+                            const uint4 rr = stgA[sbuf * OWGS_WL + (int)(fx.y & 0xFFFFu)];
+                            const int hm_ = (int)(rr.x & OWGS_AM_POS_MASK), st_ = (int)((rr.x >> 15) & OWGS_AM_POS_MASK);
+                            const int pl_ = (rr.x & OWGS_AM_POOL) ? 1 : 0;
+                            const int mm = (int)(rr.y & OWGS_AM_MEM_MASK);
+                            const int nn = pl_ ? nb : nm, base = pl_ ? A.n_ids - nb : 0;
+                            int kn = K_FALLBACK, tn = -1, sn = nn;
+#ifdef OWGS_EXT_PROF
+                            const u64 tq0 = memtime_pinned();
+                            xp_ph[0] += tq0 - tq_prev;
+#endif
+                            // every usable permit count below mem: the walk fails (U bounds the frontier, whose
+                            // permits bound this lane's)
+                            bool done = mm > sc[pl_ ? SC_U1 : SC_U0] && ((A.shortcut_ok >> pl_) & 1);
+                            if (!done) {
+                                const float rnn = __builtin_amdgcn_rcpf((float)nn);
+                                int s0 = (int)(fx.y >> 16);
+                                int p0 = mod_fast(hm_ + s0 * st_, nn, rnn);
+                                const int loff = mod_fast(lane * st_, nn, rnn), boff = mod_fast(64 * st_, nn, rnn),
+                                          roff = mod_fast(128 * st_, nn, rnn);
+                                for (int rd = 0; rd < EXT_ROUNDS; ++rd) {
+#ifdef OWGS_EXT_PROF
+                                    ++xp_rounds;
+#endif
+                                    if (s0 >= nn) {  // every position probed: forced acquire (SCPB:417-424)
+                                        done = true;
+                                        break;
+                                    }
+                                    int pa = p0 + loff;
+                                    pa -= pa >= nn ? nn : 0;
+                                    int pb = pa + boff;
+                                    pb -= pb >= nn ? nn : 0;
+                                    const int xa = base + pa, xb = base + pb;
+                                    const bool ia = s0 + lane < nn, ib = s0 + 64 + lane < nn;
+                                    const int va = ia ? P[xa] : OWGS_PENC, vb = ib ? P[xb] : OWGS_PENC;
+                                    const bool fa = va < OWGS_PLIM && va >= mm;  // (usable: flag folded in)
+                                    const bool fb = vb < OWGS_PLIM && vb >= mm;
+                                    const u64 ma = __ballot(fa), mb = __ballot(fb);
+                                    if (ma | mb) {
+                                        const int q = ma ? ffs64(ma) : ffs64(mb);
+                                        kn = K_TARGET;
+                                        tn = __builtin_amdgcn_readlane(ma ? xa : xb, q);
+                                        sn = s0 + q + (ma ? 0 : 64);
+                                        done = true;
+                                        break;
+                                    }
+                                    s0 += 128;
+                                    p0 += roff;
+                                    p0 -= p0 >= nn ? nn : 0;
+                                }
+                            }
+#ifdef OWGS_EXT_PROF
+                            const u64 tq1 = memtime_pinned();
+                            xp_ph[1] += tq1 - tq0;
+#endif
+                            if (!done) break;  // a long walk: the next pass takes this lane
+                            if (kn == K_FALLBACK) {
+                                const int hc = pl_ ? A.hb : A.hm;
+                                if (hc <= 0) break;
+                                const int64_t iL = c0 + L;
+                                const u64 sq = A.seq ? A.seq[iL] : (A.seq_base + (u64)iL);
+                                tn = select_usable(E, base, (int)rng_index(A.rng_seed, sq, (uint32_t)hc));
+                                if (tn < 0 || tn >= n_slots) break;  // (a throwing lane: the ordinary path)
+                            }
+                            if (lane == 0) {
+                                atomicSub(&P[tn], mm);
+                                fxa[L] = make_uint2(fx.x | FX_DONE | ((uint32_t)kn << 28), (uint32_t)tn | ((uint32_t)sn << 16));
+                                if (kn == K_FALLBACK) atomicMin(&sc[pl_ ? SC_U1 : SC_U0], mm - 1);  // rank 0 failed
+                            }
+                            {
+                                const uint32_t h1 = hsh((uint32_t)tn), h2 = hsh(fx.x & OWGS_REC_NOACT);
+                                if (lane == (int)(h1 >> 5)) set_t |= 1u << (h1 & 31u);
+                                if (lane == (int)(h2 >> 5)) set_a |= 1u << (h2 & 31u);
+                            }
+                            ++nE;
+#ifdef OWGS_EXT_PROF
+                            const u64 tq2 = memtime_pinned();
+                            xp_ph[2] += tq2 - tq1;
+#endif
+                            // the next stop after L: not known to fit, or meets a re-decided target or action
+                            int k0 = L + 1;
+                            L = len;
+                            for (; k0 < len; k0 += 64) {
+#ifdef OWGS_EXT_PROF
+                                ++xp_scans;
+#endif
+                                const int k = k0 + lane;
+                                uint2 f2 = make_uint2(FX_EXEMPT, 0u);
+                                int tk = -1;
+                                if (k < len) {
+                                    f2 = fxa[k];
+                                    tk = spt[k];
+                                }
+                                const bool cl = (inset(set_a, hsh(f2.x & OWGS_REC_NOACT)) | inset(set_t, hsh((uint32_t)tk))) != 0u;
+                                const bool stop = k < len && ((f2.x & FX_NF) || (!(f2.x & FX_EXEMPT) && cl));
+                                const u64 sm = __ballot(stop);
+                                const int q = sm ? ffs64(sm) : 64;
+                                // the lanes before the stop commit where they speculated: their takes again
+                                if (lane < q && k < len && tk >= 0) {
+                                    const int ck = spc[k];
+                                    if (ck) atomicSub(&P[tk], ck);
+                                }
+                                if (sm) {
+                                    L = k0 + q;
+                                    break;
+                                }
+                            }
+#ifdef OWGS_EXT_PROF
+                            tq_prev = memtime_pinned();
+                            xp_ph[3] += tq_prev - tq2;
+#endif
+                        }
+                        // lanes from the limit on that meet a re-decided lane's target or action must speculate again
+                        // (their validation assumed the re-decided lanes where they speculated: a kept one would
+                        // keep a target whose room is gone or a rank that no longer holds)
+                        if (nE > 0)
+                            for (int k0 = L; k0 < len; k0 += 64) {
+                                const int k = k0 + lane;
+                                uint2 f2 = make_uint2(FX_EXEMPT, 0u);
+                                int tk = -1;
+                                if (k < len) {
+                                    f2 = fxa[k];
+                                    tk = spt[k];
+                                }
+                                const bool cl = (inset(set_a, hsh(f2.x & OWGS_REC_NOACT)) | inset(set_t, hsh((uint32_t)tk))) != 0u;
+                                if (k < len && !(f2.x & (FX_EXEMPT | FX_DONE)) && cl) fxa[k].x = f2.x | FX_CLASH;
+                            }
+                        st_ext += (uint32_t)nE;
+#ifdef OWGS_EXT_PROF
+                        xp_cyc += memtime_pinned() - tx0;
+#endif
+                        if (lane == 0) {
+                            sc[SC_LFIN] = L;
+                            sc[SC_NEXT] = nE;
+                        }
+                    }
+                    LDS_SYNC_T(9);
+                    l = sc[SC_LFIN];
+                }
+                if (act && li >= l0 && li < l) {  // re-decided in this pass: its true decision
+                    const uint2 fo = fxa[li];
+                    if (fo.x & FX_DONE) {
+                        kind = (int)(fo.x >> 28);
+                        t = (int)(fo.y & 0xFFFFu);
+                        s_t = (int)(fo.y >> 16);
+                    }
+                }
+#endif
 #ifdef OWGS_STOP_REASONS
                 if (li == l && why) atomicAdd(&A.stats[6], 1ull << (12 * (why - 1)));
 #endif
@@ -2538,12 +2763,19 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                 const u64 tc1 = memtime_pinned();
 #endif
                 if (part) {
+#if OWGS_EXT
+                    if (li >= l && cons && !fixup) atomicAdd(&P[t], cons);  // not committed: give the memory back
+#else
                     if (li >= l && cons) atomicAdd(&P[t], cons);  // not committed: give the memory back
+#endif
                     fst[bk] = 0u;
                     bhead[bk] = 0u;
                 }
                 if (act && li >= l) {
                     keep = !nf;
+#if OWGS_EXT
+                    if (keep && fixup && sc[SC_NEXT] > 0 && (fxa[li].x & FX_CLASH)) keep = false;
+#endif
                     if (!keep && hs >= 0) hflag[hs] = l;  // the action's hot table is needed in the next pass
                     if (!keep && maxc > 1) cdirty[(par ^ 1) * OWGS_WL + lead] = 1;
                 }
@@ -2626,6 +2858,15 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
             for (int k = 0; k < 8; ++k) atomicAdd(&A.stats[8 + k], pt_acc[k]);
             atomicAdd(&A.stats[6], pt_x[0]);
             atomicAdd(&A.stats[7], pt_x[1]);
+        }
+#endif
+        if (io && lane == 0) atomicAdd(&A.stats[31], (u64)st_ext);
+#ifdef OWGS_EXT_PROF
+        if (io && lane == 0) {
+            atomicAdd(&A.stats[28], xp_cyc);
+            atomicAdd(&A.stats[29], xp_rounds);
+            atomicAdd(&A.stats[30], xp_scans);
+            for (int k = 0; k < 4; ++k) atomicAdd(&A.stats[20 + k], xp_ph[k]);
         }
 #endif
         if (tid == 0) {

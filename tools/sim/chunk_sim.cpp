@@ -92,8 +92,9 @@ int main(int argc, char** argv) {
     int A = w.home.size();
     vector<int> cur(A, 0);
     long passes = 0, probes = 0, wave_probe_max = 0, n_rej = 0, rej_same = 0, maxcm = 0, rej_conc = 0, rej_fb = 0;
-    long waves = 0, n_stop = 0, stop_conc = 0, stop_ovf = 0;
+    long waves = 0, n_stop = 0, stop_conc = 0, stop_ovf = 0, n_ext = 0, ext_gain = 0;
     vector<int> spec_t(WCH), spec_s(WCH), spec_fb(WCH), spec_k(WCH);
+    vector<char> kfv(WCH, 1);
     unordered_map<int, int> rankmap;
     for (int b = 0; b < NB; ++b) {
         for (int64_t r = w.rel_off[b]; r < w.rel_off[b + 1]; ++r) { int64_t aid = w.rel_aid[r]; release(S, out[aid], w.act[aid]); }
@@ -143,6 +144,7 @@ int main(int argc, char** argv) {
                         tot[bk] += cons;
                     }
                     static vector<long> pre(1 << 20, 0);
+                    bool stopped = false;
                     for (int64_t i = f; i < end; ++i) {
                         int a = w.act[i]; int t = spec_t[i - c0]; int bk = (unsigned)(t * 2654435761u) % B; if (B == (1<<20)) bk = t;
                         bool kf = firstl[bk] == i || spec_fb[i - c0] || tot[bk] <= S.P[t];
@@ -159,17 +161,41 @@ int main(int argc, char** argv) {
                             // shared key: another action with the same slot in [f,i) -> uncertain; concurrent fallback of same key earlier -> uncertain
                             for (int64_t j = f; j < i; ++j) { int aj = w.act[j]; if (w.slot[aj] == w.slot[a] && (aj != a || spec_fb[j - c0])) { if (kf) ck = true; kf = false; break; } }
                         }
-                        if (!kf) { lim = i; if (ck) ++stop_conc; else if (tot[bk] > S.P[t]) ++stop_ovf; break; }
+                        kfv[i - c0] = kf;
+                        if (!kf && !stopped) { lim = i; stopped = true; if (ck) ++stop_conc; else if (tot[bk] > S.P[t]) ++stop_ovf; if (mode < 7) break; }
                     }
                     for (int bk : touched) { tot[bk] = 0; firstl[bk] = -1; }
                     if (mode >= 5) for (int64_t i = f; i < end; ++i) pre[spec_t[i - c0]] = 0;
                 }
                 // exact validation in stream order
                 int64_t i = f;
+                bool ext_used = false;
+                vector<int> ext_acts, ext_tg;
                 for (; i < end; ++i) {
                     int a = w.act[i]; int fb, so;
                     int t = decide(S, i, a, cur[a], &fb, &so);
                     bool okk = (t == spec_t[i - c0]) && (fb == spec_fb[i - c0]);
+                    bool aclash = false;
+                    if (mode == 9) for (int q : ext_acts) if (q == a) aclash = true;
+                    if (mode >= 7 && i == lim && lim < end && w.maxc[a] == 1 && !ext_used && !aclash) {
+                        // extension: the stop lane is re-decided exactly in this pass; later lanes known to fit that
+                        // are neither of its action nor at its new target commit too
+                        ext_used = mode == 7;
+                        ++n_ext;
+                        int64_t l2 = i + 1;
+                        ext_acts.push_back(a); ext_tg.push_back(t);
+                        auto clash = [&](int64_t k) {
+                            for (size_t q = 0; q < ext_acts.size(); ++q)
+                                if (w.act[k] == ext_acts[q] || spec_t[k - c0] == ext_tg[q]) return true;
+                            return false;
+                        };
+                        while (l2 < end && kfv[l2 - c0] && !clash(l2)) ++l2;
+                        ext_gain += l2 - i - 1;
+                        lim = l2;
+                        acquire(S, t, a, fb); out[i] = t;
+                        if (w.maxc[a] == 1) cur[a] = fb ? (w.pool[a] ? w.bpool.size() : w.mpool.size()) : so;
+                        continue;
+                    }
                     if (mode >= 2 && i >= lim) { if (!okk) {} ++n_stop; acquire(S, t, a, fb); out[i] = t; if (w.maxc[a] == 1) cur[a] = fb ? (w.pool[a] ? w.bpool.size() : w.mpool.size()) : so; ++i; break; }
                     if (mode >= 2 && !okk) { fprintf(stderr, "UNSOUND at %ld\n", (long)i); exit(2); }
                     acquire(S, t, a, fb);
@@ -187,7 +213,7 @@ int main(int argc, char** argv) {
         }
     }
     long bad = 0; for (int64_t i = 0; i < N; ++i) if (out[i] != w.out[i]) ++bad;
-    printf("%s W=%d mode=%d: mismatches=%ld passes=%ld (%.3f/lane, %.2f per chunk) rej=%ld (same-action %ld, conc %ld, fb %ld) probes/lane=%.2f wavemax/pass=%.2f maxcm=%ld stops=%ld conc=%ld ovf=%ld\n",
+    printf("%s W=%d mode=%d: mismatches=%ld passes=%ld (%.3f/lane, %.2f per chunk) rej=%ld (same-action %ld, conc %ld, fb %ld) probes/lane=%.2f wavemax/pass=%.2f maxcm=%ld stops=%ld conc=%ld ovf=%ld ext=%ld ext_gain=%ld\n",
            d.c_str(), WCH, mode, bad, passes, (double)passes / N, (double)passes / ((double)N / WCH), n_rej, rej_same, rej_conc, rej_fb, (double)probes / N,
-           (double)wave_probe_max / passes, maxcm, n_stop, stop_conc, stop_ovf);
+           (double)wave_probe_max / passes, maxcm, n_stop, stop_conc, stop_ovf, n_ext, ext_gain);
 }
