@@ -71,7 +71,9 @@ typedef unsigned long long u64;
 #define EXT_ROUNDS 8  // walk rounds (128 steps each) a re-decision may take; a longer walk waits for the next pass
 #endif
 // fxa[li] (per lane of the pass, stream order): x = action | not known to fit << 24 | exempt << 25 | re-decidable << 26
-// | re-decided << 27 | kind << 28; y = record position | walk step << 16, after a re-decision target | step << 16
+// | re-decided << 27 | kind << 28 | clash << 30; y = target (0xFFFF none) | walk step << 16 (after a re-decision: the
+// new ones); z = the action's meta.x (home | step << 15 | pool); w = mem | took memory << 31
+#define FX_NOT 0xFFFFu
 #define FX_NF (1u << 24)
 #define FX_EXEMPT (1u << 25)
 #define FX_OK (1u << 26)
@@ -542,7 +544,7 @@ __host__ __device__ inline OwgsLayout owgs_layout(int n_slots, int pool_mode, in
     L.lq = L.skey + 8u * OWGS_WL;                   // long-walk queue: {record | rank, step, position, cum} / result
     L.fxa = L.lq + 16u * OWGS_WL;                  // per lane: validation summary / in-pass re-decision (OWGS_EXT)
     L.rc = o;
-    const uint32_t ua = (L.fxa - o) + 8u * OWGS_WL, ur = 4u * OWGS_CTC;
+    const uint32_t ua = (L.fxa - o) + 16u * OWGS_WL, ur = 4u * OWGS_CTC;
     L.uni_bytes = ua > ur ? ua : ur;
     o += L.uni_bytes;
     L.total = o;
@@ -1114,7 +1116,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     int32_t* cdirty = (int32_t*)(L + Y.cdirty);
     uint2* skey = (uint2*)(L + Y.skey);
     uint4* lq = (uint4*)(L + Y.lq);
-    uint2* fxa = (uint2*)(L + Y.fxa);
+    uint4* fxa = (uint4*)(L + Y.fxa);
     uint4* hdir = (uint4*)(L + Y.hdir);
     int32_t* hocc = (int32_t*)(L + Y.hdir + 16u * NHOT);
     int32_t* hflag = (int32_t*)(L + Y.hdir + 20u * NHOT);
@@ -2459,9 +2461,10 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                 if (act) {  // the summary the in-pass re-decisions read (commit phase)
                     const bool exempt = !part || kind == K_FALLBACK;
                     const bool rd = maxc == 1 && A.pool_mode == 0 && kind == K_TARGET && a != (int)OWGS_REC_NOACT;
-                    fxa[li] = make_uint2(((uint32_t)a & OWGS_REC_NOACT) | (nf ? FX_NF : 0u) | (exempt ? FX_EXEMPT : 0u) |
+                    fxa[li] = make_uint4(((uint32_t)a & OWGS_REC_NOACT) | (nf ? FX_NF : 0u) | (exempt ? FX_EXEMPT : 0u) |
                                              (rd ? FX_OK : 0u),
-                                         (uint32_t)sl | ((uint32_t)s_t << 16));
+                                         (part ? (uint32_t)t : FX_NOT) | ((uint32_t)s_t << 16), rc4.x,
+                                         (uint32_t)mem | ((part && cons) ? 0x80000000u : 0u));
                 }
 #endif
                 if (!io) {
@@ -2508,11 +2511,8 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         for (int k0 = l; k0 < len; k0 += 64) {
                             const int k = k0 + lane;
                             if (k < len) {
-                                const int tk = spt[k];
-                                if (tk >= 0) {
-                                    const int ck = spc[k];
-                                    if (ck) atomicAdd(&P[tk], ck);
-                                }
+                                const uint4 f2 = fxa[k];
+                                if (f2.w >> 31) atomicAdd(&P[(int)(f2.y & 0xFFFFu)], (int)(f2.w & OWGS_AM_MEM_MASK));
                             }
                         }
                         int L = l, nE = 0;
@@ -2523,15 +2523,17 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             return ((uint32_t)__shfl((int)bits, (int)(h >> 5), 64) >> (h & 31u)) & 1u;
                         };
                         while (L < len && nE < EXT_MAX) {
-                            const uint2 fx = fxa[L];
+                            const uint4 fx = fxa[L];
                             // a re-decided action's next lane waits for the next pass (its rank, and the hot table of
                             // its action, no longer hold: it re-speculates with its action's other lanes)
                             const bool a_hit = inset(set_a, hsh(fx.x & OWGS_REC_NOACT)) != 0u;
                             if (!(fx.x & FX_OK) || a_hit) break;
-                            const uint4 rr = stgA[sbuf * OWGS_WL + (int)(fx.y & 0xFFFFu)];
-                            const int hm_ = (int)(rr.x & OWGS_AM_POS_MASK), st_ = (int)((rr.x >> 15) & OWGS_AM_POS_MASK);
-                            const int pl_ = (rr.x & OWGS_AM_POOL) ? 1 : 0;
-                            const int mm = (int)(rr.y & OWGS_AM_MEM_MASK);
+                            // (uniform: scalar registers, and the pool's fields become scalar loads -- a vector load
+                            // here would wait for the I/O wave's own prefetch stream, vmcnt(0))
+                            const uint32_t fz = __builtin_amdgcn_readfirstlane(fx.z), fw = __builtin_amdgcn_readfirstlane(fx.w);
+                            const int hm_ = (int)(fz & OWGS_AM_POS_MASK), st_ = (int)((fz >> 15) & OWGS_AM_POS_MASK);
+                            const int pl_ = (fz & OWGS_AM_POOL) ? 1 : 0;
+                            const int mm = (int)(fw & OWGS_AM_MEM_MASK);
                             const int nn = pl_ ? nb : nm, base = pl_ ? A.n_ids - nb : 0;
                             int kn = K_FALLBACK, tn = -1, sn = nn;
 #ifdef OWGS_EXT_PROF
@@ -2586,14 +2588,16 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             if (kn == K_FALLBACK) {
                                 const int hc = pl_ ? A.hb : A.hm;
                                 if (hc <= 0) break;
-                                const int64_t iL = c0 + L;
-                                const u64 sq = A.seq ? A.seq[iL] : (A.seq_base + (u64)iL);
+                                // (explicit per-activation sequence numbers: the ordinary path -- a global load here
+                                // would wait for the I/O wave's prefetch stream)
+                                if (A.seq) break;
+                                const u64 sq = A.seq_base + (u64)(c0 + L);
                                 tn = select_usable(E, base, (int)rng_index(A.rng_seed, sq, (uint32_t)hc));
                                 if (tn < 0 || tn >= n_slots) break;  // (a throwing lane: the ordinary path)
                             }
                             if (lane == 0) {
                                 atomicSub(&P[tn], mm);
-                                fxa[L] = make_uint2(fx.x | FX_DONE | ((uint32_t)kn << 28), (uint32_t)tn | ((uint32_t)sn << 16));
+                                *(uint2*)&fxa[L] = make_uint2(fx.x | FX_DONE | ((uint32_t)kn << 28), (uint32_t)tn | ((uint32_t)sn << 16));
                                 if (kn == K_FALLBACK) atomicMin(&sc[pl_ ? SC_U1 : SC_U0], mm - 1);  // rank 0 failed
                             }
                             {
@@ -2614,21 +2618,15 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                 ++xp_scans;
 #endif
                                 const int k = k0 + lane;
-                                uint2 f2 = make_uint2(FX_EXEMPT, 0u);
-                                int tk = -1;
-                                if (k < len) {
-                                    f2 = fxa[k];
-                                    tk = spt[k];
-                                }
-                                const bool cl = (inset(set_a, hsh(f2.x & OWGS_REC_NOACT)) | inset(set_t, hsh((uint32_t)tk))) != 0u;
+                                uint4 f2 = make_uint4(FX_EXEMPT, FX_NOT, 0u, 0u);
+                                if (k < len) f2 = fxa[k];
+                                const uint32_t tk = f2.y & 0xFFFFu;
+                                const bool cl = (inset(set_a, hsh(f2.x & OWGS_REC_NOACT)) | inset(set_t, hsh(tk))) != 0u;
                                 const bool stop = k < len && ((f2.x & FX_NF) || (!(f2.x & FX_EXEMPT) && cl));
                                 const u64 sm = __ballot(stop);
                                 const int q = sm ? ffs64(sm) : 64;
                                 // the lanes before the stop commit where they speculated: their takes again
-                                if (lane < q && k < len && tk >= 0) {
-                                    const int ck = spc[k];
-                                    if (ck) atomicSub(&P[tk], ck);
-                                }
+                                if (lane < q && (f2.w >> 31)) atomicSub(&P[(int)tk], (int)(f2.w & OWGS_AM_MEM_MASK));
                                 if (sm) {
                                     L = k0 + q;
                                     break;
@@ -2645,13 +2643,9 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         if (nE > 0)
                             for (int k0 = L; k0 < len; k0 += 64) {
                                 const int k = k0 + lane;
-                                uint2 f2 = make_uint2(FX_EXEMPT, 0u);
-                                int tk = -1;
-                                if (k < len) {
-                                    f2 = fxa[k];
-                                    tk = spt[k];
-                                }
-                                const bool cl = (inset(set_a, hsh(f2.x & OWGS_REC_NOACT)) | inset(set_t, hsh((uint32_t)tk))) != 0u;
+                                uint4 f2 = make_uint4(FX_EXEMPT, FX_NOT, 0u, 0u);
+                                if (k < len) f2 = fxa[k];
+                                const bool cl = (inset(set_a, hsh(f2.x & OWGS_REC_NOACT)) | inset(set_t, hsh(f2.y & 0xFFFFu))) != 0u;
                                 if (k < len && !(f2.x & (FX_EXEMPT | FX_DONE)) && cl) fxa[k].x = f2.x | FX_CLASH;
                             }
                         st_ext += (uint32_t)nE;
@@ -2667,7 +2661,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                     l = sc[SC_LFIN];
                 }
                 if (act && li >= l0 && li < l) {  // re-decided in this pass: its true decision
-                    const uint2 fo = fxa[li];
+                    const uint2 fo = *(const uint2*)&fxa[li];
                     if (fo.x & FX_DONE) {
                         kind = (int)(fo.x >> 28);
                         t = (int)(fo.y & 0xFFFFu);
