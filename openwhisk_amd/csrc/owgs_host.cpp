@@ -423,7 +423,7 @@ static void base_args(owgs_ctx* c, OwgsEngineArgs& A) {
 }
 
 // Chunk width of a replay.  Wide chunks amortise a pass over more activations, but lanes of different actions that
-// meet at an invoker without room for both stop the pass.  How often that happens follows the capacity units the
+// meet at an invoker without room for both stop the pass (or cost a re-decision inside it).  How often that happens follows the capacity units the
 // managed pool offers (slot MB x invokers / mean action MB): with few units (small pools, or slots split over many
 // controllers) a narrow chunk wins (measured, round 2: C5 shard of 8, 23k units: 244 ms at 128 lanes vs 349 at 336;
 // configs[1], 19k units: 129 vs 139 ms at 256; headline, 187k units: 34 ms at 336 vs 37 at 256).  Env OWGS_CW
@@ -438,7 +438,9 @@ static int32_t chunk_width(const owgs_ctx* c) {
         slot_mb += (double)std::max<int64_t>(c->cfg.min_memory_bytes, c->mem[i] / std::max(c->cluster, 1)) / 1048576.0;
     for (int32_t m : c->a_mem) act_mb += m;
     const double units = c->a_mem.empty() || act_mb <= 0 ? 1e9 : slot_mb / (act_mb / (double)c->a_mem.size());
-    int32_t cw = units >= OWGS_WIDE_UNITS ? OWGS_WL : std::min(128, OWGS_WL);
+    // (with in-pass re-decisions, round 2: configs[1] 19k units 116 ms at 192 vs 119 at 128; configs[3] 221 vs 232;
+    // C5 shard of 8 165 vs 173; C5 shard of 4, 34k units: 102 ms at 256 vs 106 at 192 and 117 at 128)
+    int32_t cw = units >= OWGS_WIDE_UNITS ? OWGS_WL : std::min(units >= OWGS_WIDE_UNITS / 2 ? 256 : 192, OWGS_WL);
     if (const char* e = getenv("OWGS_CW")) {
         const int v = atoi(e);
         if (v >= 64 && v <= OWGS_WL) cw = v;
