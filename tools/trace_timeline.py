@@ -18,7 +18,7 @@ n = int((ids[0] > 0).sum())
 ids, ta, td = ids[:, :n], ta[:, :n], td[:, :n]
 assert (ids == ids[0]).all(), "waves disagree on the barrier sequence"
 names = {1: "chunk_start", 2: "speculate", 3: "tentative", 4: "validate", 5: "commit", 8: "long-walk queue",
-         6: "(mark) chunk loop", 7: "(mark) lane decode"}
+         6: "(mark) chunk loop", 7: "(mark) lane decode", 9: "re-decisions"}
 work = ta[:, 1:] - td[:, :-1]  # per wave: departure of barrier k-1 -> arrival at barrier k
 crit = work.max(axis=0)
 last = work.argmax(axis=0)
