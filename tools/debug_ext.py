@@ -30,6 +30,9 @@ for lib in sys.argv[3:]:
     g_inv, g_fl, g_rf = b.replay(w.stream)
     bad = np.nonzero(o_inv != g_inv)[0]
     print(lib, "mismatches", len(bad), "first", bad[:8].tolist(), b.stats(), flush=True)
+    fb = np.nonzero(o_fl != g_fl)[0]
+    if len(fb):
+        print("  flag mismatches", len(fb), [(int(j), int(o_inv[j]), int(o_fl[j]), int(g_fl[j]), int(w.stream.act[j])) for j in fb[:10]], flush=True)
     if len(bad):
         i0 = int(bad[0])
         bs = np.searchsorted(w.stream.acq_off, i0, side="right") - 1

@@ -92,7 +92,7 @@ int main(int argc, char** argv) {
     int A = w.home.size();
     vector<int> cur(A, 0);
     long passes = 0, probes = 0, wave_probe_max = 0, n_rej = 0, rej_same = 0, maxcm = 0, rej_conc = 0, rej_fb = 0;
-    long waves = 0, n_stop = 0, stop_conc = 0, stop_ovf = 0, n_ext = 0, ext_gain = 0;
+    long waves = 0, n_stop = 0, stop_conc = 0, stop_ovf = 0, n_ext = 0, ext_gain = 0, n_resume_bad = 0;
     vector<int> spec_t(WCH), spec_s(WCH), spec_fb(WCH), spec_k(WCH);
     vector<char> kfv(WCH, 1);
     unordered_map<int, int> rankmap;
@@ -175,13 +175,22 @@ int main(int argc, char** argv) {
                     int a = w.act[i]; int fb, so;
                     int t = decide(S, i, a, cur[a], &fb, &so);
                     bool okk = (t == spec_t[i - c0]) && (fb == spec_fb[i - c0]);
-                    bool aclash = false;
-                    if (mode == 9) for (int q : ext_acts) if (q == a) aclash = true;
+                    bool aclash = false, aclash_any = false;
+                    for (int q : ext_acts) if (q == a) aclash_any = true;
+                    if (mode == 9) aclash = aclash_any;
                     if (mode >= 7 && i == lim && lim < end && w.maxc[a] == 1 && !ext_used && !aclash) {
                         // extension: the stop lane is re-decided exactly in this pass; later lanes known to fit that
                         // are neither of its action nor at its new target commit too
                         ext_used = mode == 7;
                         ++n_ext;
+                        if (!spec_fb[i - c0]) {  // the kernel resumes the walk at the speculated step: same answer?
+                            int fb2, so2;
+                            const int t2 = decide(S, i, a, spec_s[i - c0], &fb2, &so2);
+                            if (t2 != t || fb2 != fb) {
+                                ++n_resume_bad;
+                                if (n_resume_bad <= 5) fprintf(stderr, "resume mismatch at %ld: exact %d/%d from cur %d, resumed %d/%d from %d (aclash %d)\n", (long)i, t, fb, cur[a], t2, fb2, spec_s[i - c0], (int)aclash_any);
+                            }
+                        }
                         int64_t l2 = i + 1;
                         ext_acts.push_back(a); ext_tg.push_back(t);
                         auto clash = [&](int64_t k) {
@@ -213,7 +222,7 @@ int main(int argc, char** argv) {
         }
     }
     long bad = 0; for (int64_t i = 0; i < N; ++i) if (out[i] != w.out[i]) ++bad;
-    printf("%s W=%d mode=%d: mismatches=%ld passes=%ld (%.3f/lane, %.2f per chunk) rej=%ld (same-action %ld, conc %ld, fb %ld) probes/lane=%.2f wavemax/pass=%.2f maxcm=%ld stops=%ld conc=%ld ovf=%ld ext=%ld ext_gain=%ld\n",
+    printf("%s W=%d mode=%d: mismatches=%ld passes=%ld (%.3f/lane, %.2f per chunk) rej=%ld (same-action %ld, conc %ld, fb %ld) probes/lane=%.2f wavemax/pass=%.2f maxcm=%ld stops=%ld conc=%ld ovf=%ld ext=%ld ext_gain=%ld resume_bad=%ld\n",
            d.c_str(), WCH, mode, bad, passes, (double)passes / N, (double)passes / ((double)N / WCH), n_rej, rej_same, rej_conc, rej_fb, (double)probes / N,
-           (double)wave_probe_max / passes, maxcm, n_stop, stop_conc, stop_ovf, n_ext, ext_gain);
+           (double)wave_probe_max / passes, maxcm, n_stop, stop_conc, stop_ovf, n_ext, ext_gain, n_resume_bad);
 }
