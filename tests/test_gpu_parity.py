@@ -206,6 +206,21 @@ def test_stream_parity_pool_capacity_bounds(kw):
     check_stream(w)
 
 
+@pytest.mark.parametrize("seed,kw", [
+    (11, dict(n_invokers=300, load=1.0, conc_frac=0.0, blackbox_frac=0.0, unhealthy_frac=0.0)),
+    (12, dict(n_invokers=257, load=1.3, conc_frac=0.1, blackbox_frac=0.1, unhealthy_frac=0.05)),
+    (13, dict(n_invokers=600, load=0.95, conc_frac=0.3, conc_range=(2, 6), shared_frac=0.4)),
+    (14, dict(n_invokers=1000, load=1.1, cluster_size=4, zipf_s=1.3)),
+])
+def test_stream_parity_in_pass_redecisions(seed, kw):
+    # small, nearly full pools: most passes stop on a lane whose invoker an earlier lane filled, and the I/O wave
+    # re-decides those lanes inside the pass -- many per pass, with fallbacks, hot actions,
+    # concurrent lanes and blackbox pools around them
+    w = W.config("headline", n_activations=60_000, seed=seed, **kw)
+    b, _, _ = check_stream(w)
+    assert b.stats()["redecided"] > 0
+
+
 def test_malformed_release_stream_fails_loudly():
     # a stream that releases one activation twice (CommonLoadBalancer never does: activationSlots.remove finds no
     # entry the second time, CLB:278-279) is rejected by the release front end (owgs_relpos_kernel's claim of the
