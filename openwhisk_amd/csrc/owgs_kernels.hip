@@ -2489,8 +2489,8 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
 #if OWGS_EXT
                 // ---- in-pass re-decisions.  Every lane before l is exact.  Lane l (maxConcurrent == 1, identity pool,
                 // a walk target) is decided exactly here instead of in another pass: the state it sees is the
-                // frontier minus the lanes before it = the tentative permits plus what the lanes from l on took
-                // (bucket lists), and its walk resumes at its speculated step (every earlier step of its walk had no
+                // frontier minus the lanes before it = the tentative permits once the lanes from l on give their takes
+                // back (below), and its walk resumes at its speculated step (every earlier step of its walk had no
                 // capacity left for it: its earlier lanes of the same action took those units, others only take
                 // more).  Moving l from its speculated target t to its true target t' only adds room at t and takes
                 // room at t', so a later lane that was known to fit stays exact unless it targets t' or belongs to
