@@ -308,8 +308,9 @@ int owgs_update_health_device(owgs_ctx* ctx, int32_t n, const uint8_t* status_de
 int owgs_selftest(owgs_ctx* ctx);
 
 /* Engine counters of the last engine launch (diagnostics): [0] resolution passes, [1] walk probes, [2] overload
- * fallbacks, [3] wave-cooperative long walks, [4] chunks, [5] passes that stopped before the chunk end;
- * [8..15] per-phase shader cycles in the diagnostic build (libowgs_prof.so). */
+ * fallbacks, [3] wave-cooperative long walks, [4] chunks, [5] passes that stopped before the chunk end,
+ * [31] lanes re-decided inside their pass; [8..15] per-phase shader cycles in the diagnostic build
+ * (libowgs_prof.so). */
 int owgs_read_stats(owgs_ctx* ctx, uint64_t* out, int32_t cap);
 
 #ifdef __cplusplus
