@@ -1,8 +1,11 @@
 import sys, numpy as np
-sys.path.insert(0,'/root/repo'); sys.path.insert(0,'/root/repo/oracle')
+import os as _os
+_root = _os.path.dirname(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))))
+sys.path.insert(0, _root); sys.path.insert(0, _os.path.join(_root, 'oracle'))
 import oracle as O
 from openwhisk_amd import workload as W
 name = sys.argv[1]; nact = int(sys.argv[2]) if len(sys.argv)>2 else None
+out_root = sys.argv[3] if len(sys.argv) > 3 else '/tmp/sim'
 w = W.config(name, n_activations=nact)
 st = O.state_for(w)
 nm, nb = st.managed_size, st.blackbox_size
@@ -23,12 +26,14 @@ for i,a in enumerate(w.actions):
 perm = st.permits()
 out, fl, rf = st.replay(w.stream)
 s = w.stream
-np.savez(f'/tmp/sim/{name}.npz', perm=perm, mpool=mpool.astype(np.int32), bpool=bpool.astype(np.int32), usable=usable.astype(np.int32),
+import os
+os.makedirs(out_root, exist_ok=True)
+np.savez(f'{out_root}/{name}.npz', perm=perm, mpool=mpool.astype(np.int32), bpool=bpool.astype(np.int32), usable=usable.astype(np.int32),
   home=home, step=step, mem=mem, maxc=maxc, pool=pool, slot=slot, act=s.act.astype(np.int32), acq_off=s.acq_off, rel_off=s.rel_off, rel_aid=s.rel_aid,
   out=out, fl=fl, rf=rf, seed=np.array([w.rng_seed],np.uint64))
 print(name, n, nm, nb, A, len(s.act), s.n_batches, len(s.rel_aid), 'fallbacks', int((fl&1).sum()), 'perm0', perm[:3])
 import os
-d=f'/tmp/sim/{name}'; os.makedirs(d, exist_ok=True)
+d=f'{out_root}/{name}'; os.makedirs(d, exist_ok=True)
 for k,v in dict(perm=perm.astype(np.int32), mpool=mpool.astype(np.int32), bpool=bpool.astype(np.int32), usable=usable.astype(np.int32),
   home=home, step=step, mem=mem, maxc=maxc, pool=pool, slot=slot, act=s.act.astype(np.int32), acq_off=s.acq_off.astype(np.int64), rel_off=s.rel_off.astype(np.int64), rel_aid=s.rel_aid.astype(np.int64),
   out=out.astype(np.int32), fl=fl.astype(np.uint8), seed=np.array([w.rng_seed],np.uint64)).items():
