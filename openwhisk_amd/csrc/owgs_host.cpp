@@ -73,6 +73,12 @@ extern "C" hipError_t owgs_launch_msg_plan(const OwgsMsgArgs* a, int32_t bits, v
                                            hipStream_t st);
 extern "C" hipError_t owgs_launch_msg_write(const OwgsMsgArgs* a, hipStream_t st);
 extern "C" size_t owgs_engine_lds_bytes(int n_slots, int pool_mode, int n_ids, int nm, int nb, int n_actions);
+extern "C" hipError_t owgs_launch_w_rebuild(const OwgsWRebuildArgs* a, hipStream_t s);
+extern "C" hipError_t owgs_launch_w_update(const OwgsWUpdateArgs* a, hipStream_t s);
+extern "C" hipError_t owgs_launch_w_relgather(const int64_t* rel_aid, int32_t n, const int32_t* out_inv,
+                                              const int32_t* act, const int32_t* act_mem, const int32_t* act_maxc,
+                                              const int32_t* act_slot, int32_t* inv, int32_t* mem, int32_t* maxc,
+                                              int32_t* slot, hipStream_t s);
 
 namespace {
 
@@ -206,6 +212,16 @@ struct owgs_ctx {
     DevBuf<ulonglong2> m_aid, m_cause;
     DevBuf<uint8_t> m_flags, m_temp;
     int64_t h_now = INT64_MIN;
+    // watched (invoker, fqn) pairs after a slot-state reset (owgs_watch.hip; w_cap == 0: none)
+    DevBuf<uint32_t> w_keys, w_vals;
+    DevBuf<int32_t> w_cnt, w_wkey, w_D, w_L, w_Lcnt, w_rel;
+    DevBuf<uint4> w_L2;
+    DevBuf<int64_t> w_off;
+    DevBuf<uint8_t> w_rfl;
+    int32_t w_cap = 0, w_live = 0;
+    DevBuf<uint32_t> s_w_keys, s_w_vals;
+    DevBuf<int32_t> s_w_wkey;
+    int32_t s_w_cap = 0, s_w_live = 0;
     // snapshot
     DevBuf<int32_t> s_permits;
     DevBuf<uint32_t> s_ct_keys, s_ct_vals;
@@ -391,6 +407,90 @@ static int reset_ctab(owgs_ctx* c) {
     return OWGS_OK;
 }
 
+// ---------------------------------------------------------------------------------------------- watched pairs
+static OwgsWatch watch_args(const owgs_ctx* c) {
+    OwgsWatch w{};
+    if (c->w_cap > 0) {
+        w.keys = c->w_keys.p;
+        w.vals = c->w_vals.p;
+        w.cap = c->w_cap;
+        w.cnt = c->w_cnt.p;
+        w.wkey = c->w_wkey.p;
+    }
+    return w;
+}
+
+static void w_drop(owgs_ctx* c) {
+    c->w_keys.release();
+    c->w_vals.release();
+    c->w_wkey.release();
+    c->w_cap = 0;
+    c->w_live = 0;
+}
+
+// after a call that may have taken pairs out of W (a release that threw NoSuchElement): its live count
+static int w_refresh(owgs_ctx* c, hipStream_t s) {
+    if (c->w_cap <= 0) return OWGS_OK;
+    int32_t live = 0;
+    HIPCHK(c, hipMemcpyAsync(&live, c->w_cnt.p, sizeof(live), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    c->w_live = live;
+    if (live <= 0) w_drop(c);
+    return OWGS_OK;
+}
+
+// A reset (updateCluster SCPB:561-584, the _invokerSlots test seam) is about to discard the concurrency map: every
+// pair with activations in flight (operationCount of its entry + d of the pair) becomes watched (owgs_watch.hip).
+static int w_rebuild(owgs_ctx* c) {
+    hipStream_t s = c->stream;
+    int32_t ovf_n = 0;
+    HIPCHK(c, hipStreamSynchronize(s));
+    if (c->ovf_cap > 0) HIPCHK(c, hipMemcpy(&ovf_n, c->d_ovf_cnt.p, sizeof(ovf_n), hipMemcpyDeviceToHost));
+    const int64_t cand = (int64_t)OWGS_CTC + ovf_n + c->w_live;
+    int64_t cap = 1024;
+    while (cap < 2 * cand) cap <<= 1;
+    DevBuf<uint32_t> nk, nv;
+    HIPCHK(c, nk.reserve((size_t)cap));
+    HIPCHK(c, nv.reserve((size_t)cap));
+    HIPCHK(c, c->w_cnt.reserve(1));
+    HIPCHK(c, hipMemsetAsync(nk.p, 0, (size_t)cap * 4, s));
+    HIPCHK(c, hipMemsetAsync(nv.p, 0, (size_t)cap * 4, s));
+    HIPCHK(c, hipMemsetAsync(c->w_cnt.p, 0, 4, s));
+    DevBuf<int32_t> nw;  // per-key counts of the new W
+    HIPCHK(c, nw.reserve((size_t)OWGS_MAX_SLOTKEYS + 1));
+    HIPCHK(c, hipMemsetAsync(nw.p, 0, ((size_t)OWGS_MAX_SLOTKEYS + 1) * 4, s));
+    OwgsWRebuildArgs a{};
+    a.ct_keys = c->d_ct_keys.p;
+    a.ct_vals = c->d_ct_vals.p;
+    a.ovf = ovf_args(c);
+    if (ovf_n <= 0) a.ovf.cap = 0;
+    a.old_w = watch_args(c);
+    a.new_w.keys = nk.p;
+    a.new_w.vals = nv.p;
+    a.new_w.cap = (int32_t)cap;
+    a.new_w.cnt = c->w_cnt.p;
+    a.new_w.wkey = nw.p;
+    HIPCHK(c, owgs_launch_w_rebuild(&a, s));
+    int32_t live = 0;
+    HIPCHK(c, hipMemcpyAsync(&live, c->w_cnt.p, sizeof(live), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    w_drop(c);
+    if (live > 0) {
+        c->w_keys = nk;
+        c->w_vals = nv;
+        c->w_wkey = nw;
+        nk.p = nv.p = nullptr;
+        nw.p = nullptr;
+        c->w_cap = (int32_t)cap;
+        c->w_live = live;
+    } else {
+        nk.release();
+        nv.release();
+        nw.release();
+    }
+    return OWGS_OK;
+}
+
 static void base_args(owgs_ctx* c, OwgsEngineArgs& A) {
     memset(&A, 0, sizeof(A));
     A.permits = c->d_permits.p;
@@ -520,6 +620,45 @@ static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s, bool launch
             fclose(f);
         }
     }
+    return OWGS_OK;
+}
+
+// after a publish run in watch mode: Z of the watched pairs its decisions tried and failed (owgs_watch.hip).  d_act =
+// the run's action handles (device), or null for explicit walks (d_xmeta / d_xslot of owgs_schedule_walks)
+static int w_update(owgs_ctx* c, int32_t n, const int32_t* d_act, const int32_t* d_out, const uint8_t* d_fl,
+                    hipStream_t s) {
+    if (c->w_cap <= 0 || n <= 0) return OWGS_OK;
+    const size_t na = std::max<size_t>(c->a_mem.size(), 1);
+    const int32_t* before = c->w_D.p;
+    const size_t had = c->w_D.n;
+    HIPCHK(c, c->w_D.reserve(na));
+    if (c->w_D.p != before || had == 0) HIPCHK(c, hipMemsetAsync(c->w_D.p, 0, c->w_D.n * 4, s));  // zero between runs
+    HIPCHK(c, c->w_L.reserve((size_t)n));
+    HIPCHK(c, c->w_L2.reserve((size_t)n));
+    HIPCHK(c, c->w_Lcnt.reserve(2));
+    OwgsWUpdateArgs a{};
+    a.n = n;
+    a.act = d_act;
+    a.act_meta = c->d_act_meta.p;
+    a.act_slot = c->d_act_slot.p;
+    a.xmeta = c->d_xmeta.p;
+    a.xslot = c->d_xslot.p;
+    a.out_inv = d_out;
+    a.out_flags = d_fl;
+    a.pool_mode = c->pool_mode;
+    a.n_ids = c->n_ids;
+    a.nm = c->nm;
+    a.nb = c->nb;
+    a.usable = c->d_usable.p;
+    a.pool_words = c->d_pool_words.p;
+    a.ct_keys = c->d_ct_keys.p;
+    a.ovf = ovf_args(c);
+    a.w = watch_args(c);
+    a.D = c->w_D.p;
+    a.L = c->w_L.p;
+    a.L2 = c->w_L2.p;
+    a.Lcnt = c->w_Lcnt.p;
+    HIPCHK(c, owgs_launch_w_update(&a, s));
     return OWGS_OK;
 }
 
@@ -669,6 +808,13 @@ void owgs_destroy(owgs_ctx* c) {
     c->m_cause.release();
     c->m_flags.release();
     c->m_temp.release();
+    DevBuf<uint32_t>* wu[] = {&c->w_keys, &c->w_vals, &c->s_w_keys, &c->s_w_vals};
+    for (auto* b : wu) b->release();
+    DevBuf<int32_t>* wi[] = {&c->w_cnt, &c->w_wkey, &c->w_D, &c->w_L, &c->w_Lcnt, &c->w_rel, &c->s_w_wkey};
+    for (auto* b : wi) b->release();
+    c->w_L2.release();
+    c->w_off.release();
+    c->w_rfl.release();
     c->r_bound.release();
     c->r_idx.release();
     c->r_cnt.release();
@@ -765,6 +911,8 @@ int owgs_update_cluster(owgs_ctx* c, int32_t new_size) {
     (void)hipSetDevice(c->cfg.device);
     const int32_t actual = new_size > 1 ? new_size : 1;
     if (c->cluster == actual) return OWGS_OK;
+    int rw = w_rebuild(c);  // in-flight concurrent activations of the discarded entries become watched pairs
+    if (rw) return rw;
     c->cluster = actual;
     const int32_t n = (int32_t)c->ids.size();
     HIPCHK(c, c->d_permits.reserve((size_t)n));
@@ -899,6 +1047,7 @@ int owgs_publish_batch(owgs_ctx* c, int32_t n, const int32_t* action, const uint
     A.out_flags = c->d_flags.p;
     int rc = run_prepass(c, A, 1, c->d_off.p, c->d_a.p, n, c->stream);
     if (!rc) rc = run_engine(c, A, c->stream);
+    if (!rc) rc = w_update(c, n, c->d_a.p, c->d_out.p, c->d_flags.p, c->stream);
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(out_invoker, c->d_out.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(out_flags, c->d_flags.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
@@ -966,12 +1115,19 @@ int owgs_release_batch(owgs_ctx* c, int32_t n, const int32_t* invoker, const int
     R.flags = c->d_rflags.p;
     R.err = c->d_err.p;
     int rs = release_scratch(c, R, n);
+    if (!rs && c->w_cap > 0) {  // room for the empty entries releases meet
+        rs = ensure_ovf(c, n, c->stream);
+        c->ovf_used_ub += n;
+    }
     if (rs) return rs;
+    R.ovf = ovf_args(c);
+    R.w = watch_args(c);
     HIPCHK(c, owgs_launch_release_seq(&R, c->stream));
     if (out_flags)
         HIPCHK(c, hipMemcpyAsync(out_flags, c->d_rflags.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    return check_err_word(c);
+    rs = w_refresh(c, c->stream);
+    return rs ? rs : check_err_word(c);
 }
 
 int owgs_schedule_walks(owgs_ctx* c, int32_t n, const uint8_t* pool, const int32_t* index, const int32_t* step,
@@ -1013,6 +1169,7 @@ int owgs_schedule_walks(owgs_ctx* c, int32_t n, const uint8_t* pool, const int32
     A.out_flags = c->d_flags.p;
     int rc = run_prepass(c, A, 1, c->d_off.p, nullptr, n, c->stream);
     if (!rc) rc = run_engine(c, A, c->stream);
+    if (!rc) rc = w_update(c, n, nullptr, c->d_out.p, c->d_flags.p, c->stream);
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(out_invoker, c->d_out.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(out_flags, c->d_flags.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
@@ -1023,6 +1180,8 @@ int owgs_schedule_walks(owgs_ctx* c, int32_t n, const uint8_t* pool, const int32
 int owgs_set_slots(owgs_ctx* c, int32_t n, const int32_t* permits) {
     if (!c || n < 0 || (n > 0 && !permits)) return OWGS_EINVAL;
     (void)hipSetDevice(c->cfg.device);
+    int rw = w_rebuild(c);
+    if (rw) return rw;
     HIPCHK(c, upload(c->d_permits, permits, (size_t)n, c->stream));
     c->n_slots = n;
     int rc = reset_ctab(c);
@@ -1069,7 +1228,7 @@ int owgs_read_concurrent(owgs_ctx* c, int32_t invoker, int32_t key, int32_t* per
     di.release();
     dk.release();
     dv.release();
-    if (v.y <= 0) return 0;  // absent (NestedSemaphore.concurrentState has no entry)
+    if (v.x < 0) return 0;  // absent (NestedSemaphore.concurrentState has no entry); present entries may count <= 0
     if (permits) *permits = v.x;
     if (op_count) *op_count = v.y;
     return 1;
@@ -1120,11 +1279,84 @@ static int replay_begin(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, 
                         uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, uint8_t* rel_flags,
                         hipStream_t hs, OwgsEngineArgs& A, bool launch);
 
+// Replay in watch mode (watched pairs exist): batch by batch, so that the Z marks of a batch's publishes are in place
+// before the next batch's releases -- releases through the ordered release kernels, publishes through one engine
+// launch per batch, then the watch update.  Reads the batch offsets back once (synchronous).
+static int replay_watch(owgs_ctx* c, int32_t nb, const int64_t* acq_off, const int32_t* act, int64_t n_act,
+                        const int64_t* rel_off, const int64_t* rel_aid, int64_t n_rel, uint64_t seq_base,
+                        int32_t* out_inv, uint8_t* out_flags, uint8_t* rel_flags, hipStream_t hs) {
+    (void)n_act;
+    (void)n_rel;
+    std::vector<int64_t> ao((size_t)nb + 1), ro((size_t)nb + 1, 0);
+    HIPCHK(c, hipMemcpyAsync(ao.data(), acq_off, ao.size() * 8, hipMemcpyDeviceToHost, hs));
+    if (rel_off) HIPCHK(c, hipMemcpyAsync(ro.data(), rel_off, ro.size() * 8, hipMemcpyDeviceToHost, hs));
+    HIPCHK(c, hipStreamSynchronize(hs));
+    std::vector<int64_t> offs((size_t)2 * nb);
+    int64_t max_r = 1;
+    for (int32_t b = 0; b < nb; ++b) {
+        offs[2 * b] = 0;
+        offs[2 * b + 1] = ao[b + 1] - ao[b];
+        max_r = std::max(max_r, ro[b + 1] - ro[b]);
+    }
+    HIPCHK(c, upload(c->w_off, offs.data(), offs.size(), hs));
+    HIPCHK(c, c->w_rel.reserve((size_t)(4 * max_r)));
+    if (!rel_flags) HIPCHK(c, c->w_rfl.reserve((size_t)max_r));
+    for (int32_t b = 0; b < nb; ++b) {
+        const int64_t nr = ro[b + 1] - ro[b], na = ao[b + 1] - ao[b];
+        if (nr > 0) {  // releaseInvoker of the batch's completions (SCPB:327-331), in stream order
+            int32_t* q = c->w_rel.p;
+            HIPCHK(c, owgs_launch_w_relgather(rel_aid + ro[b], (int32_t)nr, out_inv, act, c->d_act_mem.p,
+                                              c->d_act_maxc.p, c->d_act_slot.p, q, q + max_r, q + 2 * max_r,
+                                              q + 3 * max_r, hs));
+            OwgsReleaseArgs R{};
+            R.permits = c->d_permits.p;
+            R.n_slots = c->n_slots;
+            R.ct_keys = c->d_ct_keys.p;
+            R.ct_vals = c->d_ct_vals.p;
+            R.n = (int32_t)nr;
+            R.inv = q;
+            R.mem = q + max_r;
+            R.maxc = q + 2 * max_r;
+            R.slot = q + 3 * max_r;
+            R.flags = rel_flags ? rel_flags + ro[b] : c->w_rfl.p;
+            R.err = c->d_err.p;
+            int rs = release_scratch(c, R, (int32_t)nr);
+            if (!rs) rs = ensure_ovf(c, nr, hs);
+            if (rs) return rs;
+            c->ovf_used_ub += nr;
+            R.ovf = ovf_args(c);
+            R.w = watch_args(c);
+            HIPCHK(c, owgs_launch_release_seq(&R, hs));
+        }
+        if (na > 0) {  // the batch's publishes (SCPB:257-290), then the watch marks of their walks
+            OwgsEngineArgs A;
+            base_args(c, A);
+            A.seq_base = seq_base + (uint64_t)ao[b];
+            A.out_inv = out_inv + ao[b];
+            A.out_flags = out_flags + ao[b];
+            int rc = run_prepass(c, A, 1, c->w_off.p + 2 * b, act + ao[b], na, hs);
+            if (!rc) rc = run_engine(c, A, hs);
+            if (!rc) rc = w_update(c, (int32_t)na, act + ao[b], out_inv + ao[b], out_flags + ao[b], hs);
+            if (rc) return rc;
+        }
+    }
+    return w_refresh(c, hs);
+}
+
 int owgs_replay_device(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const int32_t* act,
                        int64_t n_activations, const int64_t* rel_off, const int64_t* rel_aid, int64_t n_releases,
                        uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, uint8_t* rel_flags, void* stream) {
     if (!c) return OWGS_EINVAL;
     hipStream_t hs = stream ? (hipStream_t)stream : c->stream;
+    if (c->w_cap > 0 && n_batches > 0) {
+        if (!acq_off || !act || !out_invoker || !out_flags || n_activations < 0 || n_releases < 0 ||
+            (n_releases > 0 && (!rel_off || !rel_aid)))
+            return OWGS_EINVAL;
+        if (c->a_mem.empty()) return c->fail(OWGS_ENOENT, "no actions registered");
+        (void)hipSetDevice(c->cfg.device);
+        return replay_watch(c, n_batches, acq_off, act, n_activations, rel_off, rel_aid, n_releases, seq_base,
+                            out_invoker, out_flags, rel_flags, hs);
+    }
     OwgsEngineArgs A;
     int rc = replay_begin(c, n_batches, acq_off, act, n_activations, rel_off, rel_aid, n_releases, seq_base,
                           out_invoker, out_flags, rel_flags, hs, A, true);
@@ -1143,6 +1375,17 @@ int owgs_replay_device_multi(owgs_ctx** cs, int32_t k, const owgs_replay_io* io,
         if (io[i].n_batches <= 0) return cs[i]->fail(OWGS_EINVAL, "multi-shard replay needs batches in every shard");
     }
     hipStream_t hs = stream ? (hipStream_t)stream : cs[0]->stream;
+    for (int32_t i = 0; i < k; ++i)
+        if (cs[i]->w_cap > 0) {  // a shard in watch mode replays batch by batch: every shard on its own
+            for (int32_t j = 0; j < k; ++j) {
+                const owgs_replay_io& x = io[j];
+                int rc = owgs_replay_device(cs[j], x.n_batches, x.acq_off, x.act, x.n_activations, x.rel_off,
+                                            x.rel_aid, x.n_releases, x.seq_base, x.out_invoker, x.out_flags,
+                                            x.rel_flags, hs);
+                if (rc) return rc;
+            }
+            return OWGS_OK;
+        }
     std::vector<OwgsEngineArgs> A((size_t)k);
     for (int32_t i = 0; i < k; ++i) {
         const owgs_replay_io& x = io[i];
@@ -1287,6 +1530,16 @@ int owgs_snapshot(owgs_ctx* c) {
             c->s_ovf_cap = c->ovf_cap;
         }
     }
+    c->s_w_cap = c->w_cap;  // watched pairs
+    c->s_w_live = c->w_live;
+    if (c->w_cap > 0) {
+        HIPCHK(c, c->s_w_keys.reserve((size_t)c->w_cap));
+        HIPCHK(c, c->s_w_vals.reserve((size_t)c->w_cap));
+        HIPCHK(c, c->s_w_wkey.reserve((size_t)OWGS_MAX_SLOTKEYS + 1));
+        HIPCHK(c, hipMemcpy(c->s_w_keys.p, c->w_keys.p, (size_t)c->w_cap * 4, hipMemcpyDeviceToDevice));
+        HIPCHK(c, hipMemcpy(c->s_w_vals.p, c->w_vals.p, (size_t)c->w_cap * 4, hipMemcpyDeviceToDevice));
+        HIPCHK(c, hipMemcpy(c->s_w_wkey.p, c->w_wkey.p, ((size_t)OWGS_MAX_SLOTKEYS + 1) * 4, hipMemcpyDeviceToDevice));
+    }
     c->has_snap = true;
     c->snap_slots = c->n_slots;
     return OWGS_OK;
@@ -1312,6 +1565,24 @@ int owgs_restore(owgs_ctx* c, void* stream) {
         }
     }
     c->ovf_used_ub = c->s_ovf_cnt;
+    if (c->w_cap != c->s_w_cap) {  // watched pairs as captured
+        w_drop(c);
+        if (c->s_w_cap > 0) {
+            HIPCHK(c, c->w_keys.reserve((size_t)c->s_w_cap));
+            HIPCHK(c, c->w_vals.reserve((size_t)c->s_w_cap));
+            HIPCHK(c, c->w_wkey.reserve((size_t)OWGS_MAX_SLOTKEYS + 1));
+            HIPCHK(c, c->w_cnt.reserve(1));
+        }
+    }
+    if (c->s_w_cap > 0) {
+        HIPCHK(c, hipMemcpyAsync(c->w_keys.p, c->s_w_keys.p, (size_t)c->s_w_cap * 4, hipMemcpyDeviceToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->w_vals.p, c->s_w_vals.p, (size_t)c->s_w_cap * 4, hipMemcpyDeviceToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->w_wkey.p, c->s_w_wkey.p, ((size_t)OWGS_MAX_SLOTKEYS + 1) * 4,
+                                 hipMemcpyDeviceToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->w_cnt.p, &c->s_w_live, sizeof(int32_t), hipMemcpyHostToDevice, s));
+        c->w_cap = c->s_w_cap;
+        c->w_live = c->s_w_live;
+    }
     return OWGS_OK;
 }
 
@@ -1511,14 +1782,21 @@ static int ack_complete(owgs_ctx* c, int32_t n, uint8_t* d_kind, int32_t* d_tick
     R.flags = c->d_rflags.p;
     R.err = c->d_err.p;
     int rs = release_scratch(c, R, n);
+    if (!rs && c->w_cap > 0) {
+        rs = ensure_ovf(c, n, st);
+        c->ovf_used_ub += n;
+    }
     if (rs) return rs;
+    R.ovf = ovf_args(c);
+    R.w = watch_args(c);
     HIPCHK(c, owgs_launch_release_seq(&R, st));
     HIPCHK(c, owgs_launch_ack_flags(n, c->k_info.p, c->d_rflags.p, d_kind, d_flags, st));
     unsigned long long cnt[2];
     HIPCHK(c, hipMemcpyAsync(cnt, c->k_cnt.p, 16, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
     c->t_live -= (long long)cnt[1];
-    return check_err_word(c);
+    rs = w_refresh(c, st);
+    return rs ? rs : check_err_word(c);
 }
 
 int owgs_process_acks_device(owgs_ctx* c, int32_t n, const uint8_t* bytes, const int64_t* off, uint8_t* out_kind,

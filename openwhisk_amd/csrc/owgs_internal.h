@@ -81,7 +81,7 @@
 #define OWGS_MAX_SLOTS_CT 32767        // invoker ids representable in the key
 #define OWGS_MAX_SLOTKEYS 131070       // fqn@version keys representable in the key (131071 would alias the tombstone)
 #define OWGS_MAX_CONC 4095             // maxConcurrent representable (c < maxConcurrent)
-#define OWGS_MAX_OPS 1048575
+#define OWGS_MAX_OPS 524287          // operationCount is a signed 20-bit field (watched pairs can count below 0)
 #define OWGS_MAX_MEM_MB 131071
 
 #define OWGS_NONE_V (-1)
@@ -132,6 +132,18 @@ struct OwgsOvf {
     int32_t* touched;    // [cap] engine release phase: overflow entries released in the current batch
     int32_t* n_touched;  // [1]
 };
+
+// Watched (invoker, fqn) pairs after a slot-state reset (owgs_watch.hip): d[p] = in-flight
+// activations of p minus the operationCount of p's entry; W = {p : d[p] > 0}.  Z[p] = the reference holds the empty
+// entry a failed concurrent try creates (NestedSemaphore.scala:61-62) while the engine's table has none.
+struct OwgsWatch {
+    uint32_t* keys;   // [cap] ct_key(invoker, slot); 0 empty, OWGS_CT_TOMB deleted
+    uint32_t* vals;   // [cap] d | Z << 31
+    int32_t cap;      // 0: no watched pairs (every kernel skips the watch paths)
+    int32_t* cnt;     // [1] live entries
+    int32_t* wkey;    // [OWGS_MAX_SLOTKEYS + 1] live entries per fqn@version key
+};
+#define OWGS_W_Z 0x80000000u
 
 struct OwgsEngineArgs {
     int32_t* permits;
@@ -260,6 +272,36 @@ struct OwgsReleaseArgs {
     int32_t* cval_s;     // [n]
     int32_t* cbeg;       // [OWGS_CTC]
     int32_t* cend;       // [OWGS_CTC]
+    OwgsWatch w;         // watched pairs (w.cap == 0: none); their releases take the ordered kernel
+};
+
+// watch kernels (owgs_watch.hip)
+struct OwgsWRebuildArgs {   // at a reset: the new W from the table's entries and the old W
+    const uint32_t* ct_keys;
+    const uint32_t* ct_vals;
+    OwgsOvf ovf;
+    OwgsWatch old_w;
+    OwgsWatch new_w;
+};
+struct OwgsWUpdateArgs {    // after a publish run: Z of the watched pairs that are absent from the table
+    int32_t n;              // decisions
+    const int32_t* act;     // registered actions (or null: explicit walks in xmeta / xslot)
+    const uint2* act_meta;
+    const int32_t* act_slot;
+    const uint2* xmeta;
+    const int32_t* xslot;
+    const int32_t* out_inv;
+    const uint8_t* out_flags;
+    int32_t pool_mode, n_ids, nm, nb;
+    const uint32_t* usable;     // identity pools
+    const int32_t* pool_words;  // [nm + nb]
+    const uint32_t* ct_keys;    // HBM image of the primary table (written back by the engine)
+    OwgsOvf ovf;
+    OwgsWatch w;
+    int32_t* D;             // [n_actions] deepest failed step + 1 per action in this run (zero between runs)
+    int32_t* L;             // [n] actions listed in D
+    uint4* L2;              // [n] {meta.x, slot, depth, 0} per listed walk
+    int32_t* Lcnt;          // [2] listed actions, listed walks
 };
 
 struct OwgsLookupArgs {

@@ -33,6 +33,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "owgs_internal.h"
+#include "owgs_table.h"
 
 typedef unsigned long long u64;
 
@@ -235,53 +236,6 @@ __device__ __forceinline__ int wave_max(int v) {
     return __builtin_amdgcn_readlane(v, 63);
 }
 
-__device__ __forceinline__ uint32_t ct_hash(uint32_t k) {
-    k ^= k >> 16;
-    k *= 0x7feb352dU;
-    k ^= k >> 15;
-    k *= 0x846ca68bU;
-    k ^= k >> 16;
-    return k;
-}
-__device__ __forceinline__ uint32_t ct_key(int inv, int slot) {
-    return (uint32_t)(inv + 1) | ((uint32_t)slot << OWGS_CT_SLOT_SHIFT);
-}
-// Concurrency table (LDS or HBM image): linear probing from a 4-entry-aligned home, so the engine reads a key's
-// first 4 candidate entries with two ds_read_b128 (bucketized linear probing).  Deleted entries are skipped, an empty
-// entry ends the chain.
-#define CT_BLK 4
-__device__ __forceinline__ uint32_t ct_home(uint32_t key) {
-    return (ct_hash(key) & (OWGS_CTC / CT_BLK - 1)) * CT_BLK;
-}
-__device__ __forceinline__ int ct_find(const uint32_t* ctk, uint32_t key) {
-    uint32_t h = ct_home(key);
-    for (int p = 0; p < OWGS_CTC; ++p) {
-        const uint32_t k = ctk[h];
-        if (k == key) return (int)h;
-        if (k == 0) return -1;
-        h = (h + 1) & (OWGS_CTC - 1);
-    }
-    return -1;
-}
-// insert a key known to be absent: claim the first empty or deleted entry of its chain (concurrent inserters of
-// different keys race by CAS)
-__device__ __forceinline__ int ct_insert(uint32_t* ctk, uint32_t key, int* fresh) {
-    uint32_t h = ct_home(key);
-    for (int p = 0; p < OWGS_CTC;) {
-        const uint32_t k = ctk[h];
-        if (k == 0 || k == OWGS_CT_TOMB) {
-            if (atomicCAS(&ctk[h], k, key) == k) {
-                *fresh = k == 0;
-                return (int)h;
-            }
-            continue;  // lost the race: re-read this entry
-        }
-        h = (h + 1) & (OWGS_CTC - 1);
-        ++p;
-    }
-    return -1;
-}
-
 // interleaved {key, value} table (engine LDS).  One aligned block of 4 entries: 1 = key found (*val, *idx),
 // 0 = an empty entry ends the chain, 2 = the chain continues in the next block.
 __device__ __forceinline__ int ct_block(uint4 e01, uint4 e23, uint32_t key, uint32_t h, uint32_t* val, int* idx) {
@@ -361,55 +315,6 @@ __device__ __forceinline__ int ct_insertv(uint2* ct, uint32_t key, int* fresh) {
             continue;  // lost the race: re-read this entry
         }
         h = (h + 1) & (OWGS_CTC - 1);
-        ++p;
-    }
-    return -1;
-}
-
-// ------------------------------------------------------------------------------------------------ overflow table
-__device__ __forceinline__ uint2 ovf_ld(const uint2* t, int i) {
-    const u64 v = __hip_atomic_load((const u64*)&t[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
-}
-__device__ __forceinline__ void ovf_st(uint2* t, int i, uint32_t k, uint32_t v) {
-    __hip_atomic_store((u64*)&t[i], (u64)k | ((u64)v << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void ovf_st_val(uint2* t, int i, uint32_t v) {
-    __hip_atomic_store(&t[i].y, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// index of key in the overflow (or -1), *val its value (0 if absent); linear probing from its hash, an empty entry
-// ends the chain
-__device__ __forceinline__ int ovf_find(const OwgsOvf& O, uint32_t key, uint32_t* val) {
-    *val = 0u;
-    if (O.cap <= 0) return -1;
-    const uint32_t m = (uint32_t)O.cap - 1u;
-    uint32_t h = ct_hash(key) & m;
-    for (int p = 0; p < O.cap; ++p) {
-        const uint2 e = ovf_ld(O.t, (int)h);
-        if (e.x == key) {
-            *val = e.y;
-            return (int)h;
-        }
-        if (e.x == 0u) return -1;
-        h = (h + 1u) & m;
-    }
-    return -1;
-}
-// insert a key absent from both tables into the first empty or deleted entry of its chain (CAS on the key word)
-__device__ __forceinline__ int ovf_insert(const OwgsOvf& O, uint32_t key, uint32_t val) {
-    if (O.cap <= 0) return -1;
-    const uint32_t m = (uint32_t)O.cap - 1u;
-    uint32_t h = ct_hash(key) & m;
-    for (int p = 0; p < O.cap;) {
-        const uint32_t k = ovf_ld(O.t, (int)h).x;
-        if (k == 0u || k == OWGS_CT_TOMB) {
-            if (atomicCAS(&O.t[h].x, k, key) == k) {
-                ovf_st_val(O.t, (int)h, val);
-                return (int)h;
-            }
-            continue;  // lost the entry: re-read it
-        }
-        h = (h + 1u) & m;
         ++p;
     }
     return -1;
@@ -598,8 +503,8 @@ __global__ __launch_bounds__(256) void owgs_lookup_kernel(OwgsLookupArgs a) {
     const uint32_t key = ct_key(a.inv[i], a.slot[i]);
     const int ix = ct_find(a.ct_keys, key);
     uint32_t v = ix >= 0 ? a.ct_vals[ix] : 0u;
-    if (ix < 0 && a.ovf.cap > 0 && *a.ovf.cnt > 0) ovf_find(a.ovf, key, &v);
-    a.out[i] = make_int2((int)(v & OWGS_CT_C_MASK), (int)(v >> OWGS_CT_C_BITS));
+    const bool found = ix >= 0 || (a.ovf.cap > 0 && *a.ovf.cnt > 0 && ovf_find(a.ovf, key, &v) >= 0);
+    a.out[i] = found ? make_int2((int)(v & OWGS_CT_C_MASK), ct_ops(v)) : make_int2(-1, 0);  // x = -1: absent
 }
 
 // home/step selection (SCPB:266-268) -> packed action meta
@@ -1334,8 +1239,8 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         }
                         uint32_t v;
                         const int ix = ct_find2(ct, A.ovf, rel_ovf, ct_key(inv, slot), &v);
-                        const int c0 = (int)(v & OWGS_CT_C_MASK), ops0 = (int)(v >> OWGS_CT_C_BITS);
-                        if (ix < 0 || ops0 == 0) {
+                        const int c0 = (int)(v & OWGS_CT_C_MASK), ops0 = ct_ops(v);
+                        if (ix < 0 || ops0 <= 0) {
                             err |= OWGS_ERR_BAD_STREAM;  // NoSuchElementException (NS:103)
                             continue;
                         }
@@ -1372,13 +1277,13 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                     rc[ix] = 0u;
                     const int R = (int)(v & 0xFFFu);
                     const uint32_t cv = ct[ix].y;
-                    const int c0 = (int)(cv & OWGS_CT_C_MASK), ops0 = (int)(cv >> OWGS_CT_C_BITS);
+                    const int c0 = (int)(cv & OWGS_CT_C_MASK), ops0 = ct_ops(cv);
                     const int j = min((int)(v >> 12), ops0);
                     const int ops1 = ops0 - j;
                     if (ops1 == 0) {
                         ct[ix] = make_uint2(OWGS_CT_TOMB, 0u);
                     } else {
-                        ct[ix].y = (uint32_t)((c0 + j) % R) | ((uint32_t)ops1 << OWGS_CT_C_BITS);
+                        ct[ix].y = ct_val((c0 + j) % R, ops1);
                     }
                 }
                 if (rel_ovf) {  // the overflow entries this batch released
@@ -1389,11 +1294,11 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         __hip_atomic_store(&A.ovf.rc[oj], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         const int R = (int)(v & 0xFFFu);
                         const uint32_t cv = ovf_ld(A.ovf.t, oj).y;
-                        const int c0 = (int)(cv & OWGS_CT_C_MASK), ops0 = (int)(cv >> OWGS_CT_C_BITS);
+                        const int c0 = (int)(cv & OWGS_CT_C_MASK), ops0 = ct_ops(cv);
                         const int j = min((int)(v >> 12), ops0);
                         const int ops1 = ops0 - j;
                         if (ops1 == 0) ovf_st(A.ovf.t, oj, OWGS_CT_TOMB, 0u);
-                        else ovf_st_val(A.ovf.t, oj, (uint32_t)((c0 + j) % R) | ((uint32_t)ops1 << OWGS_CT_C_BITS));
+                        else ovf_st_val(A.ovf.t, oj, ct_val((c0 + j) % R, ops1));
                     }
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 }
@@ -2709,7 +2614,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         const bool writer = kind == K_FALLBACK || nxt == (int)OWGS_REC_NONEXT || nxt >= l ||
                                             spt[nxt] != t;
                         if (writer) {
-                            const int c0v = (int)(cval & OWGS_CT_C_MASK), ops0 = (int)(cval >> OWGS_CT_C_BITS);
+                            const int c0v = (int)(cval & OWGS_CT_C_MASK), ops0 = ct_ops(cval);
                             const int jn = kind == K_FALLBACK ? 1 : ks + 1;
                             const int c1 = jn <= c0v ? c0v - jn
                                                      : (maxc - 1 - mod_fast(jn - c0v - 1, maxc,
@@ -2717,7 +2622,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             const int ops1 = ops0 + jn;
                             if (ops1 > OWGS_MAX_OPS) err |= OWGS_ERR_OPS;
                             int ix = cidx;
-                            const uint32_t key = ct_key(t, slot), nv = (uint32_t)c1 | ((uint32_t)ops1 << OWGS_CT_C_BITS);
+                            const uint32_t key = ct_key(t, slot), nv = ct_val(c1, ops1);
                             if (ix < 0) {  // absent when speculated (a kept lane's group may have created it since)
                                 uint32_t vv;
                                 if (ovf_on) {
@@ -2931,9 +2836,12 @@ __global__ __launch_bounds__(256) void owgs_rel_apply_kernel(OwgsReleaseArgs R) 
             atomicAdd(&R.permits[inv], R.mem[r]);
             if (R.flags) R.flags[r] = 0;
         } else {
-            const int ix = ct_find(R.ct_keys, ct_key(inv, R.slot[r]));
+            const uint32_t k = ct_key(inv, R.slot[r]);
+            const int ix = ct_find(R.ct_keys, k);
             const uint32_t v = ix >= 0 ? R.ct_vals[ix] : 0u;
-            if (ix < 0 || (int)(v >> OWGS_CT_C_BITS) <= 0) {
+            if ((R.w.cap > 0 && R.w.wkey[R.slot[r]] > 0 && w_find(R.w, k) >= 0) || (ix >= 0 && ct_ops(v) <= 0)) {
+                sel = 1;  // a watched pair, or an entry counting at or below zero: the ordered kernel, one by one
+            } else if (ix < 0) {
                 if (R.flags) R.flags[r] = OWGS_REL_NOSUCH_BIT;  // NoSuchElementException (NS:103)
             } else {
                 key = (uint32_t)ix;
@@ -2963,7 +2871,7 @@ __global__ __launch_bounds__(256) void owgs_rel_capply_kernel(OwgsReleaseArgs R)
     if (k >= OWGS_CTC) return;
     const int r = R.cval_s[p], q = p - R.cbeg[k];
     const uint32_t v = R.ct_vals[k];
-    const int c0 = (int)(v & OWGS_CT_C_MASK), o0 = (int)(v >> OWGS_CT_C_BITS), maxc = R.maxc[r];
+    const int c0 = (int)(v & OWGS_CT_C_MASK), o0 = ct_ops(v), maxc = R.maxc[r];
     uint8_t flag = 0;
     if (q < o0) {
         if ((c0 + q + 1) % maxc == 0) atomicAdd(&R.permits[R.inv[r]], R.mem[r]);
@@ -2977,31 +2885,38 @@ __global__ __launch_bounds__(256) void owgs_rel_cupdate_kernel(OwgsReleaseArgs R
     if (k >= OWGS_CTC || R.cend[k] <= R.cbeg[k]) return;
     const int r = R.cval_s[R.cbeg[k]];
     const uint32_t v = R.ct_vals[k];
-    const int c0 = (int)(v & OWGS_CT_C_MASK), o0 = (int)(v >> OWGS_CT_C_BITS), maxc = R.maxc[r];
+    const int c0 = (int)(v & OWGS_CT_C_MASK), o0 = ct_ops(v), maxc = R.maxc[r];
     const int j = min(R.cend[k] - R.cbeg[k], o0), o1 = o0 - j;
     if (o1 == 0) {
         R.ct_keys[k] = OWGS_CT_TOMB;
         R.ct_vals[k] = 0u;
     } else {
-        R.ct_vals[k] = (uint32_t)((c0 + j) % maxc) | ((uint32_t)o1 << OWGS_CT_C_BITS);
+        R.ct_vals[k] = ct_val((c0 + j) % maxc, o1);
     }
 }
 
 // the ordered part: the selected releases (all concurrent ones, or every in-range release when an overflow is
 // possible) in stream order, 64 at a time.  maxConcurrent == 1: FS.release (FS:117-120) with the overflow Error
 // leaving the state unchanged; concurrent: RS.release(1, true) applied rank+1 times inside each group of 64
-// (NS:98-113), NoSuchElementException when the entry is absent or already removed.
+// (NS:98-113), NoSuchElementException when the entry is absent or already removed.  Releases of watched pairs
+// (owgs_watch.hip) and of entries counting at or below zero run one at a time in stream order ("serial" lanes):
+// an absent watched pair with Z meets the reference's empty entry (NS:61-62), one without Z throws and lowers d.
 __global__ __launch_bounds__(64) void owgs_release_seq_kernel(OwgsReleaseArgs R) {
     __shared__ uint32_t ctk[OWGS_CTC], ctv[OWGS_CTC];
     const int lane = threadIdx.x;
+    int used = 0;
     for (int i = lane; i < OWGS_CTC; i += 64) {
         ctk[i] = R.ct_keys[i];
         ctv[i] = R.ct_vals[i];
+        used += ctk[i] != 0u;
     }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) used += __shfl_xor(used, d, 64);
     __syncthreads();
     const u64 lt_mask = lane == 0 ? 0ull : ((~0ull) >> (64 - lane));
     const int n_sel = *R.sel_cnt;
-    const bool ovf_on = R.ovf.cap > 0 && *R.ovf.cnt > 0;
+    bool ovf_on = R.ovf.cap > 0 && *R.ovf.cnt > 0;
+    int32_t err = 0;
     for (int k0 = 0; k0 < n_sel; k0 += 64) {
         const bool valid = k0 + lane < n_sel;
         const int r = valid ? R.sel_idx[k0 + lane] : 0;
@@ -3013,16 +2928,17 @@ __global__ __launch_bounds__(64) void owgs_release_seq_kernel(OwgsReleaseArgs R)
             slot = R.slot[r];
         }
         uint8_t flag = 0;
-        bool rel = false, conc = false;
+        bool rel = false, conc = false, ser = false;
         if (valid) {
             if (inv < 0) flag = OWGS_REL_NOENTRY_BIT;
             else if (inv >= R.n_slots) flag = 0;  // invokerSlots.lift -> no-op (SCPB:329)
             else if (maxc == 1) rel = true;
             else conc = true;
         }
-        int ix = -1, c0 = 0, o0 = 0;
+        int ix = -1, c0 = 0, o0 = 0, wj = -1;
         if (conc) {
             const uint32_t key = ct_key(inv, slot);
+            if (R.w.cap > 0 && R.w.wkey[slot] > 0) wj = w_find(R.w, key);
             ix = ct_find(ctk, key);
             uint32_t v = ix >= 0 ? ctv[ix] : 0u;
             if (ix < 0 && ovf_on) {  // overflow entries are indexed past the primary
@@ -3030,8 +2946,11 @@ __global__ __launch_bounds__(64) void owgs_release_seq_kernel(OwgsReleaseArgs R)
                 ix = oj >= 0 ? OWGS_CTC + oj : -1;
             }
             c0 = (int)(v & OWGS_CT_C_MASK);
-            o0 = (int)(v >> OWGS_CT_C_BITS);
-            if (ix < 0 || o0 <= 0) {
+            o0 = ct_ops(v);
+            if (wj >= 0 || (ix >= 0 && o0 <= 0)) {
+                ser = true;
+                conc = false;
+            } else if (ix < 0) {
                 conc = false;
                 flag = OWGS_REL_NOSUCH_BIT;
             }
@@ -3055,7 +2974,7 @@ __global__ __launch_bounds__(64) void owgs_release_seq_kernel(OwgsReleaseArgs R)
             if (rank == 0) {
                 const int j = min(gsz, o0);
                 const int o1 = o0 - j;
-                const uint32_t nv = (uint32_t)((c0 + j) % maxc) | ((uint32_t)o1 << OWGS_CT_C_BITS);
+                const uint32_t nv = ct_val((c0 + j) % maxc, o1);
                 if (ix >= OWGS_CTC) {
                     if (o1 == 0) ovf_st(R.ovf.t, ix - OWGS_CTC, OWGS_CT_TOMB, 0u);
                     else ovf_st_val(R.ovf.t, ix - OWGS_CTC, nv);
@@ -3067,17 +2986,94 @@ __global__ __launch_bounds__(64) void owgs_release_seq_kernel(OwgsReleaseArgs R)
                 }
             }
         }
-        // memory releases in stream order: lanes releasing to the same invoker are applied lane by lane so the
-        // overflow Error (FS:48-50) hits exactly the releases the reference rejects
-        u64 rm = __ballot(rel);
+        // memory releases (and the serial lanes) in stream order: lanes releasing to the same invoker are applied
+        // lane by lane so the overflow Error (FS:48-50) hits exactly the releases the reference rejects
+        u64 rm = __ballot(rel || ser);
         while (rm) {
             const int j = ffs64(rm);
             rm &= rm - 1;
-            if (lane == j) {
+            bool oins = false;
+            if (lane == j && ser) {
+                // one RS.release(1, true) (RS:99-108) against the current state of the entry (NS:98-113)
+                const uint32_t key = ct_key(inv, slot);
+                ix = ct_find(ctk, key);
+                uint32_t v = ix >= 0 ? ctv[ix] : 0u;
+                if (ix < 0 && ovf_on) {
+                    const int oj = ovf_find(R.ovf, key, &v);
+                    ix = oj >= 0 ? OWGS_CTC + oj : -1;
+                }
+                if (wj >= 0 && __hip_atomic_load(&R.w.keys[wj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != key)
+                    wj = -1;  // an earlier release of this group took the pair out of W
+                const uint32_t wv = wj >= 0 ? __hip_atomic_load(&R.w.vals[wj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+                bool apply = ix >= 0;
+                if (!apply && (wv & OWGS_W_Z)) {  // the reference's empty entry from a failed try takes it
+                    if (used < OWGS_CT_LDS_FILL || R.ovf.cap <= 0) {
+                        int fresh = 0;
+                        ix = ct_insert(ctk, key, &fresh);
+                        if (ix >= 0) {
+                            ctv[ix] = 0u;
+                            used += fresh;
+                        }
+                    }
+                    if (ix < 0 && R.ovf.cap > 0) {
+                        const int oj = ovf_insert(R.ovf, key, 0u);
+                        if (oj >= 0) {
+                            ix = OWGS_CTC + oj;
+                            atomicAdd(R.ovf.cnt, 1);
+                            oins = true;
+                        }
+                    }
+                    if (ix < 0) err |= OWGS_ERR_CTAB_FULL;
+                    v = 0u;
+                    apply = ix >= 0;
+                }
+                if (!apply) {
+                    flag = OWGS_REL_NOSUCH_BIT;  // NoSuchElementException (NS:103)
+                    if (wj >= 0) {  // one in-flight activation of the pair fewer whose release found nothing
+                        const int d = (int)(wv & ~OWGS_W_Z) - 1;
+                        if (d <= 0) {
+                            __hip_atomic_store(&R.w.vals[wj], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            __hip_atomic_store(&R.w.keys[wj], OWGS_CT_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            atomicSub(&R.w.wkey[slot], 1);
+                            atomicSub(R.w.cnt, 1);
+                        } else {
+                            __hip_atomic_store(&R.w.vals[wj], (uint32_t)d | (wv & OWGS_W_Z), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                    }
+                } else {
+                    const int cc = (int)(v & OWGS_CT_C_MASK), o1 = ct_ops(v) - 1;
+                    int c1 = cc + 1;
+                    const bool memrel = c1 % maxc == 0;  // RS:45-52
+                    if (memrel) c1 -= maxc;
+                    if (o1 < -OWGS_MAX_OPS) err |= OWGS_ERR_OPS;
+                    bool removed = o1 == 0;
+                    if (memrel) {
+                        const int old = R.permits[inv];
+                        if (old > 0x7FFFFFFF - mem) {
+                            flag |= OWGS_REL_OVERFLOW_BIT;
+                            removed = false;  // the Error is thrown before the map removal (NS:106-111)
+                        } else {
+                            R.permits[inv] = old + mem;
+                        }
+                    }
+                    const uint32_t nk = removed ? OWGS_CT_TOMB : key, nv = removed ? 0u : ct_val(c1, o1);
+                    if (ix >= OWGS_CTC) {
+                        ovf_st(R.ovf.t, ix - OWGS_CTC, nk, nv);
+                    } else {
+                        ctk[ix] = nk;
+                        ctv[ix] = nv;
+                    }
+                    if (removed && wj >= 0 && (wv & OWGS_W_Z))  // removal: the empty entry is gone too
+                        __hip_atomic_store(&R.w.vals[wj], wv & ~OWGS_W_Z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            } else if (lane == j) {
                 const int old = R.permits[inv];
                 if (old > 0x7FFFFFFF - mem) flag |= OWGS_REL_OVERFLOW_BIT;
                 else R.permits[inv] = old + mem;
             }
+            if (__ballot(oins)) ovf_on = true;
+            used = __builtin_amdgcn_readlane(used, j);
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         }
         if (valid && R.flags) R.flags[r] = flag;
@@ -3087,6 +3083,7 @@ __global__ __launch_bounds__(64) void owgs_release_seq_kernel(OwgsReleaseArgs R)
         R.ct_keys[i] = ctk[i];
         R.ct_vals[i] = ctv[i];
     }
+    if (err) atomicOr(R.err, err);
 }
 
 // ------------------------------------------------------------------------------------------------ self-test

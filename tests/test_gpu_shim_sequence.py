@@ -8,8 +8,10 @@ membership change (SCPB:230-248), and for every maximal run of releases followed
 owgs_register_actions call per new (invoking namespace, fqn@version), and a release names a handle of its fqn@version
 (the shim's byKey map).  Publishes that return no invoker create no ActivationEntry, so they are never released
 (CLB:278-279).  The oracle replays the same jobs one reference call at a time; decisions, overload flags, release
-flags and final permits must be bit-exact.  One variant changes the cluster size mid-stream (updateCluster throws the
-slot state away, SCPB:561-584), so the releases of earlier activations meet the new slots.
+flags and final permits must be bit-exact.  Variants change the cluster size mid-stream (updateCluster throws the
+slot state away, SCPB:561-584), so the releases of earlier activations meet the new slots -- and, for concurrent
+actions, the empty entries the reference's failed tries created (NestedSemaphore.scala:61-62): the comparison is
+with the literal oracle, and with the non-materialising one to show those cases occur.
 """
 import numpy as np
 import pytest
@@ -23,6 +25,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _jobs(w, rng, health_at, cluster_at):
+    cluster_at = cluster_at or {}
     """Queue contents in arrival order: ('inv', status) / ('clu', n) / ('rel', activation) / ('pub', activation)."""
     s = w.stream
     jobs = [("inv", w.inv_status.copy())]
@@ -32,24 +35,35 @@ def _jobs(w, rng, health_at, cluster_at):
             st[rng.choice(len(st), size=len(st) // 20, replace=False)] = UNHEALTHY
             st[rng.choice(len(st), size=len(st) // 50, replace=False)] = HEALTHY
             jobs.append(("inv", st))
-        if b == cluster_at:
-            jobs.append(("clu", 2))
+        if b in cluster_at:
+            jobs.append(("clu", cluster_at[b]))
         jobs += [("rel", int(a)) for a in s.rel_aid[s.rel_off[b]:s.rel_off[b + 1]]]
         jobs += [("pub", i) for i in range(int(s.acq_off[b]), int(s.acq_off[b + 1]))]
     return jobs
 
 
-@pytest.mark.parametrize("seed,cluster_at", [(1, None), (2, 5)])
-def test_shim_call_sequence_matches_oracle(seed, cluster_at):
+@pytest.mark.parametrize("seed,cluster_at,kw", [
+    (1, None, {}),
+    (2, {5: 2}, {}),
+    # several membership changes while concurrent activations are in flight, small nearly full pools (failed tries)
+    (3, {3: 2, 7: 3, 11: 1}, dict(conc_frac=0.5, conc_range=(2, 6), load=1.1)),
+    (4, {4: 4, 9: 2}, dict(conc_frac=0.3, shared_frac=0.4, load=1.2, n_invokers=300)),
+    (5, {2: 2, 6: 1, 10: 2}, dict(conc_frac=0.8, conc_range=(2, 3), n_invokers=200, load=1.3)),
+])
+def test_shim_call_sequence_matches_oracle(seed, cluster_at, kw):
     rng = np.random.default_rng(seed)
-    w = W.config("headline", n_activations=40_000, n_invokers=600, n_actions=1500, n_namespaces=150)
+    base = dict(n_activations=40_000, n_invokers=600, n_actions=1500, n_namespaces=150)
+    base.update(kw)
+    w = W.config("headline", **base)
     acts = w.actions
     g = GpuShardingContainerPoolBalancer(managed_fraction=w.managed_fraction, blackbox_fraction=w.blackbox_fraction,
                                          rng_seed=w.rng_seed)
-    # after updateCluster, releases of activations published before it are unmatched: a concurrent one then meets
-    # the reference's empty entries that failed tries created (NS:61-62), which the engine does not materialise
-    # (DESIGN.md section 3), so that variant compares with the oracle without them
-    o = O.BalancerState(w.managed_fraction, w.blackbox_fraction, rng_seed=w.rng_seed, zombies=cluster_at is None)
+    # the literal oracle: entries created on failed concurrent tries (NS:61-62); z = the oracle without them, to show
+    # which variants reach the releases that tell the two apart
+    o = O.BalancerState(w.managed_fraction, w.blackbox_fraction, rng_seed=w.rng_seed, zombies=True)
+    z = O.BalancerState(w.managed_fraction, w.blackbox_fraction, rng_seed=w.rng_seed, zombies=False)
+    z_rf = []
+    z_h = {}
     g_h, o_h, by_key, o_key = {}, {}, {}, {}
     n = len(w.stream.act)
     g_inv = np.full(n, -9, np.int32)
@@ -68,6 +82,7 @@ def test_shim_call_sequence_matches_oracle(seed, cluster_at):
             by_key.setdefault(x.key, h)
             o_h[k] = o.register_action(x.namespace, x.path, o_key.setdefault(x.key, len(o_key)), x.mem_mb,
                                        x.max_concurrent, x.blackbox)
+            z_h[k] = z.register_action(x.namespace, x.path, o_key[x.key], x.mem_mb, x.max_concurrent, x.blackbox)
         return g_h[k], o_h[k]
 
     jobs = _jobs(w, rng, health_at=3, cluster_at=cluster_at)
@@ -82,11 +97,13 @@ def test_shim_call_sequence_matches_oracle(seed, cluster_at):
             if kind == "inv":
                 g.update_invokers_arrays(w.inv_ids, w.inv_mem, x)
                 o.update_invokers(w.inv_ids, w.inv_mem, x)
+                z.update_invokers(w.inv_ids, w.inv_mem, x)
                 i += 1
                 continue
             if kind == "clu":
                 g.update_cluster(x)
                 o.update_cluster(x)
+                z.update_cluster(x)
                 i += 1
                 continue
             rels = []
@@ -102,9 +119,10 @@ def test_shim_call_sequence_matches_oracle(seed, cluster_at):
                 inv = g_inv[rels]
                 hk = [by_key[acts[w.stream.act[a]].key] for a in rels]
                 g_rf.append(g.release_invoker(inv, hk))
+                ok = [(acts[w.stream.act[a]].namespace, acts[w.stream.act[a]].key) for a in rels]
                 o_rf.append(np.array([{0: 0, O.THROW_NOSUCHELEMENT: 1, O.THROW_OVERFLOW: 2}.get(
-                    o.release(int(iv), o_h[(acts[w.stream.act[a]].namespace, acts[w.stream.act[a]].key)]), 8)
-                    for iv, a in zip(inv, rels)], np.uint8))
+                    o.release(int(iv), o_h[k]), 8) for iv, k in zip(inv, ok)], np.uint8))
+                z_rf.append(np.array([O._rel_bits(z.release(int(iv), z_h[k])) for iv, k in zip(inv, ok)], np.uint8))
             if pubs:
                 hs = [handle(int(w.stream.act[a])) for a in pubs]
                 sq = np.arange(seq, seq + len(pubs), dtype=np.uint64)
@@ -113,8 +131,11 @@ def test_shim_call_sequence_matches_oracle(seed, cluster_at):
                 g_inv[pubs], g_fl[pubs] = r, f
                 for k, (a, (_, oh)) in enumerate(zip(pubs, hs)):
                     o_inv[a], o_fl[a] = o.publish(oh, int(sq[k]))
+                    z.publish(z_h[(acts[w.stream.act[a]].namespace, acts[w.stream.act[a]].key)], int(sq[k]))
                     seq_of[a] = int(sq[k])
     assert np.array_equal(g_inv, o_inv), np.nonzero(g_inv != o_inv)[0][:5]
     assert np.array_equal(g_fl, o_fl)
     assert np.array_equal(np.concatenate(g_rf), np.concatenate(o_rf))
     assert np.array_equal(g.permits(), o.permits())
+    if cluster_at:  # these variants reach releases that only the reference's empty entries explain
+        assert not np.array_equal(np.concatenate(z_rf), np.concatenate(o_rf))
