@@ -629,10 +629,10 @@ static int w_update(owgs_ctx* c, int32_t n, const int32_t* d_act, const int32_t*
                     hipStream_t s) {
     if (c->w_cap <= 0 || n <= 0) return OWGS_OK;
     const size_t na = std::max<size_t>(c->a_mem.size(), 1);
-    const int32_t* before = c->w_D.p;
     const size_t had = c->w_D.n;
     HIPCHK(c, c->w_D.reserve(na));
-    if (c->w_D.p != before || had == 0) HIPCHK(c, hipMemsetAsync(c->w_D.p, 0, c->w_D.n * 4, s));  // zero between runs
+    // zero between runs; a grown buffer is new memory (hipMalloc may hand back the freed address: compare sizes)
+    if (c->w_D.n != had) HIPCHK(c, hipMemsetAsync(c->w_D.p, 0, c->w_D.n * 4, s));
     HIPCHK(c, c->w_L.reserve((size_t)n));
     HIPCHK(c, c->w_L2.reserve((size_t)n));
     HIPCHK(c, c->w_Lcnt.reserve(2));
