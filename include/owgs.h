@@ -114,6 +114,18 @@ int owgs_publish_batch(owgs_ctx* ctx, int32_t n, const int32_t* action, const ui
  * invoker < 0 means "no ActivationEntry" (flag OWGS_REL_NOENTRY, no state change). out_flags may be NULL. */
 int owgs_release_batch(owgs_ctx* ctx, int32_t n, const int32_t* invoker, const int32_t* action, uint8_t* out_flags);
 
+/* Replaces: one drained batch of the JVM shim's batching thread -- for each run r in order, releaseInvoker for the
+ * completions [rel_off[r], rel_off[r+1]) (SCPB:327-331 via CommonLoadBalancer.processCompletion, CLB:260-346; invoker
+ * and action handle of the ActivationEntry, invoker < 0 = no entry) and then the scheduling half of publish
+ * (SCPB:257-290) for the activations [pub_off[r], pub_off[r+1]).  Same results as alternating owgs_release_batch and
+ * owgs_publish_batch calls; one pinned copy in, one launch chain, one pinned copy out, one synchronisation.
+ * rel_off / pub_off have n_runs + 1 entries starting at 0; seq may be NULL (seq = seq_base + publish index);
+ * rel_flags may be NULL. */
+int owgs_process_batch(owgs_ctx* ctx, int32_t n_runs, const int32_t* rel_off, const int32_t* rel_invoker,
+                       const int32_t* rel_action, uint8_t* rel_flags, const int32_t* pub_off,
+                       const int32_t* pub_action, const uint64_t* seq, uint64_t seq_base, int32_t* out_invoker,
+                       uint8_t* out_flags);
+
 /* Replaces: ShardingContainerPoolBalancer.schedule(maxConcurrent, fqn, invokers, dispatched, slots, index, step)
  * (SCPB:398-436) called directly with an explicit walk, as the reference unit tests do (ShardingContainerPoolBalancer
  * Tests.scala:244-412).  pool = 0 managed / 1 blackbox pool of the context; key = slot-key id (see owgs_key_id). */

@@ -104,6 +104,7 @@ def lib() -> C.CDLL:
         "owgs_register_actions": (C.c_int, [P, i32, P, P, P, P, P, P, P, P, P, P, P]),
         "owgs_publish_batch": (C.c_int, [P, i32, P, P, u64, P, P]),
         "owgs_release_batch": (C.c_int, [P, i32, P, P, P]),
+        "owgs_process_batch": (C.c_int, [P, i32, P, P, P, P, P, P, P, u64, P, P]),
         "owgs_schedule_walks": (C.c_int, [P, i32, P, P, P, P, P, P, P, P, P]),
         "owgs_set_slots": (C.c_int, [P, i32, P]),
         "owgs_set_pool": (C.c_int, [P, i32, i32, P, P]),

@@ -355,6 +355,26 @@ class GpuShardingContainerPoolBalancer:
         self._chk(self._L.owgs_release_batch(self._h, len(a), _p(inv), _p(a), _p(fl)))
         return fl[: len(a)]
 
+    def process_batch(self, rel_off, rel_invokers, rel_actions, pub_off, pub_actions, seq=None, seq_base: int = 0):
+        """One drained batch of the shim's batching thread (owgs_process_batch): for each run r, releaseInvoker for
+        the completions [rel_off[r], rel_off[r+1]) then publish for [pub_off[r], pub_off[r+1]).  Returns
+        (invoker ids, overload flags, release flags)."""
+        ro = np.ascontiguousarray(rel_off, dtype=np.int32)
+        po = np.ascontiguousarray(pub_off, dtype=np.int32)
+        ri = np.ascontiguousarray(rel_invokers, dtype=np.int32)
+        ra = np.ascontiguousarray(rel_actions, dtype=np.int32)
+        pa = np.ascontiguousarray(pub_actions, dtype=np.int32)
+        nr, npub = int(ro[-1]), int(po[-1])
+        out = np.zeros(max(npub, 1), dtype=np.int32)
+        fl = np.zeros(max(npub, 1), dtype=np.uint8)
+        rf = np.zeros(max(nr, 1), dtype=np.uint8)
+        sq = None if seq is None else np.ascontiguousarray(seq, dtype=np.uint64)
+        z = np.zeros(1, np.int32)
+        self._chk(self._L.owgs_process_batch(self._h, len(ro) - 1, _p(ro), _p(ri if nr else z), _p(ra if nr else z),
+                                             _p(rf), _p(po), _p(pa if npub else z), None if sq is None else _p(sq),
+                                             seq_base, _p(out), _p(fl)))
+        return out[:npub], fl[:npub], rf[:nr]
+
     def schedule(self, max_concurrent, key, slots, index, step, pool=0, seq=None):
         """ShardingContainerPoolBalancer.schedule(maxConcurrent, fqn, invokers(pool), dispatched, slots, index, step)
         for arrays of calls (SCPB:398-436).  Scalars are broadcast.  Returns (ids, flags)."""

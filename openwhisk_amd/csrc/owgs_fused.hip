@@ -1,0 +1,95 @@
+// owgs_fused.hip -- owgs_process_batch: one drained batch of the shim's batching thread in one launch chain.
+//
+// The shim drains its queue into runs of completions followed by publishes (GpuShardingContainerPoolBalancer.scala
+// runBatch; CommonLoadBalancer.processCompletion -> releaseInvoker, SCPB:327-331, then publish, SCPB:257-290).
+// owgs_stage_releases_kernel turns each run's completions -- (invoker, action handle) pairs from the caller's
+// ActivationEntry -- into the engine's release records, so ONE engine launch replays the whole drained batch as a
+// stream of batches (releases of run r, then its publishes), exactly like a replay whose releases name activations
+// of earlier calls.  The records of a run are split by class (maxConcurrent == 1 and no-op records first, concurrent
+// ones after, stream order inside a class); rel_src maps a record back to the caller's release for its flags.
+#include <hip/hip_runtime.h>
+
+#include "owgs_internal.h"
+
+// one workgroup per run: class counts, then stable placement by ballot ranks
+__global__ __launch_bounds__(256) void owgs_stage_releases_kernel(OwgsStageArgs a) {
+    const int run = blockIdx.x;
+    const int64_t cb = a.rel_off[run], ce = a.rel_off[run + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ int t0[4], t1[4];
+    auto first_class = [&](int64_t i) {
+        const int inv = a.rel_inv[i];
+        return inv < 0 || inv >= a.n_slots || a.act_maxc[a.rel_act[i]] == 1;
+    };
+    int n0 = 0;
+    for (int64_t c = cb; c < ce; c += 256) {
+        const int64_t i = c + tid;
+        n0 += __syncthreads_count(i < ce && first_class(i));
+    }
+    const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    int base0 = 0, base1 = 0;
+    for (int64_t c = cb; c < ce; c += 256) {
+        const int64_t i = c + tid;
+        const bool valid = i < ce;
+        const bool f = valid && first_class(i);
+        const unsigned long long b0 = __ballot(f), b1 = __ballot(valid && !f);
+        if (lane == 0) {
+            t0[wave] = __popcll(b0);
+            t1[wave] = __popcll(b1);
+        }
+        __syncthreads();
+        int o0 = base0, o1 = base1, s0 = 0, s1 = 0;
+        for (int w = 0; w < 4; ++w) {
+            if (w < wave) {
+                o0 += t0[w];
+                o1 += t1[w];
+            }
+            s0 += t0[w];
+            s1 += t1[w];
+        }
+        if (valid) {
+            const int inv = a.rel_inv[i], act = a.rel_act[i];
+            const bool in = inv >= 0 && inv < a.n_slots;
+            const int64_t pos = f ? cb + o0 + __popcll(b0 & lt) : cb + n0 + o1 + __popcll(b1 & lt);
+            const uint32_t inv15 = in ? (uint32_t)inv : OWGS_RR_NOINV;  // no-op: invokerSlots.lift (SCPB:329)
+            a.rel_rec[pos] = make_uint2(inv15 | ((uint32_t)a.act_mem[act] << 15),
+                                        (uint32_t)a.act_slot[act] | ((uint32_t)a.act_maxc[act] << 17));
+            a.rel_src[pos] = (int32_t)(i - a.rel_off[0]);
+            a.rel_flags[i - a.rel_off[0]] = inv < 0 ? OWGS_REL_NOENTRY_BIT : 0;  // no ActivationEntry (CLB:278-279)
+        }
+        base0 += s0;
+        base1 += s1;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        a.relcnt[2 * run] = n0;
+        a.relcnt[2 * run + 1] = (int32_t)(ce - cb) - n0;
+    }
+}
+
+// (invoker, action handle) -> the release kernels' (invoker, memory, maxConcurrent, slot key) arrays
+__global__ __launch_bounds__(256) void owgs_relmeta_kernel(int32_t n, const int32_t* act, const int32_t* act_mem,
+                                                           const int32_t* act_maxc, const int32_t* act_slot,
+                                                           int32_t* mem, int32_t* maxc, int32_t* slot) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int a = act[i];
+    mem[i] = act_mem[a];
+    maxc[i] = act_maxc[a];
+    slot[i] = act_slot[a];
+}
+
+extern "C" hipError_t owgs_launch_stage_releases(const OwgsStageArgs* a, hipStream_t s) {
+    if (a->n_runs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(owgs_stage_releases_kernel, dim3((unsigned)a->n_runs), dim3(256), 0, s, *a);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t owgs_launch_relmeta(int32_t n, const int32_t* act, const int32_t* act_mem,
+                                          const int32_t* act_maxc, const int32_t* act_slot, int32_t* mem,
+                                          int32_t* maxc, int32_t* slot, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(owgs_relmeta_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, act, act_mem,
+                       act_maxc, act_slot, mem, maxc, slot);
+    return hipGetLastError();
+}

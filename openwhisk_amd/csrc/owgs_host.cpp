@@ -74,6 +74,10 @@ extern "C" hipError_t owgs_launch_msg_plan(const OwgsMsgArgs* a, int32_t bits, v
 extern "C" hipError_t owgs_launch_msg_write(const OwgsMsgArgs* a, hipStream_t st);
 extern "C" size_t owgs_engine_lds_bytes(int n_slots, int pool_mode, int n_ids, int nm, int nb, int n_actions);
 extern "C" hipError_t owgs_launch_w_rebuild(const OwgsWRebuildArgs* a, hipStream_t s);
+extern "C" hipError_t owgs_launch_stage_releases(const OwgsStageArgs* a, hipStream_t s);
+extern "C" hipError_t owgs_launch_relmeta(int32_t n, const int32_t* act, const int32_t* act_mem,
+                                          const int32_t* act_maxc, const int32_t* act_slot, int32_t* mem,
+                                          int32_t* maxc, int32_t* slot, hipStream_t s);
 extern "C" hipError_t owgs_launch_w_update(const OwgsWUpdateArgs* a, hipStream_t s);
 extern "C" hipError_t owgs_launch_w_relgather(const int64_t* rel_aid, int32_t n, const int32_t* out_inv,
                                               const int32_t* act, const int32_t* act_mem, const int32_t* act_maxc,
@@ -219,6 +223,14 @@ struct owgs_ctx {
     DevBuf<int64_t> w_off;
     DevBuf<uint8_t> w_rfl;
     int32_t w_cap = 0, w_live = 0;
+    // owgs_process_batch: pinned staging (inputs, outputs) and their device copies
+    void* h_pin = nullptr;
+    size_t h_pin_bytes = 0;
+    void* h_pout = nullptr;
+    size_t h_pout_bytes = 0;
+    DevBuf<uint8_t> d_pin, d_pout;
+    DevBuf<int32_t> f_src, f_cnt;
+    DevBuf<uint2> f_rec;
     DevBuf<uint32_t> s_w_keys, s_w_vals;
     DevBuf<int32_t> s_w_wkey;
     int32_t s_w_cap = 0, s_w_live = 0;
@@ -815,6 +827,14 @@ void owgs_destroy(owgs_ctx* c) {
     c->w_L2.release();
     c->w_off.release();
     c->w_rfl.release();
+    if (c->h_pin) (void)hipHostFree(c->h_pin);
+    if (c->h_pout) (void)hipHostFree(c->h_pout);
+    c->h_pin = c->h_pout = nullptr;
+    c->d_pin.release();
+    c->d_pout.release();
+    c->f_src.release();
+    c->f_cnt.release();
+    c->f_rec.release();
     c->r_bound.release();
     c->r_idx.release();
     c->r_cnt.release();
@@ -1085,6 +1105,34 @@ static int release_scratch(owgs_ctx* c, OwgsReleaseArgs& R, int32_t n) {
     return OWGS_OK;
 }
 
+// The exact release path (owgs_launch_release_seq: parallel front end, ordered kernel for overflow risk, watched pairs
+// and entries counting at or below zero) for n releases already on the device.  Asynchronous on s.
+static int release_chain(owgs_ctx* c, int32_t n, const int32_t* inv, const int32_t* mem, const int32_t* maxc,
+                         const int32_t* slot, uint8_t* flags, hipStream_t s) {
+    OwgsReleaseArgs R{};
+    R.permits = c->d_permits.p;
+    R.n_slots = c->n_slots;
+    R.ct_keys = c->d_ct_keys.p;
+    R.ct_vals = c->d_ct_vals.p;
+    R.n = n;
+    R.inv = inv;
+    R.mem = mem;
+    R.maxc = maxc;
+    R.slot = slot;
+    R.flags = flags;
+    R.err = c->d_err.p;
+    int rs = release_scratch(c, R, n);
+    if (!rs && c->w_cap > 0) {  // room for the empty entries releases of watched pairs meet
+        rs = ensure_ovf(c, n, s);
+        c->ovf_used_ub += n;
+    }
+    if (rs) return rs;
+    R.ovf = ovf_args(c);
+    R.w = watch_args(c);
+    HIPCHK(c, owgs_launch_release_seq(&R, s));
+    return OWGS_OK;
+}
+
 int owgs_release_batch(owgs_ctx* c, int32_t n, const int32_t* invoker, const int32_t* action, uint8_t* out_flags) {
     if (!c || n < 0 || (n > 0 && (!invoker || !action))) return OWGS_EINVAL;
     if (n == 0) return OWGS_OK;
@@ -1101,28 +1149,8 @@ int owgs_release_batch(owgs_ctx* c, int32_t n, const int32_t* invoker, const int
     HIPCHK(c, upload(c->d_c, mc.data(), (size_t)n, c->stream));
     HIPCHK(c, upload(c->d_d, sl.data(), (size_t)n, c->stream));
     HIPCHK(c, c->d_rflags.reserve((size_t)n));
-    OwgsReleaseArgs R{};
-    R.permits = c->d_permits.p;
-    R.n_slots = c->n_slots;
-    R.ct_keys = c->d_ct_keys.p;
-    R.ct_vals = c->d_ct_vals.p;
-    R.ovf = ovf_args(c);
-    R.n = n;
-    R.inv = c->d_a.p;
-    R.mem = c->d_b.p;
-    R.maxc = c->d_c.p;
-    R.slot = c->d_d.p;
-    R.flags = c->d_rflags.p;
-    R.err = c->d_err.p;
-    int rs = release_scratch(c, R, n);
-    if (!rs && c->w_cap > 0) {  // room for the empty entries releases meet
-        rs = ensure_ovf(c, n, c->stream);
-        c->ovf_used_ub += n;
-    }
+    int rs = release_chain(c, n, c->d_a.p, c->d_b.p, c->d_c.p, c->d_d.p, c->d_rflags.p, c->stream);
     if (rs) return rs;
-    R.ovf = ovf_args(c);
-    R.w = watch_args(c);
-    HIPCHK(c, owgs_launch_release_seq(&R, c->stream));
     if (out_flags)
         HIPCHK(c, hipMemcpyAsync(out_flags, c->d_rflags.p, (size_t)n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1308,25 +1336,9 @@ static int replay_watch(owgs_ctx* c, int32_t nb, const int64_t* acq_off, const i
             HIPCHK(c, owgs_launch_w_relgather(rel_aid + ro[b], (int32_t)nr, out_inv, act, c->d_act_mem.p,
                                               c->d_act_maxc.p, c->d_act_slot.p, q, q + max_r, q + 2 * max_r,
                                               q + 3 * max_r, hs));
-            OwgsReleaseArgs R{};
-            R.permits = c->d_permits.p;
-            R.n_slots = c->n_slots;
-            R.ct_keys = c->d_ct_keys.p;
-            R.ct_vals = c->d_ct_vals.p;
-            R.n = (int32_t)nr;
-            R.inv = q;
-            R.mem = q + max_r;
-            R.maxc = q + 2 * max_r;
-            R.slot = q + 3 * max_r;
-            R.flags = rel_flags ? rel_flags + ro[b] : c->w_rfl.p;
-            R.err = c->d_err.p;
-            int rs = release_scratch(c, R, (int32_t)nr);
-            if (!rs) rs = ensure_ovf(c, nr, hs);
+            int rs = release_chain(c, (int32_t)nr, q, q + max_r, q + 2 * max_r, q + 3 * max_r,
+                                   rel_flags ? rel_flags + ro[b] : c->w_rfl.p, hs);
             if (rs) return rs;
-            c->ovf_used_ub += nr;
-            R.ovf = ovf_args(c);
-            R.w = watch_args(c);
-            HIPCHK(c, owgs_launch_release_seq(&R, hs));
         }
         if (na > 0) {  // the batch's publishes (SCPB:257-290), then the watch marks of their walks
             OwgsEngineArgs A;
@@ -1508,6 +1520,162 @@ int owgs_replay(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const in
         HIPCHK(c, hipMemcpyAsync(rel_flags, c->d_rflags.p, (size_t)n_rel, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return check_err_word(c);
+}
+
+// One drained batch of the shim's batching thread: runs of completions then publishes.  One pinned
+// H2D of every input, one launch chain (release staging, pre-pass, ONE engine launch over all runs), one pinned D2H
+// of every output, one synchronisation.  With watched pairs (owgs_watch.hip) the runs go through the exact release
+// kernels, one engine launch per run and the watch update instead -- still one copy each way and one sync.
+int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, const int32_t* rel_invoker,
+                       const int32_t* rel_action, uint8_t* rel_flags, const int32_t* pub_off,
+                       const int32_t* pub_action, const uint64_t* seq, uint64_t seq_base, int32_t* out_invoker,
+                       uint8_t* out_flags) {
+    if (!c || n_runs < 0 || (n_runs > 0 && (!rel_off || !pub_off))) return OWGS_EINVAL;
+    if (n_runs == 0) return OWGS_OK;
+    if (rel_off[0] != 0 || pub_off[0] != 0) return c->fail(OWGS_EINVAL, "offsets must start at 0");
+    for (int32_t r = 0; r < n_runs; ++r)
+        if (rel_off[r + 1] < rel_off[r] || pub_off[r + 1] < pub_off[r]) return c->fail(OWGS_EINVAL, "offsets");
+    const int32_t NR = rel_off[n_runs], NP = pub_off[n_runs];
+    if ((NR > 0 && (!rel_invoker || !rel_action)) || (NP > 0 && (!pub_action || !out_invoker || !out_flags)))
+        return OWGS_EINVAL;
+    if (n_runs >= 0x1FFFF) return c->fail(OWGS_ERANGE, "more than 131070 runs in one call");
+    if (!registered(c, NP, pub_action) || !registered(c, NR, rel_action)) return c->fail(OWGS_ENOENT, "unknown action");
+    (void)hipSetDevice(c->cfg.device);
+    hipStream_t s = c->stream;
+    // ---- pinned staging: i64 offsets (publishes, releases, per-run {0, n}) | publish actions | release invokers |
+    // release actions | seq
+    auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    const size_t o_acq = 0, o_rel = al(o_acq + 8 * (size_t)(n_runs + 1)), o_run = al(o_rel + 8 * (size_t)(n_runs + 1));
+    const size_t o_pa = al(o_run + 16 * (size_t)n_runs), o_ri = al(o_pa + 4 * (size_t)NP);
+    const size_t o_ra = al(o_ri + 4 * (size_t)NR), o_sq = al(o_ra + 4 * (size_t)NR);
+    const size_t in_bytes = al(o_sq + (seq ? 8 * (size_t)NP : 0));
+    const size_t q_inv = 0, q_fl = al(4 * (size_t)NP), q_rf = al(q_fl + (size_t)NP), q_err = al(q_rf + (size_t)NR);
+    const size_t out_bytes = q_err + 16;
+    if (c->h_pin_bytes < in_bytes) {
+        if (c->h_pin) (void)hipHostFree(c->h_pin);
+        c->h_pin = nullptr;
+        c->h_pin_bytes = 0;
+        HIPCHK(c, hipHostMalloc(&c->h_pin, in_bytes * 2, hipHostMallocDefault));
+        c->h_pin_bytes = in_bytes * 2;
+    }
+    if (c->h_pout_bytes < out_bytes) {
+        if (c->h_pout) (void)hipHostFree(c->h_pout);
+        c->h_pout = nullptr;
+        c->h_pout_bytes = 0;
+        HIPCHK(c, hipHostMalloc(&c->h_pout, out_bytes * 2, hipHostMallocDefault));
+        c->h_pout_bytes = out_bytes * 2;
+    }
+    HIPCHK(c, hipStreamSynchronize(s));  // the previous call's copies out of the pinned buffers are done
+    char* H = (char*)c->h_pin;
+    int64_t* h_acq = (int64_t*)(H + o_acq);
+    int64_t* h_rel = (int64_t*)(H + o_rel);
+    int64_t* h_run = (int64_t*)(H + o_run);
+    for (int32_t r = 0; r <= n_runs; ++r) {
+        h_acq[r] = pub_off[r];
+        h_rel[r] = rel_off[r];
+    }
+    for (int32_t r = 0; r < n_runs; ++r) {
+        h_run[2 * r] = 0;
+        h_run[2 * r + 1] = pub_off[r + 1] - pub_off[r];
+    }
+    if (NP) memcpy(H + o_pa, pub_action, 4 * (size_t)NP);
+    if (NR) {
+        memcpy(H + o_ri, rel_invoker, 4 * (size_t)NR);
+        memcpy(H + o_ra, rel_action, 4 * (size_t)NR);
+    }
+    if (seq && NP) memcpy(H + o_sq, seq, 8 * (size_t)NP);
+    HIPCHK(c, c->d_pin.reserve(in_bytes));
+    HIPCHK(c, hipMemcpyAsync(c->d_pin.p, H, in_bytes, hipMemcpyHostToDevice, s));
+    char* D = (char*)c->d_pin.p;
+    const int64_t* d_acq = (const int64_t*)(D + o_acq);
+    const int64_t* d_rel = (const int64_t*)(D + o_rel);
+    const int64_t* d_run = (const int64_t*)(D + o_run);
+    const int32_t* d_pa = (const int32_t*)(D + o_pa);
+    const int32_t* d_ri = (const int32_t*)(D + o_ri);
+    const int32_t* d_ra = (const int32_t*)(D + o_ra);
+    const u64* d_sq = seq ? (const u64*)(D + o_sq) : nullptr;
+    HIPCHK(c, c->d_pout.reserve(out_bytes));
+    char* DO = (char*)c->d_pout.p;
+    int32_t* d_out = (int32_t*)(DO + q_inv);
+    uint8_t* d_fl = (uint8_t*)(DO + q_fl);
+    uint8_t* d_rf = (uint8_t*)(DO + q_rf);
+    int rc = OWGS_OK;
+    if (c->w_cap > 0) {  // watched pairs: the exact release kernels per run, the watch update after each publish run
+        int32_t max_r = 1;
+        for (int32_t r = 0; r < n_runs; ++r) max_r = std::max(max_r, rel_off[r + 1] - rel_off[r]);
+        HIPCHK(c, c->w_rel.reserve((size_t)3 * max_r));
+        int32_t* q = c->w_rel.p;
+        for (int32_t r = 0; r < n_runs && !rc; ++r) {
+            const int32_t nr = rel_off[r + 1] - rel_off[r], np = pub_off[r + 1] - pub_off[r];
+            if (nr > 0) {
+                HIPCHK(c, owgs_launch_relmeta(nr, d_ra + rel_off[r], c->d_act_mem.p, c->d_act_maxc.p, c->d_act_slot.p,
+                                              q, q + max_r, q + 2 * max_r, s));
+                rc = release_chain(c, nr, d_ri + rel_off[r], q, q + max_r, q + 2 * max_r, d_rf + rel_off[r], s);
+            }
+            if (!rc && np > 0) {
+                OwgsEngineArgs A;
+                base_args(c, A);
+                A.seq_base = seq_base + (uint64_t)pub_off[r];
+                A.seq = d_sq ? d_sq + pub_off[r] : nullptr;
+                A.out_inv = d_out + pub_off[r];
+                A.out_flags = d_fl + pub_off[r];
+                rc = run_prepass(c, A, 1, d_run + 2 * r, d_pa + pub_off[r], np, s);
+                if (!rc) rc = run_engine(c, A, s);
+                if (!rc) rc = w_update(c, np, d_pa + pub_off[r], d_out + pub_off[r], d_fl + pub_off[r], s);
+            }
+        }
+    } else {  // every run in ONE engine launch: the releases as engine records (owgs_fused.hip)
+        HIPCHK(c, c->f_rec.reserve((size_t)NR + 2));
+        HIPCHK(c, c->f_src.reserve((size_t)NR + 1));
+        HIPCHK(c, c->f_cnt.reserve((size_t)2 * n_runs));
+        if (NR > 0) {
+            OwgsStageArgs g{};
+            g.n_runs = n_runs;
+            g.rel_off = d_rel;
+            g.rel_inv = d_ri;
+            g.rel_act = d_ra;
+            g.act_mem = c->d_act_mem.p;
+            g.act_maxc = c->d_act_maxc.p;
+            g.act_slot = c->d_act_slot.p;
+            g.n_slots = c->n_slots;
+            g.rel_rec = c->f_rec.p;
+            g.rel_src = c->f_src.p;
+            g.relcnt = c->f_cnt.p;
+            g.rel_flags = d_rf;
+            HIPCHK(c, owgs_launch_stage_releases(&g, s));
+        }
+        if (c->a_mem.empty()) return c->fail(OWGS_ENOENT, "no actions registered");
+        OwgsEngineArgs A;
+        base_args(c, A);
+        A.seq_base = seq_base;
+        A.seq = d_sq;
+        A.out_inv = d_out;
+        A.out_flags = d_fl;
+        rc = run_prepass(c, A, n_runs, d_acq, d_pa, NP, s);
+        if (!rc && NR > 0) {
+            A.rel_off = d_rel;
+            A.relcnt = c->f_cnt.p;
+            A.rel_rec = c->f_rec.p;
+            A.rel_src = c->f_src.p;
+            A.rel_flags = d_rf;
+        }
+        if (!rc) rc = run_engine(c, A, s);
+    }
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->d_pout.p + q_err, c->d_err.p, 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->h_pout, c->d_pout.p, out_bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    const char* HO = (const char*)c->h_pout;
+    if (NP) {
+        memcpy(out_invoker, HO + q_inv, 4 * (size_t)NP);
+        memcpy(out_flags, HO + q_fl, (size_t)NP);
+    }
+    if (NR && rel_flags) memcpy(rel_flags, HO + q_rf, (size_t)NR);
+    rc = w_refresh(c, s);
+    if (rc) return rc;
+    int32_t e = 0;
+    memcpy(&e, HO + q_err, 4);
+    return e ? check_err_word(c) : OWGS_OK;
 }
 
 int owgs_snapshot(owgs_ctx* c) {

@@ -173,6 +173,8 @@ struct OwgsEngineArgs {
     const int32_t* relpos;       // [n_act] relx (see above), or null: no releases
     const int32_t* relcnt;       // [2 * n_batches] per batch: maxConcurrent == 1 records, concurrent records
     uint2* rel_rec;              // [n_rel] release records, in rel_aid order (written when the activation is decided)
+    const int32_t* rel_src;      // explicit releases (owgs_process_batch): record position -> the caller's release
+                                 // index (flags go to rel_flags[rel_src[p]]); null for a stream's own releases
     unsigned long long seq_base;
     const unsigned long long* seq; // optional explicit seq per activation
     int32_t* out_inv;
@@ -273,6 +275,22 @@ struct OwgsReleaseArgs {
     int32_t* cbeg;       // [OWGS_CTC]
     int32_t* cend;       // [OWGS_CTC]
     OwgsWatch w;         // watched pairs (w.cap == 0: none); their releases take the ordered kernel
+};
+
+// owgs_process_batch: the caller's releases (invoker, action handle) of each run as engine release records
+struct OwgsStageArgs {
+    int32_t n_runs;
+    const int64_t* rel_off;     // [n_runs + 1]
+    const int32_t* rel_inv;
+    const int32_t* rel_act;
+    const int32_t* act_mem;
+    const int32_t* act_maxc;
+    const int32_t* act_slot;
+    int32_t n_slots;
+    uint2* rel_rec;             // out [n_rel]: per run maxConcurrent == 1 (and no-op) records first, concurrent after
+    int32_t* rel_src;           // out [n_rel]: record position -> release index
+    int32_t* relcnt;            // out [2 n_runs]: records of the first class, of the second
+    uint8_t* rel_flags;         // out [n_rel]: OWGS_REL_NOENTRY_BIT for invoker < 0, else 0 (the engine adds NoSuch)
 };
 
 // watch kernels (owgs_watch.hip)

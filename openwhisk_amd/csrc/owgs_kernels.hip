@@ -130,7 +130,7 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
 
 // LDS scalars
 #define SC_LMIN 0   // [2] first lane not known to fit (pass parity)
-#define SC_CFB 2    // [2] (unused: see SC_CFT)
+#define SC_IRR 2    // explicit releases (owgs_process_batch): an entry got more releases than its operationCount
 #define SC_U0 4     // upper bound of usable permits, managed pool
 #define SC_U1 5     // blackbox pool
 #define SC_USED 6   // non-empty concurrency-table entries (live + deleted)
@@ -1053,7 +1053,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     } else {
         for (int i = tid; i < nm + nb; i += OWGS_NT) pw[i] = (int16_t)A.pool_words[i];
     }
-    if (tid < SC_N) sc[tid] = (tid < 4 || tid >= SC_CFT) ? OWGS_WL : (tid < 6 ? (int)0x80000000 : 0);
+    if (tid < SC_N) sc[tid] = ((tid < 4 && tid != SC_IRR) || tid >= SC_CFT) ? OWGS_WL : (tid < 6 ? (int)0x80000000 : 0);
     lds_sync();
     {
         int used = 0;
@@ -1241,7 +1241,11 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         const int ix = ct_find2(ct, A.ovf, rel_ovf, ct_key(inv, slot), &v);
                         const int c0 = (int)(v & OWGS_CT_C_MASK), ops0 = ct_ops(v);
                         if (ix < 0 || ops0 <= 0) {
-                            err |= OWGS_ERR_BAD_STREAM;  // NoSuchElementException (NS:103)
+                            // NoSuchElementException (NS:103): a flag for the caller's explicit releases
+                            // (owgs_process_batch), a broken stream for the engine's own records
+                            if (A.rel_src) A.rel_flags[A.rel_src[2 * (p0 + (int64_t)(k >> 1) * OWGS_ENT) + (k & 1)]] =
+                                OWGS_REL_NOSUCH_BIT;
+                            else err |= OWGS_ERR_BAD_STREAM;
                             continue;
                         }
                         uint32_t q;
@@ -1256,8 +1260,9 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                 A.ovf.touched[atomicAdd(A.ovf.n_touched, 1)] = oj;
                             }
                         }
-                        if ((int)q >= ops0) {
-                            err |= OWGS_ERR_BAD_STREAM;
+                        if ((int)q >= ops0) {  // more releases than operations: which ones fail is fixed below
+                            if (A.rel_src) sc[SC_IRR] = 1;
+                            else err |= OWGS_ERR_BAD_STREAM;
                             continue;
                         }
                         if (mod_fast(c0 + (int)q + 1, R, __builtin_amdgcn_rcpf((float)R)) == 0)  // RS:50-52
@@ -1267,6 +1272,44 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
             }
             if (rel_ovf && !io) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // HBM counters landed
             lds_sync();
+            const bool irr = A.rel_src && sc[SC_IRR];  // (every wave reads it before the reset below)
+            if (irr) {
+                // explicit releases, some entry released more often than its operationCount: in stream order the
+                // first ops0 releases find the entry, the rest throw NoSuchElementException (NS:103) after its
+                // removal.  (The counts above already give the state; only the flags need the order.)  Invalid
+                // input only -- every completion of a scheduled activation has its operation -- so one wave
+                // walks the batch's concurrent records (stream order inside the class) and counts.
+                const int64_t cb = A.rel_off[b], ce = A.rel_off[b + 1], cm = cb + A.relcnt[2 * b];
+                if (wave == 0) {
+                    for (int64_t p = cm; p < ce; ++p) {
+                        const uint2 rr = A.rel_rec[p];
+                        const int inv = (int)(rr.x & 0x7FFFu);
+                        if (inv == (int)OWGS_RR_NOINV || inv >= n_slots) continue;
+                        const uint32_t key = ct_key(inv, (int)(rr.y & 0x1FFFFu));
+                        uint32_t v;
+                        const int ix = ct_find2(ct, A.ovf, rel_ovf, key, &v);
+                        const int ops0 = ct_ops(v);
+                        if (ix < 0 || ops0 <= 0) continue;
+                        const int cnt = (int)((ix < OWGS_CTC ? rc[ix]
+                                                             : __hip_atomic_load(&A.ovf.rc[ix - OWGS_CTC], __ATOMIC_RELAXED,
+                                                                                 __HIP_MEMORY_SCOPE_AGENT)) >> 12);
+                        if (cnt <= ops0) continue;
+                        int rank = 0;  // earlier releases of the same entry
+                        for (int64_t q0 = cm; q0 < p; q0 += 64) {
+                            const int64_t qq = q0 + lane;
+                            bool same = false;
+                            if (qq < p) {
+                                const uint2 r2 = A.rel_rec[qq];
+                                same = (int)(r2.x & 0x7FFFu) == inv && (r2.y & 0x1FFFFu) == (rr.y & 0x1FFFFu);
+                            }
+                            rank += __popcll(__ballot(same));
+                        }
+                        if (lane == 0) A.rel_flags[A.rel_src[p]] = rank >= ops0 ? OWGS_REL_NOSUCH_BIT : 0;
+                    }
+                }
+                lds_sync();
+                if (tid == 0) sc[SC_IRR] = 0;
+            }
 #ifdef OWGS_PROFILE
             pt_y[0] += memtime_pinned() - tb0;
 #endif

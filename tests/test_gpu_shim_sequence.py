@@ -42,6 +42,7 @@ def _jobs(w, rng, health_at, cluster_at):
     return jobs
 
 
+@pytest.mark.parametrize("mode", ["calls", "fused"])
 @pytest.mark.parametrize("seed,cluster_at,kw", [
     (1, None, {}),
     (2, {5: 2}, {}),
@@ -50,7 +51,9 @@ def _jobs(w, rng, health_at, cluster_at):
     (4, {4: 4, 9: 2}, dict(conc_frac=0.3, shared_frac=0.4, load=1.2, n_invokers=300)),
     (5, {2: 2, 6: 1, 10: 2}, dict(conc_frac=0.8, conc_range=(2, 3), n_invokers=200, load=1.3)),
 ])
-def test_shim_call_sequence_matches_oracle(seed, cluster_at, kw):
+def test_shim_call_sequence_matches_oracle(seed, cluster_at, kw, mode):
+    """mode "calls": one owgs_release_batch per release run and one owgs_publish_batch per publish run; "fused": one
+    owgs_process_batch per drained batch (all its runs between state updates), as the shim now does."""
     rng = np.random.default_rng(seed)
     base = dict(n_activations=40_000, n_invokers=600, n_actions=1500, n_namespaces=150)
     base.update(kw)
@@ -88,12 +91,34 @@ def test_shim_call_sequence_matches_oracle(seed, cluster_at, kw):
     jobs = _jobs(w, rng, health_at=3, cluster_at=cluster_at)
     seq = 0
     pos = 0
+    fused = []  # (releases, publishes) runs collected for one owgs_process_batch call
+
+    def flush():
+        if not fused:
+            return
+        ro, po, ri, ra, pa, sq, pubs_all = [0], [0], [], [], [], [], []
+        for rels, pubs, seqs in fused:
+            ri += [int(o_inv[a]) for a in rels]
+            ra += [by_key[acts[w.stream.act[a]].key] for a in rels]
+            pa += [handle(int(w.stream.act[a]))[0] for a in pubs]
+            sq += seqs
+            pubs_all += pubs
+            ro.append(len(ri))
+            po.append(len(pa))
+        r, f, rf = g.process_batch(ro, ri, ra, po, pa, seq=np.array(sq, np.uint64))
+        g_inv[pubs_all], g_fl[pubs_all] = r, f
+        if len(rf):
+            g_rf.append(rf)
+        fused.clear()
+
     while pos < len(jobs):
         batch = jobs[pos:pos + int(rng.integers(1, 4097))]  # queue.poll + drainTo(jobs, 4095)
         pos += len(batch)
         i = 0
         while i < len(batch):
             kind, x = batch[i]
+            if kind in ("inv", "clu"):
+                flush()
             if kind == "inv":
                 g.update_invokers_arrays(w.inv_ids, w.inv_mem, x)
                 o.update_invokers(w.inv_ids, w.inv_mem, x)
@@ -114,28 +139,77 @@ def test_shim_call_sequence_matches_oracle(seed, cluster_at, kw):
             while i < len(batch) and batch[i][0] == "pub":
                 pubs.append(batch[i][1])
                 i += 1
-            rels = [a for a in rels if g_inv[a] >= 0]  # no ActivationEntry for a failed publish
+            # a fused call returns its decisions at its end: releases inside one drained batch name the invoker the
+            # oracle chose (equal to the GPU's, which the final comparison checks)
+            dec = o_inv if mode == "fused" else g_inv
+            rels = [a for a in rels if dec[a] >= 0]  # no ActivationEntry for a failed publish
             if rels:
-                inv = g_inv[rels]
+                inv = dec[rels]
                 hk = [by_key[acts[w.stream.act[a]].key] for a in rels]
-                g_rf.append(g.release_invoker(inv, hk))
+                if mode == "calls":
+                    g_rf.append(g.release_invoker(inv, hk))
                 ok = [(acts[w.stream.act[a]].namespace, acts[w.stream.act[a]].key) for a in rels]
                 o_rf.append(np.array([{0: 0, O.THROW_NOSUCHELEMENT: 1, O.THROW_OVERFLOW: 2}.get(
                     o.release(int(iv), o_h[k]), 8) for iv, k in zip(inv, ok)], np.uint8))
                 z_rf.append(np.array([O._rel_bits(z.release(int(iv), z_h[k])) for iv, k in zip(inv, ok)], np.uint8))
+            if mode == "fused":
+                fused.append((rels, pubs, list(range(seq, seq + len(pubs)))))
             if pubs:
                 hs = [handle(int(w.stream.act[a])) for a in pubs]
                 sq = np.arange(seq, seq + len(pubs), dtype=np.uint64)
                 seq += len(pubs)
-                r, f = g.publish([h for h, _ in hs], seq=sq)
-                g_inv[pubs], g_fl[pubs] = r, f
+                if mode == "calls":
+                    r, f = g.publish([h for h, _ in hs], seq=sq)
+                    g_inv[pubs], g_fl[pubs] = r, f
                 for k, (a, (_, oh)) in enumerate(zip(pubs, hs)):
                     o_inv[a], o_fl[a] = o.publish(oh, int(sq[k]))
                     z.publish(z_h[(acts[w.stream.act[a]].namespace, acts[w.stream.act[a]].key)], int(sq[k]))
                     seq_of[a] = int(sq[k])
+        flush()  # one owgs_process_batch per drained batch (fused mode)
+    flush()
     assert np.array_equal(g_inv, o_inv), np.nonzero(g_inv != o_inv)[0][:5]
     assert np.array_equal(g_fl, o_fl)
     assert np.array_equal(np.concatenate(g_rf), np.concatenate(o_rf))
     assert np.array_equal(g.permits(), o.permits())
     if cluster_at:  # these variants reach releases that only the reference's empty entries explain
         assert not np.array_equal(np.concatenate(z_rf), np.concatenate(o_rf))
+
+
+def test_fused_batch_release_flags_follow_stream_order():
+    """Releases the reference rejects, inside one owgs_process_batch call: a completion released twice in one run (the
+    second finds the entry removed: NoSuchElementException, NS:103), a concurrent fqn never scheduled on that invoker,
+    an invoker outside invokerSlots (lift: no-op, SCPB:329) and a release without ActivationEntry (CLB:278-279)."""
+    from openwhisk_amd import Action, InvokerHealth
+    MB = 1024 * 1024
+    g = GpuShardingContainerPoolBalancer(managed_fraction=1.0, blackbox_fraction=0.0)
+    o = O.BalancerState(1.0, 0.0, zombies=True)
+    n = 6
+    g.update_invokers([InvokerHealth(i, 8192 * MB) for i in range(n)])
+    o.update_invokers(np.arange(n, dtype=np.int32), np.full(n, 8192 * MB, np.int64), np.zeros(n, np.uint8))
+    acts = [Action("ns", "ns/c", "0.0.1", 256, 4), Action("ns", "ns/a", "0.0.1", 512, 1),
+            Action("ns", "ns/d", "0.0.1", 128, 3)]
+    hs, _ = g.register_actions(acts)
+    oh = [o.register_action(a.namespace, a.path, k, a.mem_mb, a.max_concurrent, a.blackbox) for k, a in enumerate(acts)]
+    pubs = [0, 0, 1, 2, 0, 2]
+    gi, gf, _ = g.process_batch([0, 0], [], [], [0, len(pubs)], [hs[p] for p in pubs])
+    oi = [o.publish(oh[p], k) for k, p in enumerate(pubs)]
+    assert [(int(a), int(b)) for a, b in zip(gi, gf)] == oi
+    x0, x2 = int(gi[0]), int(gi[3])
+    other = (x0 + 1) % n
+    # run 1: ns/c released once more than scheduled, ns/d on an invoker it never used, out of range, no entry;
+    # run 2: publishes; run 3: the second ns/c activation (same entry) and the maxConcurrent == 1 one
+    rel = [(x0, 0), (x0, 0), (other, 2), (x0, 0), (99, 1), (x0, 0), (-1, 1), (x2, 2)]  # ns/c: 3 scheduled, 4 released
+    rel3 = [(x0, 0), (int(gi[2]), 1)]
+    ri = [r for r, _ in rel] + [r for r, _ in rel3]
+    ra = [hs[a] for _, a in rel] + [hs[a] for _, a in rel3]
+    pubs2 = [2, 0, 1]
+    gi2, gf2, grf = g.process_batch([0, len(rel), len(rel), len(ri)], ri, ra, [0, 0, len(pubs2), len(pubs2)],
+                                    [hs[p] for p in pubs2], seq=np.arange(10, 13, dtype=np.uint64))
+    orf = [O._rel_bits(o.release(r, oh[a])) for r, a in rel]
+    oi2 = [o.publish(oh[p], 10 + k) for k, p in enumerate(pubs2)]
+    orf += [O._rel_bits(o.release(r, oh[a])) for r, a in rel3]
+    orf = [f if r >= 0 else 4 for f, r in zip(orf, ri)]
+    assert [(int(a), int(b)) for a, b in zip(gi2, gf2)] == oi2
+    assert grf.tolist() == orf
+    assert 1 in orf  # NoSuchElement reached
+    assert np.array_equal(g.permits(), o.permits())
