@@ -52,6 +52,7 @@ def parse(argv=None):
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--no-h2d", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-shim-path", action="store_true", help="skip the shim-path leg (per-call latency)")
     ap.add_argument("--slots", choices=("split", "weak"), default="split",
                     help="'split' (default): 16 GiB invokers, each controller's slot = 1/clusterSize of them "
                          "(configs[4]); 'weak': invoker memory 16 GiB x clusterSize so every slot stays 16 GiB")
@@ -193,6 +194,111 @@ def cpu_baseline(args, w0, n_ctl, shard0):
         out["parallel"] = {"value": nt / dtt, "unit": "decisions/s", "cores": T,
                            "sample": f"{T} threads, one shard stream each, {dtt:.2f} s wall"}
     return out
+
+
+def shim_path(w, o_inv, dev_index, drains=(64, 512, 4096), budget_jobs=(120_000, 480_000, None)):
+    """The path the JVM shim drives (integration/GpuShardingContainerPoolBalancer.scala): the shard's stream as the
+    batching thread's queue -- per batch its completions, then its publishes -- drained `drain` jobs at a time.  Each
+    drained batch splits into runs of releases followed by publishes; "calls" issues one owgs_release_batch per release
+    run and one owgs_publish_batch per publish run (host buffers, as the JNI stub hands them over), "fused" one
+    owgs_process_batch per drained batch.  Per-call latency is the C call alone (arguments prepared before the clock).
+    Decisions are compared with the oracle's replay of the same prefix."""
+    import ctypes as C
+
+    from openwhisk_amd import GpuShardingContainerPoolBalancer
+
+    s = w.stream
+    jobs_rel, jobs_pub = [], []  # per batch: release activation ids, publish ids
+    kinds = []
+    for b in range(s.n_batches):
+        r = s.rel_aid[s.rel_off[b]:s.rel_off[b + 1]]
+        kinds.append(np.concatenate([np.zeros(len(r), np.int8), np.ones(int(s.acq_off[b + 1] - s.acq_off[b]), np.int8)]))
+        jobs_rel.append(r)
+        jobs_pub.append(np.arange(s.acq_off[b], s.acq_off[b + 1]))
+    kind = np.concatenate(kinds)
+    ids = np.concatenate([np.concatenate([jobs_rel[b], jobs_pub[b]]) for b in range(s.n_batches)]).astype(np.int64)
+    b = GpuShardingContainerPoolBalancer(managed_fraction=w.managed_fraction, blackbox_fraction=w.blackbox_fraction,
+                                         rng_seed=w.rng_seed, device=dev_index)
+    b.update_invokers_arrays(w.inv_ids, w.inv_mem, w.inv_status)
+    b.update_cluster(w.cluster_size)
+    b.register_actions(w.actions)
+    b.snapshot()
+    L, h = b._L, b._h
+    p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    act = np.ascontiguousarray(s.act, np.int32)
+    legs = []
+    for drain, budget in zip(drains, budget_jobs):
+        n_jobs = len(ids) if budget is None else min(budget, len(ids))
+        for mode in ("calls", "fused"):
+            b.restore()
+            inv = np.full(len(act), -9, np.int32)
+            fl = np.zeros(len(act), np.uint8)
+            lat, n_pub = [], 0
+            for c0 in range(0, n_jobs, drain):
+                k = kind[c0:min(c0 + drain, n_jobs)]
+                x = ids[c0:c0 + len(k)]
+                # runs: maximal (releases, publishes) pairs
+                cut = np.nonzero((k[1:] == 0) & (k[:-1] == 1))[0] + 1
+                bounds = np.concatenate([[0], cut, [len(k)]])
+                runs = []
+                for r0, r1 in zip(bounds[:-1], bounds[1:]):
+                    kk, xx = k[r0:r1], x[r0:r1]
+                    rel = xx[kk == 0]
+                    # a completion follows its publish; one published earlier in the SAME drained batch (the
+                    # stream's one-batch delay at a drain boundary) names the oracle's invoker (= the GPU's, checked)
+                    ri = inv[rel]
+                    if o_inv is not None:
+                        ri = np.where(ri == -9, o_inv[rel], ri)
+                    keep = ri >= 0  # no ActivationEntry for a failed publish (CLB:278-279)
+                    runs.append((np.ascontiguousarray(ri[keep]), np.ascontiguousarray(act[rel[keep]]),
+                                 np.ascontiguousarray(xx[kk == 1])))
+                if mode == "calls":
+                    for ri, ra, pubs in runs:
+                        if len(ri):
+                            rf = np.zeros(len(ri), np.uint8)
+                            t0 = time.perf_counter()
+                            rc = L.owgs_release_batch(h, len(ri), p(ri), p(ra), p(rf))
+                            lat.append(time.perf_counter() - t0)
+                            assert rc == 0
+                        if len(pubs):
+                            pa = np.ascontiguousarray(act[pubs])
+                            sq = pubs.astype(np.uint64)
+                            o = np.zeros(len(pubs), np.int32)
+                            f = np.zeros(len(pubs), np.uint8)
+                            t0 = time.perf_counter()
+                            rc = L.owgs_publish_batch(h, len(pubs), p(pa), p(sq), 0, p(o), p(f))
+                            lat.append(time.perf_counter() - t0)
+                            assert rc == 0
+                            inv[pubs], fl[pubs] = o, f
+                            n_pub += len(pubs)
+                else:
+                    ro = np.cumsum([0] + [len(r[0]) for r in runs]).astype(np.int32)
+                    po = np.cumsum([0] + [len(r[2]) for r in runs]).astype(np.int32)
+                    ri = np.concatenate([r[0] for r in runs] + [np.zeros(1, np.int32)]).astype(np.int32)
+                    ra = np.concatenate([r[1] for r in runs] + [np.zeros(1, np.int32)]).astype(np.int32)
+                    pubs = np.concatenate([r[2] for r in runs]).astype(np.int64)
+                    pa = np.ascontiguousarray(np.concatenate([act[pubs], np.zeros(1, np.int32)]))
+                    sq = np.ascontiguousarray(np.concatenate([pubs, [0]]).astype(np.uint64))
+                    o = np.zeros(len(pubs) + 1, np.int32)
+                    f = np.zeros(len(pubs) + 1, np.uint8)
+                    rf = np.zeros(len(ri), np.uint8)
+                    t0 = time.perf_counter()
+                    rc = L.owgs_process_batch(h, len(runs), p(ro), p(ri), p(ra), p(rf), p(po), p(pa), p(sq), 0, p(o),
+                                              p(f))
+                    lat.append(time.perf_counter() - t0)
+                    assert rc == 0, (rc, L.owgs_last_error(h))
+                    inv[pubs], fl[pubs] = o[:len(pubs)], f[:len(pubs)]
+                    n_pub += len(pubs)
+            done = inv != -9
+            exact = bool(np.array_equal(inv[done], o_inv[done])) if o_inv is not None else None
+            lat_us = np.array(lat) * 1e6
+            legs.append({"drain": drain, "mode": mode, "jobs": n_jobs, "calls": len(lat), "publishes": int(n_pub),
+                         "p50_us": float(np.percentile(lat_us, 50)), "p99_us": float(np.percentile(lat_us, 99)),
+                         "decisions_per_s": n_pub / max(float(np.sum(lat)), 1e-9), "bit_exact": exact})
+    b.close()
+    return {"path": "host buffers through the C ABI as the JNI shim calls it (queue order: each batch's completions, "
+                    "then its publishes); calls = owgs_release_batch + owgs_publish_batch per run, fused = "
+                    "owgs_process_batch per drained batch; latency = the C call", "legs": legs}
 
 
 def dry_run(args):
@@ -355,6 +461,7 @@ def main():
     kern_ms = float(np.mean(eng))
 
     exact = True
+    o_ref = None
     if not args.no_check:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O
@@ -362,6 +469,8 @@ def main():
         for sh in shards:
             st = O.state_for(sh.w)
             o_inv, o_fl, o_rf = st.replay(sh.s)
+            if o_ref is None:
+                o_ref = o_inv
             exact = exact and (np.array_equal(o_inv, sh.d_out.cpu().numpy())
                                and np.array_equal(o_fl, sh.d_fl.cpu().numpy())
                                and np.array_equal(o_rf, sh.d_rf.cpu().numpy()[: len(o_rf)])
@@ -379,6 +488,10 @@ def main():
                 sh.b.restore()
                 sh.b.replay(sh.s)
         h2d_ms = (time.perf_counter() - t1) / reps * 1e3
+
+    shim = None
+    if world == 1 and K == 1 and not args.no_shim_path:
+        shim = shim_path(w, o_ref, torch.cuda.current_device())
 
     n_dec = sum(len(sh.s.act) for sh in shards)  # this rank's decisions per step
     t_step = wall / args.steps
@@ -427,6 +540,7 @@ def main():
             "h2d_inclusive": None if args.no_h2d else {
                 "value": world * n_dec / (h2d_ms * 1e-3), "unit": "decisions/s", "ms_per_step": h2d_ms,
                 "path": "owgs_replay host ABI: host checks + H2D stream + replay + D2H decisions"},
+            "shim_path": shim,
             "engine_stats": stats,
             "cpu_baseline": cpu,
         }
