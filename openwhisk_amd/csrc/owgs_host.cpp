@@ -86,6 +86,22 @@ extern "C" hipError_t owgs_launch_w_relgather(const int64_t* rel_aid, int32_t n,
 
 namespace {
 
+// diagnostic environment switches, read once per process (not on every call)
+struct EnvOpts {
+    int opts = 0, cw = 0, deal = -1;
+    bool trace = false;
+    EnvOpts() {
+        if (const char* o = getenv("OWGS_OPTS")) opts = atoi(o);
+        if (const char* e = getenv("OWGS_CW")) cw = atoi(e);
+        if (const char* e = getenv("OWGS_DEAL")) deal = atoi(e);
+        trace = getenv("OWGS_TRACE_FILE") != nullptr;
+    }
+};
+const EnvOpts& env_opts() {
+    static const EnvOpts e;
+    return e;
+}
+
 template <class T>
 struct DevBuf {
     T* p = nullptr;
@@ -223,6 +239,7 @@ struct owgs_ctx {
     DevBuf<int64_t> w_off;
     DevBuf<uint8_t> w_rfl;
     int32_t w_cap = 0, w_live = 0;
+    int32_t cw_cache = 0;  // chunk width of the current state and actions (0: recompute)
     // owgs_process_batch: pinned staging (inputs, outputs) and their device copies
     void* h_pin = nullptr;
     size_t h_pin_bytes = 0;
@@ -268,6 +285,7 @@ static hipError_t upload(DevBuf<T>& d, const T* h, size_t n, hipStream_t s) {
 // lists.  InvokerPool pads the health list so that position i holds invoker id i (InvokerSupervision.scala:191-207):
 // then pool position p is id p (managed) or N - blackboxes + p (blackbox) and the engine keeps only a usable bitmap.
 static int rebuild_pools(owgs_ctx* c) {
+    c->cw_cache = 0;
     std::vector<int32_t> words, hl;
     int32_t cnt[2], hcnt[2];
     c->shortcut_ok = 3;
@@ -525,10 +543,9 @@ static void base_args(owgs_ctx* c, OwgsEngineArgs& A) {
     A.rng_seed = c->cfg.rng_seed;
     A.stats = c->d_stats.p;
     A.err = c->d_err.p;
-    const char* o = getenv("OWGS_OPTS");
-    A.opts = o ? atoi(o) : 0;
+    A.opts = env_opts().opts;
     A.trace = nullptr;
-    if (getenv("OWGS_TRACE_FILE")) {  // diagnostic: a -DOWGS_TRACE engine logs its barrier timeline here
+    if (env_opts().trace) {  // diagnostic: a -DOWGS_TRACE engine logs its barrier timeline here
         const size_t n = (size_t)(OWGS_EW + 1) * 16384 * 2;
         if (c->d_trace.reserve(n) == hipSuccess && hipMemset(c->d_trace.p, 0, n * 8) == hipSuccess) A.trace = c->d_trace.p;
     }
@@ -543,7 +560,8 @@ static void base_args(owgs_ctx* c, OwgsEngineArgs& A) {
 #ifndef OWGS_WIDE_UNITS
 #define OWGS_WIDE_UNITS 60000.0
 #endif
-static int32_t chunk_width(const owgs_ctx* c) {
+static int32_t chunk_width(owgs_ctx* c) {
+    if (c->cw_cache > 0) return c->cw_cache;  // recomputed after a state or action change (cw_cache = 0)
     double slot_mb = 0, act_mb = 0;
     const int32_t nm = std::min<int32_t>(c->nm, (int32_t)c->mem.size());
     for (int32_t i = 0; i < nm; ++i)
@@ -553,10 +571,9 @@ static int32_t chunk_width(const owgs_ctx* c) {
     // (with in-pass re-decisions, round 2: configs[1] 19k units 116 ms at 192 vs 119 at 128; configs[3] 221 vs 232;
     // C5 shard of 8 165 vs 173; C5 shard of 4, 34k units: 102 ms at 256 vs 106 at 192 and 117 at 128)
     int32_t cw = units >= OWGS_WIDE_UNITS ? OWGS_WL : std::min(units >= OWGS_WIDE_UNITS / 2 ? 256 : 192, OWGS_WL);
-    if (const char* e = getenv("OWGS_CW")) {
-        const int v = atoi(e);
-        if (v >= 64 && v <= OWGS_WL) cw = v;
-    }
+    const int v = env_opts().cw;
+    if (v >= 64 && v <= OWGS_WL) cw = v;
+    c->cw_cache = cw;
     return cw;
 }
 
@@ -581,7 +598,7 @@ static int run_prepass(owgs_ctx* c, OwgsEngineArgs& A, int32_t n_batches, const 
     // concurrent path: 10k invokers 33.9 vs 37.5 ms), spread over every wave for small pools, where concurrent walks
     // are long (1k invokers, 30 % concurrent: 553 vs 681 ms)
     p.deal = c->nm >= 4096 ? 1 : 2;
-    if (const char* e = getenv("OWGS_DEAL")) p.deal = atoi(e);
+    if (env_opts().deal >= 0) p.deal = env_opts().deal;
     HIPCHK(c, c->d_lix.reserve((size_t)std::max<int64_t>(max_chunks, 1) * OWGS_WL));
     p.rec = c->d_rec.p;
     p.lix = c->d_lix.p;
@@ -989,6 +1006,7 @@ int owgs_register_actions(owgs_ctx* c, int32_t n, const char* ns_bytes, const in
     }
     (void)hipSetDevice(c->cfg.device);
     const int32_t base = (int32_t)c->a_mem.size();
+    c->cw_cache = 0;
     for (int32_t i = 0; i < n; ++i) {
         std::string k(key_bytes + key_off[i], (size_t)(key_off[i + 1] - key_off[i]));
         auto it = c->slot_ids.find(k);
@@ -1600,7 +1618,9 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
     uint8_t* d_fl = (uint8_t*)(DO + q_fl);
     uint8_t* d_rf = (uint8_t*)(DO + q_rf);
     int rc = OWGS_OK;
-    if (c->w_cap > 0) {  // watched pairs: the exact release kernels per run, the watch update after each publish run
+    if (c->w_cap > 0 || NP == 0) {
+        // watched pairs: the exact release kernels per run, the watch update after each publish run; a call of
+        // completions only: the release kernels alone (cheaper than an engine launch)
         int32_t max_r = 1;
         for (int32_t r = 0; r < n_runs; ++r) max_r = std::max(max_r, rel_off[r + 1] - rel_off[r]);
         HIPCHK(c, c->w_rel.reserve((size_t)3 * max_r));

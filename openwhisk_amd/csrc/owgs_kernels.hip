@@ -32,6 +32,8 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <atomic>
+
 #include "owgs_internal.h"
 #include "owgs_table.h"
 
@@ -1042,11 +1044,24 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
 
     // ---------------------------------------------------------------- state -> LDS
     uint32_t err = 0;
-    for (int i = tid; i < n_slots; i += OWGS_NT) {
-        const int v = A.permits[i];
-        if (v < -OWGS_PLIM || v >= OWGS_PLIM) err |= OWGS_ERR_PERMITS;
-        const bool unusable = A.pool_mode == 0 && i < A.n_ids && !((A.usable[i >> 5] >> (i & 31)) & 1u);
-        P[i] = unusable ? v + OWGS_PENC : v;
+    constexpr int LB = 8;  // loads in flight per thread (the state load is latency-bound)
+    for (int i0 = 0; i0 < n_slots; i0 += OWGS_NT * LB) {
+        int v[LB];
+        uint32_t u[LB];
+#pragma unroll
+        for (int k = 0; k < LB; ++k) {
+            const int i = i0 + k * OWGS_NT + tid;
+            v[k] = i < n_slots ? A.permits[i] : 0;
+            u[k] = (A.pool_mode == 0 && i < A.n_ids) ? A.usable[i >> 5] : ~0u;
+        }
+#pragma unroll
+        for (int k = 0; k < LB; ++k) {
+            const int i = i0 + k * OWGS_NT + tid;
+            if (i >= n_slots) continue;
+            if (v[k] < -OWGS_PLIM || v[k] >= OWGS_PLIM) err |= OWGS_ERR_PERMITS;
+            const bool unusable = !((u[k] >> (i & 31)) & 1u);
+            P[i] = unusable ? v[k] + OWGS_PENC : v[k];
+        }
     }
     if (A.pool_mode == 0) {
         for (int i = tid; i < words; i += OWGS_NT) ub[i] = A.usable[i];
@@ -1057,10 +1072,21 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     lds_sync();
     {
         int used = 0;
-        for (int i = tid; i < OWGS_CTC; i += OWGS_NT) {
-            const uint32_t k = A.ct_keys[i];
-            ct[i] = make_uint2(k, A.ct_vals[i]);
-            used += k != 0;
+        for (int i0 = 0; i0 < OWGS_CTC; i0 += OWGS_NT * LB) {
+            uint32_t kk[LB], vv[LB];
+#pragma unroll
+            for (int k = 0; k < LB; ++k) {
+                const int i = i0 + k * OWGS_NT + tid;
+                kk[k] = i < OWGS_CTC ? A.ct_keys[i] : 0u;
+                vv[k] = i < OWGS_CTC ? A.ct_vals[i] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < LB; ++k) {
+                const int i = i0 + k * OWGS_NT + tid;
+                if (i >= OWGS_CTC) continue;
+                ct[i] = make_uint2(kk[k], vv[k]);
+                used += kk[k] != 0;
+            }
         }
         if (used) atomicAdd(&sc[SC_USED], used);
         if (tid == 0 && A.ovf.cap > 0) sc[SC_OVF] = __hip_atomic_load(A.ovf.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3273,6 +3299,20 @@ extern "C" hipError_t owgs_launch_release_seq(const OwgsReleaseArgs* a, hipStrea
     return hipGetLastError();
 }
 
+// the engine's dynamic-LDS limit, set once per (kernel, device): the attribute is per device, and a process may drive
+// contexts on several devices
+static hipError_t lds_attr(const void* fn, int which) {
+    static std::atomic<unsigned long long> done[3];
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const unsigned long long bit = 1ull << (dev & 63);
+    if (done[which].load(std::memory_order_relaxed) & bit) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, OWGS_LDS_BYTES);
+    if (e == hipSuccess) done[which].fetch_or(bit);
+    return e;
+}
+
 extern "C" hipError_t owgs_launch_engine_multi_dev(const OwgsEngineArgs* a_host, const OwgsEngineArgs* a_dev, int k,
                                                    hipStream_t s) {
     if (k < 1 || k > OWGS_MULTI_DEV_MAX) return hipErrorInvalidValue;
@@ -3281,9 +3321,7 @@ extern "C" hipError_t owgs_launch_engine_multi_dev(const OwgsEngineArgs* a_host,
         lds = std::max(lds, owgs_engine_lds_bytes(a_host[i].n_slots, a_host[i].pool_mode, a_host[i].n_ids,
                                                   a_host[i].nm, a_host[i].nb, a_host[i].n_actions));
     if (lds > OWGS_LDS_BYTES) return hipErrorInvalidValue;
-    // per launch (cheap): the attribute is per device, and a process may drive contexts on several devices
-    const hipError_t ea = hipFuncSetAttribute((const void*)owgs_engine_multi_dev_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                              OWGS_LDS_BYTES);
+    const hipError_t ea = lds_attr((const void*)owgs_engine_multi_dev_kernel, 0);
     if (ea != hipSuccess) return ea;
     hipLaunchKernelGGL(owgs_engine_multi_dev_kernel, dim3(k), dim3(OWGS_NT), lds, s, a_dev);
     return hipGetLastError();
@@ -3299,9 +3337,7 @@ extern "C" hipError_t owgs_launch_engine_multi(const OwgsEngineArgs* a, int k, h
         M.a[i] = a[i];
     }
     if (lds > OWGS_LDS_BYTES) return hipErrorInvalidValue;
-    // per launch (cheap): the attribute is per device, and a process may drive contexts on several devices
-    const hipError_t ea = hipFuncSetAttribute((const void*)owgs_engine_multi_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                              OWGS_LDS_BYTES);
+    const hipError_t ea = lds_attr((const void*)owgs_engine_multi_kernel, 1);
     if (ea != hipSuccess) return ea;
     hipLaunchKernelGGL(owgs_engine_multi_kernel, dim3(k), dim3(OWGS_NT), lds, s, M);
     return hipGetLastError();
@@ -3310,9 +3346,7 @@ extern "C" hipError_t owgs_launch_engine_multi(const OwgsEngineArgs* a, int k, h
 extern "C" hipError_t owgs_launch_engine(const OwgsEngineArgs* a, hipStream_t s) {
     const size_t lds = owgs_engine_lds_bytes(a->n_slots, a->pool_mode, a->n_ids, a->nm, a->nb, a->n_actions);
     if (lds > OWGS_LDS_BYTES) return hipErrorInvalidValue;
-    // per launch (cheap): the attribute is per device, and a process may drive contexts on several devices
-    const hipError_t ea = hipFuncSetAttribute((const void*)owgs_engine_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                              OWGS_LDS_BYTES);
+    const hipError_t ea = lds_attr((const void*)owgs_engine_kernel, 2);
     if (ea != hipSuccess) return ea;
     OwgsEngineOne M;
     M.a[0] = *a;
