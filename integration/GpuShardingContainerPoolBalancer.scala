@@ -7,22 +7,35 @@
  *
  * Everything except the scheduling state stays as in ShardingContainerPoolBalancer (SCPB): CommonLoadBalancer keeps
  * activation bookkeeping, the Kafka send, the ack feed and processCompletion; the monitor actor keeps forwarding
- * CurrentInvokerPoolState and cluster membership.  publish() enqueues into a single batching thread that owns the
- * native context (single writer, owgs.h "Threading"), which calls owgs_publish_batch and completes the promises in
- * stream order; releaseInvoker() enqueues into the same thread (owgs_release_batch).
+ * CurrentInvokerPoolState and cluster membership (including cluster bootstrap, SCPB:159-167); the capacity/health gauges
+ * (SCPB:169-205) and the per-activation logs (SCPB:299-301, 312-314) are emitted as the reference does.  publish()
+ * enqueues into a single batching thread that owns the native context (single writer, owgs.h "Threading");
+ * releaseInvoker() enqueues into the same thread.  Each drained batch goes to the engine as ONE owgs_process_batch
+ * call (runs of completions then publishes, in queue order) through direct ByteBuffers: no JVM array is pinned across
+ * the GPU round trip.
  */
 package org.apache.openwhisk.core.loadBalancer
 
+import java.nio.{ByteBuffer, ByteOrder}
 import java.util.concurrent.{ArrayBlockingQueue, TimeUnit}
 
 import akka.actor.{Actor, ActorRef, ActorRefFactory, ActorSystem, Props}
+import akka.cluster.ClusterEvent._
+import akka.cluster.{Cluster, Member, MemberStatus}
+import akka.management.scaladsl.AkkaManagement
+import akka.management.cluster.bootstrap.ClusterBootstrap
 import akka.stream.ActorMaterializer
 import org.apache.kafka.clients.producer.RecordMetadata
+import pureconfig._
+import pureconfig.generic.auto._
 import org.apache.openwhisk.common._
-import org.apache.openwhisk.core.WhiskConfig
+import org.apache.openwhisk.common.LoggingMarkers._
 import org.apache.openwhisk.core.WhiskConfig._
 import org.apache.openwhisk.core.connector._
 import org.apache.openwhisk.core.entity._
+import org.apache.openwhisk.core.entity.size.SizeLong
+import org.apache.openwhisk.core.loadBalancer.InvokerState.{Healthy, Offline, Unhealthy, Unresponsive}
+import org.apache.openwhisk.core.{ConfigKeys, WhiskConfig}
 import org.apache.openwhisk.spi.SpiLoader
 
 import scala.collection.mutable
@@ -38,10 +51,28 @@ object OwgsNative {
   @native def updateCluster(ctx: Long, size: Int): Int
   @native def registerAction(ctx: Long, namespace: String, path: String, key: String, memMb: Int, maxConc: Int,
                              blackbox: Boolean): Int
-  @native def publishBatch(ctx: Long, actions: Array[Int], seq: Array[Long], n: Int, outInvoker: Array[Int],
-                           outFlags: Array[Byte]): Int
-  @native def releaseBatch(ctx: Long, invokers: Array[Int], actions: Array[Int], n: Int, outFlags: Array[Byte]): Int
+  /** owgs_process_batch over direct buffers (native byte order), layout in BatchBuffers. */
+  @native def processBatch(ctx: Long, in: ByteBuffer, out: ByteBuffer, nRuns: Int, nRel: Int, nPub: Int): Int
   @native def lastError(ctx: Long): String
+}
+
+/** The direct buffers of one drained batch (owgs_jni.c processBatch reads the same layout):
+ *  in  = relOff[nRuns + 1], pubOff[nRuns + 1], relInvoker[nRel], relAction[nRel], pubAction[nPub] (ints), then
+ *        seq[nPub] (longs, 8-byte aligned);
+ *  out = outInvoker[nPub] (ints), outFlags[nPub], relFlags[nRel] (bytes). */
+final class BatchBuffers {
+  var in: ByteBuffer = ByteBuffer.allocateDirect(1 << 16).order(ByteOrder.nativeOrder())
+  var out: ByteBuffer = ByteBuffer.allocateDirect(1 << 15).order(ByteOrder.nativeOrder())
+  def ensure(nRuns: Int, nRel: Int, nPub: Int): Unit = {
+    val ints = 2 * (nRuns + 1) + 2 * nRel + nPub
+    val inBytes = ((4L * ints + 7) & ~7L) + 8L * nPub
+    val outBytes = 4L * nPub + nPub + nRel
+    if (inBytes > in.capacity) in = ByteBuffer.allocateDirect((2 * inBytes).toInt).order(ByteOrder.nativeOrder())
+    if (outBytes > out.capacity) out = ByteBuffer.allocateDirect((2 * outBytes).toInt).order(ByteOrder.nativeOrder())
+    in.clear()
+    out.clear()
+  }
+  def seqOffset(nRuns: Int, nRel: Int, nPub: Int): Int = ((4 * (2 * (nRuns + 1) + 2 * nRel + nPub)) + 7) & ~7
 }
 
 class GpuShardingContainerPoolBalancer(config: WhiskConfig,
@@ -54,6 +85,17 @@ class GpuShardingContainerPoolBalancer(config: WhiskConfig,
                                                                            materializer: ActorMaterializer)
     extends CommonLoadBalancer(config, feedFactory, controllerInstance) {
 
+  /** Build a cluster of all loadbalancers, exactly as SCPB:159-167 does (bootstrap, seed nodes, or none). */
+  private val cluster: Option[Cluster] = if (loadConfigOrThrow[ClusterConfig](ConfigKeys.cluster).useClusterBootstrap) {
+    AkkaManagement(actorSystem).start()
+    ClusterBootstrap(actorSystem).start()
+    Some(Cluster(actorSystem))
+  } else if (loadConfigOrThrow[Seq[String]]("akka.cluster.seed-nodes").nonEmpty) {
+    Some(Cluster(actorSystem))
+  } else {
+    None
+  }
+
   // device and overload-RNG seed of this controller: whisk.loadbalancer.gpu.{device, rng-seed} (optional keys)
   private val gpuConfig = actorSystem.settings.config
   private def cfgInt(k: String, d: Int): Int = if (gpuConfig.hasPath(k)) gpuConfig.getInt(k) else d
@@ -63,14 +105,31 @@ class GpuShardingContainerPoolBalancer(config: WhiskConfig,
     cfgLong("whisk.loadbalancer.gpu.rng-seed", controllerInstance.asString.hashCode.toLong))
   require(ctx != 0L, "owgs_create failed (no MI355X visible or libowgs.so missing)")
 
+  // SCPB:467-468: the fractions the state uses (also for the pool views below)
+  private val managedFraction: Double = Math.max(0.0, Math.min(1.0, lbConfig.managedFraction))
+  private val blackboxFraction: Double = Math.max(1.0 - managedFraction, Math.min(1.0, lbConfig.blackboxFraction))
+
   // (invoking namespace, fqn@version) -> native action handle (registered once); fqn@version -> a handle of that
   // action for releases (a release only needs the NestedSemaphore key and the limits, NS:98-113)
   private val handles = mutable.HashMap.empty[(String, String), Int]
   private val byKey = mutable.HashMap.empty[String, Int]
-  @volatile private var invokerList: IndexedSeq[InvokerHealth] = IndexedSeq.empty
-  // userMemory by invoker id (ids are dense: InvokerPool pads the list by id, InvokerSupervision.scala:191-207)
-  @volatile private var invokerMemoryById: Array[ByteSize] = Array.empty
+
+  /** The invoker list the engine schedules against, its pools (SCPB:518-523) and userMemory by id, published by the
+   *  batching thread right after owgs_update_invokers succeeded (so a decision and the InvokerInstanceId it returns
+   *  come from the same list, as schedule() takes both from `invokers(index)`, SCPB:411-414). */
+  private final case class Pools(all: IndexedSeq[InvokerHealth], managed: IndexedSeq[InvokerHealth],
+                                 blackbox: IndexedSeq[InvokerHealth], memById: Array[ByteSize])
+  @volatile private var pools = Pools(IndexedSeq.empty, IndexedSeq.empty, IndexedSeq.empty, Array.empty)
   @volatile private var _clusterSize = 1
+
+  private def poolsOf(s: IndexedSeq[InvokerHealth]): Pools = {
+    val managed = Math.max(1, Math.ceil(s.size.toDouble * managedFraction).toInt)
+    val blackboxes = Math.max(1, Math.floor(s.size.toDouble * blackboxFraction).toInt)
+    val mem = new Array[ByteSize](if (s.isEmpty) 0 else s.map(_.id.toInt).max + 1)
+    java.util.Arrays.fill(mem.asInstanceOf[Array[AnyRef]], 0.B)
+    s.foreach(h => mem(h.id.toInt) = h.id.userMemory)
+    Pools(s, s.take(managed), s.takeRight(blackboxes), mem)
+  }
 
   private sealed trait Job
   private case class Pub(action: ExecutableWhiskActionMetaData, msg: ActivationMessage, seq: Long,
@@ -81,97 +140,106 @@ class GpuShardingContainerPoolBalancer(config: WhiskConfig,
 
   private val queue = new ArrayBlockingQueue[Job](1 << 16)
   private var seqNo = 0L
+  private val bufs = new BatchBuffers
 
   private def nativeError(what: String, rc: Int): LoadBalancerException =
     LoadBalancerException(s"$what failed ($rc): ${OwgsNative.lastError(ctx)}")
 
-  /** One drained batch of jobs, in queue order (the sequential order the engine replays). */
+  /** One drained batch of jobs, in queue order (the sequential order the engine replays).  State updates are applied
+   *  between segments; each segment of (completions, publishes) runs is ONE owgs_process_batch call. */
   private def runBatch(jobs: java.util.ArrayList[Job]): Unit = {
+    val segment = mutable.ArrayBuffer.empty[(mutable.ArrayBuffer[Rel], mutable.ArrayBuffer[Pub])]
+    def flush(): Unit = if (segment.nonEmpty) { processSegment(segment); segment.clear() }
     var i = 0
     while (i < jobs.size) {
       jobs.get(i) match {
         case Inv(s) =>
+          flush()
           val rc = OwgsNative.updateInvokers(ctx, s.map(_.id.toInt).toArray, s.map(_.id.userMemory.toBytes).toArray,
             s.map(h => statusCode(h.status)).toArray)
           if (rc < 0) logging.error(this, s"updateInvokers: ${nativeError("owgs_update_invokers", rc).getMessage}")
+          else pools = poolsOf(s)
           i += 1
         case Clu(n) =>
+          flush()
           val rc = OwgsNative.updateCluster(ctx, n)
           if (rc < 0) logging.error(this, s"updateCluster: ${nativeError("owgs_update_cluster", rc).getMessage}")
+          else _clusterSize = math.max(1, n)
           i += 1
         case _ =>
-          // maximal run of releases followed by publishes: one native call each, order preserved
+          // maximal run of releases followed by publishes, order preserved
           val rels = mutable.ArrayBuffer.empty[Rel]
           while (i < jobs.size && jobs.get(i).isInstanceOf[Rel]) { rels += jobs.get(i).asInstanceOf[Rel]; i += 1 }
-          if (rels.nonEmpty) releaseRun(rels)
           val pubs = mutable.ArrayBuffer.empty[Pub]
           while (i < jobs.size && jobs.get(i).isInstanceOf[Pub]) { pubs += jobs.get(i).asInstanceOf[Pub]; i += 1 }
-          if (pubs.nonEmpty) publishRun(pubs)
+          segment += ((rels, pubs))
       }
     }
+    flush()
   }
 
-  /** releaseInvoker (SCPB:327-331) for a run of completions.  What the reference would throw from
-   *  NestedSemaphore.releaseConcurrent / ForcibleSemaphore.release is logged per release (processCompletion's
-   *  future fails there too); a native error fails nothing else. */
-  private def releaseRun(rels: mutable.ArrayBuffer[Rel]): Unit = {
-    val known = rels.filter(r => byKey.contains(r.entry.fullyQualifiedEntityName.asString))
-    val inv = known.map(_.invoker.toInt).toArray
-    val act = known.map(r => byKey(r.entry.fullyQualifiedEntityName.asString)).toArray
-    val flags = new Array[Byte](inv.length)
-    val rc = OwgsNative.releaseBatch(ctx, inv, act, inv.length, flags)
+  /** releaseInvoker (SCPB:327-331) and the schedule() half of publish (SCPB:260-290) for the runs of one segment, in
+   *  one native call.  What the reference would throw from NestedSemaphore.releaseConcurrent / ForcibleSemaphore
+   *  .release is logged per release (processCompletion's future fails there too). */
+  private def processSegment(runs: mutable.ArrayBuffer[(mutable.ArrayBuffer[Rel], mutable.ArrayBuffer[Pub])]): Unit = {
+    // handles first: a publish whose action cannot be registered fails alone
+    val planned = runs.map { case (rels, pubs) =>
+      val known = rels.filter(r => byKey.contains(r.entry.fullyQualifiedEntityName.asString))
+      val ok = pubs.flatMap { p =>
+        val h = handleOf(p.msg.user.namespace.name.asString, p.action.fullyQualifiedName(true),
+          p.action.limits.memory.megabytes, p.action.limits.concurrency.maxConcurrent, p.action.exec.pull)
+        if (h < 0) { p.p.failure(nativeError("owgs_register_actions", h)); None } else Some((p, h))
+      }
+      (known, ok)
+    }
+    val nRuns = planned.length
+    val nRel = planned.map(_._1.length).sum
+    val nPub = planned.map(_._2.length).sum
+    if (nRel + nPub == 0) return
+    bufs.ensure(nRuns, nRel, nPub)
+    val in = bufs.in.asIntBuffer()
+    var acc = 0
+    in.put(0); planned.foreach { case (r, _) => acc += r.length; in.put(acc) }
+    acc = 0
+    in.put(0); planned.foreach { case (_, p) => acc += p.length; in.put(acc) }
+    planned.foreach(_._1.foreach(r => in.put(r.invoker.toInt)))
+    planned.foreach(_._1.foreach(r => in.put(byKey(r.entry.fullyQualifiedEntityName.asString))))
+    planned.foreach(_._2.foreach { case (_, h) => in.put(h) })
+    val seqs = bufs.in.duplicate().order(ByteOrder.nativeOrder())
+    seqs.position(bufs.seqOffset(nRuns, nRel, nPub))
+    val seqBuf = seqs.slice().order(ByteOrder.nativeOrder()).asLongBuffer()
+    planned.foreach(_._2.foreach { case (p, _) => seqBuf.put(p.seq) })
+    val rc = OwgsNative.processBatch(ctx, bufs.in, bufs.out, nRuns, nRel, nPub)
+    val pubsInOrder = planned.flatMap(_._2.map(_._1))
     if (rc < 0) {
-      logging.error(this, s"releaseInvoker: ${nativeError("owgs_release_batch", rc).getMessage}")
-    } else {
-      var k = 0
-      while (k < flags.length) {
-        val f = flags(k)
-        val e = known(k).entry
-        if ((f & 1) != 0) // NS:103: concurrentSlotsMap(actionid) on a missing key
-          logging.error(this, s"releaseInvoker: NoSuchElementException: key not found: ${e.fullyQualifiedEntityName}")
-        if ((f & 2) != 0) // FS:48-50
-          logging.error(this, s"releaseInvoker: Error: Maximum permit count exceeded (invoker ${inv(k)})")
-        k += 1
-      }
+      val e = nativeError("owgs_process_batch", rc)
+      logging.error(this, s"process batch: ${e.getMessage}")
+      pubsInOrder.foreach(_.p.failure(e))
+      return
     }
-  }
-
-  /** The schedule() half of publish (SCPB:260-290) for a run of activations; on a native error every promise of the
-   *  run fails with LoadBalancerException (nothing was acquired: the native call is all-or-nothing). */
-  private def publishRun(pubs: mutable.ArrayBuffer[Pub]): Unit = {
-    val act = new Array[Int](pubs.length)
-    var bad = false
+    val out = bufs.out
+    val mem = pools.memById
     var k = 0
-    while (k < pubs.length) {
-      val p = pubs(k)
-      val h = handleOf(p.msg.user.namespace.name.asString, p.action.fullyQualifiedName(true),
-        p.action.limits.memory.megabytes, p.action.limits.concurrency.maxConcurrent, p.action.exec.pull)
-      if (h < 0) bad = true
-      act(k) = h
+    while (k < nPub) {
+      val p = pubsInOrder(k)
+      val id = out.getInt(4 * k)
+      val overload = (out.get(4 * nPub + k) & 1) != 0
+      if (id >= 0) p.p.success(Some((InvokerInstanceId(id, userMemory = if (id < mem.length) mem(id) else 0.B), overload)))
+      else if (id == -2) // the reference's schedule() throws here (Int.MinValue hash or an id outside invokerSlots)
+        p.p.failure(new IndexOutOfBoundsException(s"schedule: invoker index out of range for activation ${p.msg.activationId}"))
+      else p.p.success(None)
       k += 1
     }
-    if (bad) {
-      // registration failed for some action: fail those promises, schedule the rest in order
-      val (failed, ok) = pubs.zip(act).partition(_._2 < 0)
-      failed.foreach { case (p, h) => p.p.failure(nativeError("owgs_register_actions", h)) }
-      if (ok.nonEmpty) publishRun(ok.map(_._1))
-      return
-    }
-    val out = new Array[Int](act.length)
-    val flags = new Array[Byte](act.length)
-    val rc = OwgsNative.publishBatch(ctx, act, pubs.map(_.seq).toArray, act.length, out, flags)
-    if (rc < 0) {
-      val e = nativeError("owgs_publish_batch", rc)
-      pubs.foreach(_.p.failure(e))
-      return
-    }
-    val mem = invokerMemoryById
-    pubs.zipWithIndex.foreach { case (p, k) =>
-      val id = out(k)
-      val r =
-        if (id >= 0) Some((InvokerInstanceId(id, userMemory = if (id < mem.length) mem(id) else 0.B), (flags(k) & 1) != 0))
-        else None // -1: no invokers; -2: the reference's schedule() would have thrown
-      p.p.success(r)
+    val known = planned.flatMap(_._1)
+    var r = 0
+    while (r < nRel) {
+      val f = out.get(5 * nPub + r)
+      val e = known(r).entry
+      if ((f & 1) != 0) // NS:103: concurrentSlotsMap(actionid) on a missing key
+        logging.error(this, s"releaseInvoker: NoSuchElementException: key not found: ${e.fullyQualifiedEntityName}")
+      if ((f & 2) != 0) // FS:48-50
+        logging.error(this, s"releaseInvoker: Error: Maximum permit count exceeded (invoker ${known(r).invoker.toInt})")
+      r += 1
     }
   }
 
@@ -222,43 +290,60 @@ class GpuShardingContainerPoolBalancer(config: WhiskConfig,
         h
     }
 
+  /** SCPB:169-205: capacity and health gauges of both pools, from the list the engine schedules against. */
+  override protected def emitMetrics() = {
+    super.emitMetrics()
+    val p = pools
+    def usableMb(s: IndexedSeq[InvokerHealth]) =
+      s.foldLeft(0L)((total, curr) => if (curr.status.isUsable) curr.id.userMemory.toMB + total else total)
+    MetricEmitter.emitGaugeMetric(INVOKER_TOTALMEM_BLACKBOX, usableMb(p.blackbox))
+    MetricEmitter.emitGaugeMetric(INVOKER_TOTALMEM_MANAGED, usableMb(p.managed))
+    MetricEmitter.emitGaugeMetric(HEALTHY_INVOKER_MANAGED, p.managed.count(_.status == Healthy))
+    MetricEmitter.emitGaugeMetric(UNHEALTHY_INVOKER_MANAGED, p.managed.count(_.status == Unhealthy))
+    MetricEmitter.emitGaugeMetric(UNRESPONSIVE_INVOKER_MANAGED, p.managed.count(_.status == Unresponsive))
+    MetricEmitter.emitGaugeMetric(OFFLINE_INVOKER_MANAGED, p.managed.count(_.status == Offline))
+    MetricEmitter.emitGaugeMetric(HEALTHY_INVOKER_BLACKBOX, p.blackbox.count(_.status == Healthy))
+    MetricEmitter.emitGaugeMetric(UNHEALTHY_INVOKER_BLACKBOX, p.blackbox.count(_.status == Unhealthy))
+    MetricEmitter.emitGaugeMetric(UNRESPONSIVE_INVOKER_BLACKBOX, p.blackbox.count(_.status == Unresponsive))
+    MetricEmitter.emitGaugeMetric(OFFLINE_INVOKER_BLACKBOX, p.blackbox.count(_.status == Offline))
+  }
+
   // state updates go through the batching thread too, so they are serialized with publishes exactly like the
   // reference's monitor actor serializes updateInvokers / updateCluster (SCPB:210-250)
   private val monitor = actorSystem.actorOf(Props(new Actor {
-    private var members = Set.empty[akka.cluster.Member]
-    override def preStart(): Unit =
-      if (actorSystem.settings.config.getStringList("akka.cluster.seed-nodes").size > 0)
-        akka.cluster.Cluster(actorSystem)
-          .subscribe(self, classOf[akka.cluster.ClusterEvent.MemberEvent], classOf[akka.cluster.ClusterEvent.ReachabilityEvent])
+    override def preStart(): Unit = {
+      cluster.foreach(_.subscribe(self, classOf[MemberEvent], classOf[ReachabilityEvent]))
+    }
+
+    // all members of the cluster that are available
+    var availableMembers = Set.empty[Member]
+
     override def receive: Receive = {
       case CurrentInvokerPoolState(newState) =>
-        invokerList = newState
-        val mem = new Array[ByteSize](if (newState.isEmpty) 0 else newState.map(_.id.toInt).max + 1)
-        java.util.Arrays.fill(mem.asInstanceOf[Array[AnyRef]], 0.B)
-        newState.foreach(h => mem(h.id.toInt) = h.id.userMemory)
-        invokerMemoryById = mem
         queue.put(Inv(newState))
-      case akka.cluster.ClusterEvent.CurrentClusterState(ms, _, _, _, _) =>
-        members = ms.filter(_.status == akka.cluster.MemberStatus.Up)
-        _clusterSize = math.max(1, members.size); queue.put(Clu(members.size))
-      case e: akka.cluster.ClusterEvent.ClusterDomainEvent =>
-        members = e match {
-          case akka.cluster.ClusterEvent.MemberUp(m)          => members + m
-          case akka.cluster.ClusterEvent.ReachableMember(m)   => members + m
-          case akka.cluster.ClusterEvent.MemberRemoved(m, _)  => members - m
-          case akka.cluster.ClusterEvent.UnreachableMember(m) => members - m
-          case _                                             => members
+      case CurrentClusterState(members, _, _, _, _) =>
+        availableMembers = members.filter(_.status == MemberStatus.Up)
+        queue.put(Clu(availableMembers.size))
+      case event: ClusterDomainEvent =>
+        availableMembers = event match {
+          case MemberUp(member)          => availableMembers + member
+          case ReachableMember(member)   => availableMembers + member
+          case MemberRemoved(member, _)  => availableMembers - member
+          case UnreachableMember(member) => availableMembers - member
+          case _                         => availableMembers
         }
-        _clusterSize = math.max(1, members.size); queue.put(Clu(members.size))
+        queue.put(Clu(availableMembers.size))
     }
   }))
 
-  override def invokerHealth(): Future[IndexedSeq[InvokerHealth]] = Future.successful(invokerList)
+  override def invokerHealth(): Future[IndexedSeq[InvokerHealth]] = Future.successful(pools.all)
   override def clusterSize: Int = _clusterSize
 
   /** SCPB:257-317 with the schedule() half (SCPB:260-290) executed natively in batches. */
   override def publish(action: ExecutableWhiskActionMetaData, msg: ActivationMessage)(
     implicit transid: TransactionId): Future[Future[Either[ActivationId, WhiskActivation]]] = {
+    val isBlackboxInvocation = action.exec.pull
+    val actionType = if (!isBlackboxInvocation) "managed" else "blackbox"
     val p = Promise[Option[(InvokerInstanceId, Boolean)]]()
     val s = synchronized { seqNo += 1; seqNo }
     queue.put(Pub(action, msg, s, p))
@@ -266,10 +351,28 @@ class GpuShardingContainerPoolBalancer(config: WhiskConfig,
       case Some((invoker, overload)) =>
         if (overload)
           MetricEmitter.emitCounterMetric(
-            if (action.exec.pull) LoggingMarkers.BLACKBOX_SYSTEM_OVERLOAD else LoggingMarkers.MANAGED_SYSTEM_OVERLOAD)
+            if (isBlackboxInvocation) LoggingMarkers.BLACKBOX_SYSTEM_OVERLOAD else LoggingMarkers.MANAGED_SYSTEM_OVERLOAD)
+        // SCPB:293-301
+        val memoryLimit = action.limits.memory
+        val memoryLimitInfo = if (memoryLimit == MemoryLimit()) { "std" } else { "non-std" }
+        val timeLimit = action.limits.timeout
+        val timeLimitInfo = if (timeLimit == TimeLimit()) { "std" } else { "non-std" }
+        logging.info(
+          this,
+          s"scheduled activation ${msg.activationId}, action '${msg.action.asString}' ($actionType), ns '${msg.user.namespace.name.asString}', mem limit ${memoryLimit.megabytes} MB (${memoryLimitInfo}), time limit ${timeLimit.duration.toMillis} ms (${timeLimitInfo}) to ${invoker}")
         val activationResult = setupActivation(msg, action, invoker)
         sendActivationToInvoker(messageProducer, msg, invoker).map(_ => activationResult)
-      case None => Future.failed(LoadBalancerException("No invokers available"))
+      case None =>
+        // SCPB:305-316: report the state of all invokers of the pool
+        val p = pools
+        val invokersToUse = if (!isBlackboxInvocation) p.managed else p.blackbox
+        val invokerStates = invokersToUse.foldLeft(Map.empty[InvokerState, Int]) { (agg, curr) =>
+          agg + (curr.status -> (agg.getOrElse(curr.status, 0) + 1))
+        }
+        logging.error(
+          this,
+          s"failed to schedule activation ${msg.activationId}, action '${msg.action.asString}' ($actionType), ns '${msg.user.namespace.name.asString}' - invokers to use: $invokerStates")
+        Future.failed(LoadBalancerException("No invokers available"))
     }
   }
 

@@ -73,6 +73,15 @@ extern "C" hipError_t owgs_launch_msg_plan(const OwgsMsgArgs* a, int32_t bits, v
                                            hipStream_t st);
 extern "C" hipError_t owgs_launch_msg_write(const OwgsMsgArgs* a, hipStream_t st);
 extern "C" size_t owgs_engine_lds_bytes(int n_slots, int pool_mode, int n_ids, int nm, int nb, int n_actions);
+// the narrow geometry (owgs_engine_narrow.hip): same ABI, 7 x 32-lane chunks
+extern "C" size_t owgs_engine_lds_bytes_narrow(int n_slots, int pool_mode, int n_ids, int nm, int nb, int n_actions);
+extern "C" hipError_t owgs_launch_prepass_narrow(const OwgsPrepassArgs* a, int32_t* cstart, int64_t max_chunks,
+                                                 hipStream_t s);
+extern "C" hipError_t owgs_launch_engine_narrow(const OwgsEngineArgs* a, hipStream_t s);
+extern "C" hipError_t owgs_launch_engine_multi_narrow(const OwgsEngineArgs* a, int k, hipStream_t s);
+extern "C" hipError_t owgs_launch_engine_multi_dev_narrow(const OwgsEngineArgs* a_host, const OwgsEngineArgs* a_dev,
+                                                          int k, hipStream_t s);
+#define OWGS_WL_NARROW (OWGS_EW * 32)
 extern "C" hipError_t owgs_launch_w_rebuild(const OwgsWRebuildArgs* a, hipStream_t s);
 extern "C" hipError_t owgs_launch_stage_releases(const OwgsStageArgs* a, hipStream_t s);
 extern "C" hipError_t owgs_launch_relmeta(int32_t n, const int32_t* act, const int32_t* act_mem,
@@ -88,9 +97,10 @@ namespace {
 
 // diagnostic environment switches, read once per process (not on every call)
 struct EnvOpts {
-    int opts = 0, cw = 0, deal = -1;
+    int opts = 0, cw = 0, deal = -1, variant = -1;
     bool trace = false;
     EnvOpts() {
+        if (const char* e = getenv("OWGS_VARIANT")) variant = atoi(e);  // force an engine geometry (diagnostics)
         if (const char* o = getenv("OWGS_OPTS")) opts = atoi(o);
         if (const char* e = getenv("OWGS_CW")) cw = atoi(e);
         if (const char* e = getenv("OWGS_DEAL")) deal = atoi(e);
@@ -240,6 +250,7 @@ struct owgs_ctx {
     DevBuf<uint8_t> w_rfl;
     int32_t w_cap = 0, w_live = 0;
     int32_t cw_cache = 0;  // chunk width of the current state and actions (0: recompute)
+    int32_t variant = 0;   // engine geometry: 0 wide chunks, 1 narrow (large pools, owgs_engine_narrow.hip)
     // owgs_process_batch: pinned staging (inputs, outputs) and their device copies
     void* h_pin = nullptr;
     size_t h_pin_bytes = 0;
@@ -359,17 +370,29 @@ static int prepare_actions(owgs_ctx* c) {
     return OWGS_OK;
 }
 
-static size_t lds_need(const owgs_ctx* c, int32_t n_actions) {
-    return owgs_engine_lds_bytes(c->n_slots, c->pool_mode, c->n_ids, c->nm, c->nb, n_actions);
+// Engine geometry for a state: 0 = wide chunks (7 x 56 lanes), 1 = narrow (7 x 32, owgs_engine_narrow.hip) when the
+// wide LDS image does not fit, -1 = neither fits.  Inputs: what the state's slot image would be.
+static int engine_variant(int32_t n_slots, int32_t pool_mode, int32_t n_ids, int32_t nm, int32_t nb) {
+    if (n_slots > OWGS_MAX_SLOTS_CT || nm > (int32_t)OWGS_AM_POS_MASK || nb > (int32_t)OWGS_AM_POS_MASK) return -1;
+    if (owgs_engine_lds_bytes(n_slots, pool_mode, n_ids, nm, nb, 0) <= OWGS_LDS_BYTES) return 0;
+    if (owgs_engine_lds_bytes_narrow(n_slots, pool_mode, n_ids, nm, nb, 0) <= OWGS_LDS_BYTES) return 1;
+    return -1;
 }
 
 static int lds_check(owgs_ctx* c) {
     if (c->n_slots > OWGS_MAX_SLOTS_CT) return c->fail(OWGS_ERANGE, "invoker ids beyond the concurrency-map key range");
     if (c->nm > (int32_t)OWGS_AM_POS_MASK || c->nb > (int32_t)OWGS_AM_POS_MASK)
         return c->fail(OWGS_ERANGE, "pool larger than 32767 positions");
-    if (lds_need(c, (int32_t)c->a_mem.size()) > OWGS_LDS_BYTES)
-        return c->fail(OWGS_ERANGE, "slot + pool + per-action state exceeds the engine's on-chip (LDS) capacity");
+    const int v = engine_variant(c->n_slots, c->pool_mode, c->n_ids, c->nm, c->nb);
+    if (v < 0) return c->fail(OWGS_ERANGE, "slot + pool state exceeds the engine's on-chip (LDS) capacity");
+    c->variant = (env_opts().variant == 1 || (env_opts().variant == 0 && v == 0)) ? env_opts().variant : v;
     return OWGS_OK;
+}
+
+static int32_t variant_wl(const owgs_ctx* c) { return c->variant ? OWGS_WL_NARROW : OWGS_WL; }
+
+static hipError_t launch_engine(const owgs_ctx* c, const OwgsEngineArgs* A, hipStream_t s) {
+    return c->variant ? owgs_launch_engine_narrow(A, s) : owgs_launch_engine(A, s);
 }
 
 static OwgsOvf ovf_args(const owgs_ctx* c) {
@@ -582,6 +605,9 @@ static int run_prepass(owgs_ctx* c, OwgsEngineArgs& A, int32_t n_batches, const 
                        int64_t n_act, hipStream_t s) {
     HIPCHK(c, c->d_rec.reserve((size_t)std::max<int64_t>(n_act, 1)));
     HIPCHK(c, c->d_cstart.reserve((size_t)n_batches + 1));
+    int rv = lds_check(c);  // the engine geometry decides the chunk width and the record layout
+    if (rv) return rv;
+    const int32_t wl = variant_wl(c);
     OwgsPrepassArgs p{};
     p.n_batches = n_batches;
     p.acq_off = acq_off;
@@ -590,7 +616,7 @@ static int run_prepass(owgs_ctx* c, OwgsEngineArgs& A, int32_t n_batches, const 
     p.act_slot = c->d_act_slot.p;
     p.xmeta = c->d_xmeta.p;
     p.xslot = c->d_xslot.p;
-    const int32_t cw = chunk_width(c);
+    const int32_t cw = std::min(chunk_width(c), wl);
     const int64_t max_chunks = n_act / cw + n_batches;
     p.cw = cw;
     A.cw = cw;
@@ -599,10 +625,11 @@ static int run_prepass(owgs_ctx* c, OwgsEngineArgs& A, int32_t n_batches, const 
     // are long (1k invokers, 30 % concurrent: 553 vs 681 ms)
     p.deal = c->nm >= 4096 ? 1 : 2;
     if (env_opts().deal >= 0) p.deal = env_opts().deal;
-    HIPCHK(c, c->d_lix.reserve((size_t)std::max<int64_t>(max_chunks, 1) * OWGS_WL));
+    HIPCHK(c, c->d_lix.reserve((size_t)std::max<int64_t>(max_chunks, 1) * wl));
     p.rec = c->d_rec.p;
     p.lix = c->d_lix.p;
-    HIPCHK(c, owgs_launch_prepass(&p, c->d_cstart.p, max_chunks, s));
+    HIPCHK(c, c->variant ? owgs_launch_prepass_narrow(&p, c->d_cstart.p, max_chunks, s)
+                         : owgs_launch_prepass(&p, c->d_cstart.p, max_chunks, s));
     A.n_batches = n_batches;
     A.acq_off = acq_off;
     A.n_act = n_act;
@@ -637,7 +664,7 @@ static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s, bool launch
     }
     if (!launch) return OWGS_OK;  // owgs_replay_device_multi launches every shard's engine at once
     HIPCHK(c, hipEventRecord(c->ev_engine[0], s));  // brackets exactly the engine launch (owgs_engine_ms)
-    HIPCHK(c, owgs_launch_engine(&A, s));
+    HIPCHK(c, launch_engine(c, &A, s));
     HIPCHK(c, hipEventRecord(c->ev_engine[1], s));
     c->ev_engine_valid = true;
     if (A.trace) {  // diagnostic timeline: raw u64 pairs, [waves][16384][2]
@@ -722,7 +749,7 @@ int owgs_limits(int32_t* max_invokers, int32_t* max_slots) {
     int32_t lo = 0, hi = OWGS_MAX_SLOTS_CT;
     while (lo < hi) {
         const int32_t mid = lo + (hi - lo + 1) / 2;
-        if (owgs_engine_lds_bytes(mid, 0, mid, mid, mid, 0) <= OWGS_LDS_BYTES) lo = mid;
+        if (engine_variant(mid, 0, mid, mid, mid) >= 0) lo = mid;
         else hi = mid - 1;
     }
     if (max_invokers) *max_invokers = lo;
@@ -892,6 +919,13 @@ int owgs_update_invokers(owgs_ctx* c, int32_t n, const int32_t* ids, const int64
     if (blackboxes < 1) blackboxes = 1;
     if (managed > owgs_coprime_max() || blackboxes > owgs_coprime_max())
         return c->fail(OWGS_ERANGE, "pool larger than the step-size kernel's range");
+    {  // validate before mutating: the state this update leads to must fit an engine geometry
+        const int32_t slots = (old_size < new_size && n > c->n_slots) ? n : c->n_slots;
+        bool identity = n <= slots;
+        for (int32_t i = 0; identity && i < n; ++i) identity = ids[i] == i;
+        if (engine_variant(slots, identity ? 0 : 1, n, std::min(managed, n), std::min(blackboxes, n)) < 0)
+            return c->fail(OWGS_ERANGE, "invoker state exceeds the engine's on-chip (LDS) capacity (owgs_limits)");
+    }
     c->ids.assign(ids, ids + n);
     c->mem.assign(user_memory_bytes, user_memory_bytes + n);
     c->status.assign(status, status + n);
@@ -1405,8 +1439,14 @@ int owgs_replay_device_multi(owgs_ctx** cs, int32_t k, const owgs_replay_io* io,
         if (io[i].n_batches <= 0) return cs[i]->fail(OWGS_EINVAL, "multi-shard replay needs batches in every shard");
     }
     hipStream_t hs = stream ? (hipStream_t)stream : cs[0]->stream;
+    bool one_launch = true;  // every shard's engine in one launch needs one geometry and no watched pairs
+    for (int32_t i = 0; i < k; ++i) {
+        const int v = engine_variant(cs[i]->n_slots, cs[i]->pool_mode, cs[i]->n_ids, cs[i]->nm, cs[i]->nb);
+        if (cs[i]->w_cap > 0 || v != engine_variant(cs[0]->n_slots, cs[0]->pool_mode, cs[0]->n_ids, cs[0]->nm, cs[0]->nb))
+            one_launch = false;
+    }
     for (int32_t i = 0; i < k; ++i)
-        if (cs[i]->w_cap > 0) {  // a shard in watch mode replays batch by batch: every shard on its own
+        if (!one_launch) {  // a shard in watch mode replays batch by batch (or geometries differ): every shard on its own
             for (int32_t j = 0; j < k; ++j) {
                 const owgs_replay_io& x = io[j];
                 int rc = owgs_replay_device(cs[j], x.n_batches, x.acq_off, x.act, x.n_activations, x.rel_off,
@@ -1425,7 +1465,8 @@ int owgs_replay_device_multi(owgs_ctx** cs, int32_t k, const owgs_replay_io* io,
     }
     for (int32_t i = 0; i < k; ++i) HIPCHK(cs[i], hipEventRecord(cs[i]->ev_engine[0], hs));
     if (k <= OWGS_MULTI_MAX) {
-        HIPCHK(cs[0], owgs_launch_engine_multi(A.data(), k, hs));
+        HIPCHK(cs[0], cs[0]->variant ? owgs_launch_engine_multi_narrow(A.data(), k, hs)
+                                     : owgs_launch_engine_multi(A.data(), k, hs));
     } else {  // argument blocks through HBM: the leader context's buffer, staged from its pinned host copy
         owgs_ctx* c0 = cs[0];
         const size_t bytes = (size_t)k * sizeof(OwgsEngineArgs);
@@ -1442,7 +1483,8 @@ int owgs_replay_device_multi(owgs_ctx** cs, int32_t k, const owgs_replay_io* io,
         memcpy(c0->h_margs, A.data(), bytes);
         HIPCHK(c0, c0->d_margs.reserve((bytes + 3) / 4));
         HIPCHK(c0, hipMemcpyAsync(c0->d_margs.p, c0->h_margs, bytes, hipMemcpyHostToDevice, hs));
-        HIPCHK(c0, owgs_launch_engine_multi_dev(A.data(), (const OwgsEngineArgs*)c0->d_margs.p, k, hs));
+        HIPCHK(c0, c0->variant ? owgs_launch_engine_multi_dev_narrow(A.data(), (const OwgsEngineArgs*)c0->d_margs.p, k, hs)
+                               : owgs_launch_engine_multi_dev(A.data(), (const OwgsEngineArgs*)c0->d_margs.p, k, hs));
         HIPCHK(c0, hipEventRecord(c0->ev_margs, hs));
         c0->ev_margs_valid = true;
     }

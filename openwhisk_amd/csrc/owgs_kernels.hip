@@ -37,6 +37,18 @@
 #include "owgs_internal.h"
 #include "owgs_table.h"
 
+// Engine geometry variants (owgs_engine_narrow.hip): the same source compiled again with narrower chunks inside its own
+// namespace, exporting only the geometry-dependent entry points (engine, pre-pass, LDS layout) under a suffix.
+#ifdef OWGS_VARIANT_NS
+#define OWGS_SHARED 0
+namespace OWGS_VARIANT_NS {
+#else
+#define OWGS_SHARED 1
+#endif
+#ifndef OWGS_GEOM
+#define OWGS_GEOM(name) name
+#endif
+
 typedef unsigned long long u64;
 
 #define K_NONE 0
@@ -459,7 +471,7 @@ __host__ __device__ inline OwgsLayout owgs_layout(int n_slots, int pool_mode, in
     return L;
 }
 
-extern "C" size_t owgs_engine_lds_bytes(int n_slots, int pool_mode, int n_ids, int nm, int nb, int n_actions) {
+extern "C" size_t OWGS_GEOM(owgs_engine_lds_bytes)(int n_slots, int pool_mode, int n_ids, int nm, int nb, int n_actions) {
     return owgs_layout(n_slots, pool_mode, n_ids, nm, nb, n_actions).total;
 }
 
@@ -3179,32 +3191,40 @@ __global__ __launch_bounds__(64) void owgs_selftest_kernel(int* bad, int trials)
 }
 
 // ------------------------------------------------------------------------------------------------ launchers
+#if OWGS_SHARED
 extern "C" hipError_t owgs_launch_selftest(int* bad, int trials, hipStream_t s) {
     hipLaunchKernelGGL(owgs_selftest_kernel, dim3(1), dim3(64), 0, s, bad, trials);
     return hipGetLastError();
 }
+#endif
 
+#if OWGS_SHARED
 extern "C" hipError_t owgs_launch_hash(const OwgsHashArgs* a, hipStream_t s) {
     if (a->n <= 0) return hipSuccess;
     const int blocks = (a->n * 64 + 255) / 256;
     hipLaunchKernelGGL(owgs_hash_kernel, dim3(blocks), dim3(256), 0, s, *a);
     return hipGetLastError();
 }
+#endif
 
+#if OWGS_SHARED
 extern "C" hipError_t owgs_launch_lookup(const OwgsLookupArgs* a, hipStream_t s) {
     if (a->n <= 0) return hipSuccess;
     hipLaunchKernelGGL(owgs_lookup_kernel, dim3((a->n + 255) / 256), dim3(256), 0, s, *a);
     return hipGetLastError();
 }
+#endif
 
+#if OWGS_SHARED
 extern "C" hipError_t owgs_launch_prepare(const OwgsPrepArgs* a, hipStream_t s) {
     if (a->n <= 0) return hipSuccess;
     hipLaunchKernelGGL(owgs_prepare_kernel, dim3((a->n + 255) / 256), dim3(256), 0, s, *a);
     return hipGetLastError();
 }
+#endif
 
 // chunk table + per-activation records; max_chunks >= sum of ceil(n_b / OWGS_WL)
-extern "C" hipError_t owgs_launch_prepass(const OwgsPrepassArgs* a, int32_t* cstart, int64_t max_chunks,
+extern "C" hipError_t OWGS_GEOM(owgs_launch_prepass)(const OwgsPrepassArgs* a, int32_t* cstart, int64_t max_chunks,
                                           hipStream_t s) {
     hipLaunchKernelGGL(owgs_chunks_kernel, dim3(1), dim3(64), 0, s, a->acq_off, a->n_batches, a->cw, cstart);
     if (max_chunks <= 0) return hipGetLastError();
@@ -3229,6 +3249,7 @@ __global__ __launch_bounds__(256) void owgs_ovf_rehash_kernel(const uint2* old_t
     if (ovf_insert(O, e.x, e.y) < 0) atomicOr(err, OWGS_ERR_CTAB_FULL);
     else atomicAdd(O.cnt, 1);
 }
+#if OWGS_SHARED
 extern "C" hipError_t owgs_launch_ovf_clear(const OwgsOvf* O, hipStream_t s) {
     if (O->cap <= 0) return hipSuccess;
     hipLaunchKernelGGL(owgs_ovf_clear_kernel, dim3((unsigned)std::min<int64_t>(1024, (O->cap + 255) / 256)), dim3(256),
@@ -3237,6 +3258,8 @@ extern "C" hipError_t owgs_launch_ovf_clear(const OwgsOvf* O, hipStream_t s) {
     if (e == hipSuccess) e = hipMemsetAsync(O->cnt, 0, sizeof(int32_t), s);
     return e;
 }
+#endif
+#if OWGS_SHARED
 extern "C" hipError_t owgs_launch_ovf_rehash(const uint2* old_t, int32_t old_cap, const OwgsOvf* O, int32_t* err,
                                             hipStream_t s) {
     if (old_cap > 0)
@@ -3244,13 +3267,17 @@ extern "C" hipError_t owgs_launch_ovf_rehash(const uint2* old_t, int32_t old_cap
                            old_cap, *O, err);
     return hipGetLastError();
 }
+#endif
 
+#if OWGS_SHARED
 extern "C" hipError_t owgs_launch_relpos(const OwgsRelposArgs* a, hipStream_t s) {
     if (a->n_rel > 0 && a->n_batches > 0)
         hipLaunchKernelGGL(owgs_relpos_kernel, dim3((unsigned)((a->n_rel + RP_T - 1) / RP_T)), dim3(RP_T), 0, s, *a);
     return hipGetLastError();
 }
+#endif
 
+#if OWGS_SHARED
 extern "C" hipError_t owgs_launch_relflags(const int64_t* rel_aid, int64_t n_rel, const int32_t* out_inv,
                                            uint8_t* rel_flags, hipStream_t s) {
     if (n_rel <= 0) return hipSuccess;
@@ -3258,9 +3285,11 @@ extern "C" hipError_t owgs_launch_relflags(const int64_t* rel_aid, int64_t n_rel
                        out_inv, rel_flags);
     return hipGetLastError();
 }
+#endif
 
 #define REL_KEY_BITS 13  // entry keys 0..OWGS_CTC (4096 = no entry)
 
+#if OWGS_SHARED
 extern "C" size_t owgs_release_scratch_bytes(int32_t n) {
     size_t b = 0, c = 0;
     (void)hipcub::DeviceSelect::Flagged(nullptr, b, hipcub::CountingInputIterator<int32_t>(0), (const uint8_t*)nullptr,
@@ -3269,7 +3298,9 @@ extern "C" size_t owgs_release_scratch_bytes(int32_t n) {
                                              (const int32_t*)nullptr, (int32_t*)nullptr, n, 0, REL_KEY_BITS);
     return b > c ? b : c;
 }
+#endif
 
+#if OWGS_SHARED
 extern "C" hipError_t owgs_launch_release_seq(const OwgsReleaseArgs* a, hipStream_t s) {
     const OwgsReleaseArgs& R = *a;
     hipError_t e = hipMemsetAsync(R.bound, 0, (size_t)std::max(R.n_slots, 1) * 8, s);
@@ -3298,6 +3329,7 @@ extern "C" hipError_t owgs_launch_release_seq(const OwgsReleaseArgs* a, hipStrea
     hipLaunchKernelGGL(owgs_release_seq_kernel, dim3(1), dim3(64), 0, s, *a);
     return hipGetLastError();
 }
+#endif
 
 // the engine's dynamic-LDS limit, set once per (kernel, device): the attribute is per device, and a process may drive
 // contexts on several devices
@@ -3313,12 +3345,12 @@ static hipError_t lds_attr(const void* fn, int which) {
     return e;
 }
 
-extern "C" hipError_t owgs_launch_engine_multi_dev(const OwgsEngineArgs* a_host, const OwgsEngineArgs* a_dev, int k,
+extern "C" hipError_t OWGS_GEOM(owgs_launch_engine_multi_dev)(const OwgsEngineArgs* a_host, const OwgsEngineArgs* a_dev, int k,
                                                    hipStream_t s) {
     if (k < 1 || k > OWGS_MULTI_DEV_MAX) return hipErrorInvalidValue;
     size_t lds = 0;
     for (int i = 0; i < k; ++i)
-        lds = std::max(lds, owgs_engine_lds_bytes(a_host[i].n_slots, a_host[i].pool_mode, a_host[i].n_ids,
+        lds = std::max(lds, OWGS_GEOM(owgs_engine_lds_bytes)(a_host[i].n_slots, a_host[i].pool_mode, a_host[i].n_ids,
                                                   a_host[i].nm, a_host[i].nb, a_host[i].n_actions));
     if (lds > OWGS_LDS_BYTES) return hipErrorInvalidValue;
     const hipError_t ea = lds_attr((const void*)owgs_engine_multi_dev_kernel, 0);
@@ -3327,12 +3359,12 @@ extern "C" hipError_t owgs_launch_engine_multi_dev(const OwgsEngineArgs* a_host,
     return hipGetLastError();
 }
 
-extern "C" hipError_t owgs_launch_engine_multi(const OwgsEngineArgs* a, int k, hipStream_t s) {
+extern "C" hipError_t OWGS_GEOM(owgs_launch_engine_multi)(const OwgsEngineArgs* a, int k, hipStream_t s) {
     if (k < 1 || k > OWGS_MULTI_MAX) return hipErrorInvalidValue;
     size_t lds = 0;
     OwgsEngineMulti M;
     for (int i = 0; i < k; ++i) {
-        lds = std::max(lds, owgs_engine_lds_bytes(a[i].n_slots, a[i].pool_mode, a[i].n_ids, a[i].nm, a[i].nb,
+        lds = std::max(lds, OWGS_GEOM(owgs_engine_lds_bytes)(a[i].n_slots, a[i].pool_mode, a[i].n_ids, a[i].nm, a[i].nb,
                                                   a[i].n_actions));
         M.a[i] = a[i];
     }
@@ -3343,8 +3375,8 @@ extern "C" hipError_t owgs_launch_engine_multi(const OwgsEngineArgs* a, int k, h
     return hipGetLastError();
 }
 
-extern "C" hipError_t owgs_launch_engine(const OwgsEngineArgs* a, hipStream_t s) {
-    const size_t lds = owgs_engine_lds_bytes(a->n_slots, a->pool_mode, a->n_ids, a->nm, a->nb, a->n_actions);
+extern "C" hipError_t OWGS_GEOM(owgs_launch_engine)(const OwgsEngineArgs* a, hipStream_t s) {
+    const size_t lds = OWGS_GEOM(owgs_engine_lds_bytes)(a->n_slots, a->pool_mode, a->n_ids, a->nm, a->nb, a->n_actions);
     if (lds > OWGS_LDS_BYTES) return hipErrorInvalidValue;
     const hipError_t ea = lds_attr((const void*)owgs_engine_kernel, 2);
     if (ea != hipSuccess) return ea;
@@ -3353,3 +3385,7 @@ extern "C" hipError_t owgs_launch_engine(const OwgsEngineArgs* a, hipStream_t s)
     hipLaunchKernelGGL(owgs_engine_kernel, dim3(1), dim3(OWGS_NT), lds, s, M);
     return hipGetLastError();
 }
+
+#ifdef OWGS_VARIANT_NS
+}  // namespace OWGS_VARIANT_NS
+#endif

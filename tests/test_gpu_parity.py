@@ -474,3 +474,37 @@ def test_concurrency_map_beyond_the_primary_table(kw):
             assert o == g, (inv, k, o, g)
             checked += o is not None
     assert checked > 0
+
+
+# ----------------------------------------------------------------------------------------------- large pools
+@pytest.mark.parametrize("n_inv", [15_000, 20_000])
+def test_large_pool_stream_parity(n_inv):
+    """More invoker ids than the wide engine's LDS image holds (~12.9k): the context switches to the narrow geometry
+    (7 x 32-lane chunks, owgs_engine_narrow.hip) and stays bit-exact with the oracle (SCPB:512-551 has no cap)."""
+    w = W.config("headline", n_invokers=n_inv, n_activations=150_000)
+    b, _, _ = check_stream(w)
+    assert b.stats()["passes"] > 0
+
+
+def test_rejected_update_leaves_the_context_unchanged():
+    """owgs_update_invokers validates the state it would build before changing anything: a pool beyond owgs_limits
+    is refused with OWGS_ERANGE and the context keeps scheduling exactly as before (same permits, same pools)."""
+    import ctypes as C
+    from openwhisk_amd import _lib
+    from openwhisk_amd._lib import OwgsError
+    mx, ms = C.c_int32(), C.c_int32()
+    _lib.lib().owgs_limits(C.byref(mx), C.byref(ms))
+    w = W.config("headline", n_invokers=2000, n_activations=40_000)
+    b = gpu_for(w)
+    before = (b.permits().copy(), b.managed_size, b.blackbox_size, b.cluster_size, b.managed_step_sizes)
+    n = mx.value + 1000
+    with pytest.raises(OwgsError) as e:
+        b.update_invokers_arrays(np.arange(n, dtype=np.int32), np.full(n, 16384 * MB, np.int64), np.zeros(n, np.uint8))
+    assert e.value.code == -34  # OWGS_ERANGE
+    after = (b.permits(), b.managed_size, b.blackbox_size, b.cluster_size, b.managed_step_sizes)
+    assert np.array_equal(before[0], after[0]) and before[1:] == after[1:]
+    st = O.state_for(w, zombies=False)
+    o_inv, o_fl, o_rf = st.replay(w.stream)
+    g_inv, g_fl, g_rf = b.replay(w.stream)
+    assert np.array_equal(o_inv, g_inv) and np.array_equal(o_fl, g_fl) and np.array_equal(o_rf, g_rf)
+    assert np.array_equal(st.permits(), b.permits())
