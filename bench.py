@@ -53,6 +53,9 @@ def parse(argv=None):
     ap.add_argument("--no-h2d", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-shim-path", action="store_true", help="skip the shim-path leg (per-call latency)")
+    ap.add_argument("--health-churn", action="store_true",
+                    help="N = 1: replay batch by batch with the per-batch health schedule of the N > 1 runs "
+                         "(cluster.health_schedule) instead of one launch per step")
     ap.add_argument("--slots", choices=("split", "weak"), default="split",
                     help="'split' (default): 16 GiB invokers, each controller's slot = 1/clusterSize of them "
                          "(configs[4]); 'weak': invoker memory 16 GiB x clusterSize so every slot stays 16 GiB")
@@ -317,13 +320,19 @@ def dry_run(args):
     n_ctl, shards = cluster_geometry(args, rank, world)
     ws = [shard_workload(args, g, n_ctl) for g in shards]
     hx = cluster.HealthExchange(dist, torch.from_numpy(ws[0].inv_status.copy()), world)
+    health = [torch.from_numpy(h) for h in cluster.health_schedule(ws[0].inv_status, ws[0].stream.n_batches)]
     t0 = time.perf_counter()
+    n_gather = 0
     for _ in range(args.steps):
-        hx.exchange()
+        for h in health:  # the configs[4] cadence: one all-gather between batches
+            agreed = hx.exchange(h)
+            assert torch.equal(agreed, h)
+            n_gather += 1
     t_step = (time.perf_counter() - t0) / max(args.steps, 1)
     t_step, = cluster.max_over_ranks(dist, [t_step], torch.device("cpu"))
     if rank == 0:
         print(json.dumps({"metric": "dry run", "value": None, "n_gpus": world, "dry_run": True,
+                          "health_allgathers_per_step": n_gather / max(args.steps, 1),
                           "config": {"workload": args.config, "cluster_size": n_ctl, "slots": args.slots,
                                      "slot_mb": int(ws[0].info["slot_mb"]), "shards": shards,
                                      "health_disagree": hx.disagreeing_ranks(), "ms_per_step": t_step * 1e3}}),
@@ -400,15 +409,40 @@ def main():
                                  self.d_rel.data_ptr(), self.d_aid.data_ptr(), len(s.rel_aid), s.seq_base,
                                  self.d_out.data_ptr(), self.d_fl.data_ptr(), self.d_rf.data_ptr(), self.sp)
 
+        def replay_batches(self, hx, timing=None):
+            """configs[4] cadence: before each batch the shards all-gather their health view (the health topic,
+            SCPB:355) and apply the agreed vector (owgs_update_health_device -> updateInvokers, SCPB:512-551); the
+            batch is one engine launch (owgs_replay_device_span)."""
+            s, b = self.s, self.b
+            b.restore(self.sp)
+            for k in range(s.n_batches):
+                h = hx.exchange(self.d_health[k])
+                b.update_health_device(len(self.w.inv_status), h.data_ptr(), self.sp)
+                b.replay_device_span(s.acq_off[k], s.acq_off[k + 1], s.rel_off[k], s.rel_off[k + 1],
+                                     self.d_act.data_ptr(), self.d_aid.data_ptr(), s.seq_base, self.d_out.data_ptr(),
+                                     self.d_fl.data_ptr(), self.d_rf.data_ptr(), self.sp)
+                if timing is not None:
+                    timing.append(b.engine_ms())
+
     shards = [Shard(g, k % MULTI_MAX == 0) for k, g in enumerate(shard_ids)]
     w, s, b = shards[0].w, shards[0].s, shards[0].b
     hx = cluster.HealthExchange(dist, torch.from_numpy(w.inv_status.copy()).to(dev), world)
+    # health between batches (configs[4]) for one shard per GPU; several shards per GPU keep one exchange per step
+    per_batch = K == 1 and (world > 1 or args.health_churn)
+    if per_batch:
+        health = cluster.health_schedule(w.inv_status, s.n_batches)
+        shards[0].health = health
+        shards[0].d_health = [t(health[k], np.uint8) for k in range(s.n_batches)]
     torch.cuda.synchronize()
     stream = shards[0].stream
     torch.cuda.set_stream(stream)
     n_gathers = [0]
 
-    def launch_all():
+    def launch_all(timing=None):
+        if per_batch:
+            shards[0].replay_batches(hx, timing)
+            n_gathers[0] += s.n_batches if world > 1 else 0
+            return
         h = None
         if world > 1:  # the health topic every controller consumes (SCPB:355): one all-gather per step
             h = hx.exchange()
@@ -456,6 +490,11 @@ def main():
     # read after instrumented replays outside the timed region (reading them inside would add a sync per step)
     eng = []
     for _ in range(max(3, min(args.steps, 5))):
+        if per_batch:  # one engine launch per batch: their durations add up to the step's kernel time
+            tm = []
+            launch_all(tm)
+            eng.append(float(np.sum(tm)))
+            continue
         launch_all()
         eng.append(float(np.mean([sh.b.engine_ms() for sh in shards[::MULTI_MAX]])))
     kern_ms = float(np.mean(eng))
@@ -468,7 +507,10 @@ def main():
 
         for sh in shards:
             st = O.state_for(sh.w)
-            o_inv, o_fl, o_rf = st.replay(sh.s)
+            if per_batch:  # the same health vector before each batch (every rank agreed: checked below)
+                o_inv, o_fl, o_rf = O.replay_with_health(st, sh.s, sh.w.inv_ids, sh.w.inv_mem, sh.health)
+            else:
+                o_inv, o_fl, o_rf = st.replay(sh.s)
             if o_ref is None:
                 o_ref = o_inv
             exact = exact and (np.array_equal(o_inv, sh.d_out.cpu().numpy())
@@ -479,7 +521,7 @@ def main():
     # host buffers through the C ABI (owgs_replay: argument checks, H2D of the stream, replay, D2H of the decisions):
     # the rate a JVM caller handing over host arrays would see; never the bench value
     h2d_ms = 0.0
-    if not args.no_h2d:
+    if not args.no_h2d and not per_batch:
         reps = 3
         torch.cuda.synchronize()
         t1 = time.perf_counter()
@@ -495,8 +537,9 @@ def main():
 
     n_dec = sum(len(sh.s.act) for sh in shards)  # this rank's decisions per step
     t_step = wall / args.steps
-    t_step, bad, kern_ms, replay_ms, h2d_ms = cluster.max_over_ranks(
-        dist, [t_step, 0.0 if exact else 1.0, kern_ms, replay_ms, h2d_ms], dev)
+    disagree = float(len(hx.disagreeing_ranks())) if per_batch else 0.0
+    t_step, bad, kern_ms, replay_ms, h2d_ms, disagree = cluster.max_over_ranks(
+        dist, [t_step, 0.0 if exact else 1.0, kern_ms, replay_ms, h2d_ms, disagree], dev)
     exact = bad == 0.0
     value = cluster.whole_job_rate(n_dec, world, t_step)
     algo = algorithmic_bytes(w)
@@ -527,6 +570,10 @@ def main():
                        "cluster_size": n_ctl, "slots": args.slots, "shards": shard_ids if world == 1 else None,
                        "invoker_memory_mb": int(w.inv_mem[0] // (1 << 20)), "slot_mb": int(w.info["slot_mb"]),
                        "health_allgathers_per_step": gathers_per_step,
+                       "health": ("per batch: all-gathered, applied with owgs_update_health_device, "
+                                  f"{s.n_batches} engine launches per step (1 % of invokers unresponsive, changing "
+                                  "every batch)") if per_batch else "static, one exchange per step",
+                       "health_disagreeing_ranks": int(disagree),
                        "parallelism": f"{n_ctl} controller shard(s), {K} per GPU, {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,

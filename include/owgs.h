@@ -160,6 +160,15 @@ int owgs_pairwise_coprime(owgs_ctx* ctx, int32_t x, int32_t* out, int32_t cap, i
 int owgs_replay_device(owgs_ctx* ctx, int32_t n_batches, const int64_t* acq_off, const int32_t* act,
                        int64_t n_activations, const int64_t* rel_off, const int64_t* rel_aid, int64_t n_releases,
                        uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, uint8_t* rel_flags, void* stream);
+/* One batch of a stream replayed batch by batch, so that state updates can come in between (configs[4]: the health
+ * all-gather between batches feeding owgs_update_health_device, i.e. updateInvokers, SCPB:512-551): releases
+ * rel_aid[r_beg, r_end) -- activations of this stream decided by EARLIER calls, their invoker read from out_invoker --
+ * then publishes act[a_beg, a_end) with seq = seq_base + i; every index is into the whole stream's arrays (device
+ * pointers).  Same results as the batch inside one owgs_replay_device call of the whole stream with the same state
+ * updates between batches.  Asynchronous on `stream`. */
+int owgs_replay_device_span(owgs_ctx* ctx, int64_t a_beg, int64_t a_end, int64_t r_beg, int64_t r_end,
+                            const int32_t* act, const int64_t* rel_aid, uint64_t seq_base, int32_t* out_invoker,
+                            uint8_t* out_flags, uint8_t* rel_flags, void* stream);
 /* Several controller shards (clusterSize > 1, one context each, same device) replayed by ONE engine launch, one
  * workgroup per shard: the reference runs one ShardingContainerPoolBalancer per controller (SCPB:126-133,
  * 485-499); this hosts up to 64 of them on one GPU (up to 8 argument blocks travel in the kernarg segment, more

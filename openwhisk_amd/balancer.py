@@ -411,6 +411,15 @@ class GpuShardingContainerPoolBalancer:
                                              vp(rel_aid), n_rel, seq_base, vp(out_inv), vp(out_flags), vp(rel_flags),
                                              vp(stream)))
 
+    def replay_device_span(self, a_beg, a_end, r_beg, r_end, act, rel_aid, seq_base, out_inv, out_flags, rel_flags,
+                           stream=None):
+        """One batch of a device-resident stream (owgs_replay_device_span): releases rel_aid[r_beg:r_end] of
+        activations decided by earlier calls, then publishes act[a_beg:a_end]; whole-stream device addresses."""
+        vp = lambda x: C.c_void_p(int(x)) if x else None  # noqa: E731
+        self._chk(self._L.owgs_replay_device_span(self._h, int(a_beg), int(a_end), int(r_beg), int(r_end), vp(act),
+                                                  vp(rel_aid), int(seq_base), vp(out_inv), vp(out_flags),
+                                                  vp(rel_flags), vp(stream)))
+
     @staticmethod
     def replay_device_multi(shards, stream=None):
         """Several controller shards in ONE engine launch (owgs_replay_device_multi, one workgroup per shard).

@@ -4,8 +4,11 @@ The reference runs `clusterSize` controllers side by side; each keeps its own Sh
 whose slots hold `1/clusterSize` of every invoker's memory (SCPB:485-507, updateCluster SCPB:561-584) and schedules
 only the activations it receives.  The shards never exchange scheduling state, so the data path has no collective
 (weak scaling).  What the controllers do share is invoker health: every controller consumes the same health topic
-(InvokerPool, SCPB:355-358).  Here that is one all-gather of the health vector per step; a shard adopts rank 0's
-view, which equals its own when the views agree (they do unless a health ping is in flight).
+(InvokerPool, SCPB:355-358).  Here that is one all-gather of the health vector between batches (configs[4]: "health
+all-gathered every batch"); a shard adopts rank 0's view, which equals its own when the views agree (they do unless a
+health ping is in flight), and applies it through owgs_update_health_device (updateInvokers, SCPB:512-551) before the
+batch's releases and publishes.  `health_schedule` gives every batch its own vector (a changing set of unresponsive
+invokers), the same on every shard.
 
 Works with any torch.distributed backend: RCCL ("nccl") on the GPUs, gloo on the CPU (tests/test_distributed.py).
 """
@@ -39,12 +42,14 @@ class HealthExchange:
         self.flat = torch.empty(world * health.numel(), dtype=health.dtype, device=health.device)
         self.gathered = self.flat.view(world, health.numel())
 
-    def exchange(self):
-        """Returns the agreed health vector (rank 0's row) as a tensor on the health device."""
+    def exchange(self, view=None):
+        """All-gathers this shard's health view (default: the initial vector) and returns the agreed one (rank 0's
+        row) as a tensor on the health device."""
+        v = self.health if view is None else view
         if self.world > 1:
-            self.dist.all_gather_into_tensor(self.flat, self.health)
+            self.dist.all_gather_into_tensor(self.flat, v)
         else:
-            self.gathered[0].copy_(self.health)
+            self.gathered[0].copy_(v)
         return self.gathered[0]
 
     def disagreeing_ranks(self) -> list[int]:
@@ -66,3 +71,18 @@ def max_over_ranks(dist, values, device) -> list[float]:
 def whole_job_rate(n_per_shard: int, world: int, t_step_max: float) -> float:
     """Weak-scaling throughput: all shards' decisions divided by the slowest shard's step time."""
     return world * n_per_shard / t_step_max
+
+
+def health_schedule(inv_status, n_batches: int, churn: float = 0.01, seed: int = 0xC4A17) -> np.ndarray:
+    """Invoker health per batch [n_batches, n_invokers] (InvokerState codes): the cluster's vector with, in every batch
+    after the first, a different `churn` fraction of the invokers Unresponsive (pings lost, InvokerSupervision.scala:
+    339-365) -- the same on every controller shard, as the health topic is."""
+    from .balancer import UNRESPONSIVE
+
+    base = np.asarray(inv_status, dtype=np.uint8)
+    out = np.repeat(base[None, :], max(n_batches, 1), axis=0)
+    n = len(base)
+    for b in range(1, n_batches):
+        rng = np.random.Generator(np.random.PCG64([seed, b]))
+        out[b, rng.choice(n, size=max(1, int(churn * n)), replace=False)] = UNRESPONSIVE
+    return out

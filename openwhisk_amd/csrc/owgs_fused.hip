@@ -14,12 +14,21 @@
 // one workgroup per run: class counts, then stable placement by ballot ranks
 __global__ __launch_bounds__(256) void owgs_stage_releases_kernel(OwgsStageArgs a) {
     const int run = blockIdx.x;
-    const int64_t cb = a.rel_off[run], ce = a.rel_off[run + 1];
+    const bool span = a.rel_off == nullptr;
+    const int64_t cb = span ? 0 : a.rel_off[run], ce = span ? a.span_nrel : a.rel_off[run + 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     __shared__ int t0[4], t1[4];
+    if (span && tid == 0) {
+        a.span_off[0] = 0;
+        a.span_off[1] = a.span_npub;
+        a.span_off[2] = 0;
+        a.span_off[3] = a.span_nrel;
+    }
+    auto inv_of = [&](int64_t i) { return span ? a.dec_inv[a.rel_aid[i]] : a.rel_inv[i]; };
+    auto act_of = [&](int64_t i) { return span ? a.dec_act[a.rel_aid[i]] : a.rel_act[i]; };
     auto first_class = [&](int64_t i) {
-        const int inv = a.rel_inv[i];
-        return inv < 0 || inv >= a.n_slots || a.act_maxc[a.rel_act[i]] == 1;
+        const int inv = inv_of(i);
+        return inv < 0 || inv >= a.n_slots || a.act_maxc[act_of(i)] == 1;
     };
     int n0 = 0;
     for (int64_t c = cb; c < ce; c += 256) {
@@ -48,14 +57,14 @@ __global__ __launch_bounds__(256) void owgs_stage_releases_kernel(OwgsStageArgs 
             s1 += t1[w];
         }
         if (valid) {
-            const int inv = a.rel_inv[i], act = a.rel_act[i];
+            const int inv = inv_of(i), act = act_of(i);
             const bool in = inv >= 0 && inv < a.n_slots;
             const int64_t pos = f ? cb + o0 + __popcll(b0 & lt) : cb + n0 + o1 + __popcll(b1 & lt);
             const uint32_t inv15 = in ? (uint32_t)inv : OWGS_RR_NOINV;  // no-op: invokerSlots.lift (SCPB:329)
             a.rel_rec[pos] = make_uint2(inv15 | ((uint32_t)a.act_mem[act] << 15),
                                         (uint32_t)a.act_slot[act] | ((uint32_t)a.act_maxc[act] << 17));
-            a.rel_src[pos] = (int32_t)(i - a.rel_off[0]);
-            a.rel_flags[i - a.rel_off[0]] = inv < 0 ? OWGS_REL_NOENTRY_BIT : 0;  // no ActivationEntry (CLB:278-279)
+            a.rel_src[pos] = (int32_t)i;
+            a.rel_flags[i] = inv < 0 ? OWGS_REL_NOENTRY_BIT : 0;  // no ActivationEntry (CLB:278-279)
         }
         base0 += s0;
         base1 += s1;

@@ -1407,6 +1407,86 @@ static int replay_watch(owgs_ctx* c, int32_t nb, const int64_t* acq_off, const i
     return w_refresh(c, hs);
 }
 
+// One batch of a device-resident stream replayed batch by batch (state updates such as a health change in between):
+// releases rel_aid[r_beg, r_end) of activations decided by earlier calls (invoker in out_invoker), then the publishes
+// act[a_beg, a_end).  The releases are staged as engine records from the earlier decisions, so the batch is one
+// engine launch (owgs_fused.hip span mode); with watched pairs: the exact release kernels + the watch update.
+int owgs_replay_device_span(owgs_ctx* c, int64_t a_beg, int64_t a_end, int64_t r_beg, int64_t r_end, const int32_t* act,
+                            const int64_t* rel_aid, uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags,
+                            uint8_t* rel_flags, void* stream) {
+    if (!c || a_beg < 0 || a_end < a_beg || r_beg < 0 || r_end < r_beg || !act || !out_invoker || !out_flags ||
+        (r_end > r_beg && !rel_aid) || a_end - a_beg >= ((int64_t)1 << 31) || r_end - r_beg >= ((int64_t)1 << 31))
+        return OWGS_EINVAL;
+    if (c->a_mem.empty()) return c->fail(OWGS_ENOENT, "no actions registered");
+    const int64_t na = a_end - a_beg, nr = r_end - r_beg;
+    if (na == 0 && nr == 0) return OWGS_OK;
+    (void)hipSetDevice(c->cfg.device);
+    hipStream_t hs = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(c, c->w_rfl.reserve((size_t)std::max<int64_t>(nr, 1)));
+    uint8_t* rf = rel_flags ? rel_flags + r_beg : c->w_rfl.p;
+    if (c->w_cap > 0) {  // watched pairs: ordered release kernels, one engine launch, the watch update
+        if (nr > 0) {
+            HIPCHK(c, c->w_rel.reserve((size_t)(4 * nr)));
+            int32_t* q = c->w_rel.p;
+            HIPCHK(c, owgs_launch_w_relgather(rel_aid + r_beg, (int32_t)nr, out_invoker, act, c->d_act_mem.p,
+                                              c->d_act_maxc.p, c->d_act_slot.p, q, q + nr, q + 2 * nr, q + 3 * nr, hs));
+            int rs = release_chain(c, (int32_t)nr, q, q + nr, q + 2 * nr, q + 3 * nr, rf, hs);
+            if (rs) return rs;
+        }
+        if (na > 0) {
+            const int64_t offs[2] = {0, na};
+            HIPCHK(c, upload(c->w_off, offs, 2, hs));
+            OwgsEngineArgs A;
+            base_args(c, A);
+            A.seq_base = seq_base + (uint64_t)a_beg;
+            A.out_inv = out_invoker + a_beg;
+            A.out_flags = out_flags + a_beg;
+            int rc = run_prepass(c, A, 1, c->w_off.p, act + a_beg, na, hs);
+            if (!rc) rc = run_engine(c, A, hs);
+            if (!rc) rc = w_update(c, (int32_t)na, act + a_beg, out_invoker + a_beg, out_flags + a_beg, hs);
+            if (rc) return rc;
+        }
+        return w_refresh(c, hs);
+    }
+    HIPCHK(c, c->f_rec.reserve((size_t)nr + 2));
+    HIPCHK(c, c->f_src.reserve((size_t)nr + 1));
+    HIPCHK(c, c->f_cnt.reserve(2));
+    HIPCHK(c, c->w_off.reserve(4));
+    OwgsStageArgs g{};
+    g.n_runs = 1;
+    g.rel_off = nullptr;  // span mode
+    g.rel_aid = rel_aid ? rel_aid + r_beg : nullptr;
+    g.dec_inv = out_invoker;
+    g.dec_act = act;
+    g.span_nrel = nr;
+    g.span_npub = na;
+    g.span_off = c->w_off.p;
+    g.act_mem = c->d_act_mem.p;
+    g.act_maxc = c->d_act_maxc.p;
+    g.act_slot = c->d_act_slot.p;
+    g.n_slots = c->n_slots;
+    g.rel_rec = c->f_rec.p;
+    g.rel_src = c->f_src.p;
+    g.relcnt = c->f_cnt.p;
+    g.rel_flags = rf;
+    HIPCHK(c, owgs_launch_stage_releases(&g, hs));
+    OwgsEngineArgs A;
+    base_args(c, A);
+    A.seq_base = seq_base + (uint64_t)a_beg;
+    A.out_inv = out_invoker + a_beg;
+    A.out_flags = out_flags + a_beg;
+    int rc = run_prepass(c, A, 1, c->w_off.p, act + a_beg, na, hs);
+    if (!rc && nr > 0) {
+        A.rel_off = c->w_off.p + 2;
+        A.relcnt = c->f_cnt.p;
+        A.rel_rec = c->f_rec.p;
+        A.rel_src = c->f_src.p;
+        A.rel_flags = rf;
+    }
+    if (!rc) rc = run_engine(c, A, hs);
+    return rc;
+}
+
 int owgs_replay_device(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const int32_t* act,
                        int64_t n_activations, const int64_t* rel_off, const int64_t* rel_aid, int64_t n_releases,
                        uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, uint8_t* rel_flags, void* stream) {

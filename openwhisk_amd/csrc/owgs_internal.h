@@ -291,6 +291,14 @@ struct OwgsStageArgs {
     int32_t* rel_src;           // out [n_rel]: record position -> release index
     int32_t* relcnt;            // out [2 n_runs]: records of the first class, of the second
     uint8_t* rel_flags;         // out [n_rel]: OWGS_REL_NOENTRY_BIT for invoker < 0, else 0 (the engine adds NoSuch)
+    // span mode (owgs_replay_device_span, one run): rel_off is null, release i names activation rel_aid[i] of the
+    // caller's stream, whose invoker and action are dec_inv[...] / dec_act[...]; span_off receives the engine's
+    // offsets {0, span_npub} (publishes) and {0, n_rel} (releases)
+    const int64_t* rel_aid;
+    const int32_t* dec_inv;
+    const int32_t* dec_act;
+    int64_t span_nrel, span_npub;
+    int64_t* span_off;
 };
 
 // watch kernels (owgs_watch.hip)

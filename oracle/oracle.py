@@ -344,6 +344,25 @@ class BalancerState:
         return out[:n], fl[:n], rf[: len(stream.rel_aid)]
 
 
+def replay_with_health(st: BalancerState, stream, ids, user_memory_bytes, health) -> tuple:
+    """Replay a stream batch by batch with updateInvokers(health[b]) (SCPB:512-551) before batch b: the literal
+    sequential order of the configs[4] cadence (health agreed between batches).  Returns (inv, flags, rel_flags)."""
+    n = len(stream.act)
+    out = np.full(max(n, 1), -9, dtype=np.int32)
+    fl = np.zeros(max(n, 1), dtype=np.uint8)
+    rf = np.zeros(max(len(stream.rel_aid), 1), dtype=np.uint8)
+    acq = np.ascontiguousarray(stream.acq_off, dtype=np.int64)
+    rel = np.ascontiguousarray(stream.rel_off, dtype=np.int64)
+    act = np.ascontiguousarray(stream.act, dtype=np.int32)
+    aid = np.ascontiguousarray(stream.rel_aid if len(stream.rel_aid) else np.zeros(1), dtype=np.int64)
+    for b in range(len(acq) - 1):
+        st.update_invokers(ids, user_memory_bytes, health[b])
+        # one batch of the stream: owo_replay over offset views (absolute indices, earlier decisions in `out`)
+        lib().owo_replay(st.h, 1, _ptr(acq[b:]), _ptr(act), _ptr(rel[b:]), _ptr(aid), int(stream.seq_base), _ptr(out),
+                         _ptr(fl), _ptr(rf))
+    return out[:n], fl[:n], rf[:len(stream.rel_aid)]
+
+
 def state_for(workload, zombies: bool = True, slot_keys: dict | None = None) -> BalancerState:
     """Oracle BalancerState set up like the workload (invokers, cluster size, actions); returns the state.
     Slot keys are interned from action.key (fqn@version) exactly as owgs_register_actions does."""

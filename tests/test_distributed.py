@@ -38,13 +38,20 @@ def _rank_main(rank, world, port, out_dir):
     w = cluster.shard_workload("headline", rank, world, n_activations=N_ACT, **KW)
     health = torch.from_numpy(w.inv_status.copy())
     hx = cluster.HealthExchange(dist, health, world)
-    agreed = hx.exchange().numpy()
+    agreed = hx.exchange().numpy().copy()
     st = O.state_for(w)
     inv, fl, rf = st.replay(w.stream)
+    # configs[4] cadence: each rank all-gathers its health view between batches and applies the agreed vector
+    # (updateInvokers, SCPB:512-551) before the batch; the schedule changes the unresponsive set every batch
+    sched = cluster.health_schedule(w.inv_status, w.stream.n_batches)
+    agreed_b = np.stack([hx.exchange(torch.from_numpy(sched[b])).numpy().copy() for b in range(len(sched))])
+    st2 = O.state_for(w)
+    inv2, fl2, rf2 = O.replay_with_health(st2, w.stream, w.inv_ids, w.inv_mem, agreed_b)
     t_step = 0.010 * (rank + 1)  # synthetic per-rank step times: the max must win
     t_max, = cluster.max_over_ranks(dist, [t_step], torch.device("cpu"))
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), agreed=agreed, disagree=np.array(hx.disagreeing_ranks()),
              inv=inv, fl=fl, rf=rf, permits=st.permits(), act=w.stream.act, t_max=t_max,
+             agreed_b=agreed_b, inv2=inv2, fl2=fl2, rf2=rf2, permits2=st2.permits(),
              rate=cluster.whole_job_rate(len(w.stream.act), world, t_max))
     dist.barrier()
     dist.destroy_process_group()
@@ -106,7 +113,7 @@ def test_bench_launches_its_own_ranks():
 
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "3",
-                          "--n-activations", "5000"], capture_output=True, text=True, timeout=600, env=env)
+                          "--n-activations", "200000"], capture_output=True, text=True, timeout=600, env=env)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
@@ -115,9 +122,35 @@ def test_bench_launches_its_own_ranks():
     assert d["config"]["cluster_size"] == 2 and d["config"]["slots"] == "split"
     assert d["config"]["slot_mb"] == 16_384 // 2  # getInvokerSlot: 16 GiB / clusterSize 2
     assert d["config"]["health_disagree"] == []
+    assert d["health_allgathers_per_step"] > 1  # one all-gather between batches, not one per step
 
 
 def test_max_over_ranks_and_rate(two_ranks):
     for r in two_ranks:
         assert float(r["t_max"]) == pytest.approx(0.020)
         assert float(r["rate"]) == pytest.approx(2 * N_ACT / 0.020)
+
+
+def test_health_change_between_batches_keeps_every_shard_exact(two_ranks):
+    """The per-batch health all-gather: both ranks agree on every batch's vector (the shared health topic), and each
+    rank's replay with that vector applied before every batch equals its shard replayed alone with the schedule --
+    the exchange adds nothing but agreement.  The changing unresponsive sets do change decisions, and normal
+    placements of batch b only go to invokers usable in batch b."""
+    from openwhisk_amd import cluster
+    import oracle as O
+
+    for r in (0, 1):
+        w = cluster.shard_workload("headline", r, 2, n_activations=N_ACT, **KW)
+        sched = cluster.health_schedule(w.inv_status, w.stream.n_batches)
+        assert np.array_equal(two_ranks[r]["agreed_b"], sched)
+        st = O.state_for(w)
+        inv, fl, rf = O.replay_with_health(st, w.stream, w.inv_ids, w.inv_mem, sched)
+        assert np.array_equal(inv, two_ranks[r]["inv2"]) and np.array_equal(fl, two_ranks[r]["fl2"])
+        assert np.array_equal(rf, two_ranks[r]["rf2"]) and np.array_equal(st.permits(), two_ranks[r]["permits2"])
+        assert not np.array_equal(inv, two_ranks[r]["inv"])  # the schedule matters
+        s = w.stream
+        for b in range(s.n_batches):
+            sl = slice(int(s.acq_off[b]), int(s.acq_off[b + 1]))
+            ib, fb = inv[sl], fl[sl]
+            normal = ib[(ib >= 0) & ((fb & 1) == 0)]
+            assert np.all(sched[b][normal] == 0)

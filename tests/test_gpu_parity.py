@@ -508,3 +508,55 @@ def test_rejected_update_leaves_the_context_unchanged():
     g_inv, g_fl, g_rf = b.replay(w.stream)
     assert np.array_equal(o_inv, g_inv) and np.array_equal(o_fl, g_fl) and np.array_equal(o_rf, g_rf)
     assert np.array_equal(st.permits(), b.permits())
+
+
+# ----------------------------------------------------------------------------------------------- per-batch health
+@pytest.mark.parametrize("cluster_at", [None, 3])
+def test_span_replay_with_health_changes_matches_oracle(cluster_at):
+    """configs[4] cadence on one GPU: before every batch the agreed health vector is applied (owgs_update_health_device
+    = updateInvokers, SCPB:512-551) and the batch replays as one owgs_replay_device_span (its releases name activations
+    decided by earlier calls).  Bit-exact with the oracle applying the same vectors between batches; one variant also
+    changes the cluster size mid-stream (updateCluster, SCPB:561-584: watched pairs)."""
+    import torch
+    from openwhisk_amd import cluster
+
+    w = W.config("headline", n_activations=250_000, n_invokers=3000, conc_frac=0.3)
+    s = w.stream
+    sched = cluster.health_schedule(w.inv_status, s.n_batches, churn=0.03)
+    b = gpu_for(w)
+    st = O.state_for(w, zombies=True)
+    dev = torch.device("cuda", 0)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
+    d_act, d_aid = t(s.act, np.int32), t(s.rel_aid, np.int64)
+    d_out = torch.full((len(s.act),), -9, dtype=torch.int32, device=dev)
+    d_fl = torch.zeros(len(s.act), dtype=torch.uint8, device=dev)
+    d_rf = torch.zeros(max(len(s.rel_aid), 1), dtype=torch.uint8, device=dev)
+    d_h = [t(sched[k], np.uint8) for k in range(s.n_batches)]
+    n = len(s.act)
+    o_inv = np.full(n, -9, np.int32)
+    o_fl = np.zeros(n, np.uint8)
+    o_rf = np.zeros(max(len(s.rel_aid), 1), np.uint8)
+    P = O._ptr
+    acq = np.ascontiguousarray(s.acq_off, np.int64)
+    rel = np.ascontiguousarray(s.rel_off, np.int64)
+    act = np.ascontiguousarray(s.act, np.int32)
+    aid = np.ascontiguousarray(s.rel_aid, np.int64)
+    for k in range(s.n_batches):
+        if k == cluster_at:
+            b.update_cluster(2)
+            st.update_cluster(2)
+        b.update_health_device(len(w.inv_status), d_h[k].data_ptr())
+        b.replay_device_span(s.acq_off[k], s.acq_off[k + 1], s.rel_off[k], s.rel_off[k + 1], d_act.data_ptr(),
+                             d_aid.data_ptr(), s.seq_base, d_out.data_ptr(), d_fl.data_ptr(), d_rf.data_ptr())
+        st.update_invokers(w.inv_ids, w.inv_mem, sched[k])
+        O.lib().owo_replay(st.h, 1, P(acq[k:]), P(act), P(rel[k:]), P(aid), int(s.seq_base), P(o_inv), P(o_fl), P(o_rf))
+    torch.cuda.synchronize()
+    g_inv = d_out.cpu().numpy()
+    bad = np.nonzero(g_inv != o_inv)[0]
+    assert len(bad) == 0, f"first mismatch at {bad[:5]}"
+    assert np.array_equal(d_fl.cpu().numpy(), o_fl)
+    assert np.array_equal(d_rf.cpu().numpy()[:len(s.rel_aid)], o_rf[:len(s.rel_aid)])
+    assert np.array_equal(b.permits(), st.permits())
+    if cluster_at is None:  # the schedule matters: a static-health replay decides differently
+        st0 = O.state_for(w, zombies=True)
+        assert not np.array_equal(st0.replay(s)[0], o_inv)
