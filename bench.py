@@ -584,7 +584,7 @@ def main():
                          "algorithmic_bytes": algo["survey"] * per_launch,
                          "algorithmic_def": f"SURVEY 8(d): {B_DECISION} B/decision + {B_RELEASE} B/release",
                          "achieved_stream_bytes": algo["stream"] * per_launch / (kern_ms * 1e-3) / 1e9},
-            "h2d_inclusive": None if args.no_h2d else {
+            "h2d_inclusive": None if (args.no_h2d or per_batch) else {
                 "value": world * n_dec / (h2d_ms * 1e-3), "unit": "decisions/s", "ms_per_step": h2d_ms,
                 "path": "owgs_replay host ABI: host checks + H2D stream + replay + D2H decisions"},
             "shim_path": shim,

@@ -1080,7 +1080,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     } else {
         for (int i = tid; i < nm + nb; i += OWGS_NT) pw[i] = (int16_t)A.pool_words[i];
     }
-    if (tid < SC_N) sc[tid] = ((tid < 4 && tid != SC_IRR) || tid >= SC_CFT) ? OWGS_WL : (tid < 6 ? (int)0x80000000 : 0);
+    if (tid < SC_N) sc[tid] = tid == SC_IRR ? 0 : ((tid < 4 || tid >= SC_CFT) ? OWGS_WL : (tid < 6 ? (int)0x80000000 : 0));
     lds_sync();
     {
         int used = 0;
