@@ -46,7 +46,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="headline", help="headline (= c5 shards for N > 1) | c1 | c2 | c3 | c4")
+    ap.add_argument("--config", default="headline", help="headline (= c5 shards for N > 1) | c1 | c2 | c2_64k | c3 | c4")
     ap.add_argument("--n-activations", type=int, default=None, help="per shard (default: the config's, 1M)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")

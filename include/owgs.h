@@ -156,7 +156,10 @@ int owgs_pairwise_coprime(owgs_ctx* ctx, int32_t x, int32_t* out, int32_t cap, i
  * rel_aid[rel_off[b]..rel_off[b+1]) (ids into this stream; their invoker is this stream's own earlier output),
  * then publishes activations [acq_off[b], acq_off[b+1]) with action act[i] and seq = seq_base + i.
  * n_activations = acq_off[n_batches], n_releases = rel_off[n_batches] (given so no device read is needed).
- * All pointers are device pointers; stream is a hipStream_t (NULL = the context's stream).  Asynchronous. */
+ * All pointers are device pointers; stream is a hipStream_t (NULL = the context's stream).  Asynchronous, with one
+ * exception: when the call's activations could fill the HBM overflow of the NestedSemaphore map past half its capacity
+ * (its upper bound: the entries it holds plus one per activation), the call first synchronises `stream`, reads the
+ * exact entry count back and, if still needed, grows and rehashes the table before launching. */
 int owgs_replay_device(owgs_ctx* ctx, int32_t n_batches, const int64_t* acq_off, const int32_t* act,
                        int64_t n_activations, const int64_t* rel_off, const int64_t* rel_aid, int64_t n_releases,
                        uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, uint8_t* rel_flags, void* stream);
@@ -165,7 +168,7 @@ int owgs_replay_device(owgs_ctx* ctx, int32_t n_batches, const int64_t* acq_off,
  * rel_aid[r_beg, r_end) -- activations of this stream decided by EARLIER calls, their invoker read from out_invoker --
  * then publishes act[a_beg, a_end) with seq = seq_base + i; every index is into the whole stream's arrays (device
  * pointers).  Same results as the batch inside one owgs_replay_device call of the whole stream with the same state
- * updates between batches.  Asynchronous on `stream`. */
+ * updates between batches.  Asynchronous on `stream` (same exception as owgs_replay_device). */
 int owgs_replay_device_span(owgs_ctx* ctx, int64_t a_beg, int64_t a_end, int64_t r_beg, int64_t r_end,
                             const int32_t* act, const int64_t* rel_aid, uint64_t seq_base, int32_t* out_invoker,
                             uint8_t* out_flags, uint8_t* rel_flags, void* stream);
@@ -173,7 +176,8 @@ int owgs_replay_device_span(owgs_ctx* ctx, int64_t a_beg, int64_t a_end, int64_t
  * workgroup per shard: the reference runs one ShardingContainerPoolBalancer per controller (SCPB:126-133,
  * 485-499); this hosts up to 64 of them on one GPU (up to 8 argument blocks travel in the kernarg segment, more
  * through a pinned host buffer and HBM owned by ctxs[0]).  io[i] holds owgs_replay_device's arguments for ctxs[i];
- * every shard needs n_batches > 0.  Same results as k separate owgs_replay_device calls.  Asynchronous on `stream`. */
+ * every shard needs n_batches > 0.  Same results as k separate owgs_replay_device calls.  Asynchronous on `stream`
+ * (same exception as owgs_replay_device, per shard). */
 typedef struct owgs_replay_io {
     int32_t n_batches;
     const int64_t* acq_off;

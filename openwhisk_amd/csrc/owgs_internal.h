@@ -39,8 +39,8 @@
 #define OWGS_EW 7                      // engine waves (+ the I/O wave: two waves per SIMD, 256 VGPRs each)
 #endif
 #ifndef OWGS_LPW
-#define OWGS_LPW 56                    // activations per engine wave (all 64 lanes serve the wave-wide walks; 56 vs 48:
-#endif                                 // headline 32.4 vs 33.5 ms once stops are re-decided inside the pass)
+#define OWGS_LPW 64                    // activations per engine wave (64 vs 56: headline 31.5 vs 32.2 ms, same box;
+#endif                                 // 56 vs 48: 32.4 vs 33.5; the other configs run narrower chunks)
 #define OWGS_ENT (OWGS_EW * 64)        // engine threads
 #define OWGS_WL (OWGS_EW * OWGS_LPW)   // chunk width: activations resolved together (one per engine lane)
 #define OWGS_NT (OWGS_ENT + 64)        // threads: engine waves + one I/O wave

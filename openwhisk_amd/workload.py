@@ -10,7 +10,10 @@ keys (invoking namespace, action), memory limits are drawn per action, a fractio
 Configs (BASELINE.json "configs"):
   c1        10 managed invokers x 2000 MB, one 256 MB action, 10k activations (ShardingContainerPoolBalancerTests
             harness shape, T-SCPB:414-497)
-  c2        1k invokers x 16 GiB, 10k actions / 1k namespaces, Zipf 1.0, 128..2048 MB, 1M activations
+  c2        1k invokers x 16 GiB, 10k actions / 1k namespaces, Zipf 1.0, 128..2048 MB, 1M activations in
+            capacity-calibrated batches (~5.3k: each batch's releases and publishes keep the pool near its capacity)
+  c2_64k    c2 in batches of 64k activations, as SURVEY 8(d) words configs[1]: releases come only between batches, so
+            each batch fills the pool within its first few thousand activations and the rest fall back (SCPB:417-424)
   c3        10k invokers, 10 % unhealthy/offline, 10 % blackbox actions, load 1.2 x capacity (overload fallback)
   c4        c2 + 30 % concurrent actions (maxConcurrent 2..500) with completion releases
   headline  10k invokers x 16 GiB, 1M activations per shard, Zipf 1.0, 128..2048 MB, 10 % blackbox, 20 % concurrent,
@@ -157,6 +160,9 @@ def config(name: str, n_activations: int | None = None, shard: int = 0, n_shards
                     seed=0x0F15C001)
     elif name == "c2":
         base = dict(n_invokers=1000, conc_frac=0.0, blackbox_frac=0.0, unhealthy_frac=0.0, seed=0x0F15C002)
+    elif name == "c2_64k":  # configs[1] in SURVEY 8(d)'s literal batching: 64k activations per batch (overloaded)
+        base = dict(n_invokers=1000, conc_frac=0.0, blackbox_frac=0.0, unhealthy_frac=0.0, seed=0x0F15C002,
+                    batch=65_536)
     elif name == "c3":
         base = dict(n_invokers=10_000, conc_frac=0.0, blackbox_frac=0.1, unhealthy_frac=0.1, load=1.2,
                     seed=0x0F15C003)

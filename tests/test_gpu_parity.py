@@ -261,9 +261,10 @@ def test_headline_full_size_parity_and_determinism():
     assert np.array_equal(g1, g2) and np.array_equal(f1, f2)
 
 
-@pytest.mark.parametrize("name", ["c2", "c3", "c4"])
+@pytest.mark.parametrize("name", ["c2", "c3", "c4", "c2_64k"])
 def test_baseline_configs_full_size_parity(name):
-    # BASELINE.json configs[1..3] at their full sizes (1M activations each), bit-exact with the oracle
+    # BASELINE.json configs[1..3] at their full sizes (1M activations each), bit-exact with the oracle; c2_64k is
+    # configs[1] in SURVEY 8(d)'s literal 64k batches (98 % overload fallbacks)
     check_stream(W.config(name))
 
 
