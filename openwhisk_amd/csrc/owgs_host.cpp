@@ -185,6 +185,16 @@ struct owgs_ctx {
     DevBuf<int32_t> d_ovf_touched, d_ovf_cnt;  // d_ovf_cnt = {entries (live + deleted), touched count}
     int32_t ovf_cap = 0;
     int64_t ovf_used_ub = 0;  // host upper bound of the overflow's entries (exact after a read-back)
+    // the overflow's entry count copied back after an engine launch without waiting (pinned word + event): read when
+    // the bound above runs out, it replaces a stream synchronisation; ovf_since = activations launched after the copy
+    int32_t* h_ovf_cnt = nullptr;
+    hipEvent_t ev_ovf = nullptr;
+    bool ovf_probe = false;
+    int64_t ovf_since = 0;
+    // owgs_update_health_device on identity pools: the status bytes and usable bitmap are updated on the device only;
+    // the host mirror (status, healthy counts) is downloaded when a host path needs it (ev_status: the copy)
+    bool status_stale = false;
+    hipEvent_t ev_status = nullptr;
     int32_t s_ovf_cnt = 0;    // snapshot: overflow entries (0: the snapshot had none)
     int32_t s_ovf_cap = 0;
     DevBuf<uint32_t> d_margs;  // owgs_replay_device_multi: shard argument blocks beyond the kernarg segment
@@ -257,7 +267,7 @@ struct owgs_ctx {
     void* h_pout = nullptr;
     size_t h_pout_bytes = 0;
     DevBuf<uint8_t> d_pin, d_pout;
-    DevBuf<int32_t> f_src, f_cnt;
+    DevBuf<int32_t> f_src, f_cnt, f_tile;
     DevBuf<uint2> f_rec;
     DevBuf<uint32_t> s_w_keys, s_w_vals;
     DevBuf<int32_t> s_w_wkey;
@@ -295,7 +305,19 @@ static hipError_t upload(DevBuf<T>& d, const T* h, size_t n, hipStream_t s) {
 // managed = take(managed), blackbox = takeRight(blackboxes) (SCPB:522-523) -> pool words / usable bitmap, healthy
 // lists.  InvokerPool pads the health list so that position i holds invoker id i (InvokerSupervision.scala:191-207):
 // then pool position p is id p (managed) or N - blackboxes + p (blackbox) and the engine keeps only a usable bitmap.
+// the host mirror of the status bytes after owgs_update_health_device's device-only path
+static int sync_status(owgs_ctx* c) {
+    if (!c->status_stale) return OWGS_OK;
+    HIPCHK(c, hipEventSynchronize(c->ev_status));
+    if (!c->status.empty())
+        HIPCHK(c, hipMemcpy(c->status.data(), c->d_status.p, c->status.size(), hipMemcpyDeviceToHost));
+    c->status_stale = false;
+    return OWGS_OK;
+}
+
 static int rebuild_pools(owgs_ctx* c) {
+    int rs = sync_status(c);
+    if (rs) return rs;
     c->cw_cache = 0;
     std::vector<int32_t> words, hl;
     int32_t cnt[2], hcnt[2];
@@ -411,11 +433,19 @@ static OwgsOvf ovf_args(const owgs_ctx* c) {
 // rehash) when the bound says so -- after reading the exact entry count back once.
 static int ensure_ovf(owgs_ctx* c, int64_t n_new, hipStream_t s) {
     auto need = [&](int64_t used) {
-        int64_t want = 2 * (used + n_new + OWGS_CTC), cap = 16384;
+        // (at least 2^19 entries, 12 MB with its scratch: the per-launch bound then runs out only every ~250k
+        // activations, so a batch-by-batch replay seldom has to read the count back)
+        int64_t want = 2 * (used + n_new + OWGS_CTC), cap = (int64_t)1 << 19;
         while (cap < want && cap < ((int64_t)1 << 30)) cap <<= 1;
         return cap;
     };
     if (c->ovf_cap >= need(c->ovf_used_ub)) return OWGS_OK;
+    if (c->ovf_probe && hipEventQuery(c->ev_ovf) == hipSuccess) {  // a count that arrived meanwhile: no wait
+        c->ovf_probe = false;
+        c->ovf_used_ub = (int64_t)*c->h_ovf_cnt + c->ovf_since;
+        if (c->ovf_cap >= need(c->ovf_used_ub)) return OWGS_OK;
+    }
+    c->ovf_probe = false;
     if (c->ovf_cap > 0) {  // exact entry count
         int32_t cnt = 0;
         HIPCHK(c, hipStreamSynchronize(s));
@@ -457,6 +487,7 @@ static int reset_ctab(owgs_ctx* c) {
         HIPCHK(c, owgs_launch_ovf_clear(&O, c->stream));
     }
     c->ovf_used_ub = 0;
+    c->ovf_probe = false;
     return OWGS_OK;
 }
 
@@ -667,6 +698,18 @@ static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s, bool launch
     HIPCHK(c, launch_engine(c, &A, s));
     HIPCHK(c, hipEventRecord(c->ev_engine[1], s));
     c->ev_engine_valid = true;
+    if (c->ovf_cap > 0) {  // the overflow's entry count for a later ensure_ovf, copied back without a wait
+        if (!c->ovf_probe) {
+            if (!c->h_ovf_cnt) HIPCHK(c, hipHostMalloc((void**)&c->h_ovf_cnt, sizeof(int32_t), hipHostMallocDefault));
+            if (!c->ev_ovf) HIPCHK(c, hipEventCreateWithFlags(&c->ev_ovf, hipEventDisableTiming));
+            HIPCHK(c, hipMemcpyAsync(c->h_ovf_cnt, c->d_ovf_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipEventRecord(c->ev_ovf, s));
+            c->ovf_probe = true;
+            c->ovf_since = 0;
+        } else {
+            c->ovf_since += A.n_act;
+        }
+    }
     if (A.trace) {  // diagnostic timeline: raw u64 pairs, [waves][16384][2]
         HIPCHK(c, hipStreamSynchronize(s));
         std::vector<unsigned long long> h(c->d_trace.n);
@@ -822,6 +865,12 @@ void owgs_destroy(owgs_ctx* c) {
     c->d_ovf_cnt.release();
     if (c->h_margs) (void)hipHostFree(c->h_margs);
     c->h_margs = nullptr;
+    if (c->h_ovf_cnt) (void)hipHostFree(c->h_ovf_cnt);
+    c->h_ovf_cnt = nullptr;
+    if (c->ev_ovf) (void)hipEventDestroy(c->ev_ovf);
+    c->ev_ovf = nullptr;
+    if (c->ev_status) (void)hipEventDestroy(c->ev_status);
+    c->ev_status = nullptr;
     if (c->ev_margs) (void)hipEventDestroy(c->ev_margs);
     c->ev_margs = nullptr;
     c->d_off.release();
@@ -878,6 +927,7 @@ void owgs_destroy(owgs_ctx* c) {
     c->d_pout.release();
     c->f_src.release();
     c->f_cnt.release();
+    c->f_tile.release();
     c->f_rec.release();
     c->r_bound.release();
     c->r_idx.release();
@@ -925,6 +975,10 @@ int owgs_update_invokers(owgs_ctx* c, int32_t n, const int32_t* ids, const int64
         for (int32_t i = 0; identity && i < n; ++i) identity = ids[i] == i;
         if (engine_variant(slots, identity ? 0 : 1, n, std::min(managed, n), std::min(blackboxes, n)) < 0)
             return c->fail(OWGS_ERANGE, "invoker state exceeds the engine's on-chip (LDS) capacity (owgs_limits)");
+    }
+    if (c->status_stale) {  // a device-only health update still in flight must land before the upload below
+        HIPCHK(c, hipEventSynchronize(c->ev_status));
+        c->status_stale = false;
     }
     c->ids.assign(ids, ids + n);
     c->mem.assign(user_memory_bytes, user_memory_bytes + n);
@@ -1469,6 +1523,8 @@ int owgs_replay_device_span(owgs_ctx* c, int64_t a_beg, int64_t a_end, int64_t r
     g.rel_src = c->f_src.p;
     g.relcnt = c->f_cnt.p;
     g.rel_flags = rf;
+    HIPCHK(c, c->f_tile.reserve((size_t)(nr / OWGS_STAGE_TILE + 1)));
+    g.tile_cnt = c->f_tile.p;
     HIPCHK(c, owgs_launch_stage_releases(&g, hs));
     OwgsEngineArgs A;
     base_args(c, A);
@@ -1875,6 +1931,7 @@ int owgs_restore(owgs_ctx* c, void* stream) {
         }
     }
     c->ovf_used_ub = c->s_ovf_cnt;
+    c->ovf_probe = false;
     if (c->w_cap != c->s_w_cap) {  // watched pairs as captured
         w_drop(c);
         if (c->s_w_cap > 0) {
@@ -1899,6 +1956,20 @@ int owgs_restore(owgs_ctx* c, void* stream) {
 int owgs_update_health_device(owgs_ctx* c, int32_t n, const uint8_t* status_dev, void* stream) {
     if (!c || n != (int32_t)c->status.size() || (n > 0 && !status_dev)) return OWGS_EINVAL;
     (void)hipSetDevice(c->cfg.device);
+    if (n && c->pool_mode == 0 && !c->pool_override[0] && !c->pool_override[1] && c->d_status.p && c->d_usable.p) {
+        // identity pools (position = id): health changes only the usable bitmap, and the engine counts the healthy
+        // invokers of each pool from it (the overload fallback's |H|, SCPB:417-424).  Nothing else depends on the
+        // status, so the update stays on the stream: the status bytes, the bitmap, and the host mirror later.
+        hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+        HIPCHK(c, hipMemcpyAsync(c->d_status.p, status_dev, (size_t)n, hipMemcpyDeviceToDevice, s));
+        HIPCHK(c, owgs_launch_usable(c->d_status.p, n, c->d_usable.p, (n + 31) / 32 + 1, s));
+        if (!c->ev_status) HIPCHK(c, hipEventCreateWithFlags(&c->ev_status, hipEventDisableTiming));
+        HIPCHK(c, hipEventRecord(c->ev_status, s));
+        c->status_stale = true;
+        return OWGS_OK;
+    }
+    int rs = sync_status(c);
+    if (rs) return rs;
     if (n) {
         HIPCHK(c, hipMemcpyAsync(c->status.data(), status_dev, (size_t)n, hipMemcpyDeviceToHost,
                                  stream ? (hipStream_t)stream : c->stream));

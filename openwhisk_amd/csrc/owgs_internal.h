@@ -299,7 +299,9 @@ struct OwgsStageArgs {
     const int32_t* dec_act;
     int64_t span_nrel, span_npub;
     int64_t* span_off;
+    int32_t* tile_cnt;          // span mode, more than OWGS_STAGE_TILE releases: first-class records per tile (scratch)
 };
+#define OWGS_STAGE_TILE 1024
 
 // watch kernels (owgs_watch.hip)
 struct OwgsWRebuildArgs {   // at a reset: the new W from the table's entries and the old W

@@ -1194,6 +1194,16 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     lds_sync();
+    // healthy invokers per pool (|H| of the overload fallback, SCPB:417-424): identity pools count them from the
+    // usable bitmap (owgs_update_health_device updates only the bitmap there); other pools take the host's counts
+    int hm_e = A.hm, hb_e = A.hb;
+    if (A.pool_mode == 0) {
+        auto rank = [&](int x) {  // usable ids below x
+            return x <= 0 ? 0 : (int)pc[x >> 5] + ((x & 31) ? __popc(ub[x >> 5] & ((1u << (x & 31)) - 1u)) : 0);
+        };
+        hm_e = rank(nm);
+        hb_e = rank(A.n_ids) - rank(A.n_ids - nb);
+    }
 
     int g = 0;    // global chunk index
     int par = 0;  // pass parity (double-buffered LDS scalars)
@@ -2340,7 +2350,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                 // (the explicit-seq and explicit-pool variants load from HBM; they are kept on their own paths so
                 // that their vmcnt waits never drain the decision stores of the common path)
                 if (spec && kind == K_FALLBACK) {
-                    const int hc = pool ? A.hb : A.hm;
+                    const int hc = pool ? hb_e : hm_e;
 #define OWGS_LAND(X)                                          \
     {                                                         \
         const int x_ = (X);                                   \
@@ -2572,7 +2582,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
 #endif
                             if (!done) break;  // a long walk: the next pass takes this lane
                             if (kn == K_FALLBACK) {
-                                const int hc = pl_ ? A.hb : A.hm;
+                                const int hc = pl_ ? hb_e : hm_e;
                                 if (hc <= 0) break;
                                 // (explicit per-activation sequence numbers: the ordinary path -- a global load here
                                 // would wait for the I/O wave's prefetch stream)
