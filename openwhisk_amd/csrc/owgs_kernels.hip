@@ -562,11 +562,30 @@ __global__ __launch_bounds__(64) void owgs_chunks_kernel(const int64_t* acq_off,
 }
 
 // one workgroup per chunk: occ (earlier lanes of the same action), next lane of the same action, nearest earlier
-// lane with the same slot key and a different action (shared fqn@version), packed with the action meta
+// lane with the same slot key and a different action (shared fqn@version), packed with the action meta.
+// Lanes are grouped by action and by slot key through two small LDS hash tables; each group is identified by its
+// first lane and holds a bit mask of its lanes, so every rank above is a popcount or a bit search over OWGS_WL bits
+// (the all-pairs scans this replaces cost O(chunk) per lane: 70 us for one full chunk, the pre-pass latency of a
+// small shim call).
+#define PP_HT (2 * OWGS_WL)  // hash slots per table (load <= 1/2)
+__device__ __forceinline__ uint32_t pp_hash(int32_t k) { return ((uint32_t)k * 2654435761u) >> 16; }
+// first lane of the group of key k: the entry's key by CAS, then the group's first lane by atomicMin (two phases with
+// a barrier between, done by the caller); returns the table slot
+__device__ __forceinline__ int pp_insert(int32_t* hk, int32_t k) {
+    uint32_t h = pp_hash(k) % PP_HT;
+    for (;;) {
+        const int32_t prev = atomicCAS(&hk[h], (int32_t)0x80000000, k);
+        if (prev == (int32_t)0x80000000 || prev == k) return (int)h;
+        h = h + 1 == PP_HT ? 0 : h + 1;
+    }
+}
+
 __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A) {
-    // (16-byte aligned: the all-pairs scans below read 4 lanes per LDS access; OWGS_WL is a multiple of 4)
+    constexpr int NWR = (OWGS_WL + 63) / 64;
     __shared__ __align__(16) int32_t s_a[OWGS_WL], s_s[OWGS_WL], s_p[OWGS_WL];
-    static_assert(OWGS_WL % 4 == 0, "4-lane reads");
+    __shared__ int32_t hk_a[PP_HT], hl_a[PP_HT], hk_s[PP_HT], hl_s[PP_HT];
+    __shared__ unsigned long long m_a[OWGS_WL][NWR], m_s[OWGS_WL][NWR];  // lane masks, by the group's first lane
+    __shared__ int32_t sh_a[OWGS_WL];  // per action group: some lane has a shared-key lane before it (pk1 != 0)
     const int g = blockIdx.x;
     if (g >= A.cstart[A.n_batches]) return;
     int lo = 0, hi = A.n_batches - 1;  // last batch with cstart[b] <= g
@@ -594,27 +613,56 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
     const int aid = (A.act && t < len) ? a : -1 - t;  // explicit walks: every lane is its own walk
     s_a[t] = aid;
     s_s[t] = slot;
+    for (int i = t; i < PP_HT; i += OWGS_WL) {
+        hk_a[i] = hk_s[i] = (int32_t)0x80000000;
+        hl_a[i] = hl_s[i] = OWGS_WL;
+    }
+    for (int i = t; i < OWGS_WL * NWR; i += OWGS_WL) {
+        (&m_a[0][0])[i] = 0ull;
+        (&m_s[0][0])[i] = 0ull;
+    }
+    sh_a[t] = 0;
     __syncthreads();
-    int occ = 0, next = (int)OWGS_REC_NONEXT, pk1 = 0, cnt = 0, lead = t;
+    int ha = 0, hs_ = 0;
     if (t < len) {
-        // lanes past len hold unique negative ids and slot 0: they match nothing below (j < t < len for pk1)
-        for (int j0 = 0; j0 < len; j0 += 4) {
-            const int4 a4 = *(const int4*)&s_a[j0];
-            const int4 s4 = *(const int4*)&s_s[j0];
-            const int av[4] = {a4.x, a4.y, a4.z, a4.w}, sv[4] = {s4.x, s4.y, s4.z, s4.w};
+        ha = pp_insert(hk_a, aid);
+        hs_ = pp_insert(hk_s, slot);
+    }
+    __syncthreads();
+    if (t < len) {
+        atomicMin(&hl_a[ha], t);
+        atomicMin(&hl_s[hs_], t);
+    }
+    __syncthreads();
+    const int lead = t < len ? hl_a[ha] : t;  // first lane of the chunk with this lane's action
+    const int slead = t < len ? hl_s[hs_] : t;
+    const unsigned long long bit = 1ull << (t & 63);
+    if (t < len) {
+        atomicOr(&m_a[lead][t >> 6], bit);
+        atomicOr(&m_s[slead][t >> 6], bit);
+    }
+    __syncthreads();
+    int occ = 0, next = (int)OWGS_REC_NONEXT, pk1 = 0, cnt = 0;
+    if (t < len) {
+        const int tw = t >> 6;
+        const unsigned long long below = bit - 1ull;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int j = j0 + u, aj = av[u];
-                if (aj == aid) {
-                    ++cnt;
-                    if (j < lead) lead = j;
-                }
-                if (j < t) {
-                    if (aj == aid) ++occ;
-                    else if (sv[u] == slot) pk1 = j + 1;
-                } else if (j > t && aj == aid && next == (int)OWGS_REC_NONEXT) {
-                    next = j;
-                }
+        for (int w = 0; w < NWR; ++w) {
+            const unsigned long long ma = m_a[lead][w];
+            // lanes with the same slot key under another action (the same action implies the same key)
+            const unsigned long long mo = m_s[slead][w] & ~ma;
+            cnt += __popcll(ma);
+            if (w < tw) {
+                occ += __popcll(ma);
+                if (mo) pk1 = 64 * w + 63 - __builtin_clzll(mo) + 1;
+            } else if (w == tw) {
+                occ += __popcll(ma & below);
+                const unsigned long long mb = mo & below;
+                if (mb) pk1 = 64 * w + 63 - __builtin_clzll(mb) + 1;
+                const unsigned long long ab = ma & ~(below | bit);
+                if (ab) next = 64 * w + __builtin_ctzll(ab);
+            } else if (next == (int)OWGS_REC_NONEXT && ma) {
+                next = 64 * w + __builtin_ctzll(ma);
             }
         }
     }
@@ -622,29 +670,26 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
     // their first lane
     const int mc = (int)((meta.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
     s_p[t] = pk1;
+    if (t < len && pk1 != 0) sh_a[lead] = 1;  // (a plain store: every writer writes 1)
     __syncthreads();
-    bool shared = false;
-    if (t < len && mc > 1)
-        for (int j0 = 0; j0 < len; j0 += 4) {
-            const int4 a4 = *(const int4*)&s_a[j0];
-            const int4 p4 = *(const int4*)&s_p[j0];
-            shared = shared || (a4.x == aid && p4.x != 0) || (a4.y == aid && p4.y != 0) || (a4.z == aid && p4.z != 0) ||
-                     (a4.w == aid && p4.w != 0);
-        }
+    const bool shared = t < len && mc > 1 && sh_a[lead] != 0;
     const bool q = t < len && A.act && cnt >= HOT_MIN && !shared && !(meta.y & (OWGS_AM_THROW | OWGS_AM_EMPTY)) &&
                    (mc == 1 || HOT_CONC_ON);
-    __syncthreads();
-    s_s[t] = (q && occ == 0) ? 1 : 0;  // qualifying leaders
+    // qualifying leaders as a lane mask: an action's hot slot = the qualifying leaders before its first lane
+    __shared__ unsigned long long m_q[NWR];
+    {
+        const unsigned long long mq = __ballot(q && occ == 0);
+        if ((t & 63) == 0) m_q[t >> 6] = mq;
+    }
     __syncthreads();
     int hs = OWGS_REC_NOHOT;
     if (q) {
         int k = 0;
-        int j0 = 0;
-        for (; j0 + 4 <= lead; j0 += 4) {
-            const int4 v = *(const int4*)&s_s[j0];
-            k += v.x + v.y + v.z + v.w;
+#pragma unroll
+        for (int w = 0; w < NWR; ++w) {
+            if (w < (lead >> 6)) k += __popcll(m_q[w]);
+            else if (w == (lead >> 6)) k += __popcll(m_q[w] & ((1ull << (lead & 63)) - 1ull));
         }
-        for (; j0 < lead; ++j0) k += s_s[j0];
         if (k < NHOT) hs = k;
     }
     // record position by class: 0 = walks of maxConcurrent == 1 actions, 1 = no walk of its own (hot-table rank,
