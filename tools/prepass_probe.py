@@ -23,3 +23,5 @@ act = w.stream.act
 for k in range(calls):
     b.publish(act[k * n:(k + 1) * n], seq_base=k * n)
 print("done", n, calls)
+if os.environ.get("PROBE_STATS"):
+    print(b.stats())
