@@ -98,8 +98,9 @@ namespace {
 // diagnostic environment switches, read once per process (not on every call)
 struct EnvOpts {
     int opts = 0, cw = 0, deal = -1, variant = -1;
-    bool trace = false;
+    bool trace = false, feat_all = false;
     EnvOpts() {
+        feat_all = getenv("OWGS_FEAT_ALL") != nullptr;  // the general engine for every launch (A/B diagnostics)
         if (const char* e = getenv("OWGS_VARIANT")) variant = atoi(e);  // force an engine geometry (diagnostics)
         if (const char* o = getenv("OWGS_OPTS")) opts = atoi(o);
         if (const char* e = getenv("OWGS_CW")) cw = atoi(e);
@@ -260,6 +261,7 @@ struct owgs_ctx {
     DevBuf<uint8_t> w_rfl;
     int32_t w_cap = 0, w_live = 0;
     int32_t cw_cache = 0;  // chunk width of the current state and actions (0: recompute)
+    bool any_conc = false;  // some registered action has maxConcurrent > 1 (the engine needs its map code)
     int32_t variant = 0;   // engine geometry: 0 wide chunks, 1 narrow (large pools, owgs_engine_narrow.hip)
     // owgs_process_batch: pinned staging (inputs, outputs) and their device copies
     void* h_pin = nullptr;
@@ -672,11 +674,14 @@ static int run_prepass(owgs_ctx* c, OwgsEngineArgs& A, int32_t n_batches, const 
 static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s, bool launch = true) {
     int rc = lds_check(c);
     if (rc) return rc;
-    rc = ensure_ovf(c, A.n_act, s);
-    if (rc) return rc;
+    // the map's overflow exists only for concurrent actions: a context without any never allocates it
+    if (c->any_conc || (A.feat & OWGS_F_CONC)) {
+        rc = ensure_ovf(c, A.n_act, s);
+        if (rc) return rc;
+        c->ovf_used_ub += A.n_act;
+    }
     A.ovf = ovf_args(c);
     A.ct_tmp = c->d_ct_tmp.p;
-    c->ovf_used_ub += A.n_act;
     // walk cursors: one tagged word per action; the tags of this launch's batches must not repeat a stored tag
     if (A.n_batches >= 0x1FFFF) return c->fail(OWGS_ERANGE, "more than 131070 batches in one call");
     const size_t na = (size_t)std::max(A.n_actions, 1);
@@ -693,6 +698,10 @@ static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s, bool launch
         HIPCHK(c, hipEventCreate(&c->ev_engine[0]));
         HIPCHK(c, hipEventCreate(&c->ev_engine[1]));
     }
+    // the engine specialisation: the map code when any registered action is concurrent (its entries, releases and
+    // overflow can only come from such actions), the general pool / sequence code when the call needs it
+    A.feat |= (c->any_conc ? OWGS_F_CONC : 0) | ((c->pool_mode != 0 || A.seq != nullptr) ? OWGS_F_GEN : 0);
+    if (env_opts().feat_all) A.feat = OWGS_F_ALL;  // diagnostics: always the general engine
     if (!launch) return OWGS_OK;  // owgs_replay_device_multi launches every shard's engine at once
     HIPCHK(c, hipEventRecord(c->ev_engine[0], s));  // brackets exactly the engine launch (owgs_engine_ms)
     HIPCHK(c, launch_engine(c, &A, s));
@@ -1112,6 +1121,7 @@ int owgs_register_actions(owgs_ctx* c, int32_t n, const char* ns_bytes, const in
         c->a_slot.push_back(sid);
         c->a_mem.push_back(mem_mb[i]);
         c->a_maxc.push_back(max_conc[i]);
+        if (max_conc[i] > 1) c->any_conc = true;
         c->a_bb.push_back(blackbox[i] ? 1 : 0);
         out_action[i] = base + i;
     }
@@ -1298,6 +1308,7 @@ int owgs_schedule_walks(owgs_ctx* c, int32_t n, const uint8_t* pool, const int32
     HIPCHK(c, c->d_flags.reserve((size_t)n));
     OwgsEngineArgs A;
     base_args(c, A);
+    A.feat = OWGS_F_ALL;  // explicit walks carry their own limits
     A.seq = seq ? c->d_seq.p : nullptr;
     A.out_inv = c->d_out.p;
     A.out_flags = c->d_flags.p;

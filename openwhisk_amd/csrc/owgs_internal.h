@@ -186,7 +186,15 @@ struct OwgsEngineArgs {
     int32_t opts;                // diagnostics (env OWGS_OPTS): bit0 = no hot-action rank tables
     int32_t cw;                  // chunk width of this replay (<= OWGS_WL)
     unsigned long long* trace;   // diagnostic build only (-DOWGS_TRACE): [waves][OWGS_TRACE_CAP] barrier timeline
+    int32_t feat;                // engine code paths this launch needs (OWGS_F_*): picks the compiled specialisation
 };
+// Engine specialisations.  The engine body is compiled once per feature set, and the host launches the smallest one
+// that covers the context and the call, so a stream without concurrent actions on identity pools runs a kernel with
+// none of the NestedSemaphore map, explicit-pool or explicit-sequence code in it (fewer instructions per pass, fewer
+// registers, a loop body that stays in the instruction cache).
+#define OWGS_F_CONC 1  // maxConcurrent > 1 actions: the concurrency map (primary + overflow), container scans
+#define OWGS_F_GEN 2   // explicit pool words (non-identity pools) or explicit per-activation sequence numbers
+#define OWGS_F_ALL 3
 
 // generateHash(namespace, action) for n actions: out[i] = abs(h(ns_i) ^ h(path_i)), Int.MinValue kept (SCPB:370-372).
 // If raw != 0, out[i] = h(ns_i) only (String.hashCode of the first string set).

@@ -1059,10 +1059,20 @@ __device__ __forceinline__ void lds_sync() {
 #define TRACE_MARK(id)
 #endif
 
+template <int FEAT>
 __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
+    // specialisation (OWGS_F_*): without F_CONC every lane is maxConcurrent == 1 (a record saying otherwise is a broken
+    // stream) and the map code is gone; without F_GEN pools are identity pools and sequence numbers implicit
+    constexpr bool kConc = (FEAT & OWGS_F_CONC) != 0;
+    constexpr bool kGen = (FEAT & OWGS_F_GEN) != 0;
+    const int pool_mode = kGen ? A.pool_mode : 0;
+    const unsigned long long* const seqp = kGen ? A.seq : nullptr;
+    auto conc_of = [&](uint32_t y) -> int {  // maxConcurrent field of a record's meta.y, as this specialisation sees it
+        return kConc ? (int)((y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK) : 1;
+    };
     extern __shared__ uint4 lds_raw[];
     char* L = (char*)lds_raw;
-    const OwgsLayout Y = owgs_layout(A.n_slots, A.pool_mode, A.n_ids, A.nm, A.nb, A.n_actions);
+    const OwgsLayout Y = owgs_layout(A.n_slots, pool_mode, A.n_ids, A.nm, A.nb, A.n_actions);
     int32_t* P = (int32_t*)(L + Y.P);
     uint32_t* ub = (uint32_t*)(L + Y.pool);
     int16_t* pw = (int16_t*)(L + Y.pool);
@@ -1109,7 +1119,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
         for (int k = 0; k < LB; ++k) {
             const int i = i0 + k * OWGS_NT + tid;
             v[k] = i < n_slots ? A.permits[i] : 0;
-            u[k] = (A.pool_mode == 0 && i < A.n_ids) ? A.usable[i >> 5] : ~0u;
+            u[k] = (pool_mode == 0 && i < A.n_ids) ? A.usable[i >> 5] : ~0u;
         }
 #pragma unroll
         for (int k = 0; k < LB; ++k) {
@@ -1120,7 +1130,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
             P[i] = unusable ? v[k] + OWGS_PENC : v[k];
         }
     }
-    if (A.pool_mode == 0) {
+    if (pool_mode == 0) {
         for (int i = tid; i < words; i += OWGS_NT) ub[i] = A.usable[i];
     } else {
         for (int i = tid; i < nm + nb; i += OWGS_NT) pw[i] = (int16_t)A.pool_words[i];
@@ -1150,7 +1160,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     }
     for (int i = tid; i < (int)(Y.uni_bytes / 4); i += OWGS_NT) ((uint32_t*)(L + Y.uni))[i] = 0u;
     lds_sync();
-    if (A.pool_mode == 0 && wave == 0) {  // prefix counts of the usable bitmap
+    if (pool_mode == 0 && wave == 0) {  // prefix counts of the usable bitmap
         int carry = 0;
         for (int w0 = 0; w0 <= words; w0 += 64) {
             const int w = w0 + lane;
@@ -1165,7 +1175,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     E.ub = ub;
     E.pw = pw;
     E.pc = pc;
-    E.pool_mode = A.pool_mode;
+    E.pool_mode = pool_mode;
     E.n_ids = A.n_ids;
     E.nm = nm;
     E.nb = nb;
@@ -1242,7 +1252,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     // healthy invokers per pool (|H| of the overload fallback, SCPB:417-424): identity pools count them from the
     // usable bitmap (owgs_update_health_device updates only the bitmap there); other pools take the host's counts
     int hm_e = A.hm, hb_e = A.hb;
-    if (A.pool_mode == 0) {
+    if (pool_mode == 0) {
         auto rank = [&](int x) {  // usable ids below x
             return x <= 0 ? 0 : (int)pc[x >> 5] + ((x & 31) ? __popc(ub[x >> 5] & ((1u << (x & 31)) - 1u)) : 0);
         };
@@ -1265,7 +1275,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
             if (!io) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             for (int ix = tid; ix < OWGS_CTC; ix += OWGS_NT) rc[ix] = 0u;
             lds_sync();
-            const bool rel_ovf = OWGS_OVF && sc[SC_OVF] > 0;  // overflow table in use (uniform)
+            const bool rel_ovf = kConc && OWGS_OVF && sc[SC_OVF] > 0;  // overflow table in use (uniform)
             if (!io) {
                 // the release records of batch b (rel_rec[rel_off[b] .. rel_off[b+1]), written when the released
                 // activations were decided): maxConcurrent == 1 -> ForcibleSemaphore.release (FS:117-120), summed
@@ -1304,7 +1314,8 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                 // concurrent: RS.release(1, true) per release through the concurrency map
                 constexpr int RQ = OWGS_REL_RQ;
                 const int64_t pb = cm >> 1, pe = (ce + 1) >> 1;
-                for (int64_t p0 = pb + tid; p0 < pe; p0 += RQ * OWGS_ENT) {
+                if (!kConc && cm < ce) err |= OWGS_ERR_BAD_STREAM;  // (a specialisation without the map)
+                for (int64_t p0 = pb + tid; kConc && p0 < pe; p0 += RQ * OWGS_ENT) {
                     uint4 rp[RQ];
 #pragma unroll
                     for (int k = 0; k < RQ; ++k) {
@@ -1458,8 +1469,8 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
 #endif
         // (a rebuild costs an HBM round trip of every live entry: at least CTC/8 new entries since the last one, so a
         // shard whose live entries stay above half the primary does not rebuild in every batch)
-        if ((sc[SC_USED] > OWGS_CTC / 2 && sc[SC_USED] >= sc[SC_CLAST] + OWGS_CTC / 8) ||
-            (A.ovf.cap > 0 && sc[SC_OVF] > A.ovf.cap / 2)) {
+        if (kConc && ((sc[SC_USED] > OWGS_CTC / 2 && sc[SC_USED] >= sc[SC_CLAST] + OWGS_CTC / 8) ||
+                      (A.ovf.cap > 0 && sc[SC_OVF] > A.ovf.cap / 2))) {
             const bool had_ovf = sc[SC_OVF] > 0;
             if (!io) {
                 for (int ix = tid; ix < OWGS_CTC; ix += OWGS_ENT) {
@@ -1522,11 +1533,11 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
             // own limit, FS:48-50, is 2^31)
             for (int i = tid; i < n_slots; i += OWGS_ENT) {
                 const int v = P[i];
-                const bool unusable = A.pool_mode == 0 && i < A.n_ids && !((ub[i >> 5] >> (i & 31)) & 1u);
+                const bool unusable = pool_mode == 0 && i < A.n_ids && !((ub[i >> 5] >> (i & 31)) & 1u);
                 if ((unusable ? v - OWGS_PENC : v) >= OWGS_PLIM) err |= OWGS_ERR_PERMITS;
             }
             int m0 = (int)0x80000000, m1 = (int)0x80000000;
-            if (A.pool_mode == 0) {
+            if (pool_mode == 0) {
                 for (int i = tid; i < nm; i += OWGS_ENT)
                     if ((ub[i >> 5] >> (i & 31)) & 1u) m0 = max(m0, P[i]);
                 for (int p = tid; p < nb; p += OWGS_ENT) {
@@ -1578,7 +1589,9 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
             const int pool = (rc4.x & OWGS_AM_POOL) ? 1 : 0;
             const bool cok = (rc4.x & OWGS_AM_COK) != 0;
             const int mem = (int)(rc4.y & OWGS_AM_MEM_MASK);
-            const int maxc = (int)((rc4.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
+            const int maxc = conc_of(rc4.y);
+            if (!kConc && held && (rc4.y & OWGS_AM_VALID) && ((rc4.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK) != 1u)
+                err |= OWGS_ERR_BAD_STREAM;  // a concurrent action in a launch of the specialisation without the map
             const bool sthrow = (rc4.y & OWGS_AM_THROW) != 0;
             const bool sempty = (rc4.y & OWGS_AM_EMPTY) != 0;
             const int a = (int)(rc4.z & OWGS_REC_NOACT);
@@ -1596,7 +1609,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
             // and the new container at x (maxConcurrent - 1 free slots) is the only step that became feasible, so the
             // next lanes start at x's step j = (pos(x) - home) * step^-1 mod n (identity pools; else from 0)
             auto fallback_cursor = [&](int x) -> uint32_t {
-                if (A.pool_mode != 0 || n <= 1) return 0u;
+                if (pool_mode != 0 || n <= 1) return 0u;
                 const int xp = x - (pool ? A.n_ids - nb : 0);
                 if (xp < 0 || xp >= n) return 0u;
                 int t0 = 0, t1 = 1, r0 = n, r1 = step % n;  // extended Euclid: step^-1 mod n (gcd(step, n) = 1)
@@ -1662,7 +1675,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
             bool keep = false;
             while (f < len) {
                 ++st_pass;
-                const bool ovf_on = OWGS_OVF && sc[SC_OVF] > 0;  // overflow keys exist: lookups fall through (uniform)
+                const bool ovf_on = kConc && OWGS_OVF && sc[SC_OVF] > 0;  // overflow keys exist: lookups fall through (uniform)
 #ifdef OWGS_PROFILE
                 const u64 tpass0 = memtime_pinned();
 #ifdef OWGS_PROF_LATER
@@ -1709,7 +1722,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         const int hpool = (d.y & OWGS_AM_POOL) ? 1 : 0;
                         const bool hcok = (d.y & OWGS_AM_COK) != 0;
                         const int hmem = (int)(d.z & OWGS_AM_MEM_MASK);
-                        const int hmc = (int)((d.z >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
+                        const int hmc = conc_of(d.z);
                         const int hslot = (int)d.w;
                         const uint32_t hcw = ccw[d.x];
                         const int hcc = (int)((hcw >> 15) & OWGS_RMASK);
@@ -1812,7 +1825,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             kind = K_HOT;
                         } else if (maxc == 1 && mem > U && ((A.shortcut_ok >> pool) & 1)) {
                             kind = K_FALLBACK;  // every usable permit < mem: the walk fails everywhere
-                        } else if (OWGS_CSCAN_ON && maxc > 1 && mem > U && A.pool_mode == 0 && n > OWGS_CSCAN_MIN_N && !ovf_on) {
+                        } else if (OWGS_CSCAN_ON && maxc > 1 && mem > U && pool_mode == 0 && n > OWGS_CSCAN_MIN_N && !ovf_on) {
                             kind = K_CSCAN;  // no invoker can open a container: capacity = the key's open ones
                             ws = s;          // (the ordinary walk's start, should the key have > 64 of them)
                             wpos = mod_fast(home + s * step, n, __builtin_amdgcn_rcpf((float)n));
@@ -1825,7 +1838,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             pf_pre = (int)(memtime_pinned() - ts_hot);
 #endif
                             
-                            if (maxc == 1 && A.pool_mode == 0) {
+                            if (maxc == 1 && pool_mode == 0) {
 #ifdef OWGS_PROFILE
                                 const u64 tf0 = memtime_pinned();
 #endif
@@ -1887,7 +1900,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             const u64 tg0 = memtime_pinned();
 #endif
                             ++st_glane;
-                            if (maxc > 1 && A.pool_mode == 0) {
+                            if (maxc > 1 && pool_mode == 0) {
                                 // identity pools, concurrent action: the permits and the first concurrency-table entry
                                 // of 4 walk steps issue together; a key whose first entry holds another key follows
                                 // its chain afterwards
@@ -2024,7 +2037,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                 // k(x) = (pos(x) - home) * step^-1 mod n, and finds the container holding rank r (cumulative free
                 // slots in walk order); none -> the walk fails everywhere (SCPB:417).  More than 64 open containers:
                 // the ordinary walk.  Only for pools larger than half the table: a smaller pool is walked faster.
-                if (!io) {
+                if (kConc && !io) {
                     u64 cm = __ballot(spec && kind == K_CSCAN);
                     int* cand = hscr + wave * 64;
                     while (cm) {
@@ -2190,7 +2203,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         const int pj = (qr.x & OWGS_AM_POOL) ? 1 : 0;
                         const int nn = pj ? nb : nm;
                         const int mj = (int)(qr.y & OWGS_AM_MEM_MASK);
-                        const int cj = (int)((qr.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
+                        const int cj = conc_of(qr.y);
                         const int slj = (int)(qr.w & 0x1FFFFu);
                         const float rmj = __builtin_amdgcn_rcpf((float)mj);
                         const float rnn = __builtin_amdgcn_rcpf((float)nn);
@@ -2214,7 +2227,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             int pv[LW_Q], id[LW_Q];
                             int p = p0 + loff;
                             if (p >= nn) p -= nn;
-                            if (A.pool_mode == 0) {
+                            if (pool_mode == 0) {
                                 // identity pools: the id is arithmetic, the usable flag folded into the permits: the
                                 // LW_Q reads of the round issue back to back, no branch between them
                                 const int base = pj ? A.n_ids - nb : 0;
@@ -2410,13 +2423,13 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     }
                     if (hc <= 0) {
                         kind = K_NONE;
-                    } else if (A.seq == nullptr && A.pool_mode == 0) {
+                    } else if (seqp == nullptr && pool_mode == 0) {
                         const int k = (int)rng_index(A.rng_seed, A.seq_base + (u64)i, (uint32_t)hc);
                         OWGS_LAND(select_usable(E, pool ? A.n_ids - nb : 0, k));
                     } else {
-                        const u64 seq = A.seq ? A.seq[i] : (A.seq_base + (u64)i);
+                        const u64 seq = seqp ? seqp[i] : (A.seq_base + (u64)i);
                         const int k = (int)rng_index(A.rng_seed, seq, (uint32_t)hc);
-                        OWGS_LAND(A.pool_mode == 0 ? select_usable(E, pool ? A.n_ids - nb : 0, k)
+                        OWGS_LAND(pool_mode == 0 ? select_usable(E, pool ? A.n_ids - nb : 0, k)
                                                    : A.hlist[(pool ? A.hm : 0) + k]);
                     }
 #undef OWGS_LAND
@@ -2501,7 +2514,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
 #if OWGS_EXT
                 if (act) {  // the summary the in-pass re-decisions read (commit phase)
                     const bool exempt = !part || kind == K_FALLBACK;
-                    const bool rd = maxc == 1 && A.pool_mode == 0 && kind == K_TARGET && a != (int)OWGS_REC_NOACT;
+                    const bool rd = maxc == 1 && pool_mode == 0 && kind == K_TARGET && a != (int)OWGS_REC_NOACT;
                     fxa[li] = make_uint4(((uint32_t)a & OWGS_REC_NOACT) | (nf ? FX_NF : 0u) | (exempt ? FX_EXEMPT : 0u) |
                                              (rd ? FX_OK : 0u),
                                          (part ? (uint32_t)t : FX_NOT) | ((uint32_t)s_t << 16), rc4.x,
@@ -2631,7 +2644,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                 if (hc <= 0) break;
                                 // (explicit per-activation sequence numbers: the ordinary path -- a global load here
                                 // would wait for the I/O wave's prefetch stream)
-                                if (A.seq) break;
+                                if (seqp) break;
                                 const u64 sq = A.seq_base + (u64)(c0 + L);
                                 tn = select_usable(E, base, (int)rng_index(A.rng_seed, sq, (uint32_t)hc));
                                 if (tn < 0 || tn >= n_slots) break;  // (a throwing lane: the ordinary path)
@@ -2918,19 +2931,22 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
 struct OwgsEngineOne {
     OwgsEngineArgs a[1];
 };
-__global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineOne M) { owgs_engine_body(M.a[blockIdx.x]); }
+template <int FEAT>
+__global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_kernel(OwgsEngineOne M) { owgs_engine_body<FEAT>(M.a[blockIdx.x]); }
 
 // several controller shards in one launch: workgroup k replays shard k (its own LDS image, state and stream); the
 // arguments stay in the kernarg segment, so every field is still a scalar load
 struct OwgsEngineMulti {
     OwgsEngineArgs a[OWGS_MULTI_MAX];
 };
+template <int FEAT>
 __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_multi_kernel(OwgsEngineMulti M) {
-    owgs_engine_body(M.a[blockIdx.x]);
+    owgs_engine_body<FEAT>(M.a[blockIdx.x]);
 }
 // more shards than the kernarg segment holds: the argument blocks in HBM (uniform per workgroup, read-only)
+template <int FEAT>
 __global__ __launch_bounds__(OWGS_NT, 1) void owgs_engine_multi_dev_kernel(const OwgsEngineArgs* __restrict__ As) {
-    owgs_engine_body(As[blockIdx.x]);
+    owgs_engine_body<FEAT>(As[blockIdx.x]);
 }
 
 // ------------------------------------------------------------------------------------------------ explicit releases
@@ -3389,7 +3405,7 @@ extern "C" hipError_t owgs_launch_release_seq(const OwgsReleaseArgs* a, hipStrea
 // the engine's dynamic-LDS limit, set once per (kernel, device): the attribute is per device, and a process may drive
 // contexts on several devices
 static hipError_t lds_attr(const void* fn, int which) {
-    static std::atomic<unsigned long long> done[3];
+    static std::atomic<unsigned long long> done[9];
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
@@ -3400,45 +3416,76 @@ static hipError_t lds_attr(const void* fn, int which) {
     return e;
 }
 
+// compiled specialisations: 0 (maxConcurrent == 1, identity pools, implicit sequence numbers), OWGS_F_CONC, and
+// OWGS_F_ALL for anything else
+static int feat_index(int feat) { return feat == 0 ? 0 : feat == OWGS_F_CONC ? 1 : 2; }
+template <template <int> class K>
+static void* pick(int fi) {
+    return fi == 0 ? K<0>::fn() : fi == 1 ? K<OWGS_F_CONC>::fn() : K<OWGS_F_ALL>::fn();
+}
+template <int F>
+struct KOne {
+    static void* fn() { return (void*)owgs_engine_kernel<F>; }
+};
+template <int F>
+struct KMulti {
+    static void* fn() { return (void*)owgs_engine_multi_kernel<F>; }
+};
+template <int F>
+struct KMultiDev {
+    static void* fn() { return (void*)owgs_engine_multi_dev_kernel<F>; }
+};
+
 extern "C" hipError_t OWGS_GEOM(owgs_launch_engine_multi_dev)(const OwgsEngineArgs* a_host, const OwgsEngineArgs* a_dev, int k,
                                                    hipStream_t s) {
     if (k < 1 || k > OWGS_MULTI_DEV_MAX) return hipErrorInvalidValue;
     size_t lds = 0;
-    for (int i = 0; i < k; ++i)
+    int feat = 0;
+    for (int i = 0; i < k; ++i) {
         lds = std::max(lds, OWGS_GEOM(owgs_engine_lds_bytes)(a_host[i].n_slots, a_host[i].pool_mode, a_host[i].n_ids,
                                                   a_host[i].nm, a_host[i].nb, a_host[i].n_actions));
+        feat |= a_host[i].feat;
+    }
     if (lds > OWGS_LDS_BYTES) return hipErrorInvalidValue;
-    const hipError_t ea = lds_attr((const void*)owgs_engine_multi_dev_kernel, 0);
+    const int fi = feat_index(feat);
+    void* fn = pick<KMultiDev>(fi);
+    const hipError_t ea = lds_attr(fn, fi);
     if (ea != hipSuccess) return ea;
-    hipLaunchKernelGGL(owgs_engine_multi_dev_kernel, dim3(k), dim3(OWGS_NT), lds, s, a_dev);
-    return hipGetLastError();
+    void* args[] = {(void*)&a_dev};
+    return hipLaunchKernel(fn, dim3(k), dim3(OWGS_NT), args, lds, s);
 }
 
 extern "C" hipError_t OWGS_GEOM(owgs_launch_engine_multi)(const OwgsEngineArgs* a, int k, hipStream_t s) {
     if (k < 1 || k > OWGS_MULTI_MAX) return hipErrorInvalidValue;
     size_t lds = 0;
+    int feat = 0;
     OwgsEngineMulti M;
     for (int i = 0; i < k; ++i) {
         lds = std::max(lds, OWGS_GEOM(owgs_engine_lds_bytes)(a[i].n_slots, a[i].pool_mode, a[i].n_ids, a[i].nm, a[i].nb,
                                                   a[i].n_actions));
+        feat |= a[i].feat;
         M.a[i] = a[i];
     }
     if (lds > OWGS_LDS_BYTES) return hipErrorInvalidValue;
-    const hipError_t ea = lds_attr((const void*)owgs_engine_multi_kernel, 1);
+    const int fi = feat_index(feat);
+    void* fn = pick<KMulti>(fi);
+    const hipError_t ea = lds_attr(fn, 3 + fi);
     if (ea != hipSuccess) return ea;
-    hipLaunchKernelGGL(owgs_engine_multi_kernel, dim3(k), dim3(OWGS_NT), lds, s, M);
-    return hipGetLastError();
+    void* args[] = {(void*)&M};
+    return hipLaunchKernel(fn, dim3(k), dim3(OWGS_NT), args, lds, s);
 }
 
 extern "C" hipError_t OWGS_GEOM(owgs_launch_engine)(const OwgsEngineArgs* a, hipStream_t s) {
     const size_t lds = OWGS_GEOM(owgs_engine_lds_bytes)(a->n_slots, a->pool_mode, a->n_ids, a->nm, a->nb, a->n_actions);
     if (lds > OWGS_LDS_BYTES) return hipErrorInvalidValue;
-    const hipError_t ea = lds_attr((const void*)owgs_engine_kernel, 2);
+    const int fi = feat_index(a->feat);
+    void* fn = pick<KOne>(fi);
+    const hipError_t ea = lds_attr(fn, 6 + fi);
     if (ea != hipSuccess) return ea;
     OwgsEngineOne M;
     M.a[0] = *a;
-    hipLaunchKernelGGL(owgs_engine_kernel, dim3(1), dim3(OWGS_NT), lds, s, M);
-    return hipGetLastError();
+    void* args[] = {(void*)&M};
+    return hipLaunchKernel(fn, dim3(1), dim3(OWGS_NT), args, lds, s);
 }
 
 #ifdef OWGS_VARIANT_NS
