@@ -452,7 +452,9 @@ class GpuShardingContainerPoolBalancer:
         out = (C.c_uint64 * 32)()
         self._chk(self._L.owgs_read_stats(self._h, out, 32))
         d = {"passes": out[0], "probes": out[1], "fallbacks": out[2], "long_walks": out[3], "chunks": out[4],
-             "stops": out[5], "general_probes": out[6], "general_lanes": out[7], "redecided": out[31]}
+             "stops": out[5], "general_probes": out[6], "general_lanes": out[7], "redecided": out[31] & 0xFFFFFFFF}
+        if out[31] >> 32:
+            d["redecided_prewalk"] = out[31] >> 32
         if any(out[28:31]) and not any(out[8:16]):  # -DOWGS_EXT_PROF build: in-pass re-decision costs
             d["redecide"] = {"cycles": out[28], "walk_rounds": out[29], "scans": out[30], "setup": out[20], "walk": out[21],
                              "apply": out[22], "scan": out[23]}

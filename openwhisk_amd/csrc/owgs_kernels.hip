@@ -85,6 +85,14 @@ typedef unsigned long long u64;
 #ifndef EXT_ROUNDS
 #define EXT_ROUNDS 8  // walk rounds (128 steps each) a re-decision may take; a longer walk waits for the next pass
 #endif
+#ifndef OWGS_PRE
+#define OWGS_PRE 0  // stopping lanes walk their own re-decision in validate, in parallel (see the commit phase)
+#endif
+#ifndef PRE_G
+#define PRE_G 6  // 4-step groups such a walk may take (beyond them the I/O wave walks it)
+#endif
+// the pre-walk's record of the invokers it skipped: one bit of a 64-bit signature per invoker
+__device__ __forceinline__ uint32_t pre_bit(int x) { return ((uint32_t)x * 0x9E3779B1u) >> 26; }
 // fxa[li] (per lane of the pass, stream order): x = action | not known to fit << 24 | exempt << 25 | re-decidable << 26
 // | re-decided << 27 | kind << 28 | clash << 30; y = target (0xFFFF none) | walk step << 16 (after a re-decision: the
 // new ones); z = the action's meta.x (home | step << 15 | pool); w = mem | took memory << 31
@@ -1000,6 +1008,20 @@ __device__ __forceinline__ int usable_before(const EngineCtx& E, int x) {
     return (int)E.pc[w] + __popc(m);
 }
 
+// position of the need-th set bit (0-based) of m, need < popc(m): halving by popcounts, no loop over the bits
+__device__ __forceinline__ int select_in_word(uint32_t m, int need) {
+    int pos = 0;
+#pragma unroll
+    for (int w = 16; w >= 1; w >>= 1) {
+        const int c = __popc(m & ((1u << w) - 1u));
+        const bool up = need >= c;
+        need -= up ? c : 0;
+        m = up ? m >> w : m;
+        pos += up ? w : 0;
+    }
+    return pos;
+}
+
 // k-th usable id (0-based) at or after id lo (identity pools): binary search over the word prefix counts
 __device__ __forceinline__ int select_usable(const EngineCtx& E, int lo, int k) {
     const int target = usable_before(E, lo) + k;  // global rank of the wanted id
@@ -1009,15 +1031,15 @@ __device__ __forceinline__ int select_usable(const EngineCtx& E, int lo, int k) 
         if ((int)E.pc[mid] <= target) a = mid;
         else z = mid - 1;
     }
-    uint32_t m = E.ub[a];
-    int need = target - (int)E.pc[a];
-    while (m) {  // need < popcount(m) when the host's healthy counts match the bitmap
-        const int bit = __ffs((int)m) - 1;
-        if (need == 0) return (a << 5) + bit;
-        m &= m - 1;
-        --need;
-    }
-    return -1;
+    const uint32_t m = E.ub[a];
+    const int need = target - (int)E.pc[a];
+    if (need < 0 || need >= __popc(m)) return -1;  // (the host's healthy counts disagree with the bitmap)
+    return (a << 5) + select_in_word(m, need);
+}
+
+// k-th usable id of a pool whose ids [lo, lo + n) are all usable (fast path), else select_usable
+__device__ __forceinline__ int select_pool(const EngineCtx& E, int lo, int k, bool all_usable) {
+    return all_usable ? lo + k : select_usable(E, lo, k);
 }
 
 // Workgroup barrier that orders LDS only: a plain __syncthreads() also waits for every outstanding global store of
@@ -1181,7 +1203,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     E.nb = nb;
 
     uint32_t st_pass = 0, st_probe = 0, st_fb = 0, st_long = 0, st_chunk = 0, st_stop = 0, st_gprobe = 0, st_glane = 0;
-    uint32_t st_ext = 0;  // in-pass re-decisions (I/O wave)
+    uint32_t st_ext = 0, st_pre = 0;  // in-pass re-decisions (I/O wave), of them from the lane's own pre-walk
 #ifdef OWGS_EXT_PROF
     u64 xp_cyc = 0, xp_rounds = 0, xp_scans = 0, xp_ph[4] = {0, 0, 0, 0};
 #endif
@@ -1259,6 +1281,8 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
         hm_e = rank(nm);
         hb_e = rank(A.n_ids) - rank(A.n_ids - nb);
     }
+    // pools whose ids are all usable: the fallback's k-th healthy invoker is arithmetic (no rank/select reads)
+    const bool full_m = pool_mode == 0 && hm_e == nm, full_b = pool_mode == 0 && hb_e == nb;
 
     int g = 0;    // global chunk index
     int par = 0;  // pass parity (double-buffered LDS scalars)
@@ -2425,7 +2449,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         kind = K_NONE;
                     } else if (seqp == nullptr && pool_mode == 0) {
                         const int k = (int)rng_index(A.rng_seed, A.seq_base + (u64)i, (uint32_t)hc);
-                        OWGS_LAND(select_usable(E, pool ? A.n_ids - nb : 0, k));
+                        OWGS_LAND(select_pool(E, pool ? A.n_ids - nb : 0, k, pool ? full_b : full_m));
                     } else {
                         const u64 seq = seqp ? seqp[i] : (A.seq_base + (u64)i);
                         const int k = (int)rng_index(A.rng_seed, seq, (uint32_t)hc);
@@ -2519,6 +2543,61 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                              (rd ? FX_OK : 0u),
                                          (part ? (uint32_t)t : FX_NOT) | ((uint32_t)s_t << 16), rc4.x,
                                          (uint32_t)mem | ((part && cons) ? 0x80000000u : 0u));
+#if OWGS_PRE
+                    // pre-walk: a lane that does not fit walks on from its speculated step now, on the permits every
+                    // earlier lane of the pass leaves where it speculated: the tentative permits (all lanes' takes)
+                    // plus the takes of this lane and the later ones at each probed invoker (bucket lists).  That is
+                    // this lane's exact decision unless an earlier lane is re-decided first; the I/O wave checks that
+                    // (commit phase) with the signature of the invokers skipped here.  Result -> lq[li] (free after
+                    // the speculation), invalid unless a target was found within PRE_G groups.
+                    uint4 pre = make_uint4(0u, 0u, 0u, 0u);
+                    if (nf && rd) {
+                        const int base = pool ? A.n_ids - nb : 0;
+                        uint32_t blo = 0u, bhi = 0u;
+                        auto bmark = [&](int x) {
+                            const uint32_t h = pre_bit(x);
+                            if (h < 32u) blo |= 1u << h;
+                            else bhi |= 1u << (h - 32u);
+                        };
+                        bmark(t);  // (a lane re-decided away from t leaves room there)
+                        int s = s_t + 1;
+                        int pos = mod_fast(home + s * step, n, __builtin_amdgcn_rcpf((float)n));
+                        bool found = false;
+                        int tp = 0, sp = 0;
+#pragma unroll 1
+                        for (int g4 = 0; g4 < PRE_G && !found && s < n; ++g4) {
+                            int ps[4], pv[4];
+                            uint32_t bh[4];
+                            int pp = pos;
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                ps[k] = base + pp;
+                                pv[k] = P[ps[k]];
+                                bh[k] = bhead[((uint32_t)ps[k] * 2654435761u) >> (32 - OWGS_NBK_LOG2)];
+                                pp += step;
+                                pp -= pp >= n ? n : 0;
+                            }
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                if (found || s + k >= n || pv[k] >= OWGS_PLIM) continue;  // (unusable: stays so)
+                                int room = pv[k];
+                                for (int m = (int)bh[k] - 1; m >= 0; m = nextl[m] - 1)
+                                    if (m > li && spt[m] == ps[k]) room += spc[m];  // later lanes' takes back
+                                if (room >= mem) {
+                                    found = true;
+                                    tp = ps[k];
+                                    sp = s + k;
+                                } else {
+                                    bmark(ps[k]);
+                                }
+                            }
+                            s += 4;
+                            pos = pp;
+                        }
+                        if (found) pre = make_uint4(0x80000000u | (uint32_t)tp, (uint32_t)sp, blo, bhi);
+                    }
+                    lq[li] = pre;
+#endif
                 }
 #endif
                 if (!io) {
@@ -2576,14 +2655,21 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         auto inset = [&](uint32_t bits, uint32_t h) {  // (whole wave: ds_bpermute)
                             return ((uint32_t)__shfl((int)bits, (int)(h >> 5), 64) >> (h & 31u)) & 1u;
                         };
+                        // lane i: the speculated target a re-decided lane left (room grew there), -1 = none
+                        int src = -1;
+                        // the pools' usable-permit bounds: only this wave changes them in this phase
+                        int u0 = sc[SC_U0], u1 = sc[SC_U1];
+                        // the stop lane's summary and pre-walk, carried from the scan that found it (uniform)
+                        uint4 fx = fxa[L], px = lq[L];
+                        bool a_hit = false;  // its action was re-decided in this pass (none yet)
                         while (L < len && nE < EXT_MAX) {
-                            const uint4 fx = fxa[L];
                             // a re-decided action's next lane waits for the next pass (its rank, and the hot table of
                             // its action, no longer hold: it re-speculates with its action's other lanes)
-                            const bool a_hit = inset(set_a, hsh(fx.x & OWGS_REC_NOACT)) != 0u;
-                            if (!(fx.x & FX_OK) || a_hit) break;
+                            const uint32_t fxx = __builtin_amdgcn_readfirstlane(fx.x);
+                            if (!(fxx & FX_OK) || a_hit) break;
                             // (uniform: scalar registers, and the pool's fields become scalar loads -- a vector load
                             // here would wait for the I/O wave's own prefetch stream, vmcnt(0))
+                            const uint32_t fy = __builtin_amdgcn_readfirstlane(fx.y);
                             const uint32_t fz = __builtin_amdgcn_readfirstlane(fx.z), fw = __builtin_amdgcn_readfirstlane(fx.w);
                             const int hm_ = (int)(fz & OWGS_AM_POS_MASK), st_ = (int)((fz >> 15) & OWGS_AM_POS_MASK);
                             const int pl_ = (fz & OWGS_AM_POOL) ? 1 : 0;
@@ -2594,15 +2680,36 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             const u64 tq0 = memtime_pinned();
                             xp_ph[0] += tq0 - tq_prev;
 #endif
+                            bool done = false;
+#if OWGS_PRE
+                            // the lane's own pre-walk (validate) assumed every earlier lane where it speculated.  Since
+                            // then the re-decided lanes moved: room grew at their old targets (none of them may be a
+                            // step the pre-walk skipped: signature test) and shrank at their new ones (the permits
+                            // here are exact for this lane: the target must still hold it)
+                            const uint32_t pxx = __builtin_amdgcn_readfirstlane(px.x);
+                            if (pxx >> 31) {
+                                const uint32_t blo = __builtin_amdgcn_readfirstlane(px.z), bhi = __builtin_amdgcn_readfirstlane(px.w);
+                                const uint32_t hb = pre_bit(src);
+                                const bool hit = src >= 0 && (((hb < 32u ? blo >> hb : bhi >> (hb - 32u)) & 1u) != 0u);
+                                if (!__ballot(hit)) {
+                                    const int tp = (int)(pxx & 0x7FFFFFFFu);
+                                    const int v = P[tp];
+                                    if (v < OWGS_PLIM && v >= mm) {
+                                        kn = K_TARGET;
+                                        tn = tp;
+                                        sn = (int)__builtin_amdgcn_readfirstlane(px.y);
+                                        done = true;
+                                        ++st_pre;
+                                    }
+                                }
+                            }
+#endif
                             // every usable permit count below mem: the walk fails (U bounds the frontier, whose
                             // permits bound this lane's)
-                            bool done = mm > sc[pl_ ? SC_U1 : SC_U0] && ((A.shortcut_ok >> pl_) & 1);
+                            if (!done) done = mm > (pl_ ? u1 : u0) && ((A.shortcut_ok >> pl_) & 1);
                             if (!done) {
                                 const float rnn = __builtin_amdgcn_rcpf((float)nn);
-                                int s0 = (int)(fx.y >> 16);
-                                int p0 = mod_fast(hm_ + s0 * st_, nn, rnn);
-                                const int loff = mod_fast(lane * st_, nn, rnn), boff = mod_fast(64 * st_, nn, rnn),
-                                          roff = mod_fast(128 * st_, nn, rnn);
+                                int s0 = (int)(fy >> 16);
                                 for (int rd = 0; rd < EXT_ROUNDS; ++rd) {
 #ifdef OWGS_EXT_PROF
                                     ++xp_rounds;
@@ -2611,11 +2718,9 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                         done = true;
                                         break;
                                     }
-                                    int pa = p0 + loff;
-                                    pa -= pa >= nn ? nn : 0;
-                                    int pb = pa + boff;
-                                    pb -= pb >= nn ? nn : 0;
-                                    const int xa = base + pa, xb = base + pb;
+                                    // walk steps s0 + lane and s0 + 64 + lane ((s0 + 127) * step < 2^31)
+                                    const int xa = base + mod_fast(hm_ + (s0 + lane) * st_, nn, rnn);
+                                    const int xb = base + mod_fast(hm_ + (s0 + 64 + lane) * st_, nn, rnn);
                                     const bool ia = s0 + lane < nn, ib = s0 + 64 + lane < nn;
                                     const int va = ia ? P[xa] : OWGS_PENC, vb = ib ? P[xb] : OWGS_PENC;
                                     const bool fa = va < OWGS_PLIM && va >= mm;  // (usable: flag folded in)
@@ -2630,8 +2735,6 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                         break;
                                     }
                                     s0 += 128;
-                                    p0 += roff;
-                                    p0 -= p0 >= nn ? nn : 0;
                                 }
                             }
 #ifdef OWGS_EXT_PROF
@@ -2646,18 +2749,22 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                 // would wait for the I/O wave's prefetch stream)
                                 if (seqp) break;
                                 const u64 sq = A.seq_base + (u64)(c0 + L);
-                                tn = select_usable(E, base, (int)rng_index(A.rng_seed, sq, (uint32_t)hc));
+                                tn = select_pool(E, base, (int)rng_index(A.rng_seed, sq, (uint32_t)hc), pl_ ? full_b : full_m);
                                 if (tn < 0 || tn >= n_slots) break;  // (a throwing lane: the ordinary path)
+                                // a failed full walk at rank 0 proves every usable permit of the pool < mem
+                                if (pl_) u1 = min(u1, mm - 1);
+                                else u0 = min(u0, mm - 1);
                             }
                             if (lane == 0) {
                                 atomicSub(&P[tn], mm);
-                                *(uint2*)&fxa[L] = make_uint2(fx.x | FX_DONE | ((uint32_t)kn << 28), (uint32_t)tn | ((uint32_t)sn << 16));
+                                *(uint2*)&fxa[L] = make_uint2(fxx | FX_DONE | ((uint32_t)kn << 28), (uint32_t)tn | ((uint32_t)sn << 16));
                                 if (kn == K_FALLBACK) atomicMin(&sc[pl_ ? SC_U1 : SC_U0], mm - 1);  // rank 0 failed
                             }
                             {
-                                const uint32_t h1 = hsh((uint32_t)tn), h2 = hsh(fx.x & OWGS_REC_NOACT);
+                                const uint32_t h1 = hsh((uint32_t)tn), h2 = hsh(fxx & OWGS_REC_NOACT);
                                 if (lane == (int)(h1 >> 5)) set_t |= 1u << (h1 & 31u);
                                 if (lane == (int)(h2 >> 5)) set_a |= 1u << (h2 & 31u);
+                                if (lane == nE) src = (int)(fy & 0xFFFFu);  // the room it left
                             }
                             ++nE;
 #ifdef OWGS_EXT_PROF
@@ -2672,10 +2779,14 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                 ++xp_scans;
 #endif
                                 const int k = k0 + lane;
-                                uint4 f2 = make_uint4(FX_EXEMPT, FX_NOT, 0u, 0u);
-                                if (k < len) f2 = fxa[k];
+                                uint4 f2 = make_uint4(FX_EXEMPT, FX_NOT, 0u, 0u), p2 = make_uint4(0u, 0u, 0u, 0u);
+                                if (k < len) {
+                                    f2 = fxa[k];
+                                    p2 = lq[k];
+                                }
                                 const uint32_t tk = f2.y & 0xFFFFu;
-                                const bool cl = (inset(set_a, hsh(f2.x & OWGS_REC_NOACT)) | inset(set_t, hsh(tk))) != 0u;
+                                const uint32_t ab = inset(set_a, hsh(f2.x & OWGS_REC_NOACT));
+                                const bool cl = (ab | inset(set_t, hsh(tk))) != 0u;
                                 const bool stop = k < len && ((f2.x & FX_NF) || (!(f2.x & FX_EXEMPT) && cl));
                                 const u64 sm = __ballot(stop);
                                 const int q = sm ? ffs64(sm) : 64;
@@ -2683,6 +2794,11 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                 if (lane < q && (f2.w >> 31)) atomicSub(&P[(int)tk], (int)(f2.w & OWGS_AM_MEM_MASK));
                                 if (sm) {
                                     L = k0 + q;
+                                    fx = make_uint4(__builtin_amdgcn_readlane(f2.x, q), __builtin_amdgcn_readlane(f2.y, q),
+                                                    __builtin_amdgcn_readlane(f2.z, q), __builtin_amdgcn_readlane(f2.w, q));
+                                    px = make_uint4(__builtin_amdgcn_readlane(p2.x, q), __builtin_amdgcn_readlane(p2.y, q),
+                                                    __builtin_amdgcn_readlane(p2.z, q), __builtin_amdgcn_readlane(p2.w, q));
+                                    a_hit = __builtin_amdgcn_readlane(ab, q) != 0u;
                                     break;
                                 }
                             }
@@ -2908,7 +3024,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
             atomicAdd(&A.stats[7], pt_x[1]);
         }
 #endif
-        if (io && lane == 0) atomicAdd(&A.stats[31], (u64)st_ext);
+        if (io && lane == 0) atomicAdd(&A.stats[31], (u64)st_ext | ((u64)st_pre << 32));
 #ifdef OWGS_EXT_PROF
         if (io && lane == 0) {
             atomicAdd(&A.stats[28], xp_cyc);

@@ -1,0 +1,21 @@
+#!/bin/bash
+# iteration: the full -m gpu suite of the regular build and its per-config rates; then for each VARIANTS name the
+# stream-parity tests and rates of openwhisk_amd/variants/libowgs_NAME.so
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/it3; mkdir -p $O; export TMPDIR=/tmp
+C=${CFGS:-headline c2 c3 c4 headline:0/8}
+if [ -z "$SKIP_SUITE" ]; then
+  timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
+  rc=$?; tail -2 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
+fi
+REPS=${REPS:-3} timeout -k 10 300 python -u tools/prof_phases.py $C > $O/rates.log 2>&1 || { tail $O/rates.log; exit 1; }
+grep -v amdgpu.ids $O/rates.log | grep -v cycles/activation | cut -c1-150
+for v in $VARIANTS; do
+  echo "== $v"
+  OWGS_LIB=openwhisk_amd/variants/libowgs_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q \
+    --timeout 120 --timeout-method thread -k "stream_parity or full_size or shard" > $O/pytest_$v.log 2>&1
+  rc=$?; tail -1 $O/pytest_$v.log; [ $rc -eq 0 ] || exit $rc
+  OWGS_LIB=openwhisk_amd/variants/libowgs_$v.so REPS=${REPS:-3} timeout -k 10 300 python -u tools/prof_phases.py $C > $O/rates_$v.log 2>&1 || exit 1
+  grep -v amdgpu.ids $O/rates_$v.log | grep -v cycles/activation | cut -c1-110; grep -o "redecided[^,}]*" $O/rates_$v.log | tr "\n" " "; echo
+done
+echo "iter3 done"
