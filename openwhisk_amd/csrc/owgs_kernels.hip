@@ -2298,6 +2298,23 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                 int cap = 0, ci = -1;
                                 uint32_t v = 0;
                                 const bool bad = in && id[q] == OWGS_PW_BADID;
+                                if (rj == 0 && cj == 1) {  // (uniform) rank 0: the first step with room, no scan
+                                    const u64 hm = __ballot(in && (bad || (id[q] >= 0 && pv[q] >= mj)));
+                                    if (hm) {
+                                        const int L = ffs64(hm);
+                                        rst = s0 + 64 * q + L;
+                                        if (__builtin_amdgcn_readlane((int)bad, L)) {
+                                            rk = K_THROW;
+                                        } else {
+                                            rk = K_TARGET;
+                                            rt = __builtin_amdgcn_readlane(id[q], L);
+                                            rks = 0;
+                                        }
+                                        found = true;
+                                        break;
+                                    }
+                                    continue;
+                                }
                                 if (cj == 1) {
                                     cap = (in && id[q] >= 0) ? cap_bf(pv[q], mj, rmj) : 0;
                                 } else if (in && id[q] >= 0) {

@@ -221,6 +221,31 @@ def test_stream_parity_in_pass_redecisions(seed, kw):
     assert b.stats()["redecided"] > 0
 
 
+def test_engine_specialisation_switch():
+    # a context with maxConcurrent == 1 actions only replays on the map-free engine (OWGS_F_*); once a
+    # concurrent action is registered, later calls take the engine with the NestedSemaphore map.  Both streams, and
+    # the state carried from one to the other, stay bit-exact with the oracle.
+    import dataclasses
+    w1 = W.config("c2", n_activations=40_000)
+    w2 = W.config("c4", n_activations=40_000)
+    assert all(a.max_concurrent == 1 for a in w1.actions) and any(a.max_concurrent > 1 for a in w2.actions)
+    keys = {}
+    st = O.state_for(w1, slot_keys=keys)
+    b = gpu_for(w1)
+    for w, stream in ((w1, w1.stream), (w2, dataclasses.replace(w2.stream, act=w2.stream.act + len(w1.actions)))):
+        if w is w2:
+            for a in w2.actions:
+                st.register_action(a.namespace, a.path, keys.setdefault(a.key, len(keys)), a.mem_mb, a.max_concurrent,
+                                   a.blackbox)
+            b.register_actions(w2.actions)
+        o_inv, o_fl, o_rf = st.replay(stream)
+        g_inv, g_fl, g_rf = b.replay(stream)
+        bad = np.nonzero(o_inv != g_inv)[0]
+        assert len(bad) == 0, f"{w.name}: first mismatch at {bad[:5]}"
+        assert np.array_equal(o_fl, g_fl) and np.array_equal(o_rf, g_rf)
+        assert np.array_equal(st.permits(), b.permits())
+
+
 def test_malformed_release_stream_fails_loudly():
     # a stream that releases one activation twice (CommonLoadBalancer never does: activationSlots.remove finds no
     # entry the second time, CLB:278-279) is rejected by the release front end (owgs_relpos_kernel's claim of the
