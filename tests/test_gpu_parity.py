@@ -228,6 +228,8 @@ def test_engine_specialisation_switch():
     import dataclasses
     w1 = W.config("c2", n_activations=40_000)
     w2 = W.config("c4", n_activations=40_000)
+    # (the generators name actions alike: the second set gets its own versions, one set of limits per fqn@version)
+    w2 = dataclasses.replace(w2, actions=[dataclasses.replace(a, version="0.0.2") for a in w2.actions])
     assert all(a.max_concurrent == 1 for a in w1.actions) and any(a.max_concurrent > 1 for a in w2.actions)
     keys = {}
     st = O.state_for(w1, slot_keys=keys)
