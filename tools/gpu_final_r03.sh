@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round-3 evidence for the shipped build.  $PART selects the call (each fits one gpurun limit):
+# Round-3 evidence for the shipped build.  $PART selects the call (each fits one gpurun limit; C + D = A + B plus an
+# A/B of the shipped library against a variant of the previous build):
 #   A: full GPU suite, smoke, HBM traffic (pmc_traffic.json) for every bench key, SQ counters
 #   B: bench line (default args), kernel trace of the bench, per-config lines, per-batch health line, shim-path
 #      kernel trace, per-phase cycles
@@ -7,12 +8,21 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r03; mkdir -p $O; export TMPDIR=/tmp
 stop() { echo "STEP $1 rc=$2 -- stopping"; exit "$2"; }
-if [ "$PART" = A ]; then STEPS=${STEPS:-"tests smoke pmc sq"}; else STEPS=${STEPS:-"bench prof cfgs churn shimprof phases"}; fi
+if [ "$PART" = A ]; then STEPS=${STEPS:-"tests smoke pmc sq"}; elif [ "$PART" = C ]; then STEPS=${STEPS:-"tests ab smoke bench prof cfgs"};
+elif [ "$PART" = D ]; then STEPS=${STEPS:-"pmc sq bench churn shimprof phases"}; else STEPS=${STEPS:-"bench prof cfgs churn shimprof phases"}; fi
 for s in $STEPS; do
   case "$s" in
     tests)
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
       rc=$?; tail -2 $O/pytest_gpu.log; [ $rc -eq 0 ] || stop tests $rc ;;
+    ab)  # rates of the shipped build against $AB_BASE (a variant library of the previous build), same box
+      for lib in openwhisk_amd/libowgs.so openwhisk_amd/variants/libowgs_${AB_BASE:-base}.so; do
+        [ -f "$lib" ] || continue
+        echo "-- $lib"
+        OWGS_LIB=$lib REPS=3 timeout -k 10 300 python -u tools/prof_phases.py c2 c4 headline:0/8 headline > $O/ab.log 2>&1
+        rc=$?; grep -v amdgpu.ids $O/ab.log | grep -v cycles/activation | cut -c1-100; [ $rc -eq 0 ] || stop ab $rc
+        cp $O/ab.log "$O/ab_$(basename $lib .so).log"
+      done ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
       rc=$?; tail -1 $O/smoke.log; [ $rc -eq 0 ] || stop smoke $rc ;;
