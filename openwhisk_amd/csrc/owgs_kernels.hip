@@ -116,12 +116,6 @@ __device__ __forceinline__ uint32_t pre_bit(int x) { return ((uint32_t)x * 0x9E3
 #define FGRP 4  // walk steps per group of the maxConcurrent == 1 fast path (their reads issue together)
 #endif
 #define CAPMAX 1024  // capacities are clamped: a lane's rank is < OWGS_WL
-#ifndef CAP_ROUNDS_L
-#define CAP_ROUNDS_L 3  // long-walk rounds before the capacity bound is summed: pools over 2048 positions
-#endif
-#ifndef CAP_ROUNDS_S
-#define CAP_ROUNDS_S 1  // ... smaller pools (the sum is cheap)
-#endif
 #ifndef LW_Q
 #define LW_Q 2  // walk steps each lane probes per round of a wave-cooperative long walk (2 vs 4: 35.4 vs 36.1 ms
                 // headline, 130 vs 137 ms configs[1], 222 vs 229 ms C5 shard 0 of 8; round 2)
@@ -2249,26 +2243,11 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         ++pw_c[1];
 #endif
                         bool found = false;
-                        int nrd = 0;  // rounds walked
                         while (s0 < nn && !found) {
 #ifdef OWGS_PROFILE
                             ++nr_;
                             const u64 tr0_ = memtime_pinned();
 #endif
-                            // a rank r > 0 still walking after a few rounds (maxConcurrent == 1, identity pool): the
-                            // pool's whole capacity for this memory, the sum of floor(permits / mem) over its usable
-                            // invokers, bounds what the rest of the walk can add; r >= that sum -> the walk fails
-                            // everywhere (SCPB:417) without walking the rest of the pool (a rank-0 walk has U for this)
-                            if (cj == 1 && rj > 0 && pool_mode == 0 && ++nrd == (nn > 2048 ? CAP_ROUNDS_L : CAP_ROUNDS_S)) {
-                                const int base = pj ? A.n_ids - nb : 0;
-                                int c = 0;
-#pragma unroll 4
-                                for (int p = lane; p < nn; p += 64) {
-                                    const int v = P[base + p];
-                                    c += v < OWGS_PLIM ? cap_bf(v, mj, rmj) : 0;  // (usable: flag folded in)
-                                }
-                                if (rj >= __builtin_amdgcn_readlane(wave_incl_scan(c), 63)) break;  // K_FALLBACK
-                            }
                             int pv[LW_Q], id[LW_Q];
                             int p = p0 + loff;
                             if (p >= nn) p -= nn;
