@@ -27,6 +27,11 @@
  *     its index with the counter RNG keyed by (rng_seed, seq) documented in DESIGN.md (replaces ThreadLocalRandom,
  *     SCPB:421).
  *   - One context = one controller shard (SCPB horizontal sharding, SCPB:126-133); contexts are single-writer.
+ *   - Calls on one context take effect in the order they are issued, whatever stream each names: an asynchronous call
+ *     (the *_device functions, owgs_restore, owgs_update_health_device) leaves its work as the context's tail, and
+ *     the next call -- on any stream, or a synchronous one -- is ordered after it on the device.  Device buffers the
+ *     caller passes to an asynchronous call are read when `stream` reaches the call's work: keep them valid (and
+ *     unmodified) until then.
  */
 #ifndef OWGS_H
 #define OWGS_H
@@ -77,6 +82,11 @@ int owgs_create(const owgs_config* cfg, owgs_ctx** out);
 void owgs_destroy(owgs_ctx* ctx);
 const char* owgs_last_error(const owgs_ctx* ctx);
 int owgs_abi_version(void);
+/* Diagnostics (runs without a GPU): each engine object (wide / narrow geometry) refuses a launch prepared for the other
+ * geometry before anything runs -- the launch wrappers compare the host's geometry tag with their own, and the kernels
+ * check it again before their first barrier (a mismatch fails the call with OWGS_EDEVICE, "engine geometry").
+ * OWGS_OK when every wrapper refused. */
+int owgs_geometry_selfcheck(void);
 /* max invokers / slots the engine holds on chip (LDS); larger pools return OWGS_ERANGE from update_invokers */
 int owgs_limits(int32_t* max_invokers, int32_t* max_slots);
 
@@ -101,6 +111,15 @@ int owgs_register_actions(owgs_ctx* ctx, int32_t n, const char* ns_bytes, const 
                           const char* path_bytes, const int32_t* path_off, const char* key_bytes,
                           const int32_t* key_off, const int32_t* mem_mb, const int32_t* max_conc,
                           const uint8_t* blackbox, int32_t* out_action, int32_t* out_hash);
+
+/* Replaces the reference's NestedSemaphore map lifetime (NestedSemaphore.scala:109-111: an entry exists only while
+ * activations of its fqn@version are in flight; nothing else is keyed by it).  The caller drops action handles it will
+ * not name again (a cold action, a superseded fqn@version): none of their activations may still be in flight and no
+ * later call may name them.  Handle ids are reused by later owgs_register_actions calls; an fqn@version key that no
+ * live handle names is recycled when registrations run out of key ids, once no map entry and no watched pair holds it
+ * (a device scan; keys still held stay pending).  A restore of a snapshot taken before a key was recycled returns
+ * OWGS_EINVAL.  With this a long-running controller never runs out of the 131,070 key / 131,070 handle ids. */
+int owgs_release_actions(owgs_ctx* ctx, int32_t n, const int32_t* actions);
 
 /* Replaces: the scheduling half of ShardingContainerPoolBalancer.publish (SCPB:257-290) -- pool selection, hash,
  * home invoker, step size and ShardingContainerPoolBalancer.schedule (SCPB:398-436) with NestedSemaphore
@@ -326,7 +345,9 @@ int owgs_snapshot(owgs_ctx* ctx);
 int owgs_restore(owgs_ctx* ctx, void* stream);
 
 /* Health all-gather hook (RCCL over xGMI, done by the caller): overwrite the status vector from a device buffer of
- * n bytes (InvokerState codes), e.g. the rank-0 row of an all_gather of CurrentInvokerPoolState. */
+ * n bytes (InvokerState codes), e.g. the rank-0 row of an all_gather of CurrentInvokerPoolState.  Asynchronous on
+ * `stream` for identity pools (the status bytes are copied and the usable bitmap rebuilt there; status_dev must stay
+ * valid until `stream` reaches the copy); later calls on any stream see the new health (see Conventions). */
 int owgs_update_health_device(owgs_ctx* ctx, int32_t n, const uint8_t* status_dev, void* stream);
 
 /* Device self-test of the engine's wave primitives (DPP scans/reductions vs a serial computation); 0 = pass. */

@@ -51,28 +51,29 @@ object OwgsNative {
   @native def updateCluster(ctx: Long, size: Int): Int
   @native def registerAction(ctx: Long, namespace: String, path: String, key: String, memMb: Int, maxConc: Int,
                              blackbox: Boolean): Int
-  /** owgs_process_batch over direct buffers (native byte order), layout in BatchBuffers. */
-  @native def processBatch(ctx: Long, in: ByteBuffer, out: ByteBuffer, nRuns: Int, nRel: Int, nPub: Int): Int
+  /** owgs_process_batch over direct buffers (native byte order), layout in BatchBuffers; the publishes' overload-RNG
+   *  sequence numbers are seqBase, seqBase + 1, ... in queue order. */
+  @native def processBatch(ctx: Long, in: ByteBuffer, out: ByteBuffer, nRuns: Int, nRel: Int, nPub: Int,
+                           seqBase: Long): Int
+  /** owgs_release_actions: handles of cold fqn@version keys (none of their activations in flight) */
+  @native def releaseActions(ctx: Long, handles: Array[Int], n: Int): Int
   @native def lastError(ctx: Long): String
 }
 
 /** The direct buffers of one drained batch (owgs_jni.c processBatch reads the same layout):
- *  in  = relOff[nRuns + 1], pubOff[nRuns + 1], relInvoker[nRel], relAction[nRel], pubAction[nPub] (ints), then
- *        seq[nPub] (longs, 8-byte aligned);
+ *  in  = relOff[nRuns + 1], pubOff[nRuns + 1], relInvoker[nRel], relAction[nRel], pubAction[nPub] (ints);
  *  out = outInvoker[nPub] (ints), outFlags[nPub], relFlags[nRel] (bytes). */
 final class BatchBuffers {
   var in: ByteBuffer = ByteBuffer.allocateDirect(1 << 16).order(ByteOrder.nativeOrder())
   var out: ByteBuffer = ByteBuffer.allocateDirect(1 << 15).order(ByteOrder.nativeOrder())
   def ensure(nRuns: Int, nRel: Int, nPub: Int): Unit = {
-    val ints = 2 * (nRuns + 1) + 2 * nRel + nPub
-    val inBytes = ((4L * ints + 7) & ~7L) + 8L * nPub
+    val inBytes = 4L * (2 * (nRuns + 1) + 2 * nRel + nPub)
     val outBytes = 4L * nPub + nPub + nRel
     if (inBytes > in.capacity) in = ByteBuffer.allocateDirect((2 * inBytes).toInt).order(ByteOrder.nativeOrder())
     if (outBytes > out.capacity) out = ByteBuffer.allocateDirect((2 * outBytes).toInt).order(ByteOrder.nativeOrder())
     in.clear()
     out.clear()
   }
-  def seqOffset(nRuns: Int, nRel: Int, nPub: Int): Int = ((4 * (2 * (nRuns + 1) + 2 * nRel + nPub)) + 7) & ~7
 }
 
 class GpuShardingContainerPoolBalancer(config: WhiskConfig,
@@ -110,36 +111,45 @@ class GpuShardingContainerPoolBalancer(config: WhiskConfig,
   private val blackboxFraction: Double = Math.max(1.0 - managedFraction, Math.min(1.0, lbConfig.blackboxFraction))
 
   // (invoking namespace, fqn@version) -> native action handle (registered once); fqn@version -> a handle of that
-  // action for releases (a release only needs the NestedSemaphore key and the limits, NS:98-113)
+  // action for releases (a release only needs the NestedSemaphore key and the limits, NS:98-113).  Per key: the
+  // handles naming it, its activations in flight and the last batch that used it; keys idle for keyIdleBatches with
+  // nothing in flight give their handles back (owgs_release_actions), as the reference's NestedSemaphore drops the
+  // key's entries at operationCount 0 (NestedSemaphore.scala:109-111): every action update bumps the version, so the
+  // set of keys a controller sees over its lifetime is unbounded.
   private val handles = mutable.HashMap.empty[(String, String), Int]
   private val byKey = mutable.HashMap.empty[String, Int]
+  private final class KeyUse(var inFlight: Int, var lastBatch: Long, val names: mutable.ArrayBuffer[(String, String)])
+  private val keyUse = mutable.HashMap.empty[String, KeyUse]
+  private var batchNo = 0L
+  private val keyIdleBatches = cfgInt("whisk.loadbalancer.gpu.key-idle-batches", 100000).toLong
 
   /** The invoker list the engine schedules against, its pools (SCPB:518-523) and userMemory by id, published by the
    *  batching thread right after owgs_update_invokers succeeded (so a decision and the InvokerInstanceId it returns
    *  come from the same list, as schedule() takes both from `invokers(index)`, SCPB:411-414). */
   private final case class Pools(all: IndexedSeq[InvokerHealth], managed: IndexedSeq[InvokerHealth],
-                                 blackbox: IndexedSeq[InvokerHealth], memById: Array[ByteSize])
+                                 blackbox: IndexedSeq[InvokerHealth], byId: Array[InvokerInstanceId])
   @volatile private var pools = Pools(IndexedSeq.empty, IndexedSeq.empty, IndexedSeq.empty, Array.empty)
   @volatile private var _clusterSize = 1
 
   private def poolsOf(s: IndexedSeq[InvokerHealth]): Pools = {
     val managed = Math.max(1, Math.ceil(s.size.toDouble * managedFraction).toInt)
     val blackboxes = Math.max(1, Math.floor(s.size.toDouble * blackboxFraction).toInt)
-    val mem = new Array[ByteSize](if (s.isEmpty) 0 else s.map(_.id.toInt).max + 1)
-    java.util.Arrays.fill(mem.asInstanceOf[Array[AnyRef]], 0.B)
-    s.foreach(h => mem(h.id.toInt) = h.id.userMemory)
-    Pools(s, s.take(managed), s.takeRight(blackboxes), mem)
+    // the pool's own InvokerInstanceId by id: schedule() returns invokers(index).id (SCPB:411-414), uniqueName and
+    // displayedName included (InstanceId.scala:31-37)
+    val byId = new Array[InvokerInstanceId](if (s.isEmpty) 0 else s.map(_.id.toInt).max + 1)
+    s.foreach(h => byId(h.id.toInt) = h.id)
+    Pools(s, s.take(managed), s.takeRight(blackboxes), byId)
   }
 
   private sealed trait Job
-  private case class Pub(action: ExecutableWhiskActionMetaData, msg: ActivationMessage, seq: Long,
+  private case class Pub(action: ExecutableWhiskActionMetaData, msg: ActivationMessage,
                          p: Promise[Option[(InvokerInstanceId, Boolean)]]) extends Job
   private case class Rel(invoker: InvokerInstanceId, entry: ActivationEntry) extends Job
   private case class Inv(state: IndexedSeq[InvokerHealth]) extends Job
   private case class Clu(size: Int) extends Job
 
   private val queue = new ArrayBlockingQueue[Job](1 << 16)
-  private var seqNo = 0L
+  private var seqNo = 0L  // overload-RNG sequence numbers, given in queue order by the batching thread
   private val bufs = new BatchBuffers
 
   private def nativeError(what: String, rc: Int): LoadBalancerException =
@@ -205,11 +215,10 @@ class GpuShardingContainerPoolBalancer(config: WhiskConfig,
     planned.foreach(_._1.foreach(r => in.put(r.invoker.toInt)))
     planned.foreach(_._1.foreach(r => in.put(byKey(r.entry.fullyQualifiedEntityName.asString))))
     planned.foreach(_._2.foreach { case (_, h) => in.put(h) })
-    val seqs = bufs.in.duplicate().order(ByteOrder.nativeOrder())
-    seqs.position(bufs.seqOffset(nRuns, nRel, nPub))
-    val seqBuf = seqs.slice().order(ByteOrder.nativeOrder()).asLongBuffer()
-    planned.foreach(_._2.foreach { case (p, _) => seqBuf.put(p.seq) })
-    val rc = OwgsNative.processBatch(ctx, bufs.in, bufs.out, nRuns, nRel, nPub)
+    // overload-RNG sequence numbers in queue order (the engine's counter RNG replaces ThreadLocalRandom, SCPB:421)
+    val seqBase = seqNo
+    seqNo += nPub
+    val rc = OwgsNative.processBatch(ctx, bufs.in, bufs.out, nRuns, nRel, nPub, seqBase)
     val pubsInOrder = planned.flatMap(_._2.map(_._1))
     if (rc < 0) {
       val e = nativeError("owgs_process_batch", rc)
@@ -218,14 +227,19 @@ class GpuShardingContainerPoolBalancer(config: WhiskConfig,
       return
     }
     val out = bufs.out
-    val mem = pools.memById
+    val byId = pools.byId
     var k = 0
     while (k < nPub) {
       val p = pubsInOrder(k)
       val id = out.getInt(4 * k)
       val overload = (out.get(4 * nPub + k) & 1) != 0
-      if (id >= 0) p.p.success(Some((InvokerInstanceId(id, userMemory = if (id < mem.length) mem(id) else 0.B), overload)))
-      else if (id == -2) // the reference's schedule() throws here (Int.MinValue hash or an id outside invokerSlots)
+      if (id >= 0) {
+        val invoker = if (id < byId.length && byId(id) != null) byId(id) else InvokerInstanceId(id, userMemory = 0.B)
+        if (overload) // SCPB:423 (logged where schedule() forces the random healthy invoker)
+          logging.warn(this, s"system is overloaded. Chose invoker${id} by random assignment.")(p.msg.transid)
+        keyUse.get(p.action.fullyQualifiedName(true).asString).foreach(_.inFlight += 1)
+        p.p.success(Some((invoker, overload)))
+      } else if (id == -2) // the reference's schedule() throws here (Int.MinValue hash or an id outside invokerSlots)
         p.p.failure(new IndexOutOfBoundsException(s"schedule: invoker index out of range for activation ${p.msg.activationId}"))
       else p.p.success(None)
       k += 1
@@ -235,12 +249,31 @@ class GpuShardingContainerPoolBalancer(config: WhiskConfig,
     while (r < nRel) {
       val f = out.get(5 * nPub + r)
       val e = known(r).entry
+      keyUse.get(e.fullyQualifiedEntityName.asString).foreach(_.inFlight -= 1)
       if ((f & 1) != 0) // NS:103: concurrentSlotsMap(actionid) on a missing key
         logging.error(this, s"releaseInvoker: NoSuchElementException: key not found: ${e.fullyQualifiedEntityName}")
       if ((f & 2) != 0) // FS:48-50
         logging.error(this, s"releaseInvoker: Error: Maximum permit count exceeded (invoker ${known(r).invoker.toInt})")
       r += 1
     }
+    batchNo += 1
+    if (batchNo % 1024 == 0) dropColdKeys()
+  }
+
+  /** Keys idle for keyIdleBatches with no activation in flight: their handles go back to the engine
+   *  (owgs_release_actions), which recycles handle and key ids; a later publish registers the action again. */
+  private def dropColdKeys(): Unit = {
+    val cold = keyUse.filter { case (_, u) => u.inFlight <= 0 && batchNo - u.lastBatch > keyIdleBatches }
+    if (cold.isEmpty) return
+    val hs = cold.values.flatMap(_.names.flatMap(handles.get)).toArray
+    val rc = OwgsNative.releaseActions(ctx, hs, hs.length)
+    if (rc < 0) logging.error(this, s"releaseActions: ${nativeError("owgs_release_actions", rc).getMessage}")
+    else
+      cold.foreach { case (key, u) =>
+        u.names.foreach(handles.remove)
+        byKey.remove(key)
+        keyUse.remove(key)
+      }
   }
 
   /** The single writer of the native context: drains the queue in batches (stream order is the sequential order).
@@ -258,7 +291,7 @@ class GpuShardingContainerPoolBalancer(config: WhiskConfig,
             logging.error(this, s"owgs batcher: $t")
             val e = LoadBalancerException(s"scheduling batch failed: $t")
             jobs.forEach {
-              case Pub(_, _, _, p) => p.tryFailure(e)
+              case Pub(_, _, p) => p.tryFailure(e)
               case _               =>
             }
         }
@@ -277,18 +310,22 @@ class GpuShardingContainerPoolBalancer(config: WhiskConfig,
   }
 
   /** Native handle of an action (registered on first use); a negative owgs error code is returned, not cached. */
-  private def handleOf(ns: String, fqn: FullyQualifiedEntityName, memMb: Int, maxConc: Int, blackbox: Boolean): Int =
-    handles.get((ns, fqn.asString)) match {
+  private def handleOf(ns: String, fqn: FullyQualifiedEntityName, memMb: Int, maxConc: Int, blackbox: Boolean): Int = {
+    val key = fqn.asString
+    val h = handles.get((ns, key)) match {
       case Some(h) => h
       case None =>
-        val h = OwgsNative.registerAction(ctx, ns, fqn.copy(version = None).asString, fqn.asString, memMb, maxConc,
-          blackbox)
+        val h = OwgsNative.registerAction(ctx, ns, fqn.copy(version = None).asString, key, memMb, maxConc, blackbox)
         if (h >= 0) {
-          handles.update((ns, fqn.asString), h)
-          byKey.getOrElseUpdate(fqn.asString, h)
+          handles.update((ns, key), h)
+          byKey.getOrElseUpdate(key, h)
+          keyUse.getOrElseUpdate(key, new KeyUse(0, batchNo, mutable.ArrayBuffer.empty)).names += ((ns, key))
         }
         h
     }
+    keyUse.get(key).foreach(_.lastBatch = batchNo)
+    h
+  }
 
   /** SCPB:169-205: capacity and health gauges of both pools, from the list the engine schedules against. */
   override protected def emitMetrics() = {
@@ -345,8 +382,7 @@ class GpuShardingContainerPoolBalancer(config: WhiskConfig,
     val isBlackboxInvocation = action.exec.pull
     val actionType = if (!isBlackboxInvocation) "managed" else "blackbox"
     val p = Promise[Option[(InvokerInstanceId, Boolean)]]()
-    val s = synchronized { seqNo += 1; seqNo }
-    queue.put(Pub(action, msg, s, p))
+    queue.put(Pub(action, msg, p))
     p.future.flatMap {
       case Some((invoker, overload)) =>
         if (overload)

@@ -107,17 +107,17 @@ JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00
 }
 
 /* One drained batch (owgs_process_batch) over direct buffers, layout as BatchBuffers in the Scala shim:
- * in  = rel_off[n_runs + 1], pub_off[n_runs + 1], rel_invoker[n_rel], rel_action[n_rel], pub_action[n_pub] (int32),
- *       then seq[n_pub] (int64, 8-byte aligned);  out = out_invoker[n_pub] (int32), out_flags[n_pub], rel_flags[n_rel]. */
+ * in  = rel_off[n_runs + 1], pub_off[n_runs + 1], rel_invoker[n_rel], rel_action[n_rel], pub_action[n_pub] (int32);
+ * out = out_invoker[n_pub] (int32), out_flags[n_pub], rel_flags[n_rel].  The publishes' overload-RNG sequence numbers
+ * are seq_base, seq_base + 1, ... (the shim numbers them in queue order). */
 JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_processBatch(
-    JNIEnv* env, jobject self, jlong h, jobject in, jobject out, jint n_runs, jint n_rel, jint n_pub) {
+    JNIEnv* env, jobject self, jlong h, jobject in, jobject out, jint n_runs, jint n_rel, jint n_pub, jlong seq_base) {
     if (!in || !out || n_runs < 0 || n_rel < 0 || n_pub < 0) return OWGS_EINVAL;
     char* pi = (char*)(*env)->GetDirectBufferAddress(env, in);
     char* po = (char*)(*env)->GetDirectBufferAddress(env, out);
     if (!pi || !po) return OWGS_EINVAL;  /* not direct buffers */
     const jlong ints = 2 * ((jlong)n_runs + 1) + 2 * (jlong)n_rel + (jlong)n_pub;
-    const jlong seq_at = (4 * ints + 7) & ~(jlong)7;
-    if ((*env)->GetDirectBufferCapacity(env, in) < seq_at + 8 * (jlong)n_pub ||
+    if ((*env)->GetDirectBufferCapacity(env, in) < 4 * ints ||
         (*env)->GetDirectBufferCapacity(env, out) < 5 * (jlong)n_pub + (jlong)n_rel)
         return OWGS_EINVAL;
     const int32_t* rel_off = (const int32_t*)pi;
@@ -125,10 +125,19 @@ JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00
     const int32_t* rel_inv = pub_off + n_runs + 1;
     const int32_t* rel_act = rel_inv + n_rel;
     const int32_t* pub_act = rel_act + n_rel;
-    const uint64_t* seq = (const uint64_t*)(pi + seq_at);
     if (n_runs > 0 && (rel_off[n_runs] != n_rel || pub_off[n_runs] != n_pub)) return OWGS_EINVAL;
     return owgs_process_batch(CTX(h), n_runs, rel_off, rel_inv, rel_act, (uint8_t*)(po + 5 * (jlong)n_pub), pub_off,
-                              pub_act, seq, 0, (int32_t*)po, (uint8_t*)(po + 4 * (jlong)n_pub));
+                              pub_act, NULL, (uint64_t)seq_base, (int32_t*)po, (uint8_t*)(po + 4 * (jlong)n_pub));
+}
+
+/* handles of cold fqn@version keys (owgs_release_actions) */
+JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_releaseActions(
+    JNIEnv* env, jobject self, jlong h, jintArray handles, jint n) {
+    if (!handles || !n_fits(env, n, handles, NULL, NULL, NULL)) return OWGS_EINVAL;
+    int32_t* ph = jcopy_in(env, handles, n, 4, 'I');
+    const int rc = ph ? owgs_release_actions(CTX(h), n, ph) : OWGS_ENOMEM;
+    free(ph);
+    return rc;
 }
 
 JNIEXPORT jint JNICALL Java_org_apache_openwhisk_core_loadBalancer_OwgsNative_00024_publishBatch(

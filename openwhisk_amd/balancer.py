@@ -331,6 +331,12 @@ class GpuShardingContainerPoolBalancer:
                                                 _p(mem), _p(mc), _p(bb), _p(out), _p(hs)))
         return out[:n], hs[:n]
 
+    def release_actions(self, handles) -> None:
+        """Drop action handles no later call names (owgs_release_actions): their ids and unused fqn@version keys are
+        reused by later registrations."""
+        h = np.ascontiguousarray(handles, dtype=np.int32)
+        self._chk(self._L.owgs_release_actions(self._h, len(h), _p(h if len(h) else np.zeros(1, np.int32))))
+
     def key_id(self, action: int) -> int:
         return self._chk(self._L.owgs_key_id(self._h, action))
 
@@ -449,8 +455,8 @@ class GpuShardingContainerPoolBalancer:
         self._chk(self._L.owgs_selftest(self._h))
 
     def stats(self) -> dict:
-        out = (C.c_uint64 * 32)()
-        self._chk(self._L.owgs_read_stats(self._h, out, 32))
+        out = (C.c_uint64 * 48)()
+        self._chk(self._L.owgs_read_stats(self._h, out, 48))
         d = {"passes": out[0], "probes": out[1], "fallbacks": out[2], "long_walks": out[3], "chunks": out[4],
              "stops": out[5], "general_probes": out[6], "general_lanes": out[7], "redecided": out[31] & 0xFFFFFFFF}
         if out[31] >> 32:
@@ -471,4 +477,5 @@ class GpuShardingContainerPoolBalancer:
             d["walks"].update({k: out[28 + i] for i, k in enumerate(walk[10:])})
             d["cycles"]["rel_sweep"] = out[26]
             d["cycles"]["ct_rebuild"] = out[27]
+            d["kernel_cycles"] = {"state_load": out[40], "batches": out[41], "write_back": out[42]}
         return d

@@ -65,6 +65,9 @@ __global__ __launch_bounds__(256) void owgs_stage_releases_kernel(OwgsStageArgs 
                                         (uint32_t)a.act_slot[act] | ((uint32_t)a.act_maxc[act] << 17));
             a.rel_src[pos] = (int32_t)i;
             a.rel_flags[i] = inv < 0 ? OWGS_REL_NOENTRY_BIT : 0;  // no ActivationEntry (CLB:278-279)
+            // what the releases can return per slot at most (every release its memory: a concurrent one returns it
+            // when its container empties): the engine refuses the call when a slot could leave its LDS range
+            if (a.bound && in) atomicAdd(&a.bound[inv], (unsigned long long)a.act_mem[act]);
         }
         base0 += s0;
         base1 += s1;

@@ -45,6 +45,9 @@ extern "C" hipError_t owgs_launch_slots(const int64_t* mem_bytes, int32_t from, 
                                        int64_t min_bytes, int32_t* permits, hipStream_t s);
 extern "C" hipError_t owgs_launch_usable(const uint8_t* status, int32_t n, uint32_t* bits, int32_t n_words,
                                         hipStream_t s);
+extern "C" hipError_t owgs_launch_slot_scan(const uint32_t* ct_keys, const uint2* ovf, int32_t ovf_cap,
+                                           const uint32_t* w_keys, int32_t w_cap, const int32_t* wkey, uint32_t* cand,
+                                           hipStream_t s);
 extern "C" hipError_t owgs_launch_ack_parse(const OwgsAckParseArgs* a, hipStream_t st);
 extern "C" hipError_t owgs_launch_aid_decode(const char* aid32, int32_t n, const uint8_t* cflags, ulonglong2* key,
                                              uint8_t* info, int32_t* inst, const int32_t* inv, hipStream_t st);
@@ -166,9 +169,16 @@ struct owgs_ctx {
 
     // actions
     std::vector<int32_t> a_mem, a_maxc, a_slot, a_hash;
-    std::vector<uint8_t> a_bb, a_cok;
-    std::vector<int32_t> slot_uses, slot_maxc, slot_mem;
+    std::vector<uint8_t> a_bb, a_cok, a_live;
+    std::vector<int32_t> free_handles;  // released action handles (owgs_release_actions), reused by registrations
+    std::vector<int32_t> slot_uses, slot_maxc, slot_mem;  // per fqn@version key: live handles naming it, its limits
+    std::vector<std::string> slot_name;
     std::unordered_map<std::string, int32_t> slot_ids;
+    // keys no live handle names: recycled (slot id reused) once no map entry and no watched pair names them any more,
+    // checked on the device when registrations run out of ids (reclaim_slots); slot_epoch counts recycled keys
+    std::vector<int32_t> pending_slots, free_slots;
+    int64_t slot_epoch = 0, snap_slot_epoch = 0;
+    DevBuf<uint32_t> d_cand;
 
     // device state
     DevBuf<int32_t> d_permits, d_pool_words, d_hlist, d_act_slot, d_act_hash, d_act_mem, d_act_maxc, d_steps,
@@ -196,6 +206,11 @@ struct owgs_ctx {
     // the host mirror (status, healthy counts) is downloaded when a host path needs it (ev_status: the copy)
     bool status_stale = false;
     hipEvent_t ev_status = nullptr;
+    // calls on one context are ordered as issued, whatever stream each names: ev_tail marks the end of the last
+    // asynchronous call's work (on tail_stream); later work on another stream waits for it (order_on / tail_mark)
+    hipEvent_t ev_tail = nullptr;
+    hipStream_t tail_stream = nullptr;
+    bool tail_valid = false;
     int32_t s_ovf_cnt = 0;    // snapshot: overflow entries (0: the snapshot had none)
     int32_t s_ovf_cap = 0;
     DevBuf<uint32_t> d_margs;  // owgs_replay_device_multi: shard argument blocks beyond the kernarg segment
@@ -260,6 +275,7 @@ struct owgs_ctx {
     DevBuf<int64_t> w_off;
     DevBuf<uint8_t> w_rfl;
     int32_t w_cap = 0, w_live = 0;
+    int32_t stats_par = 0, stats_last = 0;  // d_stats holds two counter blocks: the next launch's, the last one's
     int32_t cw_cache = 0;  // chunk width of the current state and actions (0: recompute)
     bool any_conc = false;  // some registered action has maxConcurrent > 1 (the engine needs its map code)
     int32_t variant = 0;   // engine geometry: 0 wide chunks, 1 narrow (large pools, owgs_engine_narrow.hip)
@@ -271,6 +287,7 @@ struct owgs_ctx {
     DevBuf<uint8_t> d_pin, d_pout;
     DevBuf<int32_t> f_src, f_cnt, f_tile;
     DevBuf<uint2> f_rec;
+    DevBuf<unsigned long long> f_bound;  // per slot: what a fused call's releases can return (zero between calls)
     DevBuf<uint32_t> s_w_keys, s_w_vals;
     DevBuf<int32_t> s_w_wkey;
     int32_t s_w_cap = 0, s_w_live = 0;
@@ -314,6 +331,22 @@ static int sync_status(owgs_ctx* c) {
     if (!c->status.empty())
         HIPCHK(c, hipMemcpy(c->status.data(), c->d_status.p, c->status.size(), hipMemcpyDeviceToHost));
     c->status_stale = false;
+    return OWGS_OK;
+}
+
+// make stream s wait for the work of the last asynchronous call when that ran on another stream (the caller may
+// free or reuse nothing of ours meanwhile: every buffer an earlier call reads belongs to the context or stays the
+// caller's until its stream reaches it, include/owgs.h)
+static int order_on(owgs_ctx* c, hipStream_t s) {
+    if (c->tail_valid && c->tail_stream != s) HIPCHK(c, hipStreamWaitEvent(s, c->ev_tail, 0));
+    return OWGS_OK;
+}
+// the work this asynchronous call enqueued on s is the context's new tail
+static int tail_mark(owgs_ctx* c, hipStream_t s) {
+    if (!c->ev_tail) HIPCHK(c, hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(c->ev_tail, s));
+    c->tail_stream = s;
+    c->tail_valid = true;
     return OWGS_OK;
 }
 
@@ -433,6 +466,12 @@ static OwgsOvf ovf_args(const owgs_ctx* c) {
 // The overflow holds every key the primary cannot: at most the entries it has plus one per activation of the call
 // (an activation creates at most one (invoker, fqn) entry).  Keep it at least twice that (load <= 1/2); grow (and
 // rehash) when the bound says so -- after reading the exact entry count back once.
+// n more activations may add overflow entries: the bound grows, and so does what an outstanding count probe misses
+static void ovf_add(owgs_ctx* c, int64_t n) {
+    c->ovf_used_ub += n;
+    if (c->ovf_probe) c->ovf_since += n;
+}
+
 static int ensure_ovf(owgs_ctx* c, int64_t n_new, hipStream_t s) {
     auto need = [&](int64_t used) {
         // (at least 2^19 entries, 12 MB with its scratch: the per-launch bound then runs out only every ~250k
@@ -622,8 +661,13 @@ static int32_t chunk_width(owgs_ctx* c) {
     const int32_t nm = std::min<int32_t>(c->nm, (int32_t)c->mem.size());
     for (int32_t i = 0; i < nm; ++i)
         slot_mb += (double)std::max<int64_t>(c->cfg.min_memory_bytes, c->mem[i] / std::max(c->cluster, 1)) / 1048576.0;
-    for (int32_t m : c->a_mem) act_mb += m;
-    const double units = c->a_mem.empty() || act_mb <= 0 ? 1e9 : slot_mb / (act_mb / (double)c->a_mem.size());
+    int64_t live = 0;
+    for (size_t a = 0; a < c->a_mem.size(); ++a)
+        if (c->a_live[a]) {
+            act_mb += c->a_mem[a];
+            ++live;
+        }
+    const double units = live == 0 || act_mb <= 0 ? 1e9 : slot_mb / (act_mb / (double)live);
     // (with in-pass re-decisions, round 2: configs[1] 19k units 116 ms at 192 vs 119 at 128; configs[3] 221 vs 232;
     // C5 shard of 8 165 vs 173; C5 shard of 4, 34k units: 102 ms at 256 vs 106 at 192 and 117 at 128)
     int32_t cw = units >= OWGS_WIDE_UNITS ? OWGS_WL : std::min(units >= OWGS_WIDE_UNITS / 2 ? 256 : 192, OWGS_WL);
@@ -653,6 +697,7 @@ static int run_prepass(owgs_ctx* c, OwgsEngineArgs& A, int32_t n_batches, const 
     const int64_t max_chunks = n_act / cw + n_batches;
     p.cw = cw;
     A.cw = cw;
+    p.geom = A.geom = OWGS_GEOM_TAG(wl);  // the geometry d_lix and the records below are sized for
     // lane dealing: concurrent lanes packed into the back waves for large pools (their waves then run only the
     // concurrent path: 10k invokers 33.9 vs 37.5 ms), spread over every wave for small pools, where concurrent walks
     // are long (1k invokers, 30 % concurrent: 553 vs 681 ms)
@@ -678,7 +723,7 @@ static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s, bool launch
     if (c->any_conc || (A.feat & OWGS_F_CONC)) {
         rc = ensure_ovf(c, A.n_act, s);
         if (rc) return rc;
-        c->ovf_used_ub += A.n_act;
+        ovf_add(c, A.n_act);
     }
     A.ovf = ovf_args(c);
     A.ct_tmp = c->d_ct_tmp.p;
@@ -693,7 +738,11 @@ static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s, bool launch
     A.gcur = c->d_gcur.p;
     A.cur_tag0 = c->cur_tag;
     c->cur_tag += A.n_batches;
-    HIPCHK(c, hipMemsetAsync(c->d_stats.p, 0, OWGS_NSTATS * sizeof(u64), s));
+    // counters: two blocks used in turn; each launch zeroes the other one at its end (no fill launch per call)
+    A.stats = c->d_stats.p + (size_t)c->stats_par * OWGS_NSTATS;
+    A.stats_next = c->d_stats.p + (size_t)(c->stats_par ^ 1) * OWGS_NSTATS;
+    c->stats_last = c->stats_par;
+    c->stats_par ^= 1;
     if (!c->ev_engine[0]) {
         HIPCHK(c, hipEventCreate(&c->ev_engine[0]));
         HIPCHK(c, hipEventCreate(&c->ev_engine[1]));
@@ -702,6 +751,7 @@ static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s, bool launch
     // overflow can only come from such actions), the general pool / sequence code when the call needs it
     A.feat |= (c->any_conc ? OWGS_F_CONC : 0) | ((c->pool_mode != 0 || A.seq != nullptr) ? OWGS_F_GEN : 0);
     if (env_opts().feat_all) A.feat = OWGS_F_ALL;  // diagnostics: always the general engine
+    A.geom = OWGS_GEOM_TAG(variant_wl(c));
     if (!launch) return OWGS_OK;  // owgs_replay_device_multi launches every shard's engine at once
     HIPCHK(c, hipEventRecord(c->ev_engine[0], s));  // brackets exactly the engine launch (owgs_engine_ms)
     HIPCHK(c, launch_engine(c, &A, s));
@@ -714,9 +764,7 @@ static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s, bool launch
             HIPCHK(c, hipMemcpyAsync(c->h_ovf_cnt, c->d_ovf_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
             HIPCHK(c, hipEventRecord(c->ev_ovf, s));
             c->ovf_probe = true;
-            c->ovf_since = 0;
-        } else {
-            c->ovf_since += A.n_act;
+            c->ovf_since = 0;  // (the copy follows this launch: its count includes it)
         }
     }
     if (A.trace) {  // diagnostic timeline: raw u64 pairs, [waves][16384][2]
@@ -777,6 +825,7 @@ static int check_err_word(owgs_ctx* c) {
         HIPCHK(c, hipMemset(c->d_err.p, 0, sizeof(int32_t)));
         if (e & OWGS_ERR_CTAB_FULL) return c->fail(OWGS_ENOMEM, "concurrency table full");
         if (e & OWGS_ERR_OPS) return c->fail(OWGS_ERANGE, "operationCount beyond the engine's range");
+        if (e & OWGS_ERR_GEOM) return c->fail(OWGS_EDEVICE, "engine object and host disagree on the engine geometry");
         if (e & OWGS_ERR_INTERNAL) return c->fail(OWGS_EDEVICE, "engine invariant violated");
         if (e & OWGS_ERR_PERMITS) return c->fail(OWGS_ERANGE, "slot permits outside the engine's range [-2^29, 2^29) MB");
         return c->fail(OWGS_EINVAL, "stream releases an activation that holds no slot (or a permit overflow)");
@@ -787,13 +836,72 @@ static int check_err_word(owgs_ctx* c) {
 static bool registered(const owgs_ctx* c, int32_t n, const int32_t* action) {
     const int32_t na = (int32_t)c->a_mem.size();
     for (int32_t i = 0; i < n; ++i)
-        if (action[i] < 0 || action[i] >= na) return false;
+        if (action[i] < 0 || action[i] >= na || !c->a_live[action[i]]) return false;
     return true;
+}
+
+// Keys without live handles whose ids can be reused: no entry of the NestedSemaphore map (primary table, HBM overflow)
+// and no watched pair names them any more -- the reference's map loses an entry at operationCount 0
+// (NestedSemaphore.scala:109-111), so a key whose activations have all completed leaves nothing behind.  One scan
+// over the tables on the device; keys still named stay pending for a later attempt.
+static int reclaim_slots(owgs_ctx* c) {
+    if (c->pending_slots.empty()) return OWGS_OK;
+    const size_t words = ((size_t)OWGS_MAX_SLOTKEYS + 32) / 32;
+    std::vector<uint32_t> cand(words, 0u);
+    size_t k = 0;
+    for (int32_t sid : c->pending_slots)
+        if (c->slot_uses[sid] == 0) cand[sid >> 5] |= 1u << (sid & 31);  // (re-registered keys dropped out)
+    HIPCHK(c, upload(c->d_cand, cand.data(), words, c->stream));
+    int32_t ovf_n = 0;
+    if (c->ovf_cap > 0) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipMemcpy(&ovf_n, c->d_ovf_cnt.p, sizeof(ovf_n), hipMemcpyDeviceToHost));
+    }
+    HIPCHK(c, owgs_launch_slot_scan(c->d_ct_keys.p, ovf_n > 0 ? c->d_ovf.p : nullptr, ovf_n > 0 ? c->ovf_cap : 0,
+                                    c->w_cap > 0 ? c->w_keys.p : nullptr, c->w_cap, c->w_cap > 0 ? c->w_wkey.p : nullptr,
+                                    c->d_cand.p, c->stream));
+    HIPCHK(c, hipMemcpyAsync(cand.data(), c->d_cand.p, words * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::vector<int32_t> still;
+    for (int32_t sid : c->pending_slots) {
+        if (c->slot_uses[sid] != 0) continue;  // named by a live handle again
+        if ((cand[sid >> 5] >> (sid & 31)) & 1u) {
+            c->slot_ids.erase(c->slot_name[sid]);
+            std::string().swap(c->slot_name[sid]);
+            c->free_slots.push_back(sid);
+            ++c->slot_epoch;
+            ++k;
+        } else {
+            still.push_back(sid);
+        }
+    }
+    c->pending_slots.swap(still);
+    (void)k;
+    return OWGS_OK;
 }
 
 extern "C" {
 
 int owgs_abi_version(void) { return OWGS_ABI_VERSION; }
+
+// Diagnostics: both engine objects refuse a launch prepared for the other geometry before anything runs (the launch
+// wrappers compare the geometry tag; no device is touched, so this runs without a GPU).  OWGS_OK when every wrapper
+// refused, OWGS_EDEVICE naming the one that did not.
+int owgs_geometry_selfcheck(void) {
+    OwgsEngineArgs A;
+    memset(&A, 0, sizeof(A));
+    OwgsPrepassArgs p{};
+    p.cw = 1;
+    for (int v = 0; v < 2; ++v) {
+        // the tag of the OTHER geometry (what a host sized for it would send)
+        A.geom = p.geom = OWGS_GEOM_TAG(v ? OWGS_WL : OWGS_WL_NARROW);
+        const hipError_t e1 = v ? owgs_launch_engine_narrow(&A, nullptr) : owgs_launch_engine(&A, nullptr);
+        const hipError_t e2 = v ? owgs_launch_engine_multi_narrow(&A, 1, nullptr) : owgs_launch_engine_multi(&A, 1, nullptr);
+        const hipError_t e3 = v ? owgs_launch_prepass_narrow(&p, nullptr, 1, nullptr) : owgs_launch_prepass(&p, nullptr, 1, nullptr);
+        if (e1 != hipErrorInvalidValue || e2 != hipErrorInvalidValue || e3 != hipErrorInvalidValue) return OWGS_EDEVICE;
+    }
+    return OWGS_OK;
+}
 
 int owgs_limits(int32_t* max_invokers, int32_t* max_slots) {
     // identity pools (the largest on-chip state per invoker: permits + usable bit + prefix counts): the largest
@@ -830,13 +938,13 @@ int owgs_create(const owgs_config* cfg, owgs_ctx** out) {
         return OWGS_EDEVICE;
     }
     if (c->d_ct_keys.reserve(OWGS_CTC) || c->d_ct_vals.reserve(OWGS_CTC) || c->d_ct_tmp.reserve(2 * OWGS_CTC) ||
-        c->d_stats.reserve(OWGS_NSTATS) ||
+        c->d_stats.reserve(2 * OWGS_NSTATS) ||
         c->d_err.reserve(1) || c->d_permits.reserve(1)) {
         owgs_destroy(c);
         return OWGS_ENOMEM;
     }
     if (reset_ctab(c) || hipMemset(c->d_err.p, 0, sizeof(int32_t)) != hipSuccess ||
-        hipMemset(c->d_stats.p, 0, OWGS_NSTATS * sizeof(u64)) != hipSuccess) {
+        hipMemset(c->d_stats.p, 0, 2 * OWGS_NSTATS * sizeof(u64)) != hipSuccess) {
         owgs_destroy(c);
         return OWGS_EDEVICE;
     }
@@ -880,6 +988,8 @@ void owgs_destroy(owgs_ctx* c) {
     c->ev_ovf = nullptr;
     if (c->ev_status) (void)hipEventDestroy(c->ev_status);
     c->ev_status = nullptr;
+    if (c->ev_tail) (void)hipEventDestroy(c->ev_tail);
+    c->ev_tail = nullptr;
     if (c->ev_margs) (void)hipEventDestroy(c->ev_margs);
     c->ev_margs = nullptr;
     c->d_off.release();
@@ -938,6 +1048,7 @@ void owgs_destroy(owgs_ctx* c) {
     c->f_cnt.release();
     c->f_tile.release();
     c->f_rec.release();
+    c->f_bound.release();
     c->r_bound.release();
     c->r_idx.release();
     c->r_cnt.release();
@@ -970,6 +1081,10 @@ int owgs_update_invokers(owgs_ctx* c, int32_t n, const int32_t* ids, const int64
                          const uint8_t* status) {
     if (!c || n < 0 || (n > 0 && (!ids || !user_memory_bytes || !status))) return OWGS_EINVAL;
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     const int32_t old_size = (int32_t)c->ids.size();
     const int32_t new_size = n;
     int32_t managed = d2i(std::ceil((double)new_size * c->mf));
@@ -1043,6 +1158,10 @@ int owgs_update_invokers(owgs_ctx* c, int32_t n, const int32_t* ids, const int64
 int owgs_update_cluster(owgs_ctx* c, int32_t new_size) {
     if (!c) return OWGS_EINVAL;
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     const int32_t actual = new_size > 1 ? new_size : 1;
     if (c->cluster == actual) return OWGS_OK;
     int rw = w_rebuild(c);  // in-flight concurrent activations of the discarded entries become watched pairs
@@ -1075,12 +1194,13 @@ int owgs_register_actions(owgs_ctx* c, int32_t n, const char* ns_bytes, const in
         if (ns_off[i + 1] < ns_off[i] || path_off[i + 1] < path_off[i] || key_off[i + 1] < key_off[i])
             return c->fail(OWGS_EINVAL, "offsets");
     }
-    if (c->a_mem.size() + (size_t)n > (size_t)OWGS_REC_NOACT)
-        return c->fail(OWGS_ERANGE, "too many actions");
+    // handles: released ones first, then new ids below OWGS_REC_NOACT
+    if ((size_t)n > c->free_handles.size() + ((size_t)OWGS_REC_NOACT - c->a_mem.size()))
+        return c->fail(OWGS_ERANGE, "too many live actions (release unused handles: owgs_release_actions)");
     // validate before mutating: one fqn@version has one set of limits (the action document is versioned)
+    size_t fresh = 0;
     {
         std::unordered_map<std::string, std::pair<int32_t, int32_t>> seen;
-        size_t fresh = 0;
         for (int32_t i = 0; i < n; ++i) {
             std::string k(key_bytes + key_off[i], (size_t)(key_off[i + 1] - key_off[i]));
             auto it = c->slot_ids.find(k);
@@ -1098,32 +1218,67 @@ int owgs_register_actions(owgs_ctx* c, int32_t n, const char* ns_bytes, const in
                 return c->fail(OWGS_EINVAL, "same fqn@version registered with different limits");
             }
         }
-        if (c->slot_ids.size() + fresh > (size_t)OWGS_MAX_SLOTKEYS + 1)
-            return c->fail(OWGS_ERANGE, "too many fqn@version keys");
     }
     (void)hipSetDevice(c->cfg.device);
-    const int32_t base = (int32_t)c->a_mem.size();
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
+    // key ids: recycled ones, then new ones up to OWGS_MAX_SLOTKEYS; when they run out, recycle the keys no live
+    // handle names and no map entry / watched pair holds any more
+    auto key_room = [&]() { return c->free_slots.size() + ((size_t)OWGS_MAX_SLOTKEYS + 1 - c->slot_name.size()); };
+    if (fresh > key_room()) {
+        const int rr = reclaim_slots(c);
+        if (rr) return rr;
+        if (fresh > key_room()) return c->fail(OWGS_ERANGE, "too many live fqn@version keys");
+    }
     c->cw_cache = 0;
+    std::vector<int32_t> hid((size_t)n);
     for (int32_t i = 0; i < n; ++i) {
         std::string k(key_bytes + key_off[i], (size_t)(key_off[i + 1] - key_off[i]));
         auto it = c->slot_ids.find(k);
         int32_t sid;
         if (it == c->slot_ids.end()) {
-            sid = (int32_t)c->slot_ids.size();
+            if (!c->free_slots.empty()) {
+                sid = c->free_slots.back();
+                c->free_slots.pop_back();
+                c->slot_name[sid] = k;
+                c->slot_uses[sid] = 0;
+                c->slot_maxc[sid] = max_conc[i];
+                c->slot_mem[sid] = mem_mb[i];
+            } else {
+                sid = (int32_t)c->slot_name.size();
+                c->slot_name.push_back(k);
+                c->slot_uses.push_back(0);
+                c->slot_maxc.push_back(max_conc[i]);
+                c->slot_mem.push_back(mem_mb[i]);
+            }
             c->slot_ids.emplace(std::move(k), sid);
-            c->slot_uses.push_back(0);
-            c->slot_maxc.push_back(max_conc[i]);
-            c->slot_mem.push_back(mem_mb[i]);
         } else {
             sid = it->second;
         }
         c->slot_uses[sid]++;
-        c->a_slot.push_back(sid);
-        c->a_mem.push_back(mem_mb[i]);
-        c->a_maxc.push_back(max_conc[i]);
+        int32_t a;
+        if (!c->free_handles.empty()) {
+            a = c->free_handles.back();
+            c->free_handles.pop_back();
+        } else {
+            a = (int32_t)c->a_mem.size();
+            c->a_slot.push_back(0);
+            c->a_mem.push_back(0);
+            c->a_maxc.push_back(0);
+            c->a_bb.push_back(0);
+            c->a_hash.push_back(0);
+            c->a_live.push_back(0);
+        }
+        c->a_slot[a] = sid;
+        c->a_mem[a] = mem_mb[i];
+        c->a_maxc[a] = max_conc[i];
+        c->a_bb[a] = blackbox[i] ? 1 : 0;
+        c->a_live[a] = 1;
         if (max_conc[i] > 1) c->any_conc = true;
-        c->a_bb.push_back(blackbox[i] ? 1 : 0);
-        out_action[i] = base + i;
+        hid[i] = a;
+        out_action[i] = a;
     }
     const int32_t total = (int32_t)c->a_mem.size();
     // strings -> device, hash on the GPU
@@ -1146,7 +1301,7 @@ int owgs_register_actions(owgs_ctx* c, int32_t n, const char* ns_bytes, const in
     dpo.release();
     dh.release();
     for (int32_t i = 0; i < n; ++i) {
-        c->a_hash.push_back(h[i]);
+        c->a_hash[hid[i]] = h[i];
         if (out_hash) out_hash[i] = h[i];
     }
     HIPCHK(c, upload(c->d_act_hash, c->a_hash.data(), (size_t)total, c->stream));
@@ -1154,13 +1309,38 @@ int owgs_register_actions(owgs_ctx* c, int32_t n, const char* ns_bytes, const in
     HIPCHK(c, upload(c->d_act_mem, c->a_mem.data(), (size_t)total, c->stream));
     HIPCHK(c, upload(c->d_act_maxc, c->a_maxc.data(), (size_t)total, c->stream));
     HIPCHK(c, upload(c->d_act_bb, c->a_bb.data(), (size_t)total, c->stream));
-    // a walk cursor is exact for maxConcurrent==1 actions and for fqns invoked on a single walk
+    // a walk cursor is exact for maxConcurrent==1 actions and for fqns invoked on a single walk; released
+    // handles keep their last word (never read)
     c->a_cok.resize((size_t)total);
-    for (int32_t a = 0; a < total; ++a) c->a_cok[a] = (c->a_maxc[a] == 1 || c->slot_uses[c->a_slot[a]] == 1) ? 1 : 0;
+    for (int32_t a = 0; a < total; ++a)
+        c->a_cok[a] = (c->a_live[a] && (c->a_maxc[a] == 1 || c->slot_uses[c->a_slot[a]] == 1)) ? 1 : 0;
     HIPCHK(c, upload(c->d_act_cok, c->a_cok.data(), (size_t)total, c->stream));
     int rc = prepare_actions(c);
     if (!rc) HIPCHK(c, hipStreamSynchronize(c->stream));
     return rc;
+}
+
+// The caller drops action handles (a cold action, a superseded fqn@version): no later call names them and none of
+// their activations is still in flight.  Their ids, and the fqn@version keys no live handle names any more, are reused
+// by later registrations -- the keys once nothing on the device holds them (reclaim_slots).
+int owgs_release_actions(owgs_ctx* c, int32_t n, const int32_t* actions) {
+    if (!c || n < 0 || (n > 0 && !actions)) return OWGS_EINVAL;
+    const int32_t na = (int32_t)c->a_mem.size();
+    std::vector<uint8_t> seen;
+    for (int32_t i = 0; i < n; ++i) {
+        const int32_t a = actions[i];
+        if (a < 0 || a >= na || !c->a_live[a]) return c->fail(OWGS_ENOENT, "unknown or released action");
+        if (seen.empty()) seen.assign((size_t)na, 0);
+        if (seen[a]++) return c->fail(OWGS_EINVAL, "action released twice in one call");
+    }
+    for (int32_t i = 0; i < n; ++i) {
+        const int32_t a = actions[i], sid = c->a_slot[a];
+        c->a_live[a] = 0;
+        c->free_handles.push_back(a);
+        if (--c->slot_uses[sid] == 0) c->pending_slots.push_back(sid);
+    }
+    if (n > 0) c->cw_cache = 0;
+    return OWGS_OK;
 }
 
 int owgs_publish_batch(owgs_ctx* c, int32_t n, const int32_t* action, const uint64_t* seq, uint64_t seq_base,
@@ -1169,6 +1349,10 @@ int owgs_publish_batch(owgs_ctx* c, int32_t n, const int32_t* action, const uint
     if (n == 0) return OWGS_OK;
     if (!registered(c, n, action)) return c->fail(OWGS_ENOENT, "unknown action");
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     const int64_t off[2] = {0, n};
     HIPCHK(c, upload(c->d_off, off, 2, c->stream));
     HIPCHK(c, upload(c->d_a, action, (size_t)n, c->stream));
@@ -1240,7 +1424,7 @@ static int release_chain(owgs_ctx* c, int32_t n, const int32_t* inv, const int32
     int rs = release_scratch(c, R, n);
     if (!rs && c->w_cap > 0) {  // room for the empty entries releases of watched pairs meet
         rs = ensure_ovf(c, n, s);
-        c->ovf_used_ub += n;
+        ovf_add(c, n);
     }
     if (rs) return rs;
     R.ovf = ovf_args(c);
@@ -1254,6 +1438,10 @@ int owgs_release_batch(owgs_ctx* c, int32_t n, const int32_t* invoker, const int
     if (n == 0) return OWGS_OK;
     if (!registered(c, n, action)) return c->fail(OWGS_ENOENT, "unknown action");
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     std::vector<int32_t> mem(n), mc(n), sl(n);
     for (int32_t i = 0; i < n; ++i) {
         mem[i] = c->a_mem[action[i]];
@@ -1299,6 +1487,10 @@ int owgs_schedule_walks(owgs_ctx* c, int32_t n, const uint8_t* pool, const int32
         xm[i] = make_uint2(x, y);  // no cursor: explicit walks are independent
     }
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     const int64_t off[2] = {0, n};
     HIPCHK(c, upload(c->d_off, off, 2, c->stream));
     HIPCHK(c, upload(c->d_xmeta, xm.data(), (size_t)n, c->stream));
@@ -1325,6 +1517,10 @@ int owgs_schedule_walks(owgs_ctx* c, int32_t n, const uint8_t* pool, const int32
 int owgs_set_slots(owgs_ctx* c, int32_t n, const int32_t* permits) {
     if (!c || n < 0 || (n > 0 && !permits)) return OWGS_EINVAL;
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     int rw = w_rebuild(c);
     if (rw) return rw;
     HIPCHK(c, upload(c->d_permits, permits, (size_t)n, c->stream));
@@ -1338,6 +1534,10 @@ int owgs_set_slots(owgs_ctx* c, int32_t n, const int32_t* permits) {
 int owgs_set_pool(owgs_ctx* c, int32_t pool, int32_t n, const int32_t* ids, const uint8_t* status) {
     if (!c || (pool != 0 && pool != 1) || n < 0 || (n > 0 && (!ids || !status))) return OWGS_EINVAL;
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     c->pool_override[pool] = true;
     c->ov_ids[pool].assign(ids, ids + n);
     c->ov_status[pool].assign(status, status + n);
@@ -1352,6 +1552,10 @@ int owgs_read_permits(owgs_ctx* c, int32_t* out, int32_t cap, int32_t* n_slots) 
     if (n_slots) *n_slots = c->n_slots;
     if (!out || cap <= 0 || c->n_slots == 0) return OWGS_OK;
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(out, c->d_permits.p, (size_t)std::min(cap, c->n_slots) * 4, hipMemcpyDeviceToHost));
     return OWGS_OK;
@@ -1360,6 +1564,10 @@ int owgs_read_permits(owgs_ctx* c, int32_t* out, int32_t cap, int32_t* n_slots) 
 int owgs_read_concurrent(owgs_ctx* c, int32_t invoker, int32_t key, int32_t* permits, int32_t* op_count) {
     if (!c) return OWGS_EINVAL;
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     DevBuf<int32_t> di, dk;
     DevBuf<int2> dv;
     HIPCHK(c, upload(di, &invoker, 1, c->stream));
@@ -1380,7 +1588,7 @@ int owgs_read_concurrent(owgs_ctx* c, int32_t invoker, int32_t key, int32_t* per
 }
 
 int owgs_key_id(owgs_ctx* c, int32_t action) {
-    if (!c || action < 0 || action >= (int32_t)c->a_slot.size()) return OWGS_ENOENT;
+    if (!c || action < 0 || action >= (int32_t)c->a_slot.size() || !c->a_live[action]) return OWGS_ENOENT;
     return c->a_slot[action];
 }
 
@@ -1405,6 +1613,10 @@ int owgs_pairwise_coprime(owgs_ctx* c, int32_t x, int32_t* out, int32_t cap, int
     if (!c || cap < 0) return OWGS_EINVAL;
     if (x > owgs_coprime_max()) return c->fail(OWGS_ERANGE, "x beyond the step-size kernel's range");
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     DevBuf<int32_t> d;
     HIPCHK(c, d.reserve((size_t)std::max(x, 0) + 2));
     HIPCHK(c, hipMemcpyAsync(d.p, &x, 4, hipMemcpyHostToDevice, c->stream));
@@ -1476,7 +1688,7 @@ static int replay_watch(owgs_ctx* c, int32_t nb, const int64_t* acq_off, const i
 // releases rel_aid[r_beg, r_end) of activations decided by earlier calls (invoker in out_invoker), then the publishes
 // act[a_beg, a_end).  The releases are staged as engine records from the earlier decisions, so the batch is one
 // engine launch (owgs_fused.hip span mode); with watched pairs: the exact release kernels + the watch update.
-int owgs_replay_device_span(owgs_ctx* c, int64_t a_beg, int64_t a_end, int64_t r_beg, int64_t r_end, const int32_t* act,
+static int replay_device_span_impl(owgs_ctx* c, int64_t a_beg, int64_t a_end, int64_t r_beg, int64_t r_end, const int32_t* act,
                             const int64_t* rel_aid, uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags,
                             uint8_t* rel_flags, void* stream) {
     if (!c || a_beg < 0 || a_end < a_beg || r_beg < 0 || r_end < r_beg || !act || !out_invoker || !out_flags ||
@@ -1554,7 +1766,19 @@ int owgs_replay_device_span(owgs_ctx* c, int64_t a_beg, int64_t a_end, int64_t r
     return rc;
 }
 
-int owgs_replay_device(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const int32_t* act,
+int owgs_replay_device_span(owgs_ctx* c, int64_t a_beg, int64_t a_end, int64_t r_beg, int64_t r_end, const int32_t* act,
+                            const int64_t* rel_aid, uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags,
+                            uint8_t* rel_flags, void* stream) {
+    if (!c) return OWGS_EINVAL;
+    (void)hipSetDevice(c->cfg.device);
+    hipStream_t hs_ = stream ? (hipStream_t)stream : c->stream;
+    int rc = order_on(c, hs_);
+    if (!rc) rc = replay_device_span_impl(c, a_beg, a_end, r_beg, r_end, act, rel_aid, seq_base, out_invoker, out_flags, rel_flags, stream);
+    const int rt = tail_mark(c, hs_);  // (also after a failure: whatever was enqueued stays ordered)
+    return rc ? rc : rt;
+}
+
+static int replay_device_impl(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const int32_t* act,
                        int64_t n_activations, const int64_t* rel_off, const int64_t* rel_aid, int64_t n_releases,
                        uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, uint8_t* rel_flags, void* stream) {
     if (!c) return OWGS_EINVAL;
@@ -1576,7 +1800,19 @@ int owgs_replay_device(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, c
     return OWGS_OK;
 }
 
-int owgs_replay_device_multi(owgs_ctx** cs, int32_t k, const owgs_replay_io* io, void* stream) {
+int owgs_replay_device(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const int32_t* act,
+                       int64_t n_activations, const int64_t* rel_off, const int64_t* rel_aid, int64_t n_releases,
+                       uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, uint8_t* rel_flags, void* stream) {
+    if (!c) return OWGS_EINVAL;
+    (void)hipSetDevice(c->cfg.device);
+    hipStream_t hs_ = stream ? (hipStream_t)stream : c->stream;
+    int rc = order_on(c, hs_);
+    if (!rc) rc = replay_device_impl(c, n_batches, acq_off, act, n_activations, rel_off, rel_aid, n_releases, seq_base, out_invoker, out_flags, rel_flags, stream);
+    const int rt = tail_mark(c, hs_);  // (also after a failure: whatever was enqueued stays ordered)
+    return rc ? rc : rt;
+}
+
+static int replay_device_multi_impl(owgs_ctx** cs, int32_t k, const owgs_replay_io* io, void* stream) {
     if (!cs || !io || k < 1 || k > OWGS_MULTI_DEV_MAX) return OWGS_EINVAL;
     for (int32_t i = 0; i < k; ++i) {
         if (!cs[i]) return OWGS_EINVAL;
@@ -1586,23 +1822,23 @@ int owgs_replay_device_multi(owgs_ctx** cs, int32_t k, const owgs_replay_io* io,
         if (io[i].n_batches <= 0) return cs[i]->fail(OWGS_EINVAL, "multi-shard replay needs batches in every shard");
     }
     hipStream_t hs = stream ? (hipStream_t)stream : cs[0]->stream;
-    bool one_launch = true;  // every shard's engine in one launch needs one geometry and no watched pairs
+    // every shard's engine in one launch needs one geometry and no watched pairs: the geometry each shard's launch
+    // would take (lds_check applies the diagnostic override too)
+    bool one_launch = true;
     for (int32_t i = 0; i < k; ++i) {
-        const int v = engine_variant(cs[i]->n_slots, cs[i]->pool_mode, cs[i]->n_ids, cs[i]->nm, cs[i]->nb);
-        if (cs[i]->w_cap > 0 || v != engine_variant(cs[0]->n_slots, cs[0]->pool_mode, cs[0]->n_ids, cs[0]->nm, cs[0]->nb))
-            one_launch = false;
+        const int rv = lds_check(cs[i]);
+        if (rv) return rv;
+        if (cs[i]->w_cap > 0 || cs[i]->variant != cs[0]->variant) one_launch = false;
     }
-    for (int32_t i = 0; i < k; ++i)
-        if (!one_launch) {  // a shard in watch mode replays batch by batch (or geometries differ): every shard on its own
-            for (int32_t j = 0; j < k; ++j) {
-                const owgs_replay_io& x = io[j];
-                int rc = owgs_replay_device(cs[j], x.n_batches, x.acq_off, x.act, x.n_activations, x.rel_off,
-                                            x.rel_aid, x.n_releases, x.seq_base, x.out_invoker, x.out_flags,
-                                            x.rel_flags, hs);
-                if (rc) return rc;
-            }
-            return OWGS_OK;
+    if (!one_launch) {  // a shard in watch mode replays batch by batch (or geometries differ): every shard on its own
+        for (int32_t j = 0; j < k; ++j) {
+            const owgs_replay_io& x = io[j];
+            int rc = replay_device_impl(cs[j], x.n_batches, x.acq_off, x.act, x.n_activations, x.rel_off, x.rel_aid,
+                                        x.n_releases, x.seq_base, x.out_invoker, x.out_flags, x.rel_flags, hs);
+            if (rc) return rc;
         }
+        return OWGS_OK;
+    }
     std::vector<OwgsEngineArgs> A((size_t)k);
     for (int32_t i = 0; i < k; ++i) {
         const owgs_replay_io& x = io[i];
@@ -1643,6 +1879,22 @@ int owgs_replay_device_multi(owgs_ctx** cs, int32_t k, const owgs_replay_io* io,
             HIPCHK(cs[i], owgs_launch_relflags(x.rel_aid, x.n_releases, x.out_invoker, x.rel_flags, hs));
     }
     return OWGS_OK;
+}
+
+int owgs_replay_device_multi(owgs_ctx** cs, int32_t k, const owgs_replay_io* io, void* stream) {
+    if (!cs || !io || k < 1 || k > OWGS_MULTI_DEV_MAX) return OWGS_EINVAL;
+    for (int32_t i = 0; i < k; ++i)
+        if (!cs[i]) return OWGS_EINVAL;
+    (void)hipSetDevice(cs[0]->cfg.device);
+    hipStream_t hs_ = stream ? (hipStream_t)stream : cs[0]->stream;
+    int rc = OWGS_OK;
+    for (int32_t i = 0; i < k && !rc; ++i) rc = order_on(cs[i], hs_);
+    if (!rc) rc = replay_device_multi_impl(cs, k, io, stream);
+    for (int32_t i = 0; i < k; ++i) {
+        const int rt = tail_mark(cs[i], hs_);
+        if (!rc) rc = rt;
+    }
+    return rc;
 }
 
 static int replay_begin(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const int32_t* act,
@@ -1700,6 +1952,10 @@ int owgs_replay(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const in
     if (!c || n_batches < 0 || !acq_off || !act || !out_invoker || !out_flags || !rel_off) return OWGS_EINVAL;
     if (n_batches == 0) return OWGS_OK;
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     const int64_t n_act = acq_off[n_batches], n_rel = rel_off[n_batches];
     for (int32_t b = 0; b < n_batches; ++b)
         if (acq_off[b + 1] < acq_off[b] || rel_off[b + 1] < rel_off[b]) return c->fail(OWGS_EINVAL, "offsets");
@@ -1733,6 +1989,43 @@ int owgs_replay(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const in
 // H2D of every input, one launch chain (release staging, pre-pass, ONE engine launch over all runs), one pinned D2H
 // of every output, one synchronisation.  With watched pairs (owgs_watch.hip) the runs go through the exact release
 // kernels, one engine launch per run and the watch update instead -- still one copy each way and one sync.
+// The per-run path of owgs_process_batch (watched pairs, a call of completions only, or a fused call whose releases
+// could leave the engine's permit range): per run the exact release kernels (ForcibleSemaphore's overflow Error per
+// release, FS:48-50), then an engine launch for its publishes and, with watched pairs, the watch update.
+static int process_runs(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, const int32_t* pub_off, const int64_t* d_run,
+                        const int32_t* d_pa, const int32_t* d_ri, const int32_t* d_ra, const u64* d_sq,
+                        uint64_t seq_base, int32_t* d_out, uint8_t* d_fl, uint8_t* d_rf, hipStream_t s) {
+    int rc = OWGS_OK;
+    int32_t max_r = 1;
+    for (int32_t r = 0; r < n_runs; ++r) max_r = std::max(max_r, rel_off[r + 1] - rel_off[r]);
+    HIPCHK(c, c->w_rel.reserve((size_t)3 * max_r));
+    int32_t* q = c->w_rel.p;
+    for (int32_t r = 0; r < n_runs && !rc; ++r) {
+        const int32_t nr = rel_off[r + 1] - rel_off[r], np = pub_off[r + 1] - pub_off[r];
+        if (nr > 0) {
+            HIPCHK(c, owgs_launch_relmeta(nr, d_ra + rel_off[r], c->d_act_mem.p, c->d_act_maxc.p, c->d_act_slot.p, q,
+                                          q + max_r, q + 2 * max_r, s));
+            rc = release_chain(c, nr, d_ri + rel_off[r], q, q + max_r, q + 2 * max_r, d_rf + rel_off[r], s);
+        }
+        if (!rc && np > 0) {
+            OwgsEngineArgs A;
+            base_args(c, A);
+            A.seq_base = seq_base + (uint64_t)pub_off[r];
+            A.seq = d_sq ? d_sq + pub_off[r] : nullptr;
+            A.out_inv = d_out + pub_off[r];
+            A.out_flags = d_fl + pub_off[r];
+            rc = run_prepass(c, A, 1, d_run + 2 * r, d_pa + pub_off[r], np, s);
+            if (!rc) rc = run_engine(c, A, s);
+            if (!rc) rc = w_update(c, np, d_pa + pub_off[r], d_out + pub_off[r], d_fl + pub_off[r], s);
+        }
+    }
+    return rc;
+}
+
+// One drained batch of the shim's batching thread: runs of completions then publishes.  One pinned
+// H2D of every input, one launch chain (release staging, pre-pass, ONE engine launch over all runs), one pinned D2H
+// of every output, one synchronisation.  With watched pairs (owgs_watch.hip) the runs go through the exact release
+// kernels, one engine launch per run and the watch update instead -- still one copy each way and one sync.
 int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, const int32_t* rel_invoker,
                        const int32_t* rel_action, uint8_t* rel_flags, const int32_t* pub_off,
                        const int32_t* pub_action, const uint64_t* seq, uint64_t seq_base, int32_t* out_invoker,
@@ -1748,7 +2041,22 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
     if (n_runs >= 0x1FFFF) return c->fail(OWGS_ERANGE, "more than 131070 runs in one call");
     if (!registered(c, NP, pub_action) || !registered(c, NR, rel_action)) return c->fail(OWGS_ENOENT, "unknown action");
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     hipStream_t s = c->stream;
+    // explicit sequence numbers that count up from the first one are the implicit form (seq_base + i): the engine's
+    // specialisations without the per-activation sequence loads then take the call (the shim numbers its publishes
+    // in queue order)
+    if (seq && NP > 0) {
+        bool consecutive = true;
+        for (int32_t i = 1; i < NP && consecutive; ++i) consecutive = seq[i] == seq[0] + (uint64_t)i;
+        if (consecutive) {
+            seq_base = seq[0];
+            seq = nullptr;
+        }
+    }
     // ---- pinned staging: i64 offsets (publishes, releases, per-run {0, n}) | publish actions | release invokers |
     // release actions | seq
     auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
@@ -1807,36 +2115,20 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
     uint8_t* d_fl = (uint8_t*)(DO + q_fl);
     uint8_t* d_rf = (uint8_t*)(DO + q_rf);
     int rc = OWGS_OK;
-    if (c->w_cap > 0 || NP == 0) {
+    bool fused = !(c->w_cap > 0 || NP == 0);
+    if (!fused) {
         // watched pairs: the exact release kernels per run, the watch update after each publish run; a call of
         // completions only: the release kernels alone (cheaper than an engine launch)
-        int32_t max_r = 1;
-        for (int32_t r = 0; r < n_runs; ++r) max_r = std::max(max_r, rel_off[r + 1] - rel_off[r]);
-        HIPCHK(c, c->w_rel.reserve((size_t)3 * max_r));
-        int32_t* q = c->w_rel.p;
-        for (int32_t r = 0; r < n_runs && !rc; ++r) {
-            const int32_t nr = rel_off[r + 1] - rel_off[r], np = pub_off[r + 1] - pub_off[r];
-            if (nr > 0) {
-                HIPCHK(c, owgs_launch_relmeta(nr, d_ra + rel_off[r], c->d_act_mem.p, c->d_act_maxc.p, c->d_act_slot.p,
-                                              q, q + max_r, q + 2 * max_r, s));
-                rc = release_chain(c, nr, d_ri + rel_off[r], q, q + max_r, q + 2 * max_r, d_rf + rel_off[r], s);
-            }
-            if (!rc && np > 0) {
-                OwgsEngineArgs A;
-                base_args(c, A);
-                A.seq_base = seq_base + (uint64_t)pub_off[r];
-                A.seq = d_sq ? d_sq + pub_off[r] : nullptr;
-                A.out_inv = d_out + pub_off[r];
-                A.out_flags = d_fl + pub_off[r];
-                rc = run_prepass(c, A, 1, d_run + 2 * r, d_pa + pub_off[r], np, s);
-                if (!rc) rc = run_engine(c, A, s);
-                if (!rc) rc = w_update(c, np, d_pa + pub_off[r], d_out + pub_off[r], d_fl + pub_off[r], s);
-            }
-        }
+        rc = process_runs(c, n_runs, rel_off, pub_off, d_run, d_pa, d_ri, d_ra, d_sq, seq_base, d_out, d_fl, d_rf, s);
     } else {  // every run in ONE engine launch: the releases as engine records (owgs_fused.hip)
+        if (c->a_mem.empty()) return c->fail(OWGS_ENOENT, "no actions registered");
         HIPCHK(c, c->f_rec.reserve((size_t)NR + 2));
         HIPCHK(c, c->f_src.reserve((size_t)NR + 1));
         HIPCHK(c, c->f_cnt.reserve((size_t)2 * n_runs));
+        if (c->f_bound.n < (size_t)std::max(c->n_slots, 1)) {  // zero between calls (the engine clears what it reads)
+            HIPCHK(c, c->f_bound.reserve((size_t)std::max(c->n_slots, 1)));
+            HIPCHK(c, hipMemsetAsync(c->f_bound.p, 0, c->f_bound.n * 8, s));
+        }
         if (NR > 0) {
             OwgsStageArgs g{};
             g.n_runs = n_runs;
@@ -1851,9 +2143,9 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
             g.rel_src = c->f_src.p;
             g.relcnt = c->f_cnt.p;
             g.rel_flags = d_rf;
+            g.bound = c->f_bound.p;
             HIPCHK(c, owgs_launch_stage_releases(&g, s));
         }
-        if (c->a_mem.empty()) return c->fail(OWGS_ENOENT, "no actions registered");
         OwgsEngineArgs A;
         base_args(c, A);
         A.seq_base = seq_base;
@@ -1867,6 +2159,7 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
             A.rel_rec = c->f_rec.p;
             A.rel_src = c->f_src.p;
             A.rel_flags = d_rf;
+            A.rel_bound = c->f_bound.p;
         }
         if (!rc) rc = run_engine(c, A, s);
     }
@@ -1875,6 +2168,21 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
     HIPCHK(c, hipMemcpyAsync(c->h_pout, c->d_pout.p, out_bytes, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     const char* HO = (const char*)c->h_pout;
+    int32_t e = 0;
+    memcpy(&e, HO + q_err, 4);
+    if (fused && (e & OWGS_ERR_RELRISK)) {
+        // the releases could push a slot out of the engine's range: the engine stopped before touching anything, so
+        // the call runs again through the per-run path, whose release kernels apply ForcibleSemaphore's bound
+        // release by release (FS:48-50) exactly as owgs_release_batch does
+        HIPCHK(c, hipMemsetAsync(c->d_err.p, 0, sizeof(int32_t), s));
+        HIPCHK(c, hipMemsetAsync(c->f_bound.p, 0, c->f_bound.n * 8, s));
+        rc = process_runs(c, n_runs, rel_off, pub_off, d_run, d_pa, d_ri, d_ra, d_sq, seq_base, d_out, d_fl, d_rf, s);
+        if (rc) return rc;
+        HIPCHK(c, hipMemcpyAsync(c->d_pout.p + q_err, c->d_err.p, 4, hipMemcpyDeviceToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_pout, c->d_pout.p, out_bytes, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        memcpy(&e, HO + q_err, 4);
+    }
     if (NP) {
         memcpy(out_invoker, HO + q_inv, 4 * (size_t)NP);
         memcpy(out_flags, HO + q_fl, (size_t)NP);
@@ -1882,14 +2190,16 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
     if (NR && rel_flags) memcpy(rel_flags, HO + q_rf, (size_t)NR);
     rc = w_refresh(c, s);
     if (rc) return rc;
-    int32_t e = 0;
-    memcpy(&e, HO + q_err, 4);
     return e ? check_err_word(c) : OWGS_OK;
 }
 
 int owgs_snapshot(owgs_ctx* c) {
     if (!c) return OWGS_EINVAL;
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     HIPCHK(c, c->s_permits.reserve((size_t)std::max(c->n_slots, 1)));
     HIPCHK(c, c->s_ct_keys.reserve(OWGS_CTC));
     HIPCHK(c, c->s_ct_vals.reserve(OWGS_CTC));
@@ -1919,11 +2229,14 @@ int owgs_snapshot(owgs_ctx* c) {
     }
     c->has_snap = true;
     c->snap_slots = c->n_slots;
+    c->snap_slot_epoch = c->slot_epoch;
     return OWGS_OK;
 }
 
-int owgs_restore(owgs_ctx* c, void* stream) {
+static int restore_impl(owgs_ctx* c, void* stream) {
     if (!c || !c->has_snap || c->snap_slots != c->n_slots) return OWGS_EINVAL;
+    // a key recycled since the snapshot may name another fqn@version now: the snapshot's entries would alias it
+    if (c->slot_epoch != c->snap_slot_epoch) return c->fail(OWGS_EINVAL, "keys were recycled since the snapshot");
     (void)hipSetDevice(c->cfg.device);
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     if (c->n_slots)
@@ -1964,7 +2277,17 @@ int owgs_restore(owgs_ctx* c, void* stream) {
     return OWGS_OK;
 }
 
-int owgs_update_health_device(owgs_ctx* c, int32_t n, const uint8_t* status_dev, void* stream) {
+int owgs_restore(owgs_ctx* c, void* stream) {
+    if (!c) return OWGS_EINVAL;
+    (void)hipSetDevice(c->cfg.device);
+    hipStream_t hs_ = stream ? (hipStream_t)stream : c->stream;
+    int rc = order_on(c, hs_);
+    if (!rc) rc = restore_impl(c, stream);
+    const int rt = tail_mark(c, hs_);  // (also after a failure: whatever was enqueued stays ordered)
+    return rc ? rc : rt;
+}
+
+static int update_health_device_impl(owgs_ctx* c, int32_t n, const uint8_t* status_dev, void* stream) {
     if (!c || n != (int32_t)c->status.size() || (n > 0 && !status_dev)) return OWGS_EINVAL;
     (void)hipSetDevice(c->cfg.device);
     if (n && c->pool_mode == 0 && !c->pool_override[0] && !c->pool_override[1] && c->d_status.p && c->d_usable.p) {
@@ -1993,9 +2316,23 @@ int owgs_update_health_device(owgs_ctx* c, int32_t n, const uint8_t* status_dev,
     return rc;
 }
 
+int owgs_update_health_device(owgs_ctx* c, int32_t n, const uint8_t* status_dev, void* stream) {
+    if (!c) return OWGS_EINVAL;
+    (void)hipSetDevice(c->cfg.device);
+    hipStream_t hs_ = stream ? (hipStream_t)stream : c->stream;
+    int rc = order_on(c, hs_);
+    if (!rc) rc = update_health_device_impl(c, n, status_dev, stream);
+    const int rt = tail_mark(c, hs_);  // (also after a failure: whatever was enqueued stays ordered)
+    return rc ? rc : rt;
+}
+
 int owgs_selftest(owgs_ctx* c) {
     if (!c) return OWGS_EINVAL;
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     HIPCHK(c, hipMemsetAsync(c->d_err.p, 0, sizeof(int32_t), c->stream));
     HIPCHK(c, owgs_launch_selftest(c->d_err.p, 64, c->stream));
     int32_t bad = 0;
@@ -2008,9 +2345,13 @@ int owgs_selftest(owgs_ctx* c) {
 int owgs_read_stats(owgs_ctx* c, uint64_t* out, int32_t cap) {
     if (!c || !out) return OWGS_EINVAL;
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     u64 v[OWGS_NSTATS];
     HIPCHK(c, hipDeviceSynchronize());
-    HIPCHK(c, hipMemcpy(v, c->d_stats.p, sizeof(v), hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(v, c->d_stats.p + (size_t)c->stats_last * OWGS_NSTATS, sizeof(v), hipMemcpyDeviceToHost));
     for (int32_t i = 0; i < cap && i < OWGS_NSTATS; ++i) out[i] = v[i];
     return OWGS_OK;
 }
@@ -2093,6 +2434,10 @@ int owgs_track_activations(owgs_ctx* c, int32_t n, const char* aid32, const int3
             return c->fail(OWGS_EINVAL, "activation id is not 32 characters of [0-9a-f]");
     }
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     int rc = act_reserve(c, n);
     if (rc) return rc;
     HIPCHK(c, upload(c->k_aid, aid32, (size_t)n * 32, c->stream));
@@ -2176,7 +2521,7 @@ static int ack_complete(owgs_ctx* c, int32_t n, uint8_t* d_kind, int32_t* d_tick
     int rs = release_scratch(c, R, n);
     if (!rs && c->w_cap > 0) {
         rs = ensure_ovf(c, n, st);
-        c->ovf_used_ub += n;
+        ovf_add(c, n);
     }
     if (rs) return rs;
     R.ovf = ovf_args(c);
@@ -2197,6 +2542,10 @@ int owgs_process_acks_device(owgs_ctx* c, int32_t n, const uint8_t* bytes, const
         return OWGS_EINVAL;
     if (n == 0) return OWGS_OK;
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, stream ? (hipStream_t)stream : c->stream);
+        if (ro_) return ro_;
+    }
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     HIPCHK(c, c->k_key.reserve((size_t)n));
     HIPCHK(c, c->k_info.reserve((size_t)n));
@@ -2224,6 +2573,10 @@ int owgs_process_acks(owgs_ctx* c, int32_t n, const char* bytes, const int64_t* 
     for (int32_t i = 0; i < n; ++i)
         if (off[i + 1] < off[i] || off[i] < 0) return c->fail(OWGS_EINVAL, "offsets");
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     const size_t nb = (size_t)(off[n] - off[0]);
     std::vector<int64_t> o((size_t)n + 1);
     for (int32_t i = 0; i <= n; ++i) o[i] = off[i] - off[0];
@@ -2251,6 +2604,10 @@ int owgs_complete_activations(owgs_ctx* c, int32_t n, const char* aid32, const i
         return OWGS_EINVAL;
     if (n == 0) return OWGS_OK;
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     HIPCHK(c, upload(c->k_aid, aid32, (size_t)n * 32, c->stream));
     HIPCHK(c, upload(c->k_cfl, flags, (size_t)n, c->stream));
     HIPCHK(c, upload(c->k_act, invoker, (size_t)n, c->stream));
@@ -2314,6 +2671,10 @@ int owgs_health_events(owgs_ctx* c, int32_t n, const int32_t* invoker, const uin
     if (now_ms < prev || now_ms < 0 || now_ms >= (1LL << 60))
         return c->fail(OWGS_EINVAL, "health batch: now before its last event or outside [0, 2^60)");
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     hipStream_t st = c->stream;
     const int32_t old_size = c->h_size;
     const int32_t new_size = std::max(old_size, max_ping + 1);
@@ -2376,6 +2737,10 @@ int owgs_health_read(owgs_ctx* c, int32_t cap, int32_t* n, uint8_t* status, int6
     if (!status && !user_memory_bytes && !test_actions && !ring && !next_tick) return OWGS_OK;  // size query
     if (cap < m) return c->fail(OWGS_ERANGE, "health read: capacity below the status vector size");
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     hipStream_t st = c->stream;
     if (status) HIPCHK(c, hipMemcpyAsync(status, c->h_st.p, (size_t)m, hipMemcpyDeviceToHost, st));
     if (user_memory_bytes)
@@ -2504,6 +2869,10 @@ int owgs_serialize_activations(owgs_ctx* c, const owgs_msg_batch* b, int32_t n_t
             (need_r && b->trace_off[i + 1] < b->trace_off[i]))
             return c->fail(OWGS_EINVAL, "serialize: offsets must be non-decreasing");
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
     hipStream_t st = c->stream;
     const int64_t tid0 = n ? b->tid_off[0] : 0, tidn = n ? b->tid_off[n] : 0;
     HIPCHK(c, upload(c->m_inv, b->invoker, (size_t)n, st));
@@ -2574,6 +2943,10 @@ int owgs_serialize_activations_device(owgs_ctx* c, const owgs_msg_batch* b, int3
         (cap > 0 && !out) || (b->n > 0 && (!b->content_off || !b->trace_off)))
         return OWGS_EINVAL;
     (void)hipSetDevice(c->cfg.device);
+    {
+        const int ro_ = order_on(c, stream ? (hipStream_t)stream : c->stream);
+        if (ro_) return ro_;
+    }
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     HIPCHK(c, c->m_content.reserve(1));
     HIPCHK(c, c->m_trace.reserve(1));

@@ -100,6 +100,10 @@
 #define OWGS_ERR_OPS 4
 #define OWGS_ERR_INTERNAL 8             // engine invariant violated (a pass without progress)
 #define OWGS_ERR_PERMITS 16             // slot permits outside [-2^29, 2^29) MB (the LDS encoding's range)
+#define OWGS_ERR_GEOM 32                // the launch's geometry tag is not the engine object's (nothing was touched)
+#define OWGS_ERR_RELRISK 64             // owgs_process_batch: the call's releases could push a slot's permits out of the
+                                        // LDS range; the engine returned before touching anything (the host reruns the
+                                        // call through the ordered release kernels)
 
 // LDS permits of identity pools carry the usable flag: an unusable invoker's permits are stored + OWGS_PENC, so one
 // LDS read gives both (usable permits < OWGS_PLIM <= unusable ones); HBM holds the plain values
@@ -113,7 +117,8 @@
 #define OWGS_ST_LONG 3
 #define OWGS_ST_CHUNKS 4
 #define OWGS_ST_STOPS 5
-#define OWGS_NSTATS 32  // 0-7 counters, 8-15 profile-build phase cycles, 16-31 profile-build walk counters
+#define OWGS_NSTATS 48  // 0-7 counters, 8-15 profile-build phase cycles, 16-31 profile-build walk counters,
+                        // 40-42 profile-build kernel cycles (state load, batches, write-back)
 
 #define OWGS_MULTI_MAX 8  // controller shards per owgs_engine_multi_kernel launch (kernarg: 8 x args)
 #define OWGS_MULTI_DEV_MAX 64  // owgs_engine_multi_dev_kernel: argument blocks in HBM
@@ -181,13 +186,25 @@ struct OwgsEngineArgs {
     uint8_t* out_flags;
     uint8_t* rel_flags;
     unsigned long long rng_seed;
-    unsigned long long* stats;
+    unsigned long long* stats;   // this launch's counters (zero when it starts)
+    unsigned long long* stats_next;  // the next launch's counter block: zeroed at the end of this one (no fill launch)
     int32_t* err;
     int32_t opts;                // diagnostics (env OWGS_OPTS): bit0 = no hot-action rank tables
     int32_t cw;                  // chunk width of this replay (<= OWGS_WL)
     unsigned long long* trace;   // diagnostic build only (-DOWGS_TRACE): [waves][OWGS_TRACE_CAP] barrier timeline
     int32_t feat;                // engine code paths this launch needs (OWGS_F_*): picks the compiled specialisation
+    uint32_t geom;               // OWGS_GEOM_TAG of the geometry the host sized this launch's buffers for
+    unsigned long long* rel_bound;  // owgs_process_batch: per slot, the memory the call's releases can return at most
+                                    // (staged by owgs_stage_releases_kernel; the engine checks and zeroes it), or null
 };
+// Geometry/ABI tag.  The host and an engine object must agree on the chunk width (the stride of lix, the 10-bit lane
+// fields of the records), the primary table's capacity and the argument block's layout; the host builds the tag of the
+// geometry it sized its buffers for, and every engine object's launch wrappers (and the kernels themselves, before
+// their first barrier or wait) compare it with their own: a mismatch is refused (OWGS_ERR_GEOM) instead of running
+// with out-of-bounds chunk tables.
+#define OWGS_GEOM_TAG(wl)                                                                             \
+    (0x50000000u | ((uint32_t)(wl) & 0x3FFu) | (((uint32_t)sizeof(OwgsEngineArgs) & 0x3FFu) << 10) | \
+     ((uint32_t)__builtin_ctz(OWGS_CTC) << 20))
 // Engine specialisations.  The engine body is compiled once per feature set, and the host launches the smallest one
 // that covers the context and the call, so a stream without concurrent actions on identity pools runs a kernel with
 // none of the NestedSemaphore map, explicit-pool or explicit-sequence code in it (fewer instructions per pass, fewer
@@ -249,6 +266,7 @@ struct OwgsPrepassArgs {
     uint32_t* lix;               // out [n_chunks][OWGS_WL]: stream lane | first lane of its action << 16
     int32_t cw;                  // chunk width (<= OWGS_WL)
     int32_t deal;                // lane dealing strategy (diagnostics, env OWGS_DEAL; 0 = default)
+    uint32_t geom;               // OWGS_GEOM_TAG of the host's geometry (checked like the engine's)
 };
 
 // ordered explicit releases (owgs_release_batch): one wave, releases in stream order
@@ -308,6 +326,7 @@ struct OwgsStageArgs {
     int64_t span_nrel, span_npub;
     int64_t* span_off;
     int32_t* tile_cnt;          // span mode, more than OWGS_STAGE_TILE releases: first-class records per tile (scratch)
+    unsigned long long* bound;  // or null: per slot, the memory of every release naming it (zero before the call)
 };
 #define OWGS_STAGE_TILE 1024
 

@@ -153,6 +153,7 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
 // LDS scalars
 #define SC_LMIN 0   // [2] first lane not known to fit (pass parity)
 #define SC_IRR 2    // explicit releases (owgs_process_batch): an entry got more releases than its operationCount
+#define SC_RRISK 3  // owgs_process_batch: some slot could leave the permit range through the call's releases
 #define SC_U0 4     // upper bound of usable permits, managed pool
 #define SC_U1 5     // blackbox pool
 #define SC_USED 6   // non-empty concurrency-table entries (live + deleted)
@@ -590,6 +591,7 @@ __device__ __forceinline__ int pp_insert(int32_t* hk, int32_t k) {
 
 __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A) {
     constexpr int NWR = (OWGS_WL + 63) / 64;
+    if (A.geom != OWGS_GEOM_TAG(OWGS_WL)) return;  // (uniform) another geometry's buffers: write nothing
     __shared__ __align__(16) int32_t s_a[OWGS_WL], s_s[OWGS_WL], s_p[OWGS_WL];
     __shared__ int32_t hk_a[PP_HT], hl_a[PP_HT], hk_s[PP_HT], hl_s[PP_HT];
     __shared__ unsigned long long m_a[OWGS_WL][NWR], m_s[OWGS_WL][NWR];  // lane masks, by the group's first lane
@@ -1092,6 +1094,16 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     auto conc_of = [&](uint32_t y) -> int {  // maxConcurrent field of a record's meta.y, as this specialisation sees it
         return kConc ? (int)((y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK) : 1;
     };
+    // (uniform) a launch prepared for another geometry: its chunk tables have another stride -- refuse it before the
+    // first barrier or wait of any wave
+    if (A.geom != OWGS_GEOM_TAG(OWGS_WL)) {
+        if (threadIdx.x == 0) atomicOr(A.err, OWGS_ERR_GEOM);
+        if (A.stats_next && threadIdx.x < OWGS_NSTATS) A.stats_next[threadIdx.x] = 0ull;
+        return;
+    }
+#ifdef OWGS_PROFILE
+    const u64 tk0 = memtime_pinned();  // kernel-level cycles: state load, batches, write-back (stats[40..42])
+#endif
     extern __shared__ uint4 lds_raw[];
     char* L = (char*)lds_raw;
     const OwgsLayout Y = owgs_layout(A.n_slots, pool_mode, A.n_ids, A.nm, A.nb, A.n_actions);
@@ -1134,6 +1146,11 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     // ---------------------------------------------------------------- state -> LDS
     uint32_t err = 0;
     constexpr int LB = 8;  // loads in flight per thread (the state load is latency-bound)
+    if (tid < SC_N)
+        sc[tid] = (tid == SC_IRR || tid == SC_RRISK) ? 0
+                                                     : ((tid < 4 || tid >= SC_CFT) ? OWGS_WL : (tid < 6 ? (int)0x80000000 : 0));
+    if (A.rel_bound) lds_sync();  // (SC_RRISK is set below)
+    bool rrisk = false;    // (owgs_process_batch) a slot the call's releases could push out of the LDS range
     for (int i0 = 0; i0 < n_slots; i0 += OWGS_NT * LB) {
         int v[LB];
         uint32_t u[LB];
@@ -1151,14 +1168,33 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
             const bool unusable = !((u[k] >> (i & 31)) & 1u);
             P[i] = unusable ? v[k] + OWGS_PENC : v[k];
         }
+        if (A.rel_bound) {
+#pragma unroll
+            for (int k = 0; k < LB; ++k) {
+                const int i = i0 + k * OWGS_NT + tid;
+                if (i >= n_slots) continue;
+                const unsigned long long bnd = A.rel_bound[i];
+                if (bnd) {
+                    rrisk = rrisk || (long long)v[k] + (long long)bnd >= (long long)OWGS_PLIM;
+                    A.rel_bound[i] = 0ull;
+                }
+            }
+        }
     }
+    if (rrisk) sc[SC_RRISK] = 1;
     if (pool_mode == 0) {
         for (int i = tid; i < words; i += OWGS_NT) ub[i] = A.usable[i];
     } else {
         for (int i = tid; i < nm + nb; i += OWGS_NT) pw[i] = (int16_t)A.pool_words[i];
     }
-    if (tid < SC_N) sc[tid] = tid == SC_IRR ? 0 : ((tid < 4 || tid >= SC_CFT) ? OWGS_WL : (tid < 6 ? (int)0x80000000 : 0));
     lds_sync();
+    // releases that could leave the range: nothing has been written yet -- the host replays the call through the
+    // ordered release kernels (which flag ForcibleSemaphore's overflow Error per release, FS:48-50)
+    if (A.rel_bound && sc[SC_RRISK]) {  // (uniform)
+        if (tid == 0) atomicOr(A.err, OWGS_ERR_RELRISK);
+        if (A.stats_next && tid < OWGS_NSTATS) A.stats_next[tid] = 0ull;
+        return;
+    }
     {
         int used = 0;
         for (int i0 = 0; i0 < OWGS_CTC; i0 += OWGS_NT * LB) {
@@ -1271,6 +1307,9 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     lds_sync();
+#ifdef OWGS_PROFILE
+    const u64 tk1 = memtime_pinned();
+#endif
     // healthy invokers per pool (|H| of the overload fallback, SCPB:417-424): identity pools count them from the
     // usable bitmap (owgs_update_health_device updates only the bitmap there); other pools take the host's counts
     int hm_e = A.hm, hb_e = A.hb;
@@ -3005,6 +3044,9 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     }
 
     // ---------------------------------------------------------------- LDS -> state
+#ifdef OWGS_PROFILE
+    const u64 tk2 = memtime_pinned();
+#endif
     for (int i = tid; i < n_slots; i += OWGS_NT) {
         const int v = P[i];
         A.permits[i] = v >= OWGS_PLIM ? v - OWGS_PENC : v;
@@ -3016,6 +3058,16 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
         A.ct_vals[i] = e.y;
     }
     if (err) atomicOr(A.err, (int)err);
+    if (A.stats_next && tid < OWGS_NSTATS) A.stats_next[tid] = 0ull;  // the next launch's counters start at zero
+#ifdef OWGS_PROFILE
+    if (tid == 0 && A.stats) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const u64 tk3 = memtime_pinned();
+        atomicAdd(&A.stats[40], tk1 - tk0);
+        atomicAdd(&A.stats[41], tk2 - tk1);
+        atomicAdd(&A.stats[42], tk3 - tk2);
+    }
+#endif
     if (A.stats) {
         atomicAdd(&A.stats[OWGS_ST_PROBES], (u64)st_probe);  // (the I/O wave's: its share of the hot walks)
         if (lane == 0) atomicAdd(&A.stats[OWGS_ST_LONG], (u64)st_long);
@@ -3431,6 +3483,7 @@ extern "C" hipError_t owgs_launch_prepare(const OwgsPrepArgs* a, hipStream_t s) 
 // chunk table + per-activation records; max_chunks >= sum of ceil(n_b / OWGS_WL)
 extern "C" hipError_t OWGS_GEOM(owgs_launch_prepass)(const OwgsPrepassArgs* a, int32_t* cstart, int64_t max_chunks,
                                           hipStream_t s) {
+    if (a->geom != OWGS_GEOM_TAG(OWGS_WL) || a->cw < 1 || a->cw > OWGS_WL) return hipErrorInvalidValue;
     hipLaunchKernelGGL(owgs_chunks_kernel, dim3(1), dim3(64), 0, s, a->acq_off, a->n_batches, a->cw, cstart);
     if (max_chunks <= 0) return hipGetLastError();
     OwgsPrepassArgs b = *a;
@@ -3550,6 +3603,11 @@ static hipError_t lds_attr(const void* fn, int which) {
     return e;
 }
 
+// a launch prepared for this object's geometry (the host's tag, and a chunk width its lane fields hold)
+static bool engine_args_ok(const OwgsEngineArgs& a) {
+    return a.geom == OWGS_GEOM_TAG(OWGS_WL) && a.cw >= 0 && a.cw <= OWGS_WL;
+}
+
 // compiled specialisations: 0 (maxConcurrent == 1, identity pools, implicit sequence numbers), OWGS_F_CONC, and
 // OWGS_F_ALL for anything else
 static int feat_index(int feat) { return feat == 0 ? 0 : feat == OWGS_F_CONC ? 1 : 2; }
@@ -3576,6 +3634,7 @@ extern "C" hipError_t OWGS_GEOM(owgs_launch_engine_multi_dev)(const OwgsEngineAr
     size_t lds = 0;
     int feat = 0;
     for (int i = 0; i < k; ++i) {
+        if (!engine_args_ok(a_host[i])) return hipErrorInvalidValue;
         lds = std::max(lds, OWGS_GEOM(owgs_engine_lds_bytes)(a_host[i].n_slots, a_host[i].pool_mode, a_host[i].n_ids,
                                                   a_host[i].nm, a_host[i].nb, a_host[i].n_actions));
         feat |= a_host[i].feat;
@@ -3595,6 +3654,7 @@ extern "C" hipError_t OWGS_GEOM(owgs_launch_engine_multi)(const OwgsEngineArgs* 
     int feat = 0;
     OwgsEngineMulti M;
     for (int i = 0; i < k; ++i) {
+        if (!engine_args_ok(a[i])) return hipErrorInvalidValue;
         lds = std::max(lds, OWGS_GEOM(owgs_engine_lds_bytes)(a[i].n_slots, a[i].pool_mode, a[i].n_ids, a[i].nm, a[i].nb,
                                                   a[i].n_actions));
         feat |= a[i].feat;
@@ -3610,6 +3670,7 @@ extern "C" hipError_t OWGS_GEOM(owgs_launch_engine_multi)(const OwgsEngineArgs* 
 }
 
 extern "C" hipError_t OWGS_GEOM(owgs_launch_engine)(const OwgsEngineArgs* a, hipStream_t s) {
+    if (!engine_args_ok(*a)) return hipErrorInvalidValue;
     const size_t lds = OWGS_GEOM(owgs_engine_lds_bytes)(a->n_slots, a->pool_mode, a->n_ids, a->nm, a->nb, a->n_actions);
     if (lds > OWGS_LDS_BYTES) return hipErrorInvalidValue;
     const int fi = feat_index(a->feat);

@@ -127,3 +127,40 @@ extern "C" hipError_t owgs_launch_usable(const uint8_t* status, int32_t n, uint3
     hipLaunchKernelGGL(owgs_usable_kernel, dim3((n_words + 255) / 256), dim3(256), 0, s, status, n, bits, n_words);
     return hipGetLastError();
 }
+
+// Key recycling (owgs_release_actions): cand = bitmap over fqn@version slot ids that no live action handle names; the
+// bit of every slot still held by a NestedSemaphore entry (primary table, HBM overflow: key = (invoker + 1) | slot << 15)
+// or by a watched pair (its table and its per-key count) is cleared.  What stays set is free (NestedSemaphore.scala:
+// 109-111 drops an entry at operationCount 0; nothing else on the device is keyed by slot).
+__global__ __launch_bounds__(256) void owgs_slot_scan_kernel(const uint32_t* ct_keys, const uint2* ovf, int32_t ovf_cap,
+                                                             const uint32_t* w_keys, int32_t w_cap, const int32_t* wkey,
+                                                             uint32_t* cand) {
+    const int64_t n_keys = (int64_t)OWGS_MAX_SLOTKEYS + 1;
+    const int64_t total = (int64_t)OWGS_CTC + ovf_cap + w_cap + (wkey ? n_keys : 0);
+    auto drop = [&](uint32_t s) {
+        if (s < (uint32_t)n_keys && ((cand[s >> 5] >> (s & 31)) & 1u)) atomicAnd(&cand[s >> 5], ~(1u << (s & 31)));
+    };
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        uint32_t key = 0u;
+        if (i < OWGS_CTC) {
+            key = ct_keys[i];
+        } else if (i < (int64_t)OWGS_CTC + ovf_cap) {
+            key = ovf[i - OWGS_CTC].x;
+        } else if (i < (int64_t)OWGS_CTC + ovf_cap + w_cap) {
+            key = w_keys[i - OWGS_CTC - ovf_cap];
+        } else {
+            const int64_t s = i - OWGS_CTC - ovf_cap - w_cap;
+            if (wkey[s] > 0) drop((uint32_t)s);
+            continue;
+        }
+        if (key != 0u && key != OWGS_CT_TOMB) drop(key >> OWGS_CT_SLOT_SHIFT);
+    }
+}
+
+extern "C" hipError_t owgs_launch_slot_scan(const uint32_t* ct_keys, const uint2* ovf, int32_t ovf_cap,
+                                           const uint32_t* w_keys, int32_t w_cap, const int32_t* wkey, uint32_t* cand,
+                                           hipStream_t s) {
+    hipLaunchKernelGGL(owgs_slot_scan_kernel, dim3(512), dim3(256), 0, s, ct_keys, ovf, ovf_cap, w_keys, w_cap, wkey,
+                       cand);
+    return hipGetLastError();
+}

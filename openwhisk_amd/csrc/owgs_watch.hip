@@ -114,6 +114,16 @@ __device__ int step_of(const OwgsWUpdateArgs& A, const WalkRef& w, int inv) {
         }
     }
     int idx = w.home;  // explicit pools (ids may repeat) or a step that shares a factor with n: scan the walk
+    if (A.pool_mode == 0) {
+        // identity pools: position -> id is arithmetic and usability is the bitmap (kept current by
+        // owgs_update_health_device, which does not rebuild pool_words on this path)
+        const int pos = w.pool ? inv - (A.n_ids - A.nb) : inv;
+        for (int s = 0; s < w.n + 2; ++s) {
+            if (idx == pos) return s;
+            idx = (int)(((long long)idx + w.step) % w.n);
+        }
+        return 0x7FFFFFFF;
+    }
     for (int s = 0; s < w.n + 2; ++s) {
         if (pool_word(A, w.pool, idx) == inv) return s;
         idx = (int)(((long long)idx + w.step) % w.n);

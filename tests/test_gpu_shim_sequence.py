@@ -213,3 +213,59 @@ def test_fused_batch_release_flags_follow_stream_order():
     assert grf.tolist() == orf
     assert 1 in orf  # NoSuchElement reached
     assert np.array_equal(g.permits(), o.permits())
+
+
+def test_key_and_handle_recycling_over_a_controller_lifetime():
+    """A long-running controller sees an unbounded number of fqn@version keys (every action update bumps the version).
+    The reference's NestedSemaphore map holds an entry only while activations of its key are in flight
+    (NestedSemaphore.scala:109-111); the shim drops cold handles with owgs_release_actions and the context recycles their
+    ids, and the ids of keys nothing holds any more.  Over 140,000 distinct keys (more than the 131,070 key ids), with
+    concurrent actions, releases one round later and a cluster change mid-stream (in-flight concurrent activations
+    become watched pairs and keep their keys), every decision, overload flag, release flag and the final permits equal
+    the literal oracle's, which never reuses a key."""
+    from openwhisk_amd import Action
+    MB = 1024 * 1024
+    rng = np.random.default_rng(11)
+    n_inv, total_keys, per_round = 200, 140_000, 4000
+    g = GpuShardingContainerPoolBalancer(managed_fraction=1.0, blackbox_fraction=0.0, rng_seed=5)
+    o = O.BalancerState(1.0, 0.0, rng_seed=5, zombies=True)
+    ids, mem = np.arange(n_inv, dtype=np.int32), np.full(n_inv, 8192 * MB, np.int64)
+    g.update_invokers_arrays(ids, mem, np.zeros(n_inv, np.uint8))
+    o.update_invokers(ids, mem, np.zeros(n_inv, np.uint8))
+    seq = 0
+    inflight = []       # (gpu handle, oracle handle, invoker) of the previous round's scheduled activations
+    live_prev = []      # gpu handles registered in the previous round (all of their activations complete next round)
+    max_key = 0
+    for r0 in range(0, total_keys, per_round):
+        if r0 == 60_000:
+            g.update_cluster(2)
+            o.update_cluster(2)
+        if r0 == 100_000:
+            g.update_cluster(1)
+            o.update_cluster(1)
+        k = np.arange(r0, min(r0 + per_round, total_keys))
+        conc = rng.random(len(k)) < 0.5
+        acts = [Action(f"ns{x % 97}", f"ns{x % 97}/pkg/a{x}", "0.0.1", int(rng.choice([128, 256, 512])),
+                       int(rng.integers(2, 5)) if c else 1) for x, c in zip(k, conc)]
+        gh, _ = g.register_actions(acts)
+        oh = [o.register_action(a.namespace, a.path, int(x), a.mem_mb, a.max_concurrent) for x, a in zip(k, acts)]
+        max_key = max(max_key, max(g.key_id(int(h)) for h in gh))
+        # one drained batch: the previous round's completions, then 1-2 publishes of every new action
+        pubs = np.repeat(np.arange(len(k)), rng.integers(1, 3, len(k)))
+        rng.shuffle(pubs)
+        ri = [x for _, _, x in inflight]
+        ra = [h for h, _, _ in inflight]
+        gi, gf, grf = g.process_batch([0, len(ri)], ri, ra, [0, len(pubs)], [int(gh[p]) for p in pubs],
+                                      seq_base=seq)
+        orf = [O._rel_bits(o.release(x, oo)) for _, oo, x in inflight]
+        oi = [o.publish(oh[p], seq + j) for j, p in enumerate(pubs)]
+        seq += len(pubs)
+        assert grf.tolist() == orf, r0
+        assert [(int(a), int(b)) for a, b in zip(gi, gf)] == oi, r0
+        # the previous round's actions have no activation in flight any more: drop their handles
+        if live_prev:
+            g.release_actions(live_prev)
+        live_prev = [int(h) for h in gh]
+        inflight = [(int(gh[p]), oh[p], int(x)) for p, x in zip(pubs, gi) if x >= 0]
+    assert max_key <= 131_070
+    assert np.array_equal(g.permits(), o.permits())

@@ -1,0 +1,85 @@
+"""Diagnostic: where the time of one owgs_process_batch call goes at small drains (the JVM shim's path).  Drives the
+headline shard's stream through owgs_process_batch as bench.shim_path does (fused mode), and per call records the
+wall time of the C call, the engine kernel's duration (HIP events) and -- with OWGS_LIB=openwhisk_amd/libowgs_prof.so
+-- the engine's kernel-level and per-phase cycles.  Prints one JSON line per drain size with per-call means."""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+
+import oracle as O  # noqa: E402
+from openwhisk_amd import GpuShardingContainerPoolBalancer  # noqa: E402
+from openwhisk_amd import workload as W  # noqa: E402
+
+drains = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "64,512").split(",")]
+calls = int(os.environ.get("CALLS", "300"))
+w = W.config(os.environ.get("CONFIG", "headline"))
+o_inv, _, _ = O.state_for(w).replay(w.stream)
+s = w.stream
+kind = np.concatenate([np.concatenate([np.zeros(int(s.rel_off[b + 1] - s.rel_off[b]), np.int8),
+                                       np.ones(int(s.acq_off[b + 1] - s.acq_off[b]), np.int8)]) for b in range(s.n_batches)])
+ids = np.concatenate([np.concatenate([s.rel_aid[s.rel_off[b]:s.rel_off[b + 1]], np.arange(s.acq_off[b], s.acq_off[b + 1])])
+                      for b in range(s.n_batches)]).astype(np.int64)
+act = np.ascontiguousarray(s.act, np.int32)
+b = GpuShardingContainerPoolBalancer(managed_fraction=w.managed_fraction, blackbox_fraction=w.blackbox_fraction,
+                                     rng_seed=w.rng_seed)
+b.update_invokers_arrays(w.inv_ids, w.inv_mem, w.inv_status)
+b.update_cluster(w.cluster_size)
+b.register_actions(w.actions)
+b.snapshot()
+L, h = b._L, b._h
+p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+for drain in drains:
+    b.restore()
+    inv = np.full(len(act), -9, np.int32)
+    acc, lat, eng, n_pub, n_runs = {}, [], [], 0, 0
+    for k0 in range(0, min(len(ids), calls * drain), drain):
+        k, x = kind[k0:k0 + drain], ids[k0:k0 + drain]
+        cut = np.nonzero((k[1:] == 0) & (k[:-1] == 1))[0] + 1
+        bounds = np.concatenate([[0], cut, [len(k)]])
+        ri, ra, pubs, ro, po = [], [], [], [0], [0]
+        for r0, r1 in zip(bounds[:-1], bounds[1:]):
+            kk, xx = k[r0:r1], x[r0:r1]
+            rel = xx[kk == 0]
+            rinv = np.where(inv[rel] == -9, o_inv[rel], inv[rel])
+            keep = rinv >= 0
+            ri.append(rinv[keep]), ra.append(act[rel[keep]]), pubs.append(xx[kk == 1])
+            ro.append(ro[-1] + int(keep.sum())), po.append(po[-1] + int((kk == 1).sum()))
+        ri = np.ascontiguousarray(np.concatenate(ri + [np.zeros(1, np.int32)]), np.int32)
+        ra = np.ascontiguousarray(np.concatenate(ra + [np.zeros(1, np.int32)]), np.int32)
+        pubs = np.concatenate(pubs).astype(np.int64)
+        pa = np.ascontiguousarray(np.concatenate([act[pubs], np.zeros(1, np.int32)]), np.int32)
+        sq = np.ascontiguousarray(np.concatenate([pubs, [0]]).astype(np.uint64))
+        ro, po = np.array(ro, np.int32), np.array(po, np.int32)
+        o = np.zeros(len(pubs) + 1, np.int32)
+        f = np.zeros(len(pubs) + 1, np.uint8)
+        rf = np.zeros(len(ri), np.uint8)
+        t0 = time.perf_counter()
+        rc = L.owgs_process_batch(h, len(ro) - 1, p(ro), p(ri), p(ra), p(rf), p(po), p(pa), p(sq), 0, p(o), p(f))
+        lat.append(time.perf_counter() - t0)
+        assert rc == 0, L.owgs_last_error(h)
+        inv[pubs] = o[:len(pubs)]
+        assert np.array_equal(o[:len(pubs)], o_inv[pubs])
+        n_pub += len(pubs)
+        n_runs += len(ro) - 1
+        if len(pubs):
+            eng.append(b.engine_ms())
+            st = b.stats()
+            for key in ("passes", "chunks"):
+                acc[key] = acc.get(key, 0) + st[key]
+            for grp in ("cycles", "kernel_cycles"):
+                for kk2, v in st.get(grp, {}).items():
+                    acc[f"{grp}.{kk2}"] = acc.get(f"{grp}.{kk2}", 0) + v
+    n = len(lat)
+    out = {"drain": drain, "calls": n, "publishes_per_call": n_pub / n, "runs_per_call": n_runs / n,
+           "p50_us": float(np.median(lat) * 1e6), "mean_us": float(np.mean(lat) * 1e6),
+           "engine_us_mean": float(np.mean(eng) * 1e3) if eng else None,
+           "engine_us_p50": float(np.median(eng) * 1e3) if eng else None,
+           "per_engine_call": {k2: round(v / max(len(eng), 1), 1) for k2, v in acc.items()}}
+    print(json.dumps(out), flush=True)

@@ -6,7 +6,9 @@ import oracle as O
 from openwhisk_amd import workload as W
 name = sys.argv[1]; nact = int(sys.argv[2]) if len(sys.argv)>2 else None
 out_root = sys.argv[3] if len(sys.argv) > 3 else '/tmp/sim'
-w = W.config(name, n_activations=nact)
+ns = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+w = W.config(name, n_activations=nact, n_shards=ns)
+if ns > 1: name = f'{name}_of{ns}'
 st = O.state_for(w)
 nm, nb = st.managed_size, st.blackbox_size
 ms, bs = np.array(st.managed_step_sizes,np.int32), np.array(st.blackbox_step_sizes,np.int32)
