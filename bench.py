@@ -234,6 +234,7 @@ def shim_path(w, o_inv, dev_index, drains=(64, 512, 4096), budget_jobs=(120_000,
         n_jobs = len(ids) if budget is None else min(budget, len(ids))
         for mode in ("calls", "fused"):
             b.restore()
+            rs0 = b.resident_stats()
             inv = np.full(len(act), -9, np.int32)
             fl = np.zeros(len(act), np.uint8)
             lat, n_pub = [], 0
@@ -295,13 +296,17 @@ def shim_path(w, o_inv, dev_index, drains=(64, 512, 4096), budget_jobs=(120_000,
             done = inv != -9
             exact = bool(np.array_equal(inv[done], o_inv[done])) if o_inv is not None else None
             lat_us = np.array(lat) * 1e6
+            rs1 = b.resident_stats()
             legs.append({"drain": drain, "mode": mode, "jobs": n_jobs, "calls": len(lat), "publishes": int(n_pub),
                          "p50_us": float(np.percentile(lat_us, 50)), "p99_us": float(np.percentile(lat_us, 99)),
-                         "decisions_per_s": n_pub / max(float(np.sum(lat)), 1e-9), "bit_exact": exact})
+                         "decisions_per_s": n_pub / max(float(np.sum(lat)), 1e-9), "bit_exact": exact,
+                         # owgs_process_batch's paths in this leg: resident engine calls / launches, launch-chain calls
+                         "resident": {k: rs1[k] - rs0[k] for k in ("served", "launches", "refused", "chained")}})
     b.close()
     return {"path": "host buffers through the C ABI as the JNI shim calls it (queue order: each batch's completions, "
                     "then its publishes); calls = owgs_release_batch + owgs_publish_batch per run, fused = "
-                    "owgs_process_batch per drained batch; latency = the C call", "legs": legs}
+                    "owgs_process_batch per drained batch (small calls: the resident engine, owgs_resident.hip); "
+                    "latency = the C call", "legs": legs}
 
 
 def dry_run(args):
@@ -579,6 +584,8 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": pmc["bytes"] if pmc else None,
                          "traffic_source": pmc["source"] if pmc else f"no --pmc pass recorded for this build ({key})",
+                         # what limits this kernel instead: one CU's instruction issue along the decision chain
+                         "issue": pmc.get("issue") if pmc else None,
                          "kernel": "owgs_engine_kernel" if K == 1 else "owgs_engine_multi_kernel",
                          "kernel_ms": kern_ms, "replay_ms": replay_ms, "shards_per_launch": per_launch,
                          "algorithmic_bytes": algo["survey"] * per_launch,

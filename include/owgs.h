@@ -137,9 +137,13 @@ int owgs_release_batch(owgs_ctx* ctx, int32_t n, const int32_t* invoker, const i
  * completions [rel_off[r], rel_off[r+1]) (SCPB:327-331 via CommonLoadBalancer.processCompletion, CLB:260-346; invoker
  * and action handle of the ActivationEntry, invoker < 0 = no entry) and then the scheduling half of publish
  * (SCPB:257-290) for the activations [pub_off[r], pub_off[r+1]).  Same results as alternating owgs_release_batch and
- * owgs_publish_batch calls; one pinned copy in, one launch chain, one pinned copy out, one synchronisation.
- * rel_off / pub_off have n_runs + 1 entries starting at 0; seq may be NULL (seq = seq_base + publish index);
- * rel_flags may be NULL. */
+ * owgs_publish_batch calls.  Small calls on identity pools without watched pairs (at most OWGS_RES_MAX = 1024
+ * releases + publishes by default) are served by a resident engine that keeps the slot state on chip between calls:
+ * inputs and outputs through pinned host memory, a doorbell, no launch or synchronisation per call; it writes the
+ * state back and exits when any other entry point of the context is called, or after 20 ms without a call
+ * (OWGS_RES_IDLE_US; OWGS_RESIDENT=0 disables it).  Other calls: one pinned copy in, one launch chain, one pinned copy
+ * out, one synchronisation.  rel_off / pub_off have n_runs + 1 entries starting at 0; seq may be NULL (seq = seq_base
+ * + publish index); rel_flags may be NULL. */
 int owgs_process_batch(owgs_ctx* ctx, int32_t n_runs, const int32_t* rel_off, const int32_t* rel_invoker,
                        const int32_t* rel_action, uint8_t* rel_flags, const int32_t* pub_off,
                        const int32_t* pub_action, const uint64_t* seq, uint64_t seq_base, int32_t* out_invoker,
@@ -339,6 +343,11 @@ int owgs_serialize_activations_device(owgs_ctx* ctx, const owgs_msg_batch* batch
 /* Duration of the last owgs_engine_kernel launch (HIP events recorded on its stream right before and after it);
  * waits for it to finish.  Measurement hook for bench.py's roofline. */
 int owgs_engine_ms(owgs_ctx* ctx, float* ms);
+
+/* Counters of owgs_process_batch's two paths: out[0] calls the resident engine served, [1] its launches, [2] calls it
+ * refused untouched (a release that could leave the on-chip permit range; the chain took them), [3] calls the launch
+ * chain took, [4] 1 while a resident engine is live.  Returns the number of counters (5). */
+int owgs_resident_stats(owgs_ctx* ctx, int64_t* out, int32_t cap);
 
 /* Restore the slot state captured by owgs_snapshot (bench: every timed step starts from the same state). */
 int owgs_snapshot(owgs_ctx* ctx);

@@ -97,6 +97,7 @@ def lib() -> C.CDLL:
         "owgs_health_events": (C.c_int, [P, i32, P, P, P, P, C.c_int64, i32]),
         "owgs_register_templates": (C.c_int, [P, i32, P, P, P, P, P]),
         "owgs_engine_ms": (C.c_int, [P, P]),
+        "owgs_resident_stats": (C.c_int, [P, P, i32]),
         "owgs_set_root_controller": (C.c_int, [P, C.c_char_p, i32]),
         "owgs_serialize_activations": (C.c_int, [P, P, i32, P, C.c_int64, P, P, P, P, P]),
         "owgs_serialize_activations_device": (C.c_int, [P, P, i32, P, C.c_int64, P, P, P, P, P, P]),

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -91,6 +92,8 @@ extern "C" hipError_t owgs_launch_relmeta(int32_t n, const int32_t* act, const i
                                           const int32_t* act_maxc, const int32_t* act_slot, int32_t* mem,
                                           int32_t* maxc, int32_t* slot, hipStream_t s);
 extern "C" hipError_t owgs_launch_w_update(const OwgsWUpdateArgs* a, hipStream_t s);
+extern "C" size_t owgs_resident_image_bytes(int32_t n_slots, int32_t n_ids);
+extern "C" hipError_t owgs_launch_resident(const OwgsResArgs* a, size_t lds_bytes, hipStream_t s);
 extern "C" hipError_t owgs_launch_w_relgather(const int64_t* rel_aid, int32_t n, const int32_t* out_inv,
                                               const int32_t* act, const int32_t* act_mem, const int32_t* act_maxc,
                                               const int32_t* act_slot, int32_t* inv, int32_t* mem, int32_t* maxc,
@@ -102,7 +105,14 @@ namespace {
 struct EnvOpts {
     int opts = 0, cw = 0, deal = -1, variant = -1;
     bool trace = false, feat_all = false;
+    // owgs_process_batch through the resident engine: on/off, the largest call (releases + publishes) it takes, and
+    // its idle time before it writes the state back and exits (OWGS_RESIDENT=0 sends every call down the chain)
+    int res = 1, res_max = 1024;
+    long long res_idle_us = 20000;
     EnvOpts() {
+        if (const char* e = getenv("OWGS_RESIDENT")) res = atoi(e);
+        if (const char* e = getenv("OWGS_RES_MAX")) res_max = atoi(e);
+        if (const char* e = getenv("OWGS_RES_IDLE_US")) res_idle_us = atoll(e);
         feat_all = getenv("OWGS_FEAT_ALL") != nullptr;  // the general engine for every launch (A/B diagnostics)
         if (const char* e = getenv("OWGS_VARIANT")) variant = atoi(e);  // force an engine geometry (diagnostics)
         if (const char* o = getenv("OWGS_OPTS")) opts = atoi(o);
@@ -287,6 +297,18 @@ struct owgs_ctx {
     DevBuf<uint8_t> d_pin, d_pout;
     DevBuf<int32_t> f_src, f_cnt, f_tile;
     DevBuf<uint2> f_rec;
+    // owgs_process_batch through the resident engine (owgs_resident.hip): its stream, the pinned control block and
+    // call buffers, the call counter (the doorbell), whether a launch is live, and counters for owgs_resident_stats
+    hipStream_t res_stream = nullptr;
+    hipEvent_t ev_res = nullptr;
+    int32_t* res_ctl = nullptr;
+    int32_t* res_in = nullptr;
+    char* res_out = nullptr;
+    size_t res_in_cap = 0, res_out_cap = 0;
+    int32_t res_call = 0;
+    bool res_alive = false;
+    int32_t res_stage = 0;
+    int64_t res_n_calls = 0, res_n_launches = 0, res_n_bails = 0, res_n_chained = 0;
     DevBuf<unsigned long long> f_bound;  // per slot: what a fused call's releases can return (zero between calls)
     DevBuf<uint32_t> s_w_keys, s_w_vals;
     DevBuf<int32_t> s_w_wkey;
@@ -472,14 +494,17 @@ static void ovf_add(owgs_ctx* c, int64_t n) {
     if (c->ovf_probe) c->ovf_since += n;
 }
 
+// overflow capacity for `used` entries plus n_new activations
+static int64_t ovf_need(int64_t used, int64_t n_new) {
+    // (at least 2^19 entries, 12 MB with its scratch: the per-launch bound then runs out only every ~250k
+    // activations, so a batch-by-batch replay seldom has to read the count back)
+    int64_t want = 2 * (used + n_new + OWGS_CTC), cap = (int64_t)1 << 19;
+    while (cap < want && cap < ((int64_t)1 << 30)) cap <<= 1;
+    return cap;
+}
+
 static int ensure_ovf(owgs_ctx* c, int64_t n_new, hipStream_t s) {
-    auto need = [&](int64_t used) {
-        // (at least 2^19 entries, 12 MB with its scratch: the per-launch bound then runs out only every ~250k
-        // activations, so a batch-by-batch replay seldom has to read the count back)
-        int64_t want = 2 * (used + n_new + OWGS_CTC), cap = (int64_t)1 << 19;
-        while (cap < want && cap < ((int64_t)1 << 30)) cap <<= 1;
-        return cap;
-    };
+    auto need = [&](int64_t used) { return ovf_need(used, n_new); };
     if (c->ovf_cap >= need(c->ovf_used_ub)) return OWGS_OK;
     if (c->ovf_probe && hipEventQuery(c->ev_ovf) == hipSuccess) {  // a count that arrived meanwhile: no wait
         c->ovf_probe = false;
@@ -880,6 +905,194 @@ static int reclaim_slots(owgs_ctx* c) {
     return OWGS_OK;
 }
 
+// ---------------------------------------------------------------------------------------------- resident engine
+// owgs_process_batch's small calls go to a resident engine (owgs_resident.hip) that keeps the slot state in LDS
+// between calls.  Every other entry point reads or replaces that state, so it stops the engine first (the engine
+// writes the state back to HBM and exits) -- OWGS_ENTER below; the next eligible call launches it again.
+static int res_quiesce(owgs_ctx* c) {
+    if (!c->res_alive) return OWGS_OK;
+    __atomic_store_n(&c->res_ctl[OWGS_RES_BELL], -1, __ATOMIC_RELEASE);
+    c->res_alive = false;
+    HIPCHK(c, hipStreamSynchronize(c->res_stream));
+    return OWGS_OK;
+}
+
+#define OWGS_ENTER(c)                             \
+    do {                                          \
+        (void)hipSetDevice((c)->cfg.device);      \
+        const int q_ = res_quiesce(c);            \
+        if (q_) return q_;                        \
+    } while (0)
+
+static size_t res_stage_bytes(const owgs_ctx* c) {
+    const size_t img = owgs_resident_image_bytes(c->n_slots, c->n_ids);
+    return img >= OWGS_LDS_BYTES ? 0 : std::min<size_t>(OWGS_LDS_BYTES - img, 64 * 1024) & ~(size_t)15;
+}
+
+// identity pools, no watched pairs (their releases need the ordered kernels), a call the staging area holds
+static bool res_eligible(const owgs_ctx* c, int32_t n_runs, int32_t NR, int32_t NP, bool has_seq) {
+    if (env_opts().res <= 0 || c->pool_mode != 0 || c->w_cap > 0) return false;
+    if ((int64_t)NR + NP > env_opts().res_max || NP + NR == 0) return false;
+    if (c->n_slots > OWGS_MAX_SLOTS_CT || c->n_ids > c->n_slots || c->nm > (int32_t)OWGS_AM_POS_MASK ||
+        c->nb > (int32_t)OWGS_AM_POS_MASK || c->a_mem.empty())
+        return false;
+    const size_t runs = ((size_t)n_runs + 4) & ~(size_t)3;
+    const size_t need = 8 * runs + 16 * (size_t)NR + 16 * (size_t)NP + (has_seq ? 8 * (size_t)NP : 0);
+    if (need > res_stage_bytes(c)) return false;
+    // a map that may outgrow its overflow table during the call: the chained path grows it
+    if (c->any_conc && c->res_alive && c->ovf_cap < ovf_need(c->ovf_used_ub, NP)) return false;
+    return true;
+}
+
+static int res_launch(owgs_ctx* c) {
+    if (!c->res_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->res_stream, hipStreamNonBlocking));
+    if (!c->ev_res) HIPCHK(c, hipEventCreateWithFlags(&c->ev_res, hipEventDisableTiming));
+    if (!c->res_ctl) {
+        HIPCHK(c, hipHostMalloc((void**)&c->res_ctl, OWGS_RES_CTL_WORDS * sizeof(int32_t), hipHostMallocCoherent));
+        memset(c->res_ctl, 0, OWGS_RES_CTL_WORDS * sizeof(int32_t));
+    }
+    if (c->any_conc) {  // the map's overflow, sized for this call (before the engine holds the table)
+        const int rc = ensure_ovf(c, env_opts().res_max, c->stream);
+        if (rc) return rc;
+    }
+    HIPCHK(c, c->d_ct_tmp.reserve((size_t)2 * OWGS_CTC));
+    // the state in HBM must be current: the resident stream waits for the context's stream and its last async call
+    HIPCHK(c, hipEventRecord(c->ev_res, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->res_stream, c->ev_res, 0));
+    if (c->tail_valid && c->tail_stream != c->stream) HIPCHK(c, hipStreamWaitEvent(c->res_stream, c->ev_tail, 0));
+    OwgsResArgs a{};
+    a.permits = c->d_permits.p;
+    a.n_slots = c->n_slots;
+    a.usable = c->d_usable.p;
+    a.n_ids = c->n_ids;
+    a.nm = c->nm;
+    a.nb = c->nb;
+    a.ct_keys = c->d_ct_keys.p;
+    a.ct_vals = c->d_ct_vals.p;
+    a.ct_tmp = c->d_ct_tmp.p;
+    a.ovf = ovf_args(c);
+    a.act_meta = c->d_act_meta.p;
+    a.act_slot = c->d_act_slot.p;
+    a.n_actions = (int32_t)c->a_mem.size();
+    a.rng_seed = c->cfg.rng_seed;
+    a.err = c->d_err.p;
+    a.ctl = c->res_ctl;
+    a.in = c->res_in;
+    a.out = c->res_out;
+    a.stage_bytes = (int32_t)res_stage_bytes(c);
+    a.last_call = c->res_call;
+    a.idle_ticks = env_opts().res_idle_us * 100;  // s_memrealtime: 100 MHz
+    volatile int32_t* ctl = c->res_ctl;
+    ctl[OWGS_RES_STATE] = 0;
+    ctl[OWGS_RES_DONE] = c->res_call;
+    __atomic_store_n(&c->res_ctl[OWGS_RES_BELL], c->res_call, __ATOMIC_RELEASE);
+    const size_t lds = owgs_resident_image_bytes(c->n_slots, c->n_ids) + (size_t)a.stage_bytes;
+    HIPCHK(c, owgs_launch_resident(&a, lds, c->res_stream));
+    c->res_alive = true;
+    ++c->res_n_launches;
+    return OWGS_OK;
+}
+
+// one owgs_process_batch call through the resident engine; *served = 0: refused untouched (the caller takes the chain)
+static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, const int32_t* rel_invoker,
+                       const int32_t* rel_action, uint8_t* rel_flags, const int32_t* pub_off, const int32_t* pub_action,
+                       const uint64_t* seq, uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, int* served) {
+    *served = 0;
+    const int32_t NR = rel_off[n_runs], NP = pub_off[n_runs];
+    // inputs (int32 words): rel_off, pub_off, rel_inv, rel_act, pub_act, seq (u64 at an even word); outputs (bytes):
+    // out_inv, out_flags, rel_flags
+    const size_t i_roff = 0, i_poff = (size_t)n_runs + 1, i_rinv = 2 * ((size_t)n_runs + 1), i_ract = i_rinv + NR;
+    const size_t i_pact = i_ract + NR, i_seq = (i_pact + NP + 1) & ~(size_t)1;
+    const size_t in_bytes = 4 * (i_seq + (seq ? 2 * (size_t)NP : 0));
+    const size_t o_inv = 0, o_fl = 4 * (size_t)NP, o_rfl = o_fl + NP, out_bytes = o_rfl + NR + 16;
+    if (in_bytes > c->res_in_cap || out_bytes > c->res_out_cap) {  // the engine holds the buffers' addresses
+        const int q = res_quiesce(c);
+        if (q) return q;
+        if (in_bytes > c->res_in_cap) {
+            if (c->res_in) (void)hipHostFree(c->res_in);
+            c->res_in = nullptr;
+            c->res_in_cap = 0;
+            const size_t cap = std::max<size_t>(2 * in_bytes, 64 * 1024);
+            HIPCHK(c, hipHostMalloc((void**)&c->res_in, cap, hipHostMallocCoherent));
+            c->res_in_cap = cap;
+        }
+        if (out_bytes > c->res_out_cap) {
+            if (c->res_out) (void)hipHostFree(c->res_out);
+            c->res_out = nullptr;
+            c->res_out_cap = 0;
+            const size_t cap = std::max<size_t>(2 * out_bytes, 32 * 1024);
+            HIPCHK(c, hipHostMalloc((void**)&c->res_out, cap, hipHostMallocCoherent));
+            c->res_out_cap = cap;
+        }
+    }
+    if (!c->res_alive) {
+        const int rc = res_launch(c);
+        if (rc) return rc;
+    }
+    int32_t* I = c->res_in;
+    memcpy(I + i_roff, rel_off, 4 * ((size_t)n_runs + 1));
+    memcpy(I + i_poff, pub_off, 4 * ((size_t)n_runs + 1));
+    if (NR) {
+        memcpy(I + i_rinv, rel_invoker, 4 * (size_t)NR);
+        memcpy(I + i_ract, rel_action, 4 * (size_t)NR);
+    }
+    if (NP) memcpy(I + i_pact, pub_action, 4 * (size_t)NP);
+    if (seq && NP) memcpy(I + i_seq, seq, 8 * (size_t)NP);
+    volatile int32_t* H = c->res_ctl + OWGS_RES_HDR;
+    const int32_t hdr[15] = {n_runs, NR, NP, seq ? 1 : 0, (int32_t)(uint32_t)seq_base, (int32_t)(uint32_t)(seq_base >> 32),
+                             (int32_t)i_roff, (int32_t)i_poff, (int32_t)i_rinv, (int32_t)i_ract, (int32_t)i_pact,
+                             (int32_t)i_seq, (int32_t)o_inv, (int32_t)o_fl, (int32_t)o_rfl};
+    for (int k = 0; k < 15; ++k) H[k] = hdr[k];
+    for (int attempt = 0;; ++attempt) {
+        const int32_t k = ++c->res_call;
+        __atomic_store_n(&c->res_ctl[OWGS_RES_BELL], k, __ATOMIC_RELEASE);
+        const auto t0 = std::chrono::steady_clock::now();
+        bool exited = false;
+        for (long spin = 0;; ++spin) {
+            if (__atomic_load_n(&c->res_ctl[OWGS_RES_DONE], __ATOMIC_ACQUIRE) == k) break;
+            if (__atomic_load_n(&c->res_ctl[OWGS_RES_STATE], __ATOMIC_ACQUIRE) == 2 &&
+                __atomic_load_n(&c->res_ctl[OWGS_RES_DONE], __ATOMIC_ACQUIRE) != k) {
+                exited = true;  // it went idle and wrote the state back before it saw this call
+                break;
+            }
+            if ((spin & 1023) == 1023 &&
+                std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+                c->res_alive = false;  // (nothing to wait for safely: the context is unusable from here)
+                return c->fail(OWGS_EDEVICE, "resident engine did not answer");
+            }
+            __builtin_ia32_pause();
+        }
+        if (!exited) break;
+        HIPCHK(c, hipStreamSynchronize(c->res_stream));
+        c->res_alive = false;
+        if (attempt >= 3) return c->fail(OWGS_EDEVICE, "resident engine exits before serving a call");
+        const int rc = res_launch(c);
+        if (rc) return rc;
+    }
+    const int32_t res = __atomic_load_n(&c->res_ctl[OWGS_RES_RESULT], __ATOMIC_ACQUIRE);
+    const int bail = res & 0xFF, e = res >> 8;
+    if (bail) {
+        ++c->res_n_bails;
+        return OWGS_OK;  // nothing applied: the chained path takes the call
+    }
+    ++c->res_n_calls;
+    if (c->any_conc) ovf_add(c, NP);
+    if (NP) {
+        memcpy(out_invoker, c->res_out + o_inv, 4 * (size_t)NP);
+        memcpy(out_flags, c->res_out + o_fl, (size_t)NP);
+    }
+    if (NR && rel_flags) memcpy(rel_flags, c->res_out + o_rfl, (size_t)NR);
+    *served = 1;
+    if (e) {
+        if (e & OWGS_ERR_CTAB_FULL) return c->fail(OWGS_ENOMEM, "concurrency table full");
+        if (e & OWGS_ERR_OPS) return c->fail(OWGS_ERANGE, "operationCount beyond the engine's range");
+        if (e & OWGS_ERR_INTERNAL) return c->fail(OWGS_EDEVICE, "engine invariant violated");
+        if (e & OWGS_ERR_PERMITS) return c->fail(OWGS_ERANGE, "slot permits outside the engine's range [-2^29, 2^29) MB");
+        return c->fail(OWGS_EINVAL, "call names an unknown action");
+    }
+    return OWGS_OK;
+}
+
 extern "C" {
 
 int owgs_abi_version(void) { return OWGS_ABI_VERSION; }
@@ -962,6 +1175,16 @@ int owgs_create(const owgs_config* cfg, owgs_ctx** out) {
 void owgs_destroy(owgs_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->cfg.device);
+    (void)res_quiesce(c);
+    if (c->res_stream) (void)hipStreamDestroy(c->res_stream);
+    c->res_stream = nullptr;
+    if (c->ev_res) (void)hipEventDestroy(c->ev_res);
+    c->ev_res = nullptr;
+    if (c->res_ctl) (void)hipHostFree(c->res_ctl);
+    if (c->res_in) (void)hipHostFree(c->res_in);
+    if (c->res_out) (void)hipHostFree(c->res_out);
+    c->res_ctl = c->res_in = nullptr;
+    c->res_out = nullptr;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf<int32_t>* i32s[] = {&c->d_permits, &c->d_pool_words, &c->d_hlist, &c->d_act_slot, &c->d_act_hash,
                                &c->d_act_mem,  &c->d_act_maxc,   &c->d_steps,  &c->d_cpx,     &c->d_err,
@@ -1080,7 +1303,7 @@ const char* owgs_last_error(const owgs_ctx* c) { return c ? c->err.c_str() : "nu
 int owgs_update_invokers(owgs_ctx* c, int32_t n, const int32_t* ids, const int64_t* user_memory_bytes,
                          const uint8_t* status) {
     if (!c || n < 0 || (n > 0 && (!ids || !user_memory_bytes || !status))) return OWGS_EINVAL;
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -1157,7 +1380,7 @@ int owgs_update_invokers(owgs_ctx* c, int32_t n, const int32_t* ids, const int64
 // SCPB:561-584
 int owgs_update_cluster(owgs_ctx* c, int32_t new_size) {
     if (!c) return OWGS_EINVAL;
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -1219,7 +1442,7 @@ int owgs_register_actions(owgs_ctx* c, int32_t n, const char* ns_bytes, const in
             }
         }
     }
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -1348,7 +1571,7 @@ int owgs_publish_batch(owgs_ctx* c, int32_t n, const int32_t* action, const uint
     if (!c || n < 0 || (n > 0 && (!action || !out_invoker || !out_flags))) return OWGS_EINVAL;
     if (n == 0) return OWGS_OK;
     if (!registered(c, n, action)) return c->fail(OWGS_ENOENT, "unknown action");
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -1437,7 +1660,7 @@ int owgs_release_batch(owgs_ctx* c, int32_t n, const int32_t* invoker, const int
     if (!c || n < 0 || (n > 0 && (!invoker || !action))) return OWGS_EINVAL;
     if (n == 0) return OWGS_OK;
     if (!registered(c, n, action)) return c->fail(OWGS_ENOENT, "unknown action");
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -1486,7 +1709,7 @@ int owgs_schedule_walks(owgs_ctx* c, int32_t n, const uint8_t* pool, const int32
         }
         xm[i] = make_uint2(x, y);  // no cursor: explicit walks are independent
     }
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -1516,7 +1739,7 @@ int owgs_schedule_walks(owgs_ctx* c, int32_t n, const uint8_t* pool, const int32
 
 int owgs_set_slots(owgs_ctx* c, int32_t n, const int32_t* permits) {
     if (!c || n < 0 || (n > 0 && !permits)) return OWGS_EINVAL;
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -1533,7 +1756,7 @@ int owgs_set_slots(owgs_ctx* c, int32_t n, const int32_t* permits) {
 
 int owgs_set_pool(owgs_ctx* c, int32_t pool, int32_t n, const int32_t* ids, const uint8_t* status) {
     if (!c || (pool != 0 && pool != 1) || n < 0 || (n > 0 && (!ids || !status))) return OWGS_EINVAL;
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -1551,7 +1774,7 @@ int owgs_read_permits(owgs_ctx* c, int32_t* out, int32_t cap, int32_t* n_slots) 
     if (!c) return OWGS_EINVAL;
     if (n_slots) *n_slots = c->n_slots;
     if (!out || cap <= 0 || c->n_slots == 0) return OWGS_OK;
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -1563,7 +1786,7 @@ int owgs_read_permits(owgs_ctx* c, int32_t* out, int32_t cap, int32_t* n_slots) 
 
 int owgs_read_concurrent(owgs_ctx* c, int32_t invoker, int32_t key, int32_t* permits, int32_t* op_count) {
     if (!c) return OWGS_EINVAL;
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -1612,7 +1835,7 @@ int owgs_step_sizes(owgs_ctx* c, int32_t pool, int32_t* out, int32_t cap, int32_
 int owgs_pairwise_coprime(owgs_ctx* c, int32_t x, int32_t* out, int32_t cap, int32_t* n) {
     if (!c || cap < 0) return OWGS_EINVAL;
     if (x > owgs_coprime_max()) return c->fail(OWGS_ERANGE, "x beyond the step-size kernel's range");
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -1697,7 +1920,7 @@ static int replay_device_span_impl(owgs_ctx* c, int64_t a_beg, int64_t a_end, in
     if (c->a_mem.empty()) return c->fail(OWGS_ENOENT, "no actions registered");
     const int64_t na = a_end - a_beg, nr = r_end - r_beg;
     if (na == 0 && nr == 0) return OWGS_OK;
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     hipStream_t hs = stream ? (hipStream_t)stream : c->stream;
     HIPCHK(c, c->w_rfl.reserve((size_t)std::max<int64_t>(nr, 1)));
     uint8_t* rf = rel_flags ? rel_flags + r_beg : c->w_rfl.p;
@@ -1770,7 +1993,7 @@ int owgs_replay_device_span(owgs_ctx* c, int64_t a_beg, int64_t a_end, int64_t r
                             const int64_t* rel_aid, uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags,
                             uint8_t* rel_flags, void* stream) {
     if (!c) return OWGS_EINVAL;
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     hipStream_t hs_ = stream ? (hipStream_t)stream : c->stream;
     int rc = order_on(c, hs_);
     if (!rc) rc = replay_device_span_impl(c, a_beg, a_end, r_beg, r_end, act, rel_aid, seq_base, out_invoker, out_flags, rel_flags, stream);
@@ -1804,7 +2027,7 @@ int owgs_replay_device(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, c
                        int64_t n_activations, const int64_t* rel_off, const int64_t* rel_aid, int64_t n_releases,
                        uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, uint8_t* rel_flags, void* stream) {
     if (!c) return OWGS_EINVAL;
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     hipStream_t hs_ = stream ? (hipStream_t)stream : c->stream;
     int rc = order_on(c, hs_);
     if (!rc) rc = replay_device_impl(c, n_batches, acq_off, act, n_activations, rel_off, rel_aid, n_releases, seq_base, out_invoker, out_flags, rel_flags, stream);
@@ -1886,6 +2109,10 @@ int owgs_replay_device_multi(owgs_ctx** cs, int32_t k, const owgs_replay_io* io,
     for (int32_t i = 0; i < k; ++i)
         if (!cs[i]) return OWGS_EINVAL;
     (void)hipSetDevice(cs[0]->cfg.device);
+    for (int32_t i = 0; i < k; ++i) {
+        const int q = res_quiesce(cs[i]);
+        if (q) return q;
+    }
     hipStream_t hs_ = stream ? (hipStream_t)stream : cs[0]->stream;
     int rc = OWGS_OK;
     for (int32_t i = 0; i < k && !rc; ++i) rc = order_on(cs[i], hs_);
@@ -1906,7 +2133,7 @@ static int replay_begin(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, 
         return OWGS_EINVAL;
     if (n_batches == 0) return OWGS_OK;
     if (c->a_mem.empty()) return c->fail(OWGS_ENOENT, "no actions registered");
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     base_args(c, A);
     A.seq_base = seq_base;
     A.out_inv = out_invoker;
@@ -1951,7 +2178,7 @@ int owgs_replay(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const in
                 uint8_t* rel_flags) {
     if (!c || n_batches < 0 || !acq_off || !act || !out_invoker || !out_flags || !rel_off) return OWGS_EINVAL;
     if (n_batches == 0) return OWGS_OK;
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -2040,7 +2267,7 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
         return OWGS_EINVAL;
     if (n_runs >= 0x1FFFF) return c->fail(OWGS_ERANGE, "more than 131070 runs in one call");
     if (!registered(c, NP, pub_action) || !registered(c, NR, rel_action)) return c->fail(OWGS_ENOENT, "unknown action");
-    (void)hipSetDevice(c->cfg.device);
+    (void)hipSetDevice(c->cfg.device);  // (the resident engine is stopped below only when the chain takes the call)
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -2057,6 +2284,18 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
             seq = nullptr;
         }
     }
+    // small calls: the resident engine (owgs_resident.hip), no launch, copy or synchronisation per call
+    if (res_eligible(c, n_runs, NR, NP, seq != nullptr)) {
+        int served = 0;
+        const int rr = res_process(c, n_runs, rel_off, rel_invoker, rel_action, rel_flags, pub_off, pub_action, seq,
+                                   seq_base, out_invoker, out_flags, &served);
+        if (rr || served) return rr;
+    }
+    {
+        const int q = res_quiesce(c);
+        if (q) return q;
+    }
+    ++c->res_n_chained;
     // ---- pinned staging: i64 offsets (publishes, releases, per-run {0, n}) | publish actions | release invokers |
     // release actions | seq
     auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
@@ -2195,7 +2434,7 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
 
 int owgs_snapshot(owgs_ctx* c) {
     if (!c) return OWGS_EINVAL;
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -2237,7 +2476,7 @@ static int restore_impl(owgs_ctx* c, void* stream) {
     if (!c || !c->has_snap || c->snap_slots != c->n_slots) return OWGS_EINVAL;
     // a key recycled since the snapshot may name another fqn@version now: the snapshot's entries would alias it
     if (c->slot_epoch != c->snap_slot_epoch) return c->fail(OWGS_EINVAL, "keys were recycled since the snapshot");
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     if (c->n_slots)
         HIPCHK(c, hipMemcpyAsync(c->d_permits.p, c->s_permits.p, (size_t)c->n_slots * 4, hipMemcpyDeviceToDevice, s));
@@ -2279,7 +2518,7 @@ static int restore_impl(owgs_ctx* c, void* stream) {
 
 int owgs_restore(owgs_ctx* c, void* stream) {
     if (!c) return OWGS_EINVAL;
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     hipStream_t hs_ = stream ? (hipStream_t)stream : c->stream;
     int rc = order_on(c, hs_);
     if (!rc) rc = restore_impl(c, stream);
@@ -2289,7 +2528,7 @@ int owgs_restore(owgs_ctx* c, void* stream) {
 
 static int update_health_device_impl(owgs_ctx* c, int32_t n, const uint8_t* status_dev, void* stream) {
     if (!c || n != (int32_t)c->status.size() || (n > 0 && !status_dev)) return OWGS_EINVAL;
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     if (n && c->pool_mode == 0 && !c->pool_override[0] && !c->pool_override[1] && c->d_status.p && c->d_usable.p) {
         // identity pools (position = id): health changes only the usable bitmap, and the engine counts the healthy
         // invokers of each pool from it (the overload fallback's |H|, SCPB:417-424).  Nothing else depends on the
@@ -2318,7 +2557,7 @@ static int update_health_device_impl(owgs_ctx* c, int32_t n, const uint8_t* stat
 
 int owgs_update_health_device(owgs_ctx* c, int32_t n, const uint8_t* status_dev, void* stream) {
     if (!c) return OWGS_EINVAL;
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     hipStream_t hs_ = stream ? (hipStream_t)stream : c->stream;
     int rc = order_on(c, hs_);
     if (!rc) rc = update_health_device_impl(c, n, status_dev, stream);
@@ -2328,7 +2567,7 @@ int owgs_update_health_device(owgs_ctx* c, int32_t n, const uint8_t* status_dev,
 
 int owgs_selftest(owgs_ctx* c) {
     if (!c) return OWGS_EINVAL;
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -2344,7 +2583,7 @@ int owgs_selftest(owgs_ctx* c) {
 
 int owgs_read_stats(owgs_ctx* c, uint64_t* out, int32_t cap) {
     if (!c || !out) return OWGS_EINVAL;
-    (void)hipSetDevice(c->cfg.device);
+    (void)hipSetDevice(c->cfg.device);  // (counters and events only: the resident engine keeps running)
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -2433,7 +2672,7 @@ int owgs_track_activations(owgs_ctx* c, int32_t n, const char* aid32, const int3
         if (!((ch >= '0' && ch <= '9') || (ch >= 'a' && ch <= 'f')))
             return c->fail(OWGS_EINVAL, "activation id is not 32 characters of [0-9a-f]");
     }
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -2541,7 +2780,7 @@ int owgs_process_acks_device(owgs_ctx* c, int32_t n, const uint8_t* bytes, const
     if (!c || n < 0 || (n > 0 && (!bytes || !off || !out_kind || !out_invoker || !out_ticket || !out_flags)))
         return OWGS_EINVAL;
     if (n == 0) return OWGS_OK;
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, stream ? (hipStream_t)stream : c->stream);
         if (ro_) return ro_;
@@ -2572,7 +2811,7 @@ int owgs_process_acks(owgs_ctx* c, int32_t n, const char* bytes, const int64_t* 
     if (n == 0) return OWGS_OK;
     for (int32_t i = 0; i < n; ++i)
         if (off[i + 1] < off[i] || off[i] < 0) return c->fail(OWGS_EINVAL, "offsets");
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -2603,7 +2842,7 @@ int owgs_complete_activations(owgs_ctx* c, int32_t n, const char* aid32, const i
     if (!c || n < 0 || (n > 0 && (!aid32 || !invoker || !flags || !out_kind || !out_ticket || !out_flags)))
         return OWGS_EINVAL;
     if (n == 0) return OWGS_OK;
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -2670,7 +2909,7 @@ int owgs_health_events(owgs_ctx* c, int32_t n, const int32_t* invoker, const uin
     }
     if (now_ms < prev || now_ms < 0 || now_ms >= (1LL << 60))
         return c->fail(OWGS_EINVAL, "health batch: now before its last event or outside [0, 2^60)");
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -2736,7 +2975,7 @@ int owgs_health_read(owgs_ctx* c, int32_t cap, int32_t* n, uint8_t* status, int6
     if (m == 0) return OWGS_OK;
     if (!status && !user_memory_bytes && !test_actions && !ring && !next_tick) return OWGS_OK;  // size query
     if (cap < m) return c->fail(OWGS_ERANGE, "health read: capacity below the status vector size");
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -2868,7 +3107,7 @@ int owgs_serialize_activations(owgs_ctx* c, const owgs_msg_batch* b, int32_t n_t
         if (b->tid_off[i + 1] < b->tid_off[i] || (need_c && b->content_off[i + 1] < b->content_off[i]) ||
             (need_r && b->trace_off[i + 1] < b->trace_off[i]))
             return c->fail(OWGS_EINVAL, "serialize: offsets must be non-decreasing");
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
@@ -2942,7 +3181,7 @@ int owgs_serialize_activations_device(owgs_ctx* c, const owgs_msg_batch* b, int3
     if (!c || !msg_batch_ok(b, n_topics) || cap < 0 || !out_off || !topic_start || (b->n > 0 && !out_order) ||
         (cap > 0 && !out) || (b->n > 0 && (!b->content_off || !b->trace_off)))
         return OWGS_EINVAL;
-    (void)hipSetDevice(c->cfg.device);
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, stream ? (hipStream_t)stream : c->stream);
         if (ro_) return ro_;
@@ -2973,10 +3212,17 @@ int owgs_serialize_activations_device(owgs_ctx* c, const owgs_msg_batch* b, int3
     return msg_run(c, A, n_topics, st, total, m);
 }
 
+int owgs_resident_stats(owgs_ctx* c, int64_t* out, int32_t cap) {
+    if (!c || cap < 0 || (cap > 0 && !out)) return OWGS_EINVAL;
+    const int64_t v[5] = {c->res_n_calls, c->res_n_launches, c->res_n_bails, c->res_n_chained, c->res_alive ? 1 : 0};
+    for (int32_t i = 0; i < cap && i < 5; ++i) out[i] = v[i];
+    return 5;
+}
+
 int owgs_engine_ms(owgs_ctx* c, float* ms) {
     if (!c || !ms) return OWGS_EINVAL;
     if (!c->ev_engine_valid) return c->fail(OWGS_ENOENT, "no engine launch yet");
-    (void)hipSetDevice(c->cfg.device);
+    (void)hipSetDevice(c->cfg.device);  // (counters and events only: the resident engine keeps running)
     HIPCHK(c, hipEventSynchronize(c->ev_engine[1]));
     HIPCHK(c, hipEventElapsedTime(ms, c->ev_engine[0], c->ev_engine[1]));
     return OWGS_OK;

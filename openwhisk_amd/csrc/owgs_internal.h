@@ -303,6 +303,42 @@ struct OwgsReleaseArgs {
     OwgsWatch w;         // watched pairs (w.cap == 0: none); their releases take the ordered kernel
 };
 
+// Resident engine (owgs_resident.hip): owgs_process_batch's small calls served by one workgroup that keeps the slot
+// state in LDS between calls, fed through a control block in pinned, coherent host memory.  Word indices of ctl:
+#define OWGS_RES_BELL 0     // host: call number (counts up from the launch's last_call), -1 = write back and exit
+#define OWGS_RES_DONE 16    // device: call number of the last call served (written after its outputs and result)
+#define OWGS_RES_STATE 32   // device: 1 = image loaded, 2 = written back and exiting
+#define OWGS_RES_RESULT 48  // device: the last call's outcome (0, OWGS_RES_BAIL_*) | its device error bits << 8
+#define OWGS_RES_USED 49    // device: primary-table entries (live + deleted) after the last call
+#define OWGS_RES_HDR 64     // host: the call -- n_runs, n_rel, n_pub, has_seq, seq_base lo, hi, then int32 indices
+                            // into `in` of rel_off, pub_off, rel_inv, rel_act, pub_act, seq (u64, even index), and
+                            // byte offsets into `out` of out_inv (i32), out_flags (u8), rel_flags (u8)
+#define OWGS_RES_CTL_WORDS 128
+#define OWGS_RES_BAIL_RELRISK 1  // a release could leave the LDS permit range: nothing applied, the host reruns the
+                                 // call through the ordered release kernels
+#define OWGS_RES_BAIL_STAGE 2    // the call does not fit the staging area (the host sized it: not expected)
+struct OwgsResArgs {
+    int32_t* permits;
+    int32_t n_slots;
+    const uint32_t* usable;      // identity pools only
+    int32_t n_ids, nm, nb;
+    uint32_t* ct_keys;
+    uint32_t* ct_vals;
+    uint32_t* ct_tmp;            // [2 * OWGS_CTC] scratch of the primary table's cleanup
+    OwgsOvf ovf;
+    const uint2* act_meta;
+    const int32_t* act_slot;
+    int32_t n_actions;
+    unsigned long long rng_seed;
+    int32_t* err;
+    int32_t* ctl;                // [OWGS_RES_CTL_WORDS] pinned, coherent
+    const int32_t* in;           // pinned inputs of a call
+    char* out;                   // pinned outputs of a call
+    int32_t stage_bytes;         // LDS bytes for a call's staged inputs
+    int32_t last_call;           // the bell's value at launch
+    long long idle_ticks;        // s_memrealtime ticks (100 MHz) without a call before the engine writes back and exits
+};
+
 // owgs_process_batch: the caller's releases (invoker, action handle) of each run as engine release records
 struct OwgsStageArgs {
     int32_t n_runs;

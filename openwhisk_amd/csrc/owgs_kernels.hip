@@ -67,6 +67,9 @@ typedef unsigned long long u64;
 #ifndef OWGS_OVF
 #define OWGS_OVF 1  // 0: measurement variant without the overflow table's fall-through paths
 #endif
+#ifndef OWGS_HOT_ROT
+#define OWGS_HOT_ROT 0  // engine wave (w + OWGS_HOT_ROT) % OWGS_EW walks hot slots w + 1, w + 1 + 8, .. (load balance)
+#endif
 #ifndef OWGS_HOT_IO
 #define OWGS_HOT_IO 1  // the I/O wave takes a share of the hot-action walks
 #endif
@@ -1776,7 +1779,8 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                 // slot h goes to the I/O wave when h % (OWGS_EW + 1) == 0 (it holds no lanes: its speculation is
                 // otherwise idle), else to engine wave h % (OWGS_EW + 1) - 1
                 {
-                    const int hw = OWGS_HOT_IO ? (io ? 0 : wave + 1) : (io ? NHOT : wave);
+                    const int wr = (wave + OWGS_EW - OWGS_HOT_ROT % OWGS_EW) % OWGS_EW;  // (io: unused)
+                    const int hw = OWGS_HOT_IO ? (io ? 0 : wr + 1) : (io ? NHOT : wr);
                     for (int h = hw; h < nhot; h += OWGS_HOT_IO ? OWGS_EW + 1 : OWGS_EW) {
                         const uint4 d = hdir[h];
                         if (d.z & (OWGS_AM_THROW | OWGS_AM_EMPTY)) continue;

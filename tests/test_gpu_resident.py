@@ -1,0 +1,212 @@
+"""owgs_process_batch through the resident engine (openwhisk_amd/csrc/owgs_resident.hip): the shim's small drained
+batches served by one workgroup that keeps the slot state on chip between calls, against the literal oracle driven
+one reference call at a time (releaseInvoker SCPB:327-331 via processCompletion CLB:260-346, then publish SCPB:257-290
+-> schedule SCPB:398-436 with NestedSemaphore tryAcquireConcurrent / forceAcquireConcurrent NS:32-91).
+
+Every comparison is per call (decisions, overload flags, release flags) and on the final permits; the resident
+counters (owgs_resident_stats) show which path served the calls, so a silent fallback to the launch chain fails the
+test."""
+import time
+
+import numpy as np
+import pytest
+
+import oracle as O
+from openwhisk_amd import Action, GpuShardingContainerPoolBalancer
+from openwhisk_amd import workload as W
+from openwhisk_amd.balancer import UNHEALTHY
+
+pytestmark = pytest.mark.gpu
+MB = 1024 * 1024
+
+
+class Shim:
+    """The shim's batching thread over one workload: jobs in arrival order (a batch's completions, then its
+    publishes), drained `drain` jobs at a time into runs; releases name the invoker of the activation's decision."""
+
+    def __init__(self, w, zombies=True):
+        self.w = w
+        self.g = GpuShardingContainerPoolBalancer(managed_fraction=w.managed_fraction,
+                                                  blackbox_fraction=w.blackbox_fraction, rng_seed=w.rng_seed)
+        self.o = O.BalancerState(w.managed_fraction, w.blackbox_fraction, rng_seed=w.rng_seed, zombies=zombies)
+        self.g.update_invokers_arrays(w.inv_ids, w.inv_mem, w.inv_status)
+        self.o.update_invokers(w.inv_ids, w.inv_mem, w.inv_status)
+        if w.cluster_size != 1:
+            self.g.update_cluster(w.cluster_size)
+            self.o.update_cluster(w.cluster_size)
+        self.gh, _ = self.g.register_actions(w.actions)
+        keys = {}
+        self.oh = [self.o.register_action(a.namespace, a.path, keys.setdefault(a.key, len(keys)), a.mem_mb,
+                                          a.max_concurrent, a.blackbox) for a in w.actions]
+        s = w.stream
+        self.jobs = []
+        for b in range(s.n_batches):
+            self.jobs += [(0, int(a)) for a in s.rel_aid[s.rel_off[b]:s.rel_off[b + 1]]]
+            self.jobs += [(1, i) for i in range(int(s.acq_off[b]), int(s.acq_off[b + 1]))]
+        self.pos = 0
+        self.seq = 0
+        self.dec = np.full(len(s.act), -9, np.int32)
+        self.calls = 0
+
+    def done(self):
+        return self.pos >= len(self.jobs)
+
+    def call(self, drain):
+        """one drained batch through owgs_process_batch, checked against the oracle (which replays the same jobs one
+        reference call at a time, so a release may name an activation published earlier in the same drain)"""
+        batch = self.jobs[self.pos:self.pos + drain]
+        self.pos += len(batch)
+        act = self.w.stream.act
+        ro, po, ri, ra, pa, pubs, orf, oi = [0], [0], [], [], [], [], [], []
+        i = 0
+        while i < len(batch):
+            while i < len(batch) and batch[i][0] == 0:
+                a = batch[i][1]
+                i += 1
+                if self.dec[a] < 0:  # a failed publish holds no ActivationEntry (CLB:278-279)
+                    continue
+                ri.append(int(self.dec[a]))
+                ra.append(int(self.gh[act[a]]))
+                orf.append(O._rel_bits(self.o.release(int(self.dec[a]), self.oh[act[a]])))
+            while i < len(batch) and batch[i][0] == 1:
+                a = batch[i][1]
+                i += 1
+                pubs.append(a)
+                pa.append(int(self.gh[act[a]]))
+                x, f = self.o.publish(self.oh[act[a]], self.seq + len(oi))
+                oi.append((int(x), int(f)))
+                self.dec[a] = x
+            ro.append(len(ri))
+            po.append(len(pa))
+        gi, gf, grf = self.g.process_batch(ro, ri, ra, po, pa, seq_base=self.seq)
+        self.seq += len(pubs)
+        assert grf.tolist() == orf, self.calls
+        assert [(int(x), int(f)) for x, f in zip(gi, gf)] == oi, self.calls
+        self.calls += 1
+        return len(pubs), len(ri)
+
+
+@pytest.mark.parametrize("cfg,kw", [
+    ("headline", dict(n_activations=30_000, n_invokers=1000, n_actions=2000, n_namespaces=200)),
+    ("c4", dict(n_activations=30_000)),
+    ("c2", dict(n_activations=30_000)),
+    ("c3", dict(n_activations=30_000)),
+])
+def test_resident_small_drains_match_oracle(cfg, kw):
+    """Drains of 1..600 jobs (the shim's steady state): every call is served by the resident engine, without a
+    relaunch, bit-exact with the oracle; concurrent actions, shared fqn@version keys, unhealthy invokers and overload
+    fallbacks included (configs[1..3] and a reduced headline)."""
+    w = W.config(cfg, **kw)
+    sh = Shim(w)
+    rng = np.random.default_rng(7)
+    pubs = 0
+    while not sh.done():
+        n, _ = sh.call(int(rng.integers(1, 601)))
+        pubs += n
+    st = sh.g.resident_stats()
+    assert st["served"] == sh.calls and st["chained"] == 0 and st["refused"] == 0, st
+    assert st["launches"] == 1, st
+    assert np.array_equal(sh.g.permits(), sh.o.permits())
+    assert sh.g.resident_stats()["alive"] == 0  # permits() stopped it (the state was written back)
+    assert pubs == int(w.stream.acq_off[-1])
+
+
+def test_resident_interleaved_with_the_chain_and_state_updates():
+    """Small drains on the resident engine, large ones (beyond OWGS_RES_MAX) on the launch chain, a health change
+    (owgs_update_invokers) and a snapshot read in between: each non-resident entry point stops the engine, which writes
+    the state back; the next small call launches it again from that state."""
+    w = W.config("headline", n_activations=40_000, n_invokers=800, n_actions=1500, n_namespaces=150)
+    sh = Shim(w)
+    rng = np.random.default_rng(3)
+    k = 0
+    while not sh.done():
+        k += 1
+        if k % 7 == 0:
+            sh.call(3000)  # chained
+        elif k % 11 == 0:
+            st = w.inv_status.copy()
+            st[rng.choice(len(st), size=len(st) // 25, replace=False)] = UNHEALTHY
+            sh.g.update_invokers_arrays(w.inv_ids, w.inv_mem, st)
+            sh.o.update_invokers(w.inv_ids, w.inv_mem, st)
+        elif k % 13 == 0:
+            assert np.array_equal(sh.g.permits(), sh.o.permits())
+        else:
+            sh.call(int(rng.integers(1, 400)))
+    st = sh.g.resident_stats()
+    assert st["chained"] >= 3 and st["served"] >= 20 and st["launches"] >= 5, st
+    assert np.array_equal(sh.g.permits(), sh.o.permits())
+
+
+def test_resident_engine_exits_when_idle_and_relaunches():
+    """After 20 ms without a call (OWGS_RES_IDLE_US) the engine writes the state back and exits by itself; the next
+    call launches it again and continues from that state."""
+    w = W.config("c4", n_activations=6_000)
+    sh = Shim(w)
+    for _ in range(5):
+        sh.call(200)
+        time.sleep(0.1)
+    st = sh.g.resident_stats()
+    assert st["served"] == 5 and st["launches"] == 5, st
+    while not sh.done():
+        sh.call(300)
+    assert np.array_equal(sh.g.permits(), sh.o.permits())
+
+
+def test_resident_map_beyond_the_primary_table():
+    """More live (invoker, fqn) entries than the on-chip primary holds (3,840): new keys go to the HBM overflow, and
+    the cleanup between calls keeps the primary's chains short; every call still resident and exact."""
+    rng = np.random.default_rng(5)
+    n_inv, n_act = 64, 6000
+    g = GpuShardingContainerPoolBalancer(managed_fraction=1.0, blackbox_fraction=0.0, rng_seed=9)
+    o = O.BalancerState(1.0, 0.0, rng_seed=9, zombies=True)
+    ids, mem = np.arange(n_inv, dtype=np.int32), np.full(n_inv, 1 << 40, np.int64)
+    g.update_invokers_arrays(ids, mem, np.zeros(n_inv, np.uint8))
+    o.update_invokers(ids, mem, np.zeros(n_inv, np.uint8))
+    acts = [Action(f"ns{a % 7}", f"ns{a % 7}/p/a{a}", "0.0.1", 128, 2) for a in range(n_act)]
+    gh, _ = g.register_actions(acts)
+    oh = [o.register_action(a.namespace, a.path, k, a.mem_mb, a.max_concurrent) for k, a in enumerate(acts)]
+    live = []  # (invoker, action) of activations in flight
+    seq = 0
+    for call in range(60):
+        nrel = min(len(live), int(rng.integers(0, 200)))
+        pick = rng.choice(len(live), size=nrel, replace=False) if nrel else np.zeros(0, int)
+        rel = [live[j] for j in sorted(pick)]
+        live = [x for j, x in enumerate(live) if j not in set(pick.tolist())]
+        pubs = rng.integers(0, n_act, size=int(rng.integers(100, 400)))
+        orf = [O._rel_bits(o.release(x, oh[a])) for x, a in rel]
+        oi = [o.publish(oh[a], seq + k) for k, a in enumerate(pubs)]
+        gi, gf, grf = g.process_batch([0, len(rel)], [x for x, _ in rel], [gh[a] for _, a in rel], [0, len(pubs)],
+                                      [gh[a] for a in pubs], seq_base=seq)
+        seq += len(pubs)
+        assert grf.tolist() == orf, call
+        assert [(int(x), int(f)) for x, f in zip(gi, gf)] == oi, call
+        live += [(int(x), int(a)) for x, a in zip(gi, pubs) if x >= 0]
+    st = g.resident_stats()
+    assert st["served"] == 60 and st["chained"] == 0, st
+    assert np.array_equal(g.permits(), o.permits())
+
+
+def test_resident_refuses_releases_beyond_the_permit_range():
+    """A call whose releases could push a slot beyond the on-chip permit range (2^29 MB) is refused untouched and
+    taken by the launch chain, whose release kernels apply ForcibleSemaphore's bound release by release (FS:48-50)."""
+    lim = 2**29
+    g = GpuShardingContainerPoolBalancer(managed_fraction=1.0, blackbox_fraction=0.0)
+    o = O.BalancerState(1.0, 0.0, zombies=True)
+    mem_b = (lim - 300) * MB
+    g.update_invokers_arrays(np.array([0], np.int32), np.array([mem_b], np.int64), np.zeros(1, np.uint8))
+    o.update_invokers(np.array([0], np.int32), np.array([mem_b], np.int64), np.zeros(1, np.uint8))
+    acts = [Action("ns", "ns/c", "0.0.1", 256, 4), Action("ns", "ns/a", "0.0.1", 128, 1)]
+    hs, _ = g.register_actions(acts)
+    oh = [o.register_action(a.namespace, a.path, k, a.mem_mb, a.max_concurrent, a.blackbox) for k, a in enumerate(acts)]
+    gi, gf, _ = g.process_batch([0, 0], [], [], [0, 3], [hs[0]] * 3)
+    oi = [o.publish(oh[0], k) for k in range(3)]
+    assert [(int(a), int(b)) for a, b in zip(gi, gf)] == oi
+    assert g.resident_stats()["served"] == 1
+    gi2, gf2, grf = g.process_batch([0, 3], [0, 0, 0], [hs[0]] * 3, [0, 2], [hs[0], hs[1]], seq_base=3)
+    orf = [O._rel_bits(o.release(0, oh[0])) for _ in range(3)]
+    oi2 = [o.publish(oh[p], 3 + k) for k, p in enumerate([0, 1])]
+    assert grf.tolist() == orf
+    assert [(int(a), int(b)) for a, b in zip(gi2, gf2)] == oi2
+    st = g.resident_stats()
+    assert st["refused"] == 1 and st["chained"] == 1, st
+    assert g.permits().tolist() == o.permits().tolist()

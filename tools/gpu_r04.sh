@@ -9,6 +9,12 @@ for s in ${STEPS:-tests smoke}; do
     handoff)  # cross-CU hand-off latency
       timeout -k 10 60 ./tools/micro/handoff > $O/handoff.json 2>&1
       rc=$?; cat $O/handoff.json; [ $rc -eq 0 ] || stop handoff $rc ;;
+    launchlat)  # fixed costs of a shim call: launches, copies, zero-copy, resident-kernel doorbell
+      timeout -k 10 120 ./tools/micro/launch_lat > $O/launch_lat.json 2>&1
+      rc=$?; cat $O/launch_lat.json; [ $rc -eq 0 ] || stop launchlat $rc ;;
+    restests)  # the resident engine's tests alone (fast feedback)
+      timeout -k 10 300 python -u -m pytest tests/test_gpu_resident.py tests/test_gpu_shim_sequence.py -x -v --timeout 200 --timeout-method thread > $O/pytest_res.log 2>&1
+      rc=$?; tail -3 $O/pytest_res.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error|error|assert" $O/pytest_res.log | head -30; stop restests $rc; } ;;
     tests)
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
       rc=$?; tail -2 $O/pytest_gpu.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error|error" $O/pytest_gpu.log | head -20; stop tests $rc; } ;;

@@ -23,22 +23,47 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 
-def run_pass(counter: str, argv, out_dir: str) -> list:
+def run_pass(counter: str, argv, out_dir: str):
+    """one rocprofv3 --pmc pass; counter = one name (returns its values per engine dispatch) or several separated by
+    spaces (returns {name: values})"""
+    names = counter.split()
     shutil.rmtree(out_dir, ignore_errors=True)
-    cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc", counter, "-d", out_dir, "-o", "run",
+    cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc"] + names + ["-d", out_dir, "-o", "run",
            "--output-format", "csv", "--", sys.executable, os.path.join(ROOT, "tools", "pmc_engine.py")] + argv
     with open(out_dir + ".log", "w") as log:
         rc = subprocess.call(cmd, stdout=log, stderr=subprocess.STDOUT, env=dict(os.environ, TMPDIR="/tmp"))
     if rc != 0:
         raise SystemExit(f"pmc pass {counter} rc={rc} (log {out_dir}.log)")
-    vals = []
+    vals = {n: [] for n in names}
     for f in sorted(glob.glob(os.path.join(out_dir, "**", "*counter_collection.csv"), recursive=True)):
         for row in csv.DictReader(open(f)):
-            if "engine" in row.get("Kernel_Name", "") and row["Counter_Name"] == counter:
-                vals.append(float(row["Counter_Value"]))
-    if not vals:
+            if "engine" in row.get("Kernel_Name", "") and row["Counter_Name"] in vals:
+                vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+    if not all(vals.values()):
         raise SystemExit(f"no engine dispatch in pass {counter}")
-    return vals
+    return vals[names[0]] if len(names) == 1 else vals
+
+
+ISSUE_PASSES = ("SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY",
+                "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR")
+
+
+def issue_entry(argv, base: str, n_decisions: int) -> dict:
+    """What bounds the engine instead of HBM: wave-instructions per decision and the fraction of wave cycles that
+    issue an instruction (SQ counters of the measured dispatch, two passes)."""
+    v = {}
+    for i, counters in enumerate(ISSUE_PASSES):
+        for k, x in run_pass(counters, argv, os.path.join(base, f"sq{i}")).items():
+            v[k] = x[-1]
+    insts = sum(v[k] for k in v if k.startswith("SQ_INSTS_"))
+    return {"wave_insts_per_decision": insts / n_decisions,
+            "valu_per_decision": v["SQ_INSTS_VALU"] / n_decisions,
+            "lds_per_decision": v["SQ_INSTS_LDS"] / n_decisions,
+            "issue_frac": v["SQ_ACTIVE_INST_ANY"] / v["SQ_WAVE_CYCLES"],
+            "parked_frac": v["SQ_WAIT_ANY"] / v["SQ_WAVE_CYCLES"],
+            "waves": v["SQ_WAVES"], "counters": v,
+            "source": "rocprofv3 --pmc SQ passes (tools/pmc_traffic.py): SQ_INSTS_* / decisions, "
+                      "SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES"}
 
 
 def main():
@@ -56,7 +81,8 @@ def main():
     entry = {"lib_sha": bench.lib_sha(), "bytes": int((2 * f_kib + w_kib) * 1024),
              "fetch_kib": f_kib, "write_kib": w_kib, "dispatches": [fetch, write],
              "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.py): 2 x FETCH + WRITE",
-             "algorithmic_bytes": bench.algorithmic_bytes(w)}
+             "algorithmic_bytes": bench.algorithmic_bytes(w),
+             "issue": issue_entry(argv, base, len(w.stream.act))}
     try:
         d = json.load(open(bench.PMC_FILE))
     except (OSError, ValueError):
