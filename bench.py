@@ -199,7 +199,8 @@ def cpu_baseline(args, w0, n_ctl, shard0):
     return out
 
 
-def shim_path(w, o_inv, dev_index, drains=(64, 512, 4096), budget_jobs=(120_000, 480_000, None)):
+def shim_path(w, o_inv, dev_index, drains=(64, 512, 4096), budget_jobs=(120_000, 480_000, None),
+              modes=("calls", "fused")):
     """The path the JVM shim drives (integration/GpuShardingContainerPoolBalancer.scala): the shard's stream as the
     batching thread's queue -- per batch its completions, then its publishes -- drained `drain` jobs at a time.  Each
     drained batch splits into runs of releases followed by publishes; "calls" issues one owgs_release_batch per release
@@ -232,7 +233,7 @@ def shim_path(w, o_inv, dev_index, drains=(64, 512, 4096), budget_jobs=(120_000,
     legs = []
     for drain, budget in zip(drains, budget_jobs):
         n_jobs = len(ids) if budget is None else min(budget, len(ids))
-        for mode in ("calls", "fused"):
+        for mode in modes:
             b.restore()
             rs0 = b.resident_stats()
             inv = np.full(len(act), -9, np.int32)
@@ -301,7 +302,7 @@ def shim_path(w, o_inv, dev_index, drains=(64, 512, 4096), budget_jobs=(120_000,
                          "p50_us": float(np.percentile(lat_us, 50)), "p99_us": float(np.percentile(lat_us, 99)),
                          "decisions_per_s": n_pub / max(float(np.sum(lat)), 1e-9), "bit_exact": exact,
                          # owgs_process_batch's paths in this leg: resident engine calls / launches, launch-chain calls
-                         "resident": {k: rs1[k] - rs0[k] for k in ("served", "launches", "refused", "chained")}})
+                         "resident": {k: rs1[k] - rs0[k] for k in rs1 if k != "alive"}})
     b.close()
     return {"path": "host buffers through the C ABI as the JNI shim calls it (queue order: each batch's completions, "
                     "then its publishes); calls = owgs_release_batch + owgs_publish_batch per run, fused = "

@@ -346,7 +346,10 @@ int owgs_engine_ms(owgs_ctx* ctx, float* ms);
 
 /* Counters of owgs_process_batch's two paths: out[0] calls the resident engine served, [1] its launches, [2] calls it
  * refused untouched (a release that could leave the on-chip permit range; the chain took them), [3] calls the launch
- * chain took, [4] 1 while a resident engine is live.  Returns the number of counters (5). */
+ * chain took, [4] 1 while a resident engine is live; then, summed over the served calls: [5] walk rounds, [6]
+ * decisions, [7] staging cycles, [8] release cycles, [9] publish cycles, [10] overflow lookups, [11] walks that
+ * started at a cursor, [12] walks skipped by the pool permit bound, [13] decisions of grouped walks.  Returns the
+ * number of counters (14). */
 int owgs_resident_stats(owgs_ctx* ctx, int64_t* out, int32_t cap);
 
 /* Restore the slot state captured by owgs_snapshot (bench: every timed step starts from the same state). */

@@ -227,11 +227,13 @@ class GpuShardingContainerPoolBalancer:
     def resident_stats(self) -> dict:
         """owgs_process_batch's paths: calls the resident engine served, its launches, calls it refused untouched,
         calls the launch chain took, and whether a resident engine is live."""
-        out = np.zeros(5, np.int64)
-        n = self._L.owgs_resident_stats(self._h, _p(out), 5)
+        out = np.zeros(14, np.int64)
+        n = self._L.owgs_resident_stats(self._h, _p(out), 14)
         if n < 0:
             self._chk(n)
-        return dict(zip(("served", "launches", "refused", "chained", "alive"), (int(x) for x in out)))
+        return dict(zip(("served", "launches", "refused", "chained", "alive", "walk_rounds", "decisions",
+                         "stage_cycles", "release_cycles", "publish_cycles", "overflow_lookups", "cursor_walks",
+                         "bound_skips", "grouped_decisions"), (int(x) for x in out)))
 
     def set_health_tid(self, start_ms: int):
         """TransactionId.invokerHealth's start time (TransactionId.scala:225): health acks echo it."""

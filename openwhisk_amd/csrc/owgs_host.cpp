@@ -309,6 +309,10 @@ struct owgs_ctx {
     bool res_alive = false;
     int32_t res_stage = 0;
     int64_t res_n_calls = 0, res_n_launches = 0, res_n_bails = 0, res_n_chained = 0;
+    int64_t res_prof[OWGS_RES_NPROF] = {};
+    DevBuf<uint2> d_res_cur;        // per action: {cursor generation, first walk step that may fit}
+    std::vector<uint2> res_meta;    // act_meta as of the live launch (every change of it stops the engine first)
+    uint32_t res_gen_seen = 0;      // the last cursor generation the engine reported
     DevBuf<unsigned long long> f_bound;  // per slot: what a fused call's releases can return (zero between calls)
     DevBuf<uint32_t> s_w_keys, s_w_vals;
     DevBuf<int32_t> s_w_wkey;
@@ -937,8 +941,9 @@ static bool res_eligible(const owgs_ctx* c, int32_t n_runs, int32_t NR, int32_t 
         c->nb > (int32_t)OWGS_AM_POS_MASK || c->a_mem.empty())
         return false;
     const size_t runs = ((size_t)n_runs + 4) & ~(size_t)3;
-    const size_t need = 8 * runs + 16 * (size_t)NR + 16 * (size_t)NP + (has_seq ? 8 * (size_t)NP : 0);
-    if (need > res_stage_bytes(c)) return false;
+    const size_t in_b = 8 * runs + 16 * (size_t)NR + 16 * (size_t)NP + (has_seq ? 8 * (size_t)NP : 0);
+    const size_t need = in_b + 8 * (size_t)NP + 16 + 5 * (size_t)NP + (size_t)NR + 32;  // + cursors, outputs
+    if (need > res_stage_bytes(c) || res_stage_bytes(c) < 4096) return false;
     // a map that may outgrow its overflow table during the call: the chained path grows it
     if (c->any_conc && c->res_alive && c->ovf_cap < ovf_need(c->ovf_used_ub, NP)) return false;
     return true;
@@ -956,6 +961,20 @@ static int res_launch(owgs_ctx* c) {
         if (rc) return rc;
     }
     HIPCHK(c, c->d_ct_tmp.reserve((size_t)2 * OWGS_CTC));
+    {  // walk cursors: a new buffer starts at generation 0, below every generation a launch uses
+        const size_t na = std::max<size_t>(c->a_mem.size(), 1);
+        if (c->d_res_cur.n < na) {
+            HIPCHK(c, c->d_res_cur.reserve(na + na / 2));
+            HIPCHK(c, hipMemsetAsync(c->d_res_cur.p, 0, c->d_res_cur.n * sizeof(uint2), c->stream));
+        }
+    }
+    // the action meta the host writes into each call's records (as the device computed it)
+    c->res_meta.resize(c->a_mem.size());
+    if (!c->res_meta.empty()) {
+        HIPCHK(c, hipMemcpyAsync(c->res_meta.data(), c->d_act_meta.p, c->res_meta.size() * sizeof(uint2),
+                                 hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
     // the state in HBM must be current: the resident stream waits for the context's stream and its last async call
     HIPCHK(c, hipEventRecord(c->ev_res, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->res_stream, c->ev_res, 0));
@@ -981,6 +1000,8 @@ static int res_launch(owgs_ctx* c) {
     a.out = c->res_out;
     a.stage_bytes = (int32_t)res_stage_bytes(c);
     a.last_call = c->res_call;
+    a.cur = c->d_res_cur.p;
+    a.gen_base = ++c->res_gen_seen;  // above every generation stored by earlier launches
     a.idle_ticks = env_opts().res_idle_us * 100;  // s_memrealtime: 100 MHz
     volatile int32_t* ctl = c->res_ctl;
     ctl[OWGS_RES_STATE] = 0;
@@ -999,16 +1020,17 @@ static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
                        const uint64_t* seq, uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, int* served) {
     *served = 0;
     const int32_t NR = rel_off[n_runs], NP = pub_off[n_runs];
-    // inputs (int32 words): rel_off, pub_off, rel_inv, rel_act, pub_act, seq (u64 at an even word); outputs (bytes):
-    // out_inv, out_flags, rel_flags
-    const size_t i_roff = 0, i_poff = (size_t)n_runs + 1, i_rinv = 2 * ((size_t)n_runs + 1), i_ract = i_rinv + NR;
-    const size_t i_pact = i_ract + NR, i_seq = (i_pact + NP + 1) & ~(size_t)1;
-    const size_t in_bytes = 4 * (i_seq + (seq ? 2 * (size_t)NP : 0));
-    const size_t o_inv = 0, o_fl = 4 * (size_t)NP, o_rfl = o_fl + NP, out_bytes = o_rfl + NR + 16;
-    if (in_bytes > c->res_in_cap || out_bytes > c->res_out_cap) {  // the engine holds the buffers' addresses
-        const int q = res_quiesce(c);
+    // the call's input block (16-byte aligned parts): rel_off | pub_off | release records | publish records | seq;
+    // records are complete (action meta and slot key), so the engine's staging is a copy
+    auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    const size_t b_poff = al(4 * ((size_t)n_runs + 1)), b_rel = b_poff + al(4 * ((size_t)n_runs + 1));
+    const size_t b_pub = b_rel + 16 * (size_t)NR, b_seq = b_pub + 16 * (size_t)NP;
+    const size_t in_bytes = al(b_seq + (seq ? 8 * (size_t)NP : 0));
+    const size_t o_fl = 4 * (size_t)NP, o_rfl = o_fl + NP, out_bytes = al(o_rfl + NR) + 16;
+    if (std::max<size_t>(in_bytes, 4096) > c->res_in_cap || out_bytes > c->res_out_cap) {  // (the engine holds the
+        const int q = res_quiesce(c);                                                        // buffers' addresses)
         if (q) return q;
-        if (in_bytes > c->res_in_cap) {
+        if (std::max<size_t>(in_bytes, 4096) > c->res_in_cap) {
             if (c->res_in) (void)hipHostFree(c->res_in);
             c->res_in = nullptr;
             c->res_in_cap = 0;
@@ -1029,20 +1051,33 @@ static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
         const int rc = res_launch(c);
         if (rc) return rc;
     }
-    int32_t* I = c->res_in;
-    memcpy(I + i_roff, rel_off, 4 * ((size_t)n_runs + 1));
-    memcpy(I + i_poff, pub_off, 4 * ((size_t)n_runs + 1));
-    if (NR) {
-        memcpy(I + i_rinv, rel_invoker, 4 * (size_t)NR);
-        memcpy(I + i_ract, rel_action, 4 * (size_t)NR);
+    char* B = (char*)c->res_in;
+    memcpy(B, rel_off, 4 * ((size_t)n_runs + 1));
+    memcpy(B + b_poff, pub_off, 4 * ((size_t)n_runs + 1));
+    uint64_t rsum = 0;
+    uint32_t* R = (uint32_t*)(B + b_rel);
+    for (int32_t j = 0; j < NR; ++j) {
+        const int32_t a = rel_action[j], inv = rel_invoker[j];
+        R[4 * j] = (uint32_t)inv;
+        R[4 * j + 1] = c->res_meta[a].y;
+        R[4 * j + 2] = (uint32_t)c->a_slot[a];
+        R[4 * j + 3] = 0u;
+        if (inv >= 0 && inv < c->n_slots) rsum += (uint64_t)c->a_mem[a];
     }
-    if (NP) memcpy(I + i_pact, pub_action, 4 * (size_t)NP);
-    if (seq && NP) memcpy(I + i_seq, seq, 8 * (size_t)NP);
+    uint32_t* Q = (uint32_t*)(B + b_pub);
+    for (int32_t i = 0; i < NP; ++i) {
+        const int32_t a = pub_action[i];
+        Q[4 * i] = c->res_meta[a].x;
+        Q[4 * i + 1] = c->res_meta[a].y;
+        Q[4 * i + 2] = (uint32_t)c->a_slot[a];
+        Q[4 * i + 3] = (uint32_t)a;
+    }
+    if (seq && NP) memcpy(B + b_seq, seq, 8 * (size_t)NP);
     volatile int32_t* H = c->res_ctl + OWGS_RES_HDR;
-    const int32_t hdr[15] = {n_runs, NR, NP, seq ? 1 : 0, (int32_t)(uint32_t)seq_base, (int32_t)(uint32_t)(seq_base >> 32),
-                             (int32_t)i_roff, (int32_t)i_poff, (int32_t)i_rinv, (int32_t)i_ract, (int32_t)i_pact,
-                             (int32_t)i_seq, (int32_t)o_inv, (int32_t)o_fl, (int32_t)o_rfl};
-    for (int k = 0; k < 15; ++k) H[k] = hdr[k];
+    const int32_t hdr[13] = {n_runs, NR, NP, seq ? 1 : 0, (int32_t)(uint32_t)seq_base, (int32_t)(uint32_t)(seq_base >> 32),
+                             (int32_t)b_poff, (int32_t)b_rel, (int32_t)b_pub, (int32_t)b_seq, (int32_t)in_bytes,
+                             (int32_t)(uint32_t)rsum, (int32_t)(uint32_t)(rsum >> 32)};
+    for (int k = 0; k < 13; ++k) H[k] = hdr[k];
     for (int attempt = 0;; ++attempt) {
         const int32_t k = ++c->res_call;
         __atomic_store_n(&c->res_ctl[OWGS_RES_BELL], k, __ATOMIC_RELEASE);
@@ -1076,9 +1111,11 @@ static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
         return OWGS_OK;  // nothing applied: the chained path takes the call
     }
     ++c->res_n_calls;
+    c->res_gen_seen = (uint32_t)__atomic_load_n(&c->res_ctl[OWGS_RES_GEN], __ATOMIC_ACQUIRE);
+    for (int k = 0; k < OWGS_RES_NPROF; ++k) c->res_prof[k] += (uint32_t)c->res_ctl[OWGS_RES_PROF + k];
     if (c->any_conc) ovf_add(c, NP);
     if (NP) {
-        memcpy(out_invoker, c->res_out + o_inv, 4 * (size_t)NP);
+        memcpy(out_invoker, c->res_out, 4 * (size_t)NP);
         memcpy(out_flags, c->res_out + o_fl, (size_t)NP);
     }
     if (NR && rel_flags) memcpy(rel_flags, c->res_out + o_rfl, (size_t)NR);
@@ -1185,6 +1222,7 @@ void owgs_destroy(owgs_ctx* c) {
     if (c->res_out) (void)hipHostFree(c->res_out);
     c->res_ctl = c->res_in = nullptr;
     c->res_out = nullptr;
+    c->d_res_cur.release();
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf<int32_t>* i32s[] = {&c->d_permits, &c->d_pool_words, &c->d_hlist, &c->d_act_slot, &c->d_act_hash,
                                &c->d_act_mem,  &c->d_act_maxc,   &c->d_steps,  &c->d_cpx,     &c->d_err,
@@ -3216,7 +3254,8 @@ int owgs_resident_stats(owgs_ctx* c, int64_t* out, int32_t cap) {
     if (!c || cap < 0 || (cap > 0 && !out)) return OWGS_EINVAL;
     const int64_t v[5] = {c->res_n_calls, c->res_n_launches, c->res_n_bails, c->res_n_chained, c->res_alive ? 1 : 0};
     for (int32_t i = 0; i < cap && i < 5; ++i) out[i] = v[i];
-    return 5;
+    for (int32_t i = 5; i < cap && i < 5 + OWGS_RES_NPROF; ++i) out[i] = c->res_prof[i - 5];
+    return 5 + OWGS_RES_NPROF;
 }
 
 int owgs_engine_ms(owgs_ctx* c, float* ms) {

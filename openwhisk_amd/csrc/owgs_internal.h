@@ -310,9 +310,18 @@ struct OwgsReleaseArgs {
 #define OWGS_RES_STATE 32   // device: 1 = image loaded, 2 = written back and exiting
 #define OWGS_RES_RESULT 48  // device: the last call's outcome (0, OWGS_RES_BAIL_*) | its device error bits << 8
 #define OWGS_RES_USED 49    // device: primary-table entries (live + deleted) after the last call
-#define OWGS_RES_HDR 64     // host: the call -- n_runs, n_rel, n_pub, has_seq, seq_base lo, hi, then int32 indices
-                            // into `in` of rel_off, pub_off, rel_inv, rel_act, pub_act, seq (u64, even index), and
-                            // byte offsets into `out` of out_inv (i32), out_flags (u8), rel_flags (u8)
+#define OWGS_RES_GEN 50     // device: the walk-cursor generation reached (the host's next launch starts past it)
+#define OWGS_RES_PROF 96    // device: the last call's counters (OWGS_RES_NPROF words: walk rounds, decisions,
+                            // staging / release / publish cycles, overflow lookups, cursor hits, U shortcuts,
+                            // decisions of the grouped walks)
+#define OWGS_RES_NPROF 9
+#define OWGS_RES_HDR 64     // host: the call -- n_runs, n_rel, n_pub, has_seq, seq_base lo, hi, then byte offsets in
+                            // the input block of pub_off, the release records, the publish records, seq (u64), the
+                            // block's length, and the memory the releases return at most (lo, hi).  The block:
+                            // rel_off i32[n_runs + 1] | pub_off | releases uint4 {invoker, meta.y, slot, -} |
+                            // publishes uint4 {meta.x, meta.y, slot, action} | seq u64[n_pub], 16-byte aligned parts.
+                            // Outputs (block `out`): out_inv i32[n_pub] | out_flags u8[n_pub] | rel_flags u8[n_rel]
+#define OWGS_RES_NHDR 16
 #define OWGS_RES_CTL_WORDS 128
 #define OWGS_RES_BAIL_RELRISK 1  // a release could leave the LDS permit range: nothing applied, the host reruns the
                                  // call through the ordered release kernels
@@ -336,6 +345,8 @@ struct OwgsResArgs {
     char* out;                   // pinned outputs of a call
     int32_t stage_bytes;         // LDS bytes for a call's staged inputs
     int32_t last_call;           // the bell's value at launch
+    uint2* cur;                  // [n_actions] walk cursor of each action: {generation, first walk step that may fit}
+    uint32_t gen_base;           // first cursor generation of this launch (above every generation stored in cur)
     long long idle_ticks;        // s_memrealtime ticks (100 MHz) without a call before the engine writes back and exits
 };
 

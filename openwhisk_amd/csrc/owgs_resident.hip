@@ -55,6 +55,11 @@ __device__ __forceinline__ int mod_fast(int x, int n, float rn) {
     r -= r >= n ? n : 0;
     return r;
 }
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d, 64));
+    return v;
+}
 // position of the need-th set bit of m (need < popc(m))
 __device__ __forceinline__ int select_in_word(uint32_t m, int need) {
     int pos = 0;
@@ -69,8 +74,9 @@ __device__ __forceinline__ int select_in_word(uint32_t m, int need) {
     return pos;
 }
 
+#define RES_CC 2048  // walk-cursor cache entries (LDS, 16 KB)
 struct ResLayout {
-    uint32_t P, ub, pc, ct, sc, stage, end;
+    uint32_t P, ub, pc, ct, sc, cc, stage, end;
 };
 __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
     const uint32_t words = (uint32_t)(n_ids + 31) / 32;
@@ -80,7 +86,8 @@ __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
     y.pc = y.ub + ((words + 4u) & ~3u) * 4u;
     y.ct = y.pc + ((words + 2u + 3u) & ~3u) * 4u;
     y.sc = y.ct + OWGS_CTC * 8u;
-    y.stage = y.sc + 64u * 4u;
+    y.cc = y.sc + 64u * 4u;
+    y.stage = y.cc + RES_CC * 8u;
     y.end = y.stage;
     return y;
 }
@@ -93,7 +100,11 @@ __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
 #define RS_ERR 4
 #define RS_LIVE 5    // cleanup: live primary entries
 #define RS_BAIL 6
+#define RS_GEN 7     // walk-cursor generation: counts release runs (permits rise only there)
 #define RS_RSUM 8    // (u64, 8-aligned) memory the call's releases return at most
+#define RS_U0 10     // upper bound of every usable permit count of the managed / blackbox pool
+#define RS_U1 11
+#define RS_TOMB 12   // deleted primary entries (the cleanup between calls runs when they pile up)
 
 // primary table (LDS, interleaved {key, value}): index of key or -1, *val (0 if absent); chains end at an empty entry
 __device__ __forceinline__ int ct_lookup(const uint2* ct, uint32_t key, uint32_t* val) {
@@ -134,30 +145,38 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
     uint32_t* pc = (uint32_t*)(Lb + Y.pc);
     uint2* ct = (uint2*)(Lb + Y.ct);
     int32_t* sc = (int32_t*)(Lb + Y.sc);
+    uint2* cc = (uint2*)(Lb + Y.cc);
     char* stg = Lb + Y.stage;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int n_slots = A.n_slots, nm = A.nm, nb = A.nb;
     const int words = (A.n_ids + 31) >> 5;
 
     // ------------------------------------------------------------------ state -> LDS (once per launch)
-    if (tid < 16) sc[tid] = 0;
+    if (tid < 16) sc[tid] = (tid == RS_U0 || tid == RS_U1) ? (int)0x80000000 : (tid == RS_GEN ? (int)A.gen_base : 0);
+    for (int i = tid; i < RES_CC; i += 256) cc[i] = make_uint2(0u, 0u);
     __syncthreads();
     {
-        int used = 0, mx = (int)0x80000000, e = 0;
+        int used = 0, tombs = 0, mx = (int)0x80000000, u0 = (int)0x80000000, u1 = (int)0x80000000, e = 0;
         for (int i = tid; i < n_slots; i += 256) {
             const int v = A.permits[i];
             const bool unusable = !(i < A.n_ids && ((A.usable[i >> 5] >> (i & 31)) & 1u));
             if (v < -OWGS_PLIM || v >= OWGS_PLIM) e |= OWGS_ERR_PERMITS;
             P[i] = unusable ? v + OWGS_PENC : v;
             mx = max(mx, v);
+            if (!unusable && i < nm) u0 = max(u0, v);
+            if (!unusable && i >= A.n_ids - nb && i < A.n_ids) u1 = max(u1, v);
         }
+        atomicMax(&sc[RS_U0], u0);
+        atomicMax(&sc[RS_U1], u1);
         for (int i = tid; i <= words; i += 256) ub[i] = i < words ? A.usable[i] : 0u;
         for (int i = tid; i < OWGS_CTC; i += 256) {
             const uint32_t k = A.ct_keys[i];
             ct[i] = make_uint2(k, A.ct_vals[i]);
             used += k != 0u;
+            tombs += k == OWGS_CT_TOMB;
         }
         if (used) atomicAdd(&sc[RS_USED], used);
+        if (tombs) atomicAdd(&sc[RS_TOMB], tombs);
         atomicMax(&sc[RS_MAXP], mx);
         if (e) atomicOr(&sc[RS_ERR], e);
         if (tid == 0 && A.ovf.cap > 0)
@@ -226,73 +245,67 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
         const int k = sc[RS_K];
         if (k < 0) break;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the host's inputs, written before the bell
-        const int32_t* H = A.ctl + OWGS_RES_HDR;
-        const int n_runs = ld_sys(H + 0), NR = ld_sys(H + 1), NP = ld_sys(H + 2), has_seq = ld_sys(H + 3);
-        const u64 seq_base = (u64)(uint32_t)ld_sys(H + 4) | ((u64)(uint32_t)ld_sys(H + 5) << 32);
-        const int i_roff = ld_sys(H + 6), i_poff = ld_sys(H + 7), i_rinv = ld_sys(H + 8), i_ract = ld_sys(H + 9),
-                  i_pact = ld_sys(H + 10), i_seq = ld_sys(H + 11);
-        const int o_inv = ld_sys(H + 12), o_fl = ld_sys(H + 13), o_rfl = ld_sys(H + 14);
-        // staging: run offsets, releases {inv, meta.y, slot, -}, publishes {meta.x, meta.y, slot, -}, sequence numbers
-        const uint32_t s_roff = 0, s_poff = s_roff + (((uint32_t)n_runs + 4u) & ~3u) * 4u;
-        const uint32_t s_rel = s_poff + (((uint32_t)n_runs + 4u) & ~3u) * 4u;
-        const uint32_t s_pub = s_rel + (uint32_t)NR * 16u, s_seq = s_pub + (uint32_t)NP * 16u;
-        const uint32_t s_end = s_seq + (has_seq ? (uint32_t)NP * 8u : 0u);
-        if (tid == 0) {
-            sc[RS_BAIL] = s_end > (uint32_t)A.stage_bytes ? OWGS_RES_BAIL_STAGE : 0;
-            *(u64*)&sc[RS_RSUM] = 0ull;
+        const u64 t_call = clock64();
+        // ---- the call: its header (control block) and its input block (pinned host memory) into LDS.  The host
+        // wrote the records complete (action meta and slot key per publish and release), so staging is a copy: the
+        // header and the first 4 KB of the block are read together (one PCIe round trip for a small call)
+        int32_t* hdr = sc + 32;  // RS_HDR words
+        if (tid < OWGS_RES_NHDR) hdr[tid] = ld_sys(A.ctl + OWGS_RES_HDR + tid);
+        {
+            const uint4 v = ((const uint4*)A.in)[tid];  // (the block holds >= 4 KB: its capacity is larger)
+            ((uint4*)stg)[tid] = v;
         }
         __syncthreads();
-        int32_t* roff = (int32_t*)(stg + s_roff);
+        const int n_runs = hdr[0], NR = hdr[1], NP = hdr[2], has_seq = hdr[3];
+        const u64 seq_base = (u64)(uint32_t)hdr[4] | ((u64)(uint32_t)hdr[5] << 32);
+        const uint32_t s_poff = (uint32_t)hdr[6], s_rel = (uint32_t)hdr[7], s_pub = (uint32_t)hdr[8],
+                       s_seq = (uint32_t)hdr[9], s_in = (uint32_t)hdr[10];
+        const u64 rsum = (u64)(uint32_t)hdr[11] | ((u64)(uint32_t)hdr[12] << 32);  // memory the releases return at most
+        // LDS after the input block: each publish's walk cursor {generation, step}, then the outputs (mirrored by the
+        // host's output block): out_inv i32[NP], out_flags u8[NP], rel_flags u8[NR]
+        const uint32_t s_cur = (s_in + 15u) & ~15u, s_out = (s_cur + 8u * (uint32_t)NP + 15u) & ~15u;
+        const uint32_t s_ofl = s_out + 4u * (uint32_t)NP, s_orf = s_ofl + (uint32_t)NP;
+        const uint32_t s_end = (s_orf + (uint32_t)NR + 15u) & ~15u;
+        if (tid == 0) sc[RS_BAIL] = s_end > (uint32_t)A.stage_bytes ? OWGS_RES_BAIL_STAGE : 0;
+        __syncthreads();
+        int32_t* roff = (int32_t*)(stg);
         int32_t* poff = (int32_t*)(stg + s_poff);
         uint4* rel = (uint4*)(stg + s_rel);
         uint4* pub = (uint4*)(stg + s_pub);
         u64* sq = (u64*)(stg + s_seq);
+        uint2* pcur = (uint2*)(stg + s_cur);
         if (sc[RS_BAIL] == 0) {
-            for (int r = tid; r <= n_runs; r += 256) {
-                roff[r] = ld_sys(A.in + i_roff + r);
-                poff[r] = ld_sys(A.in + i_poff + r);
-            }
-            u64 rsum = 0;
-            int e = 0;
-            // one pass over both lists: every host-memory read of an iteration is in flight together (PCIe latency),
-            // then the action meta gathers (HBM, L2-resident)
-            for (int x = tid; x < max(NR, NP); x += 256) {
-                const bool hr = x < NR, hp = x < NP;
-                const int inv = hr ? ld_sys(A.in + i_rinv + x) : -1, ar = hr ? ld_sys(A.in + i_ract + x) : 0;
-                const int ap = hp ? ld_sys(A.in + i_pact + x) : 0;
-                uint32_t s_lo = 0u, s_hi = 0u;
-                if (hp && has_seq) {
-                    s_lo = (uint32_t)ld_sys(A.in + i_seq + 2 * x);
-                    s_hi = (uint32_t)ld_sys(A.in + i_seq + 2 * x + 1);
+            // the rest of a block beyond 4 KB, four 16-byte reads in flight per thread
+            for (uint32_t o = 4096u + 16u * tid; o < s_in; o += 4u * 16u * 256u) {
+                uint4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t ou = o + (uint32_t)u * 16u * 256u;
+                    v[u] = ou < s_in ? ((const uint4*)A.in)[ou / 16u] : make_uint4(0u, 0u, 0u, 0u);
                 }
-                const bool okr = ar >= 0 && ar < A.n_actions, okp = ap >= 0 && ap < A.n_actions;
-                if ((hr && !okr) || (hp && !okp)) e |= OWGS_ERR_BAD_STREAM;
-                const uint32_t my = (hr && okr) ? A.act_meta[ar].y : 0u;
-                const uint32_t rs = (hr && okr) ? (uint32_t)A.act_slot[ar] : 0u;
-                const uint2 m = (hp && okp) ? A.act_meta[ap] : make_uint2(0u, OWGS_AM_EMPTY);
-                const uint32_t ps = (hp && okp) ? (uint32_t)A.act_slot[ap] : 0u;
-                if (hr) {
-                    rel[x] = make_uint4((uint32_t)inv, my, rs, 0u);
-                    if (inv >= 0 && inv < n_slots) rsum += my & OWGS_AM_MEM_MASK;
-                }
-                if (hp) {
-                    pub[x] = make_uint4(m.x, m.y, ps, 0u);
-                    if (has_seq) sq[x] = (u64)s_lo | ((u64)s_hi << 32);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t ou = o + (uint32_t)u * 16u * 256u;
+                    if (ou < s_in) ((uint4*)stg)[ou / 16u] = v[u];
                 }
             }
-            if (rsum) atomicAdd((u64*)&sc[RS_RSUM], rsum);
-            if (e) atomicOr(&sc[RS_ERR], e);
+            __syncthreads();
+            // every publish's walk cursor (one gather: the decision loop then waits on nothing in HBM)
+            for (int i = tid; i < NP; i += 256) {
+                const uint32_t a = pub[i].w;
+                pcur[i] = (A.cur && a < (uint32_t)A.n_actions) ? A.cur[a] : make_uint2(0u, 0u);
+            }
         }
         __syncthreads();
         // releases that could leave the LDS permit range: exact maximum first, then refuse the call untouched
-        if (sc[RS_BAIL] == 0 && (long long)sc[RS_MAXP] + (long long)*(u64*)&sc[RS_RSUM] >= (long long)OWGS_PLIM) {
+        if (sc[RS_BAIL] == 0 && (long long)sc[RS_MAXP] + (long long)rsum >= (long long)OWGS_PLIM) {
             if (tid == 0) sc[RS_MAXP] = (int)0x80000000;
             __syncthreads();
             int mx = (int)0x80000000;
             for (int i = tid; i < n_slots; i += 256) mx = max(mx, P[i] >= OWGS_PLIM ? P[i] - OWGS_PENC : P[i]);
             atomicMax(&sc[RS_MAXP], mx);
             __syncthreads();
-            if (tid == 0 && (long long)sc[RS_MAXP] + (long long)*(u64*)&sc[RS_RSUM] >= (long long)OWGS_PLIM)
+            if (tid == 0 && (long long)sc[RS_MAXP] + (long long)rsum >= (long long)OWGS_PLIM)
                 sc[RS_BAIL] = OWGS_RES_BAIL_RELRISK;
             __syncthreads();
         }
@@ -300,10 +313,18 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
         if (bail == 0 && wave == 0) {
             int err = 0;
             bool ovf_on = sc[RS_OVF] > 0;
-            int used = sc[RS_USED];
-            int32_t* out_inv = (int32_t*)(A.out + o_inv);
-            uint8_t* out_fl = (uint8_t*)(A.out + o_fl);
-            uint8_t* rel_fl = (uint8_t*)(A.out + o_rfl);
+            int used = sc[RS_USED], tombs = 0;  // (tombs: per lane, deleted entries made - reused this call)
+            // maxConcurrent == 1 walks: U = an upper bound of every usable permit count of the pool (a walk with
+            // mem > U fails everywhere: straight to the fallback), and per action the first walk step that may
+            // still fit (a cache keyed by action, valid while no release raised a permit: generation = release runs)
+            int U0 = sc[RS_U0], U1 = sc[RS_U1];
+            uint32_t gen = (uint32_t)sc[RS_GEN];
+            uint32_t pr_rounds = 0, pr_dec = 0, pr_ovf = 0, pr_hit = 0, pr_u = 0, pr_grp = 0;
+            const u64 pr_stage = clock64() - t_call;  // header, staging and the range check
+            u64 pr_rel = 0, pr_pub = 0;
+            int32_t* out_inv = (int32_t*)(stg + s_out);  // (LDS; copied to host memory after the call)
+            uint8_t* out_fl = (uint8_t*)(stg + s_ofl);
+            uint8_t* rel_fl = (uint8_t*)(stg + s_orf);
             // a new (invoker, fqn) entry (lane 0): the primary while it has room, else the overflow (the engine's rule)
             auto insert = [&](uint32_t key, uint32_t nv) -> int {
                 int ix = -1;
@@ -314,6 +335,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                         if (kk == 0u || kk == OWGS_CT_TOMB) {
                             ct[h] = make_uint2(key, nv);
                             used += kk == 0u;
+                            tombs -= kk == OWGS_CT_TOMB;
                             ix = (int)h;
                             break;
                         }
@@ -334,6 +356,8 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
             for (int r = 0; r < n_runs; ++r) {
                 // ---- completions of run r (releaseInvoker SCPB:327-331 via processCompletion CLB:260-346)
                 const int rb = roff[r], re = roff[r + 1];
+                if (re > rb) ++gen;  // permits may rise: every walk cursor of an earlier generation is stale
+                const u64 tr0 = clock64();
                 for (int j0 = rb; j0 < re; j0 += 64) {
                     const int j = j0 + lane;
                     const bool valid = j < re;
@@ -369,20 +393,158 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 const uint32_t nk = removed ? OWGS_CT_TOMB : key, nv = removed ? 0u : ct_val(c1, o1);
                                 if (ix < OWGS_CTC) ct[ix] = make_uint2(nk, nv);
                                 else ovf_st(A.ovf.t, ix - OWGS_CTC, nk, nv);
+                                tombs += removed && ix < OWGS_CTC;
                             }
                         }
                         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                     }
                     if (valid) rel_fl[j] = flag;
+                    // the pools' permit bounds follow what the releases raised
+                    const int pn = in ? P[inv] : (int)0x80000000;
+                    const int um = wave_max_i(pn < OWGS_PLIM ? pn : (int)0x80000000);
+                    U0 = max(U0, um);
+                    U1 = max(U1, um);
                 }
+                const u64 tr1 = clock64();
+                pr_rel += tr1 - tr0;
                 // ---- publishes of run r (SCPB:257-290 -> schedule SCPB:398-436)
                 const int pb = poff[r], pe = poff[r + 1];
+                const u64 tp0 = clock64();
                 for (int i0 = pb; i0 < pe; i0 += 64) {
                     const int nq = min(64, pe - i0);
                     const uint4 me = lane < nq ? pub[i0 + lane] : make_uint4(0u, OWGS_AM_EMPTY, 0u, 0u);
                     const u64 myseq = has_seq ? (lane < nq ? sq[i0 + lane] : 0ull) : seq_base + (u64)(i0 + lane);
+                    const uint2 mycur = lane < nq ? pcur[i0 + lane] : make_uint2(0u, 0u);  // (staged)
                     int o_v = OWGS_NONE_V, o_f = 0;
+                    // per lane (decision i0 + lane): the fields of a plain decision -- maxConcurrent == 1, a pool,
+                    // memory the pool's bound U does not exclude -- and where its walk may start (the HBM cursor
+                    // gathered at staging, the LDS cache; a stale cursor of the same generation is still a lower bound)
+                    const int l_mem = (int)(me.y & OWGS_AM_MEM_MASK);
+                    const int l_pool = (me.x & OWGS_AM_POOL) ? 1 : 0;
+                    const bool l_plain = lane < nq && !(me.y & (OWGS_AM_EMPTY | OWGS_AM_THROW)) &&
+                                         ((me.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK) <= 1u &&
+                                         l_mem <= (l_pool ? U1 : U0);
+                    int l_sbeg = 0;
+                    {
+                        const uint32_t lch = (me.w * 2654435761u) >> (32 - 10);
+                        const uint2 lce = cc[lch];
+                        const int lcs = (int)cc[lch + RES_CC / 2].x;
+                        if (mycur.x == gen) l_sbeg = (int)mycur.y;
+                        if (lce.x == me.w + 1u && lce.y == gen) l_sbeg = max(l_sbeg, lcs);
+                    }
                     for (int q = 0; q < nq; ++q) {
+                        // ---- up to 4 consecutive plain decisions walk together, 16 lanes each (4 probes per lane:
+                        // 64 walk steps per round), against the state before all of them; then in stream order each
+                        // is exact unless an earlier one of the group took the room at its target (permits only fall
+                        // inside a run, so every step a walk passed is still full).  The first one that is not exact,
+                        // and every fallback, goes to the single-decision path below.
+                        const u64 npm = ~(__ballot(l_plain) >> q);
+                        const int g = npm ? min(__builtin_ctzll(npm), 4) : 4;
+                        if (g >= 2) {
+                            const int grp = lane >> 4, u = lane & 15;
+                            const bool gact = grp < g;
+                            const int dq = q + (gact ? grp : 0);
+                            const uint32_t gmx = (uint32_t)__shfl((int)me.x, dq, 64);
+                            const int gmem = __shfl(l_mem, dq, 64), gsb = __shfl(l_sbeg, dq, 64);
+                            const int ghome = (int)(gmx & OWGS_AM_POS_MASK), gstep = (int)((gmx >> 15) & OWGS_AM_POS_MASK);
+                            const int gpool = (gmx & OWGS_AM_POOL) ? 1 : 0;
+                            const int gn = gpool ? nb : nm, gbase = gpool ? A.n_ids - nb : 0;
+                            const float grn = __builtin_amdgcn_rcpf((float)gn);
+                            int gp = mod_fast(ghome + (gsb + u) * gstep, gn, grn);
+                            const int gadv = mod_fast(16 * gstep, gn, grn);
+                            int gs = gsb, gt = -1, gts = gn, gpv = 0;
+                            bool gdone = !gact || gs >= gn;
+                            while (__ballot(!gdone)) {
+                                ++pr_rounds;
+                                int pk[4], vk[4];
+                                int pp = gp;
+#pragma unroll
+                                for (int k = 0; k < 4; ++k) {
+                                    pk[k] = pp;
+                                    vk[k] = P[gbase + pp];
+                                    pp += gadv;
+                                    pp -= pp >= gn ? gn : 0;
+                                }
+                                u64 B[4];
+#pragma unroll
+                                for (int k = 0; k < 4; ++k)
+                                    B[k] = __ballot(!gdone & (gs + 16 * k + u < gn) & (vk[k] >= gmem) & (vk[k] < OWGS_PLIM));
+                                int kf = 4, L = 0, sp = pk[0], sv = vk[0];
+#pragma unroll
+                                for (int k = 3; k >= 0; --k) {  // this group's first hit in walk order (k, then lane)
+                                    const uint32_t m = (uint32_t)(B[k] >> (16 * grp)) & 0xFFFFu;
+                                    if (m) {
+                                        kf = k;
+                                        L = __builtin_ctz(m);
+                                        sp = pk[k];
+                                        sv = vk[k];
+                                    }
+                                }
+                                const int src = (grp << 4) + L;
+                                const int hp = __shfl(sp, src, 64), hv = __shfl(sv, src, 64);
+                                if (!gdone) {
+                                    if (kf < 4) {
+                                        gt = gbase + hp;
+                                        gpv = hv;
+                                        gts = gs + 16 * kf + L;
+                                        gdone = true;
+                                    } else {
+                                        gs += 64;
+                                        gp = pp;
+                                        gdone = gs >= gn;  // every pool position probed: the walk failed
+                                    }
+                                }
+                            }
+                            // in stream order: accept while exact
+                            int ge = 0, at0 = -1, at1 = -1, at2 = -1, am0 = 0, am1 = 0, am2 = 0;
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                if (k >= g || ge < k) break;
+                                const int tk = __builtin_amdgcn_readlane(gt, 16 * k);
+                                const int pvk = __builtin_amdgcn_readlane(gpv, 16 * k);
+                                const int tsk = __builtin_amdgcn_readlane(gts, 16 * k);
+                                const int memk = __builtin_amdgcn_readlane(l_mem, q + k);
+                                const int ak = __builtin_amdgcn_readlane((int)me.w, q + k);
+                                const int pk_ = (__builtin_amdgcn_readlane((int)me.x, q + k) & OWGS_AM_POOL) ? 1 : 0;
+                                const uint32_t chk = ((uint32_t)ak * 2654435761u) >> (32 - 10);
+                                if (tk < 0) {  // no room anywhere for memk (then, so now): cursor past the pool, U below memk
+                                    const int nk = pk_ ? nb : nm;
+                                    if (lane == 0) {
+                                        cc[chk] = make_uint2((uint32_t)ak + 1u, gen);
+                                        cc[chk + RES_CC / 2].x = (uint32_t)nk;
+                                    }
+                                    if (pk_) U1 = min(U1, memk - 1);
+                                    else U0 = min(U0, memk - 1);
+                                    break;
+                                }
+                                int room = pvk;
+                                if (k > 0 && at0 == tk) room -= am0;
+                                if (k > 1 && at1 == tk) room -= am1;
+                                if (k > 2 && at2 == tk) room -= am2;
+                                if (room < memk) break;  // an earlier decision of the group took it: decide again
+                                if (k == 0) { at0 = tk; am0 = memk; }
+                                if (k == 1) { at1 = tk; am1 = memk; }
+                                if (k == 2) { at2 = tk; am2 = memk; }
+                                if (lane == 0) {
+                                    atomicSub(&P[tk], memk);  // tryAcquire (FS:63-71)
+                                    cc[chk] = make_uint2((uint32_t)ak + 1u, gen);
+                                    cc[chk + RES_CC / 2].x = (uint32_t)tsk;
+                                    if (A.cur) A.cur[ak] = make_uint2(gen, (uint32_t)tsk);
+                                }
+                                if (lane == q + k) {
+                                    o_v = tk;
+                                    o_f = 0;
+                                }
+                                ++ge;
+                            }
+                            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                            if (ge > 0) {
+                                pr_dec += ge;
+                                pr_grp += ge;
+                                q += ge - 1;
+                                continue;
+                            }
+                        }
                         const uint32_t mx = (uint32_t)__builtin_amdgcn_readlane((int)me.x, q);
                         const uint32_t my = (uint32_t)__builtin_amdgcn_readlane((int)me.y, q);
                         const int slot = __builtin_amdgcn_readlane((int)me.z, q);
@@ -397,13 +559,61 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             const int mem = (int)(my & OWGS_AM_MEM_MASK);
                             const int maxc = (int)((my >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
                             const int n = pool ? nb : nm, base = pool ? A.n_ids - nb : 0;
+                            const int a = __builtin_amdgcn_readlane((int)me.w, q);
+                            const uint32_t ch = ((uint32_t)a * 2654435761u) >> (32 - 10);  // RES_CC / 2 = 2^10 entries
+                            int s_beg = 0;
+                            if (maxc <= 1) {
+                                const uint2 ce = cc[ch];
+                                const uint32_t hg = (uint32_t)__builtin_amdgcn_readlane((int)mycur.x, q);
+                                const int hs = __builtin_amdgcn_readlane((int)mycur.y, q);
+                                if (mem > (pool ? U1 : U0)) {
+                                    s_beg = n;  // no usable invoker has mem: every walk fails
+                                    ++pr_u;
+                                } else {
+                                    if (hg == gen) s_beg = hs;
+                                    if (ce.x == (uint32_t)a + 1u && ce.y == gen) s_beg = max(s_beg, (int)cc[ch + RES_CC / 2].x);
+                                    pr_hit += s_beg > 0;
+                                }
+                            }
                             const float rn = __builtin_amdgcn_rcpf((float)n);
-                            int p = mod_fast(home + lane * step, n, rn);
+                            int p = mod_fast(home + (s_beg + lane) * step, n, rn);
                             const int adv = mod_fast(64 * step, n, rn);
-                            int t = -1, tix = -1;
+                            int t = -1, tix = -1, tp = 0, ts = n;  // target, its map entry, its permits, its walk step
                             uint32_t tv = 0u;
-                            // every pool position once: probes n and n + 1 repeat the first two with the same state
-                            for (int s0 = 0; s0 < n; s0 += 64) {
+                            if (maxc <= 1) {
+                                // 4 probes per lane per round (256 walk steps): the 4 permit reads are in flight together
+                                for (int s0 = s_beg; s0 < n; s0 += 256) {
+                                    ++pr_rounds;
+                                    int pk[4], vk[4];
+                                    int pp = p;
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k) {
+                                        pk[k] = pp;
+                                        vk[k] = P[base + pp];
+                                        pp += adv;
+                                        pp -= pp >= n ? n : 0;
+                                    }
+                                    u64 mk[4];
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k)
+                                        mk[k] = __ballot(s0 + 64 * k + lane < n && vk[k] >= mem && vk[k] < OWGS_PLIM);
+                                    const int kf = mk[0] ? 0 : mk[1] ? 1 : mk[2] ? 2 : mk[3] ? 3 : 4;
+                                    if (kf < 4) {
+                                        const u64 m = kf == 0 ? mk[0] : kf == 1 ? mk[1] : kf == 2 ? mk[2] : mk[3];
+                                        const int L = ffs64(m);
+                                        const int pl = kf == 0 ? pk[0] : kf == 1 ? pk[1] : kf == 2 ? pk[2] : pk[3];
+                                        const int vl = kf == 0 ? vk[0] : kf == 1 ? vk[1] : kf == 2 ? vk[2] : vk[3];
+                                        t = base + __builtin_amdgcn_readlane(pl, L);
+                                        tp = __builtin_amdgcn_readlane(vl, L);
+                                        ts = s0 + 64 * kf + L;
+                                        break;
+                                    }
+                                    p = pp;
+                                }
+                            }
+                            // concurrent: every pool position once (probes n and n + 1 repeat the first two)
+                            for (int s0 = s_beg; maxc > 1 && s0 < n; s0 += 64) {
+                                ++pr_rounds;
                                 const bool valid = s0 + lane < n;
                                 const int id = base + p;
                                 const int pv = valid ? P[id] : OWGS_PENC;
@@ -415,7 +625,13 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 } else {
                                     ok = false;
                                     if (pv < OWGS_PLIM) {  // usable: a free slot of the key's container, or memory
-                                        ix = ct_lookup2(ct, A.ovf, ovf_on, ct_key(id, slot), &v);
+                                        const uint32_t key = ct_key(id, slot);
+                                        ix = ct_lookup(ct, key, &v);
+                                        if (ix < 0 && ovf_on) {  // (an HBM round trip: counted)
+                                            ++pr_ovf;
+                                            const int oj = ovf_find(A.ovf, key, &v);
+                                            ix = oj >= 0 ? OWGS_CTC + oj : -1;
+                                        }
                                         ok = (v & OWGS_CT_C_MASK) != 0u || pv >= mem;
                                     }
                                 }
@@ -423,12 +639,23 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 if (m) {
                                     const int L = ffs64(m);
                                     t = __builtin_amdgcn_readlane(id, L);
+                                    ts = s0 + L;
+                                    tp = __builtin_amdgcn_readlane(pv, L);
                                     tix = __builtin_amdgcn_readlane(ix, L);
                                     tv = (uint32_t)__builtin_amdgcn_readlane((int)v, L);
                                     break;
                                 }
                                 p += adv;
                                 p -= p >= n ? n : 0;
+                            }
+                            if (maxc <= 1 && lane == 0) {  // the walk's steps before ts had no room for mem
+                                cc[ch] = make_uint2((uint32_t)a + 1u, gen);
+                                cc[ch + RES_CC / 2].x = (uint32_t)ts;
+                                if (A.cur) A.cur[a] = make_uint2(gen, (uint32_t)ts);
+                            }
+                            if (maxc <= 1 && t < 0) {  // a failed walk: no usable permit count reaches mem
+                                if (pool) U1 = min(U1, mem - 1);
+                                else U0 = min(U0, mem - 1);
                             }
                             if (t < 0) {  // overload: a random healthy invoker, forced (SCPB:417-424)
                                 const int Hn = pool ? hb_e : hm_e;
@@ -437,21 +664,29 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                                     ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(myseq >> 32), q) << 32);
                                     const int kk = (int)rng_index(A.rng_seed, sqv, (uint32_t)Hn);
                                     t = (pool ? full_b : full_m) ? base + kk : select_usable(base, kk);
-                                    if (t < 0) err |= OWGS_ERR_INTERNAL;
-                                    else if (maxc > 1) tix = ct_lookup2(ct, A.ovf, ovf_on, ct_key(t, slot), &tv);
+                                    if (t < 0) {
+                                        err |= OWGS_ERR_INTERNAL;
+                                    } else {
+                                        tp = P[t];
+                                        if (maxc > 1) tix = ct_lookup2(ct, A.ovf, ovf_on, ct_key(t, slot), &tv);
+                                    }
                                     fl = 1;
                                 }
                             }
                             x = t;
                             if (t >= 0 && lane == 0) {
                                 // tryAcquireConcurrent / forceAcquireConcurrent at t (NS:32-91, FS:63-110)
+                                // (permit takes are LDS atomics without a return: the next decision's reads of the
+                                // same wave come after them, and nothing waits for a value)
+                                bool took = true;
                                 if (maxc <= 1) {
-                                    P[t] -= mem;
+                                    atomicSub(&P[t], mem);
                                 } else {
                                     const int c0 = tix >= 0 ? (int)(tv & OWGS_CT_C_MASK) : 0;
                                     const int o0 = tix >= 0 ? ct_ops(tv) : 0;
                                     const bool slot_free = c0 >= 1;  // RS.tryAcquire(1) (NS:63)
-                                    if (!slot_free) P[t] -= mem;     // a new container: its memory (NS:70-79)
+                                    took = !slot_free;
+                                    if (took) atomicSub(&P[t], mem);  // a new container: its memory (NS:70-79)
                                     const int c1 = slot_free ? c0 - 1 : maxc - 1;
                                     const int o1 = o0 + 1;
                                     if (o1 > OWGS_MAX_OPS) err |= OWGS_ERR_OPS;
@@ -460,8 +695,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                     else if (tix < OWGS_CTC) ct[tix].y = nv;
                                     else ovf_st_val(A.ovf.t, tix - OWGS_CTC, nv);
                                 }
-                                const int pt = P[t] >= OWGS_PLIM ? P[t] - OWGS_PENC : P[t];
-                                if (pt < -OWGS_PLIM) err |= OWGS_ERR_PERMITS;
+                                if (took && tp - mem < -OWGS_PLIM) err |= OWGS_ERR_PERMITS;
                             }
                             // lane 0's table updates (used, overflow in use) for every lane's next lookups
                             used = __builtin_amdgcn_readfirstlane(used);
@@ -472,34 +706,48 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             o_v = x;
                             o_f = fl;
                         }
+                        ++pr_dec;
                     }
                     if (lane < nq) {
                         out_inv[i0 + lane] = o_v;
                         out_fl[i0 + lane] = (uint8_t)o_f;
                     }
                 }
+                pr_pub += clock64() - tp0;
             }
             // the call's releases may have raised permits: the range bound grows by what they returned at most
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) err |= __shfl_xor(err, d, 64);
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) pr_ovf += __shfl_xor(pr_ovf, d, 64);
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) tombs += __shfl_xor(tombs, d, 64);
             if (lane == 0) {
+                int32_t* pr = A.ctl + OWGS_RES_PROF;
+                st_sys(pr + 0, (int)pr_rounds);
+                st_sys(pr + 1, (int)pr_dec);
+                st_sys(pr + 2, (int)min(pr_stage, (u64)0x7FFFFFFF));
+                st_sys(pr + 3, (int)min(pr_rel, (u64)0x7FFFFFFF));
+                st_sys(pr + 4, (int)min(pr_pub, (u64)0x7FFFFFFF));
+                st_sys(pr + 5, (int)pr_ovf);
+                st_sys(pr + 6, (int)pr_hit);
+                st_sys(pr + 7, (int)pr_u);
+                st_sys(pr + 8, (int)pr_grp);
+                st_sys(&A.ctl[OWGS_RES_GEN], (int)gen);
                 sc[RS_USED] = used;
-                const long long mp = (long long)sc[RS_MAXP] + (long long)*(u64*)&sc[RS_RSUM];
+                sc[RS_TOMB] += tombs;
+                sc[RS_U0] = U0;
+                sc[RS_U1] = U1;
+                sc[RS_GEN] = gen;
+                const long long mp = (long long)sc[RS_MAXP] + (long long)rsum;
                 sc[RS_MAXP] = (int)min(mp, (long long)0x7FFFFFFF);
                 if (err) atomicOr(&sc[RS_ERR], err);
             }
         }
         __syncthreads();
         // ---- primary-table cleanup between calls: deleted entries keep chains long and fill the primary
-        if (sc[RS_USED] > OWGS_CTC / 2) {
-            int live = 0;
-            for (int i = tid; i < OWGS_CTC; i += 256) live += ct[i].x != 0u && ct[i].x != OWGS_CT_TOMB;
-            if (tid == 0) sc[RS_LIVE] = 0;
-            __syncthreads();
-            if (live) atomicAdd(&sc[RS_LIVE], live);
-            __syncthreads();
-            const int nlive = sc[RS_LIVE];
-            if (sc[RS_USED] - nlive >= OWGS_CTC / 8) {  // (uniform) enough deleted entries to pay for a rebuild
+        if (sc[RS_USED] > OWGS_CTC / 2 && sc[RS_TOMB] >= OWGS_CTC / 8) {  // (uniform) enough deleted entries
+            {
                 if (tid == 0) sc[RS_LIVE] = 0;
                 __syncthreads();
                 for (int i = tid; i < OWGS_CTC; i += 256) {
@@ -512,6 +760,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 }
                 __threadfence_block();
                 __syncthreads();
+                const int nlive = sc[RS_LIVE];
                 for (int i = tid; i < OWGS_CTC; i += 256) ct[i] = make_uint2(0u, 0u);
                 __syncthreads();
                 for (int j = tid; j < nlive; j += 256) {  // distinct keys into an empty table: claim by CAS
@@ -525,11 +774,20 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                         h = (h + 1) & (OWGS_CTC - 1);
                     }
                 }
-                if (tid == 0) sc[RS_USED] = nlive;
+                if (tid == 0) {
+                    sc[RS_USED] = nlive;
+                    sc[RS_TOMB] = 0;
+                }
                 __syncthreads();
             }
         }
-        // ---- answer: outputs are in host memory before the result and the done word
+        // ---- answer: the outputs to host memory (16-byte stores), then the result and the done word
+        if (bail == 0) {
+            for (uint32_t o = 16u * tid; o < s_end - s_out; o += 16u * 256u)
+                *(uint4*)(A.out + o) = *(const uint4*)(stg + s_out + o);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // every wave's output stores are done (system scope) ...
+        __syncthreads();                               // ... before thread 0 answers
         if (tid == 0) {
             const int e = sc[RS_ERR];  // (reported in the result word, not the context's error word)
             sc[RS_ERR] = 0;

@@ -10,7 +10,7 @@ for s in ${STEPS:-tests smoke}; do
       timeout -k 10 60 ./tools/micro/handoff > $O/handoff.json 2>&1
       rc=$?; cat $O/handoff.json; [ $rc -eq 0 ] || stop handoff $rc ;;
     launchlat)  # fixed costs of a shim call: launches, copies, zero-copy, resident-kernel doorbell
-      timeout -k 10 120 ./tools/micro/launch_lat > $O/launch_lat.json 2>&1
+      timeout -k 10 90 ./tools/micro/launch_lat > $O/launch_lat.json 2>&1
       rc=$?; cat $O/launch_lat.json; [ $rc -eq 0 ] || stop launchlat $rc ;;
     restests)  # the resident engine's tests alone (fast feedback)
       timeout -k 10 300 python -u -m pytest tests/test_gpu_resident.py tests/test_gpu_shim_sequence.py -x -v --timeout 200 --timeout-method thread > $O/pytest_res.log 2>&1
@@ -24,6 +24,15 @@ for s in ${STEPS:-tests smoke}; do
     shim)  # the bench's shim-path leg (calls vs fused) at drains 64 / 512
       timeout -k 10 300 python tools/shim_leg.py --drains 64,512 > $O/shim.json 2> $O/shim.err
       rc=$?; cut -c1-1500 $O/shim.json; [ $rc -eq 0 ] || { tail -5 $O/shim.err; stop shim $rc; } ;;
+    resrate)  # sequential resident engine vs the launch chain on whole streams in 1500-job drains (decisions/s)
+      rm -f $O/resrate.jsonl
+      for c in ${RES_CFGS:-headline c2 c4 headline:0/8}; do
+        OWGS_RES_MAX=2048 timeout -k 10 300 python tools/shim_leg.py --config $c --drains 1500 --budget 150000 --modes fused >> $O/resrate.jsonl 2>> $O/resrate.err
+        rc=$?; [ $rc -eq 0 ] || { tail -5 $O/resrate.err; stop resrate $rc; }
+        OWGS_RESIDENT=0 timeout -k 10 300 python tools/shim_leg.py --config $c --drains 1500 --budget 150000 --modes fused >> $O/resrate.jsonl 2>> $O/resrate.err
+        rc=$?; [ $rc -eq 0 ] || { tail -5 $O/resrate.err; stop resrate $rc; }
+      done
+      cut -c1-600 $O/resrate.jsonl ;;
     shimphases)  # per-call engine cycles at small drains (profile build)
       OWGS_LIB=openwhisk_amd/libowgs_prof.so CALLS=300 timeout -k 10 300 python tools/shim_phases.py 64,512 > $O/shimphases.jsonl 2> $O/shimphases.err
       rc=$?; cat $O/shimphases.jsonl; [ $rc -eq 0 ] || { tail -5 $O/shimphases.err; stop shimphases $rc; } ;;

@@ -36,17 +36,21 @@ __global__ void io_k(const int* in, int* out, int n) {
 __device__ __forceinline__ int ld_sys(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
 __device__ __forceinline__ void st_sys(int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
 
-// resident: ctl[0] = doorbell (call number from the host, -1 = stop), ctl[64] = answer
-__global__ __launch_bounds__(256) void resident_k(int* ctl, const int* in, int* out, int n, int max_idle) {
+// resident: ctl[0] = doorbell (call number from the host, -1 = stop), ctl[64] = answer, ctl[32] = 1 once started,
+// ctl[96] = polls done (written at exit); exits after idle_ticks (s_memrealtime, 100 MHz) without a new call
+__global__ __launch_bounds__(256) void resident_k(int* ctl, const int* in, int* out, int n, long long idle_ticks) {
     __shared__ int s_k;
-    int last = 0, idle = 0;
+    int last = 0, polls = 0;
+    if (threadIdx.x == 0) st_sys(ctl + 32, 1);
+    unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         if (threadIdx.x == 0) {
             int k;
             for (;;) {
                 k = ld_sys(ctl);
+                ++polls;
                 if (k != last) break;
-                if (++idle > max_idle) {
+                if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > idle_ticks) {
                     k = -1;
                     break;
                 }
@@ -57,8 +61,7 @@ __global__ __launch_bounds__(256) void resident_k(int* ctl, const int* in, int* 
         __syncthreads();
         const int k = s_k;
         __syncthreads();
-        if (k < 0) return;
-        idle = 0;
+        if (k < 0) break;
         last = k;
         if (n > 0) {
             for (int i = threadIdx.x; i < n; i += blockDim.x) {
@@ -69,7 +72,9 @@ __global__ __launch_bounds__(256) void resident_k(int* ctl, const int* in, int* 
             __syncthreads();
         }
         if (threadIdx.x == 0) st_sys(ctl + 64, k);
+        t0 = __builtin_amdgcn_s_memrealtime();
     }
+    if (threadIdx.x == 0) st_sys(ctl + 96, polls);
 }
 
 static double p50(std::vector<double>& v) {
@@ -137,34 +142,51 @@ int main() {
         if (i >= W) t.push_back(us_since(t0));
     }
     report("zerocopy", t, false);
-    // resident kernel round trips
-    for (int io = 0; io < 2; ++io) {
+    // resident kernel round trips; every wait is bounded by wall-clock time
+    for (int mode = 0; mode < 3; ++mode) {  // 0: doorbell, 1: + 1 KB in/out, 2: doorbell after a hipStreamQuery flush
+        const int io = mode == 1;
+        const char* name = mode == 0 ? "doorbell" : mode == 1 ? "doorbell_io" : "doorbell_flushed";
         volatile int* vc = ctl;
         vc[0] = 0;
+        vc[32] = 0;
         vc[64] = 0;
-        hipLaunchKernelGGL(resident_k, dim3(1), dim3(256), 0, s, ctl, hin, hout, io ? NI : 0, 1 << 22);
+        vc[96] = 0;
+        auto tl = clk::now();
+        hipLaunchKernelGGL(resident_k, dim3(1), dim3(256), 0, s, ctl, hin, hout, io ? NI : 0, 20000000ll);  // 200 ms idle
+        if (mode == 2) (void)hipStreamQuery(s);
+        bool alive = false;
+        while (us_since(tl) < 2e6) {
+            if (__atomic_load_n(&ctl[32], __ATOMIC_ACQUIRE) == 1) {
+                alive = true;
+                break;
+            }
+        }
+        const double t_alive = us_since(tl);
         t.clear();
-        bool ok = true;
-        for (int i = 1; i <= N + W && ok; ++i) {
+        int served = 0;
+        for (int i = 1; i <= N + W && alive; ++i) {
             auto t0 = clk::now();
             __atomic_store_n(&ctl[0], i, __ATOMIC_RELEASE);
-            long spins = 0;
-            while (__atomic_load_n(&ctl[64], __ATOMIC_ACQUIRE) != i) {
-                if (++spins > 200000000L) {
-                    ok = false;
+            bool ok = false;
+            while (us_since(t0) < 100000) {
+                if (__atomic_load_n(&ctl[64], __ATOMIC_ACQUIRE) == i) {
+                    ok = true;
                     break;
                 }
             }
-            if (io && ok && hout[NI - 1] != NI - 1 + i) ok = false;
+            if (!ok || (io && hout[NI - 1] != NI - 1 + i)) break;
+            ++served;
             if (i > W) t.push_back(us_since(t0));
         }
         __atomic_store_n(&ctl[0], -1, __ATOMIC_RELEASE);
         CK(hipStreamSynchronize(s));
-        if (!ok) {
-            printf(", \"%s\": \"failed\"", io ? "doorbell_io" : "doorbell");
-            continue;
+        printf(", \"%s\": {\"start_us\": %.1f, \"served\": %d, \"polls\": %d", name, t_alive, served, ctl[96]);
+        if (t.size() > 10) {
+            const double a = p50(t), b = p99(t);
+            printf(", \"p50\": %.2f, \"p99\": %.2f", a, b);
         }
-        report(io ? "doorbell_io" : "doorbell", t, false);
+        printf("}");
+        fflush(stdout);
     }
     printf("}}\n");
     return 0;

@@ -1,7 +1,7 @@
 """Diagnostic: analyse a barrier timeline written by a -DOWGS_TRACE engine (env OWGS_TRACE_FILE).
 
-For every pass-loop barrier (1 chunk start, 2 after speculation, 3 after tentative consumption, 4 before commit,
-5 end of pass) and every wave: cycles from the previous barrier's departure to this arrival (the wave's own work),
+For every pass-loop barrier (1 chunk start, 8 after the hot-action and per-lane walks, 2 after the queued long walks,
+3 after tentative consumption, 4 before commit, 5 end of pass) and every wave: cycles from the previous barrier's departure to this arrival (the wave's own work),
 which wave arrived last (the critical path), and the barrier's own cost (last arrival -> departure)."""
 import sys
 
@@ -17,7 +17,9 @@ td = ev[:, :, 1].astype(np.int64)
 n = int((ids[0] > 0).sum())
 ids, ta, td = ids[:, :n], ta[:, :n], td[:, :n]
 assert (ids == ids[0]).all(), "waves disagree on the barrier sequence"
-names = {1: "chunk_start", 2: "speculate", 3: "tentative", 4: "validate", 5: "commit", 8: "long-walk queue",
+# a phase is named after what runs before the barrier that ends it: barrier 8 ends the hot-action and per-lane walks
+# (and the long-walk queue's push), barrier 2 the queued long walks (round 3's files used the two names swapped)
+names = {1: "chunk_start", 2: "long walks", 3: "tentative", 4: "validate", 5: "commit", 8: "speculate",
          6: "(mark) chunk loop", 7: "(mark) lane decode", 9: "re-decisions"}
 work = ta[:, 1:] - td[:, :-1]  # per wave: departure of barrier k-1 -> arrival at barrier k
 crit = work.max(axis=0)
@@ -36,8 +38,8 @@ for x in range(kind.size):
     if kind[x] == 5:
         state = False
 rows = [(names[k], kind == k) for k in sorted(names)]
-rows += [(names[k] + "/first", (kind == k) & first) for k in (2, 3, 4, 5)]
-rows += [(names[k] + "/later", (kind == k) & ~first) for k in (2, 3, 4, 5)]
+rows += [(names[k] + "/first", (kind == k) & first) for k in (8, 2, 3, 4, 5)]
+rows += [(names[k] + "/later", (kind == k) & ~first) for k in (8, 2, 3, 4, 5)]
 for label, m in rows:
     if not m.any():
         continue
