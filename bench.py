@@ -228,7 +228,7 @@ def shim_path(w, o_inv, dev_index, drains=(64, 512, 4096), budget_jobs=(120_000,
     b.register_actions(w.actions)
     b.snapshot()
     L, h = b._L, b._h
-    p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    p = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
     act = np.ascontiguousarray(s.act, np.int32)
     legs = []
     for drain, budget in zip(drains, budget_jobs):
@@ -238,7 +238,7 @@ def shim_path(w, o_inv, dev_index, drains=(64, 512, 4096), budget_jobs=(120_000,
             rs0 = b.resident_stats()
             inv = np.full(len(act), -9, np.int32)
             fl = np.zeros(len(act), np.uint8)
-            lat, n_pub = [], 0
+            lat, clat, n_pub = [], [], 0
             for c0 in range(0, n_jobs, drain):
                 k = kind[c0:min(c0 + drain, n_jobs)]
                 x = ids[c0:c0 + len(k)]
@@ -261,18 +261,22 @@ def shim_path(w, o_inv, dev_index, drains=(64, 512, 4096), budget_jobs=(120_000,
                     for ri, ra, pubs in runs:
                         if len(ri):
                             rf = np.zeros(len(ri), np.uint8)
+                            args = (h, len(ri), p(ri), p(ra), p(rf))
                             t0 = time.perf_counter()
-                            rc = L.owgs_release_batch(h, len(ri), p(ri), p(ra), p(rf))
+                            rc = L.owgs_release_batch(*args)
                             lat.append(time.perf_counter() - t0)
+                            clat.append(b.last_call_ns())
                             assert rc == 0
                         if len(pubs):
                             pa = np.ascontiguousarray(act[pubs])
                             sq = pubs.astype(np.uint64)
                             o = np.zeros(len(pubs), np.int32)
                             f = np.zeros(len(pubs), np.uint8)
+                            args = (h, len(pubs), p(pa), p(sq), 0, p(o), p(f))
                             t0 = time.perf_counter()
-                            rc = L.owgs_publish_batch(h, len(pubs), p(pa), p(sq), 0, p(o), p(f))
+                            rc = L.owgs_publish_batch(*args)
                             lat.append(time.perf_counter() - t0)
+                            clat.append(b.last_call_ns())
                             assert rc == 0
                             inv[pubs], fl[pubs] = o, f
                             n_pub += len(pubs)
@@ -287,27 +291,34 @@ def shim_path(w, o_inv, dev_index, drains=(64, 512, 4096), budget_jobs=(120_000,
                     o = np.zeros(len(pubs) + 1, np.int32)
                     f = np.zeros(len(pubs) + 1, np.uint8)
                     rf = np.zeros(len(ri), np.uint8)
+                    # (the buffers' addresses before the clock: the JNI shim hands over direct-buffer addresses; numpy's
+                    # ctypes conversion costs ~2.7 us per pointer on the host, more than the call itself at small drains)
+                    args = (h, len(runs), p(ro), p(ri), p(ra), p(rf), p(po), p(pa), p(sq), 0, p(o), p(f))
                     t0 = time.perf_counter()
-                    rc = L.owgs_process_batch(h, len(runs), p(ro), p(ri), p(ra), p(rf), p(po), p(pa), p(sq), 0, p(o),
-                                              p(f))
+                    rc = L.owgs_process_batch(*args)
                     lat.append(time.perf_counter() - t0)
+                    clat.append(b.last_call_ns())
                     assert rc == 0, (rc, L.owgs_last_error(h))
                     inv[pubs], fl[pubs] = o[:len(pubs)], f[:len(pubs)]
                     n_pub += len(pubs)
             done = inv != -9
             exact = bool(np.array_equal(inv[done], o_inv[done])) if o_inv is not None else None
-            lat_us = np.array(lat) * 1e6
+            lat_us = np.array(clat) * 1e-3  # the C call, timed inside the library
+            py_us = np.array(lat) * 1e6     # the same calls seen from Python (+ ctypes' argument conversion)
             rs1 = b.resident_stats()
             legs.append({"drain": drain, "mode": mode, "jobs": n_jobs, "calls": len(lat), "publishes": int(n_pub),
                          "p50_us": float(np.percentile(lat_us, 50)), "p99_us": float(np.percentile(lat_us, 99)),
-                         "decisions_per_s": n_pub / max(float(np.sum(lat)), 1e-9), "bit_exact": exact,
+                         "decisions_per_s": n_pub / max(float(np.sum(lat_us)) * 1e-6, 1e-9),
+                         "py_p50_us": float(np.percentile(py_us, 50)), "py_p99_us": float(np.percentile(py_us, 99)),
+                         "bit_exact": exact,
                          # owgs_process_batch's paths in this leg: resident engine calls / launches, launch-chain calls
-                         "resident": {k: rs1[k] - rs0[k] for k in rs1 if k != "alive"}})
+                         "resident": {k: rs1[k] - rs0[k] for k in rs1 if k not in ("alive", "last_call_ns")}})
     b.close()
     return {"path": "host buffers through the C ABI as the JNI shim calls it (queue order: each batch's completions, "
                     "then its publishes); calls = owgs_release_batch + owgs_publish_batch per run, fused = "
                     "owgs_process_batch per drained batch (small calls: the resident engine, owgs_resident.hip); "
-                    "latency = the C call", "legs": legs}
+                    "latency = the C call, timed inside the library (py_* = the same calls timed from Python, "
+                    "ctypes' call overhead included)", "legs": legs}
 
 
 def dry_run(args):

@@ -348,8 +348,9 @@ int owgs_engine_ms(owgs_ctx* ctx, float* ms);
  * refused untouched (a release that could leave the on-chip permit range; the chain took them), [3] calls the launch
  * chain took, [4] 1 while a resident engine is live; then, summed over the served calls: [5] walk rounds, [6]
  * decisions, [7] staging cycles, [8] release cycles, [9] publish cycles, [10] overflow lookups, [11] walks that
- * started at a cursor, [12] walks skipped by the pool permit bound, [13] decisions of grouped walks.  Returns the
- * number of counters (14). */
+ * started at a cursor, [12] walks skipped by the pool permit bound, [13] decisions of grouped walks; [14] the
+ * duration in ns of the last owgs_publish_batch / owgs_release_batch / owgs_process_batch call, entry to return, timed
+ * inside the library.  Returns the number of counters (15). */
 int owgs_resident_stats(owgs_ctx* ctx, int64_t* out, int32_t cap);
 
 /* Restore the slot state captured by owgs_snapshot (bench: every timed step starts from the same state). */

@@ -227,13 +227,19 @@ class GpuShardingContainerPoolBalancer:
     def resident_stats(self) -> dict:
         """owgs_process_batch's paths: calls the resident engine served, its launches, calls it refused untouched,
         calls the launch chain took, and whether a resident engine is live."""
-        out = np.zeros(14, np.int64)
-        n = self._L.owgs_resident_stats(self._h, _p(out), 14)
+        out = np.zeros(15, np.int64)
+        n = self._L.owgs_resident_stats(self._h, _p(out), 15)
         if n < 0:
             self._chk(n)
         return dict(zip(("served", "launches", "refused", "chained", "alive", "walk_rounds", "decisions",
                          "stage_cycles", "release_cycles", "publish_cycles", "overflow_lookups", "cursor_walks",
-                         "bound_skips", "grouped_decisions"), (int(x) for x in out)))
+                         "bound_skips", "grouped_decisions", "last_call_ns"), (int(x) for x in out)))
+
+    def last_call_ns(self) -> int:
+        """Duration of the last publish / release / process_batch call, timed inside the library (no ctypes cost)."""
+        out = np.zeros(15, np.int64)
+        self._L.owgs_resident_stats(self._h, _p(out), 15)
+        return int(out[14])
 
     def set_health_tid(self, start_ms: int):
         """TransactionId.invokerHealth's start time (TransactionId.scala:225): health acks echo it."""

@@ -313,6 +313,7 @@ struct owgs_ctx {
     DevBuf<uint2> d_res_cur;        // per action: {cursor generation, first walk step that may fit}
     std::vector<uint2> res_meta;    // act_meta as of the live launch (every change of it stops the engine first)
     uint32_t res_gen_seen = 0;      // the last cursor generation the engine reported
+    int64_t last_call_ns = 0;       // duration of the last publish / release / process_batch call, timed inside the library
     DevBuf<unsigned long long> f_bound;  // per slot: what a fused call's releases can return (zero between calls)
     DevBuf<uint32_t> s_w_keys, s_w_vals;
     DevBuf<int32_t> s_w_wkey;
@@ -1130,6 +1131,17 @@ static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
     return OWGS_OK;
 }
 
+// times one ABI call, entry to return, into c->last_call_ns (the latency the JNI shim sees, without the host
+// language's call overhead)
+struct CallTimer {
+    owgs_ctx* c;
+    std::chrono::steady_clock::time_point t0;
+    explicit CallTimer(owgs_ctx* c_) : c(c_), t0(std::chrono::steady_clock::now()) {}
+    ~CallTimer() {
+        if (c) c->last_call_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    }
+};
+
 extern "C" {
 
 int owgs_abi_version(void) { return OWGS_ABI_VERSION; }
@@ -1607,6 +1619,7 @@ int owgs_release_actions(owgs_ctx* c, int32_t n, const int32_t* actions) {
 int owgs_publish_batch(owgs_ctx* c, int32_t n, const int32_t* action, const uint64_t* seq, uint64_t seq_base,
                        int32_t* out_invoker, uint8_t* out_flags) {
     if (!c || n < 0 || (n > 0 && (!action || !out_invoker || !out_flags))) return OWGS_EINVAL;
+    const CallTimer timer_(c);
     if (n == 0) return OWGS_OK;
     if (!registered(c, n, action)) return c->fail(OWGS_ENOENT, "unknown action");
     OWGS_ENTER(c);
@@ -1695,6 +1708,7 @@ static int release_chain(owgs_ctx* c, int32_t n, const int32_t* inv, const int32
 }
 
 int owgs_release_batch(owgs_ctx* c, int32_t n, const int32_t* invoker, const int32_t* action, uint8_t* out_flags) {
+    const CallTimer timer_(c);
     if (!c || n < 0 || (n > 0 && (!invoker || !action))) return OWGS_EINVAL;
     if (n == 0) return OWGS_OK;
     if (!registered(c, n, action)) return c->fail(OWGS_ENOENT, "unknown action");
@@ -2295,6 +2309,7 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
                        const int32_t* rel_action, uint8_t* rel_flags, const int32_t* pub_off,
                        const int32_t* pub_action, const uint64_t* seq, uint64_t seq_base, int32_t* out_invoker,
                        uint8_t* out_flags) {
+    const CallTimer timer_(c);
     if (!c || n_runs < 0 || (n_runs > 0 && (!rel_off || !pub_off))) return OWGS_EINVAL;
     if (n_runs == 0) return OWGS_OK;
     if (rel_off[0] != 0 || pub_off[0] != 0) return c->fail(OWGS_EINVAL, "offsets must start at 0");
@@ -3255,7 +3270,8 @@ int owgs_resident_stats(owgs_ctx* c, int64_t* out, int32_t cap) {
     const int64_t v[5] = {c->res_n_calls, c->res_n_launches, c->res_n_bails, c->res_n_chained, c->res_alive ? 1 : 0};
     for (int32_t i = 0; i < cap && i < 5; ++i) out[i] = v[i];
     for (int32_t i = 5; i < cap && i < 5 + OWGS_RES_NPROF; ++i) out[i] = c->res_prof[i - 5];
-    return 5 + OWGS_RES_NPROF;
+    if (cap > 5 + OWGS_RES_NPROF) out[5 + OWGS_RES_NPROF] = c->last_call_ns;
+    return 6 + OWGS_RES_NPROF;
 }
 
 int owgs_engine_ms(owgs_ctx* c, float* ms) {

@@ -44,6 +44,11 @@ for s in ${STEPS:-tests smoke}; do
     bench)
       timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
       rc=$?; cut -c1-400 $O/bench.json; [ $rc -eq 0 ] || { tail -20 $O/bench.err; stop bench $rc; } ;;
+    benchprof)  # kernel stats of the default bench command (profiles/r04_kernel_stats.csv)
+      rm -rf $O/benchprof
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/benchprof -o run --output-format csv -- \
+        python3 bench.py --no-shim-path > $O/benchprof.log 2>&1
+      rc=$?; tail -1 $O/benchprof.log | cut -c1-300; [ $rc -eq 0 ] || stop benchprof $rc ;;
     phases)
       OWGS_LIB=openwhisk_amd/libowgs_prof.so REPS=2 timeout -k 10 400 python tools/prof_phases.py ${PHASE_CFGS:-headline c2 c4 headline:0/8} > $O/phases.log 2>&1
       rc=$?; cut -c1-200 $O/phases.log; [ $rc -eq 0 ] || stop phases $rc ;;

@@ -60,8 +60,9 @@ for drain in drains:
         o = np.zeros(len(pubs) + 1, np.int32)
         f = np.zeros(len(pubs) + 1, np.uint8)
         rf = np.zeros(len(ri), np.uint8)
+        args = (h, len(ro) - 1, p(ro), p(ri), p(ra), p(rf), p(po), p(pa), p(sq), 0, p(o), p(f))
         t0 = time.perf_counter()
-        rc = L.owgs_process_batch(h, len(ro) - 1, p(ro), p(ri), p(ra), p(rf), p(po), p(pa), p(sq), 0, p(o), p(f))
+        rc = L.owgs_process_batch(*args)
         lat.append(time.perf_counter() - t0)
         assert rc == 0, L.owgs_last_error(h)
         inv[pubs] = o[:len(pubs)]
