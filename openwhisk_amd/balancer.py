@@ -67,6 +67,10 @@ def _blob(items) -> tuple[np.ndarray, np.ndarray]:
     return np.frombuffer(b"".join(enc) + b"\0", dtype=np.uint8), off
 
 
+_RES_PROF = ("walk_rounds", "decisions", "stage_cycles", "release_cycles", "publish_cycles", "overflow_lookups",
+             "cursor_walks", "bound_skips", "grouped_decisions")
+
+
 class GpuShardingContainerPoolBalancer:
     """One controller shard (SCPB:147-332) backed by the MI355X engine."""
 
@@ -231,9 +235,14 @@ class GpuShardingContainerPoolBalancer:
         n = self._L.owgs_resident_stats(self._h, _p(out), 15)
         if n < 0:
             self._chk(n)
-        return dict(zip(("served", "launches", "refused", "chained", "alive", "walk_rounds", "decisions",
-                         "stage_cycles", "release_cycles", "publish_cycles", "overflow_lookups", "cursor_walks",
-                         "bound_skips", "grouped_decisions", "last_call_ns"), (int(x) for x in out)))
+        return dict(zip(("served", "launches", "refused", "chained", "alive") + _RES_PROF + ("last_call_ns",),
+                        (int(x) for x in out)))
+
+    def stream_mode_stats(self) -> dict | None:
+        """The last replay's resident-engine counters when it ran in stream mode (OWGS_SPEC_REPLAY), else None."""
+        out = np.zeros(25, np.int64)
+        self._chk(min(0, self._L.owgs_resident_stats(self._h, _p(out), 25)))
+        return dict(zip(_RES_PROF, (int(x) for x in out[16:25]))) if out[15] else None
 
     def last_call_ns(self) -> int:
         """Duration of the last publish / release / process_batch call, timed inside the library (no ctypes cost)."""

@@ -109,8 +109,16 @@ struct EnvOpts {
     // its idle time before it writes the state back and exits (OWGS_RESIDENT=0 sends every call down the chain)
     int res = 1, res_max = 1024;
     long long res_idle_us = 20000;
+    // the resident engine's speculative walks: walk steps each publish probes on its own before the in-order
+    // validation (0: every decision walked one at a time)
+    int res_spec = 16;
+    // owgs_replay_device through the resident engine's stream mode (one wave deciding, speculative walks) instead of
+    // the chunked engine, where it applies (identity pools, no watched pairs)
+    int spec_replay = 0;
     EnvOpts() {
+        if (const char* e = getenv("OWGS_SPEC_REPLAY")) spec_replay = atoi(e);
         if (const char* e = getenv("OWGS_RESIDENT")) res = atoi(e);
+        if (const char* e = getenv("OWGS_RES_SPEC")) res_spec = atoi(e);
         if (const char* e = getenv("OWGS_RES_MAX")) res_max = atoi(e);
         if (const char* e = getenv("OWGS_RES_IDLE_US")) res_idle_us = atoll(e);
         feat_all = getenv("OWGS_FEAT_ALL") != nullptr;  // the general engine for every launch (A/B diagnostics)
@@ -314,6 +322,8 @@ struct owgs_ctx {
     std::vector<uint2> res_meta;    // act_meta as of the live launch (every change of it stops the engine first)
     uint32_t res_gen_seen = 0;      // the last cursor generation the engine reported
     int64_t last_call_ns = 0;       // duration of the last publish / release / process_batch call, timed inside the library
+    DevBuf<unsigned long long> d_spec_stats;  // stream-mode replays: summed resident-engine counters (owgs_resident_stats)
+    bool spec_last = false;         // the last replay ran in stream mode
     DevBuf<unsigned long long> f_bound;  // per slot: what a fused call's releases can return (zero between calls)
     DevBuf<uint32_t> s_w_keys, s_w_vals;
     DevBuf<int32_t> s_w_wkey;
@@ -1004,6 +1014,7 @@ static int res_launch(owgs_ctx* c) {
     a.cur = c->d_res_cur.p;
     a.gen_base = ++c->res_gen_seen;  // above every generation stored by earlier launches
     a.idle_ticks = env_opts().res_idle_us * 100;  // s_memrealtime: 100 MHz
+    a.spec = std::max(0, env_opts().res_spec);
     volatile int32_t* ctl = c->res_ctl;
     ctl[OWGS_RES_STATE] = 0;
     ctl[OWGS_RES_DONE] = c->res_call;
@@ -1959,6 +1970,11 @@ static int replay_watch(owgs_ctx* c, int32_t nb, const int64_t* acq_off, const i
     return w_refresh(c, hs);
 }
 
+static bool spec_replay_eligible(const owgs_ctx* c);
+static int spec_replay(owgs_ctx* c, int32_t nb, const int64_t* acq_off, const int32_t* act, int64_t n_act,
+                       const int64_t* rel_off, const int64_t* rel_aid, int64_t n_rel, uint64_t seq_base,
+                       int32_t* out_inv, uint8_t* out_flags, uint8_t* rel_flags, hipStream_t hs);
+
 // One batch of a device-resident stream replayed batch by batch (state updates such as a health change in between):
 // releases rel_aid[r_beg, r_end) of activations decided by earlier calls (invoker in out_invoker), then the publishes
 // act[a_beg, a_end).  The releases are staged as engine records from the earlier decisions, so the batch is one
@@ -2000,6 +2016,13 @@ static int replay_device_span_impl(owgs_ctx* c, int64_t a_beg, int64_t a_end, in
         }
         return w_refresh(c, hs);
     }
+    if (spec_replay_eligible(c)) {  // one batch through the resident engine's stream mode
+        const int64_t offs[4] = {a_beg, a_end, r_beg, r_end};
+        HIPCHK(c, upload(c->w_off, offs, 4, hs));
+        return spec_replay(c, 1, c->w_off.p, act, na, nr > 0 ? c->w_off.p + 2 : nullptr, rel_aid, nr, seq_base,
+                           out_invoker, out_flags, rel_flags, hs);
+    }
+    c->spec_last = false;
     HIPCHK(c, c->f_rec.reserve((size_t)nr + 2));
     HIPCHK(c, c->f_src.reserve((size_t)nr + 1));
     HIPCHK(c, c->f_cnt.reserve(2));
@@ -2053,11 +2076,94 @@ int owgs_replay_device_span(owgs_ctx* c, int64_t a_beg, int64_t a_end, int64_t r
     return rc ? rc : rt;
 }
 
+// owgs_replay_device through the resident engine in stream mode (owgs_resident.hip): one workgroup loads the state,
+// replays every batch -- its releases, then its publishes, in pieces the staging area holds -- with one wave deciding
+// (speculative walks, in-order validation) and writes the state back.  Identity pools, no watched pairs.
+static bool spec_replay_eligible(const owgs_ctx* c) {
+    if (env_opts().spec_replay <= 0 || env_opts().res_spec <= 0 || c->pool_mode != 0 || c->w_cap > 0) return false;
+    if (c->n_slots > OWGS_MAX_SLOTS_CT || c->n_ids > c->n_slots || c->nm > (int32_t)OWGS_AM_POS_MASK ||
+        c->nb > (int32_t)OWGS_AM_POS_MASK || c->a_mem.empty())
+        return false;
+    return res_stage_bytes(c) >= 8192;
+}
+
+static int spec_replay(owgs_ctx* c, int32_t nb, const int64_t* acq_off, const int32_t* act, int64_t n_act,
+                       const int64_t* rel_off, const int64_t* rel_aid, int64_t n_rel, uint64_t seq_base,
+                       int32_t* out_inv, uint8_t* out_flags, uint8_t* rel_flags, hipStream_t hs) {
+    if (c->any_conc) {
+        const int rc = ensure_ovf(c, (int32_t)std::min<int64_t>(n_act, INT32_MAX), hs);
+        if (rc) return rc;
+        ovf_add(c, (int32_t)std::min<int64_t>(n_act, INT32_MAX));
+    }
+    HIPCHK(c, c->d_ct_tmp.reserve((size_t)2 * OWGS_CTC));
+    const size_t na = std::max<size_t>(c->a_mem.size(), 1);
+    // walk cursors: generations above every stored one; each release piece may start a new generation
+    if (c->d_res_cur.n < na || (uint64_t)c->res_gen_seen + (uint64_t)n_rel + 2 >= 0xFFFFFF00ull) {
+        HIPCHK(c, c->d_res_cur.reserve(std::max(na + na / 2, c->d_res_cur.n)));
+        HIPCHK(c, hipMemsetAsync(c->d_res_cur.p, 0, c->d_res_cur.n * sizeof(uint2), hs));
+        c->res_gen_seen = 0;
+    }
+    HIPCHK(c, c->d_spec_stats.reserve(OWGS_RES_NPROF));
+    HIPCHK(c, hipMemsetAsync(c->d_spec_stats.p, 0, OWGS_RES_NPROF * sizeof(unsigned long long), hs));
+    OwgsResArgs a{};
+    a.permits = c->d_permits.p;
+    a.n_slots = c->n_slots;
+    a.usable = c->d_usable.p;
+    a.n_ids = c->n_ids;
+    a.nm = c->nm;
+    a.nb = c->nb;
+    a.ct_keys = c->d_ct_keys.p;
+    a.ct_vals = c->d_ct_vals.p;
+    a.ct_tmp = c->d_ct_tmp.p;
+    a.ovf = ovf_args(c);
+    a.act_meta = c->d_act_meta.p;
+    a.act_slot = c->d_act_slot.p;
+    a.n_actions = (int32_t)c->a_mem.size();
+    a.rng_seed = c->cfg.rng_seed;
+    a.err = c->d_err.p;
+    a.stage_bytes = (int32_t)res_stage_bytes(c);
+    a.cur = c->d_res_cur.p;
+    a.gen_base = ++c->res_gen_seen;
+    c->res_gen_seen += (uint32_t)n_rel + 1;
+    a.spec = std::max(0, env_opts().res_spec);
+    a.smode = 1;
+    a.s_nb = nb;
+    a.s_acq_off = acq_off;
+    a.s_act = act;
+    a.s_rel_off = n_rel > 0 ? rel_off : nullptr;
+    a.s_rel_aid = rel_aid;
+    a.s_seq_base = seq_base;
+    a.s_out_inv = out_inv;
+    a.s_out_fl = out_flags;
+    a.s_rel_fl = rel_flags;
+    a.s_stats = c->d_spec_stats.p;
+    if (!c->ev_engine[0]) {
+        HIPCHK(c, hipEventCreate(&c->ev_engine[0]));
+        HIPCHK(c, hipEventCreate(&c->ev_engine[1]));
+    }
+    const size_t lds = owgs_resident_image_bytes(c->n_slots, c->n_ids) + (size_t)a.stage_bytes;
+    HIPCHK(c, hipEventRecord(c->ev_engine[0], hs));
+    HIPCHK(c, owgs_launch_resident(&a, lds, hs));
+    HIPCHK(c, hipEventRecord(c->ev_engine[1], hs));
+    c->ev_engine_valid = true;
+    c->spec_last = true;
+    return OWGS_OK;
+}
+
 static int replay_device_impl(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const int32_t* act,
                        int64_t n_activations, const int64_t* rel_off, const int64_t* rel_aid, int64_t n_releases,
                        uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, uint8_t* rel_flags, void* stream) {
     if (!c) return OWGS_EINVAL;
     hipStream_t hs = stream ? (hipStream_t)stream : c->stream;
+    if (n_batches > 0 && spec_replay_eligible(c)) {
+        if (!acq_off || !act || !out_invoker || !out_flags || n_activations < 0 || n_activations >= ((int64_t)1 << 31) ||
+            n_releases < 0 || (n_releases > 0 && (!rel_off || !rel_aid)))
+            return OWGS_EINVAL;
+        (void)hipSetDevice(c->cfg.device);
+        return spec_replay(c, n_batches, acq_off, act, n_activations, rel_off, rel_aid, n_releases, seq_base,
+                           out_invoker, out_flags, rel_flags, hs);
+    }
+    c->spec_last = false;
     if (c->w_cap > 0 && n_batches > 0) {
         if (!acq_off || !act || !out_invoker || !out_flags || n_activations < 0 || n_releases < 0 ||
             (n_releases > 0 && (!rel_off || !rel_aid)))
@@ -3271,7 +3377,18 @@ int owgs_resident_stats(owgs_ctx* c, int64_t* out, int32_t cap) {
     for (int32_t i = 0; i < cap && i < 5; ++i) out[i] = v[i];
     for (int32_t i = 5; i < cap && i < 5 + OWGS_RES_NPROF; ++i) out[i] = c->res_prof[i - 5];
     if (cap > 5 + OWGS_RES_NPROF) out[5 + OWGS_RES_NPROF] = c->last_call_ns;
-    return 6 + OWGS_RES_NPROF;
+    // the last replay in stream mode: its counters, summed over the launch (a synchronisation: diagnostics)
+    if (cap > 6 + OWGS_RES_NPROF) {
+        out[6 + OWGS_RES_NPROF] = c->spec_last ? 1 : 0;
+        unsigned long long v[OWGS_RES_NPROF] = {};
+        if (c->spec_last && c->d_spec_stats.p) {
+            (void)hipSetDevice(c->cfg.device);
+            HIPCHK(c, hipDeviceSynchronize());
+            HIPCHK(c, hipMemcpy(v, c->d_spec_stats.p, sizeof(v), hipMemcpyDeviceToHost));
+        }
+        for (int32_t i = 0; i < OWGS_RES_NPROF && 7 + OWGS_RES_NPROF + i < cap; ++i) out[7 + OWGS_RES_NPROF + i] = (int64_t)v[i];
+    }
+    return 7 + 2 * OWGS_RES_NPROF;
 }
 
 int owgs_engine_ms(owgs_ctx* c, float* ms) {

@@ -348,6 +348,19 @@ struct OwgsResArgs {
     uint2* cur;                  // [n_actions] walk cursor of each action: {generation, first walk step that may fit}
     uint32_t gen_base;           // first cursor generation of this launch (above every generation stored in cur)
     long long idle_ticks;        // s_memrealtime ticks (100 MHz) without a call before the engine writes back and exits
+    int32_t spec;                // walk steps of each publish's speculative walk (0: decisions one at a time only)
+    // stream mode (owgs_replay_device through this engine): no doorbell, the stream's batches from HBM
+    int32_t smode;
+    int32_t s_nb;
+    const int64_t* s_acq_off;    // [s_nb + 1]
+    const int32_t* s_act;        // [n_activations] action handle of each activation
+    const int64_t* s_rel_off;    // [s_nb + 1] or null
+    const int64_t* s_rel_aid;    // released activations (decided by an earlier batch)
+    unsigned long long s_seq_base;
+    int32_t* s_out_inv;
+    uint8_t* s_out_fl;
+    uint8_t* s_rel_fl;           // or null
+    unsigned long long* s_stats; // [OWGS_RES_NPROF] summed counters, or null
 };
 
 // owgs_process_batch: the caller's releases (invoker, action handle) of each run as engine release records

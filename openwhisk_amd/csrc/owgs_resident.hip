@@ -60,6 +60,32 @@ __device__ __forceinline__ int wave_max_i(int v) {
     for (int d = 32; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d, 64));
     return v;
 }
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = min(v, __shfl_xor(v, d, 64));
+    return v;
+}
+// walk-cursor cache (LDS): per action (hashed) the first walk step that may still fit, valid for one cursor generation;
+// an entry is one 64-bit word {action + 1 | generation mod 2^15 << 17, step}, written by atomic exchange so that lanes
+// storing into the same entry leave one whole entry (the cache is cleared when the generation wraps mod 2^15)
+__device__ __forceinline__ uint32_t cc_tag(uint32_t a, uint32_t gen) { return (a + 1u) | ((gen & 0x7FFFu) << 17); }
+__device__ __forceinline__ uint32_t cc_slot(uint32_t a) { return (a * 2654435761u) >> (32 - 11); }
+__device__ __forceinline__ int cc_get(const uint2* cc, uint32_t a, uint32_t gen) {
+    const uint2 e = cc[cc_slot(a)];
+    return e.x == cc_tag(a, gen) ? (int)e.y : 0;
+}
+__device__ __forceinline__ void cc_put(uint2* cc, uint32_t a, uint32_t gen, int step) {
+    (void)__hip_atomic_exchange((u64*)&cc[cc_slot(a)], ((u64)(uint32_t)step << 32) | cc_tag(a, gen), __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// speculative walk outcomes (resident engine, per decision of a chunk)
+#define SP_NONE 0    // no decision in this lane
+#define SP_TRIV 1    // decided without touching the state (None, the throw, a fallback without a healthy invoker)
+#define SP_FOUND 2   // a target with room at the chunk's start: holds unless the decisions before took that room
+#define SP_FORCED 3  // every pool position was full: the fallback's invoker, forced
+#define SP_STOP 4    // decided alone: concurrent, or the walk was not finished within the budget
+#define SP_FAIL 5    // (transient) the walk found no room anywhere
+
 // position of the need-th set bit of m (need < popc(m))
 __device__ __forceinline__ int select_in_word(uint32_t m, int need) {
     int pos = 0;
@@ -76,7 +102,7 @@ __device__ __forceinline__ int select_in_word(uint32_t m, int need) {
 
 #define RES_CC 2048  // walk-cursor cache entries (LDS, 16 KB)
 struct ResLayout {
-    uint32_t P, ub, pc, ct, sc, cc, stage, end;
+    uint32_t P, ub, pc, ct, sc, cc, mv, stage, end;
 };
 __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
     const uint32_t words = (uint32_t)(n_ids + 31) / 32;
@@ -87,7 +113,8 @@ __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
     y.ct = y.pc + ((words + 2u + 3u) & ~3u) * 4u;
     y.sc = y.ct + OWGS_CTC * 8u;
     y.cc = y.sc + 64u * 4u;
-    y.stage = y.cc + RES_CC * 8u;
+    y.mv = y.cc + RES_CC * 8u;
+    y.stage = y.mv + 64u * 4u;
     y.end = y.stage;
     return y;
 }
@@ -146,6 +173,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
     uint2* ct = (uint2*)(Lb + Y.ct);
     int32_t* sc = (int32_t*)(Lb + Y.sc);
     uint2* cc = (uint2*)(Lb + Y.cc);
+    int32_t* mv = (int32_t*)(Lb + Y.mv);
     char* stg = Lb + Y.stage;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int n_slots = A.n_slots, nm = A.nm, nb = A.nb;
@@ -220,13 +248,74 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
         if (need < 0 || need >= __popc(m)) return -1;
         return (a << 5) + select_in_word(m, need);
     };
-    if (tid == 0) st_sys(&A.ctl[OWGS_RES_STATE], 1);
+    // stream mode (owgs_replay_device): no doorbell; the calls are the stream's batches, each as pieces of its
+    // releases and then of its publishes that fit the staging area, read from HBM
+    const bool smode = A.smode != 0;
+    if (tid == 0 && !smode) st_sys(&A.ctl[OWGS_RES_STATE], 1);
+    int s_b = 0, s_ph = 0;                  // (thread 0, stream mode) batch, phase (0 releases, 1 publishes),
+    long long s_o = 0, s_r0 = 0, s_r1 = 0, s_p0 = 0, s_p1 = 0;  // offset in the phase, the batch's ranges
+    bool s_loaded = false;
+    const int s_rcap = min(4096, (A.stage_bytes - 96) / 17), s_pcap = min(2048, (A.stage_bytes - 128) / 29);
 
     // ------------------------------------------------------------------ calls
     int last = A.last_call;
     u64 t_idle = __builtin_amdgcn_s_memrealtime();
     for (;;) {
-        if (tid == 0) {
+        if (smode) {
+            if (tid == 0) {
+                int kk = -1, nr = 0, np = 0;
+                long long base = 0;
+                while (s_b < A.s_nb) {
+                    if (!s_loaded) {  // the batch's ranges (four independent loads: one round trip)
+                        s_r0 = A.s_rel_off ? A.s_rel_off[s_b] : 0;
+                        s_r1 = A.s_rel_off ? A.s_rel_off[s_b + 1] : 0;
+                        s_p0 = A.s_acq_off[s_b];
+                        s_p1 = A.s_acq_off[s_b + 1];
+                        s_loaded = true;
+                    }
+                    if (s_ph == 0) {
+                        if (s_r0 + s_o < s_r1) {
+                            base = s_r0 + s_o;
+                            nr = (int)min((long long)s_rcap, s_r1 - base);
+                            s_o += nr;
+                            kk = 1;
+                            break;
+                        }
+                        s_ph = 1;
+                        s_o = 0;
+                    } else {
+                        if (s_p0 + s_o < s_p1) {
+                            base = s_p0 + s_o;
+                            np = (int)min((long long)s_pcap, s_p1 - base);
+                            s_o += np;
+                            kk = 1;
+                            break;
+                        }
+                        s_ph = 0;
+                        s_o = 0;
+                        s_loaded = false;
+                        ++s_b;
+                    }
+                }
+                int32_t* h = sc + 32;
+                const u64 sb = A.s_seq_base + (u64)(np ? base : 0);
+                h[0] = 1;
+                h[1] = nr;
+                h[2] = np;
+                h[3] = 0;
+                h[4] = (int32_t)(uint32_t)sb;
+                h[5] = (int32_t)(uint32_t)(sb >> 32);
+                h[6] = 16;
+                h[7] = 32;
+                h[8] = 32 + 16 * nr;
+                h[9] = 32 + 16 * nr + 16 * np;
+                h[10] = h[9];
+                h[11] = h[12] = 0;
+                h[13] = (int32_t)base;  // first release / publish of the piece in the stream
+                sc[RS_K] = kk;
+                *(u64*)&sc[RS_RSUM] = 0ull;
+            }
+        } else if (tid == 0) {
             int k = last;
             bool stop = false;
             for (long long spin = 0;; ++spin) {
@@ -250,8 +339,8 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
         // wrote the records complete (action meta and slot key per publish and release), so staging is a copy: the
         // header and the first 4 KB of the block are read together (one PCIe round trip for a small call)
         int32_t* hdr = sc + 32;  // RS_HDR words
-        if (tid < OWGS_RES_NHDR) hdr[tid] = ld_sys(A.ctl + OWGS_RES_HDR + tid);
-        {
+        if (!smode) {
+            if (tid < OWGS_RES_NHDR) hdr[tid] = ld_sys(A.ctl + OWGS_RES_HDR + tid);
             const uint4 v = ((const uint4*)A.in)[tid];  // (the block holds >= 4 KB: its capacity is larger)
             ((uint4*)stg)[tid] = v;
         }
@@ -260,7 +349,8 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
         const u64 seq_base = (u64)(uint32_t)hdr[4] | ((u64)(uint32_t)hdr[5] << 32);
         const uint32_t s_poff = (uint32_t)hdr[6], s_rel = (uint32_t)hdr[7], s_pub = (uint32_t)hdr[8],
                        s_seq = (uint32_t)hdr[9], s_in = (uint32_t)hdr[10];
-        const u64 rsum = (u64)(uint32_t)hdr[11] | ((u64)(uint32_t)hdr[12] << 32);  // memory the releases return at most
+        const long long s_first = hdr[13];  // (stream mode) the piece's first release / publish in the stream
+        u64 rsum = (u64)(uint32_t)hdr[11] | ((u64)(uint32_t)hdr[12] << 32);  // memory the releases return at most
         // LDS after the input block: each publish's walk cursor {generation, step}, then the outputs (mirrored by the
         // host's output block): out_inv i32[NP], out_flags u8[NP], rel_flags u8[NR]
         const uint32_t s_cur = (s_in + 15u) & ~15u, s_out = (s_cur + 8u * (uint32_t)NP + 15u) & ~15u;
@@ -274,7 +364,36 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
         uint4* pub = (uint4*)(stg + s_pub);
         u64* sq = (u64*)(stg + s_seq);
         uint2* pcur = (uint2*)(stg + s_cur);
-        if (sc[RS_BAIL] == 0) {
+        if (sc[RS_BAIL] == 0 && smode) {
+            // the piece's records from the stream in HBM: a release names an activation decided earlier in this
+            // launch (its invoker read through L2: written by wave 0's stores of an earlier piece), a publish an action
+            if (tid == 0) {
+                roff[0] = poff[0] = 0;
+                roff[1] = NR;
+                poff[1] = NP;
+            }
+            u64 rs = 0;
+            for (int j = tid; j < NR; j += 256) {
+                const long long aid = A.s_rel_aid[s_first + j];
+                const int inv = __hip_atomic_load(A.s_out_inv + aid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int a = A.s_act[aid];
+                const uint2 m = A.act_meta[a];
+                rel[j] = make_uint4((uint32_t)inv, m.y, (uint32_t)A.act_slot[a], 0u);
+                if (inv >= 0 && inv < n_slots) rs += (u64)(m.y & OWGS_AM_MEM_MASK);
+            }
+            for (int i = tid; i < NP; i += 256) {
+                const int a = A.s_act[s_first + i];
+                const uint2 m = A.act_meta[a];
+                pub[i] = make_uint4(m.x, m.y, (uint32_t)A.act_slot[a], (uint32_t)a);
+            }
+            if (rs) atomicAdd((u64*)&sc[RS_RSUM], rs);
+            __syncthreads();
+            rsum = *(const u64*)&sc[RS_RSUM];
+            for (int i = tid; i < NP; i += 256) {
+                const uint32_t a = pub[i].w;
+                pcur[i] = (A.cur && a < (uint32_t)A.n_actions) ? A.cur[a] : make_uint2(0u, 0u);
+            }
+        } else if (sc[RS_BAIL] == 0) {
             // the rest of a block beyond 4 KB, four 16-byte reads in flight per thread
             for (uint32_t o = 4096u + 16u * tid; o < s_in; o += 4u * 16u * 256u) {
                 uint4 v[4];
@@ -356,7 +475,11 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
             for (int r = 0; r < n_runs; ++r) {
                 // ---- completions of run r (releaseInvoker SCPB:327-331 via processCompletion CLB:260-346)
                 const int rb = roff[r], re = roff[r + 1];
-                if (re > rb) ++gen;  // permits may rise: every walk cursor of an earlier generation is stale
+                if (re > rb) {
+                    ++gen;  // permits may rise: every walk cursor of an earlier generation is stale
+                    if ((gen & 0x7FFFu) == 0u)  // the cache's generation field wraps: no entry may match again
+                        for (int i = lane; i < RES_CC; i += 64) cc[i] = make_uint2(0u, 0u);
+                }
                 const u64 tr0 = clock64();
                 for (int j0 = rb; j0 < re; j0 += 64) {
                     const int j = j0 + lane;
@@ -421,130 +544,16 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                     // gathered at staging, the LDS cache; a stale cursor of the same generation is still a lower bound)
                     const int l_mem = (int)(me.y & OWGS_AM_MEM_MASK);
                     const int l_pool = (me.x & OWGS_AM_POOL) ? 1 : 0;
-                    const bool l_plain = lane < nq && !(me.y & (OWGS_AM_EMPTY | OWGS_AM_THROW)) &&
-                                         ((me.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK) <= 1u &&
-                                         l_mem <= (l_pool ? U1 : U0);
+                    const bool l_c1 = lane < nq && !(me.y & (OWGS_AM_EMPTY | OWGS_AM_THROW)) &&
+                                      ((me.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK) <= 1u;
+                    const bool l_plain = l_c1 && l_mem <= (l_pool ? U1 : U0);
                     int l_sbeg = 0;
-                    {
-                        const uint32_t lch = (me.w * 2654435761u) >> (32 - 10);
-                        const uint2 lce = cc[lch];
-                        const int lcs = (int)cc[lch + RES_CC / 2].x;
-                        if (mycur.x == gen) l_sbeg = (int)mycur.y;
-                        if (lce.x == me.w + 1u && lce.y == gen) l_sbeg = max(l_sbeg, lcs);
-                    }
-                    for (int q = 0; q < nq; ++q) {
-                        // ---- up to 4 consecutive plain decisions walk together, 16 lanes each (4 probes per lane:
-                        // 64 walk steps per round), against the state before all of them; then in stream order each
-                        // is exact unless an earlier one of the group took the room at its target (permits only fall
-                        // inside a run, so every step a walk passed is still full).  The first one that is not exact,
-                        // and every fallback, goes to the single-decision path below.
-                        const u64 npm = ~(__ballot(l_plain) >> q);
-                        const int g = npm ? min(__builtin_ctzll(npm), 4) : 4;
-                        if (g >= 2) {
-                            const int grp = lane >> 4, u = lane & 15;
-                            const bool gact = grp < g;
-                            const int dq = q + (gact ? grp : 0);
-                            const uint32_t gmx = (uint32_t)__shfl((int)me.x, dq, 64);
-                            const int gmem = __shfl(l_mem, dq, 64), gsb = __shfl(l_sbeg, dq, 64);
-                            const int ghome = (int)(gmx & OWGS_AM_POS_MASK), gstep = (int)((gmx >> 15) & OWGS_AM_POS_MASK);
-                            const int gpool = (gmx & OWGS_AM_POOL) ? 1 : 0;
-                            const int gn = gpool ? nb : nm, gbase = gpool ? A.n_ids - nb : 0;
-                            const float grn = __builtin_amdgcn_rcpf((float)gn);
-                            int gp = mod_fast(ghome + (gsb + u) * gstep, gn, grn);
-                            const int gadv = mod_fast(16 * gstep, gn, grn);
-                            int gs = gsb, gt = -1, gts = gn, gpv = 0;
-                            bool gdone = !gact || gs >= gn;
-                            while (__ballot(!gdone)) {
-                                ++pr_rounds;
-                                int pk[4], vk[4];
-                                int pp = gp;
-#pragma unroll
-                                for (int k = 0; k < 4; ++k) {
-                                    pk[k] = pp;
-                                    vk[k] = P[gbase + pp];
-                                    pp += gadv;
-                                    pp -= pp >= gn ? gn : 0;
-                                }
-                                u64 B[4];
-#pragma unroll
-                                for (int k = 0; k < 4; ++k)
-                                    B[k] = __ballot(!gdone & (gs + 16 * k + u < gn) & (vk[k] >= gmem) & (vk[k] < OWGS_PLIM));
-                                int kf = 4, L = 0, sp = pk[0], sv = vk[0];
-#pragma unroll
-                                for (int k = 3; k >= 0; --k) {  // this group's first hit in walk order (k, then lane)
-                                    const uint32_t m = (uint32_t)(B[k] >> (16 * grp)) & 0xFFFFu;
-                                    if (m) {
-                                        kf = k;
-                                        L = __builtin_ctz(m);
-                                        sp = pk[k];
-                                        sv = vk[k];
-                                    }
-                                }
-                                const int src = (grp << 4) + L;
-                                const int hp = __shfl(sp, src, 64), hv = __shfl(sv, src, 64);
-                                if (!gdone) {
-                                    if (kf < 4) {
-                                        gt = gbase + hp;
-                                        gpv = hv;
-                                        gts = gs + 16 * kf + L;
-                                        gdone = true;
-                                    } else {
-                                        gs += 64;
-                                        gp = pp;
-                                        gdone = gs >= gn;  // every pool position probed: the walk failed
-                                    }
-                                }
-                            }
-                            // in stream order: accept while exact
-                            int ge = 0, at0 = -1, at1 = -1, at2 = -1, am0 = 0, am1 = 0, am2 = 0;
-#pragma unroll
-                            for (int k = 0; k < 4; ++k) {
-                                if (k >= g || ge < k) break;
-                                const int tk = __builtin_amdgcn_readlane(gt, 16 * k);
-                                const int pvk = __builtin_amdgcn_readlane(gpv, 16 * k);
-                                const int tsk = __builtin_amdgcn_readlane(gts, 16 * k);
-                                const int memk = __builtin_amdgcn_readlane(l_mem, q + k);
-                                const int ak = __builtin_amdgcn_readlane((int)me.w, q + k);
-                                const int pk_ = (__builtin_amdgcn_readlane((int)me.x, q + k) & OWGS_AM_POOL) ? 1 : 0;
-                                const uint32_t chk = ((uint32_t)ak * 2654435761u) >> (32 - 10);
-                                if (tk < 0) {  // no room anywhere for memk (then, so now): cursor past the pool, U below memk
-                                    const int nk = pk_ ? nb : nm;
-                                    if (lane == 0) {
-                                        cc[chk] = make_uint2((uint32_t)ak + 1u, gen);
-                                        cc[chk + RES_CC / 2].x = (uint32_t)nk;
-                                    }
-                                    if (pk_) U1 = min(U1, memk - 1);
-                                    else U0 = min(U0, memk - 1);
-                                    break;
-                                }
-                                int room = pvk;
-                                if (k > 0 && at0 == tk) room -= am0;
-                                if (k > 1 && at1 == tk) room -= am1;
-                                if (k > 2 && at2 == tk) room -= am2;
-                                if (room < memk) break;  // an earlier decision of the group took it: decide again
-                                if (k == 0) { at0 = tk; am0 = memk; }
-                                if (k == 1) { at1 = tk; am1 = memk; }
-                                if (k == 2) { at2 = tk; am2 = memk; }
-                                if (lane == 0) {
-                                    atomicSub(&P[tk], memk);  // tryAcquire (FS:63-71)
-                                    cc[chk] = make_uint2((uint32_t)ak + 1u, gen);
-                                    cc[chk + RES_CC / 2].x = (uint32_t)tsk;
-                                    if (A.cur) A.cur[ak] = make_uint2(gen, (uint32_t)tsk);
-                                }
-                                if (lane == q + k) {
-                                    o_v = tk;
-                                    o_f = 0;
-                                }
-                                ++ge;
-                            }
-                            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                            if (ge > 0) {
-                                pr_dec += ge;
-                                pr_grp += ge;
-                                q += ge - 1;
-                                continue;
-                            }
-                        }
+                    if (mycur.x == gen) l_sbeg = (int)mycur.y;
+                    l_sbeg = max(l_sbeg, cc_get(cc, me.w, gen));
+
+                    // one decision alone, exact against the state now: decision q of the chunk, its walk starting no
+                    // earlier than step smin (the steps before smin are known to have no room for it)
+                    auto decide_one = [&](int q, int smin) {
                         const uint32_t mx = (uint32_t)__builtin_amdgcn_readlane((int)me.x, q);
                         const uint32_t my = (uint32_t)__builtin_amdgcn_readlane((int)me.y, q);
                         const int slot = __builtin_amdgcn_readlane((int)me.z, q);
@@ -560,10 +569,8 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             const int maxc = (int)((my >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
                             const int n = pool ? nb : nm, base = pool ? A.n_ids - nb : 0;
                             const int a = __builtin_amdgcn_readlane((int)me.w, q);
-                            const uint32_t ch = ((uint32_t)a * 2654435761u) >> (32 - 10);  // RES_CC / 2 = 2^10 entries
                             int s_beg = 0;
                             if (maxc <= 1) {
-                                const uint2 ce = cc[ch];
                                 const uint32_t hg = (uint32_t)__builtin_amdgcn_readlane((int)mycur.x, q);
                                 const int hs = __builtin_amdgcn_readlane((int)mycur.y, q);
                                 if (mem > (pool ? U1 : U0)) {
@@ -571,12 +578,13 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                     ++pr_u;
                                 } else {
                                     if (hg == gen) s_beg = hs;
-                                    if (ce.x == (uint32_t)a + 1u && ce.y == gen) s_beg = max(s_beg, (int)cc[ch + RES_CC / 2].x);
+                                    s_beg = max(s_beg, cc_get(cc, (uint32_t)a, gen));
                                     pr_hit += s_beg > 0;
+                                    s_beg = max(s_beg, smin);
                                 }
                             }
                             const float rn = __builtin_amdgcn_rcpf((float)n);
-                            int p = mod_fast(home + (s_beg + lane) * step, n, rn);
+                            int p = mod_fast(home + (min(s_beg, n - 1) + lane) * step, n, rn);
                             const int adv = mod_fast(64 * step, n, rn);
                             int t = -1, tix = -1, tp = 0, ts = n;  // target, its map entry, its permits, its walk step
                             uint32_t tv = 0u;
@@ -617,23 +625,18 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 const bool valid = s0 + lane < n;
                                 const int id = base + p;
                                 const int pv = valid ? P[id] : OWGS_PENC;
-                                bool ok;
+                                bool ok = false;
                                 int ix = -1;
                                 uint32_t v = 0u;
-                                if (maxc <= 1) {
-                                    ok = pv >= mem && pv < OWGS_PLIM;  // usable (folded) and tryAcquire (FS:63-71)
-                                } else {
-                                    ok = false;
-                                    if (pv < OWGS_PLIM) {  // usable: a free slot of the key's container, or memory
-                                        const uint32_t key = ct_key(id, slot);
-                                        ix = ct_lookup(ct, key, &v);
-                                        if (ix < 0 && ovf_on) {  // (an HBM round trip: counted)
-                                            ++pr_ovf;
-                                            const int oj = ovf_find(A.ovf, key, &v);
-                                            ix = oj >= 0 ? OWGS_CTC + oj : -1;
-                                        }
-                                        ok = (v & OWGS_CT_C_MASK) != 0u || pv >= mem;
+                                if (pv < OWGS_PLIM) {  // usable: a free slot of the key's container, or memory
+                                    const uint32_t key = ct_key(id, slot);
+                                    ix = ct_lookup(ct, key, &v);
+                                    if (ix < 0 && ovf_on) {  // (an HBM round trip: counted)
+                                        ++pr_ovf;
+                                        const int oj = ovf_find(A.ovf, key, &v);
+                                        ix = oj >= 0 ? OWGS_CTC + oj : -1;
                                     }
+                                    ok = (v & OWGS_CT_C_MASK) != 0u || pv >= mem;
                                 }
                                 const u64 m = __ballot(ok);
                                 if (m) {
@@ -649,8 +652,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 p -= p >= n ? n : 0;
                             }
                             if (maxc <= 1 && lane == 0) {  // the walk's steps before ts had no room for mem
-                                cc[ch] = make_uint2((uint32_t)a + 1u, gen);
-                                cc[ch + RES_CC / 2].x = (uint32_t)ts;
+                                cc_put(cc, (uint32_t)a, gen, ts);
                                 if (A.cur) A.cur[a] = make_uint2(gen, (uint32_t)ts);
                             }
                             if (maxc <= 1 && t < 0) {  // a failed walk: no usable permit count reaches mem
@@ -706,8 +708,355 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             o_v = x;
                             o_f = fl;
                         }
-                        ++pr_dec;
+                    };
+
+                    if (A.spec > 0) {
+                        // ---- speculation: every maxConcurrent == 1 decision walks on its own against the state at
+                        // the chunk's start, A.spec steps at most (4 permit reads in flight per round).  Permits only
+                        // fall inside a run (releases come first, SCPB:327-331 via CLB:260-346), so a step full then is
+                        // full at the decision's turn: the walk's target stays the decision's unless the decisions
+                        // before it took the room there, and a walk that found no room anywhere is a fallback whatever
+                        // came before (SCPB:417-424).
+                        int sp = lane < nq ? SP_STOP : SP_NONE;
+                        int sp_t = -1, sp_ts = 0;  // target, its walk step (SP_FOUND, SP_FORCED), or the step to resume
+                        if (lane < nq && (me.y & (OWGS_AM_EMPTY | OWGS_AM_THROW))) {
+                            sp = SP_TRIV;  // None (SCPB:288-290) or the Int.MinValue throw (SCPB:266-268)
+                            o_v = (me.y & OWGS_AM_EMPTY) ? OWGS_NONE_V : OWGS_THROW_V;
+                        }
+                        const int l_n = l_pool ? nb : nm, l_base = l_pool ? A.n_ids - nb : 0;
+                        const int l_home = (int)(me.x & OWGS_AM_POS_MASK), l_step = (int)((me.x >> 15) & OWGS_AM_POS_MASK);
+                        // repeats of one action in the chunk share its walk: the k-th (rank k among the chunk's plain
+                        // decisions of that action) passes over the room the k before it take, so it walks to the step
+                        // where the capacity for its memory met so far, sum of floor(permits / mem), exceeds k
+                        int need = 0;
+                        {
+                            const int abits = 32 - __clz(max(A.n_actions - 1, 1));
+                            u64 same = __ballot(l_plain);
+                            for (int b = 0; b < abits; ++b) {
+                                const bool bit = (me.w >> b) & 1u;
+                                const u64 m = __ballot(l_plain && bit);
+                                same &= bit ? m : ~m;
+                            }
+                            need = l_plain ? (int)__popcll(same & ((1ull << lane) - 1ull)) : 0;
+                        }
+                        const int rank = need;
+                        const float rmem = __builtin_amdgcn_rcpf((float)max(l_mem, 1));
+                        bool walking = false;
+                        int wp = 0, ws = l_sbeg;
+                        if (l_c1) {
+                            if (!l_plain || l_sbeg >= l_n) {
+                                sp = SP_FAIL;  // mem above the pool's bound U, or a cursor past every step
+                            } else {
+                                walking = true;
+                                wp = mod_fast(l_home + ws * l_step, l_n, __builtin_amdgcn_rcpf((float)l_n));
+                            }
+                        }
+                        for (int it = 0; __ballot(walking); it += 4) {
+                            if (walking) {
+                                int pk[4], vk[4];
+                                int pp = wp;
+#pragma unroll
+                                for (int k = 0; k < 4; ++k) {
+                                    pk[k] = pp;
+                                    vk[k] = P[l_base + pp];
+                                    pp += l_step;
+                                    pp -= pp >= l_n ? l_n : 0;
+                                }
+                                int kf = 4;
+#pragma unroll
+                                for (int k = 0; k < 4; ++k) {
+                                    const int v = vk[k];
+                                    if (kf == 4 && ws + k < l_n && v >= l_mem && v < OWGS_PLIM) {
+                                        if (v >= (need + 1) * l_mem) {
+                                            kf = k;
+                                        } else {  // room for 1..need activations here (v < 64 mem: exact after correction)
+                                            int c = (int)((float)v * rmem);
+                                            c -= c * l_mem > v ? 1 : 0;
+                                            c += (c + 1) * l_mem <= v ? 1 : 0;
+                                            need -= c;
+                                        }
+                                    }
+                                }
+                                if (kf < 4) {
+                                    sp = SP_FOUND;
+                                    sp_t = l_base + (kf == 0 ? pk[0] : kf == 1 ? pk[1] : kf == 2 ? pk[2] : pk[3]);
+                                    sp_ts = ws + kf;
+                                    walking = false;
+                                } else {
+                                    ws += 4;
+                                    wp = pp;
+                                    if (ws >= l_n) {
+                                        sp = SP_FAIL;  // every pool position probed
+                                        walking = false;
+                                    } else if (it + 4 >= A.spec) {
+                                        sp = SP_STOP;  // the rest of the walk: one at a time, from ws
+                                        sp_ts = ws;
+                                        walking = false;
+                                    }
+                                }
+                            }
+                        }
+                        pr_rounds += (uint32_t)__popcll(__ballot(l_c1 && l_plain));
+                        // concurrent decisions (maxConcurrent > 1): the first of each fqn@version key in the chunk walks
+                        // too; a step takes it when the invoker is usable and the key's container there has a free slot
+                        // or the invoker has the memory (tryAcquireConcurrent, NS:57-82).  Only decisions of the same key
+                        // change its map entries, so the walk and the entry it found hold at its turn, unless the
+                        // decisions before took the memory it needs; a repeat of a key in the chunk is decided alone
+                        const int l_maxc = (int)((me.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
+                        const bool l_cc = lane < nq && !(me.y & (OWGS_AM_EMPTY | OWGS_AM_THROW)) && l_maxc > 1;
+                        int c_ix = -1;       // the target's map entry (primary index, OWGS_CTC + overflow index, -1 none)
+                        uint32_t c_v = 0u;   // and its value at the chunk's start
+                        if (__ballot(l_cc)) {
+                            u64 same = __ballot(l_cc);
+                            for (int b = 0; b < 17; ++b) {
+                                const bool bit = (me.z >> b) & 1u;
+                                const u64 m = __ballot(l_cc && bit);
+                                same &= bit ? m : ~m;
+                            }
+                            bool cw = l_cc && (same & ((1ull << lane) - 1ull)) == 0ull;
+                            int cpos = cw ? mod_fast(l_home, l_n, __builtin_amdgcn_rcpf((float)l_n)) : 0, cst = 0;
+                            while (__ballot(cw)) {
+                                if (cw) {
+                                    const int id = l_base + cpos;
+                                    const int pv = P[id];
+                                    bool ok = false;
+                                    int ix = -1;
+                                    uint32_t v = 0u;
+                                    if (pv < OWGS_PLIM) {
+                                        const uint32_t key = ct_key(id, (int)me.z);
+                                        ix = ct_lookup(ct, key, &v);
+                                        if (ix < 0 && ovf_on) {
+                                            ++pr_ovf;
+                                            const int oj = ovf_find(A.ovf, key, &v);
+                                            ix = oj >= 0 ? OWGS_CTC + oj : -1;
+                                        }
+                                        ok = (v & OWGS_CT_C_MASK) != 0u || pv >= l_mem;
+                                    }
+                                    if (ok) {
+                                        sp = SP_FOUND;
+                                        sp_t = id;
+                                        c_ix = ix;
+                                        c_v = v;
+                                        cw = false;
+                                    } else if (++cst >= l_n) {
+                                        sp = SP_FAIL;  // every pool position: forced below
+                                        cw = false;
+                                    } else if (cst >= A.spec) {
+                                        cw = false;    // SP_STOP: decided alone
+                                    } else {
+                                        cpos += l_step;
+                                        cpos -= cpos >= l_n ? l_n : 0;
+                                    }
+                                }
+                            }
+                        }
+                        // a failed walk bounds the pool's usable permits below its memory (U), and the fallback's
+                        // healthy invoker depends on the sequence number alone: forced now, committed in order below
+                        if (sp == SP_FAIL) {
+                            const int Hn = l_pool ? hb_e : hm_e;
+                            if (Hn > 0) {
+                                const int kk = (int)rng_index(A.rng_seed, myseq, (uint32_t)Hn);
+                                sp_t = (l_pool ? full_b : full_m) ? l_base + kk : select_usable(l_base, kk);
+                                sp = sp_t >= 0 ? SP_FORCED : SP_TRIV;
+                                o_v = OWGS_NONE_V;
+                                o_f = 1;
+                                if (sp_t < 0) err |= OWGS_ERR_INTERNAL;
+                                else if (l_cc)  // forceAcquireConcurrent: a free slot of the key's container there, or memory
+                                    c_ix = ct_lookup2(ct, A.ovf, ovf_on, ct_key(sp_t, (int)me.z), &c_v);
+                            } else {
+                                sp = SP_TRIV;  // no healthy invoker: None
+                                o_v = OWGS_NONE_V;
+                            }
+                            sp_ts = l_n;
+                        }
+                        // (a repeat's outcome holds once the repeats before it are decided, so only the first of
+                        // each action proves anything about the state at the chunk's start: the bound U, the cursor)
+                        {
+                            const bool fl0 = l_c1 && rank == 0 && (sp == SP_FORCED || sp == SP_TRIV);
+                            U0 = min(U0, wave_min_i(fl0 && !l_pool ? l_mem - 1 : 0x7FFFFFFF));
+                            U1 = min(U1, wave_min_i(fl0 && l_pool ? l_mem - 1 : 0x7FFFFFFF));
+                        }
+                        // every first walk's cursor (the steps before it had no room then, so none now)
+                        if (l_c1 && rank == 0) {
+                            const int cs = sp == SP_FOUND ? sp_ts : sp == SP_STOP ? sp_ts : l_n;
+                            cc_put(cc, me.w, gen, cs);
+                            if (A.cur) A.cur[me.w] = make_uint2(gen, (uint32_t)cs);
+                        }
+                        mv[lane] = l_mem;
+                        const int tbits = 32 - __clz(max(A.n_ids - 1, 1));
+                        // ---- in stream order: the longest prefix whose speculative targets still hold commits at
+                        // once; the first one that does not (or a concurrent decision, or an unfinished walk) is decided
+                        // alone, then the next prefix
+                        const bool c_slot = l_cc && (c_v & OWGS_CT_C_MASK) != 0u;  // takes a free slot, no memory
+                        for (int q = 0;;) {
+                            const bool cand = lane >= q && (sp == SP_FOUND || sp == SP_FORCED);
+                            const bool take = cand && !c_slot;
+                            // the memory taken at my target by the candidates before me (same target: all bits agree)
+                            u64 eq = __ballot(take);
+                            for (int b = 0; b < tbits; ++b) {
+                                const bool bit = (sp_t >> b) & 1;
+                                const u64 m = __ballot(take && bit);
+                                eq &= bit ? m : ~m;
+                            }
+                            eq &= (1ull << lane) - 1ull;
+                            int S = 0;
+                            if (take)
+                                while (eq) {
+                                    S += mv[ffs64(eq)];
+                                    eq &= eq - 1ull;
+                                }
+                            const int room = take ? P[sp_t] : 0;
+                            const bool ok = lane < q || sp == SP_NONE || sp == SP_TRIV || sp == SP_FORCED ||
+                                            (sp == SP_FOUND && (c_slot || room - S >= l_mem));
+                            const u64 bad = __ballot(!ok);
+                            const int f = bad ? ffs64(bad) : 64;
+                            uint32_t nv = 0u;
+                            if (cand && lane < f) {
+                                if (take) {
+                                    atomicSub(&P[sp_t], l_mem);  // tryAcquire (FS:63-71) / forceAcquire (FS:102-110)
+                                    if (room - S - l_mem < -OWGS_PLIM) err |= OWGS_ERR_PERMITS;
+                                }
+                                if (l_cc) {  // the key's container at the target: a slot taken, or a new one (NS:63-79)
+                                    const int c0 = c_ix >= 0 ? (int)(c_v & OWGS_CT_C_MASK) : 0;
+                                    const int o0 = c_ix >= 0 ? ct_ops(c_v) : 0;
+                                    const int c1 = c_slot ? c0 - 1 : l_maxc - 1, o1 = o0 + 1;
+                                    if (o1 > OWGS_MAX_OPS) err |= OWGS_ERR_OPS;
+                                    nv = ct_val(c1, o1);
+                                    if (c_ix >= 0 && c_ix < OWGS_CTC) ct[c_ix].y = nv;
+                                    else if (c_ix >= OWGS_CTC) ovf_st_val(A.ovf.t, c_ix - OWGS_CTC, nv);
+                                }
+                                o_v = sp_t;
+                                o_f = sp == SP_FORCED ? 1 : 0;
+                            }
+                            // new (invoker, fqn) entries, one at a time in stream order (lane 0 inserts)
+                            for (u64 ins = __ballot(cand && lane < f && l_cc && c_ix < 0); ins; ins &= ins - 1ull) {
+                                const int j = ffs64(ins);
+                                const uint32_t key = ct_key(__builtin_amdgcn_readlane(sp_t, j),
+                                                            __builtin_amdgcn_readlane((int)me.z, j));
+                                const uint32_t nvj = (uint32_t)__builtin_amdgcn_readlane((int)nv, j);
+                                if (lane == 0) insert(key, nvj);
+                                used = __builtin_amdgcn_readfirstlane(used);
+                                ovf_on = __builtin_amdgcn_readfirstlane((int)ovf_on) != 0;
+                                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                            }
+                            pr_grp += (uint32_t)__popcll(__ballot(cand && lane < f));
+                            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                            if (f >= nq) break;
+                            decide_one(f, __builtin_amdgcn_readlane(sp_ts, f));
+                            q = f + 1;
+                        }
+                    } else {
+                        for (int q = 0; q < nq; ++q) {
+                            // ---- up to 4 consecutive plain decisions walk together, 16 lanes each (4 probes per lane:
+                            // 64 walk steps per round), against the state before all of them; then in stream order
+                            // each is exact unless an earlier one of the group took the room at its target (permits
+                            // only fall inside a run, so every step a walk passed is still full).  The first one that
+                            // is not exact, and every fallback, goes to the single-decision path.
+                            const u64 npm = ~(__ballot(l_plain) >> q);
+                            const int g = npm ? min(__builtin_ctzll(npm), 4) : 4;
+                            if (g >= 2) {
+                                const int grp = lane >> 4, u = lane & 15;
+                                const bool gact = grp < g;
+                                const int dq = q + (gact ? grp : 0);
+                                const uint32_t gmx = (uint32_t)__shfl((int)me.x, dq, 64);
+                                const int gmem = __shfl(l_mem, dq, 64), gsb = __shfl(l_sbeg, dq, 64);
+                                const int ghome = (int)(gmx & OWGS_AM_POS_MASK), gstep = (int)((gmx >> 15) & OWGS_AM_POS_MASK);
+                                const int gpool = (gmx & OWGS_AM_POOL) ? 1 : 0;
+                                const int gn = gpool ? nb : nm, gbase = gpool ? A.n_ids - nb : 0;
+                                const float grn = __builtin_amdgcn_rcpf((float)gn);
+                                int gp = mod_fast(ghome + (gsb + u) * gstep, gn, grn);
+                                const int gadv = mod_fast(16 * gstep, gn, grn);
+                                int gs = gsb, gt = -1, gts = gn, gpv = 0;
+                                bool gdone = !gact || gs >= gn;
+                                while (__ballot(!gdone)) {
+                                    ++pr_rounds;
+                                    int pk[4], vk[4];
+                                    int pp = gp;
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k) {
+                                        pk[k] = pp;
+                                        vk[k] = P[gbase + pp];
+                                        pp += gadv;
+                                        pp -= pp >= gn ? gn : 0;
+                                    }
+                                    u64 B[4];
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k)
+                                        B[k] = __ballot(!gdone & (gs + 16 * k + u < gn) & (vk[k] >= gmem) & (vk[k] < OWGS_PLIM));
+                                    int kf = 4, L = 0, sp = pk[0], sv = vk[0];
+#pragma unroll
+                                    for (int k = 3; k >= 0; --k) {  // this group's first hit in walk order (k, then lane)
+                                        const uint32_t m = (uint32_t)(B[k] >> (16 * grp)) & 0xFFFFu;
+                                        if (m) {
+                                            kf = k;
+                                            L = __builtin_ctz(m);
+                                            sp = pk[k];
+                                            sv = vk[k];
+                                        }
+                                    }
+                                    const int src = (grp << 4) + L;
+                                    const int hp = __shfl(sp, src, 64), hv = __shfl(sv, src, 64);
+                                    if (!gdone) {
+                                        if (kf < 4) {
+                                            gt = gbase + hp;
+                                            gpv = hv;
+                                            gts = gs + 16 * kf + L;
+                                            gdone = true;
+                                        } else {
+                                            gs += 64;
+                                            gp = pp;
+                                            gdone = gs >= gn;  // every pool position probed: the walk failed
+                                        }
+                                    }
+                                }
+                                // in stream order: accept while exact
+                                int ge = 0, at0 = -1, at1 = -1, at2 = -1, am0 = 0, am1 = 0, am2 = 0;
+#pragma unroll
+                                for (int k = 0; k < 4; ++k) {
+                                    if (k >= g || ge < k) break;
+                                    const int tk = __builtin_amdgcn_readlane(gt, 16 * k);
+                                    const int pvk = __builtin_amdgcn_readlane(gpv, 16 * k);
+                                    const int tsk = __builtin_amdgcn_readlane(gts, 16 * k);
+                                    const int memk = __builtin_amdgcn_readlane(l_mem, q + k);
+                                    const int ak = __builtin_amdgcn_readlane((int)me.w, q + k);
+                                    const int pk_ = (__builtin_amdgcn_readlane((int)me.x, q + k) & OWGS_AM_POOL) ? 1 : 0;
+                                    if (tk < 0) {  // no room anywhere for memk (then, so now): cursor past the pool, U below memk
+                                        const int nk = pk_ ? nb : nm;
+                                        if (lane == 0) cc_put(cc, (uint32_t)ak, gen, nk);
+                                        if (pk_) U1 = min(U1, memk - 1);
+                                        else U0 = min(U0, memk - 1);
+                                        break;
+                                    }
+                                    int room = pvk;
+                                    if (k > 0 && at0 == tk) room -= am0;
+                                    if (k > 1 && at1 == tk) room -= am1;
+                                    if (k > 2 && at2 == tk) room -= am2;
+                                    if (room < memk) break;  // an earlier decision of the group took it: decide again
+                                    if (k == 0) { at0 = tk; am0 = memk; }
+                                    if (k == 1) { at1 = tk; am1 = memk; }
+                                    if (k == 2) { at2 = tk; am2 = memk; }
+                                    if (lane == 0) {
+                                        atomicSub(&P[tk], memk);  // tryAcquire (FS:63-71)
+                                        cc_put(cc, (uint32_t)ak, gen, tsk);
+                                        if (A.cur) A.cur[ak] = make_uint2(gen, (uint32_t)tsk);
+                                    }
+                                    if (lane == q + k) {
+                                        o_v = tk;
+                                        o_f = 0;
+                                    }
+                                    ++ge;
+                                }
+                                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                                if (ge > 0) {
+                                    pr_grp += ge;
+                                    q += ge - 1;
+                                    continue;
+                                }
+                            }
+                            decide_one(q, 0);
+                        }
                     }
+                    pr_dec += nq;
                     if (lane < nq) {
                         out_inv[i0 + lane] = o_v;
                         out_fl[i0 + lane] = (uint8_t)o_f;
@@ -722,7 +1071,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
             for (int d = 32; d >= 1; d >>= 1) pr_ovf += __shfl_xor(pr_ovf, d, 64);
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) tombs += __shfl_xor(tombs, d, 64);
-            if (lane == 0) {
+            if (lane == 0 && !smode) {
                 int32_t* pr = A.ctl + OWGS_RES_PROF;
                 st_sys(pr + 0, (int)pr_rounds);
                 st_sys(pr + 1, (int)pr_dec);
@@ -734,6 +1083,18 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 st_sys(pr + 7, (int)pr_u);
                 st_sys(pr + 8, (int)pr_grp);
                 st_sys(&A.ctl[OWGS_RES_GEN], (int)gen);
+            } else if (lane == 0 && A.s_stats) {  // stream mode: summed over the launch (owgs_resident_stats' order)
+                A.s_stats[0] += pr_rounds;
+                A.s_stats[1] += pr_dec;
+                A.s_stats[2] += pr_stage;
+                A.s_stats[3] += pr_rel;
+                A.s_stats[4] += pr_pub;
+                A.s_stats[5] += (uint32_t)pr_ovf;
+                A.s_stats[6] += pr_hit;
+                A.s_stats[7] += pr_u;
+                A.s_stats[8] += pr_grp;
+            }
+            if (lane == 0) {
                 sc[RS_USED] = used;
                 sc[RS_TOMB] += tombs;
                 sc[RS_U0] = U0;
@@ -781,6 +1142,26 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 __syncthreads();
             }
         }
+        if (smode) {  // ---- stream mode: the outputs into the stream's arrays; an error or a refusal ends the replay
+            if (bail == 0) {
+                const int32_t* oi = (const int32_t*)(stg + s_out);
+                for (int i = tid; i < NP; i += 256) {
+                    A.s_out_inv[s_first + i] = oi[i];
+                    A.s_out_fl[s_first + i] = (uint8_t)stg[s_ofl + i];
+                }
+                if (A.s_rel_fl)
+                    for (int j = tid; j < NR; j += 256) A.s_rel_fl[s_first + j] = (uint8_t)stg[s_orf + j];
+            }
+            __threadfence();  // (the next piece's releases read these decisions through L2)
+            __syncthreads();
+            const int e = sc[RS_ERR] | (bail ? OWGS_ERR_RELRISK : 0);
+            __syncthreads();
+            if (e) {
+                if (tid == 0) atomicOr(A.err, e);
+                break;
+            }
+            continue;
+        }
         // ---- answer: the outputs to host memory (16-byte stores), then the result and the done word
         if (bail == 0) {
             for (uint32_t o = 16u * tid; o < s_end - s_out; o += 16u * 256u)
@@ -815,7 +1196,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
     if (tid == 0 && A.ovf.cap > 0) __hip_atomic_store(A.ovf.cnt, sc[RS_OVF], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __threadfence();
     __syncthreads();
-    if (tid == 0) {
+    if (tid == 0 && !smode) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         st_sys(&A.ctl[OWGS_RES_STATE], 2);
     }

@@ -210,3 +210,61 @@ def test_resident_refuses_releases_beyond_the_permit_range():
     st = g.resident_stats()
     assert st["refused"] == 1 and st["chained"] == 1, st
     assert g.permits().tolist() == o.permits().tolist()
+
+
+def _hot_small_pool(seed=11, n_activations=20_000):
+    """A few invokers near full, a handful of hot actions (Zipf 1.5), 40 % concurrent ones with small
+    maxConcurrent: repeats of one action in a chunk, clashes at one invoker and walks past the speculation's budget are
+    the common case, not the exception."""
+    return W.generate(name="hot", n_invokers=24, user_memory_mb=2048, n_actions=30, n_namespaces=5, zipf_s=1.5,
+                      conc_frac=0.4, conc_range=(2, 4), blackbox_frac=0.2, unhealthy_frac=0.1, shared_frac=0.3,
+                      n_activations=n_activations, load=1.05, delay_mean=3.0, seed=seed)
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_resident_speculation_on_hot_small_pools(seed):
+    """The resident engine's speculative walks (every decision of a chunk walks against the state at the chunk's
+    start; in stream order the prefix whose targets still hold commits at once, repeats of one action take the room
+    the earlier ones leave, the first decision that does not hold is decided alone) on the hardest inputs for it:
+    bit-exact with the oracle call by call."""
+    w = _hot_small_pool(seed)
+    sh = Shim(w)
+    rng = np.random.default_rng(seed)
+    while not sh.done():
+        sh.call(int(rng.integers(1, 300)))
+    st = sh.g.resident_stats()
+    assert st["served"] == sh.calls and st["chained"] == 0, st
+    assert st["grouped_decisions"] > 0, st  # decisions committed from speculation
+    assert np.array_equal(sh.g.permits(), sh.o.permits())
+
+
+_BUDGET_SCRIPT = r"""
+import sys
+sys.path[:0] = [{root!r}, {oracle!r}, {tests!r}]
+import numpy as np
+import test_gpu_resident as T
+for seed in (11, 12):
+    w = T._hot_small_pool(seed, n_activations=8_000)
+    sh = T.Shim(w)
+    rng = np.random.default_rng(seed)
+    while not sh.done():
+        sh.call(int(rng.integers(1, 200)))
+    assert np.array_equal(sh.g.permits(), sh.o.permits())
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("budget", ["0", "1", "4"])
+def test_resident_speculation_budgets(budget):
+    """Walk budgets of 0 (no speculation: decisions one at a time), 1 and 4 steps (most walks unfinished: decided
+    alone from where the speculation stopped) give the same decisions (OWGS_RES_SPEC is read once per process, so each
+    budget runs in a child process)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    code = _BUDGET_SCRIPT.format(root=root, oracle=os.path.join(root, "oracle"), tests=here)
+    env = dict(os.environ, OWGS_RES_SPEC=budget)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

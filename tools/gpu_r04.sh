@@ -44,6 +44,19 @@ for s in ${STEPS:-tests smoke}; do
     bench)
       timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
       rc=$?; cut -c1-400 $O/bench.json; [ $rc -eq 0 ] || { tail -20 $O/bench.err; stop bench $rc; } ;;
+    spectests)  # the parity suite (full-size streams included) with the replay path as the environment sets it
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_resident.py -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest_parity.log 2>&1
+      rc=$?; tail -2 $O/pytest_parity.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error|error|assert" $O/pytest_parity.log | head -30; stop spectests $rc; } ;;
+    vtests)  # the resident engine's tests under each variant library in $V (openwhisk_amd/variants/libowgs_<v>.so)
+      for v in $V; do
+        OWGS_LIB=openwhisk_amd/variants/libowgs_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_resident.py tests/test_gpu_shim_sequence.py -x -v --timeout 120 --timeout-method thread > $O/pytest_v_$v.log 2>&1
+        rc=$?; echo "== $v"; tail -2 $O/pytest_v_$v.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error|error|assert" $O/pytest_v_$v.log | head -30; stop vtests $rc; }
+      done ;;
+    vshim)  # the shim leg under each variant library in $V
+      for v in $V; do
+        OWGS_LIB=openwhisk_amd/variants/libowgs_$v.so timeout -k 10 300 python tools/shim_leg.py --drains 64,512 > $O/shim_v_$v.json 2> $O/shim_v_$v.err
+        rc=$?; echo "== $v"; cut -c1-1500 $O/shim_v_$v.json; [ $rc -eq 0 ] || { tail -5 $O/shim_v_$v.err; stop vshim $rc; }
+      done ;;
     benchprof)  # kernel stats of the default bench command (profiles/r04_kernel_stats.csv)
       rm -rf $O/benchprof
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/benchprof -o run --output-format csv -- \
