@@ -502,7 +502,8 @@ def main():
     wall = time.perf_counter() - t0
     gathers_per_step = n_gathers[0] / max(args.steps, 1)
     replay_ms = float(np.mean([a.elapsed_time(c) for a, c in evs]))
-    stats = b.stats()
+    smode = b.stream_mode_stats()  # the replay ran through the resident engine's stream mode (OWGS_SPEC_REPLAY)
+    stats = smode if smode is not None else b.stats()
     # the dominant kernel alone: HIP events the library records around each engine launch on the replay stream,
     # read after instrumented replays outside the timed region (reading them inside would add a sync per step)
     eng = []
@@ -598,7 +599,8 @@ def main():
                          "traffic_source": pmc["source"] if pmc else f"no --pmc pass recorded for this build ({key})",
                          # what limits this kernel instead: one CU's instruction issue along the decision chain
                          "issue": pmc.get("issue") if pmc else None,
-                         "kernel": "owgs_engine_kernel" if K == 1 else "owgs_engine_multi_kernel",
+                         "kernel": ("owgs_resident_kernel" if smode is not None else
+                                    "owgs_engine_kernel" if K == 1 else "owgs_engine_multi_kernel"),
                          "kernel_ms": kern_ms, "replay_ms": replay_ms, "shards_per_launch": per_launch,
                          "algorithmic_bytes": algo["survey"] * per_launch,
                          "algorithmic_def": f"SURVEY 8(d): {B_DECISION} B/decision + {B_RELEASE} B/release",

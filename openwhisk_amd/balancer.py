@@ -68,7 +68,9 @@ def _blob(items) -> tuple[np.ndarray, np.ndarray]:
 
 
 _RES_PROF = ("walk_rounds", "decisions", "stage_cycles", "release_cycles", "publish_cycles", "overflow_lookups",
-             "cursor_walks", "bound_skips", "grouped_decisions")
+             "cursor_walks", "bound_skips", "grouped_decisions", "validation_passes", "decided_alone",
+             "alone_cycles")
+_NRP = len(_RES_PROF)
 
 
 class GpuShardingContainerPoolBalancer:
@@ -231,8 +233,8 @@ class GpuShardingContainerPoolBalancer:
     def resident_stats(self) -> dict:
         """owgs_process_batch's paths: calls the resident engine served, its launches, calls it refused untouched,
         calls the launch chain took, and whether a resident engine is live."""
-        out = np.zeros(15, np.int64)
-        n = self._L.owgs_resident_stats(self._h, _p(out), 15)
+        out = np.zeros(6 + _NRP, np.int64)
+        n = self._L.owgs_resident_stats(self._h, _p(out), 6 + _NRP)
         if n < 0:
             self._chk(n)
         return dict(zip(("served", "launches", "refused", "chained", "alive") + _RES_PROF + ("last_call_ns",),
@@ -240,15 +242,15 @@ class GpuShardingContainerPoolBalancer:
 
     def stream_mode_stats(self) -> dict | None:
         """The last replay's resident-engine counters when it ran in stream mode (OWGS_SPEC_REPLAY), else None."""
-        out = np.zeros(25, np.int64)
-        self._chk(min(0, self._L.owgs_resident_stats(self._h, _p(out), 25)))
-        return dict(zip(_RES_PROF, (int(x) for x in out[16:25]))) if out[15] else None
+        out = np.zeros(7 + 2 * _NRP, np.int64)
+        self._chk(min(0, self._L.owgs_resident_stats(self._h, _p(out), 7 + 2 * _NRP)))
+        return dict(zip(_RES_PROF, (int(x) for x in out[7 + _NRP:]))) if out[6 + _NRP] else None
 
     def last_call_ns(self) -> int:
         """Duration of the last publish / release / process_batch call, timed inside the library (no ctypes cost)."""
-        out = np.zeros(15, np.int64)
-        self._L.owgs_resident_stats(self._h, _p(out), 15)
-        return int(out[14])
+        out = np.zeros(6 + _NRP, np.int64)
+        self._L.owgs_resident_stats(self._h, _p(out), 6 + _NRP)
+        return int(out[5 + _NRP])
 
     def set_health_tid(self, start_ms: int):
         """TransactionId.invokerHealth's start time (TransactionId.scala:225): health acks echo it."""

@@ -314,7 +314,7 @@ struct OwgsReleaseArgs {
 #define OWGS_RES_PROF 96    // device: the last call's counters (OWGS_RES_NPROF words: walk rounds, decisions,
                             // staging / release / publish cycles, overflow lookups, cursor hits, U shortcuts,
                             // decisions of the grouped walks)
-#define OWGS_RES_NPROF 9
+#define OWGS_RES_NPROF 12  // (+ validation passes, decisions decided alone, their cycles)
 #define OWGS_RES_HDR 64     // host: the call -- n_runs, n_rel, n_pub, has_seq, seq_base lo, hi, then byte offsets in
                             // the input block of pub_off, the release records, the publish records, seq (u64), the
                             // block's length, and the memory the releases return at most (lo, hi).  The block:

@@ -438,7 +438,8 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
             // still fit (a cache keyed by action, valid while no release raised a permit: generation = release runs)
             int U0 = sc[RS_U0], U1 = sc[RS_U1];
             uint32_t gen = (uint32_t)sc[RS_GEN];
-            uint32_t pr_rounds = 0, pr_dec = 0, pr_ovf = 0, pr_hit = 0, pr_u = 0, pr_grp = 0;
+            uint32_t pr_rounds = 0, pr_dec = 0, pr_ovf = 0, pr_hit = 0, pr_u = 0, pr_grp = 0, pr_pass = 0, pr_alone = 0;
+            u64 pr_alone_cyc = 0;
             const u64 pr_stage = clock64() - t_call;  // header, staging and the range check
             u64 pr_rel = 0, pr_pub = 0;
             int32_t* out_inv = (int32_t*)(stg + s_out);  // (LDS; copied to host memory after the call)
@@ -554,6 +555,8 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                     // one decision alone, exact against the state now: decision q of the chunk, its walk starting no
                     // earlier than step smin (the steps before smin are known to have no room for it)
                     auto decide_one = [&](int q, int smin) {
+                        const u64 ta0 = clock64();
+                        ++pr_alone;
                         const uint32_t mx = (uint32_t)__builtin_amdgcn_readlane((int)me.x, q);
                         const uint32_t my = (uint32_t)__builtin_amdgcn_readlane((int)me.y, q);
                         const int slot = __builtin_amdgcn_readlane((int)me.z, q);
@@ -708,6 +711,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             o_v = x;
                             o_f = fl;
                         }
+                        pr_alone_cyc += clock64() - ta0;
                     };
 
                     if (A.spec > 0) {
@@ -797,15 +801,18 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             }
                         }
                         pr_rounds += (uint32_t)__popcll(__ballot(l_c1 && l_plain));
-                        // concurrent decisions (maxConcurrent > 1): the first of each fqn@version key in the chunk walks
-                        // too; a step takes it when the invoker is usable and the key's container there has a free slot
-                        // or the invoker has the memory (tryAcquireConcurrent, NS:57-82).  Only decisions of the same key
-                        // change its map entries, so the walk and the entry it found hold at its turn, unless the
-                        // decisions before took the memory it needs; a repeat of a key in the chunk is decided alone
+                        // concurrent decisions (maxConcurrent > 1) walk too; a step takes one when the invoker is usable
+                        // and the key's container there has a free slot or the invoker has the memory for a new one
+                        // (tryAcquireConcurrent, NS:57-82).  Only decisions of the same fqn@version key change its map
+                        // entries, so the k-th decision of a key in the chunk (rank k) walks past the capacity the k
+                        // before it use -- free slots, then maxConcurrent per container the memory holds -- and lands
+                        // where they leave it, with the entry they leave; that holds unless the decisions before took
+                        // the memory it needs, or one of its key was decided alone (then the key's later ones are too)
                         const int l_maxc = (int)((me.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
                         const bool l_cc = lane < nq && !(me.y & (OWGS_AM_EMPTY | OWGS_AM_THROW)) && l_maxc > 1;
-                        int c_ix = -1;       // the target's map entry (primary index, OWGS_CTC + overflow index, -1 none)
-                        uint32_t c_v = 0u;   // and its value at the chunk's start
+                        int c_ix = -1;        // the target's map entry (primary index, OWGS_CTC + overflow index, -1 none)
+                        uint32_t c_nv = 0u;   // the entry's value after this decision
+                        bool c_take = false;  // the decision opens a container: it takes memory (NS:70-79)
                         if (__ballot(l_cc)) {
                             u64 same = __ballot(l_cc);
                             for (int b = 0; b < 17; ++b) {
@@ -813,36 +820,64 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 const u64 m = __ballot(l_cc && bit);
                                 same &= bit ? m : ~m;
                             }
-                            bool cw = l_cc && (same & ((1ull << lane) - 1ull)) == 0ull;
+                            const int c_rank = (int)__popcll(same & ((1ull << lane) - 1ull));
+                            int cneed = c_rank;
+                            const float rmx = __builtin_amdgcn_rcpf((float)max(l_maxc, 1));
+                            bool cw = l_cc;
                             int cpos = cw ? mod_fast(l_home, l_n, __builtin_amdgcn_rcpf((float)l_n)) : 0, cst = 0;
                             while (__ballot(cw)) {
                                 if (cw) {
                                     const int id = l_base + cpos;
                                     const int pv = P[id];
                                     bool ok = false;
-                                    int ix = -1;
-                                    uint32_t v = 0u;
                                     if (pv < OWGS_PLIM) {
                                         const uint32_t key = ct_key(id, (int)me.z);
-                                        ix = ct_lookup(ct, key, &v);
+                                        uint32_t v = 0u;
+                                        int ix = ct_lookup(ct, key, &v);
                                         if (ix < 0 && ovf_on) {
                                             ++pr_ovf;
                                             const int oj = ovf_find(A.ovf, key, &v);
                                             ix = oj >= 0 ? OWGS_CTC + oj : -1;
                                         }
-                                        ok = (v & OWGS_CT_C_MASK) != 0u || pv >= l_mem;
+                                        const int c0 = (int)(v & OWGS_CT_C_MASK), o0 = ix >= 0 ? ct_ops(v) : 0;
+                                        int c1 = 0;
+                                        if (cneed < c0) {  // a free slot of the key's container
+                                            ok = true;
+                                            c1 = c0 - cneed - 1;
+                                        } else {  // containers the memory holds, maxConcurrent slots each
+                                            const int kp = cneed - c0;
+                                            int qc = (int)((float)kp * rmx);
+                                            qc -= qc * l_maxc > kp ? 1 : 0;
+                                            qc += (qc + 1) * l_maxc <= kp ? 1 : 0;
+                                            const int j = kp - qc * l_maxc;  // (kp < 64: exact)
+                                            if (pv >= (qc + 1) * l_mem) {
+                                                ok = true;
+                                                c_take = j == 0;
+                                                c1 = l_maxc - j - 1;
+                                            } else if (pv >= l_mem) {
+                                                int m = (int)((float)pv * rmem);
+                                                m -= m * l_mem > pv ? 1 : 0;
+                                                m += (m + 1) * l_mem <= pv ? 1 : 0;
+                                                cneed -= c0 + m * l_maxc;
+                                            } else {
+                                                cneed -= c0;
+                                            }
+                                        }
+                                        if (ok) {
+                                            if (o0 + cneed + 1 > OWGS_MAX_OPS) err |= OWGS_ERR_OPS;
+                                            c_ix = ix;
+                                            c_nv = ct_val(c1, o0 + cneed + 1);
+                                        }
                                     }
                                     if (ok) {
                                         sp = SP_FOUND;
                                         sp_t = id;
-                                        c_ix = ix;
-                                        c_v = v;
                                         cw = false;
                                     } else if (++cst >= l_n) {
-                                        sp = SP_FAIL;  // every pool position: forced below
-                                        cw = false;
-                                    } else if (cst >= A.spec) {
-                                        cw = false;    // SP_STOP: decided alone
+                                        if (c_rank == 0) sp = SP_FAIL;  // every pool position: forced below (a repeat:
+                                        cw = false;                     // decided alone)
+                                    } else if (cst >= max(1, A.spec >> 2)) {
+                                        cw = false;    // SP_STOP: decided alone (budget: a map lookup per step)
                                     } else {
                                         cpos += l_step;
                                         cpos -= cpos >= l_n ? l_n : 0;
@@ -861,8 +896,14 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 o_v = OWGS_NONE_V;
                                 o_f = 1;
                                 if (sp_t < 0) err |= OWGS_ERR_INTERNAL;
-                                else if (l_cc)  // forceAcquireConcurrent: a free slot of the key's container there, or memory
-                                    c_ix = ct_lookup2(ct, A.ovf, ovf_on, ct_key(sp_t, (int)me.z), &c_v);
+                                else if (l_cc) {  // forceAcquireConcurrent: a free slot of the key's container there, or memory
+                                    uint32_t v = 0u;
+                                    c_ix = ct_lookup2(ct, A.ovf, ovf_on, ct_key(sp_t, (int)me.z), &v);
+                                    const int c0 = (int)(v & OWGS_CT_C_MASK), o0 = c_ix >= 0 ? ct_ops(v) : 0;
+                                    c_take = c0 == 0;
+                                    c_nv = ct_val(c_take ? l_maxc - 1 : c0 - 1, o0 + 1);
+                                    if (o0 + 1 > OWGS_MAX_OPS) err |= OWGS_ERR_OPS;
+                                }
                             } else {
                                 sp = SP_TRIV;  // no healthy invoker: None
                                 o_v = OWGS_NONE_V;
@@ -887,8 +928,8 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                         // ---- in stream order: the longest prefix whose speculative targets still hold commits at
                         // once; the first one that does not (or a concurrent decision, or an unfinished walk) is decided
                         // alone, then the next prefix
-                        const bool c_slot = l_cc && (c_v & OWGS_CT_C_MASK) != 0u;  // takes a free slot, no memory
-                        for (int q = 0;;) {
+                        const bool c_slot = l_cc && !c_take;  // takes a free slot, no memory
+                        for (int q = 0;; ++pr_pass) {
                             const bool cand = lane >= q && (sp == SP_FOUND || sp == SP_FORCED);
                             const bool take = cand && !c_slot;
                             // the memory taken at my target by the candidates before me (same target: all bits agree)
@@ -910,31 +951,33 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                             (sp == SP_FOUND && (c_slot || room - S >= l_mem));
                             const u64 bad = __ballot(!ok);
                             const int f = bad ? ffs64(bad) : 64;
-                            uint32_t nv = 0u;
                             if (cand && lane < f) {
                                 if (take) {
                                     atomicSub(&P[sp_t], l_mem);  // tryAcquire (FS:63-71) / forceAcquire (FS:102-110)
                                     if (room - S - l_mem < -OWGS_PLIM) err |= OWGS_ERR_PERMITS;
                                 }
-                                if (l_cc) {  // the key's container at the target: a slot taken, or a new one (NS:63-79)
-                                    const int c0 = c_ix >= 0 ? (int)(c_v & OWGS_CT_C_MASK) : 0;
-                                    const int o0 = c_ix >= 0 ? ct_ops(c_v) : 0;
-                                    const int c1 = c_slot ? c0 - 1 : l_maxc - 1, o1 = o0 + 1;
-                                    if (o1 > OWGS_MAX_OPS) err |= OWGS_ERR_OPS;
-                                    nv = ct_val(c1, o1);
-                                    if (c_ix >= 0 && c_ix < OWGS_CTC) ct[c_ix].y = nv;
-                                    else if (c_ix >= OWGS_CTC) ovf_st_val(A.ovf.t, c_ix - OWGS_CTC, nv);
-                                }
+                                // the key's container at the target: a slot taken, or a new one (NS:63-79); decisions of
+                                // one key at one invoker leave values whose operationCount grows with each: the largest
+                                // is the last one's
+                                if (l_cc && c_ix >= 0 && c_ix < OWGS_CTC) atomicMax(&ct[c_ix].y, c_nv);
+                                else if (l_cc && c_ix >= OWGS_CTC) atomicMax(&A.ovf.t[c_ix - OWGS_CTC].y, c_nv);
                                 o_v = sp_t;
                                 o_f = sp == SP_FORCED ? 1 : 0;
                             }
-                            // new (invoker, fqn) entries, one at a time in stream order (lane 0 inserts)
+                            // entries absent at the chunk's start, one at a time in stream order (lane 0): the first
+                            // decision of a key at an invoker inserts it, the later ones find it
                             for (u64 ins = __ballot(cand && lane < f && l_cc && c_ix < 0); ins; ins &= ins - 1ull) {
                                 const int j = ffs64(ins);
                                 const uint32_t key = ct_key(__builtin_amdgcn_readlane(sp_t, j),
                                                             __builtin_amdgcn_readlane((int)me.z, j));
-                                const uint32_t nvj = (uint32_t)__builtin_amdgcn_readlane((int)nv, j);
-                                if (lane == 0) insert(key, nvj);
+                                const uint32_t nvj = (uint32_t)__builtin_amdgcn_readlane((int)c_nv, j);
+                                if (lane == 0) {
+                                    uint32_t v0;
+                                    const int ix = ct_lookup2(ct, A.ovf, ovf_on, key, &v0);
+                                    if (ix < 0) insert(key, nvj);
+                                    else if (ix < OWGS_CTC) ct[ix].y = max(v0, nvj);
+                                    else ovf_st_val(A.ovf.t, ix - OWGS_CTC, max(v0, nvj));
+                                }
                                 used = __builtin_amdgcn_readfirstlane(used);
                                 ovf_on = __builtin_amdgcn_readfirstlane((int)ovf_on) != 0;
                                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -943,6 +986,10 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                             if (f >= nq) break;
                             decide_one(f, __builtin_amdgcn_readlane(sp_ts, f));
+                            if (__builtin_amdgcn_readlane((int)l_cc, f)) {  // the key's later decisions assumed its
+                                const uint32_t zf = (uint32_t)__builtin_amdgcn_readlane((int)me.z, f);  // prediction
+                                if (lane > f && l_cc && me.z == zf) sp = SP_STOP;
+                            }
                             q = f + 1;
                         }
                     } else {
@@ -1082,6 +1129,9 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 st_sys(pr + 6, (int)pr_hit);
                 st_sys(pr + 7, (int)pr_u);
                 st_sys(pr + 8, (int)pr_grp);
+                st_sys(pr + 9, (int)pr_pass);
+                st_sys(pr + 10, (int)pr_alone);
+                st_sys(pr + 11, (int)min(pr_alone_cyc, (u64)0x7FFFFFFF));
                 st_sys(&A.ctl[OWGS_RES_GEN], (int)gen);
             } else if (lane == 0 && A.s_stats) {  // stream mode: summed over the launch (owgs_resident_stats' order)
                 A.s_stats[0] += pr_rounds;
@@ -1093,6 +1143,9 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 A.s_stats[6] += pr_hit;
                 A.s_stats[7] += pr_u;
                 A.s_stats[8] += pr_grp;
+                A.s_stats[9] += pr_pass;
+                A.s_stats[10] += pr_alone;
+                A.s_stats[11] += pr_alone_cyc;
             }
             if (lane == 0) {
                 sc[RS_USED] = used;
