@@ -349,11 +349,13 @@ int owgs_engine_ms(owgs_ctx* ctx, float* ms);
  * chain took, [4] 1 while a resident engine is live; then, summed over the served calls: [5] walk rounds, [6]
  * decisions, [7] staging cycles, [8] release cycles, [9] publish cycles, [10] overflow lookups, [11] walks that
  * started at a cursor, [12] walks skipped by the pool permit bound, [13] decisions committed from speculative walks,
- * [14] validation passes, [15] decisions decided alone, [16] their cycles; [17] the duration in ns of the last
- * owgs_publish_batch / owgs_release_batch / owgs_process_batch call, entry to return, timed inside the library; [18] 1
- * when the last owgs_replay / owgs_replay_device(_span) ran through the resident engine's stream mode
- * (OWGS_SPEC_REPLAY), [19..30] that replay's counters [5..16] summed over its launch (a device synchronisation).
- * Returns the number of counters (31). */
+ * [14] validation passes, [15] decisions decided alone, [16] their cycles, [17] speculation cycles, [18] validation
+ * cycles (the decisions decided alone included), [19..23] cycles of the speculation's rank matching, plain walks and
+ * concurrent walks, of the validation's map inserts and of the releases' concurrent part; [24] the duration in ns of
+ * the last owgs_publish_batch / owgs_release_batch / owgs_process_batch call, entry to return, timed inside the
+ * library; [25] 1 when the last owgs_replay / owgs_replay_device(_span) ran through the resident engine's stream mode
+ * (OWGS_SPEC_REPLAY), [26..44] that replay's counters [5..23] summed over its launch (a device synchronisation).
+ * Returns the number of counters (45). */
 int owgs_resident_stats(owgs_ctx* ctx, int64_t* out, int32_t cap);
 
 /* Restore the slot state captured by owgs_snapshot (bench: every timed step starts from the same state). */

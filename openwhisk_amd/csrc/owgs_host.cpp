@@ -323,6 +323,7 @@ struct owgs_ctx {
     uint32_t res_gen_seen = 0;      // the last cursor generation the engine reported
     int64_t last_call_ns = 0;       // duration of the last publish / release / process_batch call, timed inside the library
     DevBuf<unsigned long long> d_spec_stats;  // stream-mode replays: summed resident-engine counters (owgs_resident_stats)
+    DevBuf<uint32_t> d_claim;       // stream-mode replays: released activations (a second release is a malformed stream)
     bool spec_last = false;         // the last replay ran in stream mode
     DevBuf<unsigned long long> f_bound;  // per slot: what a fused call's releases can return (zero between calls)
     DevBuf<uint32_t> s_w_keys, s_w_vals;
@@ -1973,7 +1974,7 @@ static int replay_watch(owgs_ctx* c, int32_t nb, const int64_t* acq_off, const i
 static bool spec_replay_eligible(const owgs_ctx* c);
 static int spec_replay(owgs_ctx* c, int32_t nb, const int64_t* acq_off, const int32_t* act, int64_t n_act,
                        const int64_t* rel_off, const int64_t* rel_aid, int64_t n_rel, uint64_t seq_base,
-                       int32_t* out_inv, uint8_t* out_flags, uint8_t* rel_flags, hipStream_t hs);
+                       int32_t* out_inv, uint8_t* out_flags, uint8_t* rel_flags, hipStream_t hs, int64_t aid_end);
 
 // One batch of a device-resident stream replayed batch by batch (state updates such as a health change in between):
 // releases rel_aid[r_beg, r_end) of activations decided by earlier calls (invoker in out_invoker), then the publishes
@@ -2020,7 +2021,7 @@ static int replay_device_span_impl(owgs_ctx* c, int64_t a_beg, int64_t a_end, in
         const int64_t offs[4] = {a_beg, a_end, r_beg, r_end};
         HIPCHK(c, upload(c->w_off, offs, 4, hs));
         return spec_replay(c, 1, c->w_off.p, act, na, nr > 0 ? c->w_off.p + 2 : nullptr, rel_aid, nr, seq_base,
-                           out_invoker, out_flags, rel_flags, hs);
+                           out_invoker, out_flags, rel_flags, hs, a_beg);
     }
     c->spec_last = false;
     HIPCHK(c, c->f_rec.reserve((size_t)nr + 2));
@@ -2087,9 +2088,10 @@ static bool spec_replay_eligible(const owgs_ctx* c) {
     return res_stage_bytes(c) >= 8192;
 }
 
+// (n_act: the call's activations; aid_end: the end of the activation index range the stream arrays cover)
 static int spec_replay(owgs_ctx* c, int32_t nb, const int64_t* acq_off, const int32_t* act, int64_t n_act,
                        const int64_t* rel_off, const int64_t* rel_aid, int64_t n_rel, uint64_t seq_base,
-                       int32_t* out_inv, uint8_t* out_flags, uint8_t* rel_flags, hipStream_t hs) {
+                       int32_t* out_inv, uint8_t* out_flags, uint8_t* rel_flags, hipStream_t hs, int64_t aid_end) {
     if (c->any_conc) {
         const int rc = ensure_ovf(c, (int32_t)std::min<int64_t>(n_act, INT32_MAX), hs);
         if (rc) return rc;
@@ -2128,6 +2130,7 @@ static int spec_replay(owgs_ctx* c, int32_t nb, const int64_t* acq_off, const in
     a.spec = std::max(0, env_opts().res_spec);
     a.smode = 1;
     a.s_nb = nb;
+    a.s_nact = aid_end;
     a.s_acq_off = acq_off;
     a.s_act = act;
     a.s_rel_off = n_rel > 0 ? rel_off : nullptr;
@@ -2137,6 +2140,12 @@ static int spec_replay(owgs_ctx* c, int32_t nb, const int64_t* acq_off, const in
     a.s_out_fl = out_flags;
     a.s_rel_fl = rel_flags;
     a.s_stats = c->d_spec_stats.p;
+    if (nb > 1 || aid_end == n_act) {  // a whole stream: every release names a distinct activation (spans: each alone)
+        const size_t words = (size_t)(aid_end + 31) / 32 + 1;
+        HIPCHK(c, c->d_claim.reserve(words));
+        HIPCHK(c, hipMemsetAsync(c->d_claim.p, 0, words * sizeof(uint32_t), hs));
+        a.s_claim = c->d_claim.p;
+    }
     if (!c->ev_engine[0]) {
         HIPCHK(c, hipEventCreate(&c->ev_engine[0]));
         HIPCHK(c, hipEventCreate(&c->ev_engine[1]));
@@ -2161,7 +2170,7 @@ static int replay_device_impl(owgs_ctx* c, int32_t n_batches, const int64_t* acq
             return OWGS_EINVAL;
         (void)hipSetDevice(c->cfg.device);
         return spec_replay(c, n_batches, acq_off, act, n_activations, rel_off, rel_aid, n_releases, seq_base,
-                           out_invoker, out_flags, rel_flags, hs);
+                           out_invoker, out_flags, rel_flags, hs, n_activations);
     }
     c->spec_last = false;
     if (c->w_cap > 0 && n_batches > 0) {

@@ -314,7 +314,10 @@ struct OwgsReleaseArgs {
 #define OWGS_RES_PROF 96    // device: the last call's counters (OWGS_RES_NPROF words: walk rounds, decisions,
                             // staging / release / publish cycles, overflow lookups, cursor hits, U shortcuts,
                             // decisions of the grouped walks)
-#define OWGS_RES_NPROF 12  // (+ validation passes, decisions decided alone, their cycles)
+#define OWGS_RES_NPROF 19  // (+ validation passes, decisions decided alone, their cycles, speculation and
+                           // validation cycles: validation includes the decisions decided alone; speculation's
+                           // rank matching, plain walks, concurrent walks; validation's entry inserts; the
+                           // releases' concurrent part)
 #define OWGS_RES_HDR 64     // host: the call -- n_runs, n_rel, n_pub, has_seq, seq_base lo, hi, then byte offsets in
                             // the input block of pub_off, the release records, the publish records, seq (u64), the
                             // block's length, and the memory the releases return at most (lo, hi).  The block:
@@ -352,6 +355,7 @@ struct OwgsResArgs {
     // stream mode (owgs_replay_device through this engine): no doorbell, the stream's batches from HBM
     int32_t smode;
     int32_t s_nb;
+    long long s_nact;            // activations in the stream (a release must name one of them)
     const int64_t* s_acq_off;    // [s_nb + 1]
     const int32_t* s_act;        // [n_activations] action handle of each activation
     const int64_t* s_rel_off;    // [s_nb + 1] or null
@@ -361,6 +365,7 @@ struct OwgsResArgs {
     uint8_t* s_out_fl;
     uint8_t* s_rel_fl;           // or null
     unsigned long long* s_stats; // [OWGS_RES_NPROF] summed counters, or null
+    uint32_t* s_claim;           // one bit per activation, zeroed: a second release of one is refused (or null)
 };
 
 // owgs_process_batch: the caller's releases (invoker, action handle) of each run as engine release records

@@ -312,6 +312,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 h[10] = h[9];
                 h[11] = h[12] = 0;
                 h[13] = (int32_t)base;  // first release / publish of the piece in the stream
+                h[14] = (int32_t)s_p0;  // the batch's first activation (its releases name earlier ones)
                 sc[RS_K] = kk;
                 *(u64*)&sc[RS_RSUM] = 0ull;
             }
@@ -372,26 +373,90 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 roff[1] = NR;
                 poff[1] = NP;
             }
+            // (8 records per thread per round, each level of the gathers issued for all 8 before the next: three
+            // dependent HBM round trips per round instead of per record)
             u64 rs = 0;
-            for (int j = tid; j < NR; j += 256) {
-                const long long aid = A.s_rel_aid[s_first + j];
-                const int inv = __hip_atomic_load(A.s_out_inv + aid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const int a = A.s_act[aid];
-                const uint2 m = A.act_meta[a];
-                rel[j] = make_uint4((uint32_t)inv, m.y, (uint32_t)A.act_slot[a], 0u);
-                if (inv >= 0 && inv < n_slots) rs += (u64)(m.y & OWGS_AM_MEM_MASK);
+            for (int j0 = 0; j0 < NR; j0 += 8 * 256) {
+                long long aid[8];
+                int inv[8], a[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int j = j0 + u * 256 + tid;
+                    aid[u] = j < NR ? A.s_rel_aid[s_first + j] : -1;
+                    // (device streams are not checked on the host): a release names an activation of an earlier batch
+                    if (j < NR && (aid[u] < 0 || aid[u] >= A.s_nact || aid[u] >= (long long)hdr[14])) {
+                        atomicOr(&sc[RS_ERR], OWGS_ERR_BAD_STREAM);
+                        aid[u] = -1;
+                    }
+                }
+                if (A.s_claim) {  // ... and at most once (CommonLoadBalancer removes its entry, CLB:278-279)
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        if (aid[u] >= 0) {
+                            const uint32_t bit = 1u << (aid[u] & 31);
+                            if (atomicOr(&A.s_claim[aid[u] >> 5], bit) & bit) {
+                                atomicOr(&sc[RS_ERR], OWGS_ERR_BAD_STREAM);
+                                aid[u] = -1;
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    inv[u] = aid[u] >= 0 ? __hip_atomic_load(A.s_out_inv + aid[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : -1;
+                    a[u] = aid[u] >= 0 ? A.s_act[aid[u]] : 0;
+                    if ((uint32_t)a[u] >= (uint32_t)A.n_actions) {
+                        atomicOr(&sc[RS_ERR], OWGS_ERR_BAD_STREAM);
+                        a[u] = 0;
+                        inv[u] = -1;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int j = j0 + u * 256 + tid;
+                    if (j < NR) {
+                        const uint32_t my = A.act_meta[a[u]].y;
+                        rel[j] = make_uint4((uint32_t)inv[u], my, (uint32_t)A.act_slot[a[u]], 0u);
+                        if (inv[u] >= 0 && inv[u] < n_slots) rs += (u64)(my & OWGS_AM_MEM_MASK);
+                    }
+                }
             }
-            for (int i = tid; i < NP; i += 256) {
-                const int a = A.s_act[s_first + i];
-                const uint2 m = A.act_meta[a];
-                pub[i] = make_uint4(m.x, m.y, (uint32_t)A.act_slot[a], (uint32_t)a);
+            for (int i0 = 0; i0 < NP; i0 += 8 * 256) {
+                int a[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int i = i0 + u * 256 + tid;
+                    a[u] = i < NP ? A.s_act[s_first + i] : -1;
+                    if (i < NP && (uint32_t)a[u] >= (uint32_t)A.n_actions) {
+                        atomicOr(&sc[RS_ERR], OWGS_ERR_BAD_STREAM);
+                        a[u] = 0;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int i = i0 + u * 256 + tid;
+                    if (i < NP) {
+                        const uint2 m = A.act_meta[a[u]];
+                        pub[i] = make_uint4(m.x, m.y, (uint32_t)A.act_slot[a[u]], (uint32_t)a[u]);
+                    }
+                }
             }
             if (rs) atomicAdd((u64*)&sc[RS_RSUM], rs);
             __syncthreads();
             rsum = *(const u64*)&sc[RS_RSUM];
-            for (int i = tid; i < NP; i += 256) {
-                const uint32_t a = pub[i].w;
-                pcur[i] = (A.cur && a < (uint32_t)A.n_actions) ? A.cur[a] : make_uint2(0u, 0u);
+            for (int i0 = 0; i0 < NP; i0 += 8 * 256) {
+                uint2 cu[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int i = i0 + u * 256 + tid;
+                    const uint32_t a = i < NP ? pub[i].w : 0xFFFFFFFFu;
+                    cu[u] = (A.cur && a < (uint32_t)A.n_actions) ? A.cur[a] : make_uint2(0u, 0u);
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int i = i0 + u * 256 + tid;
+                    if (i < NP) pcur[i] = cu[u];
+                }
             }
         } else if (sc[RS_BAIL] == 0) {
             // the rest of a block beyond 4 KB, four 16-byte reads in flight per thread
@@ -439,7 +504,8 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
             int U0 = sc[RS_U0], U1 = sc[RS_U1];
             uint32_t gen = (uint32_t)sc[RS_GEN];
             uint32_t pr_rounds = 0, pr_dec = 0, pr_ovf = 0, pr_hit = 0, pr_u = 0, pr_grp = 0, pr_pass = 0, pr_alone = 0;
-            u64 pr_alone_cyc = 0;
+            u64 pr_alone_cyc = 0, pr_spec_cyc = 0, pr_val_cyc = 0;
+            u64 pr_c_match = 0, pr_c_pwalk = 0, pr_c_cwalk = 0, pr_c_ins = 0, pr_c_relc = 0;
             const u64 pr_stage = clock64() - t_call;  // header, staging and the range check
             u64 pr_rel = 0, pr_pub = 0;
             int32_t* out_inv = (int32_t*)(stg + s_out);  // (LDS; copied to host memory after the call)
@@ -494,13 +560,51 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                     if (valid && inv < 0) flag = OWGS_REL_NOENTRY_BIT;  // no ActivationEntry (CLB:278-279)
                     // maxConcurrent == 1: ForcibleSemaphore.release (FS:117-120), order-free (range checked above)
                     if (in && maxc <= 1) atomicAdd(&P[inv], mem);
-                    // concurrent: RS.release(1, true) on the entry, in queue order (NS:98-113)
-                    u64 cm = __ballot(in && maxc > 1);
+                    // concurrent: RS.release(1, true) on the entry, in queue order (NS:98-113).  Every lane looks its
+                    // entry up at once; releases of different entries commute, so the primary-table entries that one
+                    // lane of this group releases are updated in parallel, and entries with several releases here
+                    // (and overflow entries) one release at a time in queue order
+                    const u64 trc = clock64();
+                    const bool cr = in && maxc > 1;
+                    const uint32_t rkey = cr ? ct_key(inv, (int)(rr.z & 0x1FFFFu)) : 0u;
+                    uint32_t rv = 0u;
+                    int rix = -1;
+                    if (cr) rix = ct_lookup2(ct, A.ovf, ovf_on, rkey, &rv);
+                    const bool prim = cr && rix >= 0 && rix < OWGS_CTC;
+                    u64 dup = 0ull;
+                    if (__ballot(prim) & (__ballot(prim) - 1ull)) {  // two or more: same-entry releases?
+                        u64 eq = __ballot(prim);
+                        for (int b = 0; b < 12; ++b) {
+                            const bool bit = (rix >> b) & 1;
+                            const u64 m = __ballot(prim && bit);
+                            eq &= bit ? m : ~m;
+                        }
+                        dup = __ballot(prim && (eq & ~(1ull << lane)) != 0ull);
+                    }
+                    if (cr && rix < 0) flag = OWGS_REL_NOSUCH_BIT;  // NoSuchElementException (NS:103)
+                    if (prim && !((dup >> lane) & 1ull)) {
+                        const int c0 = (int)(rv & OWGS_CT_C_MASK), o0 = ct_ops(rv);
+                        if (o0 <= 0) {
+                            flag = OWGS_REL_NOSUCH_BIT;
+                        } else {
+                            int c1 = c0 + 1;
+                            const int o1 = o0 - 1;
+                            if (c1 % maxc == 0) {  // RS:45-52: a whole container free -> its memory
+                                c1 -= maxc;
+                                atomicAdd(&P[inv], mem);
+                            }
+                            const bool removed = o1 == 0;  // NS:109-111
+                            ct[rix] = make_uint2(removed ? OWGS_CT_TOMB : rkey, removed ? 0u : ct_val(c1, o1));
+                            tombs += removed;
+                        }
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    u64 cm = dup | __ballot(cr && rix >= OWGS_CTC);
                     while (cm) {
                         const int q = ffs64(cm);
                         cm &= cm - 1;
                         if (lane == q) {
-                            const uint32_t key = ct_key(inv, (int)(rr.z & 0x1FFFFu));
+                            const uint32_t key = rkey;
                             uint32_t v;
                             const int ix = ct_lookup2(ct, A.ovf, ovf_on, key, &v);
                             const int c0 = (int)(v & OWGS_CT_C_MASK), o0 = ct_ops(v);
@@ -522,6 +626,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                         }
                         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                     }
+                    pr_c_relc += clock64() - trc;
                     if (valid) rel_fl[j] = flag;
                     // the pools' permit bounds follow what the releases raised
                     const int pn = in ? P[inv] : (int)0x80000000;
@@ -715,6 +820,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                     };
 
                     if (A.spec > 0) {
+                        const u64 tsp0 = clock64();
                         // ---- speculation: every maxConcurrent == 1 decision walks on its own against the state at
                         // the chunk's start, A.spec steps at most (4 permit reads in flight per round).  Permits only
                         // fall inside a run (releases come first, SCPB:327-331 via CLB:260-346), so a step full then is
@@ -732,17 +838,23 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                         // repeats of one action in the chunk share its walk: the k-th (rank k among the chunk's plain
                         // decisions of that action) passes over the room the k before it take, so it walks to the step
                         // where the capacity for its memory met so far, sum of floor(permits / mem), exceeds k
-                        int need = 0;
+                        const int l_maxc = (int)((me.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
+                        const bool l_cc = lane < nq && !(me.y & (OWGS_AM_EMPTY | OWGS_AM_THROW)) && l_maxc > 1;
+                        const u64 lt = (1ull << lane) - 1ull;
+                        u64 same_a;  // the chunk's walking lanes of my action (one walk, one memory size)
                         {
+                            const bool in = l_plain || l_cc;
                             const int abits = 32 - __clz(max(A.n_actions - 1, 1));
-                            u64 same = __ballot(l_plain);
+                            same_a = __ballot(in);
                             for (int b = 0; b < abits; ++b) {
                                 const bool bit = (me.w >> b) & 1u;
-                                const u64 m = __ballot(l_plain && bit);
-                                same &= bit ? m : ~m;
+                                const u64 m = __ballot(in && bit);
+                                same_a &= bit ? m : ~m;
                             }
-                            need = l_plain ? (int)__popcll(same & ((1ull << lane) - 1ull)) : 0;
                         }
+                        int need = l_plain ? (int)__popcll(same_a & lt) : 0;
+                        const u64 tm1 = clock64();
+                        pr_c_match += tm1 - tsp0;
                         const int rank = need;
                         const float rmem = __builtin_amdgcn_rcpf((float)max(l_mem, 1));
                         bool walking = false;
@@ -801,6 +913,8 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             }
                         }
                         pr_rounds += (uint32_t)__popcll(__ballot(l_c1 && l_plain));
+                        const u64 tm2 = clock64();
+                        pr_c_pwalk += tm2 - tm1;
                         // concurrent decisions (maxConcurrent > 1) walk too; a step takes one when the invoker is usable
                         // and the key's container there has a free slot or the invoker has the memory for a new one
                         // (tryAcquireConcurrent, NS:57-82).  Only decisions of the same fqn@version key change its map
@@ -808,22 +922,22 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                         // before it use -- free slots, then maxConcurrent per container the memory holds -- and lands
                         // where they leave it, with the entry they leave; that holds unless the decisions before took
                         // the memory it needs, or one of its key was decided alone (then the key's later ones are too)
-                        const int l_maxc = (int)((me.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
-                        const bool l_cc = lane < nq && !(me.y & (OWGS_AM_EMPTY | OWGS_AM_THROW)) && l_maxc > 1;
                         int c_ix = -1;        // the target's map entry (primary index, OWGS_CTC + overflow index, -1 none)
                         uint32_t c_nv = 0u;   // the entry's value after this decision
                         bool c_take = false;  // the decision opens a container: it takes memory (NS:70-79)
                         if (__ballot(l_cc)) {
-                            u64 same = __ballot(l_cc);
+                            // another action of the same key earlier in the chunk walks differently and shares the
+                            // key's entries: its effect on mine is not predicted, so such a decision is decided alone
+                            u64 same_s = __ballot(l_cc);
                             for (int b = 0; b < 17; ++b) {
                                 const bool bit = (me.z >> b) & 1u;
                                 const u64 m = __ballot(l_cc && bit);
-                                same &= bit ? m : ~m;
+                                same_s &= bit ? m : ~m;
                             }
-                            const int c_rank = (int)__popcll(same & ((1ull << lane) - 1ull));
+                            const int c_rank = (int)__popcll(same_a & lt);
                             int cneed = c_rank;
                             const float rmx = __builtin_amdgcn_rcpf((float)max(l_maxc, 1));
-                            bool cw = l_cc;
+                            bool cw = l_cc && (same_s & ~same_a & lt) == 0ull;
                             int cpos = cw ? mod_fast(l_home, l_n, __builtin_amdgcn_rcpf((float)l_n)) : 0, cst = 0;
                             while (__ballot(cw)) {
                                 if (cw) {
@@ -925,11 +1039,15 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                         }
                         mv[lane] = l_mem;
                         const int tbits = 32 - __clz(max(A.n_ids - 1, 1));
+                        const u64 tsp1 = clock64();
+                        pr_spec_cyc += tsp1 - tsp0;
                         // ---- in stream order: the longest prefix whose speculative targets still hold commits at
                         // once; the first one that does not (or a concurrent decision, or an unfinished walk) is decided
                         // alone, then the next prefix
                         const bool c_slot = l_cc && !c_take;  // takes a free slot, no memory
-                        for (int q = 0;; ++pr_pass) {
+                        pr_c_cwalk += clock64() - tm2;
+                        for (int q = 0;;) {
+                            ++pr_pass;
                             const bool cand = lane >= q && (sp == SP_FOUND || sp == SP_FORCED);
                             const bool take = cand && !c_slot;
                             // the memory taken at my target by the candidates before me (same target: all bits agree)
@@ -966,6 +1084,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             }
                             // entries absent at the chunk's start, one at a time in stream order (lane 0): the first
                             // decision of a key at an invoker inserts it, the later ones find it
+                            const u64 ti0 = clock64();
                             for (u64 ins = __ballot(cand && lane < f && l_cc && c_ix < 0); ins; ins &= ins - 1ull) {
                                 const int j = ffs64(ins);
                                 const uint32_t key = ct_key(__builtin_amdgcn_readlane(sp_t, j),
@@ -982,9 +1101,13 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 ovf_on = __builtin_amdgcn_readfirstlane((int)ovf_on) != 0;
                                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                             }
+                            pr_c_ins += clock64() - ti0;
                             pr_grp += (uint32_t)__popcll(__ballot(cand && lane < f));
                             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                            if (f >= nq) break;
+                            if (f >= nq) {
+                                pr_val_cyc += clock64() - tsp1;
+                                break;
+                            }
                             decide_one(f, __builtin_amdgcn_readlane(sp_ts, f));
                             if (__builtin_amdgcn_readlane((int)l_cc, f)) {  // the key's later decisions assumed its
                                 const uint32_t zf = (uint32_t)__builtin_amdgcn_readlane((int)me.z, f);  // prediction
@@ -1132,6 +1255,13 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 st_sys(pr + 9, (int)pr_pass);
                 st_sys(pr + 10, (int)pr_alone);
                 st_sys(pr + 11, (int)min(pr_alone_cyc, (u64)0x7FFFFFFF));
+                st_sys(pr + 12, (int)min(pr_spec_cyc, (u64)0x7FFFFFFF));
+                st_sys(pr + 13, (int)min(pr_val_cyc, (u64)0x7FFFFFFF));
+                st_sys(pr + 14, (int)min(pr_c_match, (u64)0x7FFFFFFF));
+                st_sys(pr + 15, (int)min(pr_c_pwalk, (u64)0x7FFFFFFF));
+                st_sys(pr + 16, (int)min(pr_c_cwalk, (u64)0x7FFFFFFF));
+                st_sys(pr + 17, (int)min(pr_c_ins, (u64)0x7FFFFFFF));
+                st_sys(pr + 18, (int)min(pr_c_relc, (u64)0x7FFFFFFF));
                 st_sys(&A.ctl[OWGS_RES_GEN], (int)gen);
             } else if (lane == 0 && A.s_stats) {  // stream mode: summed over the launch (owgs_resident_stats' order)
                 A.s_stats[0] += pr_rounds;
@@ -1146,6 +1276,13 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 A.s_stats[9] += pr_pass;
                 A.s_stats[10] += pr_alone;
                 A.s_stats[11] += pr_alone_cyc;
+                A.s_stats[12] += pr_spec_cyc;
+                A.s_stats[13] += pr_val_cyc;
+                A.s_stats[14] += pr_c_match;
+                A.s_stats[15] += pr_c_pwalk;
+                A.s_stats[16] += pr_c_cwalk;
+                A.s_stats[17] += pr_c_ins;
+                A.s_stats[18] += pr_c_relc;
             }
             if (lane == 0) {
                 sc[RS_USED] = used;

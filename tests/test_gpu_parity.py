@@ -218,7 +218,10 @@ def test_stream_parity_in_pass_redecisions(seed, kw):
     # concurrent lanes and blackbox pools around them
     w = W.config("headline", n_activations=60_000, seed=seed, **kw)
     b, _, _ = check_stream(w)
-    assert b.stats()["redecided"] > 0
+    if b.stream_mode_stats() is None:  # (the chunked engine's counter; stream mode decides such lanes alone)
+        assert b.stats()["redecided"] > 0
+    else:
+        assert b.stream_mode_stats()["decided_alone"] > 0
 
 
 def test_engine_specialisation_switch():
@@ -540,7 +543,8 @@ def test_large_pool_stream_parity(n_inv):
     (7 x 32-lane chunks, owgs_engine_narrow.hip) and stays bit-exact with the oracle (SCPB:512-551 has no cap)."""
     w = W.config("headline", n_invokers=n_inv, n_activations=150_000)
     b, _, _ = check_stream(w)
-    assert b.stats()["passes"] > 0
+    st = b.stream_mode_stats()
+    assert (b.stats()["passes"] if st is None else st["decisions"]) > 0
 
 
 def test_rejected_update_leaves_the_context_unchanged():

@@ -44,6 +44,11 @@ for s in ${STEPS:-tests smoke}; do
     bench)
       timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
       rc=$?; cut -c1-400 $O/bench.json; [ $rc -eq 0 ] || { tail -20 $O/bench.err; stop bench $rc; } ;;
+    dbgres)  # permits after every resident call, per config (tools/debug_resident.py)
+      for c in ${DBG_CFGS:-headline c4 hot}; do
+        timeout -k 10 200 python -u tools/debug_resident.py $c >> $O/dbgres.log 2>&1; rc=$?
+        tail -12 $O/dbgres.log | cut -c1-400; [ $rc -eq 0 ] || [ $rc -eq 1 ] || stop dbgres $rc
+      done ;;
     spectests)  # the parity suite (full-size streams included) with the replay path as the environment sets it
       timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_resident.py -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest_parity.log 2>&1
       rc=$?; tail -2 $O/pytest_parity.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error|error|assert" $O/pytest_parity.log | head -30; stop spectests $rc; } ;;
