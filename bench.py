@@ -306,13 +306,15 @@ def shim_path(w, o_inv, dev_index, drains=(64, 512, 4096), budget_jobs=(120_000,
             lat_us = np.array(clat) * 1e-3  # the C call, timed inside the library
             py_us = np.array(lat) * 1e6     # the same calls seen from Python (+ ctypes' argument conversion)
             rs1 = b.resident_stats()
+            fill = b.resident_table_fill()
             legs.append({"drain": drain, "mode": mode, "jobs": n_jobs, "calls": len(lat), "publishes": int(n_pub),
                          "p50_us": float(np.percentile(lat_us, 50)), "p99_us": float(np.percentile(lat_us, 99)),
                          "decisions_per_s": n_pub / max(float(np.sum(lat_us)) * 1e-6, 1e-9),
                          "py_p50_us": float(np.percentile(py_us, 50)), "py_p99_us": float(np.percentile(py_us, 99)),
                          "bit_exact": exact,
                          # owgs_process_batch's paths in this leg: resident engine calls / launches, launch-chain calls
-                         "resident": {k: rs1[k] - rs0[k] for k in rs1 if k not in ("alive", "last_call_ns")}})
+                         "resident": {k: rs1[k] - rs0[k] for k in rs1 if k not in ("alive", "last_call_ns")},
+                         "map_fill_max": fill[0], "map_deleted_max": fill[1]})
     b.close()
     return {"path": "host buffers through the C ABI as the JNI shim calls it (queue order: each batch's completions, "
                     "then its publishes); calls = owgs_release_batch + owgs_publish_batch per run, fused = "

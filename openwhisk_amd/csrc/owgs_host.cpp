@@ -318,6 +318,7 @@ struct owgs_ctx {
     int32_t res_stage = 0;
     int64_t res_n_calls = 0, res_n_launches = 0, res_n_bails = 0, res_n_chained = 0;
     int64_t res_prof[OWGS_RES_NPROF] = {};
+    int64_t res_used_max = 0, res_tombs_max = 0;  // the primary table's fill after served calls (largest seen)
     DevBuf<uint2> d_res_cur;        // per action: {cursor generation, first walk step that may fit}
     std::vector<uint2> res_meta;    // act_meta as of the live launch (every change of it stops the engine first)
     uint32_t res_gen_seen = 0;      // the last cursor generation the engine reported
@@ -1085,6 +1086,56 @@ static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
         Q[4 * i + 2] = (uint32_t)c->a_slot[a];
         Q[4 * i + 3] = (uint32_t)a;
     }
+    // per chunk of 64 publishes of a run (the engine's speculation unit): each publish's rank among the chunk's
+    // publishes of its action, and whether an earlier concurrent publish of the chunk has its fqn@version key under
+    // another action (owgs_resident.hip, RES_RANK_SHIFT / RES_SHARED)
+    {
+        struct Tab {  // 128-entry open addressing, cleared by its used list
+            uint32_t k[128];
+            int32_t v[128];
+            int32_t w[128];
+            uint8_t used[128];
+            int32_t list[64];
+            int n = 0;
+            Tab() { memset(used, 0, sizeof(used)); }
+            int find(uint32_t key) {
+                uint32_t h = (key * 2654435761u) >> 25;
+                while (used[h] && k[h] != key) h = (h + 1) & 127;
+                if (!used[h]) {
+                    used[h] = 1;
+                    k[h] = key;
+                    v[h] = 0;
+                    w[h] = -1;
+                    list[n++] = (int)h;
+                }
+                return (int)h;
+            }
+            void clear() {
+                for (int i = 0; i < n; ++i) used[list[i]] = 0;
+                n = 0;
+            }
+        };
+        static thread_local Tab ta, ts;
+        for (int32_t r = 0; r < n_runs; ++r)
+            for (int32_t c0 = pub_off[r]; c0 < pub_off[r + 1]; c0 += 64) {
+                const int32_t c1 = std::min(c0 + 64, pub_off[r + 1]);
+                for (int32_t i = c0; i < c1; ++i) {
+                    const int32_t a = pub_action[i];
+                    const int ha = ta.find((uint32_t)a);
+                    uint32_t wd = (uint32_t)a | ((uint32_t)ta.v[ha]++ << 17);
+                    const uint32_t my = c->res_meta[a].y;
+                    if (!(my & (OWGS_AM_EMPTY | OWGS_AM_THROW)) && c->a_maxc[a] > 1) {
+                        const int hs = ts.find((uint32_t)c->a_slot[a]);
+                        if (ts.w[hs] < 0) ts.w[hs] = a;                     // first concurrent action of the key
+                        else if (ts.w[hs] != a) ts.v[hs] = 1;                // a second action: later ones are shared
+                        if (ts.w[hs] != a || ts.v[hs]) wd |= 1u << 23;
+                    }
+                    Q[4 * i + 3] = wd;
+                }
+                ta.clear();
+                ts.clear();
+            }
+    }
     if (seq && NP) memcpy(B + b_seq, seq, 8 * (size_t)NP);
     volatile int32_t* H = c->res_ctl + OWGS_RES_HDR;
     const int32_t hdr[13] = {n_runs, NR, NP, seq ? 1 : 0, (int32_t)(uint32_t)seq_base, (int32_t)(uint32_t)(seq_base >> 32),
@@ -1126,6 +1177,8 @@ static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
     ++c->res_n_calls;
     c->res_gen_seen = (uint32_t)__atomic_load_n(&c->res_ctl[OWGS_RES_GEN], __ATOMIC_ACQUIRE);
     for (int k = 0; k < OWGS_RES_NPROF; ++k) c->res_prof[k] += (uint32_t)c->res_ctl[OWGS_RES_PROF + k];
+    c->res_used_max = std::max<int64_t>(c->res_used_max, c->res_ctl[OWGS_RES_USED]);
+    c->res_tombs_max = std::max<int64_t>(c->res_tombs_max, c->res_ctl[OWGS_RES_TOMBS]);
     if (c->any_conc) ovf_add(c, NP);
     if (NP) {
         memcpy(out_invoker, c->res_out, 4 * (size_t)NP);
@@ -3397,7 +3450,9 @@ int owgs_resident_stats(owgs_ctx* c, int64_t* out, int32_t cap) {
         }
         for (int32_t i = 0; i < OWGS_RES_NPROF && 7 + OWGS_RES_NPROF + i < cap; ++i) out[7 + OWGS_RES_NPROF + i] = (int64_t)v[i];
     }
-    return 7 + 2 * OWGS_RES_NPROF;
+    if (cap > 7 + 2 * OWGS_RES_NPROF) out[7 + 2 * OWGS_RES_NPROF] = c->res_used_max;
+    if (cap > 8 + 2 * OWGS_RES_NPROF) out[8 + 2 * OWGS_RES_NPROF] = c->res_tombs_max;
+    return 9 + 2 * OWGS_RES_NPROF;
 }
 
 int owgs_engine_ms(owgs_ctx* c, float* ms) {

@@ -311,6 +311,7 @@ struct OwgsReleaseArgs {
 #define OWGS_RES_RESULT 48  // device: the last call's outcome (0, OWGS_RES_BAIL_*) | its device error bits << 8
 #define OWGS_RES_USED 49    // device: primary-table entries (live + deleted) after the last call
 #define OWGS_RES_GEN 50     // device: the walk-cursor generation reached (the host's next launch starts past it)
+#define OWGS_RES_TOMBS 51   // device: deleted primary-table entries after the last call
 #define OWGS_RES_PROF 96    // device: the last call's counters (OWGS_RES_NPROF words: walk rounds, decisions,
                             // staging / release / publish cycles, overflow lookups, cursor hits, U shortcuts,
                             // decisions of the grouped walks)

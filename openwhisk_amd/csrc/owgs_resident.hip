@@ -78,6 +78,12 @@ __device__ __forceinline__ void cc_put(uint2* cc, uint32_t a, uint32_t gen, int 
     (void)__hip_atomic_exchange((u64*)&cc[cc_slot(a)], ((u64)(uint32_t)step << 32) | cc_tag(a, gen), __ATOMIC_RELAXED,
                                 __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// publish record .w: action handle | rank << 17 (earlier publishes of the same action in the decision's chunk of 64,
+// at most 63) | RES_SHARED (an earlier concurrent publish of the chunk has the same fqn@version key under another
+// action); written by the host (pinned calls) or by the staging waves (stream mode)
+#define RES_ACT_MASK 0x1FFFFu
+#define RES_RANK_SHIFT 17
+#define RES_SHARED (1u << 23)
 // speculative walk outcomes (resident engine, per decision of a chunk)
 #define SP_NONE 0    // no decision in this lane
 #define SP_TRIV 1    // decided without touching the state (None, the throw, a fallback without a healthy invoker)
@@ -101,8 +107,17 @@ __device__ __forceinline__ int select_in_word(uint32_t m, int need) {
 }
 
 #define RES_CC 2048  // walk-cursor cache entries (LDS, 16 KB)
+#define RES_BF 2048  // Bloom filter words over the primary table's keys (LDS, 8 KB)
+// the primary table is rebuilt between calls once it holds more than RES_CLEAN_USED entries of which at least
+// RES_CLEAN_TOMBS are deleted ones (deleted entries lengthen every probe chain through them)
+#ifndef RES_CLEAN_USED
+#define RES_CLEAN_USED (OWGS_CTC / 2)
+#endif
+#ifndef RES_CLEAN_TOMBS
+#define RES_CLEAN_TOMBS (OWGS_CTC / 8)
+#endif
 struct ResLayout {
-    uint32_t P, ub, pc, ct, sc, cc, mv, stage, end;
+    uint32_t P, ub, pc, ct, sc, cc, mv, bf, stage, end;
 };
 __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
     const uint32_t words = (uint32_t)(n_ids + 31) / 32;
@@ -114,7 +129,8 @@ __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
     y.sc = y.ct + OWGS_CTC * 8u;
     y.cc = y.sc + 64u * 4u;
     y.mv = y.cc + RES_CC * 8u;
-    y.stage = y.mv + 64u * 4u;
+    y.bf = y.mv + 64u * 4u;
+    y.stage = y.bf + RES_BF * 4u;
     y.end = y.stage;
     return y;
 }
@@ -133,10 +149,25 @@ __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
 #define RS_U1 11
 #define RS_TOMB 12   // deleted primary entries (the cleanup between calls runs when they pile up)
 
+// blocked Bloom filter over the primary table's keys (LDS, RES_BF words): one word and three bits per key, set on
+// every insert into the primary and rebuilt with it; a key whose bits are not all set is not in the primary, so a
+// lookup that misses -- the common case on a concurrent walk -- reads one word instead of a probe chain
+__device__ __forceinline__ uint2 bf_pos(uint32_t key) {
+    const uint32_t h = ct_hash(key * 0x9E3779B1u);
+    return make_uint2(h & (RES_BF - 1), (1u << ((h >> 11) & 31)) | (1u << ((h >> 16) & 31)) | (1u << ((h >> 21) & 31)));
+}
+__device__ __forceinline__ void bf_add(uint32_t* bf, uint32_t key) {
+    const uint2 b = bf_pos(key);
+    atomicOr(&bf[b.x], b.y);
+}
 // primary table (LDS, interleaved {key, value}): index of key or -1, *val (0 if absent); chains end at an empty entry
-__device__ __forceinline__ int ct_lookup(const uint2* ct, uint32_t key, uint32_t* val) {
+__device__ __forceinline__ int ct_lookup(const uint2* ct, const uint32_t* bf, uint32_t key, uint32_t* val) {
     uint32_t h = ct_home(key);
     *val = 0u;
+    {
+        const uint2 b = bf_pos(key);
+        if ((bf[b.x] & b.y) != b.y) return -1;
+    }
     for (int p = 0; p < OWGS_CTC / CT_BLK; ++p) {
         const uint4 e01 = *(const uint4*)&ct[h];
         const uint4 e23 = *(const uint4*)&ct[h + 2];
@@ -151,8 +182,9 @@ __device__ __forceinline__ int ct_lookup(const uint2* ct, uint32_t key, uint32_t
     return -1;
 }
 // both tables: index < OWGS_CTC primary, OWGS_CTC + j overflow entry j
-__device__ __forceinline__ int ct_lookup2(const uint2* ct, const OwgsOvf& O, bool ovf_on, uint32_t key, uint32_t* val) {
-    int i = ct_lookup(ct, key, val);
+__device__ __forceinline__ int ct_lookup2(const uint2* ct, const uint32_t* bf, const OwgsOvf& O, bool ovf_on,
+                                          uint32_t key, uint32_t* val) {
+    int i = ct_lookup(ct, bf, key, val);
     if (i < 0 && ovf_on) {
         const int j = ovf_find(O, key, val);
         i = j >= 0 ? OWGS_CTC + j : -1;
@@ -174,6 +206,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
     int32_t* sc = (int32_t*)(Lb + Y.sc);
     uint2* cc = (uint2*)(Lb + Y.cc);
     int32_t* mv = (int32_t*)(Lb + Y.mv);
+    uint32_t* bf = (uint32_t*)(Lb + Y.bf);
     char* stg = Lb + Y.stage;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int n_slots = A.n_slots, nm = A.nm, nb = A.nb;
@@ -182,6 +215,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
     // ------------------------------------------------------------------ state -> LDS (once per launch)
     if (tid < 16) sc[tid] = (tid == RS_U0 || tid == RS_U1) ? (int)0x80000000 : (tid == RS_GEN ? (int)A.gen_base : 0);
     for (int i = tid; i < RES_CC; i += 256) cc[i] = make_uint2(0u, 0u);
+    for (int i = tid; i < RES_BF; i += 256) bf[i] = 0u;
     __syncthreads();
     {
         int used = 0, tombs = 0, mx = (int)0x80000000, u0 = (int)0x80000000, u1 = (int)0x80000000, e = 0;
@@ -200,6 +234,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
         for (int i = tid; i < OWGS_CTC; i += 256) {
             const uint32_t k = A.ct_keys[i];
             ct[i] = make_uint2(k, A.ct_vals[i]);
+            if (k != 0u && k != OWGS_CT_TOMB) bf_add(bf, k);
             used += k != 0u;
             tombs += k == OWGS_CT_TOMB;
         }
@@ -443,13 +478,41 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
             }
             if (rs) atomicAdd((u64*)&sc[RS_RSUM], rs);
             __syncthreads();
+            // each chunk's ranks (the host writes them for pinned calls): the waves take a chunk each in turn
+            for (int c = wave; c * 64 < NP; c += 4) {
+                const int i = c * 64 + lane;
+                const bool v = i < NP;
+                const uint4 r = v ? pub[i] : make_uint4(0u, 0u, 0u, 0u);
+                const bool conc = v && !(r.y & (OWGS_AM_EMPTY | OWGS_AM_THROW)) &&
+                                  ((r.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK) > 1u;
+                const int abits = 32 - __clz(max(A.n_actions - 1, 1));
+                u64 same_a = __ballot(v);
+                for (int b = 0; b < abits; ++b) {
+                    const bool bit = (r.w >> b) & 1u;
+                    const u64 m = __ballot(v && bit);
+                    same_a &= bit ? m : ~m;
+                }
+                const u64 lt = (1ull << lane) - 1ull;
+                bool shared = false;
+                if (__ballot(conc)) {
+                    u64 same_s = __ballot(conc);
+                    for (int b = 0; b < 17; ++b) {
+                        const bool bit = (r.z >> b) & 1u;
+                        const u64 m = __ballot(conc && bit);
+                        same_s &= bit ? m : ~m;
+                    }
+                    shared = conc && (same_s & ~same_a & lt) != 0ull;
+                }
+                if (v) pub[i].w = r.w | ((uint32_t)__popcll(same_a & lt) << RES_RANK_SHIFT) | (shared ? RES_SHARED : 0u);
+            }
+            __syncthreads();
             rsum = *(const u64*)&sc[RS_RSUM];
             for (int i0 = 0; i0 < NP; i0 += 8 * 256) {
                 uint2 cu[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     const int i = i0 + u * 256 + tid;
-                    const uint32_t a = i < NP ? pub[i].w : 0xFFFFFFFFu;
+                    const uint32_t a = i < NP ? (pub[i].w & RES_ACT_MASK) : 0xFFFFFFFFu;
                     cu[u] = (A.cur && a < (uint32_t)A.n_actions) ? A.cur[a] : make_uint2(0u, 0u);
                 }
 #pragma unroll
@@ -476,7 +539,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
             __syncthreads();
             // every publish's walk cursor (one gather: the decision loop then waits on nothing in HBM)
             for (int i = tid; i < NP; i += 256) {
-                const uint32_t a = pub[i].w;
+                const uint32_t a = pub[i].w & RES_ACT_MASK;
                 pcur[i] = (A.cur && a < (uint32_t)A.n_actions) ? A.cur[a] : make_uint2(0u, 0u);
             }
         }
@@ -520,6 +583,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                         const uint32_t kk = ct[h].x;
                         if (kk == 0u || kk == OWGS_CT_TOMB) {
                             ct[h] = make_uint2(key, nv);
+                            bf_add(bf, key);
                             used += kk == 0u;
                             tombs -= kk == OWGS_CT_TOMB;
                             ix = (int)h;
@@ -569,33 +633,54 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                     const uint32_t rkey = cr ? ct_key(inv, (int)(rr.z & 0x1FFFFu)) : 0u;
                     uint32_t rv = 0u;
                     int rix = -1;
-                    if (cr) rix = ct_lookup2(ct, A.ovf, ovf_on, rkey, &rv);
+                    if (cr) rix = ct_lookup2(ct, bf, A.ovf, ovf_on, rkey, &rv);
                     const bool prim = cr && rix >= 0 && rix < OWGS_CTC;
-                    u64 dup = 0ull;
-                    if (__ballot(prim) & (__ballot(prim) - 1ull)) {  // two or more: same-entry releases?
-                        u64 eq = __ballot(prim);
+                    // releases of one primary entry in this group: the j-th of them (queue order) finds the entry as
+                    // the j before it leave it -- RS.release(1, true) j times from (c0, o0): c0 + j free slots, a
+                    // container's memory back each time that count reaches a multiple of maxConcurrent, the entry
+                    // removed when operationCount reaches 0 and every later release a NoSuchElement -- so all of them
+                    // apply at once (closed form) when they agree on maxConcurrent and memory; else one at a time
+                    u64 eq = 0ull, dup = 0ull;
+                    const u64 pm = __ballot(prim);
+                    if (pm & (pm - 1ull)) {
+                        eq = pm;
                         for (int b = 0; b < 12; ++b) {
                             const bool bit = (rix >> b) & 1;
                             const u64 m = __ballot(prim && bit);
                             eq &= bit ? m : ~m;
                         }
-                        dup = __ballot(prim && (eq & ~(1ull << lane)) != 0ull);
+                        if (!prim) eq = 0ull;
+                        // a group whose releases disagree on maxConcurrent or memory: one at a time
+                        const int lead = eq ? ffs64(eq) : 0;
+                        const int lmaxc = __shfl(maxc, lead, 64), lmem = __shfl(mem, lead, 64);
+                        dup = __ballot(prim && (eq & (eq - 1ull)) && (lmaxc != maxc || lmem != mem));
+                        const u64 bad = dup;  // every lane of a disagreeing group goes one at a time
+                        dup = 0ull;
+                        for (u64 bb = bad; bb;) {
+                            const int q = ffs64(bb);
+                            const int rq = __builtin_amdgcn_readlane(rix, q);
+                            const u64 grp = __ballot(prim && rix == rq);
+                            dup |= grp;
+                            bb &= ~grp;
+                        }
+                    } else {
+                        eq = prim ? (1ull << lane) : 0ull;
                     }
                     if (cr && rix < 0) flag = OWGS_REL_NOSUCH_BIT;  // NoSuchElementException (NS:103)
                     if (prim && !((dup >> lane) & 1ull)) {
                         const int c0 = (int)(rv & OWGS_CT_C_MASK), o0 = ct_ops(rv);
-                        if (o0 <= 0) {
-                            flag = OWGS_REL_NOSUCH_BIT;
+                        const int j = (int)__popcll(eq & ((1ull << lane) - 1ull)), cnt = (int)__popcll(eq);
+                        if (j >= o0) {
+                            flag = OWGS_REL_NOSUCH_BIT;  // the entry is gone by this release (NS:103)
                         } else {
-                            int c1 = c0 + 1;
-                            const int o1 = o0 - 1;
-                            if (c1 % maxc == 0) {  // RS:45-52: a whole container free -> its memory
-                                c1 -= maxc;
-                                atomicAdd(&P[inv], mem);
+                            if ((c0 + j + 1) % maxc == 0) atomicAdd(&P[inv], mem);  // RS:45-52: a container free
+                            const int jj = min(cnt, o0);
+                            if (j == jj - 1) {  // the group's last release that finds the entry writes it
+                                const int o1 = o0 - jj, c1 = (c0 + jj) % maxc;
+                                const bool removed = o1 == 0;  // NS:109-111
+                                ct[rix] = make_uint2(removed ? OWGS_CT_TOMB : rkey, removed ? 0u : ct_val(c1, o1));
+                                tombs += removed;
                             }
-                            const bool removed = o1 == 0;  // NS:109-111
-                            ct[rix] = make_uint2(removed ? OWGS_CT_TOMB : rkey, removed ? 0u : ct_val(c1, o1));
-                            tombs += removed;
                         }
                     }
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -606,7 +691,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                         if (lane == q) {
                             const uint32_t key = rkey;
                             uint32_t v;
-                            const int ix = ct_lookup2(ct, A.ovf, ovf_on, key, &v);
+                            const int ix = ct_lookup2(ct, bf, A.ovf, ovf_on, key, &v);
                             const int c0 = (int)(v & OWGS_CT_C_MASK), o0 = ct_ops(v);
                             if (ix < 0 || o0 <= 0) {
                                 flag = OWGS_REL_NOSUCH_BIT;  // NoSuchElementException (NS:103)
@@ -642,6 +727,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 for (int i0 = pb; i0 < pe; i0 += 64) {
                     const int nq = min(64, pe - i0);
                     const uint4 me = lane < nq ? pub[i0 + lane] : make_uint4(0u, OWGS_AM_EMPTY, 0u, 0u);
+                    const uint32_t l_act = me.w & RES_ACT_MASK;
                     const u64 myseq = has_seq ? (lane < nq ? sq[i0 + lane] : 0ull) : seq_base + (u64)(i0 + lane);
                     const uint2 mycur = lane < nq ? pcur[i0 + lane] : make_uint2(0u, 0u);  // (staged)
                     int o_v = OWGS_NONE_V, o_f = 0;
@@ -655,7 +741,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                     const bool l_plain = l_c1 && l_mem <= (l_pool ? U1 : U0);
                     int l_sbeg = 0;
                     if (mycur.x == gen) l_sbeg = (int)mycur.y;
-                    l_sbeg = max(l_sbeg, cc_get(cc, me.w, gen));
+                    l_sbeg = max(l_sbeg, cc_get(cc, l_act, gen));
 
                     // one decision alone, exact against the state now: decision q of the chunk, its walk starting no
                     // earlier than step smin (the steps before smin are known to have no room for it)
@@ -676,7 +762,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             const int mem = (int)(my & OWGS_AM_MEM_MASK);
                             const int maxc = (int)((my >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
                             const int n = pool ? nb : nm, base = pool ? A.n_ids - nb : 0;
-                            const int a = __builtin_amdgcn_readlane((int)me.w, q);
+                            const int a = __builtin_amdgcn_readlane((int)l_act, q);
                             int s_beg = 0;
                             if (maxc <= 1) {
                                 const uint32_t hg = (uint32_t)__builtin_amdgcn_readlane((int)mycur.x, q);
@@ -738,7 +824,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 uint32_t v = 0u;
                                 if (pv < OWGS_PLIM) {  // usable: a free slot of the key's container, or memory
                                     const uint32_t key = ct_key(id, slot);
-                                    ix = ct_lookup(ct, key, &v);
+                                    ix = ct_lookup(ct, bf, key, &v);
                                     if (ix < 0 && ovf_on) {  // (an HBM round trip: counted)
                                         ++pr_ovf;
                                         const int oj = ovf_find(A.ovf, key, &v);
@@ -778,7 +864,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                         err |= OWGS_ERR_INTERNAL;
                                     } else {
                                         tp = P[t];
-                                        if (maxc > 1) tix = ct_lookup2(ct, A.ovf, ovf_on, ct_key(t, slot), &tv);
+                                        if (maxc > 1) tix = ct_lookup2(ct, bf, A.ovf, ovf_on, ct_key(t, slot), &tv);
                                     }
                                     fl = 1;
                                 }
@@ -840,19 +926,9 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                         // where the capacity for its memory met so far, sum of floor(permits / mem), exceeds k
                         const int l_maxc = (int)((me.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
                         const bool l_cc = lane < nq && !(me.y & (OWGS_AM_EMPTY | OWGS_AM_THROW)) && l_maxc > 1;
-                        const u64 lt = (1ull << lane) - 1ull;
-                        u64 same_a;  // the chunk's walking lanes of my action (one walk, one memory size)
-                        {
-                            const bool in = l_plain || l_cc;
-                            const int abits = 32 - __clz(max(A.n_actions - 1, 1));
-                            same_a = __ballot(in);
-                            for (int b = 0; b < abits; ++b) {
-                                const bool bit = (me.w >> b) & 1u;
-                                const u64 m = __ballot(in && bit);
-                                same_a &= bit ? m : ~m;
-                            }
-                        }
-                        int need = l_plain ? (int)__popcll(same_a & lt) : 0;
+                        // rank among the chunk's publishes of my action (one walk, one memory size), from the record
+                        const int l_rank = (int)((me.w >> RES_RANK_SHIFT) & 63u);
+                        int need = l_plain ? l_rank : 0;
                         const u64 tm1 = clock64();
                         pr_c_match += tm1 - tsp0;
                         const int rank = need;
@@ -928,16 +1004,10 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                         if (__ballot(l_cc)) {
                             // another action of the same key earlier in the chunk walks differently and shares the
                             // key's entries: its effect on mine is not predicted, so such a decision is decided alone
-                            u64 same_s = __ballot(l_cc);
-                            for (int b = 0; b < 17; ++b) {
-                                const bool bit = (me.z >> b) & 1u;
-                                const u64 m = __ballot(l_cc && bit);
-                                same_s &= bit ? m : ~m;
-                            }
-                            const int c_rank = (int)__popcll(same_a & lt);
+                            const int c_rank = l_rank;
                             int cneed = c_rank;
                             const float rmx = __builtin_amdgcn_rcpf((float)max(l_maxc, 1));
-                            bool cw = l_cc && (same_s & ~same_a & lt) == 0ull;
+                            bool cw = l_cc && !(me.w & RES_SHARED);
                             int cpos = cw ? mod_fast(l_home, l_n, __builtin_amdgcn_rcpf((float)l_n)) : 0, cst = 0;
                             while (__ballot(cw)) {
                                 if (cw) {
@@ -947,7 +1017,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                     if (pv < OWGS_PLIM) {
                                         const uint32_t key = ct_key(id, (int)me.z);
                                         uint32_t v = 0u;
-                                        int ix = ct_lookup(ct, key, &v);
+                                        int ix = ct_lookup(ct, bf, key, &v);
                                         if (ix < 0 && ovf_on) {
                                             ++pr_ovf;
                                             const int oj = ovf_find(A.ovf, key, &v);
@@ -1012,7 +1082,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 if (sp_t < 0) err |= OWGS_ERR_INTERNAL;
                                 else if (l_cc) {  // forceAcquireConcurrent: a free slot of the key's container there, or memory
                                     uint32_t v = 0u;
-                                    c_ix = ct_lookup2(ct, A.ovf, ovf_on, ct_key(sp_t, (int)me.z), &v);
+                                    c_ix = ct_lookup2(ct, bf, A.ovf, ovf_on, ct_key(sp_t, (int)me.z), &v);
                                     const int c0 = (int)(v & OWGS_CT_C_MASK), o0 = c_ix >= 0 ? ct_ops(v) : 0;
                                     c_take = c0 == 0;
                                     c_nv = ct_val(c_take ? l_maxc - 1 : c0 - 1, o0 + 1);
@@ -1034,8 +1104,8 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                         // every first walk's cursor (the steps before it had no room then, so none now)
                         if (l_c1 && rank == 0) {
                             const int cs = sp == SP_FOUND ? sp_ts : sp == SP_STOP ? sp_ts : l_n;
-                            cc_put(cc, me.w, gen, cs);
-                            if (A.cur) A.cur[me.w] = make_uint2(gen, (uint32_t)cs);
+                            cc_put(cc, l_act, gen, cs);
+                            if (A.cur) A.cur[l_act] = make_uint2(gen, (uint32_t)cs);
                         }
                         mv[lane] = l_mem;
                         const int tbits = 32 - __clz(max(A.n_ids - 1, 1));
@@ -1050,30 +1120,40 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             ++pr_pass;
                             const bool cand = lane >= q && (sp == SP_FOUND || sp == SP_FORCED);
                             const bool take = cand && !c_slot;
-                            // the memory taken at my target by the candidates before me (same target: all bits agree)
-                            u64 eq = __ballot(take);
-                            for (int b = 0; b < tbits; ++b) {
-                                const bool bit = (sp_t >> b) & 1;
-                                const u64 m = __ballot(take && bit);
-                                eq &= bit ? m : ~m;
-                            }
-                            eq &= (1ull << lane) - 1ull;
-                            int S = 0;
-                            if (take)
-                                while (eq) {
-                                    S += mv[ffs64(eq)];
-                                    eq &= eq - 1ull;
+                            // every candidate takes its memory at once (LDS atomics); then F = the permits left at its
+                            // target after all of them.  A decision that walked there holds iff the permits before it
+                            // minus its own take and the takes before it stay >= 0, i.e. iff F plus the takes AFTER it
+                            // at the same invoker is >= 0: always when F >= 0; only targets that went negative need the
+                            // per-invoker sums (a ballot match on the target id)
+                            if (take) atomicSub(&P[sp_t], l_mem);  // tryAcquire (FS:63-71) / forceAcquire (FS:102-110)
+                            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // (every lane's take before the reads)
+                            const int F = take ? P[sp_t] : 0;
+                            bool fits = true;
+                            if (__ballot(take && sp == SP_FOUND && F < 0)) {
+                                const bool mt = take && F < 0;
+                                u64 eq = __ballot(mt);
+                                for (int b = 0; b < tbits; ++b) {
+                                    const bool bit = (sp_t >> b) & 1;
+                                    const u64 m = __ballot(mt && bit);
+                                    eq &= bit ? m : ~m;
                                 }
-                            const int room = take ? P[sp_t] : 0;
+                                eq &= ~((2ull << lane) - 1ull);  // the takes after me
+                                int later = 0;
+                                if (mt)
+                                    while (eq) {
+                                        later += mv[ffs64(eq)];
+                                        eq &= eq - 1ull;
+                                    }
+                                fits = !mt || F + later >= 0;
+                            }
                             const bool ok = lane < q || sp == SP_NONE || sp == SP_TRIV || sp == SP_FORCED ||
-                                            (sp == SP_FOUND && (c_slot || room - S >= l_mem));
+                                            (sp == SP_FOUND && (c_slot || fits));
                             const u64 bad = __ballot(!ok);
                             const int f = bad ? ffs64(bad) : 64;
+                            if (take && lane >= f) atomicAdd(&P[sp_t], l_mem);  // the takes from the first miss on: back
+                            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                             if (cand && lane < f) {
-                                if (take) {
-                                    atomicSub(&P[sp_t], l_mem);  // tryAcquire (FS:63-71) / forceAcquire (FS:102-110)
-                                    if (room - S - l_mem < -OWGS_PLIM) err |= OWGS_ERR_PERMITS;
-                                }
+                                if (take && P[sp_t] < -OWGS_PLIM) err |= OWGS_ERR_PERMITS;  // (after the give-backs)
                                 // the key's container at the target: a slot taken, or a new one (NS:63-79); decisions of
                                 // one key at one invoker leave values whose operationCount grows with each: the largest
                                 // is the last one's
@@ -1092,7 +1172,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 const uint32_t nvj = (uint32_t)__builtin_amdgcn_readlane((int)c_nv, j);
                                 if (lane == 0) {
                                     uint32_t v0;
-                                    const int ix = ct_lookup2(ct, A.ovf, ovf_on, key, &v0);
+                                    const int ix = ct_lookup2(ct, bf, A.ovf, ovf_on, key, &v0);
                                     if (ix < 0) insert(key, nvj);
                                     else if (ix < OWGS_CTC) ct[ix].y = max(v0, nvj);
                                     else ovf_st_val(A.ovf.t, ix - OWGS_CTC, max(v0, nvj));
@@ -1188,7 +1268,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                     const int pvk = __builtin_amdgcn_readlane(gpv, 16 * k);
                                     const int tsk = __builtin_amdgcn_readlane(gts, 16 * k);
                                     const int memk = __builtin_amdgcn_readlane(l_mem, q + k);
-                                    const int ak = __builtin_amdgcn_readlane((int)me.w, q + k);
+                                    const int ak = __builtin_amdgcn_readlane((int)l_act, q + k);
                                     const int pk_ = (__builtin_amdgcn_readlane((int)me.x, q + k) & OWGS_AM_POOL) ? 1 : 0;
                                     if (tk < 0) {  // no room anywhere for memk (then, so now): cursor past the pool, U below memk
                                         const int nk = pk_ ? nb : nm;
@@ -1297,7 +1377,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
         }
         __syncthreads();
         // ---- primary-table cleanup between calls: deleted entries keep chains long and fill the primary
-        if (sc[RS_USED] > OWGS_CTC / 2 && sc[RS_TOMB] >= OWGS_CTC / 8) {  // (uniform) enough deleted entries
+        if (sc[RS_USED] > RES_CLEAN_USED && sc[RS_TOMB] >= RES_CLEAN_TOMBS) {  // (uniform) enough deleted entries
             {
                 if (tid == 0) sc[RS_LIVE] = 0;
                 __syncthreads();
@@ -1313,6 +1393,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 __syncthreads();
                 const int nlive = sc[RS_LIVE];
                 for (int i = tid; i < OWGS_CTC; i += 256) ct[i] = make_uint2(0u, 0u);
+                for (int i = tid; i < RES_BF; i += 256) bf[i] = 0u;
                 __syncthreads();
                 for (int j = tid; j < nlive; j += 256) {  // distinct keys into an empty table: claim by CAS
                     const uint32_t kk = A.ct_tmp[2 * j], vv = A.ct_tmp[2 * j + 1];
@@ -1320,6 +1401,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                     for (int p = 0; p < OWGS_CTC; ++p) {
                         if (atomicCAS((uint32_t*)&ct[h], 0u, kk) == 0u) {
                             ct[h].y = vv;
+                            bf_add(bf, kk);
                             break;
                         }
                         h = (h + 1) & (OWGS_CTC - 1);
@@ -1365,6 +1447,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             st_sys(&A.ctl[OWGS_RES_RESULT], bail | (e << 8));
             st_sys(&A.ctl[OWGS_RES_USED], sc[RS_USED]);
+            st_sys(&A.ctl[OWGS_RES_TOMBS], sc[RS_TOMB]);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             st_sys(&A.ctl[OWGS_RES_DONE], k);
         }
