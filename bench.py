@@ -236,6 +236,7 @@ def shim_path(w, o_inv, dev_index, drains=(64, 512, 4096), budget_jobs=(120_000,
         for mode in modes:
             b.restore()
             rs0 = b.resident_stats()
+            hn0 = b.resident_table_fill()[2:]
             inv = np.full(len(act), -9, np.int32)
             fl = np.zeros(len(act), np.uint8)
             lat, clat, n_pub = [], [], 0
@@ -314,7 +315,9 @@ def shim_path(w, o_inv, dev_index, drains=(64, 512, 4096), budget_jobs=(120_000,
                          "bit_exact": exact,
                          # owgs_process_batch's paths in this leg: resident engine calls / launches, launch-chain calls
                          "resident": {k: rs1[k] - rs0[k] for k in rs1 if k not in ("alive", "last_call_ns")},
-                         "map_fill_max": fill[0], "map_deleted_max": fill[1]})
+                         "map_fill_max": fill[0], "map_deleted_max": fill[1],
+                         "host_build_us_mean": (fill[2] - hn0[0]) * 1e-3 / max(rs1["served"] - rs0["served"], 1),
+                         "host_wait_us_mean": (fill[3] - hn0[1]) * 1e-3 / max(rs1["served"] - rs0["served"], 1)})
     b.close()
     return {"path": "host buffers through the C ABI as the JNI shim calls it (queue order: each batch's completions, "
                     "then its publishes); calls = owgs_release_batch + owgs_publish_batch per run, fused = "

@@ -355,8 +355,9 @@ int owgs_engine_ms(owgs_ctx* ctx, float* ms);
  * the last owgs_publish_batch / owgs_release_batch / owgs_process_batch call, entry to return, timed inside the
  * library; [25] 1 when the last owgs_replay / owgs_replay_device(_span) ran through the resident engine's stream mode
  * (OWGS_SPEC_REPLAY), [26..44] that replay's counters [5..23] summed over its launch (a device synchronisation);
- * [45], [46] the largest primary-table fill (live + deleted entries) and deleted entries after a served call.
- * Returns the number of counters (47). */
+ * [45], [46] the largest primary-table fill (live + deleted entries) and deleted entries after a served call; [47],
+ * [48] host nanoseconds over the served calls: building the call (records, chunk ranks), bell to answer.  Returns the
+ * number of counters (49). */
 int owgs_resident_stats(owgs_ctx* ctx, int64_t* out, int32_t cap);
 
 /* Restore the slot state captured by owgs_snapshot (bench: every timed step starts from the same state). */

@@ -242,10 +242,11 @@ class GpuShardingContainerPoolBalancer:
                         (int(x) for x in out)))
 
     def resident_table_fill(self) -> tuple:
-        """The largest primary-table fill (live + deleted entries) and deleted entries after a served resident call."""
-        out = np.zeros(9 + 2 * _NRP, np.int64)
-        self._chk(min(0, self._L.owgs_resident_stats(self._h, _p(out), 9 + 2 * _NRP)))
-        return int(out[7 + 2 * _NRP]), int(out[8 + 2 * _NRP])
+        """The largest primary-table fill (live + deleted entries) and deleted entries after a served resident call,
+        and the host nanoseconds over served calls spent building them and waiting from bell to answer."""
+        out = np.zeros(11 + 2 * _NRP, np.int64)
+        self._chk(min(0, self._L.owgs_resident_stats(self._h, _p(out), 11 + 2 * _NRP)))
+        return tuple(int(x) for x in out[7 + 2 * _NRP:11 + 2 * _NRP])
 
     def stream_mode_stats(self) -> dict | None:
         """The last replay's resident-engine counters when it ran in stream mode (OWGS_SPEC_REPLAY), else None."""

@@ -319,6 +319,7 @@ struct owgs_ctx {
     int64_t res_n_calls = 0, res_n_launches = 0, res_n_bails = 0, res_n_chained = 0;
     int64_t res_prof[OWGS_RES_NPROF] = {};
     int64_t res_used_max = 0, res_tombs_max = 0;  // the primary table's fill after served calls (largest seen)
+    int64_t res_host_ns[2] = {};    // served calls: host time building the call (records, ranks), bell-to-answer wait
     DevBuf<uint2> d_res_cur;        // per action: {cursor generation, first walk step that may fit}
     std::vector<uint2> res_meta;    // act_meta as of the live launch (every change of it stops the engine first)
     uint32_t res_gen_seen = 0;      // the last cursor generation the engine reported
@@ -1033,6 +1034,7 @@ static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
                        const int32_t* rel_action, uint8_t* rel_flags, const int32_t* pub_off, const int32_t* pub_action,
                        const uint64_t* seq, uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, int* served) {
     *served = 0;
+    const auto th0 = std::chrono::steady_clock::now();
     const int32_t NR = rel_off[n_runs], NP = pub_off[n_runs];
     // the call's input block (16-byte aligned parts): rel_off | pub_off | release records | publish records | seq;
     // records are complete (action meta and slot key), so the engine's staging is a copy
@@ -1142,6 +1144,7 @@ static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
                              (int32_t)b_poff, (int32_t)b_rel, (int32_t)b_pub, (int32_t)b_seq, (int32_t)in_bytes,
                              (int32_t)(uint32_t)rsum, (int32_t)(uint32_t)(rsum >> 32)};
     for (int k = 0; k < 13; ++k) H[k] = hdr[k];
+    const auto th1 = std::chrono::steady_clock::now();
     for (int attempt = 0;; ++attempt) {
         const int32_t k = ++c->res_call;
         __atomic_store_n(&c->res_ctl[OWGS_RES_BELL], k, __ATOMIC_RELEASE);
@@ -1170,6 +1173,11 @@ static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
     }
     const int32_t res = __atomic_load_n(&c->res_ctl[OWGS_RES_RESULT], __ATOMIC_ACQUIRE);
     const int bail = res & 0xFF, e = res >> 8;
+    {
+        const auto th2 = std::chrono::steady_clock::now();
+        c->res_host_ns[0] += std::chrono::duration_cast<std::chrono::nanoseconds>(th1 - th0).count();
+        c->res_host_ns[1] += std::chrono::duration_cast<std::chrono::nanoseconds>(th2 - th1).count();
+    }
     if (bail) {
         ++c->res_n_bails;
         return OWGS_OK;  // nothing applied: the chained path takes the call
@@ -3452,7 +3460,9 @@ int owgs_resident_stats(owgs_ctx* c, int64_t* out, int32_t cap) {
     }
     if (cap > 7 + 2 * OWGS_RES_NPROF) out[7 + 2 * OWGS_RES_NPROF] = c->res_used_max;
     if (cap > 8 + 2 * OWGS_RES_NPROF) out[8 + 2 * OWGS_RES_NPROF] = c->res_tombs_max;
-    return 9 + 2 * OWGS_RES_NPROF;
+    if (cap > 9 + 2 * OWGS_RES_NPROF) out[9 + 2 * OWGS_RES_NPROF] = c->res_host_ns[0];
+    if (cap > 10 + 2 * OWGS_RES_NPROF) out[10 + 2 * OWGS_RES_NPROF] = c->res_host_ns[1];
+    return 11 + 2 * OWGS_RES_NPROF;
 }
 
 int owgs_engine_ms(owgs_ctx* c, float* ms) {

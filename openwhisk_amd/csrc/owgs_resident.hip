@@ -164,7 +164,7 @@ __device__ __forceinline__ void bf_add(uint32_t* bf, uint32_t key) {
 __device__ __forceinline__ int ct_lookup(const uint2* ct, const uint32_t* bf, uint32_t key, uint32_t* val) {
     uint32_t h = ct_home(key);
     *val = 0u;
-    {
+    if (bf) {  // (null: the caller tested the filter)
         const uint2 b = bf_pos(key);
         if ((bf[b.x] & b.y) != b.y) return -1;
     }
@@ -375,9 +375,9 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
         // wrote the records complete (action meta and slot key per publish and release), so staging is a copy: the
         // header and the first 4 KB of the block are read together (one PCIe round trip for a small call)
         int32_t* hdr = sc + 32;  // RS_HDR words
-        if (!smode) {
+        if (!smode) {  // (the block holds >= 4 KB: its capacity is larger; reading 16 KB at once measured slower)
             if (tid < OWGS_RES_NHDR) hdr[tid] = ld_sys(A.ctl + OWGS_RES_HDR + tid);
-            const uint4 v = ((const uint4*)A.in)[tid];  // (the block holds >= 4 KB: its capacity is larger)
+            const uint4 v = ((const uint4*)A.in)[tid];
             ((uint4*)stg)[tid] = v;
         }
         __syncthreads();
@@ -1009,62 +1009,87 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             const float rmx = __builtin_amdgcn_rcpf((float)max(l_maxc, 1));
                             bool cw = l_cc && !(me.w & RES_SHARED);
                             int cpos = cw ? mod_fast(l_home, l_n, __builtin_amdgcn_rcpf((float)l_n)) : 0, cst = 0;
+                            // 4 walk steps per round: their permits and Bloom-filter words read together, the map
+                            // probed only where the filter says the key may be
+                            const int cbudget = max(4, A.spec >> 2);  // (8 steps measured slower: longer rounds)
                             while (__ballot(cw)) {
                                 if (cw) {
-                                    const int id = l_base + cpos;
-                                    const int pv = P[id];
-                                    bool ok = false;
-                                    if (pv < OWGS_PLIM) {
-                                        const uint32_t key = ct_key(id, (int)me.z);
-                                        uint32_t v = 0u;
-                                        int ix = ct_lookup(ct, bf, key, &v);
-                                        if (ix < 0 && ovf_on) {
-                                            ++pr_ovf;
-                                            const int oj = ovf_find(A.ovf, key, &v);
-                                            ix = oj >= 0 ? OWGS_CTC + oj : -1;
-                                        }
-                                        const int c0 = (int)(v & OWGS_CT_C_MASK), o0 = ix >= 0 ? ct_ops(v) : 0;
-                                        int c1 = 0;
-                                        if (cneed < c0) {  // a free slot of the key's container
-                                            ok = true;
-                                            c1 = c0 - cneed - 1;
-                                        } else {  // containers the memory holds, maxConcurrent slots each
-                                            const int kp = cneed - c0;
-                                            int qc = (int)((float)kp * rmx);
-                                            qc -= qc * l_maxc > kp ? 1 : 0;
-                                            qc += (qc + 1) * l_maxc <= kp ? 1 : 0;
-                                            const int j = kp - qc * l_maxc;  // (kp < 64: exact)
-                                            if (pv >= (qc + 1) * l_mem) {
+                                    int idk[4], pvk[4];
+                                    bool bk[4];
+                                    int pp = cpos;
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k) {
+                                        idk[k] = l_base + pp;
+                                        pvk[k] = P[idk[k]];
+                                        pp += l_step;
+                                        pp -= pp >= l_n ? l_n : 0;
+                                    }
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k) {
+                                        const uint2 b = bf_pos(ct_key(idk[k], (int)me.z));
+                                        bk[k] = (bf[b.x] & b.y) == b.y;
+                                    }
+                                    int kf = 4;
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k) {
+                                        const int pv = pvk[k];
+                                        if (kf == 4 && cst + k < l_n && pv < OWGS_PLIM) {
+                                            const uint32_t key = ct_key(idk[k], (int)me.z);
+                                            uint32_t v = 0u;
+                                            int ix = bk[k] ? ct_lookup(ct, nullptr, key, &v) : -1;
+                                            if (ix < 0 && ovf_on) {
+                                                ++pr_ovf;
+                                                const int oj = ovf_find(A.ovf, key, &v);
+                                                ix = oj >= 0 ? OWGS_CTC + oj : -1;
+                                            }
+                                            const int c0 = (int)(v & OWGS_CT_C_MASK), o0 = ix >= 0 ? ct_ops(v) : 0;
+                                            bool ok = false;
+                                            int c1 = 0;
+                                            bool tk = false;
+                                            if (cneed < c0) {  // a free slot of the key's container
                                                 ok = true;
-                                                c_take = j == 0;
-                                                c1 = l_maxc - j - 1;
-                                            } else if (pv >= l_mem) {
-                                                int m = (int)((float)pv * rmem);
-                                                m -= m * l_mem > pv ? 1 : 0;
-                                                m += (m + 1) * l_mem <= pv ? 1 : 0;
-                                                cneed -= c0 + m * l_maxc;
-                                            } else {
-                                                cneed -= c0;
+                                                c1 = c0 - cneed - 1;
+                                            } else {  // containers the memory holds, maxConcurrent slots each
+                                                const int kp = cneed - c0;
+                                                int qc = (int)((float)kp * rmx);
+                                                qc -= qc * l_maxc > kp ? 1 : 0;
+                                                qc += (qc + 1) * l_maxc <= kp ? 1 : 0;
+                                                const int j = kp - qc * l_maxc;  // (kp < 64: exact)
+                                                if (pv >= (qc + 1) * l_mem) {
+                                                    ok = true;
+                                                    tk = j == 0;
+                                                    c1 = l_maxc - j - 1;
+                                                } else if (pv >= l_mem) {
+                                                    int m = (int)((float)pv * rmem);
+                                                    m -= m * l_mem > pv ? 1 : 0;
+                                                    m += (m + 1) * l_mem <= pv ? 1 : 0;
+                                                    cneed -= c0 + m * l_maxc;
+                                                } else {
+                                                    cneed -= c0;
+                                                }
+                                            }
+                                            if (ok) {
+                                                if (o0 + cneed + 1 > OWGS_MAX_OPS) err |= OWGS_ERR_OPS;
+                                                kf = k;
+                                                c_ix = ix;
+                                                c_take = tk;
+                                                c_nv = ct_val(c1, o0 + cneed + 1);
                                             }
                                         }
-                                        if (ok) {
-                                            if (o0 + cneed + 1 > OWGS_MAX_OPS) err |= OWGS_ERR_OPS;
-                                            c_ix = ix;
-                                            c_nv = ct_val(c1, o0 + cneed + 1);
-                                        }
                                     }
-                                    if (ok) {
+                                    if (kf < 4) {
                                         sp = SP_FOUND;
-                                        sp_t = id;
+                                        sp_t = kf == 0 ? idk[0] : kf == 1 ? idk[1] : kf == 2 ? idk[2] : idk[3];
                                         cw = false;
-                                    } else if (++cst >= l_n) {
-                                        if (c_rank == 0) sp = SP_FAIL;  // every pool position: forced below (a repeat:
-                                        cw = false;                     // decided alone)
-                                    } else if (cst >= max(1, A.spec >> 2)) {
-                                        cw = false;    // SP_STOP: decided alone (budget: a map lookup per step)
                                     } else {
-                                        cpos += l_step;
-                                        cpos -= cpos >= l_n ? l_n : 0;
+                                        cst += 4;
+                                        cpos = pp;
+                                        if (cst >= l_n) {
+                                            if (c_rank == 0) sp = SP_FAIL;  // every pool position: forced below (a
+                                            cw = false;                     // repeat: decided alone)
+                                        } else if (cst >= cbudget) {
+                                            cw = false;  // SP_STOP: decided alone
+                                        }
                                     }
                                 }
                             }
