@@ -60,11 +60,6 @@ __device__ __forceinline__ int wave_max_i(int v) {
     for (int d = 32; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d, 64));
     return v;
 }
-__device__ __forceinline__ int wave_or_i(int v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v |= __shfl_xor(v, d, 64);
-    return v;
-}
 __device__ __forceinline__ int wave_min_i(int v) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v = min(v, __shfl_xor(v, d, 64));
@@ -122,7 +117,7 @@ __device__ __forceinline__ int select_in_word(uint32_t m, int need) {
 #define RES_CLEAN_TOMBS (OWGS_CTC / 8)
 #endif
 struct ResLayout {
-    uint32_t P, ub, pc, ct, sc, cc, mv, bf, cr, stage, end;
+    uint32_t P, ub, pc, ct, sc, cc, mv, bf, stage, end;
 };
 __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
     const uint32_t words = (uint32_t)(n_ids + 31) / 32;
@@ -135,8 +130,7 @@ __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
     y.cc = y.sc + 64u * 4u;
     y.mv = y.cc + RES_CC * 8u;
     y.bf = y.mv + 64u * 4u;
-    y.cr = y.bf + RES_BF * 4u;
-    y.stage = y.cr + 64u * 16u;
+    y.stage = y.bf + RES_BF * 4u;
     y.end = y.stage;
     return y;
 }
@@ -154,9 +148,6 @@ __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
 #define RS_U0 10     // upper bound of every usable permit count of the managed / blackbox pool
 #define RS_U1 11
 #define RS_TOMB 12   // deleted primary entries (the cleanup between calls runs when they pile up)
-#define RS_OVFON 13  // the map's overflow holds entries (wave 0's view, for wave 1's lookups)
-#define RS_PCW 14    // wave 1's concurrent-walk cycles and overflow lookups in the call
-#define RS_PCO 15
 
 // blocked Bloom filter over the primary table's keys (LDS, RES_BF words): one word and three bits per key, set on
 // every insert into the primary and rebuilt with it; a key whose bits are not all set is not in the primary, so a
@@ -216,7 +207,6 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
     uint2* cc = (uint2*)(Lb + Y.cc);
     int32_t* mv = (int32_t*)(Lb + Y.mv);
     uint32_t* bf = (uint32_t*)(Lb + Y.bf);
-    uint4* cres = (uint4*)(Lb + Y.cr);  // a chunk's concurrent speculation (wave 1) for wave 0's validation
     char* stg = Lb + Y.stage;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int n_slots = A.n_slots, nm = A.nm, nb = A.nb;
@@ -402,10 +392,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
         const uint32_t s_cur = (s_in + 15u) & ~15u, s_out = (s_cur + 8u * (uint32_t)NP + 15u) & ~15u;
         const uint32_t s_ofl = s_out + 4u * (uint32_t)NP, s_orf = s_ofl + (uint32_t)NP;
         const uint32_t s_end = (s_orf + (uint32_t)NR + 15u) & ~15u;
-        if (tid == 0) {
-            sc[RS_BAIL] = s_end > (uint32_t)A.stage_bytes ? OWGS_RES_BAIL_STAGE : 0;
-            sc[RS_PCW] = sc[RS_PCO] = 0;
-        }
+        if (tid == 0) sc[RS_BAIL] = s_end > (uint32_t)A.stage_bytes ? OWGS_RES_BAIL_STAGE : 0;
         __syncthreads();
         int32_t* roff = (int32_t*)(stg);
         int32_t* poff = (int32_t*)(stg + s_poff);
@@ -570,7 +557,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
             __syncthreads();
         }
         const int bail = sc[RS_BAIL];
-        if (bail == 0) {  // (wave 0 decides; wave 1 speculates each chunk's concurrent decisions beside it)
+        if (bail == 0 && wave == 0) {
             int err = 0;
             bool ovf_on = sc[RS_OVF] > 0;
             int used = sc[RS_USED], tombs = 0;  // (tombs: per lane, deleted entries made - reused this call)
@@ -618,7 +605,6 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
             };
             for (int r = 0; r < n_runs; ++r) {
                 // ---- completions of run r (releaseInvoker SCPB:327-331 via processCompletion CLB:260-346)
-                if (wave == 0) {
                 const int rb = roff[r], re = roff[r + 1];
                 if (re > rb) {
                     ++gen;  // permits may rise: every walk cursor of an earlier generation is stale
@@ -735,7 +721,6 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 }
                 const u64 tr1 = clock64();
                 pr_rel += tr1 - tr0;
-                }
                 // ---- publishes of run r (SCPB:257-290 -> schedule SCPB:398-436)
                 const int pb = poff[r], pe = poff[r + 1];
                 const u64 tp0 = clock64();
@@ -944,15 +929,13 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                         // rank among the chunk's publishes of my action (one walk, one memory size), from the record
                         const int l_rank = (int)((me.w >> RES_RANK_SHIFT) & 63u);
                         int need = l_plain ? l_rank : 0;
-                        if (wave == 0 && lane == 0) sc[RS_OVFON] = ovf_on ? 1 : 0;
-                        __syncthreads();  // wave 0's commits of the chunk before are in LDS (and its view of the map)
                         const u64 tm1 = clock64();
                         pr_c_match += tm1 - tsp0;
                         const int rank = need;
                         const float rmem = __builtin_amdgcn_rcpf((float)max(l_mem, 1));
                         bool walking = false;
                         int wp = 0, ws = l_sbeg;
-                        if (l_c1 && wave == 0) {
+                        if (l_c1) {
                             if (!l_plain || l_sbeg >= l_n) {
                                 sp = SP_FAIL;  // mem above the pool's bound U, or a cursor past every step
                             } else {
@@ -1018,7 +1001,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                         int c_ix = -1;        // the target's map entry (primary index, OWGS_CTC + overflow index, -1 none)
                         uint32_t c_nv = 0u;   // the entry's value after this decision
                         bool c_take = false;  // the decision opens a container: it takes memory (NS:70-79)
-                        if (wave == 1 && __ballot(l_cc)) {
+                        if (__ballot(l_cc)) {
                             // another action of the same key earlier in the chunk walks differently and shares the
                             // key's entries: its effect on mine is not predicted, so such a decision is decided alone
                             const int c_rank = l_rank;
@@ -1054,7 +1037,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                             const uint32_t key = ct_key(idk[k], (int)me.z);
                                             uint32_t v = 0u;
                                             int ix = bk[k] ? ct_lookup(ct, nullptr, key, &v) : -1;
-                                            if (ix < 0 && sc[RS_OVFON]) {
+                                            if (ix < 0 && ovf_on) {
                                                 ++pr_ovf;
                                                 const int oj = ovf_find(A.ovf, key, &v);
                                                 ix = oj >= 0 ? OWGS_CTC + oj : -1;
@@ -1124,7 +1107,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 if (sp_t < 0) err |= OWGS_ERR_INTERNAL;
                                 else if (l_cc) {  // forceAcquireConcurrent: a free slot of the key's container there, or memory
                                     uint32_t v = 0u;
-                                    c_ix = ct_lookup2(ct, bf, A.ovf, sc[RS_OVFON] != 0, ct_key(sp_t, (int)me.z), &v);
+                                    c_ix = ct_lookup2(ct, bf, A.ovf, ovf_on, ct_key(sp_t, (int)me.z), &v);
                                     const int c0 = (int)(v & OWGS_CT_C_MASK), o0 = c_ix >= 0 ? ct_ops(v) : 0;
                                     c_take = c0 == 0;
                                     c_nv = ct_val(c_take ? l_maxc - 1 : c0 - 1, o0 + 1);
@@ -1135,29 +1118,6 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 o_v = OWGS_NONE_V;
                             }
                             sp_ts = l_n;
-                        }
-                        if (wave == 1) {  // the concurrent outcomes to wave 0
-                            if (l_cc)
-                                cres[lane] = make_uint4((uint32_t)sp | (c_take ? 16u : 0u) | (o_f ? 32u : 0u),
-                                                        (uint32_t)(sp == SP_TRIV ? o_v : sp_t), (uint32_t)c_ix, c_nv);
-                            const int e1 = wave_or_i(err);
-                            if (lane == 0) {
-                                if (e1) atomicOr(&sc[RS_ERR], e1);
-                                atomicAdd((uint32_t*)&sc[RS_PCW], (uint32_t)min(clock64() - tm2, (u64)0xFFFFFFF));
-                            }
-                            err = 0;
-                        }
-                        __syncthreads();  // wave 1's outcomes are in LDS
-                        if (wave == 0) {
-                        if (l_cc) {
-                            const uint4 cr = cres[lane];
-                            sp = (int)(cr.x & 15u);
-                            c_take = (cr.x & 16u) != 0u;
-                            if (cr.x & 32u) o_f = 1;
-                            if (sp == SP_TRIV) o_v = (int)cr.y;
-                            else sp_t = (int)cr.y;
-                            c_ix = (int)cr.z;
-                            c_nv = cr.w;
                         }
                         // (a repeat's outcome holds once the repeats before it are decided, so only the first of
                         // each action proves anything about the state at the chunk's start: the bound U, the cursor)
@@ -1260,8 +1220,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             }
                             q = f + 1;
                         }
-                        }  // wave 0
-                    } else if (wave == 0) {
+                    } else {
                         for (int q = 0; q < nq; ++q) {
                             // ---- up to 4 consecutive plain decisions walk together, 16 lanes each (4 probes per lane:
                             // 64 walk steps per round), against the state before all of them; then in stream order
@@ -1373,7 +1332,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                         }
                     }
                     pr_dec += nq;
-                    if (wave == 0 && lane < nq) {
+                    if (lane < nq) {
                         out_inv[i0 + lane] = o_v;
                         out_fl[i0 + lane] = (uint8_t)o_f;
                     }
@@ -1381,7 +1340,6 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 pr_pub += clock64() - tp0;
             }
             // the call's releases may have raised permits: the range bound grows by what they returned at most
-            if (wave == 0) {
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) err |= __shfl_xor(err, d, 64);
 #pragma unroll
@@ -1441,7 +1399,6 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 sc[RS_MAXP] = (int)min(mp, (long long)0x7FFFFFFF);
                 if (err) atomicOr(&sc[RS_ERR], err);
             }
-            }  // wave 0
         }
         __syncthreads();
         // ---- primary-table cleanup between calls: deleted entries keep chains long and fill the primary
