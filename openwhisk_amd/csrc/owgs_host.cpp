@@ -1014,7 +1014,7 @@ static int res_launch(owgs_ctx* c) {
     a.out = c->res_out;
     a.stage_bytes = (int32_t)res_stage_bytes(c);
     a.last_call = c->res_call;
-    a.cur = c->d_res_cur.p;
+    a.cur = c->d_res_cur.p;  // (dropping them measured slower: drains inside a batch's publishes keep the generation)
     a.gen_base = ++c->res_gen_seen;  // above every generation stored by earlier launches
     a.idle_ticks = env_opts().res_idle_us * 100;  // s_memrealtime: 100 MHz
     a.spec = std::max(0, env_opts().res_spec);
