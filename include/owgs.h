@@ -166,6 +166,10 @@ int owgs_set_pool(owgs_ctx* ctx, int32_t pool, int32_t n, const int32_t* ids, co
 int owgs_read_permits(owgs_ctx* ctx, int32_t* out, int32_t cap, int32_t* n_slots);
 int owgs_read_concurrent(owgs_ctx* ctx, int32_t invoker, int32_t key, int32_t* permits, int32_t* op_count);
 int owgs_key_id(owgs_ctx* ctx, int32_t action);
+/* Diagnostics (synchronises): the NestedSemaphore map's fill -- live and deleted entries of the on-chip primary table,
+ * entries (live + deleted) and capacity of the HBM overflow. */
+int owgs_map_fill(owgs_ctx* ctx, int32_t* primary_live, int32_t* primary_deleted, int32_t* overflow_entries,
+                  int32_t* overflow_cap);
 int owgs_state_info(owgs_ctx* ctx, int32_t* n_invokers, int32_t* managed, int32_t* blackbox, int32_t* cluster_size);
 int owgs_step_sizes(owgs_ctx* ctx, int32_t pool, int32_t* out, int32_t cap, int32_t* n);
 

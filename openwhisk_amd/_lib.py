@@ -112,6 +112,7 @@ def lib() -> C.CDLL:
         "owgs_read_permits": (C.c_int, [P, P, i32, P]),
         "owgs_read_concurrent": (C.c_int, [P, i32, i32, P, P]),
         "owgs_key_id": (C.c_int, [P, i32]),
+        "owgs_map_fill": (C.c_int, [P, P, P, P, P]),
         "owgs_release_actions": (C.c_int, [P, i32, P]),
         "owgs_geometry_selfcheck": (C.c_int, []),
         "owgs_state_info": (C.c_int, [P, P, P, P, P]),

@@ -241,6 +241,12 @@ class GpuShardingContainerPoolBalancer:
         return dict(zip(("served", "launches", "refused", "chained", "alive") + _RES_PROF + ("last_call_ns",),
                         (int(x) for x in out)))
 
+    def map_fill(self) -> dict:
+        """The NestedSemaphore map's fill: live / deleted primary (LDS-image) entries, overflow entries and capacity."""
+        v = [C.c_int32(0) for _ in range(4)]
+        self._chk(self._L.owgs_map_fill(self._h, *[C.byref(x) for x in v]))
+        return dict(zip(("primary_live", "primary_deleted", "overflow_entries", "overflow_cap"), (x.value for x in v)))
+
     def resident_table_fill(self) -> tuple:
         """The largest primary-table fill (live + deleted entries) and deleted entries after a served resident call,
         and the host nanoseconds over served calls spent building them and waiting from bell to answer."""

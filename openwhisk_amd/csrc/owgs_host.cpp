@@ -1935,6 +1935,31 @@ int owgs_read_concurrent(owgs_ctx* c, int32_t invoker, int32_t key, int32_t* per
     return 1;
 }
 
+int owgs_map_fill(owgs_ctx* c, int32_t* primary_live, int32_t* primary_deleted, int32_t* overflow_entries,
+                  int32_t* overflow_cap) {
+    if (!c) return OWGS_EINVAL;
+    OWGS_ENTER(c);
+    {
+        const int ro_ = order_on(c, c->stream);
+        if (ro_) return ro_;
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::vector<uint32_t> k(OWGS_CTC);
+    int32_t oc = 0;
+    if (c->d_ct_keys.p) HIPCHK(c, hipMemcpy(k.data(), c->d_ct_keys.p, OWGS_CTC * 4, hipMemcpyDeviceToHost));
+    if (c->ovf_cap > 0 && c->d_ovf_cnt.p) HIPCHK(c, hipMemcpy(&oc, c->d_ovf_cnt.p, 4, hipMemcpyDeviceToHost));
+    int32_t live = 0, del = 0;
+    for (uint32_t x : k) {
+        live += x != 0u && x != OWGS_CT_TOMB;
+        del += x == OWGS_CT_TOMB;
+    }
+    if (primary_live) *primary_live = c->d_ct_keys.p ? live : 0;
+    if (primary_deleted) *primary_deleted = c->d_ct_keys.p ? del : 0;
+    if (overflow_entries) *overflow_entries = oc;
+    if (overflow_cap) *overflow_cap = c->ovf_cap;
+    return OWGS_OK;
+}
+
 int owgs_key_id(owgs_ctx* c, int32_t action) {
     if (!c || action < 0 || action >= (int32_t)c->a_slot.size() || !c->a_live[action]) return OWGS_ENOENT;
     return c->a_slot[action];
