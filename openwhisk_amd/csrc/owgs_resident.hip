@@ -1190,7 +1190,42 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             // entries absent at the chunk's start, one at a time in stream order (lane 0): the first
                             // decision of a key at an invoker inserts it, the later ones find it
                             const u64 ti0 = clock64();
-                            for (u64 ins = __ballot(cand && lane < f && l_cc && c_ix < 0); ins; ins &= ins - 1ull) {
+                            u64 insm = __ballot(cand && lane < f && l_cc && c_ix < 0);
+                            if (insm && !ovf_on && used + (int)__popcll(insm) < OWGS_CT_LDS_FILL) {
+                                // all at once while the primary has room for every one of them: each lane walks its
+                                // key's chain from its home and claims the first empty or deleted entry by CAS; lanes
+                                // of one key race for the same entry, the losers find the key there and merge their
+                                // value (operationCount order: atomicMax), lanes of other keys move on
+                                bool fresh = false;
+                                if ((insm >> lane) & 1ull) {
+                                    const uint32_t key = ct_key(sp_t, (int)me.z);
+                                    uint32_t h = ct_home(key);
+                                    for (int p = 0; p < OWGS_CTC;) {
+                                        const uint32_t k = ct[h].x;
+                                        if (k == key) {
+                                            atomicMax(&ct[h].y, c_nv);
+                                            break;
+                                        }
+                                        if (k == 0u || k == OWGS_CT_TOMB) {
+                                            const uint32_t old = atomicCAS((uint32_t*)&ct[h].x, k, key);
+                                            if (old == k) {
+                                                atomicMax(&ct[h].y, c_nv);  // (a free entry holds value 0)
+                                                bf_add(bf, key);
+                                                fresh = k == 0u;
+                                                tombs -= k == OWGS_CT_TOMB;
+                                                break;
+                                            }
+                                            continue;  // lost the entry: read it again
+                                        }
+                                        h = (h + 1) & (OWGS_CTC - 1);
+                                        ++p;
+                                    }
+                                }
+                                used = __builtin_amdgcn_readfirstlane(used) + (int)__popcll(__ballot(fresh));
+                                insm = 0ull;
+                                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                            }
+                            for (u64 ins = insm; ins; ins &= ins - 1ull) {
                                 const int j = ffs64(ins);
                                 const uint32_t key = ct_key(__builtin_amdgcn_readlane(sp_t, j),
                                                             __builtin_amdgcn_readlane((int)me.z, j));
