@@ -955,7 +955,7 @@ static bool res_eligible(const owgs_ctx* c, int32_t n_runs, int32_t NR, int32_t 
         c->nb > (int32_t)OWGS_AM_POS_MASK || c->a_mem.empty())
         return false;
     const size_t runs = ((size_t)n_runs + 4) & ~(size_t)3;
-    const size_t in_b = 8 * runs + 16 * (size_t)NR + 16 * (size_t)NP + (has_seq ? 8 * (size_t)NP : 0);
+    const size_t in_b = 8 * runs + (4 * (size_t)NP + 16) + 16 * (size_t)NR + 16 * (size_t)NP + (has_seq ? 8 * (size_t)NP : 0);
     const size_t need = in_b + 8 * (size_t)NP + 16 + 5 * (size_t)NP + (size_t)NR + 32;  // + cursors, outputs
     if (need > res_stage_bytes(c) || res_stage_bytes(c) < 4096) return false;
     // a map that may outgrow its overflow table during the call: the chained path grows it
@@ -1036,10 +1036,12 @@ static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
     *served = 0;
     const auto th0 = std::chrono::steady_clock::now();
     const int32_t NR = rel_off[n_runs], NP = pub_off[n_runs];
-    // the call's input block (16-byte aligned parts): rel_off | pub_off | release records | publish records | seq;
-    // records are complete (action meta and slot key), so the engine's staging is a copy
+    // the call's input block (16-byte aligned parts): rel_off | pub_off | publish action handles | release records |
+    // publish records | seq; records are complete (action meta and slot key), so the engine's staging is a copy; the
+    // handles come early so that the engine gathers the walk cursors while the rest of the block crosses PCIe
     auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
-    const size_t b_poff = al(4 * ((size_t)n_runs + 1)), b_rel = b_poff + al(4 * ((size_t)n_runs + 1));
+    const size_t b_poff = al(4 * ((size_t)n_runs + 1)), b_aid = b_poff + al(4 * ((size_t)n_runs + 1));
+    const size_t b_rel = b_aid + al(4 * (size_t)NP);
     const size_t b_pub = b_rel + 16 * (size_t)NR, b_seq = b_pub + 16 * (size_t)NP;
     const size_t in_bytes = al(b_seq + (seq ? 8 * (size_t)NP : 0));
     const size_t o_fl = 4 * (size_t)NP, o_rfl = o_fl + NP, out_bytes = al(o_rfl + NR) + 16;
@@ -1070,6 +1072,7 @@ static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
     char* B = (char*)c->res_in;
     memcpy(B, rel_off, 4 * ((size_t)n_runs + 1));
     memcpy(B + b_poff, pub_off, 4 * ((size_t)n_runs + 1));
+    if (NP) memcpy(B + b_aid, pub_action, 4 * (size_t)NP);
     uint64_t rsum = 0;
     uint32_t* R = (uint32_t*)(B + b_rel);
     for (int32_t j = 0; j < NR; ++j) {
@@ -1140,10 +1143,10 @@ static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
     }
     if (seq && NP) memcpy(B + b_seq, seq, 8 * (size_t)NP);
     volatile int32_t* H = c->res_ctl + OWGS_RES_HDR;
-    const int32_t hdr[13] = {n_runs, NR, NP, seq ? 1 : 0, (int32_t)(uint32_t)seq_base, (int32_t)(uint32_t)(seq_base >> 32),
+    const int32_t hdr[14] = {n_runs, NR, NP, seq ? 1 : 0, (int32_t)(uint32_t)seq_base, (int32_t)(uint32_t)(seq_base >> 32),
                              (int32_t)b_poff, (int32_t)b_rel, (int32_t)b_pub, (int32_t)b_seq, (int32_t)in_bytes,
-                             (int32_t)(uint32_t)rsum, (int32_t)(uint32_t)(rsum >> 32)};
-    for (int k = 0; k < 13; ++k) H[k] = hdr[k];
+                             (int32_t)(uint32_t)rsum, (int32_t)(uint32_t)(rsum >> 32), (int32_t)b_aid};
+    for (int k = 0; k < 14; ++k) H[k] = hdr[k];
     const auto th1 = std::chrono::steady_clock::now();
     for (int attempt = 0;; ++attempt) {
         const int32_t k = ++c->res_call;

@@ -321,8 +321,9 @@ struct OwgsReleaseArgs {
                            // releases' concurrent part)
 #define OWGS_RES_HDR 64     // host: the call -- n_runs, n_rel, n_pub, has_seq, seq_base lo, hi, then byte offsets in
                             // the input block of pub_off, the release records, the publish records, seq (u64), the
-                            // block's length, and the memory the releases return at most (lo, hi).  The block:
-                            // rel_off i32[n_runs + 1] | pub_off | releases uint4 {invoker, meta.y, slot, -} |
+                            // block's length, the memory the releases return at most (lo, hi), and the byte
+                            // offset of the publish action handles.  The block: rel_off i32[n_runs + 1] | pub_off |
+                            // publish action handles i32[n_pub] | releases uint4 {invoker, meta.y, slot, -} |
                             // publishes uint4 {meta.x, meta.y, slot, action} | seq u64[n_pub], 16-byte aligned parts.
                             // Outputs (block `out`): out_inv i32[n_pub] | out_flags u8[n_pub] | rel_flags u8[n_rel]
 #define OWGS_RES_NHDR 16

@@ -522,6 +522,20 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 }
             }
         } else if (sc[RS_BAIL] == 0) {
+            // the publishes' walk cursors, gathered from HBM while the rest of the block crosses PCIe when their
+            // action handles came with the first 4 KB (at most 1024 publishes: 4 per thread)
+            const uint32_t s_aid = (uint32_t)hdr[13];
+            const bool early = A.cur && NP <= 1024 && s_aid + 4u * (uint32_t)NP <= 4096u;
+            uint2 cu[4];
+            if (early) {
+                const int32_t* aid = (const int32_t*)(stg + s_aid);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = tid + 256 * u;
+                    const uint32_t a = i < NP ? (uint32_t)aid[i] : 0xFFFFFFFFu;
+                    cu[u] = a < (uint32_t)A.n_actions ? A.cur[a] : make_uint2(0u, 0u);
+                }
+            }
             // the rest of a block beyond 4 KB, four 16-byte reads in flight per thread
             for (uint32_t o = 4096u + 16u * tid; o < s_in; o += 4u * 16u * 256u) {
                 uint4 v[4];
@@ -538,9 +552,15 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
             }
             __syncthreads();
             // every publish's walk cursor (one gather: the decision loop then waits on nothing in HBM)
-            for (int i = tid; i < NP; i += 256) {
-                const uint32_t a = pub[i].w & RES_ACT_MASK;
-                pcur[i] = (A.cur && a < (uint32_t)A.n_actions) ? A.cur[a] : make_uint2(0u, 0u);
+            if (early) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (tid + 256 * u < NP) pcur[tid + 256 * u] = cu[u];
+            } else {
+                for (int i = tid; i < NP; i += 256) {
+                    const uint32_t a = pub[i].w & RES_ACT_MASK;
+                    pcur[i] = (A.cur && a < (uint32_t)A.n_actions) ? A.cur[a] : make_uint2(0u, 0u);
+                }
             }
         }
         __syncthreads();
