@@ -108,6 +108,9 @@ __device__ __forceinline__ int select_in_word(uint32_t m, int need) {
 
 #define RES_CC 2048  // walk-cursor cache entries (LDS, 16 KB)
 #define RES_BF 2048  // Bloom filter words over the primary table's keys (LDS, 8 KB)
+#ifndef RES_FIRST_READ_KB
+#define RES_FIRST_READ_KB 4  // a call's input block: KB read together with the header (the rest in a second round)
+#endif
 // the primary table is rebuilt between calls once it holds more than RES_CLEAN_USED entries of which at least
 // RES_CLEAN_TOMBS are deleted ones (deleted entries lengthen every probe chain through them)
 #ifndef RES_CLEAN_USED
@@ -377,8 +380,14 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
         int32_t* hdr = sc + 32;  // RS_HDR words
         if (!smode) {  // (the block holds >= 4 KB: its capacity is larger; reading 16 KB at once measured slower)
             if (tid < OWGS_RES_NHDR) hdr[tid] = ld_sys(A.ctl + OWGS_RES_HDR + tid);
+#if RES_FIRST_READ_KB == 8
+            const uint4 v0 = ((const uint4*)A.in)[tid], v1 = ((const uint4*)A.in)[tid + 256];
+            ((uint4*)stg)[tid] = v0;
+            if (16 * (tid + 256) < A.stage_bytes) ((uint4*)stg)[tid + 256] = v1;
+#else
             const uint4 v = ((const uint4*)A.in)[tid];
             ((uint4*)stg)[tid] = v;
+#endif
         }
         __syncthreads();
         const int n_runs = hdr[0], NR = hdr[1], NP = hdr[2], has_seq = hdr[3];
@@ -525,7 +534,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
             // the publishes' walk cursors, gathered from HBM while the rest of the block crosses PCIe when their
             // action handles came with the first 4 KB (at most 1024 publishes: 4 per thread)
             const uint32_t s_aid = (uint32_t)hdr[13];
-            const bool early = A.cur && NP <= 1024 && s_aid + 4u * (uint32_t)NP <= 4096u;
+            const bool early = A.cur && NP <= 1024 && s_aid + 4u * (uint32_t)NP <= 1024u * RES_FIRST_READ_KB;
             uint2 cu[4];
             if (early) {
                 const int32_t* aid = (const int32_t*)(stg + s_aid);
@@ -537,7 +546,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 }
             }
             // the rest of a block beyond 4 KB, four 16-byte reads in flight per thread
-            for (uint32_t o = 4096u + 16u * tid; o < s_in; o += 4u * 16u * 256u) {
+            for (uint32_t o = 1024u * RES_FIRST_READ_KB + 16u * tid; o < s_in; o += 4u * 16u * 256u) {
                 uint4 v[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
