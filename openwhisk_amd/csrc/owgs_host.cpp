@@ -955,8 +955,10 @@ static bool res_eligible(const owgs_ctx* c, int32_t n_runs, int32_t NR, int32_t 
         c->nb > (int32_t)OWGS_AM_POS_MASK || c->a_mem.empty())
         return false;
     const size_t runs = ((size_t)n_runs + 4) & ~(size_t)3;
-    const size_t in_b = 8 * runs + (4 * (size_t)NP + 16) + 16 * (size_t)NR + 16 * (size_t)NP + (has_seq ? 8 * (size_t)NP : 0);
-    const size_t need = in_b + 8 * (size_t)NP + 16 + 5 * (size_t)NP + (size_t)NR + 32;  // + cursors, outputs
+    const size_t in_b = 8 * runs + (4 * (size_t)NP + 16) + 2 * (4 * (size_t)NR + 16) + (has_seq ? 8 * (size_t)NP : 0);
+    // + the records the engine gathers, cursors, outputs
+    const size_t need = in_b + 16 + 16 * (size_t)NR + 16 * (size_t)NP + 8 * (size_t)NP + 16 + 5 * (size_t)NP +
+                        (size_t)NR + 32;
     if (need > res_stage_bytes(c) || res_stage_bytes(c) < 4096) return false;
     // a map that may outgrow its overflow table during the call: the chained path grows it
     if (c->any_conc && c->res_alive && c->ovf_cap < ovf_need(c->ovf_used_ub, NP)) return false;
@@ -1036,13 +1038,14 @@ static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
     *served = 0;
     const auto th0 = std::chrono::steady_clock::now();
     const int32_t NR = rel_off[n_runs], NP = pub_off[n_runs];
-    // the call's input block (16-byte aligned parts): rel_off | pub_off | publish action handles | release records |
-    // publish records | seq; records are complete (action meta and slot key), so the engine's staging is a copy; the
-    // handles come early so that the engine gathers the walk cursors while the rest of the block crosses PCIe
+    // the call's input block (16-byte aligned parts): rel_off | pub_off | publish words (action | rank << 17 |
+    // shared << 23) | release invokers | release actions | seq.  Handles only: the engine gathers each record's
+    // action meta and slot key from HBM, so a call of up to ~1000 jobs crosses PCIe in the engine's first 4 KB read
     auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
     const size_t b_poff = al(4 * ((size_t)n_runs + 1)), b_aid = b_poff + al(4 * ((size_t)n_runs + 1));
-    const size_t b_rel = b_aid + al(4 * (size_t)NP);
-    const size_t b_pub = b_rel + 16 * (size_t)NR, b_seq = b_pub + 16 * (size_t)NP;
+    const size_t b_rel = b_aid + al(4 * (size_t)NP);   // release invokers
+    const size_t b_pub = b_rel + al(4 * (size_t)NR);   // release actions
+    const size_t b_seq = b_pub + al(4 * (size_t)NR);
     const size_t in_bytes = al(b_seq + (seq ? 8 * (size_t)NP : 0));
     const size_t o_fl = 4 * (size_t)NP, o_rfl = o_fl + NP, out_bytes = al(o_rfl + NR) + 16;
     if (std::max<size_t>(in_bytes, 4096) > c->res_in_cap || out_bytes > c->res_out_cap) {  // (the engine holds the
@@ -1072,25 +1075,14 @@ static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
     char* B = (char*)c->res_in;
     memcpy(B, rel_off, 4 * ((size_t)n_runs + 1));
     memcpy(B + b_poff, pub_off, 4 * ((size_t)n_runs + 1));
-    if (NP) memcpy(B + b_aid, pub_action, 4 * (size_t)NP);
+    if (NR) {
+        memcpy(B + b_rel, rel_invoker, 4 * (size_t)NR);
+        memcpy(B + b_pub, rel_action, 4 * (size_t)NR);
+    }
     uint64_t rsum = 0;
-    uint32_t* R = (uint32_t*)(B + b_rel);
-    for (int32_t j = 0; j < NR; ++j) {
-        const int32_t a = rel_action[j], inv = rel_invoker[j];
-        R[4 * j] = (uint32_t)inv;
-        R[4 * j + 1] = c->res_meta[a].y;
-        R[4 * j + 2] = (uint32_t)c->a_slot[a];
-        R[4 * j + 3] = 0u;
-        if (inv >= 0 && inv < c->n_slots) rsum += (uint64_t)c->a_mem[a];
-    }
-    uint32_t* Q = (uint32_t*)(B + b_pub);
-    for (int32_t i = 0; i < NP; ++i) {
-        const int32_t a = pub_action[i];
-        Q[4 * i] = c->res_meta[a].x;
-        Q[4 * i + 1] = c->res_meta[a].y;
-        Q[4 * i + 2] = (uint32_t)c->a_slot[a];
-        Q[4 * i + 3] = (uint32_t)a;
-    }
+    for (int32_t j = 0; j < NR; ++j)
+        if (rel_invoker[j] >= 0 && rel_invoker[j] < c->n_slots) rsum += (uint64_t)c->a_mem[rel_action[j]];
+    uint32_t* Q = (uint32_t*)(B + b_aid);
     // per chunk of 64 publishes of a run (the engine's speculation unit): each publish's rank among the chunk's
     // publishes of its action, and whether an earlier concurrent publish of the chunk has its fqn@version key under
     // another action (owgs_resident.hip, RES_RANK_SHIFT / RES_SHARED)
@@ -1135,7 +1127,7 @@ static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
                         else if (ts.w[hs] != a) ts.v[hs] = 1;                // a second action: later ones are shared
                         if (ts.w[hs] != a || ts.v[hs]) wd |= 1u << 23;
                     }
-                    Q[4 * i + 3] = wd;
+                    Q[i] = wd;
                 }
                 ta.clear();
                 ts.clear();

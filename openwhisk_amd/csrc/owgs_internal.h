@@ -320,11 +320,13 @@ struct OwgsReleaseArgs {
                            // rank matching, plain walks, concurrent walks; validation's entry inserts; the
                            // releases' concurrent part)
 #define OWGS_RES_HDR 64     // host: the call -- n_runs, n_rel, n_pub, has_seq, seq_base lo, hi, then byte offsets in
-                            // the input block of pub_off, the release records, the publish records, seq (u64), the
+                            // the input block of pub_off, the release invokers, the release actions, seq (u64), the
                             // block's length, the memory the releases return at most (lo, hi), and the byte
-                            // offset of the publish action handles.  The block: rel_off i32[n_runs + 1] | pub_off |
-                            // publish action handles i32[n_pub] | releases uint4 {invoker, meta.y, slot, -} |
-                            // publishes uint4 {meta.x, meta.y, slot, action} | seq u64[n_pub], 16-byte aligned parts.
+                            // offset of the publish words.  The block: rel_off i32[n_runs + 1] | pub_off |
+                            // publish words u32[n_pub] (action | rank << 17 | shared << 23) | release invokers
+                            // i32[n_rel] | release actions i32[n_rel] | seq u64[n_pub], 16-byte aligned parts (the
+                            // engine gathers each record's action meta and slot key from HBM; stream mode's header
+                            // names its record arrays in LDS instead: see spec_replay).
                             // Outputs (block `out`): out_inv i32[n_pub] | out_flags u8[n_pub] | rel_flags u8[n_rel]
 #define OWGS_RES_NHDR 16
 #define OWGS_RES_CTL_WORDS 128

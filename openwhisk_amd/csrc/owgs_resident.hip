@@ -374,9 +374,10 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
         if (k < 0) break;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the host's inputs, written before the bell
         const u64 t_call = clock64();
-        // ---- the call: its header (control block) and its input block (pinned host memory) into LDS.  The host
-        // wrote the records complete (action meta and slot key per publish and release), so staging is a copy: the
-        // header and the first 4 KB of the block are read together (one PCIe round trip for a small call)
+        // ---- the call: its header (control block) and its input block (pinned host memory) into LDS.  The block holds
+        // handles only (a word per publish: action, rank, shared flag; an invoker and an action per release): the
+        // engine gathers each record's action meta and slot key from HBM.  The header and the first 4 KB of the block
+        // are read together (one PCIe round trip for a call of up to ~1000 jobs)
         int32_t* hdr = sc + 32;  // RS_HDR words
         if (!smode) {  // (the block holds >= 4 KB: its capacity is larger; reading 16 KB at once measured slower)
             if (tid < OWGS_RES_NHDR) hdr[tid] = ld_sys(A.ctl + OWGS_RES_HDR + tid);
@@ -392,13 +393,17 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
         __syncthreads();
         const int n_runs = hdr[0], NR = hdr[1], NP = hdr[2], has_seq = hdr[3];
         const u64 seq_base = (u64)(uint32_t)hdr[4] | ((u64)(uint32_t)hdr[5] << 32);
-        const uint32_t s_poff = (uint32_t)hdr[6], s_rel = (uint32_t)hdr[7], s_pub = (uint32_t)hdr[8],
-                       s_seq = (uint32_t)hdr[9], s_in = (uint32_t)hdr[10];
+        const uint32_t s_poff = (uint32_t)hdr[6], s_seq = (uint32_t)hdr[9], s_in = (uint32_t)hdr[10];
         const long long s_first = hdr[13];  // (stream mode) the piece's first release / publish in the stream
         u64 rsum = (u64)(uint32_t)hdr[11] | ((u64)(uint32_t)hdr[12] << 32);  // memory the releases return at most
-        // LDS after the input block: each publish's walk cursor {generation, step}, then the outputs (mirrored by the
-        // host's output block): out_inv i32[NP], out_flags u8[NP], rel_flags u8[NR]
-        const uint32_t s_cur = (s_in + 15u) & ~15u, s_out = (s_cur + 8u * (uint32_t)NP + 15u) & ~15u;
+        // LDS after the input block: the records {invoker, meta.y, slot key, 0} per release and {meta.x, meta.y, slot
+        // key, word} per publish (stream mode: inside the block, at the header's offsets), each publish's walk
+        // cursor {generation, step}, then the outputs (mirrored by the host's output block): out_inv i32[NP],
+        // out_flags u8[NP], rel_flags u8[NR]
+        const uint32_t s_rel = smode ? (uint32_t)hdr[7] : ((s_in + 15u) & ~15u);
+        const uint32_t s_pub = smode ? (uint32_t)hdr[8] : s_rel + 16u * (uint32_t)NR;
+        const uint32_t s_cur = smode ? ((s_in + 15u) & ~15u) : s_pub + 16u * (uint32_t)NP;
+        const uint32_t s_out = (s_cur + 8u * (uint32_t)NP + 15u) & ~15u;
         const uint32_t s_ofl = s_out + 4u * (uint32_t)NP, s_orf = s_ofl + (uint32_t)NP;
         const uint32_t s_end = (s_orf + (uint32_t)NR + 15u) & ~15u;
         if (tid == 0) sc[RS_BAIL] = s_end > (uint32_t)A.stage_bytes ? OWGS_RES_BAIL_STAGE : 0;
@@ -531,20 +536,6 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 }
             }
         } else if (sc[RS_BAIL] == 0) {
-            // the publishes' walk cursors, gathered from HBM while the rest of the block crosses PCIe when their
-            // action handles came with the first 4 KB (at most 1024 publishes: 4 per thread)
-            const uint32_t s_aid = (uint32_t)hdr[13];
-            const bool early = A.cur && NP <= 1024 && s_aid + 4u * (uint32_t)NP <= 1024u * RES_FIRST_READ_KB;
-            uint2 cu[4];
-            if (early) {
-                const int32_t* aid = (const int32_t*)(stg + s_aid);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int i = tid + 256 * u;
-                    const uint32_t a = i < NP ? (uint32_t)aid[i] : 0xFFFFFFFFu;
-                    cu[u] = a < (uint32_t)A.n_actions ? A.cur[a] : make_uint2(0u, 0u);
-                }
-            }
             // the rest of a block beyond 4 KB, four 16-byte reads in flight per thread
             for (uint32_t o = 1024u * RES_FIRST_READ_KB + 16u * tid; o < s_in; o += 4u * 16u * 256u) {
                 uint4 v[4];
@@ -559,16 +550,37 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                     if (ou < s_in) ((uint4*)stg)[ou / 16u] = v[u];
                 }
             }
-            __syncthreads();
-            // every publish's walk cursor (one gather: the decision loop then waits on nothing in HBM)
-            if (early) {
+            if (s_in > 1024u * RES_FIRST_READ_KB) __syncthreads();
+            // every record's action meta and slot key, and every publish's walk cursor, gathered from HBM (four
+            // records of each kind per thread in flight: one HBM round trip for a call of up to 1024 of each; the
+            // decision loop then waits on nothing in HBM)
+            const int32_t* rinv = (const int32_t*)(stg + (uint32_t)hdr[7]);
+            const int32_t* ract = (const int32_t*)(stg + (uint32_t)hdr[8]);
+            const uint32_t* pw = (const uint32_t*)(stg + (uint32_t)hdr[13]);
+            for (int b0 = 0; b0 < max(NR, NP); b0 += 4 * 256) {
+                uint2 pm[4], cu[4];
+                uint32_t ps[4], rm[4], rs[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (tid + 256 * u < NP) pcur[tid + 256 * u] = cu[u];
-            } else {
-                for (int i = tid; i < NP; i += 256) {
-                    const uint32_t a = pub[i].w & RES_ACT_MASK;
-                    pcur[i] = (A.cur && a < (uint32_t)A.n_actions) ? A.cur[a] : make_uint2(0u, 0u);
+                for (int u = 0; u < 4; ++u) {
+                    const int i = b0 + 256 * u + tid;
+                    const uint32_t a = i < NP ? (pw[i] & RES_ACT_MASK) : 0xFFFFFFFFu;
+                    const bool ok = a < (uint32_t)A.n_actions;
+                    pm[u] = ok ? A.act_meta[a] : make_uint2(0u, 0u);
+                    ps[u] = ok ? (uint32_t)A.act_slot[a] : 0u;
+                    cu[u] = (ok && A.cur) ? A.cur[a] : make_uint2(0u, 0u);
+                    const uint32_t r = i < NR ? (uint32_t)ract[i] : 0xFFFFFFFFu;
+                    const bool rok = r < (uint32_t)A.n_actions;
+                    rm[u] = rok ? A.act_meta[r].y : 0u;
+                    rs[u] = rok ? (uint32_t)A.act_slot[r] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = b0 + 256 * u + tid;
+                    if (i < NP) {
+                        pub[i] = make_uint4(pm[u].x, pm[u].y, ps[u], pw[i]);
+                        pcur[i] = cu[u];
+                    }
+                    if (i < NR) rel[i] = make_uint4((uint32_t)rinv[i], rm[u], rs[u], 0u);
                 }
             }
         }
