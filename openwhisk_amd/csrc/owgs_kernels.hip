@@ -2926,7 +2926,9 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         }
                         ccw[lead] = ((uint32_t)(occ + 1) << 15) | ns;
                         if (cok && a != (int)OWGS_REC_NOACT && ns != (cw & 0x7FFFu)) {
+#ifndef OWGS_EXP_NOGCUR  // (diagnostic: no cursor stores; later chunks walk from the batch's first step)
                             A.gcur[a] = (btag << 15) | ns;  // for the later chunks of this batch
+#endif
                             if (kind == K_FALLBACK && maxc > 1) {
                                 // backward move: the next chunk's gathered cursors predate it (see `stale`), and
                                 // the store must reach L2 before the chunk after that gathers again
