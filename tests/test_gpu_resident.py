@@ -111,6 +111,27 @@ def test_resident_small_drains_match_oracle(cfg, kw):
     assert pubs == int(w.stream.acq_off[-1])
 
 
+@pytest.mark.parametrize("cfg,kw", [
+    ("headline", dict(n_activations=40_000, n_invokers=1000, n_actions=2000, n_namespaces=200)),
+    ("c4", dict(n_activations=40_000)),
+])
+def test_resident_calls_beyond_the_first_read(cfg, kw):
+    """Drains of 900..1024 jobs (up to OWGS_RES_MAX): the call block (4 B per publish, 8 B per release) outgrows the
+    engine's first 4 KB read of pinned memory, so the rest of the block is read and the records gathered after it;
+    bit-exact with the oracle, every call on the resident engine."""
+    w = W.config(cfg, **kw)
+    sh = Shim(w)
+    rng = np.random.default_rng(11)
+    big = 0
+    while not sh.done():
+        n, r = sh.call(int(rng.integers(900, 1025)))
+        big += (4 * n + 8 * r) > 4096
+    st = sh.g.resident_stats()
+    assert big >= 5, big
+    assert st["served"] == sh.calls and st["chained"] == 0 and st["refused"] == 0, st
+    assert np.array_equal(sh.g.permits(), sh.o.permits())
+
+
 def test_resident_interleaved_with_the_chain_and_state_updates():
     """Small drains on the resident engine, large ones (beyond OWGS_RES_MAX) on the launch chain, a health change
     (owgs_update_invokers) and a snapshot read in between: each non-resident entry point stops the engine, which writes
