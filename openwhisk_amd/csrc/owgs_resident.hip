@@ -184,6 +184,22 @@ __device__ __forceinline__ int ct_lookup(const uint2* ct, const uint32_t* bf, ui
     }
     return -1;
 }
+// the rest of a lookup whose first block (e01, e23 at ct_home(key)) the caller read: hit, chain end, or the next blocks
+__device__ __forceinline__ int ct_lookup_after(const uint2* ct, uint32_t key, uint4 e01, uint4 e23, uint32_t* val) {
+    uint32_t h = ct_home(key);
+    *val = 0u;
+    for (int p = 0;;) {
+        const bool h0 = e01.x == key, h1 = e01.z == key, h2 = e23.x == key, h3 = e23.z == key;
+        if (h0 || h1 || h2 || h3) {
+            *val = h0 ? e01.y : h1 ? e01.w : h2 ? e23.y : e23.w;
+            return (int)h + (h0 ? 0 : h1 ? 1 : h2 ? 2 : 3);
+        }
+        if (e01.x == 0u || e01.z == 0u || e23.x == 0u || e23.z == 0u || ++p == OWGS_CTC / CT_BLK) return -1;
+        h = (h + CT_BLK) & (OWGS_CTC - 1);
+        e01 = *(const uint4*)&ct[h];
+        e23 = *(const uint4*)&ct[h + 2];
+    }
+}
 // both tables: index < OWGS_CTC primary, OWGS_CTC + j overflow entry j
 __device__ __forceinline__ int ct_lookup2(const uint2* ct, const uint32_t* bf, const OwgsOvf& O, bool ovf_on,
                                           uint32_t key, uint32_t* val) {
@@ -859,13 +875,18 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 ++pr_rounds;
                                 const bool valid = s0 + lane < n;
                                 const int id = base + p;
+                                // the permit count, the key's filter word and its first map block, read together
+                                const uint32_t key = ct_key(id, slot);
+                                const uint2 fb = bf_pos(key);
+                                const uint32_t fh = ct_home(key);
                                 const int pv = valid ? P[id] : OWGS_PENC;
+                                const uint32_t fw = bf[fb.x];
+                                const uint4 f01 = *(const uint4*)&ct[fh], f23 = *(const uint4*)&ct[fh + 2];
                                 bool ok = false;
                                 int ix = -1;
                                 uint32_t v = 0u;
                                 if (pv < OWGS_PLIM) {  // usable: a free slot of the key's container, or memory
-                                    const uint32_t key = ct_key(id, slot);
-                                    ix = ct_lookup(ct, bf, key, &v);
+                                    ix = (fw & fb.y) == fb.y ? ct_lookup_after(ct, key, f01, f23, &v) : -1;
                                     if (ix < 0 && ovf_on) {  // (an HBM round trip: counted)
                                         ++pr_ovf;
                                         const int oj = ovf_find(A.ovf, key, &v);
@@ -1070,6 +1091,18 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                         const uint2 b = bf_pos(ct_key(idk[k], (int)me.z));
                                         bk[k] = (bf[b.x] & b.y) == b.y;
                                     }
+                                    // the first map block of every step the filter passes, read together (the
+                                    // lookups below only continue a chain past it)
+                                    uint4 fa[4], fb[4];
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k) {
+                                        fa[k] = fb[k] = make_uint4(0u, 0u, 0u, 0u);
+                                        if (bk[k]) {
+                                            const uint32_t h = ct_home(ct_key(idk[k], (int)me.z));
+                                            fa[k] = *(const uint4*)&ct[h];
+                                            fb[k] = *(const uint4*)&ct[h + 2];
+                                        }
+                                    }
                                     int kf = 4;
 #pragma unroll
                                     for (int k = 0; k < 4; ++k) {
@@ -1077,7 +1110,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                         if (kf == 4 && cst + k < l_n && pv < OWGS_PLIM) {
                                             const uint32_t key = ct_key(idk[k], (int)me.z);
                                             uint32_t v = 0u;
-                                            int ix = bk[k] ? ct_lookup(ct, nullptr, key, &v) : -1;
+                                            int ix = bk[k] ? ct_lookup_after(ct, key, fa[k], fb[k], &v) : -1;
                                             if (ix < 0 && ovf_on) {
                                                 ++pr_ovf;
                                                 const int oj = ovf_find(A.ovf, key, &v);
