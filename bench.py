@@ -318,12 +318,131 @@ def shim_path(w, o_inv, dev_index, drains=(64, 512, 4096), budget_jobs=(120_000,
                          "map_fill_max": fill[0], "map_deleted_max": fill[1],
                          "host_build_us_mean": (fill[2] - hn0[0]) * 1e-3 / max(rs1["served"] - rs0["served"], 1),
                          "host_wait_us_mean": (fill[3] - hn0[1]) * 1e-3 / max(rs1["served"] - rs0["served"], 1)})
+    legs += shim_extra_legs(w, b, kind, ids, act, o_inv)
     b.close()
     return {"path": "host buffers through the C ABI as the JNI shim calls it (queue order: each batch's completions, "
                     "then its publishes); calls = owgs_release_batch + owgs_publish_batch per run, fused = "
                     "owgs_process_batch per drained batch (small calls: the resident engine, owgs_resident.hip); "
                     "latency = the C call, timed inside the library (py_* = the same calls timed from Python, "
                     "ctypes' call overhead included)", "legs": legs}
+
+
+def _fused_drain(b, kind, ids, act, inv, o_ref, c0, c1):
+    """One drained batch jobs [c0, c1) through owgs_process_batch as the shim calls it; returns (C-call ns, publishes)."""
+    import ctypes as C
+    p = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
+    k, x = kind[c0:c1], ids[c0:c1]
+    cut = np.nonzero((k[1:] == 0) & (k[:-1] == 1))[0] + 1
+    bounds = np.concatenate([[0], cut, [len(k)]])
+    runs = []
+    for r0, r1 in zip(bounds[:-1], bounds[1:]):
+        kk, xx = k[r0:r1], x[r0:r1]
+        rel = xx[kk == 0]
+        ri = inv[rel]
+        ri = np.where(ri == -9, o_ref[rel], ri)  # (published earlier in this drained batch: the oracle's = the GPU's)
+        keep = ri >= 0  # no ActivationEntry for a failed publish (CLB:278-279)
+        runs.append((ri[keep], act[rel[keep]], xx[kk == 1]))
+    ro = np.cumsum([0] + [len(r[0]) for r in runs]).astype(np.int32)
+    po = np.cumsum([0] + [len(r[2]) for r in runs]).astype(np.int32)
+    ri = np.concatenate([r[0] for r in runs] + [np.zeros(1, np.int32)]).astype(np.int32)
+    ra = np.concatenate([r[1] for r in runs] + [np.zeros(1, np.int32)]).astype(np.int32)
+    pubs = np.concatenate([r[2] for r in runs]).astype(np.int64)
+    pa = np.ascontiguousarray(np.concatenate([act[pubs], np.zeros(1, np.int32)]))
+    sq = np.ascontiguousarray(np.concatenate([pubs, [0]]).astype(np.uint64))
+    o = np.zeros(len(pubs) + 1, np.int32)
+    f = np.zeros(len(pubs) + 1, np.uint8)
+    rf = np.zeros(len(ri), np.uint8)
+    args = (b._h, len(runs), p(ro), p(ri), p(ra), p(rf), p(po), p(pa), p(sq), 0, p(o), p(f))
+    rc = b._L.owgs_process_batch(*args)
+    assert rc == 0, (rc, b._L.owgs_last_error(b._h))
+    inv[pubs] = o[:len(pubs)]
+    return b.last_call_ns(), len(pubs)
+
+
+def shim_extra_legs(w, b, kind, ids, act, o_inv, budget=480_000, seed=0x5EED):
+    """Two more fused legs of the shim path:
+    "mixed": drain sizes as a loaded batching thread produces them -- log-uniform over 1..4096 jobs, so the calls flip
+    between the resident engine (<= OWGS_RES_MAX jobs) and the launch chain; p50 / p99 per drain class and overall.
+    "reset": 512-job drains with updateCluster(2) (SCPB:561-584) at a batch boundary a third into the leg: the
+    activations in flight become watched pairs (their releases meet the new state, NS:61-62 / NS:98-113); what share
+    of the calls after the change the resident engine serves, and their latency.  Both are checked against the oracle
+    (the reset leg against an oracle replay with the same membership change)."""
+    import oracle as O
+    s = w.stream
+    out = []
+    n_jobs = min(budget, len(ids))
+    # -- mixed drain sizes
+    rng = np.random.default_rng(seed)
+    b.restore()
+    rs0 = b.resident_stats()
+    inv = np.full(len(act), -9, np.int32)
+    lat, sizes, n_pub, c0 = [], [], 0, 0
+    while c0 < n_jobs:
+        d = int(np.exp(rng.uniform(0.0, np.log(4096.0)))) or 1
+        c1 = min(c0 + d, n_jobs)
+        ns, npub = _fused_drain(b, kind, ids, act, inv, o_inv, c0, c1)
+        lat.append(ns * 1e-3)
+        sizes.append(c1 - c0)
+        n_pub += npub
+        c0 = c1
+    rs1 = b.resident_stats()
+    lat, sizes = np.array(lat), np.array(sizes)
+    done = inv != -9
+    small = sizes <= 1024
+    out.append({"mode": "fused-mixed", "drain": "log-uniform 1..4096", "jobs": n_jobs, "calls": len(lat),
+                "publishes": int(n_pub), "p50_us": float(np.percentile(lat, 50)), "p99_us": float(np.percentile(lat, 99)),
+                "p50_us_le1024": float(np.percentile(lat[small], 50)), "p99_us_le1024": float(np.percentile(lat[small], 99)),
+                "p50_us_gt1024": float(np.percentile(lat[~small], 50)) if (~small).any() else None,
+                "p99_us_gt1024": float(np.percentile(lat[~small], 99)) if (~small).any() else None,
+                "decisions_per_s": n_pub / max(float(lat.sum()) * 1e-6, 1e-9),
+                "bit_exact": bool(np.array_equal(inv[done], o_inv[done])),
+                "resident": {k: rs1[k] - rs0[k] for k in rs1 if k not in ("alive", "last_call_ns")}})
+    # -- membership change mid-leg
+    job_batch = np.repeat(np.arange(s.n_batches), np.diff(s.rel_off) + np.diff(s.acq_off))
+    first_job = np.concatenate([[0], np.cumsum(np.diff(s.rel_off) + np.diff(s.acq_off))])
+    b0 = max(1, int(job_batch[min(n_jobs // 3, len(job_batch) - 1)]))
+    end_b = int(job_batch[n_jobs - 1]) + 1  # (the leg stops at a batch end: the oracle replays whole batches)
+    n_jobs_r = int(first_job[end_b])
+    st = O.state_for(w)
+    o_r = np.full(len(act), -9, np.int32)
+    fl_r = np.zeros(len(act), np.uint8)
+    rf_r = np.zeros(max(len(s.rel_aid), 1), np.uint8)
+    acq = np.ascontiguousarray(s.acq_off, np.int64)
+    rel = np.ascontiguousarray(s.rel_off, np.int64)
+    aid = np.ascontiguousarray(s.rel_aid, np.int64)
+    for bb in range(end_b):
+        if bb == b0:
+            st.update_cluster(2)
+        O.lib().owo_replay(st.h, 1, O._ptr(acq[bb:]), O._ptr(np.ascontiguousarray(s.act, np.int32)),
+                           O._ptr(rel[bb:]), O._ptr(aid), int(s.seq_base), O._ptr(o_r), O._ptr(fl_r), O._ptr(rf_r))
+    b.restore()
+    inv = np.full(len(act), -9, np.int32)
+    lat_a, n_pub, c0 = [], 0, 0
+    cut = int(first_job[b0])
+    st_mid = None
+    while c0 < n_jobs_r:
+        if c0 == cut:
+            b.update_cluster(2)
+            st_mid = b.resident_stats()
+        c1 = min(c0 + 512, cut if c0 < cut else n_jobs_r)
+        ns, npub = _fused_drain(b, kind, ids, act, inv, o_r, c0, c1)
+        if c0 >= cut:
+            lat_a.append(ns * 1e-3)
+            n_pub += npub
+        c0 = c1
+    rs2 = b.resident_stats()
+    b.update_cluster(w.cluster_size)  # (the context is restored by the next leg / closed)
+    done = inv != -9
+    lat_a = np.array(lat_a)
+    served = rs2["served"] - st_mid["served"]
+    out.append({"mode": "fused-reset", "drain": 512, "jobs": n_jobs_r, "reset_at_batch": b0, "cluster_size_after": 2,
+                "calls_after": len(lat_a), "resident_served_after": int(served),
+                "resident_fraction_after": served / max(len(lat_a), 1),
+                "watch_calls": rs2["watch_calls"] - st_mid["watch_calls"],
+                "p50_us_after": float(np.percentile(lat_a, 50)), "p99_us_after": float(np.percentile(lat_a, 99)),
+                "decisions_per_s_after": n_pub / max(float(lat_a.sum()) * 1e-6, 1e-9),
+                "bit_exact": bool(np.array_equal(inv[done], o_r[done])) and int(done.sum()) == int(s.acq_off[end_b])})
+    return out
 
 
 def dry_run(args):
@@ -345,9 +464,10 @@ def dry_run(args):
     health = [torch.from_numpy(h) for h in cluster.health_schedule(ws[0].inv_status, ws[0].stream.n_batches)]
     t0 = time.perf_counter()
     n_gather = 0
+    flat = [torch.empty(world * len(health[0]), dtype=torch.uint8) for _ in health]  # one buffer per batch (GPU path)
     for _ in range(args.steps):
-        for h in health:  # the configs[4] cadence: one all-gather between batches
-            agreed = hx.exchange(h)
+        for k, h in enumerate(health):  # the configs[4] cadence: one all-gather between batches
+            agreed = hx.exchange_into(h, flat[k])
             assert torch.equal(agreed, h)
             n_gather += 1
     t_step = (time.perf_counter() - t0) / max(args.steps, 1)
@@ -434,11 +554,31 @@ def main():
         def replay_batches(self, hx, timing=None):
             """configs[4] cadence: before each batch the shards all-gather their health view (the health topic,
             SCPB:355) and apply the agreed vector (owgs_update_health_device -> updateInvokers, SCPB:512-551); the
-            batch is one engine launch (owgs_replay_device_span)."""
+            batch is one engine launch (owgs_replay_device_span).  The health of batch k + 1 is an input known before
+            the batch, so its all-gather runs on a side stream while batch k's engine runs (one batch ahead, its own
+            buffer); the engine stream waits only for the exchange of the batch it is about to apply."""
             s, b = self.s, self.b
+            main = torch.cuda.current_stream()
+            if getattr(self, "hside", None) is None:
+                self.hside = torch.cuda.Stream()
+                self.hflat = [torch.empty(hx.world * len(self.w.inv_status), dtype=torch.uint8, device=dev)
+                              for _ in range(s.n_batches)]
+                self.hev = [torch.cuda.Event() for _ in range(s.n_batches)]
+            self.hside.wait_stream(main)  # (the previous step has read every buffer it overwrites)
+            agreed = [None] * s.n_batches
+
+            def gather(k):
+                with torch.cuda.stream(self.hside):
+                    agreed[k] = hx.exchange_into(self.d_health[k], self.hflat[k])
+                    self.hev[k].record(self.hside)
+
             b.restore(self.sp)
+            gather(0)
             for k in range(s.n_batches):
-                h = hx.exchange(self.d_health[k])
+                if k + 1 < s.n_batches:
+                    gather(k + 1)  # in flight while batch k's engine runs
+                main.wait_event(self.hev[k])
+                h = agreed[k]
                 b.update_health_device(len(self.w.inv_status), h.data_ptr(), self.sp)
                 b.replay_device_span(s.acq_off[k], s.acq_off[k + 1], s.rel_off[k], s.rel_off[k + 1],
                                      self.d_act.data_ptr(), self.d_aid.data_ptr(), s.seq_base, self.d_out.data_ptr(),

@@ -234,12 +234,15 @@ class GpuShardingContainerPoolBalancer:
     def resident_stats(self) -> dict:
         """owgs_process_batch's paths: calls the resident engine served, its launches, calls it refused untouched,
         calls the launch chain took, and whether a resident engine is live."""
-        out = np.zeros(6 + _NRP, np.int64)
-        n = self._L.owgs_resident_stats(self._h, _p(out), 6 + _NRP)
+        out = np.zeros(13 + 2 * _NRP, np.int64)
+        n = self._L.owgs_resident_stats(self._h, _p(out), 13 + 2 * _NRP)
         if n < 0:
             self._chk(n)
-        return dict(zip(("served", "launches", "refused", "chained", "alive") + _RES_PROF + ("last_call_ns",),
-                        (int(x) for x in out)))
+        d = dict(zip(("served", "launches", "refused", "chained", "alive") + _RES_PROF + ("last_call_ns",),
+                     (int(x) for x in out[:6 + _NRP])))
+        d["life_exits"] = int(out[11 + 2 * _NRP])  # launches ended by the lifetime bound (OWGS_RES_LIFE_US)
+        d["watch_calls"] = int(out[12 + 2 * _NRP])  # served calls while watched pairs existed
+        return d
 
     def map_fill(self) -> dict:
         """The NestedSemaphore map's fill: live / deleted primary (LDS-image) entries, overflow entries and capacity."""

@@ -52,6 +52,16 @@ class HealthExchange:
             self.gathered[0].copy_(v)
         return self.gathered[0]
 
+    def exchange_into(self, view, flat):
+        """As exchange, into a caller's buffer of world * n bytes (one per batch: exchanges of later batches can run
+        ahead on another stream while earlier batches still read theirs); returns the agreed row (rank 0's)."""
+        if self.world > 1:
+            self.dist.all_gather_into_tensor(flat, view)
+        else:
+            flat[:view.numel()].copy_(view)
+        self.gathered.copy_(flat.view(self.world, -1))  # (diagnostics: disagreeing_ranks reads the last exchange)
+        return flat[:view.numel()]
+
     def disagreeing_ranks(self) -> list[int]:
         """Ranks whose last gathered view differs from rank 0's (diagnostics)."""
         g = self.gathered.cpu().numpy()

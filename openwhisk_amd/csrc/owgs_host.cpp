@@ -109,6 +109,14 @@ struct EnvOpts {
     // its idle time before it writes the state back and exits (OWGS_RESIDENT=0 sends every call down the chain)
     int res = 1, res_max = 1024;
     long long res_idle_us = 20000;
+    // ... and its lifetime: it exits between calls once this long after its launch even when busy (it holds a hardware
+    // queue that another context's stream may share; GPU_MAX_HW_QUEUES is 4), the next call relaunches it
+    long long res_life_us = 100000;
+    // watched pairs (after updateCluster) on the resident engine (0: such calls take the launch chain, as in round 4)
+    int res_watch = 1;
+    // (tests) the doorbell's and the walk-cursor generation's values at the context's first launch: start a context
+    // just below their wrap limits
+    long long res_call_base = 0, res_gen_base = 0;
     // the resident engine's speculative walks: walk steps each publish probes on its own before the in-order
     // validation (0: every decision walked one at a time)
     int res_spec = 16;
@@ -121,6 +129,10 @@ struct EnvOpts {
         if (const char* e = getenv("OWGS_RES_SPEC")) res_spec = atoi(e);
         if (const char* e = getenv("OWGS_RES_MAX")) res_max = atoi(e);
         if (const char* e = getenv("OWGS_RES_IDLE_US")) res_idle_us = atoll(e);
+        if (const char* e = getenv("OWGS_RES_LIFE_US")) res_life_us = atoll(e);
+        if (const char* e = getenv("OWGS_RES_WATCH")) res_watch = atoi(e);
+        if (const char* e = getenv("OWGS_RES_CALL_BASE")) res_call_base = atoll(e);
+        if (const char* e = getenv("OWGS_RES_GEN_BASE")) res_gen_base = atoll(e);
         feat_all = getenv("OWGS_FEAT_ALL") != nullptr;  // the general engine for every launch (A/B diagnostics)
         if (const char* e = getenv("OWGS_VARIANT")) variant = atoi(e);  // force an engine geometry (diagnostics)
         if (const char* o = getenv("OWGS_OPTS")) opts = atoi(o);
@@ -316,10 +328,14 @@ struct owgs_ctx {
     int32_t res_call = 0;
     bool res_alive = false;
     int32_t res_stage = 0;
-    int64_t res_n_calls = 0, res_n_launches = 0, res_n_bails = 0, res_n_chained = 0;
+    int64_t res_n_calls = 0, res_n_launches = 0, res_n_bails = 0, res_n_chained = 0, res_n_life = 0;
+    int64_t res_n_watch_calls = 0;  // served calls while watched pairs existed
     int64_t res_prof[OWGS_RES_NPROF] = {};
     int64_t res_used_max = 0, res_tombs_max = 0;  // the primary table's fill after served calls (largest seen)
     int64_t res_host_ns[2] = {};    // served calls: host time building the call (records, ranks), bell-to-answer wait
+    DevBuf<uint4> d_w_sidx;         // resident engine: watched pairs by fqn@version key (built at its launch)
+    DevBuf<uint2> d_w_list;
+    int32_t w_scap = 0;
     DevBuf<uint2> d_res_cur;        // per action: {cursor generation, first walk step that may fit}
     std::vector<uint2> res_meta;    // act_meta as of the live launch (every change of it stops the engine first)
     uint32_t res_gen_seen = 0;      // the last cursor generation the engine reported
@@ -871,6 +887,10 @@ static int check_err_word(owgs_ctx* c) {
         if (e & OWGS_ERR_GEOM) return c->fail(OWGS_EDEVICE, "engine object and host disagree on the engine geometry");
         if (e & OWGS_ERR_INTERNAL) return c->fail(OWGS_EDEVICE, "engine invariant violated");
         if (e & OWGS_ERR_PERMITS) return c->fail(OWGS_ERANGE, "slot permits outside the engine's range [-2^29, 2^29) MB");
+        if (e & OWGS_ERR_RELRISK)  // (stream mode only: the chunked engine applies such releases and flags FS:48-50)
+            return c->fail(OWGS_ERANGE, "stream-mode replay stopped before a release that could overflow a slot's "
+                                        "permits (ForcibleSemaphore.release FS:48-50): the rest of the stream is not "
+                                        "applied; replay it with OWGS_SPEC_REPLAY=0");
         return c->fail(OWGS_EINVAL, "stream releases an activation that holds no slot (or a permit overflow)");
     }
     return OWGS_OK;
@@ -927,11 +947,20 @@ static int reclaim_slots(owgs_ctx* c) {
 // owgs_process_batch's small calls go to a resident engine (owgs_resident.hip) that keeps the slot state in LDS
 // between calls.  Every other entry point reads or replaces that state, so it stops the engine first (the engine
 // writes the state back to HBM and exits) -- OWGS_ENTER below; the next eligible call launches it again.
+// after the engine's stream has drained: count an exit the lifetime bound caused (diagnostics)
+static void res_reap(owgs_ctx* c) {
+    if (__atomic_load_n(&c->res_ctl[OWGS_RES_STATE], __ATOMIC_ACQUIRE) == 2 &&
+        __atomic_load_n(&c->res_ctl[OWGS_RES_WHY], __ATOMIC_ACQUIRE) == 2)
+        ++c->res_n_life;
+    c->res_ctl[OWGS_RES_STATE] = 0;
+}
 static int res_quiesce(owgs_ctx* c) {
     if (!c->res_alive) return OWGS_OK;
     __atomic_store_n(&c->res_ctl[OWGS_RES_BELL], -1, __ATOMIC_RELEASE);
     c->res_alive = false;
     HIPCHK(c, hipStreamSynchronize(c->res_stream));
+    res_reap(c);
+    if (c->w_cap > 0 && c->w_live <= 0) w_drop(c);  // the engine's calls took the last pairs out of W
     return OWGS_OK;
 }
 
@@ -947,9 +976,10 @@ static size_t res_stage_bytes(const owgs_ctx* c) {
     return img >= OWGS_LDS_BYTES ? 0 : std::min<size_t>(OWGS_LDS_BYTES - img, 64 * 1024) & ~(size_t)15;
 }
 
-// identity pools, no watched pairs (their releases need the ordered kernels), a call the staging area holds
+// identity pools, a call the staging area holds (watched pairs included: the engine applies their releases and marks)
 static bool res_eligible(const owgs_ctx* c, int32_t n_runs, int32_t NR, int32_t NP, bool has_seq) {
-    if (env_opts().res <= 0 || c->pool_mode != 0 || c->w_cap > 0) return false;
+    if (env_opts().res <= 0 || c->pool_mode != 0) return false;
+    if (c->w_cap > 0 && env_opts().res_watch <= 0) return false;
     if ((int64_t)NR + NP > env_opts().res_max || NP + NR == 0) return false;
     if (c->n_slots > OWGS_MAX_SLOTS_CT || c->n_ids > c->n_slots || c->nm > (int32_t)OWGS_AM_POS_MASK ||
         c->nb > (int32_t)OWGS_AM_POS_MASK || c->a_mem.empty())
@@ -965,6 +995,85 @@ static bool res_eligible(const owgs_ctx* c, int32_t n_runs, int32_t NR, int32_t 
     return true;
 }
 
+// The resident engine's index of the watched pairs: per fqn@version key with watched pairs
+// {slot + 1, first, count, primary action} in an open-addressing table, and the key's pairs {W index, walk step of the
+// pair's invoker in the primary action's walk} sorted by step, so that a decision marks the pairs before its step by
+// reading a prefix.  The primary action is the key's lowest live concurrent handle; another action of the key computes
+// each pair's step itself.  Built at every launch (W, the pools and the actions only change while no engine runs).
+static int res_w_index(owgs_ctx* c) {
+    c->w_scap = 0;
+    if (c->w_cap <= 0) return OWGS_OK;
+    std::vector<uint32_t> keys((size_t)c->w_cap);
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(keys.data(), c->w_keys.p, keys.size() * 4, hipMemcpyDeviceToHost));
+    std::unordered_map<int32_t, std::vector<uint2>> by_slot;  // slot -> {W index, step}
+    for (int32_t j = 0; j < c->w_cap; ++j) {
+        const uint32_t k = keys[(size_t)j];
+        if (k == 0u || k == OWGS_CT_TOMB) continue;
+        by_slot[(int32_t)(k >> OWGS_CT_SLOT_SHIFT)].push_back(make_uint2((uint32_t)j, 0x7FFFFFFFu));
+    }
+    std::unordered_map<int32_t, int32_t> prim;
+    for (size_t a = 0; a < c->a_mem.size(); ++a)
+        if (c->a_live[a] && c->a_maxc[a] > 1 && by_slot.count(c->a_slot[a]) && !prim.count(c->a_slot[a]))
+            prim[c->a_slot[a]] = (int32_t)a;
+    auto inv_mod = [](int64_t x, int64_t n) {
+        int64_t t = 0, nt = 1, r = n, nr = x % n;
+        while (nr) {
+            const int64_t q = r / nr;
+            int64_t tmp = t - q * nt;
+            t = nt;
+            nt = tmp;
+            tmp = r - q * nr;
+            r = nr;
+            nr = tmp;
+        }
+        return t < 0 ? t + n : t;
+    };
+    std::vector<uint2> list;
+    std::vector<uint4> sidx;
+    size_t scap = 16;
+    while (scap < 2 * by_slot.size()) scap <<= 1;
+    sidx.assign(scap, make_uint4(0u, 0u, 0u, 0u));
+    for (auto& kv : by_slot) {
+        const int32_t slot = kv.first;
+        auto it = prim.find(slot);
+        const int32_t pa = it == prim.end() ? -1 : it->second;  // (none: every decision of the key computes steps)
+        if (pa >= 0 && (size_t)pa < c->res_meta.size() && !(c->res_meta[pa].y & (OWGS_AM_EMPTY | OWGS_AM_THROW))) {
+            const uint32_t mx = c->res_meta[pa].x;
+            const int64_t pool = (mx & OWGS_AM_POOL) ? 1 : 0, n = pool ? c->nb : c->nm;
+            const int64_t base = pool ? c->n_ids - c->nb : 0, home = mx & OWGS_AM_POS_MASK;
+            const int64_t step = (mx >> 15) & OWGS_AM_POS_MASK;
+            const int64_t is = n > 1 ? inv_mod(step % n, n) : 0;
+            for (uint2& e : kv.second) {
+                const int64_t x = (int64_t)(keys[e.x] & 0x7FFFu) - 1, pos = x - base;
+                if (n > 0 && pos >= 0 && pos < n) e.y = (uint32_t)(n > 1 ? ((pos - home + n) % n) * is % n : 0);
+            }
+            std::sort(kv.second.begin(), kv.second.end(), [](const uint2& a, const uint2& b) { return a.y < b.y; });
+        }
+        uint32_t h = 0;
+        {  // ct_hash(slot + 1), as the device probes
+            uint32_t k = (uint32_t)slot + 1u;
+            k ^= k >> 16;
+            k *= 0x7feb352dU;
+            k ^= k >> 15;
+            k *= 0x846ca68bU;
+            k ^= k >> 16;
+            h = k & (uint32_t)(scap - 1);
+        }
+        while (sidx[h].x != 0u) h = (h + 1u) & (uint32_t)(scap - 1);
+        sidx[h] = make_uint4((uint32_t)slot + 1u, (uint32_t)list.size(), (uint32_t)kv.second.size(),
+                             pa >= 0 ? (uint32_t)pa : 0xFFFFFFFFu);
+        list.insert(list.end(), kv.second.begin(), kv.second.end());
+    }
+    if (list.empty()) list.push_back(make_uint2(0u, 0u));
+    HIPCHK(c, c->d_w_sidx.reserve(scap));
+    HIPCHK(c, c->d_w_list.reserve(list.size()));
+    HIPCHK(c, hipMemcpy(c->d_w_sidx.p, sidx.data(), scap * sizeof(uint4), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_w_list.p, list.data(), list.size() * sizeof(uint2), hipMemcpyHostToDevice));
+    c->w_scap = (int32_t)scap;
+    return OWGS_OK;
+}
+
 static int res_launch(owgs_ctx* c) {
     if (!c->res_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->res_stream, hipStreamNonBlocking));
     if (!c->ev_res) HIPCHK(c, hipEventCreateWithFlags(&c->ev_res, hipEventDisableTiming));
@@ -977,11 +1086,20 @@ static int res_launch(owgs_ctx* c) {
         if (rc) return rc;
     }
     HIPCHK(c, c->d_ct_tmp.reserve((size_t)2 * OWGS_CTC));
-    {  // walk cursors: a new buffer starts at generation 0, below every generation a launch uses
+    if (c->res_n_launches == 0) {  // (tests: start below the wrap limits)
+        c->res_call = (int32_t)std::min<long long>(std::max<long long>(env_opts().res_call_base, 0), OWGS_RES_CALL_LIMIT);
+        c->res_gen_seen = (uint32_t)std::min<long long>(std::max<long long>(env_opts().res_gen_base, 0), 0xFFFFFFFFll);
+    } else {
+        c->res_call = 0;  // a fresh engine: the bell counts up from 0 again (it stays in [0, 2^31): -1 is the stop word)
+    }
+    {  // walk cursors: a new buffer starts at generation 0, below every generation a launch uses; a generation near
+       // its 32-bit wrap starts over from 0 (every stored cursor cleared: an equal generation must mean this launch's)
         const size_t na = std::max<size_t>(c->a_mem.size(), 1);
-        if (c->d_res_cur.n < na) {
-            HIPCHK(c, c->d_res_cur.reserve(na + na / 2));
+        const bool wrap = (uint64_t)c->res_gen_seen + 2 >= OWGS_RES_GEN_LIMIT;
+        if (c->d_res_cur.n < na || wrap) {
+            if (c->d_res_cur.n < na) HIPCHK(c, c->d_res_cur.reserve(na + na / 2));
             HIPCHK(c, hipMemsetAsync(c->d_res_cur.p, 0, c->d_res_cur.n * sizeof(uint2), c->stream));
+            if (wrap) c->res_gen_seen = 0;
         }
     }
     // the action meta the host writes into each call's records (as the device computed it)
@@ -990,6 +1108,10 @@ static int res_launch(owgs_ctx* c) {
         HIPCHK(c, hipMemcpyAsync(c->res_meta.data(), c->d_act_meta.p, c->res_meta.size() * sizeof(uint2),
                                  hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    {
+        const int rc = res_w_index(c);
+        if (rc) return rc;
     }
     // the state in HBM must be current: the resident stream waits for the context's stream and its last async call
     HIPCHK(c, hipEventRecord(c->ev_res, c->stream));
@@ -1019,7 +1141,13 @@ static int res_launch(owgs_ctx* c) {
     a.cur = c->d_res_cur.p;  // (dropping them measured slower: drains inside a batch's publishes keep the generation)
     a.gen_base = ++c->res_gen_seen;  // above every generation stored by earlier launches
     a.idle_ticks = env_opts().res_idle_us * 100;  // s_memrealtime: 100 MHz
+    a.life_ticks = std::max(0ll, env_opts().res_life_us) * 100;
     a.spec = std::max(0, env_opts().res_spec);
+    a.w = watch_args(c);
+    a.w_sidx = c->d_w_sidx.p;
+    a.w_scap = c->w_scap;
+    a.w_list = c->d_w_list.p;
+    if (c->w_cap > 0) c->res_ctl[OWGS_RES_WLIVE] = c->w_live;
     volatile int32_t* ctl = c->res_ctl;
     ctl[OWGS_RES_STATE] = 0;
     ctl[OWGS_RES_DONE] = c->res_call;
@@ -1067,6 +1195,13 @@ static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
             HIPCHK(c, hipHostMalloc((void**)&c->res_out, cap, hipHostMallocCoherent));
             c->res_out_cap = cap;
         }
+    }
+    // the doorbell and the cursor generation stay below their limits: an engine near either is stopped (it writes
+    // the state back) and the relaunch below starts both over
+    if (c->res_alive && (c->res_call >= OWGS_RES_CALL_LIMIT - 8 ||
+                         (uint64_t)c->res_gen_seen + (uint64_t)n_runs + 2 >= OWGS_RES_GEN_LIMIT)) {
+        const int q = res_quiesce(c);
+        if (q) return q;
     }
     if (!c->res_alive) {
         const int rc = res_launch(c);
@@ -1161,6 +1296,7 @@ static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
         }
         if (!exited) break;
         HIPCHK(c, hipStreamSynchronize(c->res_stream));
+        res_reap(c);
         c->res_alive = false;
         if (attempt >= 3) return c->fail(OWGS_EDEVICE, "resident engine exits before serving a call");
         const int rc = res_launch(c);
@@ -1178,6 +1314,10 @@ static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
         return OWGS_OK;  // nothing applied: the chained path takes the call
     }
     ++c->res_n_calls;
+    if (c->w_cap > 0) {  // watched pairs left (W itself is dropped once the engine has stopped: res_quiesce)
+        c->w_live = __atomic_load_n(&c->res_ctl[OWGS_RES_WLIVE], __ATOMIC_ACQUIRE);
+        ++c->res_n_watch_calls;
+    }
     c->res_gen_seen = (uint32_t)__atomic_load_n(&c->res_ctl[OWGS_RES_GEN], __ATOMIC_ACQUIRE);
     for (int k = 0; k < OWGS_RES_NPROF; ++k) c->res_prof[k] += (uint32_t)c->res_ctl[OWGS_RES_PROF + k];
     c->res_used_max = std::max<int64_t>(c->res_used_max, c->res_ctl[OWGS_RES_USED]);
@@ -2838,8 +2978,10 @@ int owgs_read_stats(owgs_ctx* c, uint64_t* out, int32_t cap) {
         if (ro_) return ro_;
     }
     u64 v[OWGS_NSTATS];
-    HIPCHK(c, hipDeviceSynchronize());
-    HIPCHK(c, hipMemcpy(v, c->d_stats.p + (size_t)c->stats_last * OWGS_NSTATS, sizeof(v), hipMemcpyDeviceToHost));
+    // (the context's stream only: a live resident engine runs on its own stream and is not waited for)
+    HIPCHK(c, hipMemcpyAsync(v, c->d_stats.p + (size_t)c->stats_last * OWGS_NSTATS, sizeof(v), hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     for (int32_t i = 0; i < cap && i < OWGS_NSTATS; ++i) out[i] = v[i];
     return OWGS_OK;
 }
@@ -3473,8 +3615,10 @@ int owgs_resident_stats(owgs_ctx* c, int64_t* out, int32_t cap) {
         unsigned long long v[OWGS_RES_NPROF] = {};
         if (c->spec_last && c->d_spec_stats.p) {
             (void)hipSetDevice(c->cfg.device);
-            HIPCHK(c, hipDeviceSynchronize());
-            HIPCHK(c, hipMemcpy(v, c->d_spec_stats.p, sizeof(v), hipMemcpyDeviceToHost));
+            const int ro_ = order_on(c, c->stream);  // (after the stream-mode replay; a live shim engine is not waited for)
+            if (ro_) return ro_;
+            HIPCHK(c, hipMemcpyAsync(v, c->d_spec_stats.p, sizeof(v), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
         }
         for (int32_t i = 0; i < OWGS_RES_NPROF && 7 + OWGS_RES_NPROF + i < cap; ++i) out[7 + OWGS_RES_NPROF + i] = (int64_t)v[i];
     }
@@ -3482,7 +3626,9 @@ int owgs_resident_stats(owgs_ctx* c, int64_t* out, int32_t cap) {
     if (cap > 8 + 2 * OWGS_RES_NPROF) out[8 + 2 * OWGS_RES_NPROF] = c->res_tombs_max;
     if (cap > 9 + 2 * OWGS_RES_NPROF) out[9 + 2 * OWGS_RES_NPROF] = c->res_host_ns[0];
     if (cap > 10 + 2 * OWGS_RES_NPROF) out[10 + 2 * OWGS_RES_NPROF] = c->res_host_ns[1];
-    return 11 + 2 * OWGS_RES_NPROF;
+    if (cap > 11 + 2 * OWGS_RES_NPROF) out[11 + 2 * OWGS_RES_NPROF] = c->res_n_life;
+    if (cap > 12 + 2 * OWGS_RES_NPROF) out[12 + 2 * OWGS_RES_NPROF] = c->res_n_watch_calls;
+    return 13 + 2 * OWGS_RES_NPROF;
 }
 
 int owgs_engine_ms(owgs_ctx* c, float* ms) {

@@ -312,6 +312,8 @@ struct OwgsReleaseArgs {
 #define OWGS_RES_USED 49    // device: primary-table entries (live + deleted) after the last call
 #define OWGS_RES_GEN 50     // device: the walk-cursor generation reached (the host's next launch starts past it)
 #define OWGS_RES_TOMBS 51   // device: deleted primary-table entries after the last call
+#define OWGS_RES_WHY 52     // device: why the engine exited (0 the stop word, 1 idle, 2 its lifetime)
+#define OWGS_RES_WLIVE 53   // device: watched pairs left after the last call (when the launch has any)
 #define OWGS_RES_PROF 96    // device: the last call's counters (OWGS_RES_NPROF words: walk rounds, decisions,
                             // staging / release / publish cycles, overflow lookups, cursor hits, U shortcuts,
                             // decisions of the grouped walks)
@@ -329,6 +331,8 @@ struct OwgsReleaseArgs {
                             // names its record arrays in LDS instead: see spec_replay).
                             // Outputs (block `out`): out_inv i32[n_pub] | out_flags u8[n_pub] | rel_flags u8[n_rel]
 #define OWGS_RES_NHDR 16
+#define OWGS_RES_CALL_LIMIT 0x7FFFFF00ll     // the bell stays below this (a negative bell is the stop word)
+#define OWGS_RES_GEN_LIMIT 0xFFFFFF00ull     // the walk-cursor generation stays below this (compared by equality)
 #define OWGS_RES_CTL_WORDS 128
 #define OWGS_RES_BAIL_RELRISK 1  // a release could leave the LDS permit range: nothing applied, the host reruns the
                                  // call through the ordered release kernels
@@ -355,7 +359,17 @@ struct OwgsResArgs {
     uint2* cur;                  // [n_actions] walk cursor of each action: {generation, first walk step that may fit}
     uint32_t gen_base;           // first cursor generation of this launch (above every generation stored in cur)
     long long idle_ticks;        // s_memrealtime ticks (100 MHz) without a call before the engine writes back and exits
+    long long life_ticks;        // ... and ticks after its launch, checked between calls (0: no bound)
     int32_t spec;                // walk steps of each publish's speculative walk (0: decisions one at a time only)
+    // watched pairs after a reset (w.cap == 0: none): their releases in queue order with the
+    // empty-entry rule, and the Z marks of the walks that tried and failed at them, inside the engine.  The host indexes
+    // W by fqn@version key at launch: w_sidx (open addressing, w_scap a power of two) {slot + 1, first, count, primary
+    // action} -> w_list[first .. first + count) {W index, walk step of the pair's invoker in the primary action's walk
+    // (0x7FFFFFFF: not in its pool)}, by step
+    OwgsWatch w;
+    const uint4* w_sidx;
+    int32_t w_scap;
+    const uint2* w_list;
     // stream mode (owgs_replay_device through this engine): no doorbell, the stream's batches from HBM
     int32_t smode;
     int32_t s_nb;

@@ -108,6 +108,7 @@ __device__ __forceinline__ int select_in_word(uint32_t m, int need) {
 
 #define RES_CC 2048  // walk-cursor cache entries (LDS, 16 KB)
 #define RES_BF 2048  // Bloom filter words over the primary table's keys (LDS, 8 KB)
+#define RES_WF 256   // watched-key filter words (LDS, 1 KB): one bit per hashed fqn@version key with watched pairs
 #ifndef RES_FIRST_READ_KB
 #define RES_FIRST_READ_KB 4  // a call's input block: KB read together with the header (the rest in a second round)
 #endif
@@ -120,7 +121,7 @@ __device__ __forceinline__ int select_in_word(uint32_t m, int need) {
 #define RES_CLEAN_TOMBS (OWGS_CTC / 8)
 #endif
 struct ResLayout {
-    uint32_t P, ub, pc, ct, sc, cc, mv, bf, stage, end;
+    uint32_t P, ub, pc, ct, sc, cc, mv, bf, wf, stage, end;
 };
 __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
     const uint32_t words = (uint32_t)(n_ids + 31) / 32;
@@ -133,7 +134,8 @@ __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
     y.cc = y.sc + 64u * 4u;
     y.mv = y.cc + RES_CC * 8u;
     y.bf = y.mv + 64u * 4u;
-    y.stage = y.bf + RES_BF * 4u;
+    y.wf = y.bf + RES_BF * 4u;
+    y.stage = y.wf + RES_WF * 4u;
     y.end = y.stage;
     return y;
 }
@@ -200,6 +202,41 @@ __device__ __forceinline__ int ct_lookup_after(const uint2* ct, uint32_t key, ui
         e23 = *(const uint4*)&ct[h + 2];
     }
 }
+// watched pairs: the filter bit of an fqn@version key, the key's entry of the host-built
+// index (A.w_sidx: {slot + 1, first, count, primary action}), and x^-1 mod n for a walk step coprime to n
+__device__ __forceinline__ uint32_t wf_bit(uint32_t slot) { return (slot * 2654435761u) >> 19; }
+__device__ __forceinline__ bool wf_test(const uint32_t* wf, uint32_t slot) {
+    const uint32_t b = wf_bit(slot);
+    return (wf[b >> 5] >> (b & 31)) & 1u;
+}
+__device__ __forceinline__ bool res_w_sfind(const OwgsResArgs& A, uint32_t slot, uint4* e) {
+    const uint32_t m = (uint32_t)A.w_scap - 1u;
+    uint32_t h = ct_hash(slot + 1u) & m;
+    for (int p = 0; p < A.w_scap; ++p) {
+        const uint4 v = A.w_sidx[h];
+        if (v.x == slot + 1u) {
+            *e = v;
+            return true;
+        }
+        if (v.x == 0u) return false;
+        h = (h + 1u) & m;
+    }
+    return false;
+}
+__device__ __forceinline__ int res_inv_mod(int x, int n) {
+    int t = 0, nt = 1, r = n, nr = x % n;
+    while (nr) {
+        const int q = r / nr;
+        int tmp = t - q * nt;
+        t = nt;
+        nt = tmp;
+        tmp = r - q * nr;
+        r = nr;
+        nr = tmp;
+    }
+    return t < 0 ? t + n : t;
+}
+
 // both tables: index < OWGS_CTC primary, OWGS_CTC + j overflow entry j
 __device__ __forceinline__ int ct_lookup2(const uint2* ct, const uint32_t* bf, const OwgsOvf& O, bool ovf_on,
                                           uint32_t key, uint32_t* val) {
@@ -213,7 +250,9 @@ __device__ __forceinline__ int ct_lookup2(const uint2* ct, const uint32_t* bf, c
 
 }  // namespace
 
-// One workgroup of 256 threads; wave 0 decides, every wave loads, stages and writes back.
+// One workgroup of 256 threads; wave 0 decides, every wave loads, stages and writes back.  SMODE: stream mode
+// (owgs_replay_device, OWGS_SPEC_REPLAY=1) -- a separate instantiation, so the shim's engine carries none of its code.
+template <bool SMODE>
 __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
     extern __shared__ uint4 lds_raw[];
     char* Lb = (char*)lds_raw;
@@ -226,6 +265,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
     uint2* cc = (uint2*)(Lb + Y.cc);
     int32_t* mv = (int32_t*)(Lb + Y.mv);
     uint32_t* bf = (uint32_t*)(Lb + Y.bf);
+    uint32_t* wf = (uint32_t*)(Lb + Y.wf);
     char* stg = Lb + Y.stage;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int n_slots = A.n_slots, nm = A.nm, nb = A.nb;
@@ -235,7 +275,15 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
     if (tid < 16) sc[tid] = (tid == RS_U0 || tid == RS_U1) ? (int)0x80000000 : (tid == RS_GEN ? (int)A.gen_base : 0);
     for (int i = tid; i < RES_CC; i += 256) cc[i] = make_uint2(0u, 0u);
     for (int i = tid; i < RES_BF; i += 256) bf[i] = 0u;
+    for (int i = tid; i < RES_WF; i += 256) wf[i] = 0u;
     __syncthreads();
+    for (int i = tid; A.w.cap > 0 && i < A.w_scap; i += 256) {  // the keys with watched pairs
+        const uint32_t k = A.w_sidx[i].x;
+        if (k != 0u) {
+            const uint32_t b = wf_bit(k - 1u);
+            atomicOr(&wf[b >> 5], 1u << (b & 31));
+        }
+    }
     {
         int used = 0, tombs = 0, mx = (int)0x80000000, u0 = (int)0x80000000, u1 = (int)0x80000000, e = 0;
         for (int i = tid; i < n_slots; i += 256) {
@@ -304,7 +352,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
     };
     // stream mode (owgs_replay_device): no doorbell; the calls are the stream's batches, each as pieces of its
     // releases and then of its publishes that fit the staging area, read from HBM
-    const bool smode = A.smode != 0;
+    constexpr bool smode = SMODE;
     if (tid == 0 && !smode) st_sys(&A.ctl[OWGS_RES_STATE], 1);
     int s_b = 0, s_ph = 0;                  // (thread 0, stream mode) batch, phase (0 releases, 1 publishes),
     long long s_o = 0, s_r0 = 0, s_r1 = 0, s_p0 = 0, s_p1 = 0;  // offset in the phase, the batch's ranges
@@ -314,6 +362,8 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
     // ------------------------------------------------------------------ calls
     int last = A.last_call;
     u64 t_idle = __builtin_amdgcn_s_memrealtime();
+    const u64 t_launch = t_idle;
+    int why = 0;  // (thread 0) why the engine exits: 0 the stop word, 1 idle, 2 its lifetime (OWGS_RES_WHY)
     for (;;) {
         if (smode) {
             if (tid == 0) {
@@ -377,8 +427,12 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 k = ld_sys(&A.ctl[OWGS_RES_BELL]);
                 if (k != last) break;
                 const u64 now = __builtin_amdgcn_s_memrealtime();
-                if ((long long)(now - t_idle) > A.idle_ticks || spin > (1ll << 32)) {
+                // idle, or (between calls) past the launch's lifetime: the hardware queue this kernel holds may be
+                // shared with another context's stream, whose launches wait behind it until it exits
+                const bool life = A.life_ticks > 0 && (long long)(now - t_launch) > A.life_ticks;
+                if ((long long)(now - t_idle) > A.idle_ticks || life || spin > (1ll << 32)) {
                     stop = true;
+                    why = life ? 2 : 1;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(4);
@@ -691,7 +745,11 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                     uint32_t rv = 0u;
                     int rix = -1;
                     if (cr) rix = ct_lookup2(ct, bf, A.ovf, ovf_on, rkey, &rv);
-                    const bool prim = cr && rix >= 0 && rix < OWGS_CTC;
+                    // a release of an fqn@version key with watched pairs: below, with the empty-entry rule
+                    const bool wat = cr && A.w.cap > 0 && wf_test(wf, rr.z & 0x1FFFFu) &&
+                                     __hip_atomic_load(&A.w.wkey[rr.z & 0x1FFFFu], __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT) > 0;
+                    const bool prim = cr && !wat && rix >= 0 && rix < OWGS_CTC;
                     // releases of one primary entry in this group: the j-th of them (queue order) finds the entry as
                     // the j before it leave it -- RS.release(1, true) j times from (c0, o0): c0 + j free slots, a
                     // container's memory back each time that count reaches a multiple of maxConcurrent, the entry
@@ -723,7 +781,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                     } else {
                         eq = prim ? (1ull << lane) : 0ull;
                     }
-                    if (cr && rix < 0) flag = OWGS_REL_NOSUCH_BIT;  // NoSuchElementException (NS:103)
+                    if (cr && !wat && rix < 0) flag = OWGS_REL_NOSUCH_BIT;  // NoSuchElementException (NS:103)
                     if (prim && !((dup >> lane) & 1ull)) {
                         const int c0 = (int)(rv & OWGS_CT_C_MASK), o0 = ct_ops(rv);
                         const int j = (int)__popcll(eq & ((1ull << lane) - 1ull)), cnt = (int)__popcll(eq);
@@ -741,7 +799,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                         }
                     }
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                    u64 cm = dup | __ballot(cr && rix >= OWGS_CTC);
+                    u64 cm = dup | __ballot(cr && !wat && rix >= OWGS_CTC);
                     while (cm) {
                         const int q = ffs64(cm);
                         cm &= cm - 1;
@@ -767,6 +825,87 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             }
                         }
                         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    }
+                    // releases of keys with watched pairs (after updateCluster, SCPB:561-584, discarded the entries of
+                    // activations still in flight): releaseConcurrent (NS:98-113) applies RS.release(1, true) to the
+                    // entry it finds -- operationCount may count below 0 -- and removes it at 0; an absent entry throws
+                    // NoSuchElement (NS:103) unless the reference holds the empty entry a failed try left (Z,
+                    // getOrElseUpdate NS:61-62), which then takes the release.  d (in flight - operationCount) falls
+                    // only with a throw; the pair leaves W at 0.  Releases of distinct keys commute: each lane applies
+                    // its own at once; a key with several releases in the group, and every release that needs the
+                    // empty entry inserted, go one at a time in queue order
+                    if (__ballot(wat)) {
+                        u64 wdup = 0ull;
+                        for (u64 bb = __ballot(wat); bb;) {
+                            const int q = ffs64(bb);
+                            const uint32_t kq = (uint32_t)__builtin_amdgcn_readlane((int)rkey, q);
+                            const u64 g = __ballot(wat && rkey == kq);
+                            if (g & (g - 1ull)) wdup |= g;
+                            bb &= ~g;
+                        }
+                        const int wslot = (int)(rr.z & 0x1FFFFu);
+                        // one RS.release(1, true) on a present entry (ix, v), or the throw / the empty entry's turn
+                        auto w_apply = [&](int ix, uint32_t v, int wj, uint32_t wv) {
+                            const int cc0 = (int)(v & OWGS_CT_C_MASK), o1 = ct_ops(v) - 1;
+                            int c1 = cc0 + 1;
+                            if (c1 % maxc == 0) {  // RS:45-52: a whole container free -> its memory
+                                c1 -= maxc;
+                                atomicAdd(&P[inv], mem);
+                            }
+                            if (o1 < -OWGS_MAX_OPS) err |= OWGS_ERR_OPS;
+                            const bool removed = o1 == 0;  // NS:109-111
+                            const uint32_t nk = removed ? OWGS_CT_TOMB : rkey, nv = removed ? 0u : ct_val(c1, o1);
+                            if (ix < OWGS_CTC) ct[ix] = make_uint2(nk, nv);
+                            else ovf_st(A.ovf.t, ix - OWGS_CTC, nk, nv);
+                            tombs += removed && ix < OWGS_CTC;
+                            if (removed && wj >= 0 && (wv & OWGS_W_Z))  // the removal drops the empty entry too
+                                __hip_atomic_store(&A.w.vals[wj], wv & ~OWGS_W_Z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        };
+                        auto w_throw = [&](int wj, uint32_t wv) {
+                            flag = OWGS_REL_NOSUCH_BIT;  // NoSuchElementException (NS:103)
+                            if (wj < 0) return;
+                            const int d = (int)(wv & ~OWGS_W_Z) - 1;  // one in-flight activation fewer, entry absent
+                            if (d <= 0) {
+                                __hip_atomic_store(&A.w.vals[wj], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                __hip_atomic_store(&A.w.keys[wj], OWGS_CT_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                atomicSub(&A.w.wkey[wslot], 1);
+                                atomicSub(A.w.cnt, 1);
+                            } else {
+                                __hip_atomic_store(&A.w.vals[wj], (uint32_t)d | (wv & OWGS_W_Z), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+                            }
+                        };
+                        bool wser = wat && ((wdup >> lane) & 1ull);
+                        if (wat && !wser) {
+                            const int wj = w_find(A.w, rkey);
+                            const uint32_t wv = wj >= 0 ? __hip_atomic_load(&A.w.vals[wj], __ATOMIC_RELAXED,
+                                                                             __HIP_MEMORY_SCOPE_AGENT)
+                                                        : 0u;
+                            if (rix >= 0) w_apply(rix, rv, wj, wv);
+                            else if (wv & OWGS_W_Z) wser = true;  // the empty entry goes into the table: one at a time
+                            else w_throw(wj, wv);
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                        for (u64 sm = __ballot(wser); sm; sm &= sm - 1ull) {
+                            const int q = ffs64(sm);
+                            if (lane == q) {
+                                const int wj = w_find(A.w, rkey);
+                                const uint32_t wv = wj >= 0 ? __hip_atomic_load(&A.w.vals[wj], __ATOMIC_RELAXED,
+                                                                                 __HIP_MEMORY_SCOPE_AGENT)
+                                                            : 0u;
+                                uint32_t v;
+                                int ix = ct_lookup2(ct, bf, A.ovf, ovf_on, rkey, &v);
+                                if (ix < 0 && (wv & OWGS_W_Z)) {  // the reference's empty entry {0, 0} takes it
+                                    ix = insert(rkey, 0u);
+                                    v = 0u;
+                                }
+                                if (ix >= 0) w_apply(ix, v, wj, wv);
+                                else w_throw(wj, wv);
+                            }
+                            used = __builtin_amdgcn_readlane(used, q);
+                            ovf_on = __builtin_amdgcn_readlane((int)ovf_on, q) != 0;
+                            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                        }
                     }
                     pr_c_relc += clock64() - trc;
                     if (valid) rel_fl[j] = flag;
@@ -1256,8 +1395,10 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 // the key's container at the target: a slot taken, or a new one (NS:63-79); decisions of
                                 // one key at one invoker leave values whose operationCount grows with each: the largest
                                 // is the last one's
-                                if (l_cc && c_ix >= 0 && c_ix < OWGS_CTC) atomicMax(&ct[c_ix].y, c_nv);
-                                else if (l_cc && c_ix >= OWGS_CTC) atomicMax(&A.ovf.t[c_ix - OWGS_CTC].y, c_nv);
+                                // (signed: c | operationCount << 12 as an int orders by operationCount, which a
+                                // watched pair's entry may hold below 0)
+                                if (l_cc && c_ix >= 0 && c_ix < OWGS_CTC) atomicMax((int*)&ct[c_ix].y, (int)c_nv);
+                                else if (l_cc && c_ix >= OWGS_CTC) atomicMax((int*)&A.ovf.t[c_ix - OWGS_CTC].y, (int)c_nv);
                                 o_v = sp_t;
                                 o_f = sp == SP_FORCED ? 1 : 0;
                             }
@@ -1277,13 +1418,13 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                     for (int p = 0; p < OWGS_CTC;) {
                                         const uint32_t k = ct[h].x;
                                         if (k == key) {
-                                            atomicMax(&ct[h].y, c_nv);
+                                            atomicMax((int*)&ct[h].y, (int)c_nv);
                                             break;
                                         }
                                         if (k == 0u || k == OWGS_CT_TOMB) {
                                             const uint32_t old = atomicCAS((uint32_t*)&ct[h].x, k, key);
                                             if (old == k) {
-                                                atomicMax(&ct[h].y, c_nv);  // (a free entry holds value 0)
+                                                atomicMax((int*)&ct[h].y, (int)c_nv);  // (a free entry holds 0)
                                                 bf_add(bf, key);
                                                 fresh = k == 0u;
                                                 tombs -= k == OWGS_CT_TOMB;
@@ -1307,9 +1448,10 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 if (lane == 0) {
                                     uint32_t v0;
                                     const int ix = ct_lookup2(ct, bf, A.ovf, ovf_on, key, &v0);
+                                    const uint32_t mv0 = (uint32_t)max((int)v0, (int)nvj);  // (signed, as above)
                                     if (ix < 0) insert(key, nvj);
-                                    else if (ix < OWGS_CTC) ct[ix].y = max(v0, nvj);
-                                    else ovf_st_val(A.ovf.t, ix - OWGS_CTC, max(v0, nvj));
+                                    else if (ix < OWGS_CTC) ct[ix].y = mv0;
+                                    else ovf_st_val(A.ovf.t, ix - OWGS_CTC, mv0);
                                 }
                                 used = __builtin_amdgcn_readfirstlane(used);
                                 ovf_on = __builtin_amdgcn_readfirstlane((int)ovf_on) != 0;
@@ -1444,6 +1586,64 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                     if (lane < nq) {
                         out_inv[i0 + lane] = o_v;
                         out_fl[i0 + lane] = (uint8_t)o_f;
+                    }
+                    // Z marks (watched pairs): a concurrent decision's walk tried every usable invoker before the step
+                    // it took -- all of them before an overload fallback -- and a failed try leaves the reference an
+                    // empty entry (getOrElseUpdate, NS:61-62).  Per action of the chunk its deepest walk marks the
+                    // watched pairs of its key at the steps before (the host's index lists them by step in the
+                    // key's primary action's walk; another action of the key computes each pair's step).  A mark on a
+                    // pair whose entry is present is never read: the entry's removal clears it
+                    if (A.w.cap > 0) {
+                        const int wmx = (int)((me.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
+                        const bool wd = lane < nq && !(me.y & (OWGS_AM_EMPTY | OWGS_AM_THROW)) && wmx > 1 && o_v >= 0 &&
+                                        wf_test(wf, me.z & 0x1FFFFu);
+                        if (__ballot(wd)) {
+                            const int wpool = (me.x & OWGS_AM_POOL) ? 1 : 0;
+                            const int wn = wpool ? nb : nm, wbase = wpool ? A.n_ids - nb : 0;
+                            const int whome = (int)(me.x & OWGS_AM_POS_MASK), wstep = (int)((me.x >> 15) & OWGS_AM_POS_MASK);
+                            int winv = 0, depth = 0;
+                            if (wd) {
+                                winv = wn > 1 ? res_inv_mod(wstep % wn, wn) : 0;
+                                if (o_f & 1) {
+                                    depth = 0x7FFFFFFF;  // n + 2 failed probes, then the forced acquire (SCPB:417-424)
+                                } else {
+                                    const int d = (o_v - wbase - whome + wn) % wn;
+                                    depth = wn > 1 ? (int)(((long long)d * winv) % wn) : 0;
+                                }
+                            }
+                            bool lead = false;
+                            for (u64 bb = __ballot(wd); bb;) {  // one leader per action: its deepest walk
+                                const int q = ffs64(bb);
+                                const uint32_t aq = (uint32_t)__builtin_amdgcn_readlane((int)l_act, q);
+                                const bool in_g = wd && l_act == aq;
+                                const int dd = wave_max_i(in_g ? depth : -1);
+                                if (lane == q) {
+                                    lead = true;
+                                    depth = dd;
+                                }
+                                bb &= ~__ballot(in_g);
+                            }
+                            uint4 e;
+                            if (lead && depth > 0 && res_w_sfind(A, me.z & 0x1FFFFu, &e)) {
+                                const bool primary = e.w == l_act;
+                                for (uint32_t k = e.y; k < e.y + e.z; ++k) {
+                                    const uint2 pe = A.w_list[k];
+                                    if (primary && (int)pe.y >= depth) break;  // (the list is by step)
+                                    const uint32_t key = __hip_atomic_load(&A.w.keys[pe.x], __ATOMIC_RELAXED,
+                                                                           __HIP_MEMORY_SCOPE_AGENT);
+                                    if (key == 0u || key == OWGS_CT_TOMB) continue;
+                                    const int x = (int)(key & 0x7FFFu) - 1;
+                                    if (x < 0 || x >= A.n_ids || !((ub[x >> 5] >> (x & 31)) & 1u)) continue;  // not tried
+                                    if (!primary) {
+                                        const int pos = x - wbase;
+                                        if (pos < 0 || pos >= wn) continue;
+                                        const int s = wn > 1 ? (int)(((long long)((pos - whome + wn) % wn) * winv) % wn) : 0;
+                                        if (s >= depth) continue;
+                                    }
+                                    atomicOr(&A.w.vals[pe.x], OWGS_W_Z);
+                                }
+                            }
+                        }
                     }
                 }
                 pr_pub += clock64() - tp0;
@@ -1582,6 +1782,8 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
             st_sys(&A.ctl[OWGS_RES_RESULT], bail | (e << 8));
             st_sys(&A.ctl[OWGS_RES_USED], sc[RS_USED]);
             st_sys(&A.ctl[OWGS_RES_TOMBS], sc[RS_TOMB]);
+            if (A.w.cap > 0)
+                st_sys(&A.ctl[OWGS_RES_WLIVE], __hip_atomic_load(A.w.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             st_sys(&A.ctl[OWGS_RES_DONE], k);
         }
@@ -1604,6 +1806,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
     __threadfence();
     __syncthreads();
     if (tid == 0 && !smode) {
+        st_sys(&A.ctl[OWGS_RES_WHY], why);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         st_sys(&A.ctl[OWGS_RES_STATE], 2);
     }
@@ -1616,12 +1819,16 @@ extern "C" size_t owgs_resident_image_bytes(int32_t n_slots, int32_t n_ids) {
 extern "C" hipError_t owgs_launch_resident(const OwgsResArgs* a, size_t lds_bytes, hipStream_t s) {
     static bool attr = false;  // (per process: one device geometry)
     if (!attr) {
-        const hipError_t e = hipFuncSetAttribute((const void*)owgs_resident_kernel,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, OWGS_LDS_BYTES);
+        hipError_t e = hipFuncSetAttribute((const void*)owgs_resident_kernel<false>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, OWGS_LDS_BYTES);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)owgs_resident_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    OWGS_LDS_BYTES);
         if (e != hipSuccess) return e;
         attr = true;
     }
     if (lds_bytes > OWGS_LDS_BYTES || a->n_slots > OWGS_MAX_SLOTS_CT) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(owgs_resident_kernel, dim3(1), dim3(256), lds_bytes, s, *a);
+    if (a->smode) hipLaunchKernelGGL(owgs_resident_kernel<true>, dim3(1), dim3(256), lds_bytes, s, *a);
+    else hipLaunchKernelGGL(owgs_resident_kernel<false>, dim3(1), dim3(256), lds_bytes, s, *a);
     return hipGetLastError();
 }

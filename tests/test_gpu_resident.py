@@ -24,20 +24,27 @@ class Shim:
     """The shim's batching thread over one workload: jobs in arrival order (a batch's completions, then its
     publishes), drained `drain` jobs at a time into runs; releases name the invoker of the activation's decision."""
 
-    def __init__(self, w, zombies=True):
+    def __init__(self, w, zombies=True, shadow=False):
         self.w = w
         self.g = GpuShardingContainerPoolBalancer(managed_fraction=w.managed_fraction,
                                                   blackbox_fraction=w.blackbox_fraction, rng_seed=w.rng_seed)
         self.o = O.BalancerState(w.managed_fraction, w.blackbox_fraction, rng_seed=w.rng_seed, zombies=zombies)
-        self.g.update_invokers_arrays(w.inv_ids, w.inv_mem, w.inv_status)
-        self.o.update_invokers(w.inv_ids, w.inv_mem, w.inv_status)
-        if w.cluster_size != 1:
-            self.g.update_cluster(w.cluster_size)
-            self.o.update_cluster(w.cluster_size)
+        # shadow: the oracle WITHOUT the reference's empty entries, driven alike (its release flags show whether a
+        # stream reaches the releases that only those entries explain)
+        self.z = O.BalancerState(w.managed_fraction, w.blackbox_fraction, rng_seed=w.rng_seed, zombies=False) \
+            if shadow else None
+        self.z_rf, self.o_rf = [], []
+        for b in (self.g, self.o) + ((self.z,) if self.z else ()):
+            (b.update_invokers_arrays if b is self.g else b.update_invokers)(w.inv_ids, w.inv_mem, w.inv_status)
+            if w.cluster_size != 1:
+                b.update_cluster(w.cluster_size)
         self.gh, _ = self.g.register_actions(w.actions)
         keys = {}
         self.oh = [self.o.register_action(a.namespace, a.path, keys.setdefault(a.key, len(keys)), a.mem_mb,
                                           a.max_concurrent, a.blackbox) for a in w.actions]
+        if self.z:
+            for a in w.actions:
+                self.z.register_action(a.namespace, a.path, keys[a.key], a.mem_mb, a.max_concurrent, a.blackbox)
         s = w.stream
         self.jobs = []
         for b in range(s.n_batches):
@@ -68,12 +75,17 @@ class Shim:
                 ri.append(int(self.dec[a]))
                 ra.append(int(self.gh[act[a]]))
                 orf.append(O._rel_bits(self.o.release(int(self.dec[a]), self.oh[act[a]])))
+                if self.z:
+                    self.z_rf.append(O._rel_bits(self.z.release(int(self.dec[a]), self.oh[act[a]])))
+                    self.o_rf.append(orf[-1])
             while i < len(batch) and batch[i][0] == 1:
                 a = batch[i][1]
                 i += 1
                 pubs.append(a)
                 pa.append(int(self.gh[act[a]]))
                 x, f = self.o.publish(self.oh[act[a]], self.seq + len(oi))
+                if self.z:
+                    self.z.publish(self.oh[act[a]], self.seq + len(oi))
                 oi.append((int(x), int(f)))
                 self.dec[a] = x
             ro.append(len(ri))
@@ -105,7 +117,7 @@ def test_resident_small_drains_match_oracle(cfg, kw):
         pubs += n
     st = sh.g.resident_stats()
     assert st["served"] == sh.calls and st["chained"] == 0 and st["refused"] == 0, st
-    assert st["launches"] == 1, st
+    assert st["launches"] - st["life_exits"] == 1, st  # (relaunches only at the lifetime bound, OWGS_RES_LIFE_US)
     assert np.array_equal(sh.g.permits(), sh.o.permits())
     assert sh.g.resident_stats()["alive"] == 0  # permits() stopped it (the state was written back)
     assert pubs == int(w.stream.acq_off[-1])
@@ -167,7 +179,7 @@ def test_resident_engine_exits_when_idle_and_relaunches():
         sh.call(200)
         time.sleep(0.1)
     st = sh.g.resident_stats()
-    assert st["served"] == 5 and st["launches"] == 5, st
+    assert st["served"] == 5 and st["launches"] - st["life_exits"] == 5, st
     while not sh.done():
         sh.call(300)
     assert np.array_equal(sh.g.permits(), sh.o.permits())
@@ -289,3 +301,128 @@ def test_resident_speculation_budgets(budget):
     env = dict(os.environ, OWGS_RES_SPEC=budget)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+_WRAP_SCRIPT = r"""
+import sys
+sys.path[:0] = [{root!r}, {oracle!r}, {tests!r}]
+import numpy as np
+import test_gpu_resident as T
+from openwhisk_amd import workload as W
+w = W.config("c4", n_activations=60_000)
+sh = T.Shim(w)
+rng = np.random.default_rng(4)
+while not sh.done():
+    sh.call(int(rng.integers(20, 120)))
+st = sh.g.resident_stats()
+assert st["served"] == sh.calls and st["chained"] == 0 and st["refused"] == 0, st
+assert st["launches"] - st["life_exits"] >= 3, st
+assert np.array_equal(sh.g.permits(), sh.o.permits())
+print("ok", sh.calls, st["launches"], st["life_exits"])
+"""
+
+
+def test_resident_doorbell_and_cursor_generation_wrap():
+    """The doorbell counts calls and the walk-cursor generation counts release runs, both for the life of a context
+    (ADVICE r04): a context started just below both limits (OWGS_RES_CALL_BASE, OWGS_RES_GEN_BASE; read once per
+    process, so a child process) crosses them -- the library stops the engine before either wraps and the relaunch
+    starts both over (the stored cursors cleared) -- and every call stays resident and bit-exact."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    code = _WRAP_SCRIPT.format(root=root, oracle=os.path.join(root, "oracle"), tests=here)
+    env = dict(os.environ, OWGS_RES_CALL_BASE=str(0x7FFFFF00 - 8 - 150), OWGS_RES_GEN_BASE=str(0xFFFFFF00 - 2 - 400),
+               OWGS_RES_IDLE_US="2000000", OWGS_RES_LIFE_US="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_resident_lifetime_bound_and_other_contexts_on_shared_queues():
+    """The resident engine holds its stream's hardware queue while it runs, and GPU_MAX_HW_QUEUES (4) makes the
+    streams of several contexts share queues: three contexts in one process, each driven by its own thread -- one
+    serving small drains on the resident engine without pause, two taking the launch chain (drains beyond OWGS_RES_MAX)
+    and device replays -- all finish, every call bit-exact, because the engine exits between calls at its lifetime
+    bound (OWGS_RES_LIFE_US, 100 ms) and is relaunched."""
+    import threading
+    res = {}
+
+    def resident():
+        sh = Shim(W.config("c4", n_activations=120_000))
+        rng = np.random.default_rng(1)
+        while not sh.done():
+            sh.call(int(rng.integers(50, 400)))
+        res["resident"] = (sh.g.resident_stats(), np.array_equal(sh.g.permits(), sh.o.permits()))
+
+    def chained(name, cfg):
+        sh = Shim(W.config(cfg, n_activations=60_000))
+        while not sh.done():
+            sh.call(3000)
+        st = sh.g.resident_stats()
+        res[name] = (st, np.array_equal(sh.g.permits(), sh.o.permits()))
+
+    def replays():
+        w = W.config("c2", n_activations=200_000)
+        o = O.state_for(w)
+        g = GpuShardingContainerPoolBalancer(managed_fraction=w.managed_fraction,
+                                             blackbox_fraction=w.blackbox_fraction, rng_seed=w.rng_seed)
+        g.update_invokers_arrays(w.inv_ids, w.inv_mem, w.inv_status)
+        g.register_actions(w.actions)
+        out, fl, rf = g.replay(w.stream)
+        oo, of, orf = o.replay(w.stream)
+        res["replay"] = (np.array_equal(out, oo) and np.array_equal(fl, of), np.array_equal(g.permits(), o.permits()))
+
+    ts = [threading.Thread(target=resident), threading.Thread(target=chained, args=("chain", "headline")),
+          threading.Thread(target=replays)]
+    t0 = time.time()
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in ts), f"a context did not finish within 100 s ({time.time() - t0:.1f} s)"
+    st, ok = res["resident"]
+    assert ok and st["served"] > 100 and st["chained"] == 0, st
+    st, ok = res["chain"]
+    assert ok and st["chained"] > 0, st
+    assert res["replay"] == (True, True)
+
+
+@pytest.mark.parametrize("cfg,kw,sizes", [
+    ("c4", dict(n_activations=60_000), (2, 1)),
+    ("headline", dict(n_activations=60_000, n_invokers=1000, n_actions=2000, n_namespaces=200, conc_frac=0.3), (2,)),
+    ("hot", None, (2, 3)),
+])
+def test_resident_serves_watched_pairs_after_membership_changes(cfg, kw, sizes):
+    """updateCluster (SCPB:561-584) discards the NestedSemaphore entries of activations still in flight, so their
+    releases meet the new state: a present entry takes RS.release(1, true) whatever its operationCount, an absent one
+    throws NoSuchElement (NS:103) unless a failed concurrent try left the reference an empty entry (NS:61-62).  The
+    resident engine applies these releases and marks the failed tries itself, so the shim's small drains stay on it
+    after a membership change: >= 95 % of the calls after the change are resident-served, every call bit-exact with
+    the literal oracle, and the oracle without empty entries disagrees (the stream reaches those releases)."""
+    w = _hot_small_pool(21, n_activations=30_000) if cfg == "hot" else W.config(cfg, **kw)
+    sh = Shim(w, shadow=True)
+    rng = np.random.default_rng(17)
+    n_jobs = len(sh.jobs)
+    at = [int(n_jobs * (k + 1) / (len(sizes) + 2)) for k in range(len(sizes))]
+    before = after = 0
+    st0 = None
+    while not sh.done():
+        if at and sh.pos >= at[0]:
+            at.pop(0)
+            x = sizes[len(sizes) - len(at) - 1]
+            for b in (sh.g, sh.o, sh.z):
+                b.update_cluster(x)
+            if st0 is None:
+                st0 = sh.g.resident_stats()
+        sh.call(int(rng.integers(1, 600)))
+        if st0 is None:
+            before += 1
+        else:
+            after += 1
+    st = sh.g.resident_stats()
+    served_after = st["served"] - st0["served"]
+    assert served_after >= 0.95 * after, (served_after, after, st)
+    assert st["watch_calls"] > 0, st
+    assert np.array_equal(sh.g.permits(), sh.o.permits())
+    assert sh.z_rf != sh.o_rf  # releases only the reference's empty entries explain were reached

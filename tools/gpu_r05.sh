@@ -1,0 +1,82 @@
+#!/bin/bash
+# Round-5 GPU steps, selected by $STEPS (space separated); outputs under gpurun_out/r05/$TAG.  Each step runs under its
+# own time limit and the script stops at the first step that fails (no GPU step after a failure).
+#   tests      full GPU suite                       restests  the resident / shim suites only
+#   smoke      __graft_entry__.smoke()              bench     bench line (default args)
+#   prof       kernel trace of the bench            cfgs      one bench line per config
+#   pmc        HBM traffic per bench key            sq        SQ counters of the headline engine
+#   shim       the shim leg (drains 64, 512, 4096)  abshim    same-box A/B of the shim leg vs variants/libowgs_$AB_BASE.so
+#   abcfg      same-box A/B of per-config engine rates vs variants/libowgs_$AB_BASE.so
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/r05/${TAG:-a}; mkdir -p $O; export TMPDIR=/tmp
+stop() { echo "STEP $1 rc=$2 -- stopping"; exit "$2"; }
+for s in ${STEPS:-tests}; do
+  case "$s" in
+    tests)
+      timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
+      rc=$?; tail -2 $O/pytest_gpu.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/pytest_gpu.log | head -20; stop tests $rc; } ;;
+    restests)
+      timeout -k 10 500 python -u -m pytest tests/test_gpu_resident.py tests/test_gpu_shim_sequence.py ${TESTSEL} -x -v --timeout 200 --timeout-method thread > $O/pytest_res.log 2>&1
+      rc=$?; tail -2 $O/pytest_res.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/pytest_res.log | head -20; stop restests $rc; } ;;
+    sel)  # the tests named by $TESTSEL
+      timeout -k 10 600 python -u -m pytest $TESTSEL -x -v --timeout 200 --timeout-method thread > $O/pytest_sel.log 2>&1
+      rc=$?; tail -2 $O/pytest_sel.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/pytest_sel.log | head -20; stop sel $rc; } ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
+      rc=$?; tail -1 $O/smoke.log; [ $rc -eq 0 ] || stop smoke $rc ;;
+    bench)
+      timeout -k 10 400 python bench.py ${BENCHARGS} > $O/bench.json 2> $O/bench.err
+      rc=$?; cut -c1-400 $O/bench.json; [ $rc -eq 0 ] || { tail -20 $O/bench.err; stop bench $rc; } ;;
+    prof)
+      rm -rf $O/prof
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- \
+        python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-check --no-h2d --no-shim-path > $O/prof.log 2>&1
+      rc=$?; tail -1 $O/prof.log | cut -c1-200; [ $rc -eq 0 ] || stop prof $rc ;;
+    cfgs)
+      rm -f $O/cfgs.jsonl
+      for c in "--config c2" "--config c2_64k" "--config c3" "--config c4" "--cluster-size 2" "--cluster-size 4" "--cluster-size 8"; do
+        timeout -k 10 400 python bench.py $c --steps 5 --warmup 1 --no-h2d --no-shim-path >> $O/cfgs.jsonl 2>> $O/cfgs.err
+        rc=$?; tail -1 $O/cfgs.jsonl | cut -c1-160; [ $rc -eq 0 ] || { tail -20 $O/cfgs.err; stop "cfg $c" $rc; }
+      done ;;
+    pmc)
+      for c in ${PMCCFGS:-"" "--cluster-size 8" "--config c2" "--config c4"}; do
+        f=$O/pmc_traffic$(echo $c | tr -d ' -').log
+        timeout -k 10 400 python3 tools/pmc_traffic.py $c > $f 2>&1
+        rc=$?; tail -1 $f | cut -c1-200; [ $rc -eq 0 ] || stop "pmc $c" $rc
+      done
+      cp pmc_traffic.json $O/pmc_traffic.json ;;
+    sq)
+      timeout -k 10 600 bash tools/pmc_run.sh --config headline > $O/sq.log 2>&1
+      rc=$?; tail -3 $O/sq.log; [ $rc -eq 0 ] || stop sq $rc
+      cp gpurun_out/pmc/summary.txt $O/sq_pmc.txt ;;
+    shim)
+      timeout -k 10 300 python tools/shim_leg.py --drains ${DRAINS:-64,512,4096} > $O/shim.json 2> $O/shim.err
+      rc=$?; cut -c1-300 $O/shim.json; [ $rc -eq 0 ] || { tail -5 $O/shim.err; stop shim $rc; } ;;
+    abshim)  # alternating runs on one box: in-tree library, then the base variant, twice
+      B=openwhisk_amd/variants/libowgs_${AB_BASE:-r04}.so
+      for i in 1 2; do
+        for lib in openwhisk_amd/libowgs.so $B; do
+          n=$(basename $lib .so)_$i
+          OWGS_LIB=$lib timeout -k 10 200 python tools/shim_leg.py --drains ${DRAINS:-64,512} --modes fused > $O/shim_$n.json 2> $O/shim_$n.err || { tail -5 $O/shim_$n.err; stop abshim 1; }
+          python3 -c "
+import json
+d=json.load(open('$O/shim_$n.json'))
+for l in d['legs']:
+    r=l.get('resident') or {}; s=max(1, r.get('served', 0))
+    print('$n', l['mode'], l['drain'], 'p50', l['p50_us'], 'p99', l.get('p99_us'), round(l['decisions_per_s']/1e6,2), 'M/s pub', round(r.get('publish_cycles',0)/s), 'alone', round(r.get('alone_cycles',0)/s))
+" | tee -a $O/abshim.txt
+        done
+      done ;;
+    abcfg)  # engine rates per config, in-tree library vs the base variant, alternating
+      B=openwhisk_amd/variants/libowgs_${AB_BASE:-r04}.so
+      for i in 1 2; do
+        for lib in openwhisk_amd/libowgs.so $B; do
+          echo "-- $lib" >> $O/abcfg.txt
+          OWGS_LIB=$lib REPS=3 timeout -k 10 300 python -u tools/prof_phases.py ${ABCFGS:-c2 c4 headline:0/8 headline} > $O/abcfg_$i.log 2>&1
+          rc=$?; grep -v amdgpu.ids $O/abcfg_$i.log | grep -v cycles/activation | cut -c1-120 | tee -a $O/abcfg.txt; [ $rc -eq 0 ] || stop abcfg $rc
+        done
+      done ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "ALL STEPS OK"
