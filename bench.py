@@ -53,6 +53,9 @@ def parse(argv=None):
     ap.add_argument("--no-h2d", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-shim-path", action="store_true", help="skip the shim-path leg (per-call latency)")
+    ap.add_argument("--health-group", type=int, default=8,
+                    help="per-batch health cadence: batches per engine launch (owgs_replay_device_group; 1 = one "
+                         "owgs_update_health_device + owgs_replay_device_span per batch)")
     ap.add_argument("--health-churn", action="store_true",
                     help="N = 1: replay batch by batch with the per-batch health schedule of the N > 1 runs "
                          "(cluster.health_schedule) instead of one launch per step")
@@ -389,9 +392,13 @@ def shim_extra_legs(w, b, kind, ids, act, o_inv, budget=480_000, seed=0x5EED):
     lat, sizes = np.array(lat), np.array(sizes)
     done = inv != -9
     small = sizes <= 1024
+    flip = small & np.concatenate([[False], sizes[:-1] > 1024])  # a small call right after a chained one: relaunch
     out.append({"mode": "fused-mixed", "drain": "log-uniform 1..4096", "jobs": n_jobs, "calls": len(lat),
                 "publishes": int(n_pub), "p50_us": float(np.percentile(lat, 50)), "p99_us": float(np.percentile(lat, 99)),
                 "p50_us_le1024": float(np.percentile(lat[small], 50)), "p99_us_le1024": float(np.percentile(lat[small], 99)),
+                "p50_us_le1024_after_chain": float(np.percentile(lat[flip], 50)) if flip.any() else None,
+                "p50_us_le1024_steady": float(np.percentile(lat[small & ~flip], 50)),
+                "p99_us_le1024_steady": float(np.percentile(lat[small & ~flip], 99)),
                 "p50_us_gt1024": float(np.percentile(lat[~small], 50)) if (~small).any() else None,
                 "p99_us_gt1024": float(np.percentile(lat[~small], 99)) if (~small).any() else None,
                 "decisions_per_s": n_pub / max(float(lat.sum()) * 1e-6, 1e-9),
@@ -417,7 +424,7 @@ def shim_extra_legs(w, b, kind, ids, act, o_inv, budget=480_000, seed=0x5EED):
                            O._ptr(rel[bb:]), O._ptr(aid), int(s.seq_base), O._ptr(o_r), O._ptr(fl_r), O._ptr(rf_r))
     b.restore()
     inv = np.full(len(act), -9, np.int32)
-    lat_a, n_pub, c0 = [], 0, 0
+    lat_a, lat_b, n_pub, c0 = [], [], 0, 0
     cut = int(first_job[b0])
     st_mid = None
     while c0 < n_jobs_r:
@@ -429,6 +436,8 @@ def shim_extra_legs(w, b, kind, ids, act, o_inv, budget=480_000, seed=0x5EED):
         if c0 >= cut:
             lat_a.append(ns * 1e-3)
             n_pub += npub
+        else:
+            lat_b.append(ns * 1e-3)
         c0 = c1
     rs2 = b.resident_stats()
     b.update_cluster(w.cluster_size)  # (the context is restored by the next leg / closed)
@@ -439,6 +448,7 @@ def shim_extra_legs(w, b, kind, ids, act, o_inv, budget=480_000, seed=0x5EED):
                 "calls_after": len(lat_a), "resident_served_after": int(served),
                 "resident_fraction_after": served / max(len(lat_a), 1),
                 "watch_calls": rs2["watch_calls"] - st_mid["watch_calls"],
+                "p50_us_before": float(np.percentile(lat_b, 50)), "p99_us_before": float(np.percentile(lat_b, 99)),
                 "p50_us_after": float(np.percentile(lat_a, 50)), "p99_us_after": float(np.percentile(lat_a, 99)),
                 "decisions_per_s_after": n_pub / max(float(lat_a.sum()) * 1e-6, 1e-9),
                 "bit_exact": bool(np.array_equal(inv[done], o_r[done])) and int(done.sum()) == int(s.acq_off[end_b])})
@@ -573,16 +583,39 @@ def main():
                     self.hev[k].record(self.hside)
 
             b.restore(self.sp)
-            gather(0)
-            for k in range(s.n_batches):
-                if k + 1 < s.n_batches:
-                    gather(k + 1)  # in flight while batch k's engine runs
-                main.wait_event(self.hev[k])
-                h = agreed[k]
-                b.update_health_device(len(self.w.inv_status), h.data_ptr(), self.sp)
-                b.replay_device_span(s.acq_off[k], s.acq_off[k + 1], s.rel_off[k], s.rel_off[k + 1],
-                                     self.d_act.data_ptr(), self.d_aid.data_ptr(), s.seq_base, self.d_out.data_ptr(),
-                                     self.d_fl.data_ptr(), self.d_rf.data_ptr(), self.sp)
+            G = max(1, args.health_group)
+            if G == 1:
+                gather(0)
+                for k in range(s.n_batches):
+                    if k + 1 < s.n_batches:
+                        gather(k + 1)  # in flight while batch k's engine runs
+                    main.wait_event(self.hev[k])
+                    h = agreed[k]
+                    b.update_health_device(len(self.w.inv_status), h.data_ptr(), self.sp)
+                    b.replay_device_span(s.acq_off[k], s.acq_off[k + 1], s.rel_off[k], s.rel_off[k + 1],
+                                         self.d_act.data_ptr(), self.d_aid.data_ptr(), s.seq_base, self.d_out.data_ptr(),
+                                         self.d_fl.data_ptr(), self.d_rf.data_ptr(), self.sp)
+                    if timing is not None:
+                        timing.append(b.engine_ms())
+                return
+            # G batches per engine launch (owgs_replay_device_group): the engine applies each batch's agreed health
+            # itself; the exchanges of group g + 1 run on the side stream while group g's engine runs
+            nid = len(self.w.inv_status)
+            stride = hx.world * nid  # row k of the per-batch buffers (rank 0's row first: the agreed vector)
+            if getattr(self, "hall", None) is None:
+                self.hall = torch.empty((s.n_batches, stride), dtype=torch.uint8, device=dev)
+                self.hflat = [self.hall[k] for k in range(s.n_batches)]
+            groups = [(g0, min(g0 + G, s.n_batches)) for g0 in range(0, s.n_batches, G)]
+            for k in range(groups[0][0], groups[0][1]):
+                gather(k)
+            for j, (g0, g1) in enumerate(groups):
+                if j + 1 < len(groups):
+                    for k in range(*groups[j + 1]):
+                        gather(k)  # in flight while this group's engine runs
+                main.wait_event(self.hev[g1 - 1])
+                b.replay_device_group(s.acq_off[g0:g1 + 1], s.rel_off[g0:g1 + 1], self.d_act.data_ptr(),
+                                      self.d_aid.data_ptr(), s.seq_base, self.d_out.data_ptr(), self.d_fl.data_ptr(),
+                                      self.d_rf.data_ptr(), self.hall[g0].data_ptr(), stride, nid, self.sp)
                 if timing is not None:
                     timing.append(b.engine_ms())
 
@@ -733,9 +766,14 @@ def main():
                        "cluster_size": n_ctl, "slots": args.slots, "shards": shard_ids if world == 1 else None,
                        "invoker_memory_mb": int(w.inv_mem[0] // (1 << 20)), "slot_mb": int(w.info["slot_mb"]),
                        "health_allgathers_per_step": gathers_per_step,
-                       "health": ("per batch: all-gathered, applied with owgs_update_health_device, "
-                                  f"{s.n_batches} engine launches per step (1 % of invokers unresponsive, changing "
-                                  "every batch)") if per_batch else "static, one exchange per step",
+                       "health": (("per batch: all-gathered one group ahead on a side stream, applied by the "
+                                   f"engine before each batch, {args.health_group} batches per engine launch "
+                                   f"(owgs_replay_device_group: {-(-s.n_batches // args.health_group)} launches per "
+                                   "step; 1 % of invokers unresponsive, changing every batch)")
+                                  if args.health_group > 1 else
+                                  ("per batch: all-gathered one batch ahead, applied with owgs_update_health_device, "
+                                   f"{s.n_batches} engine launches per step (1 % of invokers unresponsive, changing "
+                                   "every batch)")) if per_batch else "static, one exchange per step",
                        "health_disagreeing_ranks": int(disagree),
                        "parallelism": f"{n_ctl} controller shard(s), {K} per GPU, {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

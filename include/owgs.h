@@ -199,6 +199,19 @@ int owgs_replay_device(owgs_ctx* ctx, int32_t n_batches, const int64_t* acq_off,
 int owgs_replay_device_span(owgs_ctx* ctx, int64_t a_beg, int64_t a_end, int64_t r_beg, int64_t r_end,
                             const int32_t* act, const int64_t* rel_aid, uint64_t seq_base, int32_t* out_invoker,
                             uint8_t* out_flags, uint8_t* rel_flags, void* stream);
+/* Consecutive batches of a stream replayed batch by batch in ONE engine launch, with a health vector applied before
+ * each batch (configs[4]'s cadence: the health all-gathered between batches, applied as updateInvokers with a new
+ * status vector, SCPB:512-551, before the batch's releases).  acq_off / rel_off are HOST arrays [n_batches + 1] of
+ * indices into the whole stream's device arrays (as owgs_replay_device_span's a_beg..r_end, per batch); releases may
+ * name activations decided by earlier calls or by earlier batches of this group.  status_dev (device, nullable):
+ * row b = status_dev + b * status_stride holds n_status InvokerState codes (n_status = the context's invokers);
+ * after the call the context's health is the last row's.  Same results as owgs_update_health_device(row b) +
+ * owgs_replay_device_span(batch b) for every b.  Identity pools without watched pairs run one launch; otherwise the
+ * call takes exactly that batch-by-batch sequence.  Asynchronous on `stream` (same exception as owgs_replay_device). */
+int owgs_replay_device_group(owgs_ctx* ctx, int32_t n_batches, const int64_t* acq_off, const int64_t* rel_off,
+                             const int32_t* act, const int64_t* rel_aid, uint64_t seq_base, int32_t* out_invoker,
+                             uint8_t* out_flags, uint8_t* rel_flags, const uint8_t* status_dev, int64_t status_stride,
+                             int32_t n_status, void* stream);
 /* Several controller shards (clusterSize > 1, one context each, same device) replayed by ONE engine launch, one
  * workgroup per shard: the reference runs one ShardingContainerPoolBalancer per controller (SCPB:126-133,
  * 485-499); this hosts up to 64 of them on one GPU (up to 8 argument blocks travel in the kernarg segment, more

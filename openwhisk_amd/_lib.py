@@ -127,6 +127,7 @@ def lib() -> C.CDLL:
         "owgs_replay_device": (C.c_int, [P, i32, P, P, C.c_int64, P, P, C.c_int64, u64, P, P, P, P]),
         "owgs_replay_device_multi": (C.c_int, [P, i32, P, P]),
         "owgs_replay_device_span": (C.c_int, [P, C.c_int64, C.c_int64, C.c_int64, C.c_int64, P, P, u64, P, P, P, P]),
+        "owgs_replay_device_group": (C.c_int, [P, C.c_int32, P, P, P, P, u64, P, P, P, P, C.c_int64, C.c_int32, P]),
         "owgs_replay": (C.c_int, [P, i32, P, P, P, P, u64, P, P, P]),
         "owgs_snapshot": (C.c_int, [P]),
         "owgs_restore": (C.c_int, [P, P]),

@@ -471,6 +471,18 @@ class GpuShardingContainerPoolBalancer:
                                                   vp(rel_aid), int(seq_base), vp(out_inv), vp(out_flags),
                                                   vp(rel_flags), vp(stream)))
 
+    def replay_device_group(self, acq_off, rel_off, act, rel_aid, seq_base, out_inv, out_flags, rel_flags,
+                            status=None, status_stride=0, n_status=0, stream=None):
+        """Consecutive batches of a device-resident stream in one engine launch (owgs_replay_device_group):
+        acq_off / rel_off are the group's host offsets (n_batches + 1 each, whole-stream indices); status (device
+        address, optional): per batch a row of n_status InvokerState codes applied before the batch."""
+        vp = lambda x: C.c_void_p(int(x)) if x else None  # noqa: E731
+        ao = np.ascontiguousarray(acq_off, dtype=np.int64)
+        ro = np.ascontiguousarray(rel_off, dtype=np.int64)
+        self._chk(self._L.owgs_replay_device_group(self._h, len(ao) - 1, _p(ao), _p(ro), vp(act), vp(rel_aid),
+                                                   int(seq_base), vp(out_inv), vp(out_flags), vp(rel_flags),
+                                                   vp(status), int(status_stride), int(n_status), vp(stream)))
+
     @staticmethod
     def replay_device_multi(shards, stream=None):
         """Several controller shards in ONE engine launch (owgs_replay_device_multi, one workgroup per shard).

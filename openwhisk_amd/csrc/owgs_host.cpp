@@ -44,6 +44,8 @@ extern "C" hipError_t owgs_launch_coprime(const int32_t* xs, int32_t n_pools, in
                                           int32_t* counts, hipStream_t s);
 extern "C" hipError_t owgs_launch_slots(const int64_t* mem_bytes, int32_t from, int32_t n, int32_t cluster,
                                        int64_t min_bytes, int32_t* permits, hipStream_t s);
+extern "C" hipError_t owgs_launch_usable_rows(const uint8_t* status, int64_t stride, int32_t n, int32_t rows,
+                                              uint32_t* bits, int32_t n_words, hipStream_t s);
 extern "C" hipError_t owgs_launch_usable(const uint8_t* status, int32_t n, uint32_t* bits, int32_t n_words,
                                         hipStream_t s);
 extern "C" hipError_t owgs_launch_slot_scan(const uint32_t* ct_keys, const uint2* ovf, int32_t ovf_cap,
@@ -226,12 +228,17 @@ struct owgs_ctx {
     DevBuf<int32_t> d_ovf_touched, d_ovf_cnt;  // d_ovf_cnt = {entries (live + deleted), touched count}
     int32_t ovf_cap = 0;
     int64_t ovf_used_ub = 0;  // host upper bound of the overflow's entries (exact after a read-back)
-    // the overflow's entry count copied back after an engine launch without waiting (pinned word + event): read when
-    // the bound above runs out, it replaces a stream synchronisation; ovf_since = activations launched after the copy
-    int32_t* h_ovf_cnt = nullptr;
-    hipEvent_t ev_ovf = nullptr;
-    bool ovf_probe = false;
-    int64_t ovf_since = 0;
+    // the overflow's entry count copied back after engine launches without waiting (a ring of pinned words +
+    // events): read when the bound above runs out.  A probe that has arrived replaces the bound; otherwise the host
+    // waits for an OLDER probe than the newest -- the launches after it keep the GPU busy meanwhile -- instead of
+    // draining the stream (a batch-by-batch replay then never idles the engine stream on this bound)
+    static constexpr int OVF_PROBES = 4;
+    int32_t* h_ovf_cnt = nullptr;                   // [OVF_PROBES]
+    hipEvent_t ev_ovf[OVF_PROBES] = {};
+    bool ovf_probe[OVF_PROBES] = {};                // slot recorded and not yet consumed
+    int64_t ovf_probe_added[OVF_PROBES] = {};       // ovf_added at the slot's recording (its launch included)
+    int64_t ovf_added = 0;                          // activations ever added to the bound
+    int ovf_probe_next = 0;
     // owgs_update_health_device on identity pools: the status bytes and usable bitmap are updated on the device only;
     // the host mirror (status, healthy counts) is downloaded when a host path needs it (ev_status: the copy)
     bool status_stale = false;
@@ -303,6 +310,13 @@ struct owgs_ctx {
     DevBuf<int32_t> w_cnt, w_wkey, w_D, w_L, w_Lcnt, w_rel;
     DevBuf<uint4> w_L2;
     DevBuf<int64_t> w_off;
+    // owgs_replay_device_group: its batch offsets, the usable bitmap of each batch's health, and (during the call) the
+    // first activation of the group (releases of earlier ones get their records from those decisions)
+    DevBuf<int64_t> g_off;
+    DevBuf<uint32_t> d_hwords;
+    const uint32_t* grp_hwords = nullptr;
+    int32_t grp_hstride = 0;
+    int64_t grp_a0 = 0;
     DevBuf<uint8_t> w_rfl;
     int32_t w_cap = 0, w_live = 0;
     int32_t stats_par = 0, stats_last = 0;  // d_stats holds two counter blocks: the next launch's, the last one's
@@ -336,6 +350,7 @@ struct owgs_ctx {
     DevBuf<uint4> d_w_sidx;         // resident engine: watched pairs by fqn@version key (built at its launch)
     DevBuf<uint2> d_w_list;
     int32_t w_scap = 0;
+    uint64_t res_cache_epoch = 1, res_cache_seen = 0;  // res_meta / the watched-pair index are current when equal
     DevBuf<uint2> d_res_cur;        // per action: {cursor generation, first walk step that may fit}
     std::vector<uint2> res_meta;    // act_meta as of the live launch (every change of it stops the engine first)
     uint32_t res_gen_seen = 0;      // the last cursor generation the engine reported
@@ -461,6 +476,7 @@ static int rebuild_pools(owgs_ctx* c) {
 }
 
 static int prepare_actions(owgs_ctx* c) {
+    ++c->res_cache_epoch;  // (the resident engine's host copies of the action meta / watched-pair index)
     const int32_t n = (int32_t)c->a_mem.size();
     if (n == 0) return OWGS_OK;
     if (!c->d_steps.p) HIPCHK(c, c->d_steps.reserve(2));
@@ -525,7 +541,54 @@ static OwgsOvf ovf_args(const owgs_ctx* c) {
 // n more activations may add overflow entries: the bound grows, and so does what an outstanding count probe misses
 static void ovf_add(owgs_ctx* c, int64_t n) {
     c->ovf_used_ub += n;
-    if (c->ovf_probe) c->ovf_since += n;
+    c->ovf_added += n;
+}
+static void ovf_probes_clear(owgs_ctx* c) {
+    for (int k = 0; k < owgs_ctx::OVF_PROBES; ++k) c->ovf_probe[k] = false;
+}
+// after an engine launch on s: copy the entry count back into the next free probe slot (no wait)
+static int ovf_probe_record(owgs_ctx* c, hipStream_t s) {
+    if (!c->h_ovf_cnt) {
+        HIPCHK(c, hipHostMalloc((void**)&c->h_ovf_cnt, owgs_ctx::OVF_PROBES * sizeof(int32_t), hipHostMallocDefault));
+        for (int k = 0; k < owgs_ctx::OVF_PROBES; ++k)
+            HIPCHK(c, hipEventCreateWithFlags(&c->ev_ovf[k], hipEventDisableTiming));
+    }
+    const int k = c->ovf_probe_next;
+    if (c->ovf_probe[k] && hipEventQuery(c->ev_ovf[k]) != hipSuccess) return OWGS_OK;  // (still in flight: skip)
+    HIPCHK(c, hipMemcpyAsync(&c->h_ovf_cnt[k], c->d_ovf_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipEventRecord(c->ev_ovf[k], s));
+    c->ovf_probe[k] = true;
+    c->ovf_probe_added[k] = c->ovf_added;
+    c->ovf_probe_next = (k + 1) % owgs_ctx::OVF_PROBES;
+    return OWGS_OK;
+}
+// the bound from the newest probe that has arrived (wait_older: first wait for the second-newest outstanding one)
+static int ovf_probe_refresh(owgs_ctx* c, bool wait_older) {
+    int newest = -1, second = -1;
+    for (int k = 0; k < owgs_ctx::OVF_PROBES; ++k) {
+        if (!c->ovf_probe[k]) continue;
+        if (newest < 0 || c->ovf_probe_added[k] > c->ovf_probe_added[newest]) {
+            second = newest;
+            newest = k;
+        } else if (second < 0 || c->ovf_probe_added[k] > c->ovf_probe_added[second]) {
+            second = k;
+        }
+    }
+    if (wait_older) {
+        const int w = second >= 0 ? second : newest;
+        if (w < 0) return OWGS_OK;
+        HIPCHK(c, hipEventSynchronize(c->ev_ovf[w]));
+    }
+    int best = -1;
+    for (int k = 0; k < owgs_ctx::OVF_PROBES; ++k)
+        if (c->ovf_probe[k] && hipEventQuery(c->ev_ovf[k]) == hipSuccess &&
+            (best < 0 || c->ovf_probe_added[k] > c->ovf_probe_added[best]))
+            best = k;
+    if (best < 0) return OWGS_OK;
+    c->ovf_used_ub = std::min(c->ovf_used_ub, (int64_t)c->h_ovf_cnt[best] + (c->ovf_added - c->ovf_probe_added[best]));
+    for (int k = 0; k < owgs_ctx::OVF_PROBES; ++k)  // this probe and older ones are consumed
+        if (c->ovf_probe[k] && c->ovf_probe_added[k] <= c->ovf_probe_added[best]) c->ovf_probe[k] = false;
+    return OWGS_OK;
 }
 
 // overflow capacity for `used` entries plus n_new activations
@@ -540,12 +603,13 @@ static int64_t ovf_need(int64_t used, int64_t n_new) {
 static int ensure_ovf(owgs_ctx* c, int64_t n_new, hipStream_t s) {
     auto need = [&](int64_t used) { return ovf_need(used, n_new); };
     if (c->ovf_cap >= need(c->ovf_used_ub)) return OWGS_OK;
-    if (c->ovf_probe && hipEventQuery(c->ev_ovf) == hipSuccess) {  // a count that arrived meanwhile: no wait
-        c->ovf_probe = false;
-        c->ovf_used_ub = (int64_t)*c->h_ovf_cnt + c->ovf_since;
+    {  // a count that arrived meanwhile, else one of an older launch (the GPU keeps the later ones)
+        int rc = ovf_probe_refresh(c, false);
+        if (!rc && c->ovf_cap < need(c->ovf_used_ub)) rc = ovf_probe_refresh(c, true);
+        if (rc) return rc;
         if (c->ovf_cap >= need(c->ovf_used_ub)) return OWGS_OK;
     }
-    c->ovf_probe = false;
+    ovf_probes_clear(c);
     if (c->ovf_cap > 0) {  // exact entry count
         int32_t cnt = 0;
         HIPCHK(c, hipStreamSynchronize(s));
@@ -587,7 +651,7 @@ static int reset_ctab(owgs_ctx* c) {
         HIPCHK(c, owgs_launch_ovf_clear(&O, c->stream));
     }
     c->ovf_used_ub = 0;
-    c->ovf_probe = false;
+    ovf_probes_clear(c);
     return OWGS_OK;
 }
 
@@ -605,6 +669,7 @@ static OwgsWatch watch_args(const owgs_ctx* c) {
 }
 
 static void w_drop(owgs_ctx* c) {
+    ++c->res_cache_epoch;  // (the resident engine's host copies of the action meta / watched-pair index)
     c->w_keys.release();
     c->w_vals.release();
     c->w_wkey.release();
@@ -626,6 +691,7 @@ static int w_refresh(owgs_ctx* c, hipStream_t s) {
 // A reset (updateCluster SCPB:561-584, the _invokerSlots test seam) is about to discard the concurrency map: every
 // pair with activations in flight (operationCount of its entry + d of the pair) becomes watched (owgs_watch.hip).
 static int w_rebuild(owgs_ctx* c) {
+    ++c->res_cache_epoch;  // (the resident engine's host copies of the action meta / watched-pair index)
     hipStream_t s = c->stream;
     int32_t ovf_n = 0;
     HIPCHK(c, hipStreamSynchronize(s));
@@ -698,6 +764,8 @@ static void base_args(owgs_ctx* c, OwgsEngineArgs& A) {
     A.stats = c->d_stats.p;
     A.err = c->d_err.p;
     A.opts = env_opts().opts;
+    A.hwords = c->grp_hwords;
+    A.hstride = c->grp_hstride;
     A.trace = nullptr;
     if (env_opts().trace) {  // diagnostic: a -DOWGS_TRACE engine logs its barrier timeline here
         const size_t n = (size_t)(OWGS_EW + 1) * 16384 * 2;
@@ -780,9 +848,10 @@ static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s, bool launch
     if (rc) return rc;
     // the map's overflow exists only for concurrent actions: a context without any never allocates it
     if (c->any_conc || (A.feat & OWGS_F_CONC)) {
-        rc = ensure_ovf(c, A.n_act, s);
+        const int64_t n_new = A.n_act - c->grp_a0;  // (a group launch indexes the whole stream from its first batch)
+        rc = ensure_ovf(c, n_new, s);
         if (rc) return rc;
-        ovf_add(c, A.n_act);
+        ovf_add(c, n_new);
     }
     A.ovf = ovf_args(c);
     A.ct_tmp = c->d_ct_tmp.p;
@@ -817,14 +886,8 @@ static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s, bool launch
     HIPCHK(c, hipEventRecord(c->ev_engine[1], s));
     c->ev_engine_valid = true;
     if (c->ovf_cap > 0) {  // the overflow's entry count for a later ensure_ovf, copied back without a wait
-        if (!c->ovf_probe) {
-            if (!c->h_ovf_cnt) HIPCHK(c, hipHostMalloc((void**)&c->h_ovf_cnt, sizeof(int32_t), hipHostMallocDefault));
-            if (!c->ev_ovf) HIPCHK(c, hipEventCreateWithFlags(&c->ev_ovf, hipEventDisableTiming));
-            HIPCHK(c, hipMemcpyAsync(c->h_ovf_cnt, c->d_ovf_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-            HIPCHK(c, hipEventRecord(c->ev_ovf, s));
-            c->ovf_probe = true;
-            c->ovf_since = 0;  // (the copy follows this launch: its count includes it)
-        }
+        const int rc = ovf_probe_record(c, s);
+        if (rc) return rc;
     }
     if (A.trace) {  // diagnostic timeline: raw u64 pairs, [waves][16384][2]
         HIPCHK(c, hipStreamSynchronize(s));
@@ -1102,16 +1165,22 @@ static int res_launch(owgs_ctx* c) {
             if (wrap) c->res_gen_seen = 0;
         }
     }
-    // the action meta the host writes into each call's records (as the device computed it)
-    c->res_meta.resize(c->a_mem.size());
-    if (!c->res_meta.empty()) {
-        HIPCHK(c, hipMemcpyAsync(c->res_meta.data(), c->d_act_meta.p, c->res_meta.size() * sizeof(uint2),
-                                 hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+    // the action meta the host writes into each call's records (as the device computed it) and the watched-pair
+    // index: downloaded / rebuilt only when actions, pools or W changed since the last launch (a relaunch after a
+    // chained call would otherwise pay a synchronised copy of every action's meta)
+    const bool fresh = c->res_cache_seen == c->res_cache_epoch && c->res_meta.size() == c->a_mem.size();
+    if (!fresh) {
+        c->res_meta.resize(c->a_mem.size());
+        if (!c->res_meta.empty()) {
+            HIPCHK(c, hipMemcpyAsync(c->res_meta.data(), c->d_act_meta.p, c->res_meta.size() * sizeof(uint2),
+                                     hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+        }
     }
-    {
+    if (!fresh || (c->w_cap > 0) != (c->w_scap > 0)) {
         const int rc = res_w_index(c);
         if (rc) return rc;
+        c->res_cache_seen = c->res_cache_epoch;
     }
     // the state in HBM must be current: the resident stream waits for the context's stream and its last async call
     HIPCHK(c, hipEventRecord(c->ev_res, c->stream));
@@ -1465,8 +1534,10 @@ void owgs_destroy(owgs_ctx* c) {
     c->h_margs = nullptr;
     if (c->h_ovf_cnt) (void)hipHostFree(c->h_ovf_cnt);
     c->h_ovf_cnt = nullptr;
-    if (c->ev_ovf) (void)hipEventDestroy(c->ev_ovf);
-    c->ev_ovf = nullptr;
+    for (int k = 0; k < owgs_ctx::OVF_PROBES; ++k) {
+        if (c->ev_ovf[k]) (void)hipEventDestroy(c->ev_ovf[k]);
+        c->ev_ovf[k] = nullptr;
+    }
     if (c->ev_status) (void)hipEventDestroy(c->ev_status);
     c->ev_status = nullptr;
     if (c->ev_tail) (void)hipEventDestroy(c->ev_tail);
@@ -1663,6 +1734,7 @@ int owgs_register_actions(owgs_ctx* c, int32_t n, const char* ns_bytes, const in
                           const char* path_bytes, const int32_t* path_off, const char* key_bytes,
                           const int32_t* key_off, const int32_t* mem_mb, const int32_t* max_conc,
                           const uint8_t* blackbox, int32_t* out_action, int32_t* out_hash) {
+    if (c) ++c->res_cache_epoch;
     if (!c || n < 0) return OWGS_EINVAL;
     if (n == 0) return OWGS_OK;
     if (!ns_off || !path_off || !key_off || !mem_mb || !max_conc || !blackbox || !key_bytes || !out_action)
@@ -1805,6 +1877,7 @@ int owgs_register_actions(owgs_ctx* c, int32_t n, const char* ns_bytes, const in
 // their activations is still in flight.  Their ids, and the fqn@version keys no live handle names any more, are reused
 // by later registrations -- the keys once nothing on the device holds them (reclaim_slots).
 int owgs_release_actions(owgs_ctx* c, int32_t n, const int32_t* actions) {
+    if (c) ++c->res_cache_epoch;
     if (!c || n < 0 || (n > 0 && !actions)) return OWGS_EINVAL;
     const int32_t na = (int32_t)c->a_mem.size();
     std::vector<uint8_t> seen;
@@ -2423,6 +2496,77 @@ int owgs_replay_device(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, c
     return rc ? rc : rt;
 }
 
+static int update_health_device_impl(owgs_ctx* c, int32_t n, const uint8_t* status_dev, void* stream);
+
+// owgs_replay_device_group: batches [0, n) of the caller's host offsets in one engine launch, health row b applied by
+// the engine before batch b (identity pools, no watched pairs); otherwise health + span per batch
+static int replay_device_group_impl(owgs_ctx* c, int32_t nb, const int64_t* acq_off, const int64_t* rel_off,
+                                    const int32_t* act, const int64_t* rel_aid, uint64_t seq_base, int32_t* out_invoker,
+                                    uint8_t* out_flags, uint8_t* rel_flags, const uint8_t* status_dev,
+                                    int64_t status_stride, int32_t n_status, void* stream) {
+    if (nb <= 0 || !acq_off || !rel_off || !act || !out_invoker || !out_flags) return OWGS_EINVAL;
+    for (int32_t b = 0; b < nb; ++b)
+        if (acq_off[b + 1] < acq_off[b] || rel_off[b + 1] < rel_off[b]) return c->fail(OWGS_EINVAL, "offsets");
+    if (acq_off[0] < 0 || rel_off[0] < 0 || acq_off[nb] >= ((int64_t)1 << 31)) return c->fail(OWGS_EINVAL, "offsets");
+    if (rel_off[nb] > rel_off[0] && !rel_aid) return OWGS_EINVAL;
+    if (status_dev && (n_status <= 0 || status_stride < n_status)) return c->fail(OWGS_EINVAL, "health rows");
+    if (c->a_mem.empty()) return c->fail(OWGS_ENOENT, "no actions registered");
+    if (c->w_cap > 0 || c->pool_mode != 0 || spec_replay_eligible(c) || (status_dev && n_status != c->n_ids)) {
+        for (int32_t b = 0; b < nb; ++b) {  // the batch-by-batch sequence the call stands for
+            int rc = status_dev ? update_health_device_impl(c, n_status, status_dev + (int64_t)b * status_stride, stream)
+                                : OWGS_OK;
+            if (!rc)
+                rc = replay_device_span_impl(c, acq_off[b], acq_off[b + 1], rel_off[b], rel_off[b + 1], act, rel_aid,
+                                             seq_base, out_invoker, out_flags, rel_flags, stream);
+            if (rc) return rc;
+        }
+        return OWGS_OK;
+    }
+    hipStream_t hs = stream ? (hipStream_t)stream : c->stream;
+    const int64_t a0 = acq_off[0], r0 = rel_off[0], n_rel = rel_off[nb] - r0;
+    std::vector<int64_t> offs((size_t)2 * (nb + 1));
+    for (int32_t b = 0; b <= nb; ++b) {
+        offs[b] = acq_off[b];                      // absolute: the engine indexes the stream's arrays
+        offs[nb + 1 + b] = rel_off[b] - r0;        // relative to the group's first release
+    }
+    HIPCHK(c, upload(c->g_off, offs.data(), offs.size(), hs));
+    if (status_dev) {
+        const int32_t words = (c->n_ids + 31) / 32;
+        HIPCHK(c, c->d_hwords.reserve((size_t)nb * std::max(words, 1)));
+        HIPCHK(c, owgs_launch_usable_rows(status_dev, status_stride, n_status, nb, c->d_hwords.p, words, hs));
+        c->grp_hwords = c->d_hwords.p;
+        c->grp_hstride = words;
+    }
+    c->grp_a0 = a0;
+    OwgsEngineArgs A;
+    int rc = replay_begin(c, nb, c->g_off.p, act, acq_off[nb], n_rel > 0 ? c->g_off.p + nb + 1 : nullptr,
+                          n_rel > 0 ? rel_aid + r0 : nullptr, n_rel, seq_base, out_invoker, out_flags,
+                          rel_flags ? rel_flags + r0 : nullptr, hs, A, true);
+    c->grp_hwords = nullptr;
+    c->grp_hstride = 0;
+    c->grp_a0 = 0;
+    if (rc) return rc;
+    if (n_rel > 0 && rel_flags) HIPCHK(c, owgs_launch_relflags(rel_aid + r0, n_rel, out_invoker, rel_flags + r0, hs));
+    // the context's health after the group: the last batch's (status bytes + bitmap, as owgs_update_health_device)
+    if (status_dev) return update_health_device_impl(c, n_status, status_dev + (int64_t)(nb - 1) * status_stride, stream);
+    return OWGS_OK;
+}
+
+int owgs_replay_device_group(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, const int64_t* rel_off,
+                             const int32_t* act, const int64_t* rel_aid, uint64_t seq_base, int32_t* out_invoker,
+                             uint8_t* out_flags, uint8_t* rel_flags, const uint8_t* status_dev, int64_t status_stride,
+                             int32_t n_status, void* stream) {
+    if (!c) return OWGS_EINVAL;
+    OWGS_ENTER(c);
+    hipStream_t hs_ = stream ? (hipStream_t)stream : c->stream;
+    int rc = order_on(c, hs_);
+    if (!rc)
+        rc = replay_device_group_impl(c, n_batches, acq_off, rel_off, act, rel_aid, seq_base, out_invoker, out_flags,
+                                      rel_flags, status_dev, status_stride, n_status, stream);
+    const int rt = tail_mark(c, hs_);
+    return rc ? rc : rt;
+}
+
 static int replay_device_multi_impl(owgs_ctx** cs, int32_t k, const owgs_replay_io* io, void* stream) {
     if (!cs || !io || k < 1 || k > OWGS_MULTI_DEV_MAX) return OWGS_EINVAL;
     for (int32_t i = 0; i < k; ++i) {
@@ -2552,6 +2696,10 @@ static int replay_begin(owgs_ctx* c, int32_t n_batches, const int64_t* acq_off, 
         ra.relx = c->d_relx.p;
         ra.relcnt = c->d_relcnt.p;
         ra.err = c->d_err.p;
+        ra.decided_below = c->grp_a0;  // (group launches: earlier activations' records come from their decisions)
+        ra.out_inv = out_invoker;
+        ra.act_slot = c->d_act_slot.p;
+        ra.rel_rec = c->d_rel_rec.p;
         HIPCHK(c, owgs_launch_relpos(&ra, hs));
         A.rel_off = rel_off;
         A.relpos = c->d_relx.p;
@@ -2883,7 +3031,7 @@ static int restore_impl(owgs_ctx* c, void* stream) {
         }
     }
     c->ovf_used_ub = c->s_ovf_cnt;
-    c->ovf_probe = false;
+    ovf_probes_clear(c);
     if (c->w_cap != c->s_w_cap) {  // watched pairs as captured
         w_drop(c);
         if (c->s_w_cap > 0) {
@@ -2906,6 +3054,7 @@ static int restore_impl(owgs_ctx* c, void* stream) {
 }
 
 int owgs_restore(owgs_ctx* c, void* stream) {
+    if (c) ++c->res_cache_epoch;
     if (!c) return OWGS_EINVAL;
     OWGS_ENTER(c);
     hipStream_t hs_ = stream ? (hipStream_t)stream : c->stream;

@@ -196,6 +196,10 @@ struct OwgsEngineArgs {
     uint32_t geom;               // OWGS_GEOM_TAG of the geometry the host sized this launch's buffers for
     unsigned long long* rel_bound;  // owgs_process_batch: per slot, the memory the call's releases can return at most
                                     // (staged by owgs_stage_releases_kernel; the engine checks and zeroes it), or null
+    // identity pools, owgs_replay_device_group: the usable bitmap batch b applies before its releases (updateInvokers
+    // with a new health vector, SCPB:512-551) at hwords + b * hstride, or null
+    const uint32_t* hwords;
+    int32_t hstride;
 };
 // Geometry/ABI tag.  The host and an engine object must agree on the chunk width (the stride of lix, the 10-bit lane
 // fields of the records), the primary table's capacity and the argument block's layout; the host builds the tag of the
@@ -251,6 +255,12 @@ struct OwgsRelposArgs {
     int32_t* relx;               // out [n_act] (memset -1)
     int32_t* relcnt;             // out [2 * n_batches] (memset 0)
     int32_t* err;
+    // a group of batches replayed in its own launch (owgs_replay_device_group): a release of an activation decided by
+    // an EARLIER launch (aid < decided_below) gets its record written here from that decision, not by the engine
+    int64_t decided_below;
+    const int32_t* out_inv;
+    const int32_t* act_slot;
+    uint2* rel_rec;
 };
 
 struct OwgsPrepassArgs {

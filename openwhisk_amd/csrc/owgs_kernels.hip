@@ -972,6 +972,16 @@ __global__ __launch_bounds__(RP_T) void owgs_relpos_kernel(OwgsRelposArgs R) {
         const int base = s_base[b - bw][cls] + off;
         pos = cls ? R.rel_off[b + 1] - 1 - base : R.rel_off[b] + base;
     }
+    if (live && aid < R.decided_below) {
+        // decided by an earlier launch: the record from that decision (the engine writes the others when it decides)
+        const int a = R.act[aid];
+        const uint2 m = R.act_meta[a];
+        const int x = R.out_inv[aid];
+        const uint32_t inv15 = x >= 0 ? (uint32_t)x : OWGS_RR_NOINV;
+        R.rel_rec[pos] = make_uint2(inv15 | ((m.y & OWGS_AM_MEM_MASK) << 15),
+                                    (uint32_t)R.act_slot[a] | (((m.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK) << 17));
+        return;
+    }
     if (live && atomicCAS(&R.relx[aid], -1, (int32_t)pos) != -1) atomicOr(R.err, OWGS_ERR_BAD_STREAM);
 }
 
@@ -1316,20 +1326,52 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     // healthy invokers per pool (|H| of the overload fallback, SCPB:417-424): identity pools count them from the
     // usable bitmap (owgs_update_health_device updates only the bitmap there); other pools take the host's counts
     int hm_e = A.hm, hb_e = A.hb;
+    auto rank = [&](int x) {  // usable ids below x (identity pools)
+        return x <= 0 ? 0 : (int)pc[x >> 5] + ((x & 31) ? __popc(ub[x >> 5] & ((1u << (x & 31)) - 1u)) : 0);
+    };
     if (pool_mode == 0) {
-        auto rank = [&](int x) {  // usable ids below x
-            return x <= 0 ? 0 : (int)pc[x >> 5] + ((x & 31) ? __popc(ub[x >> 5] & ((1u << (x & 31)) - 1u)) : 0);
-        };
         hm_e = rank(nm);
         hb_e = rank(A.n_ids) - rank(A.n_ids - nb);
     }
     // pools whose ids are all usable: the fallback's k-th healthy invoker is arithmetic (no rank/select reads)
-    const bool full_m = pool_mode == 0 && hm_e == nm, full_b = pool_mode == 0 && hb_e == nb;
+    bool full_m = pool_mode == 0 && hm_e == nm, full_b = pool_mode == 0 && hb_e == nb;
 
     int g = 0;    // global chunk index
     int par = 0;  // pass parity (double-buffered LDS scalars)
     for (int b = 0; b < A.n_batches; ++b) {
         const int64_t a_beg = A.acq_off[b], a_end = A.acq_off[b + 1];
+        if (A.hwords && pool_mode == 0) {
+            // ============================================================ health of batch b (updateInvokers,
+            // SCPB:512-551: the status vector only; slots and pools unchanged): the usable bitmap, the usable flag folded
+            // into each changed invoker's permits, the bitmap's prefix counts and each pool's healthy count.  (The walk
+            // cursors are per batch, the bound U is recomputed below from the new bitmap.)
+            const uint32_t* hw = A.hwords + (int64_t)b * A.hstride;
+            lds_sync();  // (the previous batch's readers of the bitmap are done)
+            for (int w = tid; w < words; w += OWGS_NT) {
+                const uint32_t nw = hw[w], ow = ub[w];
+                for (uint32_t ch = nw ^ ow; ch; ch &= ch - 1u) {
+                    const int bit = __builtin_ctz(ch), i = (w << 5) + bit;
+                    if (i < A.n_ids && i < n_slots) P[i] += ((nw >> bit) & 1u) ? -OWGS_PENC : OWGS_PENC;
+                }
+                ub[w] = nw;
+            }
+            lds_sync();
+            if (wave == 0) {  // prefix counts of the usable bitmap
+                int carry = 0;
+                for (int w0 = 0; w0 <= words; w0 += 64) {
+                    const int w = w0 + lane;
+                    const int c = w < words ? __popc(ub[w]) : 0;
+                    const int inc = wave_incl_scan(c);
+                    if (w <= words) pc[w] = (uint32_t)(carry + inc - c);
+                    carry += __builtin_amdgcn_readlane(inc, 63);
+                }
+            }
+            lds_sync();
+            hm_e = rank(nm);
+            hb_e = rank(A.n_ids) - rank(A.n_ids - nb);
+            full_m = hm_e == nm;
+            full_b = hb_e == nb;
+        }
 
         // ============================================================ releases of batch b (SCPB:327-331)
 #ifdef OWGS_PROFILE

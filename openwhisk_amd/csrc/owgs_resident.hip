@@ -109,6 +109,7 @@ __device__ __forceinline__ int select_in_word(uint32_t m, int need) {
 #define RES_CC 2048  // walk-cursor cache entries (LDS, 16 KB)
 #define RES_BF 2048  // Bloom filter words over the primary table's keys (LDS, 8 KB)
 #define RES_WF 256   // watched-key filter words (LDS, 1 KB): one bit per hashed fqn@version key with watched pairs
+#define RES_WL 128   // watched-walk list (LDS, 1 KB): {action, deepest walk} of a run's decisions with watched keys
 #ifndef RES_FIRST_READ_KB
 #define RES_FIRST_READ_KB 4  // a call's input block: KB read together with the header (the rest in a second round)
 #endif
@@ -121,7 +122,7 @@ __device__ __forceinline__ int select_in_word(uint32_t m, int need) {
 #define RES_CLEAN_TOMBS (OWGS_CTC / 8)
 #endif
 struct ResLayout {
-    uint32_t P, ub, pc, ct, sc, cc, mv, bf, wf, stage, end;
+    uint32_t P, ub, pc, ct, sc, cc, mv, bf, wf, wl, stage, end;
 };
 __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
     const uint32_t words = (uint32_t)(n_ids + 31) / 32;
@@ -135,7 +136,8 @@ __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
     y.mv = y.cc + RES_CC * 8u;
     y.bf = y.mv + 64u * 4u;
     y.wf = y.bf + RES_BF * 4u;
-    y.stage = y.wf + RES_WF * 4u;
+    y.wl = y.wf + RES_WF * 4u;
+    y.stage = y.wl + RES_WL * 8u;
     y.end = y.stage;
     return y;
 }
@@ -153,6 +155,7 @@ __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
 #define RS_U0 10     // upper bound of every usable permit count of the managed / blackbox pool
 #define RS_U1 11
 #define RS_TOMB 12   // deleted primary entries (the cleanup between calls runs when they pile up)
+#define RS_WLN 13    // entries of the watched-walk list (wl)
 
 // blocked Bloom filter over the primary table's keys (LDS, RES_BF words): one word and three bits per key, set on
 // every insert into the primary and rebuilt with it; a key whose bits are not all set is not in the primary, so a
@@ -266,6 +269,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
     int32_t* mv = (int32_t*)(Lb + Y.mv);
     uint32_t* bf = (uint32_t*)(Lb + Y.bf);
     uint32_t* wf = (uint32_t*)(Lb + Y.wf);
+    uint2* wl = (uint2*)(Lb + Y.wl);
     char* stg = Lb + Y.stage;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int n_slots = A.n_slots, nm = A.nm, nb = A.nb;
@@ -714,6 +718,68 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 if (ix < 0) err |= OWGS_ERR_CTAB_FULL;
                 return ix;
             };
+            // watched-walk list -> Z marks: every entry (one lane each) marks the watched pairs of its action's key
+            // at the walk steps before its deepest walk (the host's index lists a key's pairs by step in the key's
+            // primary action's walk; another action of the key computes each pair's step); a mark on a pair whose
+            // entry is present is never read (the entry's removal clears it)
+            auto w_flush = [&]() {
+                const int nl = sc[RS_WLN];
+                for (int j0 = 0; j0 < nl; j0 += 64) {
+                    const int j = j0 + lane;
+                    uint4 e;
+                    const uint2 we = j < nl ? wl[j] : make_uint2(0u, 0u);
+                    const uint32_t a = we.x;
+                    const int depth = (int)we.y;
+                    uint2 am = make_uint2(0u, 0u);
+                    uint32_t aslot = 0u;
+                    if (j < nl) {
+                        am = A.act_meta[a];
+                        aslot = (uint32_t)A.act_slot[a];
+                    }
+                    if (j < nl && res_w_sfind(A, aslot, &e)) {
+                        const int wpool = (am.x & OWGS_AM_POOL) ? 1 : 0;
+                        const int wn = wpool ? nb : nm, wbase = wpool ? A.n_ids - nb : 0;
+                        const int whome = (int)(am.x & OWGS_AM_POS_MASK), wstep = (int)((am.x >> 15) & OWGS_AM_POS_MASK);
+                        const bool primary = e.w == a;
+                        const int winv = (!primary && wn > 1) ? res_inv_mod(wstep % wn, wn) : 0;
+                        const uint32_t kend = e.y + e.z;
+                        // four pairs per round: their list entries, then their W keys, read together
+                        for (uint32_t k0 = e.y; k0 < kend; k0 += 4) {
+                            uint2 pe[4];
+                            uint32_t key[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u)
+                                pe[u] = k0 + u < kend ? A.w_list[k0 + u] : make_uint2(0u, 0x7FFFFFFFu);
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const bool go = k0 + u < kend && (!primary || (int)pe[u].y < depth);
+                                key[u] = go ? __hip_atomic_load(&A.w.keys[pe[u].x], __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT)
+                                            : 0u;
+                            }
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                if (key[u] == 0u || key[u] == OWGS_CT_TOMB) continue;
+                                const int x = (int)(key[u] & 0x7FFFu) - 1;
+                                if (x < 0 || x >= A.n_ids || !((ub[x >> 5] >> (x & 31)) & 1u)) continue;  // not tried
+                                if (!primary) {
+                                    const int pos = x - wbase;
+                                    if (pos < 0 || pos >= wn) continue;
+                                    const int st = wn > 1 ? (int)(((long long)((pos - whome + wn) % wn) * winv) % wn) : 0;
+                                    if (st >= depth) continue;
+                                }
+                                atomicOr(&A.w.vals[pe[u].x], OWGS_W_Z);
+                            }
+                            if (primary && (int)pe[3].y >= depth) break;  // (the list is by step)
+                        }
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                if (lane == 0) sc[RS_WLN] = 0;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            };
+            if (lane == 0) sc[RS_WLN] = 0;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             for (int r = 0; r < n_runs; ++r) {
                 // ---- completions of run r (releaseInvoker SCPB:327-331 via processCompletion CLB:260-346)
                 const int rb = roff[r], re = roff[r + 1];
@@ -746,9 +812,9 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                     int rix = -1;
                     if (cr) rix = ct_lookup2(ct, bf, A.ovf, ovf_on, rkey, &rv);
                     // a release of an fqn@version key with watched pairs: below, with the empty-entry rule
-                    const bool wat = cr && A.w.cap > 0 && wf_test(wf, rr.z & 0x1FFFFu) &&
-                                     __hip_atomic_load(&A.w.wkey[rr.z & 0x1FFFFu], __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT) > 0;
+                    // (the filter may pass a key without watched pairs: the path below is releaseConcurrent's
+                    // general rule, equal to the closed form for such keys)
+                    const bool wat = cr && A.w.cap > 0 && wf_test(wf, rr.z & 0x1FFFFu);
                     const bool prim = cr && !wat && rix >= 0 && rix < OWGS_CTC;
                     // releases of one primary entry in this group: the j-th of them (queue order) finds the entry as
                     // the j before it leave it -- RS.release(1, true) j times from (c0, o0): c0 + j free slots, a
@@ -1589,63 +1655,55 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                     }
                     // Z marks (watched pairs): a concurrent decision's walk tried every usable invoker before the step
                     // it took -- all of them before an overload fallback -- and a failed try leaves the reference an
-                    // empty entry (getOrElseUpdate, NS:61-62).  Per action of the chunk its deepest walk marks the
-                    // watched pairs of its key at the steps before (the host's index lists them by step in the
-                    // key's primary action's walk; another action of the key computes each pair's step).  A mark on a
-                    // pair whose entry is present is never read: the entry's removal clears it
+                    // empty entry (getOrElseUpdate, NS:61-62).  Per action its deepest walk of the run goes into the
+                    // watched-walk list (wl); at the run's end (w_flush, before the next run's releases) every entry
+                    // marks the watched pairs of its key at the steps before
                     if (A.w.cap > 0) {
                         const int wmx = (int)((me.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
                         const bool wd = lane < nq && !(me.y & (OWGS_AM_EMPTY | OWGS_AM_THROW)) && wmx > 1 && o_v >= 0 &&
                                         wf_test(wf, me.z & 0x1FFFFu);
                         if (__ballot(wd)) {
-                            const int wpool = (me.x & OWGS_AM_POOL) ? 1 : 0;
-                            const int wn = wpool ? nb : nm, wbase = wpool ? A.n_ids - nb : 0;
-                            const int whome = (int)(me.x & OWGS_AM_POS_MASK), wstep = (int)((me.x >> 15) & OWGS_AM_POS_MASK);
-                            int winv = 0, depth = 0;
+                            int depth = 0;
                             if (wd) {
-                                winv = wn > 1 ? res_inv_mod(wstep % wn, wn) : 0;
+                                const int wpool = (me.x & OWGS_AM_POOL) ? 1 : 0;
+                                const int wn = wpool ? nb : nm, wbase = wpool ? A.n_ids - nb : 0;
+                                const int whome = (int)(me.x & OWGS_AM_POS_MASK), wstep = (int)((me.x >> 15) & OWGS_AM_POS_MASK);
                                 if (o_f & 1) {
                                     depth = 0x7FFFFFFF;  // n + 2 failed probes, then the forced acquire (SCPB:417-424)
-                                } else {
+                                } else if (wn > 1) {
                                     const int d = (o_v - wbase - whome + wn) % wn;
-                                    depth = wn > 1 ? (int)(((long long)d * winv) % wn) : 0;
+                                    depth = (int)(((long long)d * res_inv_mod(wstep % wn, wn)) % wn);
                                 }
                             }
-                            bool lead = false;
-                            for (u64 bb = __ballot(wd); bb;) {  // one leader per action: its deepest walk
+                            for (u64 bb = __ballot(wd && depth > 0); bb;) {  // one entry per action: its deepest walk
                                 const int q = ffs64(bb);
                                 const uint32_t aq = (uint32_t)__builtin_amdgcn_readlane((int)l_act, q);
-                                const bool in_g = wd && l_act == aq;
+                                const bool in_g = wd && depth > 0 && l_act == aq;
                                 const int dd = wave_max_i(in_g ? depth : -1);
-                                if (lane == q) {
-                                    lead = true;
-                                    depth = dd;
-                                }
                                 bb &= ~__ballot(in_g);
-                            }
-                            uint4 e;
-                            if (lead && depth > 0 && res_w_sfind(A, me.z & 0x1FFFFu, &e)) {
-                                const bool primary = e.w == l_act;
-                                for (uint32_t k = e.y; k < e.y + e.z; ++k) {
-                                    const uint2 pe = A.w_list[k];
-                                    if (primary && (int)pe.y >= depth) break;  // (the list is by step)
-                                    const uint32_t key = __hip_atomic_load(&A.w.keys[pe.x], __ATOMIC_RELAXED,
-                                                                           __HIP_MEMORY_SCOPE_AGENT);
-                                    if (key == 0u || key == OWGS_CT_TOMB) continue;
-                                    const int x = (int)(key & 0x7FFFu) - 1;
-                                    if (x < 0 || x >= A.n_ids || !((ub[x >> 5] >> (x & 31)) & 1u)) continue;  // not tried
-                                    if (!primary) {
-                                        const int pos = x - wbase;
-                                        if (pos < 0 || pos >= wn) continue;
-                                        const int s = wn > 1 ? (int)(((long long)((pos - whome + wn) % wn) * winv) % wn) : 0;
-                                        if (s >= depth) continue;
+                                const int nl = sc[RS_WLN];
+                                const u64 hit = __ballot((lane < nl && wl[lane].x == aq) ||
+                                                         (lane + 64 < nl && wl[lane + 64].x == aq));
+                                if (hit) {
+                                    const int h = ffs64(hit);
+                                    const int j = wl[h].x == aq ? h : h + 64;
+                                    if (lane == 0) wl[j].y = (uint32_t)max((int)wl[j].y, dd);
+                                } else {
+                                    if (nl >= RES_WL) {
+                                        w_flush();
                                     }
-                                    atomicOr(&A.w.vals[pe.x], OWGS_W_Z);
+                                    if (lane == 0) {
+                                        const int j = sc[RS_WLN];
+                                        wl[j] = make_uint2(aq, (uint32_t)dd);
+                                        sc[RS_WLN] = j + 1;
+                                    }
                                 }
+                                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                             }
                         }
                     }
                 }
+                if (A.w.cap > 0) w_flush();
                 pr_pub += clock64() - tp0;
             }
             // the call's releases may have raised permits: the range bound grows by what they returned at most

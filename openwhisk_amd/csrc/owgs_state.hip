@@ -103,6 +103,29 @@ __global__ __launch_bounds__(256) void owgs_usable_kernel(const uint8_t* status,
     bits[wd] = b;
 }
 
+// the usable bitmap of every row of a [rows][stride] status matrix (one row per batch: the health each batch of a group
+// replay applies before its releases, owgs_replay_device_group) into bits[row * n_words ..]
+__global__ __launch_bounds__(256) void owgs_usable_rows_kernel(const uint8_t* status, int64_t stride, int32_t n,
+                                                               uint32_t* bits, int32_t n_words) {
+    const int wd = blockIdx.x * 256 + threadIdx.x, row = blockIdx.y;
+    if (wd >= n_words) return;
+    const uint8_t* st = status + (int64_t)row * stride;
+    uint32_t b = 0;
+    for (int k = 0; k < 32; ++k) {
+        const int i = wd * 32 + k;
+        if (i < n && st[i] == 0) b |= 1u << k;  // OWGS_HEALTHY
+    }
+    bits[(int64_t)row * n_words + wd] = b;
+}
+
+extern "C" hipError_t owgs_launch_usable_rows(const uint8_t* status, int64_t stride, int32_t n, int32_t rows,
+                                              uint32_t* bits, int32_t n_words, hipStream_t s) {
+    if (rows <= 0 || n_words <= 0) return hipSuccess;
+    hipLaunchKernelGGL(owgs_usable_rows_kernel, dim3((unsigned)((n_words + 255) / 256), (unsigned)rows), dim3(256), 0, s,
+                       status, stride, n, bits, n_words);
+    return hipGetLastError();
+}
+
 extern "C" int32_t owgs_coprime_max(void) { return CP_MAX; }
 
 // xs[0..n_pools) on the device; out[p * out_stride ..] receives pool p's list, counts[p] its length.

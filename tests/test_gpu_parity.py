@@ -666,3 +666,64 @@ def test_health_on_one_stream_replay_on_another_is_ordered():
     assert len(bad) == 0, f"first mismatch at {bad[:5]}"
     assert np.array_equal(d_fl.cpu().numpy(), o_fl)
     assert np.array_equal(b.permits(), st.permits())
+
+
+@pytest.mark.parametrize("cfg,kw,group,cluster_at", [
+    ("headline", dict(n_activations=250_000, n_invokers=3000, conc_frac=0.3), 4, None),
+    ("headline", dict(n_activations=250_000, n_invokers=3000, conc_frac=0.3), 1, None),
+    ("c4", dict(n_activations=200_000), 5, None),
+    ("c2", dict(n_activations=200_000), 64, None),
+    ("headline", dict(n_activations=150_000, n_invokers=2000, conc_frac=0.3), 3, 2),
+])
+def test_group_replay_with_per_batch_health_matches_oracle(cfg, kw, group, cluster_at):
+    """configs[4] cadence with several batches per engine launch (owgs_replay_device_group): the engine applies batch
+    b's health vector itself before the batch's releases (updateInvokers, SCPB:512-551: usable bitmap, the usable flag
+    of each changed invoker's permits, the pools' healthy counts), and the group's releases name activations decided
+    by earlier launches (records written from those decisions) or by earlier batches of the group.  Bit-exact with the
+    oracle applying the same vector before every batch; one variant changes the cluster size between groups (watched
+    pairs: the call takes its batch-by-batch fallback)."""
+    import torch
+    from openwhisk_amd import cluster
+
+    w = W.config(cfg, **kw)
+    s = w.stream
+    sched = cluster.health_schedule(w.inv_status, s.n_batches, churn=0.03)
+    b = gpu_for(w)
+    st = O.state_for(w, zombies=True)
+    dev = torch.device("cuda", 0)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
+    d_act, d_aid = t(s.act, np.int32), t(s.rel_aid, np.int64)
+    d_out = torch.full((len(s.act),), -9, dtype=torch.int32, device=dev)
+    d_fl = torch.zeros(len(s.act), dtype=torch.uint8, device=dev)
+    d_rf = torch.zeros(max(len(s.rel_aid), 1), dtype=torch.uint8, device=dev)
+    nid = len(w.inv_status)
+    d_h = t(np.stack(sched), np.uint8)  # [n_batches][n_invokers]
+    n = len(s.act)
+    o_inv = np.full(n, -9, np.int32)
+    o_fl = np.zeros(n, np.uint8)
+    o_rf = np.zeros(max(len(s.rel_aid), 1), np.uint8)
+    P = O._ptr
+    acq = np.ascontiguousarray(s.acq_off, np.int64)
+    rel = np.ascontiguousarray(s.rel_off, np.int64)
+    act = np.ascontiguousarray(s.act, np.int32)
+    aid = np.ascontiguousarray(s.rel_aid, np.int64)
+    for g0 in range(0, s.n_batches, group):
+        g1 = min(g0 + group, s.n_batches)
+        if cluster_at is not None and g0 >= cluster_at and g0 - group < cluster_at:
+            b.update_cluster(2)
+            st.update_cluster(2)
+        b.replay_device_group(acq[g0:g1 + 1], rel[g0:g1 + 1], d_act.data_ptr(), d_aid.data_ptr(), s.seq_base,
+                              d_out.data_ptr(), d_fl.data_ptr(), d_rf.data_ptr(), d_h[g0].data_ptr(), nid, nid)
+        for k in range(g0, g1):
+            st.update_invokers(w.inv_ids, w.inv_mem, sched[k])
+            O.lib().owo_replay(st.h, 1, P(acq[k:]), P(act), P(rel[k:]), P(aid), int(s.seq_base), P(o_inv), P(o_fl),
+                               P(o_rf))
+    torch.cuda.synchronize()
+    g_inv = d_out.cpu().numpy()
+    bad = np.nonzero(g_inv != o_inv)[0]
+    assert len(bad) == 0, f"first mismatch at {bad[:5]} gpu {g_inv[bad[:5]]} oracle {o_inv[bad[:5]]}"
+    assert np.array_equal(d_fl.cpu().numpy(), o_fl)
+    assert np.array_equal(d_rf.cpu().numpy()[:len(s.rel_aid)], o_rf[:len(s.rel_aid)])
+    assert np.array_equal(b.permits(), st.permits())
+    # the context's health after the call is the last batch's (a later publish sees it)
+    assert np.array_equal(b.resident_stats()["alive"], 0)

@@ -63,7 +63,9 @@ import json
 d=json.load(open('$O/shim_$n.json'))
 for l in d['legs']:
     r=l.get('resident') or {}; s=max(1, r.get('served', 0))
-    print('$n', l['mode'], l['drain'], 'p50', l['p50_us'], 'p99', l.get('p99_us'), round(l['decisions_per_s']/1e6,2), 'M/s pub', round(r.get('publish_cycles',0)/s), 'alone', round(r.get('alone_cycles',0)/s))
+    if l['mode'] == 'fused-reset':
+        print('$n', l['mode'], 'resident', l['resident_fraction_after'], 'p50 before/after', round(l['p50_us_before'],1), round(l['p50_us_after'],1), 'p99', round(l['p99_us_after'],1), 'exact', l['bit_exact']); continue
+    print('$n', l['mode'], l['drain'], 'p50', round(l['p50_us'],1), 'p99', round(l.get('p99_us'),1), round(l['decisions_per_s']/1e6,2), 'M/s pub', round(r.get('publish_cycles',0)/s), 'alone', round(r.get('alone_cycles',0)/s), 'launches', r.get('launches'), 'chained', r.get('chained'))
 " | tee -a $O/abshim.txt
         done
       done ;;
@@ -76,6 +78,27 @@ for l in d['legs']:
           rc=$?; grep -v amdgpu.ids $O/abcfg_$i.log | grep -v cycles/activation | cut -c1-120 | tee -a $O/abcfg.txt; [ $rc -eq 0 ] || stop abcfg $rc
         done
       done ;;
+    churn)  # configs[4] cadence on one GPU (health exchanged and applied before every batch) vs one launch per step
+      rm -f $O/churn.jsonl
+      for c in "" "--cluster-size 8"; do
+        for h in "" "--health-churn" "--health-churn --health-group 1"; do
+          timeout -k 10 400 python bench.py $h $c --steps 5 --warmup 1 --no-shim-path --no-cpu-baseline --no-h2d >> $O/churn.jsonl 2>> $O/churn.err
+          rc=$?; tail -1 $O/churn.jsonl | cut -c1-200; [ $rc -eq 0 ] || { tail -20 $O/churn.err; stop "churn $h $c" $rc; }
+        done
+      done ;;
+    churnprof)  # kernel trace of the per-batch cadence (gaps between a span's launches)
+      rm -rf $O/churnprof
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/churnprof -o run --output-format csv -- \
+        python3 bench.py --health-churn ${CHURNARGS} --steps 3 --warmup 1 --no-cpu-baseline --no-check --no-h2d --no-shim-path > $O/churnprof.log 2>&1
+      rc=$?; tail -1 $O/churnprof.log | cut -c1-200; [ $rc -eq 0 ] || stop churnprof $rc ;;
+    spanhost)  # host microseconds per call of the per-batch cadence (calls that wait for the GPU)
+      for n in 1 8; do
+        timeout -k 10 300 python tools/span_host_timing.py $n >> $O/spanhost.jsonl 2>> $O/spanhost.err
+        rc=$?; tail -1 $O/spanhost.jsonl | cut -c1-600; [ $rc -eq 0 ] || { tail -5 $O/spanhost.err; stop spanhost $rc; }
+      done ;;
+    p99)  # per-call counters of the 512-job shim leg: the slowest 1 % against the median
+      timeout -k 10 300 python tools/shim_p99.py > $O/p99.json 2> $O/p99.err
+      rc=$?; cut -c1-600 $O/p99.json; [ $rc -eq 0 ] || { tail -5 $O/p99.err; stop p99 $rc; } ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
