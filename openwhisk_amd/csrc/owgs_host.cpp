@@ -44,6 +44,12 @@ extern "C" hipError_t owgs_launch_coprime(const int32_t* xs, int32_t n_pools, in
                                           int32_t* counts, hipStream_t s);
 extern "C" hipError_t owgs_launch_slots(const int64_t* mem_bytes, int32_t from, int32_t n, int32_t cluster,
                                        int64_t min_bytes, int32_t* permits, hipStream_t s);
+extern "C" hipError_t owgs_launch_seq(const OwgsSeqArgs* a, hipStream_t s);
+extern "C" hipError_t owgs_launch_seq_rehash(const uint4* old, int32_t old_cap, const OwgsSeqArgs* a, hipStream_t s);
+extern "C" hipError_t owgs_launch_seq_migrate(const uint32_t* ct_keys, const uint32_t* ct_vals, int32_t n_ct,
+                                              const uint2* ovf, int32_t ovf_cap, const uint32_t* w_keys,
+                                              const uint32_t* w_vals, int32_t w_cap, const OwgsSeqArgs* a, hipStream_t s);
+extern "C" hipError_t owgs_launch_seq_lookup(const OwgsSeqArgs* a, int32_t inv, int32_t slot, int32_t* out, hipStream_t s);
 extern "C" hipError_t owgs_launch_usable_rows(const uint8_t* status, int64_t stride, int32_t n, int32_t rows,
                                               uint32_t* bits, int32_t n_words, hipStream_t s);
 extern "C" hipError_t owgs_launch_usable(const uint8_t* status, int32_t n, uint32_t* bits, int32_t n_words,
@@ -313,6 +319,12 @@ struct owgs_ctx {
     // owgs_replay_device_group: its batch offsets, the usable bitmap of each batch's health, and (during the call) the
     // first activation of the group (releases of earlier ones get their records from those decisions)
     DevBuf<int64_t> g_off;
+    // large-state engine (owgs_seq.hip): a state beyond every on-chip geometry (owgs_limits) or maxConcurrent beyond
+    // OWGS_MAX_CONC runs there -- permits in HBM, the NestedSemaphore maps in one HBM table q_map
+    bool large = false, big_conc = false;
+    DevBuf<uint4> q_map;
+    int32_t q_cap = 0;
+    DevBuf<int32_t> q_filled, q_state, q_look;
     DevBuf<uint32_t> d_hwords;
     const uint32_t* grp_hwords = nullptr;
     int32_t grp_hstride = 0;
@@ -971,7 +983,8 @@ static bool registered(const owgs_ctx* c, int32_t n, const int32_t* action) {
 // (NestedSemaphore.scala:109-111), so a key whose activations have all completed leaves nothing behind.  One scan
 // over the tables on the device; keys still named stay pending for a later attempt.
 static int reclaim_slots(owgs_ctx* c) {
-    if (c->pending_slots.empty()) return OWGS_OK;
+    // (the large-state engine's map keeps the reference's empty entries, which never leave: its keys stay taken)
+    if (c->pending_slots.empty() || c->large) return OWGS_OK;
     const size_t words = ((size_t)OWGS_MAX_SLOTKEYS + 32) / 32;
     std::vector<uint32_t> cand(words, 0u);
     size_t k = 0;
@@ -1041,7 +1054,7 @@ static size_t res_stage_bytes(const owgs_ctx* c) {
 
 // identity pools, a call the staging area holds (watched pairs included: the engine applies their releases and marks)
 static bool res_eligible(const owgs_ctx* c, int32_t n_runs, int32_t NR, int32_t NP, bool has_seq) {
-    if (env_opts().res <= 0 || c->pool_mode != 0) return false;
+    if (env_opts().res <= 0 || c->pool_mode != 0 || c->large) return false;
     if (c->w_cap > 0 && env_opts().res_watch <= 0) return false;
     if ((int64_t)NR + NP > env_opts().res_max || NP + NR == 0) return false;
     if (c->n_slots > OWGS_MAX_SLOTS_CT || c->n_ids > c->n_slots || c->nm > (int32_t)OWGS_AM_POS_MASK ||
@@ -1408,6 +1421,187 @@ static int res_process(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
     return OWGS_OK;
 }
 
+// ---------------------------------------------------------------------------------------------- large-state engine
+// owgs_seq.hip: contexts whose state no on-chip geometry holds (owgs_limits), or with maxConcurrent > OWGS_MAX_CONC.
+// Identity pools; every call through it is synchronous (the host reads where the kernel stopped to grow the map).
+#define OWGS_NOT_LARGE(c)                                                                                   \
+    do {                                                                                                  \
+        if ((c)->large)                                                                                   \
+            return (c)->fail(OWGS_ERANGE, "not available for a state beyond owgs_limits (large-state engine)"); \
+    } while (0)
+
+static bool large_fits(int32_t n_ids, int32_t nm, int32_t nb) {
+    return n_ids <= OWGS_SEQ_MAX_WORDS * 32 && nm <= owgs_coprime_max() && nb <= owgs_coprime_max();
+}
+
+static OwgsSeqArgs seq_args(owgs_ctx* c) {
+    OwgsSeqArgs S{};
+    S.permits = c->d_permits.p;
+    S.n_slots = c->n_slots;
+    S.usable = c->d_usable.p;
+    S.n_ids = c->n_ids;
+    S.nm = c->nm;
+    S.nb = c->nb;
+    S.msteps = c->d_steps.p;
+    S.n_msteps = (int32_t)c->msteps.size();
+    S.bsteps = c->d_steps.p + c->steps_stride;
+    S.n_bsteps = (int32_t)c->bsteps.size();
+    S.act_hash = c->d_act_hash.p;
+    S.act_mem = c->d_act_mem.p;
+    S.act_maxc = c->d_act_maxc.p;
+    S.act_slot = c->d_act_slot.p;
+    S.act_bb = c->d_act_bb.p;
+    S.map = c->q_map.p;
+    S.map_cap = c->q_cap;
+    S.map_filled = c->q_filled.p;
+    S.rng_seed = c->cfg.rng_seed;
+    S.state = c->q_state.p;
+    S.err = c->d_err.p;
+    return S;
+}
+
+// the map keeps `room` more entries under half its capacity: read its fill, grow (rehash live entries) if needed
+static int seq_reserve(owgs_ctx* c, int64_t room, hipStream_t s) {
+    HIPCHK(c, c->q_state.reserve(8));
+    if (!c->q_filled.p) {
+        HIPCHK(c, c->q_filled.reserve(1));
+        HIPCHK(c, hipMemsetAsync(c->q_filled.p, 0, 4, s));
+    }
+    int32_t filled = 0;
+    if (c->q_cap > 0) {
+        HIPCHK(c, hipMemcpyAsync(&filled, c->q_filled.p, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        if ((int64_t)c->q_cap >= 2 * ((int64_t)filled + room)) return OWGS_OK;
+    }
+    int64_t cap = (int64_t)1 << 16;
+    while (cap < 4 * ((int64_t)filled + room)) cap <<= 1;
+    if (cap > ((int64_t)1 << 30)) return c->fail(OWGS_ENOMEM, "NestedSemaphore map beyond 2^30 entries");
+    DevBuf<uint4> nt;
+    HIPCHK(c, nt.reserve((size_t)cap));
+    HIPCHK(c, hipMemsetAsync(nt.p, 0, (size_t)cap * sizeof(uint4), s));
+    HIPCHK(c, hipMemsetAsync(c->q_filled.p, 0, 4, s));  // (the rehash counts the live entries again)
+    if (c->q_cap > 0) {
+        OwgsSeqArgs S = seq_args(c);
+        S.map = nt.p;
+        S.map_cap = (int32_t)cap;
+        HIPCHK(c, owgs_launch_seq_rehash(c->q_map.p, c->q_cap, &S, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+    }
+    c->q_map.release();
+    c->q_map = nt;
+    nt.p = nullptr;
+    c->q_cap = (int32_t)cap;
+    return OWGS_OK;
+}
+
+// the context switches to the large-state engine: the on-chip map's entries (and the empty entries watched pairs stand
+// for) move into the large map; the on-chip map and W are then unused
+static int seq_migrate(owgs_ctx* c) {
+    hipStream_t s = c->stream;
+    int32_t ovf_n = 0;
+    if (c->ovf_cap > 0) {
+        HIPCHK(c, hipStreamSynchronize(s));
+        HIPCHK(c, hipMemcpy(&ovf_n, c->d_ovf_cnt.p, sizeof(ovf_n), hipMemcpyDeviceToHost));
+    }
+    int rc = seq_reserve(c, (int64_t)OWGS_CTC + ovf_n + std::max(c->w_cap, 0) + 4096, s);
+    if (rc) return rc;
+    OwgsSeqArgs S = seq_args(c);
+    if (c->d_ct_keys.p || (c->w_cap > 0))
+        HIPCHK(c, owgs_launch_seq_migrate(c->d_ct_keys.p, c->d_ct_vals.p, c->d_ct_keys.p ? OWGS_CTC : 0,
+                                          ovf_n > 0 ? c->d_ovf.p : nullptr, c->ovf_cap, c->w_cap > 0 ? c->w_keys.p : nullptr,
+                                          c->w_vals.p, c->w_cap, &S, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    rc = check_err_word(c);
+    if (rc) return rc;
+    w_drop(c);
+    return reset_ctab(c);
+}
+
+// runs through the large-state engine (S: its runs, releases, publishes, outputs); resumes after map growth
+static int seq_run(owgs_ctx* c, const OwgsSeqArgs& S0, hipStream_t s) {
+    const int64_t room = 2 * ((int64_t)std::max(c->nm, c->nb) + 2) + 4096;
+    for (int resume = 0;; resume = 1) {
+        const int rc = seq_reserve(c, room, s);
+        if (rc) return rc;
+        OwgsSeqArgs S = S0;
+        S.map = c->q_map.p;
+        S.map_cap = c->q_cap;
+        S.map_filled = c->q_filled.p;
+        S.state = c->q_state.p;
+        S.resume = resume;
+        HIPCHK(c, owgs_launch_seq(&S, s));
+        int32_t st[5] = {0, 0, 0, 0, 0};
+        HIPCHK(c, hipMemcpyAsync(st, c->q_state.p, sizeof(st), hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        if (st[0] == 0) break;
+    }
+    return check_err_word(c);
+}
+
+// runs of explicit (host) releases and publishes, as owgs_process_batch / owgs_publish_batch / owgs_release_batch
+static int seq_host_runs(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, const int32_t* rel_inv,
+                         const int32_t* rel_act, uint8_t* rel_flags, const int32_t* pub_off, const int32_t* pub_act,
+                         const uint64_t* seq, uint64_t seq_base, int32_t* out_inv, uint8_t* out_flags) {
+    hipStream_t s = c->stream;
+    const int32_t NR = rel_off[n_runs], NP = pub_off[n_runs];
+    std::vector<int64_t> offs((size_t)2 * (n_runs + 1));
+    for (int32_t r = 0; r <= n_runs; ++r) {
+        offs[r] = rel_off[r];
+        offs[n_runs + 1 + r] = pub_off[r];
+    }
+    HIPCHK(c, upload(c->g_off, offs.data(), offs.size(), s));
+    if (NR) {
+        HIPCHK(c, upload(c->d_b, rel_inv, (size_t)NR, s));
+        HIPCHK(c, upload(c->d_c, rel_act, (size_t)NR, s));
+        HIPCHK(c, c->d_rflags.reserve((size_t)NR));
+    }
+    if (NP) {
+        HIPCHK(c, upload(c->d_a, pub_act, (size_t)NP, s));
+        HIPCHK(c, c->d_out.reserve((size_t)NP));
+        HIPCHK(c, c->d_flags.reserve((size_t)NP));
+        if (seq) HIPCHK(c, upload(c->d_seq, (const u64*)seq, (size_t)NP, s));
+    }
+    OwgsSeqArgs S = seq_args(c);
+    S.n_runs = n_runs;
+    S.rel_off = c->g_off.p;
+    S.pub_off = c->g_off.p + n_runs + 1;
+    S.rel_inv = c->d_b.p;
+    S.rel_act = c->d_c.p;
+    S.rel_flags = NR ? c->d_rflags.p : nullptr;
+    S.pub_act = c->d_a.p;
+    S.seq = (seq && NP) ? c->d_seq.p : nullptr;
+    S.seq_base = seq_base;
+    S.out_inv = c->d_out.p;
+    S.out_flags = c->d_flags.p;
+    const int rc = seq_run(c, S, s);
+    if (NP) {
+        HIPCHK(c, hipMemcpyAsync(out_inv, c->d_out.p, (size_t)NP * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(out_flags, c->d_flags.p, (size_t)NP, hipMemcpyDeviceToHost, s));
+    }
+    if (NR && rel_flags) HIPCHK(c, hipMemcpyAsync(rel_flags, c->d_rflags.p, (size_t)NR, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    return rc;
+}
+
+// a device-resident stream's batches (releases by activation: invoker out_inv[aid], action act[aid])
+static int seq_device_runs(owgs_ctx* c, int32_t n_runs, const int64_t* d_rel_off, const int64_t* d_pub_off,
+                           const int32_t* act, const int64_t* rel_aid, uint64_t seq_base, int32_t* out_inv,
+                           uint8_t* out_flags, uint8_t* rel_flags, hipStream_t s) {
+    OwgsSeqArgs S = seq_args(c);
+    S.n_runs = n_runs;
+    S.rel_off = d_rel_off;
+    S.pub_off = d_pub_off;
+    S.rel_aid = rel_aid;
+    S.dec_inv = out_inv;
+    S.dec_act = act;
+    S.rel_flags = rel_flags;
+    S.pub_act = act;
+    S.seq_base = seq_base;
+    S.out_inv = out_inv;
+    S.out_flags = out_flags;
+    return seq_run(c, S, s);
+}
+
 // times one ABI call, entry to return, into c->last_call_ns (the latency the JNI shim sees, without the host
 // language's call overhead)
 struct CallTimer {
@@ -1521,6 +1715,10 @@ void owgs_destroy(owgs_ctx* c) {
     DevBuf<uint32_t>* u32s[] = {&c->d_usable, &c->d_ct_keys, &c->d_ct_vals, &c->d_ct_tmp, &c->s_ct_keys, &c->s_ct_vals};
     for (auto* b : u32s) b->release();
     c->d_act_bb.release();
+    c->q_map.release();
+    c->q_filled.release();
+    c->q_state.release();
+    c->q_look.release();
     c->d_act_cok.release();
     c->d_act_meta.release();
     c->d_stats.release();
@@ -1639,6 +1837,7 @@ int owgs_update_invokers(owgs_ctx* c, int32_t n, const int32_t* ids, const int64
     }
     const int32_t old_size = (int32_t)c->ids.size();
     const int32_t new_size = n;
+    bool large_next = false;
     int32_t managed = d2i(std::ceil((double)new_size * c->mf));
     if (managed < 1) managed = 1;
     int32_t blackboxes = d2i(std::floor((double)new_size * c->bf));
@@ -1649,8 +1848,9 @@ int owgs_update_invokers(owgs_ctx* c, int32_t n, const int32_t* ids, const int64
         const int32_t slots = (old_size < new_size && n > c->n_slots) ? n : c->n_slots;
         bool identity = n <= slots;
         for (int32_t i = 0; identity && i < n; ++i) identity = ids[i] == i;
-        if (engine_variant(slots, identity ? 0 : 1, n, std::min(managed, n), std::min(blackboxes, n)) < 0)
-            return c->fail(OWGS_ERANGE, "invoker state exceeds the engine's on-chip (LDS) capacity (owgs_limits)");
+        large_next = engine_variant(slots, identity ? 0 : 1, n, std::min(managed, n), std::min(blackboxes, n)) < 0;
+        if (large_next && !(identity && large_fits(n, std::min(managed, n), std::min(blackboxes, n))))
+            return c->fail(OWGS_ERANGE, "invoker state exceeds every engine (owgs_limits; explicit pools on chip only)");
     }
     if (c->status_stale) {  // a device-only health update still in flight must land before the upload below
         HIPCHK(c, hipEventSynchronize(c->ev_status));
@@ -1699,10 +1899,13 @@ int owgs_update_invokers(owgs_ctx* c, int32_t n, const int32_t* ids, const int64
             c->n_slots = n;
         }
     }
+    const bool was_large = c->large;
+    c->large = large_next || c->big_conc;
     int rc = rebuild_pools(c);
+    if (!rc && c->large && !was_large) rc = seq_migrate(c);
     if (!rc) rc = prepare_actions(c);
     if (!rc) HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (!rc) rc = lds_check(c);
+    if (!rc && !c->large) rc = lds_check(c);
     return rc;
 }
 
@@ -1716,15 +1919,20 @@ int owgs_update_cluster(owgs_ctx* c, int32_t new_size) {
     }
     const int32_t actual = new_size > 1 ? new_size : 1;
     if (c->cluster == actual) return OWGS_OK;
-    int rw = w_rebuild(c);  // in-flight concurrent activations of the discarded entries become watched pairs
-    if (rw) return rw;
+    if (!c->large) {
+        int rw = w_rebuild(c);  // in-flight concurrent activations of the discarded entries become watched pairs
+        if (rw) return rw;
+    } else if (c->q_cap > 0) {  // large-state engine: the map (with its empty entries) is discarded with the slots
+        HIPCHK(c, hipMemsetAsync(c->q_map.p, 0, (size_t)c->q_cap * sizeof(uint4), c->stream));
+        HIPCHK(c, hipMemsetAsync(c->q_filled.p, 0, 4, c->stream));
+    }
     c->cluster = actual;
     const int32_t n = (int32_t)c->ids.size();
     HIPCHK(c, c->d_permits.reserve((size_t)n));
     HIPCHK(c, owgs_launch_slots(c->d_mem_bytes.p, 0, n, c->cluster, c->cfg.min_memory_bytes, c->d_permits.p,
                                 c->stream));
     c->n_slots = n;
-    int rc = reset_ctab(c);
+    int rc = c->large ? OWGS_OK : reset_ctab(c);
     if (!rc) rc = rebuild_pools(c);
     if (!rc) HIPCHK(c, hipStreamSynchronize(c->stream));
     return rc;
@@ -1742,7 +1950,7 @@ int owgs_register_actions(owgs_ctx* c, int32_t n, const char* ns_bytes, const in
     for (int32_t i = 0; i < n; ++i) {
         // MemoryLimit/ConcurrencyLimit guarantee positive values (MemoryLimit.scala:68-69); the reference's
         // require(...) checks (FS:96, NS:85) would throw on anything else
-        if (mem_mb[i] <= 0 || mem_mb[i] > OWGS_MAX_MEM_MB || max_conc[i] < 1 || max_conc[i] > OWGS_MAX_CONC)
+        if (mem_mb[i] <= 0 || mem_mb[i] > OWGS_MAX_MEM_MB || max_conc[i] < 1)
             return c->fail(OWGS_EINVAL, "mem/maxConcurrent");
         if (ns_off[i + 1] < ns_off[i] || path_off[i + 1] < path_off[i] || key_off[i + 1] < key_off[i])
             return c->fail(OWGS_EINVAL, "offsets");
@@ -1830,6 +2038,15 @@ int owgs_register_actions(owgs_ctx* c, int32_t n, const char* ns_bytes, const in
         c->a_bb[a] = blackbox[i] ? 1 : 0;
         c->a_live[a] = 1;
         if (max_conc[i] > 1) c->any_conc = true;
+        if (max_conc[i] > OWGS_MAX_CONC && !c->big_conc) {  // beyond the on-chip map's field: the large-state engine
+            if (!c->ids.empty() && c->pool_mode != 0) return c->fail(OWGS_ERANGE, "maxConcurrent beyond 4095 needs identity pools");
+            c->big_conc = true;
+            if (!c->large) {
+                c->large = true;
+                const int rm = seq_migrate(c);
+                if (rm) return rm;
+            }
+        }
         hid[i] = a;
         out_action[i] = a;
     }
@@ -1907,6 +2124,10 @@ int owgs_publish_batch(owgs_ctx* c, int32_t n, const int32_t* action, const uint
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
+    }
+    if (c->large) {
+        const int32_t ro[2] = {0, 0}, po[2] = {0, n};
+        return seq_host_runs(c, 1, ro, nullptr, nullptr, nullptr, po, action, seq, seq_base, out_invoker, out_flags);
     }
     const int64_t off[2] = {0, n};
     HIPCHK(c, upload(c->d_off, off, 2, c->stream));
@@ -1998,6 +2219,13 @@ int owgs_release_batch(owgs_ctx* c, int32_t n, const int32_t* invoker, const int
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
     }
+    if (c->large) {
+        const int32_t ro[2] = {0, n}, po[2] = {0, 0};
+        std::vector<uint8_t> fl((size_t)n);
+        const int rc = seq_host_runs(c, 1, ro, invoker, action, fl.data(), po, nullptr, nullptr, 0, nullptr, nullptr);
+        if (out_flags) memcpy(out_flags, fl.data(), (size_t)n);
+        return rc;
+    }
     std::vector<int32_t> mem(n), mc(n), sl(n);
     for (int32_t i = 0; i < n; ++i) {
         mem[i] = c->a_mem[action[i]];
@@ -2023,6 +2251,7 @@ int owgs_schedule_walks(owgs_ctx* c, int32_t n, const uint8_t* pool, const int32
                         int32_t* out_invoker, uint8_t* out_flags) {
     if (!c || n < 0 || (n > 0 && (!pool || !index || !step || !mem_mb || !max_conc || !key || !out_invoker || !out_flags)))
         return OWGS_EINVAL;
+    OWGS_NOT_LARGE(c);
     if (n == 0) return OWGS_OK;
     std::vector<uint2> xm(n);
     for (int32_t i = 0; i < n; ++i) {
@@ -2072,6 +2301,7 @@ int owgs_schedule_walks(owgs_ctx* c, int32_t n, const uint8_t* pool, const int32
 
 int owgs_set_slots(owgs_ctx* c, int32_t n, const int32_t* permits) {
     if (!c || n < 0 || (n > 0 && !permits)) return OWGS_EINVAL;
+    OWGS_NOT_LARGE(c);
     OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
@@ -2089,6 +2319,7 @@ int owgs_set_slots(owgs_ctx* c, int32_t n, const int32_t* permits) {
 
 int owgs_set_pool(owgs_ctx* c, int32_t pool, int32_t n, const int32_t* ids, const uint8_t* status) {
     if (!c || (pool != 0 && pool != 1) || n < 0 || (n > 0 && (!ids || !status))) return OWGS_EINVAL;
+    OWGS_NOT_LARGE(c);
     OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
@@ -2123,6 +2354,19 @@ int owgs_read_concurrent(owgs_ctx* c, int32_t invoker, int32_t key, int32_t* per
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
+    }
+    if (c->large) {  // the large-state engine's map (it holds the reference's empty entries too)
+        HIPCHK(c, c->q_look.reserve(4));
+        if (c->q_cap <= 0) return 0;
+        OwgsSeqArgs S = seq_args(c);
+        HIPCHK(c, owgs_launch_seq_lookup(&S, invoker, key, c->q_look.p, c->stream));
+        int32_t v[3];
+        HIPCHK(c, hipMemcpyAsync(v, c->q_look.p, sizeof(v), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (!v[0]) return 0;
+        if (permits) *permits = v[1];
+        if (op_count) *op_count = v[2];
+        return 1;
     }
     DevBuf<int32_t> di, dk;
     DevBuf<int2> dv;
@@ -2285,6 +2529,12 @@ static int replay_device_span_impl(owgs_ctx* c, int64_t a_beg, int64_t a_end, in
     if (na == 0 && nr == 0) return OWGS_OK;
     OWGS_ENTER(c);
     hipStream_t hs = stream ? (hipStream_t)stream : c->stream;
+    if (c->large) {  // one run: the batch's releases, then its publishes (whole-stream indices)
+        const int64_t offs[4] = {r_beg, r_end, a_beg, a_end};
+        HIPCHK(c, upload(c->g_off, offs, 4, hs));
+        return seq_device_runs(c, 1, c->g_off.p, c->g_off.p + 2, act, rel_aid, seq_base, out_invoker, out_flags,
+                               rel_flags, hs);
+    }
     HIPCHK(c, c->w_rfl.reserve((size_t)std::max<int64_t>(nr, 1)));
     uint8_t* rf = rel_flags ? rel_flags + r_beg : c->w_rfl.p;
     if (c->w_cap > 0) {  // watched pairs: ordered release kernels, one engine launch, the watch update
@@ -2458,6 +2708,19 @@ static int replay_device_impl(owgs_ctx* c, int32_t n_batches, const int64_t* acq
                        uint64_t seq_base, int32_t* out_invoker, uint8_t* out_flags, uint8_t* rel_flags, void* stream) {
     if (!c) return OWGS_EINVAL;
     hipStream_t hs = stream ? (hipStream_t)stream : c->stream;
+    if (n_batches > 0 && c->large) {
+        if (!acq_off || !act || !out_invoker || !out_flags || n_activations < 0 || n_releases < 0 ||
+            (n_releases > 0 && (!rel_off || !rel_aid)))
+            return OWGS_EINVAL;
+        if (c->a_mem.empty()) return c->fail(OWGS_ENOENT, "no actions registered");
+        const int64_t* ro = rel_off;
+        if (!ro) {  // no releases: zero offsets
+            std::vector<int64_t> z((size_t)n_batches + 1, 0);
+            HIPCHK(c, upload(c->g_off, z.data(), z.size(), hs));
+            ro = c->g_off.p;
+        }
+        return seq_device_runs(c, n_batches, ro, acq_off, act, rel_aid, seq_base, out_invoker, out_flags, rel_flags, hs);
+    }
     if (n_batches > 0 && spec_replay_eligible(c)) {
         if (!acq_off || !act || !out_invoker || !out_flags || n_activations < 0 || n_activations >= ((int64_t)1 << 31) ||
             n_releases < 0 || (n_releases > 0 && (!rel_off || !rel_aid)))
@@ -2511,7 +2774,8 @@ static int replay_device_group_impl(owgs_ctx* c, int32_t nb, const int64_t* acq_
     if (rel_off[nb] > rel_off[0] && !rel_aid) return OWGS_EINVAL;
     if (status_dev && (n_status <= 0 || status_stride < n_status)) return c->fail(OWGS_EINVAL, "health rows");
     if (c->a_mem.empty()) return c->fail(OWGS_ENOENT, "no actions registered");
-    if (c->w_cap > 0 || c->pool_mode != 0 || spec_replay_eligible(c) || (status_dev && n_status != c->n_ids)) {
+    if (c->large || c->w_cap > 0 || c->pool_mode != 0 || spec_replay_eligible(c) ||
+        (status_dev && n_status != c->n_ids)) {
         for (int32_t b = 0; b < nb; ++b) {  // the batch-by-batch sequence the call stands for
             int rc = status_dev ? update_health_device_impl(c, n_status, status_dev + (int64_t)b * status_stride, stream)
                                 : OWGS_OK;
@@ -2821,6 +3085,9 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
             seq = nullptr;
         }
     }
+    if (c->large)
+        return seq_host_runs(c, n_runs, rel_off, rel_invoker, rel_action, rel_flags, pub_off, pub_action, seq,
+                             seq_base, out_invoker, out_flags);
     // small calls: the resident engine (owgs_resident.hip), no launch, copy or synchronisation per call
     if (res_eligible(c, n_runs, NR, NP, seq != nullptr)) {
         int served = 0;
@@ -2971,6 +3238,7 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
 
 int owgs_snapshot(owgs_ctx* c) {
     if (!c) return OWGS_EINVAL;
+    OWGS_NOT_LARGE(c);
     OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
@@ -3011,6 +3279,7 @@ int owgs_snapshot(owgs_ctx* c) {
 
 static int restore_impl(owgs_ctx* c, void* stream) {
     if (!c || !c->has_snap || c->snap_slots != c->n_slots) return OWGS_EINVAL;
+    OWGS_NOT_LARGE(c);
     // a key recycled since the snapshot may name another fqn@version now: the snapshot's entries would alias it
     if (c->slot_epoch != c->snap_slot_epoch) return c->fail(OWGS_EINVAL, "keys were recycled since the snapshot");
     OWGS_ENTER(c);
@@ -3204,6 +3473,7 @@ int owgs_activations_live(owgs_ctx* c, int64_t* live) {
 int owgs_track_activations(owgs_ctx* c, int32_t n, const char* aid32, const int32_t* action, const int32_t* ticket,
                            int32_t* out_ticket, uint8_t* out_existed) {
     if (!c || n < 0 || (n > 0 && (!aid32 || !action || !ticket || !out_ticket || !out_existed))) return OWGS_EINVAL;
+    OWGS_NOT_LARGE(c);
     if (n == 0) return OWGS_OK;
     if (!registered(c, n, action)) return c->fail(OWGS_ENOENT, "unknown action");
     // ActivationId.asString is 32 chars of [0-9a-f]; reject a malformed batch before any entry is created
@@ -3319,6 +3589,7 @@ int owgs_process_acks_device(owgs_ctx* c, int32_t n, const uint8_t* bytes, const
                              int32_t* out_invoker, int32_t* out_ticket, uint8_t* out_flags, void* stream) {
     if (!c || n < 0 || (n > 0 && (!bytes || !off || !out_kind || !out_invoker || !out_ticket || !out_flags)))
         return OWGS_EINVAL;
+    OWGS_NOT_LARGE(c);
     if (n == 0) return OWGS_OK;
     OWGS_ENTER(c);
     {
@@ -3348,6 +3619,7 @@ int owgs_process_acks(owgs_ctx* c, int32_t n, const char* bytes, const int64_t* 
                       int32_t* out_invoker, int32_t* out_ticket, uint8_t* out_flags) {
     if (!c || n < 0 || (n > 0 && (!bytes || !off || !out_kind || !out_invoker || !out_ticket || !out_flags)))
         return OWGS_EINVAL;
+    OWGS_NOT_LARGE(c);
     if (n == 0) return OWGS_OK;
     for (int32_t i = 0; i < n; ++i)
         if (off[i + 1] < off[i] || off[i] < 0) return c->fail(OWGS_EINVAL, "offsets");
@@ -3381,6 +3653,7 @@ int owgs_complete_activations(owgs_ctx* c, int32_t n, const char* aid32, const i
                               uint8_t* out_kind, int32_t* out_ticket, uint8_t* out_flags) {
     if (!c || n < 0 || (n > 0 && (!aid32 || !invoker || !flags || !out_kind || !out_ticket || !out_flags)))
         return OWGS_EINVAL;
+    OWGS_NOT_LARGE(c);
     if (n == 0) return OWGS_OK;
     OWGS_ENTER(c);
     {

@@ -396,6 +396,46 @@ struct OwgsResArgs {
     uint32_t* s_claim;           // one bit per activation, zeroed: a second release of one is refused (or null)
 };
 
+// Large-state engine (owgs_seq.hip): contexts beyond the on-chip image (owgs_limits) or with maxConcurrent beyond
+// OWGS_MAX_CONC.  Permits in HBM, one HBM map keyed by the full (invoker, fqn@version) pair, 32-bit walk positions.
+#define OWGS_SEQ_MAX_WORDS 4096  // usable-bitmap words (131,072 invoker ids; the pool step kernel allows 65,535 each)
+struct OwgsSeqArgs {
+    int32_t* permits;
+    int32_t n_slots;
+    const uint32_t* usable;       // identity pools: bitmap over ids [0, n_ids)
+    int32_t n_ids, nm, nb;
+    const int32_t* msteps;        // pairwiseCoprimeNumbersUntil of each pool (SCPB:379-384)
+    int32_t n_msteps;
+    const int32_t* bsteps;
+    int32_t n_bsteps;
+    const int32_t* act_hash;      // generateHash (SCPB:370-372) per action handle
+    const int32_t* act_mem;
+    const int32_t* act_maxc;
+    const int32_t* act_slot;
+    const uint8_t* act_bb;
+    uint4* map;                   // [map_cap] {invoker + 1 (0 empty, ~0 deleted), slot, free slots, operationCount}
+    int32_t map_cap;              // a power of two
+    int32_t* map_filled;          // non-empty entries (live + deleted)
+    int32_t n_runs;
+    const int64_t* rel_off;       // [n_runs + 1] releases of each run (indices into the release arrays)
+    const int64_t* pub_off;       // [n_runs + 1] publishes of each run (indices into pub_act / out_*)
+    const int64_t* rel_aid;       // releases by activation (stream replays): invoker dec_inv[aid], action dec_act[aid]
+    const int32_t* dec_inv;
+    const int32_t* dec_act;
+    const int32_t* rel_inv;       // explicit releases (rel_aid null): invoker and action handle
+    const int32_t* rel_act;
+    uint8_t* rel_flags;           // or null
+    const int32_t* pub_act;
+    const unsigned long long* seq;  // or null: seq_base + index
+    unsigned long long seq_base;
+    int32_t* out_inv;
+    uint8_t* out_flags;
+    unsigned long long rng_seed;
+    int32_t* state;               // [5] {stopped for a map growth, run, phase, index lo, hi} -- resumed when resume != 0
+    int32_t resume;
+    int32_t* err;
+};
+
 // owgs_process_batch: the caller's releases (invoker, action handle) of each run as engine release records
 struct OwgsStageArgs {
     int32_t n_runs;

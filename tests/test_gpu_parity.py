@@ -548,8 +548,9 @@ def test_large_pool_stream_parity(n_inv):
 
 
 def test_rejected_update_leaves_the_context_unchanged():
-    """owgs_update_invokers validates the state it would build before changing anything: a pool beyond owgs_limits
-    is refused with OWGS_ERANGE and the context keeps scheduling exactly as before (same permits, same pools)."""
+    """owgs_update_invokers validates the state it would build before changing anything: a pool beyond every engine
+    (the on-chip ones, owgs_limits, and the large-state engine's 65,535 pool positions) is refused with OWGS_ERANGE and
+    the context keeps scheduling exactly as before (same permits, same pools)."""
     import ctypes as C
     from openwhisk_amd import _lib
     from openwhisk_amd._lib import OwgsError
@@ -558,7 +559,7 @@ def test_rejected_update_leaves_the_context_unchanged():
     w = W.config("headline", n_invokers=2000, n_activations=40_000)
     b = gpu_for(w)
     before = (b.permits().copy(), b.managed_size, b.blackbox_size, b.cluster_size, b.managed_step_sizes)
-    n = mx.value + 1000
+    n = 140_000  # managed pool 126,000 positions
     with pytest.raises(OwgsError) as e:
         b.update_invokers_arrays(np.arange(n, dtype=np.int32), np.full(n, 16384 * MB, np.int64), np.zeros(n, np.uint8))
     assert e.value.code == -34  # OWGS_ERANGE
@@ -727,3 +728,101 @@ def test_group_replay_with_per_batch_health_matches_oracle(cfg, kw, group, clust
     assert np.array_equal(b.permits(), st.permits())
     # the context's health after the call is the last batch's (a later publish sees it)
     assert np.array_equal(b.resident_stats()["alive"], 0)
+
+
+# ----------------------------------------------------------------------------------------------- large-state engine
+def test_large_pool_40k_invokers_stream_matches_oracle():
+    """A 40,000-invoker pool (beyond every on-chip geometry, owgs_limits ~20.6k; 36,000 managed positions beyond the
+    15-bit key and walk fields) runs on the large-state engine (owgs_seq.hip: permits in HBM, one HBM map keyed by
+    the full (invoker, fqn@version) pair): the whole stream with concurrent actions and releases bit-exact with the
+    oracle -- decisions, overload flags, release flags, final permits."""
+    import ctypes as C
+    from openwhisk_amd import _lib
+    mx, ms = C.c_int32(), C.c_int32()
+    _lib.lib().owgs_limits(C.byref(mx), C.byref(ms))
+    w = W.config("headline", n_invokers=40_000, n_activations=80_000, n_actions=4000, n_namespaces=400,
+                 conc_frac=0.3, user_memory_mb=1024)
+    assert len(w.inv_ids) > mx.value and w.stream.n_batches > 3 and len(w.stream.rel_aid) > 10_000
+    b, g_inv, g_fl = check_stream(w)
+    assert (g_fl & 1).sum() >= 0 and (g_inv >= 0).all()
+
+
+def test_large_pool_shim_sequence_with_membership_change():
+    """The shim's call sequence (owgs_process_batch per drained batch) on a 25,000-invoker pool, with updateCluster
+    mid-stream (SCPB:561-584: the entries of in-flight concurrent activations are discarded; their releases meet the
+    new state and the empty entries failed tries leave, NS:61-62 -- the large-state engine keeps those literally),
+    call by call against the literal oracle."""
+    import test_gpu_resident as R
+    w = W.config("headline", n_invokers=25_000, n_activations=70_000, n_actions=3000, n_namespaces=300,
+                 conc_frac=0.4, load=1.1, user_memory_mb=1024)
+    assert len(w.stream.rel_aid) > 10_000
+    sh = R.Shim(w, shadow=True)
+    rng = np.random.default_rng(9)
+    half = len(sh.jobs) // 2
+    changed = False
+    while not sh.done():
+        if not changed and sh.pos >= half:
+            for x in (sh.g, sh.o, sh.z):
+                x.update_cluster(2)
+            changed = True
+        sh.call(int(rng.integers(1, 3000)))
+    assert np.array_equal(sh.g.permits(), sh.o.permits())
+    assert sh.g.resident_stats()["served"] == 0  # (no resident engine for a large state)
+    assert sh.z_rf != sh.o_rf  # releases only the reference's empty entries explain were reached
+
+
+def test_maxconcurrent_beyond_4095_and_growth_into_the_large_engine():
+    """maxConcurrent is bounded only by configuration in the reference (ConcurrencyLimit.scala:52,71); beyond the
+    on-chip map's 12-bit field the context moves to the large-state engine, carrying the on-chip map's entries (and the
+    empty entries watched pairs stand for) over -- here mid-stream, with activations in flight -- and so does a pool
+    that grows past owgs_limits.  Call by call against the literal oracle."""
+    from openwhisk_amd import Action
+    MB = 1024 * 1024
+    rng = np.random.default_rng(3)
+    g = gpu(managed_fraction=1.0, blackbox_fraction=0.0, rng_seed=4)
+    o = O.BalancerState(1.0, 0.0, rng_seed=4, zombies=True)
+    n0 = 300
+    ids, mem = np.arange(n0, dtype=np.int32), np.full(n0, 4096 * MB, np.int64)
+    g.update_invokers_arrays(ids, mem, np.zeros(n0, np.uint8))
+    o.update_invokers(ids, mem, np.zeros(n0, np.uint8))
+    acts = [Action(f"ns{a % 5}", f"ns{a % 5}/p/a{a}", "0.0.1", int(rng.choice([128, 256, 512])),
+                   int(rng.integers(2, 9)) if a % 3 else 1) for a in range(200)]
+    gh, _ = g.register_actions(acts)
+    oh = [o.register_action(a.namespace, a.path, k, a.mem_mb, a.max_concurrent) for k, a in enumerate(acts)]
+    live, seq = [], 0
+
+    def call(n_pub, n_rel):
+        nonlocal live, seq
+        pick = rng.choice(len(live), size=min(n_rel, len(live)), replace=False) if live else np.zeros(0, int)
+        rel = [live[j] for j in sorted(pick)]
+        keep = set(pick.tolist())
+        live = [x for j, x in enumerate(live) if j not in keep]
+        pubs = rng.integers(0, len(gh), size=n_pub)
+        orf = [O._rel_bits(o.release(x, oh[a])) for x, a in rel]
+        oi = [o.publish(oh[a], seq + k) for k, a in enumerate(pubs)]
+        gi, gf, grf = g.process_batch([0, len(rel)], [x for x, _ in rel], [gh[a] for _, a in rel], [0, len(pubs)],
+                                      [gh[a] for a in pubs], seq_base=seq)
+        seq += len(pubs)
+        assert grf.tolist() == orf
+        assert [(int(x), int(f)) for x, f in zip(gi, gf)] == oi
+        live += [(int(x), int(a)) for x, a in zip(gi, pubs) if x >= 0]
+
+    for _ in range(20):
+        call(400, 150)
+    g.update_cluster(2)  # watched pairs on the on-chip engine ...
+    o.update_cluster(2)
+    for _ in range(5):
+        call(300, 150)
+    big = [Action("nsx", "nsx/p/big", "0.0.1", 256, 10_000), Action("nsx", "nsx/p/big2", "0.0.1", 128, 70_000)]
+    gh2, _ = g.register_actions(big)  # ... carried into the large engine here
+    oh += [o.register_action(a.namespace, a.path, len(oh) + k, a.mem_mb, a.max_concurrent) for k, a in enumerate(big)]
+    gh = np.concatenate([gh, gh2])
+    for _ in range(10):
+        call(400, 200)
+    n1 = 30_000  # the pool grows past owgs_limits (the large engine already holds the state)
+    ids, mem = np.arange(n1, dtype=np.int32), np.full(n1, 2048 * MB, np.int64)
+    g.update_invokers_arrays(ids, mem, np.zeros(n1, np.uint8))
+    o.update_invokers(ids, mem, np.zeros(n1, np.uint8))
+    for _ in range(10):
+        call(400, 200)
+    assert np.array_equal(g.permits(), o.permits())
