@@ -2973,9 +2973,12 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
 #endif
                             if (kind == K_FALLBACK && maxc > 1) {
                                 // backward move: the next chunk's gathered cursors predate it (see `stale`), and
-                                // the store must reach L2 before the chunk after that gathers again
+                                // the store must reach L2 before the chunk after that gathers again.  The gather is
+                                // this workgroup's I/O wave reading L2 directly (sc1, same XCD), so the store's
+                                // completion is enough: vmcnt(0) here, not an agent-scope fence -- that one writes
+                                // back every dirty line of the XCD's L2 (buffer_wbl2), partial output lines included
                                 sc[SC_CBWD] = g + 1;
-                                __threadfence();
+                                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                             }
                         }
                     }

@@ -39,9 +39,10 @@ for s in ${STEPS:-tests}; do
         rc=$?; tail -1 $O/cfgs.jsonl | cut -c1-160; [ $rc -eq 0 ] || { tail -20 $O/cfgs.err; stop "cfg $c" $rc; }
       done ;;
     pmc)
-      for c in ${PMCCFGS:-"" "--cluster-size 8" "--config c2" "--config c4"}; do
+      IFS=',' read -ra CF <<< "${PMCCFGS:-,--cluster-size 8,--config c2,--config c4}"  # (comma-separated; empty = headline)
+      for c in "${CF[@]}"; do
         f=$O/pmc_traffic$(echo $c | tr -d ' -').log
-        timeout -k 10 400 python3 tools/pmc_traffic.py $c > $f 2>&1
+        timeout -k 10 400 python3 tools/pmc_traffic.py ${c} > $f 2>&1
         rc=$?; tail -1 $f | cut -c1-200; [ $rc -eq 0 ] || stop "pmc $c" $rc
       done
       cp pmc_traffic.json $O/pmc_traffic.json ;;
