@@ -52,12 +52,29 @@ __device__ __forceinline__ uint32_t sq_hash(uint32_t inv, uint32_t slot) {
     k ^= k >> 16;
     return k;
 }
+// The mutable state (permits, the map) is read past the CU's L1 (agent-scope relaxed loads: `sc1`, L2): the map's
+// key words are claimed by atomics, which L2 performs, so an L1 copy of such a line could be stale.  Stores are
+// write-through; `mem_done` waits for them (vmcnt covers stores) before a later load of the wave may need them -- this
+// replaces an agent-scope fence per decision, which also wrote back and invalidated the caches (~3.5 us each).
+__device__ __forceinline__ int ld_i(const int32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ uint32_t ld_u(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint4 ld_e(const uint4* p) {
+    const uint32_t* q = (const uint32_t*)p;
+    return make_uint4(ld_u(q), ld_u(q + 1), ld_u(q + 2), ld_u(q + 3));
+}
+__device__ __forceinline__ void mem_done() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
 // the map: entry {invoker + 1 (0 empty, ~0 deleted), slot, free slots c, operationCount}; index of (inv, slot) or -1
 __device__ __forceinline__ int sq_find(const OwgsSeqArgs& S, int inv, int slot, uint4* e) {
     const uint32_t m = (uint32_t)S.map_cap - 1u;
     uint32_t h = sq_hash((uint32_t)inv, (uint32_t)slot) & m;
     for (int p = 0; p < S.map_cap; ++p) {
-        const uint4 v = S.map[h];
+        const uint4 v = ld_e(&S.map[h]);
         if (v.x == 0u) return -1;
         if (v.x == (uint32_t)inv + 1u && v.y == (uint32_t)slot) {
             *e = v;
@@ -72,7 +89,7 @@ __device__ __forceinline__ int sq_insert(const OwgsSeqArgs& S, int inv, int slot
     const uint32_t m = (uint32_t)S.map_cap - 1u;
     uint32_t h = sq_hash((uint32_t)inv, (uint32_t)slot) & m;
     for (int p = 0; p < S.map_cap;) {
-        const uint32_t k = S.map[h].x;
+        const uint32_t k = ld_u(&S.map[h].x);
         if (k == 0u || k == 0xFFFFFFFFu) {
             if (atomicCAS(&S.map[h].x, k, (uint32_t)inv + 1u) == k) {
                 S.map[h].y = (uint32_t)slot;
@@ -114,7 +131,6 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
         }
     }
     __syncthreads();
-    auto usable = [&](int x) -> bool { return x >= 0 && x < S.n_ids && ((S.usable[x >> 5] >> (x & 31)) & 1u); };
     auto usable_before = [&](int x) -> int {
         if (x <= 0) return 0;
         const int w = x >> 5, b = x & 31;
@@ -136,6 +152,9 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
     };
     const int hm = usable_before(S.nm), hb = usable_before(S.n_ids) - usable_before(S.n_ids - S.nb);
     int err = 0;
+    // an upper bound of the map's non-empty entries (live + deleted) for the growth check: the count at launch plus
+    // every insert of this launch (an insert that reuses a deleted entry counts too)
+    long long filled = ld_i(S.map_filled);
     int r = S.resume ? S.state[1] : 0, ph = S.resume ? S.state[2] : 0;
     long long j = S.resume ? ((long long)(uint32_t)S.state[3] | ((long long)S.state[4] << 32)) : -1;
     bool stop = false;
@@ -144,29 +163,39 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
         if (ph == 0) {
             const long long re = S.rel_off[r + 1];
             if (j < 0) j = S.rel_off[r];
-            for (; j < re; ++j) {
-                if (lane == 0) {
-                    int inv, a;
+            // in groups of 64: lane q gathers release j0 + q's invoker and action fields, lane 0 applies them in order
+            while (j < re) {
+                const long long j0 = j;
+                const int nq = (int)min(64ll, re - j0);
+                int g_inv = -1, g_a = 0, g_mem = 0, g_maxc = 0, g_slot = 0;
+                if (lane < nq) {
                     if (S.rel_aid) {
-                        const long long aid = S.rel_aid[j];
-                        inv = S.dec_inv[aid];
-                        a = S.dec_act[aid];
+                        const long long aid = S.rel_aid[j0 + lane];
+                        g_inv = ld_i(&S.dec_inv[aid]);  // (decided by this launch too: past L1)
+                        g_a = S.dec_act[aid];
                     } else {
-                        inv = S.rel_inv[j];
-                        a = S.rel_act[j];
+                        g_inv = S.rel_inv[j0 + lane];
+                        g_a = S.rel_act[j0 + lane];
                     }
-                    uint8_t f = 0;
-                    if (inv < 0) {
-                        f = OWGS_REL_NOENTRY_BIT;  // no ActivationEntry (CLB:278-279)
-                    } else if (inv < S.n_slots) {  // invokerSlots.lift (SCPB:329)
-                        const int mem = S.act_mem[a], maxc = S.act_maxc[a];
+                }
+                if (lane < nq && g_inv >= 0 && g_inv < S.n_slots) {
+                    g_mem = S.act_mem[g_a];
+                    g_maxc = S.act_maxc[g_a];
+                    g_slot = S.act_slot[g_a];
+                }
+                int my_f = 0;
+                for (int q = 0; q < nq; ++q) {
+                    const int inv = __builtin_amdgcn_readlane(g_inv, q);
+                    int f = 0;
+                    if (inv >= 0 && inv < S.n_slots && lane == 0) {  // invokerSlots.lift (SCPB:329)
+                        const int mem = __builtin_amdgcn_readlane(g_mem, q), maxc = __builtin_amdgcn_readlane(g_maxc, q);
                         if (maxc <= 1) {
-                            const int p = S.permits[inv], nx = jadd(p, mem);
+                            const int p = ld_i(&S.permits[inv]), nx = jadd(p, mem);
                             if (nx < p) f = OWGS_REL_OVERFLOW_BIT;  // FS:48-50
                             else S.permits[inv] = nx;
                         } else {
                             uint4 e;
-                            const int ix = sq_find(S, inv, S.act_slot[a], &e);
+                            const int ix = sq_find(S, inv, __builtin_amdgcn_readlane(g_slot, q), &e);
                             if (ix < 0) {
                                 f = OWGS_REL_NOSUCH_BIT;  // NoSuchElementException (NS:103)
                             } else {  // RS.release(1, true) (RS:99-108, 42-56)
@@ -177,7 +206,7 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                                 const int c1 = mrel ? jsub(n2, maxc) : n2;
                                 bool removed = arel;
                                 if (mrel) {
-                                    const int p = S.permits[inv], nx = jadd(p, mem);
+                                    const int p = ld_i(&S.permits[inv]), nx = jadd(p, mem);
                                     if (nx < p) {
                                         f = OWGS_REL_OVERFLOW_BIT;  // the Error after the RS update: no removal
                                         removed = false;
@@ -193,137 +222,185 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                             }
                         }
                     }
-                    if (S.rel_flags) S.rel_flags[j] = f;
+                    f = __builtin_amdgcn_readlane(f, 0) | (inv < 0 ? OWGS_REL_NOENTRY_BIT : 0);  // (CLB:278-279)
+                    if (lane == q) my_f = f;
+                    // (lane 0 alone reads and writes the state here: its own accesses stay in program order)
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 }
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                if (S.rel_flags && lane < nq) S.rel_flags[j0 + lane] = (uint8_t)my_f;
+                j = j0 + nq;
             }
+            mem_done();  // (the publishes' walks read these permits and entries from every lane)
             ph = 1;
             j = -1;
         }
         // ---------------------------------------------------------------- publishes (one decision at a time)
+        // in groups of 64: lane q gathers decision j0 + q's action fields up front (one round trip per group, not
+        // two per decision) and keeps its outputs until the group ends
         const long long pe = S.pub_off[r + 1];
         if (j < 0) j = S.pub_off[r];
-        for (; j < pe; ++j) {
-            const int a = S.pub_act[j];
-            const int mem = S.act_mem[a], maxc = S.act_maxc[a], slot = S.act_slot[a], hash = S.act_hash[a];
-            const int pool = S.act_bb[a] ? 1 : 0;
-            const int n = pool ? S.nb : S.nm, base = pool ? S.n_ids - S.nb : 0;
-            const int k = pool ? S.n_bsteps : S.n_msteps;
-            const u64 seq = S.seq ? S.seq[j] : S.seq_base + (u64)j;
-            int out = OWGS_NONE_V, fl = 0;
-            // a walk can leave up to n entries (every usable step it passes): grow the map first if that could cross
-            // 3/4 of it (the host resumes here)
-            if (maxc > 1 && 4 * ((long long)*S.map_filled + n + 2) > 3 * (long long)S.map_cap) {
-                stop = true;
-                break;
+        while (j < pe && !stop) {
+            const long long j0 = j;
+            const int nq = (int)min(64ll, pe - j0);
+            int g_a = 0, g_mem = 0, g_maxc = 0, g_slot = 0, g_hash = 0, g_bb = 0;
+            u64 g_seq = 0;
+            if (lane < nq) {
+                g_a = S.pub_act[j0 + lane];
+                g_seq = S.seq ? S.seq[j0 + lane] : S.seq_base + (u64)(j0 + lane);
             }
-            if (n <= 0) {
-                out = OWGS_NONE_V;  // no invokers in the pool: None (SCPB:288-290)
-            } else if (hash % n < 0 || hash % k < 0) {
-                out = OWGS_THROW_V;  // Int.MinValue hash: stepSizes / invokers index out of bounds (SCPB:266-268)
-            } else {
-                const long long home = hash % n, step = (long long)(pool ? S.bsteps : S.msteps)[hash % k] % n;
-                int t = -1, ts = 0;
-                // probes s = s0 + 64 u + lane, u = 0..3, in walk order (u, then lane)
-                for (long long s0 = 0; s0 < (long long)n + 2 && t < 0; s0 += 256) {
-                    bool ok[4], tried[4];
-                    int id[4];
+            if (lane < nq) {
+                g_mem = S.act_mem[g_a];
+                g_maxc = S.act_maxc[g_a];
+                g_slot = S.act_slot[g_a];
+                g_hash = S.act_hash[g_a];
+                g_bb = S.act_bb[g_a];
+            }
+            int my_out = OWGS_NONE_V, my_fl = 0;
+            int q = 0;
+            for (; q < nq; ++q) {
+                const int mem = __builtin_amdgcn_readlane(g_mem, q), maxc = __builtin_amdgcn_readlane(g_maxc, q);
+                const int slot = __builtin_amdgcn_readlane(g_slot, q), hash = __builtin_amdgcn_readlane(g_hash, q);
+                const int pool = __builtin_amdgcn_readlane(g_bb, q) ? 1 : 0;
+                const u64 seq = ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(g_seq >> 32), q) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g_seq, q);
+                const int n = pool ? S.nb : S.nm, base = pool ? S.n_ids - S.nb : 0;
+                const int k = pool ? S.n_bsteps : S.n_msteps;
+                int out = OWGS_NONE_V, fl = 0;
+                // a walk can leave up to n entries (every usable step it passes): grow the map first if that could
+                // cross 3/4 of it (the host resumes here)
+                if (maxc > 1 && 4 * (filled + n + 2) > 3 * (long long)S.map_cap) {
+                    stop = true;
+                    break;
+                }
+                if (n <= 0) {
+                    out = OWGS_NONE_V;  // no invokers in the pool: None (SCPB:288-290)
+                } else if (hash % n < 0 || hash % k < 0) {
+                    out = OWGS_THROW_V;  // Int.MinValue hash: stepSizes / invokers index out of bounds (SCPB:266-268)
+                } else {
+                    const long long home = hash % n, step = (long long)(pool ? S.bsteps : S.msteps)[hash % k] % n;
+                    int t = -1;
+                    // probes s = s0 + 64 u + lane, u = 0..3, in walk order (u, then lane); position (home + s step) mod
+                    // n kept incrementally (one 64-bit remainder per decision, then 32-bit adds of 64 steps mod n)
+                    const uint32_t un = (uint32_t)n, d64 = (uint32_t)((64ll * step) % n);
+                    uint32_t pos = (uint32_t)((home + (long long)lane * step) % n);
+                    auto adv = [&](uint32_t x) -> uint32_t {
+                        const uint32_t y = x + d64;  // (both < n < 2^31: no wrap)
+                        return y >= un ? y - un : y;
+                    };
+                    for (long long s0 = 0; s0 < (long long)n + 2 && t < 0; s0 += 256) {
+                        bool ok[4], tried[4];
+                        int id[4];
+                        int pvs[4];
+                        uint32_t uw[4];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const long long s = s0 + 64 * u + lane;
-                        id[u] = base + (int)((home + (s % n) * step) % n);
-                        tried[u] = s < (long long)n + 2 && usable(id[u]);
-                        ok[u] = false;
-                        if (tried[u]) {
-                            const int pv = S.permits[id[u]];
-                            if (maxc <= 1) {
-                                ok[u] = pv >= mem;  // tryAcquire (FS:63-71)
-                            } else {
-                                uint4 e;
-                                const int ix = sq_find(S, id[u], slot, &e);
-                                ok[u] = (ix >= 0 && (int)e.z >= 1) || pv >= mem;  // a free slot, or memory (NS:57-82)
-                            }
+                        for (int u = 0; u < 4; ++u) {  // every position is inside the pool: all loads at once
+                            id[u] = base + (int)pos;
+                            pos = adv(pos);
+                            uw[u] = S.usable[id[u] >> 5];
+                            pvs[u] = id[u] < S.n_slots ? ld_i(&S.permits[id[u]]) : 0;
                         }
-                    }
-                    int uf = 4, lf = 64;
-#pragma unroll
-                    for (int u = 3; u >= 0; --u) {
-                        const u64 m = __ballot(ok[u]);
-                        if (m) {
-                            uf = u;
-                            lf = ffs64(m);
-                        }
-                    }
-                    if (maxc > 1) {
-                        // the tries that failed before the first success leave empty entries (getOrElseUpdate,
-                        // NS:61-62); steps n and n + 1 repeat positions 0 and 1, whose entries the first pass made
 #pragma unroll
                         for (int u = 0; u < 4; ++u) {
                             const long long s = s0 + 64 * u + lane;
-                            const bool before = u < uf || (u == uf && lane < lf);
-                            if (tried[u] && !ok[u] && before && s < n) {
+                            tried[u] = s < (long long)n + 2 && ((uw[u] >> (id[u] & 31)) & 1u) && id[u] < S.n_slots;
+                            ok[u] = false;
+                            if (tried[u]) {
+                                const int pv = pvs[u];
+                                if (maxc <= 1) {
+                                    ok[u] = pv >= mem;  // tryAcquire (FS:63-71)
+                                } else {
+                                    uint4 e;
+                                    const int ix = sq_find(S, id[u], slot, &e);
+                                    ok[u] = (ix >= 0 && (int)e.z >= 1) || pv >= mem;  // a free slot, or memory (NS:57-82)
+                                }
+                            }
+                        }
+                        int uf = 4, lf = 64;
+#pragma unroll
+                        for (int u = 3; u >= 0; --u) {
+                            const u64 m = __ballot(ok[u]);
+                            if (m) {
+                                uf = u;
+                                lf = ffs64(m);
+                            }
+                        }
+                        if (maxc > 1) {
+                            // the tries that failed before the first success leave empty entries (getOrElseUpdate,
+                            // NS:61-62); steps n and n + 1 repeat positions 0 and 1, whose entries the first pass made
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const long long s = s0 + 64 * u + lane;
+                                const bool before = u < uf || (u == uf && lane < lf);
+                                bool ins = false;
+                                if (tried[u] && !ok[u] && before && s < n) {
+                                    uint4 e;
+                                    ins = sq_find(S, id[u], slot, &e) < 0;
+                                    if (ins && sq_insert(S, id[u], slot, 0, 0) < 0) err = 1;
+                                }
+                                filled += __popcll(__ballot(ins));
+                            }
+                            mem_done();
+                        }
+                        if (uf < 4) t = __shfl(uf == 0 ? id[0] : uf == 1 ? id[1] : uf == 2 ? id[2] : id[3], lf, 64);
+                    }
+                    if (t < 0) {  // n + 2 failed probes: a random healthy invoker, forced (SCPB:417-424)
+                        const int H = pool ? hb : hm;
+                        if (H > 0) {
+                            const int kk = (int)rng_index(S.rng_seed, seq, (uint32_t)H);
+                            t = select_usable(base, kk);
+                            if (t < 0) err = 1;
+                            fl = 1;
+                        }
+                    }
+                    if (t >= 0) {
+                        out = t;
+                        if (lane == 0) {
+                            if (maxc <= 1) {
+                                // tryAcquire succeeded / forceAcquire (FS:107-110)
+                                S.permits[t] = jsub(ld_i(&S.permits[t]), mem);
+                            } else {
                                 uint4 e;
-                                if (sq_find(S, id[u], slot, &e) < 0 && sq_insert(S, id[u], slot, 0, 0) < 0) err = 1;
+                                int ix = sq_find(S, t, slot, &e);
+                                if (ix < 0) {  // getOrElseUpdate (NS:61-62)
+                                    ++filled;  // (lane 0's copy; broadcast below)
+                                    ix = sq_insert(S, t, slot, 0, 0);
+                                    e = make_uint4(0u, 0u, 0u, 0u);
+                                    if (ix < 0) err = 1;
+                                }
+                                int c = (int)e.z, ops = (int)e.w;
+                                if (c - 1 >= 0) {  // RS.tryAcquire(1) (RS:62-70)
+                                    c = c - 1;
+                                    ops = jadd(ops, 1);
+                                } else {  // the memory (tried above, or forced): RS.release(maxConcurrent - 1, false)
+                                    S.permits[t] = jsub(ld_i(&S.permits[t]), mem);
+                                    ops = jadd(ops, 1);
+                                    const int n2 = jadd(c, maxc - 1);
+                                    c = n2 % maxc == 0 ? jsub(n2, maxc) : n2;
+                                }
+                                if (ix >= 0) {
+                                    S.map[ix].z = (uint32_t)c;
+                                    S.map[ix].w = (uint32_t)ops;
+                                }
                             }
                         }
-                        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-                    }
-                    if (uf < 4) {
-                        t = __shfl(uf == 0 ? id[0] : uf == 1 ? id[1] : uf == 2 ? id[2] : id[3], lf, 64);
-                        ts = (int)(s0 + 64 * uf + lf);
+                    } else {
+                        out = OWGS_NONE_V;  // no healthy invoker: None (SCPB:419-420)
                     }
                 }
-                (void)ts;
-                bool force = false;
-                if (t < 0) {  // n + 2 failed probes: a random healthy invoker, forced (SCPB:417-424)
-                    const int H = pool ? hb : hm;
-                    if (H > 0) {
-                        const int kk = (int)rng_index(S.rng_seed, seq, (uint32_t)H);
-                        t = select_usable(base, kk);
-                        if (t < 0) err = 1;
-                        force = true;
-                        fl = 1;
-                    }
+                if (lane == q) {
+                    my_out = out;
+                    my_fl = fl;
                 }
-                if (t >= 0) {
-                    out = t;
-                    if (lane == 0) {
-                        if (maxc <= 1) {
-                            S.permits[t] = jsub(S.permits[t], mem);  // tryAcquire succeeded / forceAcquire (FS:107-110)
-                        } else {
-                            uint4 e;
-                            int ix = sq_find(S, t, slot, &e);
-                            if (ix < 0) {  // getOrElseUpdate (NS:61-62)
-                                ix = sq_insert(S, t, slot, 0, 0);
-                                e = make_uint4(0u, 0u, 0u, 0u);
-                                if (ix < 0) err = 1;
-                            }
-                            int c = (int)e.z, ops = (int)e.w;
-                            if (c - 1 >= 0) {  // RS.tryAcquire(1) (RS:62-70)
-                                c = c - 1;
-                                ops = jadd(ops, 1);
-                            } else {  // the memory (tried above, or forced): RS.release(maxConcurrent - 1, false)
-                                S.permits[t] = jsub(S.permits[t], mem);
-                                ops = jadd(ops, 1);
-                                const int n2 = jadd(c, maxc - 1);
-                                c = n2 % maxc == 0 ? jsub(n2, maxc) : n2;
-                            }
-                            if (ix >= 0) {
-                                S.map[ix].z = (uint32_t)c;
-                                S.map[ix].w = (uint32_t)ops;
-                            }
-                        }
-                    }
-                    (void)force;
-                } else {
-                    out = OWGS_NONE_V;  // no healthy invoker: None (SCPB:419-420)
-                }
+                filled = ((long long)__builtin_amdgcn_readlane((int)(filled >> 32), 0) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)filled, 0);
+                mem_done();  // (lane 0's permit and entry stores, before the next decision reads them)
             }
-            if (lane == 0) {
-                S.out_inv[j] = out;
-                S.out_flags[j] = (uint8_t)fl;
+            if (lane < q) {  // the decided part of the group (all of it unless the map must grow first)
+                S.out_inv[j0 + lane] = my_out;
+                S.out_flags[j0 + lane] = (uint8_t)my_fl;
             }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+            mem_done();  // (a later run's releases read these decisions)
+            j = j0 + q;
         }
         if (stop) break;
     }

@@ -100,6 +100,9 @@ for l in d['legs']:
     p99)  # per-call counters of the 512-job shim leg: the slowest 1 % against the median
       timeout -k 10 300 python tools/shim_p99.py > $O/p99.json 2> $O/p99.err
       rc=$?; cut -c1-600 $O/p99.json; [ $rc -eq 0 ] || { tail -5 $O/p99.err; stop p99 $rc; } ;;
+    large)  # large-state engine rate (pools beyond the on-chip image) against the one-core oracle
+      timeout -k 10 400 python -u tools/time_large.py ${LARGEN:-40000 25000} > $O/large.jsonl 2> $O/large.err
+      rc=$?; cut -c1-400 $O/large.jsonl; [ $rc -eq 0 ] || { tail -5 $O/large.err; stop large $rc; } ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
