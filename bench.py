@@ -199,6 +199,9 @@ def cpu_baseline(args, w0, n_ctl, shard0):
         nt, dtt = _oracle_replay(ws, reps=1)
         out["parallel"] = {"value": nt / dtt, "unit": "decisions/s", "cores": T,
                            "sample": f"{T} threads, one shard stream each, {dtt:.2f} s wall"}
+        # (also in the sample text, which every reader of the line keeps: the whole host against the one GPU)
+        out["sample"] += (f"; {T} host threads replaying {T} independent shard streams: {nt / dtt / 1e6:.1f} M "
+                          f"decisions/s aggregate")
     return out
 
 

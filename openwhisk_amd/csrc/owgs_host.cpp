@@ -325,6 +325,8 @@ struct owgs_ctx {
     DevBuf<uint4> q_map;
     int32_t q_cap = 0;
     DevBuf<int32_t> q_filled, q_state, q_look;
+    DevBuf<uint4> q_cur;   // walk cursors of the large-state engine, per action {generation, step, position, 0}
+    uint32_t q_gen = 1;    // the next call's first generation: cursors never outlive the call that wrote them
     DevBuf<uint32_t> d_hwords;
     const uint32_t* grp_hwords = nullptr;
     int32_t grp_hstride = 0;
@@ -1451,6 +1453,9 @@ static OwgsSeqArgs seq_args(owgs_ctx* c) {
     S.act_maxc = c->d_act_maxc.p;
     S.act_slot = c->d_act_slot.p;
     S.act_bb = c->d_act_bb.p;
+    S.cur = c->q_cur.p;
+    S.n_actions = c->q_cur.p ? (int32_t)c->a_mem.size() : 0;
+    S.gen0 = c->q_gen;
     S.map = c->q_map.p;
     S.map_cap = c->q_cap;
     S.map_filled = c->q_filled.p;
@@ -1520,21 +1525,44 @@ static int seq_migrate(owgs_ctx* c) {
 // runs through the large-state engine (S: its runs, releases, publishes, outputs); resumes after map growth
 static int seq_run(owgs_ctx* c, const OwgsSeqArgs& S0, hipStream_t s) {
     const int64_t room = 2 * ((int64_t)std::max(c->nm, c->nb) + 2) + 4096;
+    // walk cursors: one per action, tagged with a generation that no earlier call used (state changes between calls
+    // -- health, cluster size, restores -- need no invalidation); all zero again before the counter could wrap
+    const size_t na = c->a_mem.size();
+    if (na > 0 && c->q_cur.n < na) {
+        DevBuf<uint4> nc;
+        HIPCHK(c, nc.reserve(na + na / 2 + 64));
+        HIPCHK(c, hipMemsetAsync(nc.p, 0, nc.n * sizeof(uint4), s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        c->q_cur.release();
+        c->q_cur = nc;
+        nc.p = nullptr;
+        nc.n = 0;
+    }
+    if (c->q_gen > 0xF0000000u) {
+        if (c->q_cur.p) HIPCHK(c, hipMemsetAsync(c->q_cur.p, 0, c->q_cur.n * sizeof(uint4), s));
+        c->q_gen = 1;
+    }
+    uint32_t gen = c->q_gen;
     for (int resume = 0;; resume = 1) {
         const int rc = seq_reserve(c, room, s);
         if (rc) return rc;
         OwgsSeqArgs S = S0;
+        S.cur = na > 0 ? c->q_cur.p : nullptr;
+        S.n_actions = (int32_t)na;
+        S.gen0 = gen;
         S.map = c->q_map.p;
         S.map_cap = c->q_cap;
         S.map_filled = c->q_filled.p;
         S.state = c->q_state.p;
         S.resume = resume;
         HIPCHK(c, owgs_launch_seq(&S, s));
-        int32_t st[5] = {0, 0, 0, 0, 0};
+        int32_t st[6] = {0, 0, 0, 0, 0, 0};
         HIPCHK(c, hipMemcpyAsync(st, c->q_state.p, sizeof(st), hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
+        gen = (uint32_t)st[5];  // (a resumed launch continues the generation it stopped in)
         if (st[0] == 0) break;
     }
+    c->q_gen = gen + 1u;
     return check_err_word(c);
 }
 
@@ -1718,6 +1746,7 @@ void owgs_destroy(owgs_ctx* c) {
     c->q_map.release();
     c->q_filled.release();
     c->q_state.release();
+    c->q_cur.release();
     c->q_look.release();
     c->d_act_cok.release();
     c->d_act_meta.release();
@@ -3473,7 +3502,6 @@ int owgs_activations_live(owgs_ctx* c, int64_t* live) {
 int owgs_track_activations(owgs_ctx* c, int32_t n, const char* aid32, const int32_t* action, const int32_t* ticket,
                            int32_t* out_ticket, uint8_t* out_existed) {
     if (!c || n < 0 || (n > 0 && (!aid32 || !action || !ticket || !out_ticket || !out_existed))) return OWGS_EINVAL;
-    OWGS_NOT_LARGE(c);
     if (n == 0) return OWGS_OK;
     if (!registered(c, n, action)) return c->fail(OWGS_ENOENT, "unknown action");
     // ActivationId.asString is 32 chars of [0-9a-f]; reject a malformed batch before any entry is created
@@ -3554,6 +3582,27 @@ static int ack_complete(owgs_ctx* c, int32_t n, uint8_t* d_kind, int32_t* d_tick
     a.out_ticket = d_ticket;
     a.counters = c->k_cnt.p;
     HIPCHK(c, owgs_launch_ack_complete(&T, &a, st));
+    if (c->large) {  // the large-state engine applies the records in message order (owgs_seq.hip)
+        const int64_t offs[4] = {0, (int64_t)n, 0, 0};
+        HIPCHK(c, upload(c->g_off, offs, 4, st));
+        OwgsSeqArgs S = seq_args(c);
+        S.n_runs = 1;
+        S.rel_off = c->g_off.p;
+        S.pub_off = c->g_off.p + 2;
+        S.rel_inv = c->k_r0.p;
+        S.rel_mem = c->k_r1.p;
+        S.rel_maxc = c->k_r2.p;
+        S.rel_slot = c->k_r3.p;
+        S.rel_flags = c->d_rflags.p;
+        int rs = seq_run(c, S, st);
+        if (rs) return rs;
+        HIPCHK(c, owgs_launch_ack_flags(n, c->k_info.p, c->d_rflags.p, d_kind, d_flags, st));
+        unsigned long long cnt[2];
+        HIPCHK(c, hipMemcpyAsync(cnt, c->k_cnt.p, 16, hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        c->t_live -= (long long)cnt[1];
+        return check_err_word(c);
+    }
     OwgsReleaseArgs R{};
     R.permits = c->d_permits.p;
     R.n_slots = c->n_slots;
@@ -3589,7 +3638,6 @@ int owgs_process_acks_device(owgs_ctx* c, int32_t n, const uint8_t* bytes, const
                              int32_t* out_invoker, int32_t* out_ticket, uint8_t* out_flags, void* stream) {
     if (!c || n < 0 || (n > 0 && (!bytes || !off || !out_kind || !out_invoker || !out_ticket || !out_flags)))
         return OWGS_EINVAL;
-    OWGS_NOT_LARGE(c);
     if (n == 0) return OWGS_OK;
     OWGS_ENTER(c);
     {
@@ -3619,7 +3667,6 @@ int owgs_process_acks(owgs_ctx* c, int32_t n, const char* bytes, const int64_t* 
                       int32_t* out_invoker, int32_t* out_ticket, uint8_t* out_flags) {
     if (!c || n < 0 || (n > 0 && (!bytes || !off || !out_kind || !out_invoker || !out_ticket || !out_flags)))
         return OWGS_EINVAL;
-    OWGS_NOT_LARGE(c);
     if (n == 0) return OWGS_OK;
     for (int32_t i = 0; i < n; ++i)
         if (off[i + 1] < off[i] || off[i] < 0) return c->fail(OWGS_EINVAL, "offsets");
@@ -3653,7 +3700,6 @@ int owgs_complete_activations(owgs_ctx* c, int32_t n, const char* aid32, const i
                               uint8_t* out_kind, int32_t* out_ticket, uint8_t* out_flags) {
     if (!c || n < 0 || (n > 0 && (!aid32 || !invoker || !flags || !out_kind || !out_ticket || !out_flags)))
         return OWGS_EINVAL;
-    OWGS_NOT_LARGE(c);
     if (n == 0) return OWGS_OK;
     OWGS_ENTER(c);
     {

@@ -413,6 +413,10 @@ struct OwgsSeqArgs {
     const int32_t* act_maxc;
     const int32_t* act_slot;
     const uint8_t* act_bb;
+    uint4* cur;                   // [n_actions] walk cursor {generation, first step that may still fit, its pool
+                                  //   position, 0} (maxConcurrent == 1 actions)
+    int32_t n_actions;
+    uint32_t gen0;                // this call's first cursor generation (release runs count up from it)
     uint4* map;                   // [map_cap] {invoker + 1 (0 empty, ~0 deleted), slot, free slots, operationCount}
     int32_t map_cap;              // a power of two
     int32_t* map_filled;          // non-empty entries (live + deleted)
@@ -424,6 +428,9 @@ struct OwgsSeqArgs {
     const int32_t* dec_act;
     const int32_t* rel_inv;       // explicit releases (rel_aid null): invoker and action handle
     const int32_t* rel_act;
+    const int32_t* rel_mem;       // or, for the completion path's records (rel_act null): memory, maxConcurrent and
+    const int32_t* rel_maxc;      //   fqn@version key of each release
+    const int32_t* rel_slot;
     uint8_t* rel_flags;           // or null
     const int32_t* pub_act;
     const unsigned long long* seq;  // or null: seq_base + index

@@ -18,7 +18,7 @@
 //     invoker, forced (SCPB:417-424, forceAcquireConcurrent NS:84-91).
 //
 // The map grows without bound like the reference's TrieMap: the kernel stops before an operation that could take the
-// table past 3/4 full, reports where, and the host grows the table and resumes there (owgs_host.cpp seq_run).
+// table past half full, reports where, and the host grows the table and resumes there (owgs_host.cpp seq_run).
 #include <hip/hip_runtime.h>
 
 #include "owgs_internal.h"
@@ -83,6 +83,39 @@ __device__ __forceinline__ int sq_find(const OwgsSeqArgs& S, int inv, int slot, 
         h = (h + 1u) & m;
     }
     return -1;
+}
+// four lookups of one lane at once (the walk's four steps of a round): each probe round issues the loads of every
+// chain still open together, so the round trips overlap instead of adding up
+__device__ __forceinline__ void sq_find4(const OwgsSeqArgs& S, const int* inv, int slot, const bool* go, int* ix,
+                                         uint4* e) {
+    const uint32_t m = (uint32_t)S.map_cap - 1u;
+    uint32_t h[4];
+    bool open[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        h[u] = sq_hash((uint32_t)inv[u], (uint32_t)slot) & m;
+        open[u] = go[u];
+        ix[u] = -1;
+        e[u] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    for (int p = 0; p < S.map_cap && (open[0] || open[1] || open[2] || open[3]); ++p) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = open[u] ? ld_e(&S.map[h[u]]) : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (!open[u]) continue;
+            if (v[u].x == 0u) {
+                open[u] = false;  // absent
+            } else if (v[u].x == (uint32_t)inv[u] + 1u && v[u].y == (uint32_t)slot) {
+                ix[u] = (int)h[u];
+                e[u] = v[u];
+                open[u] = false;
+            } else {
+                h[u] = (h[u] + 1u) & m;
+            }
+        }
+    }
 }
 // insert (inv, slot) known to be absent (distinct keys may race: the key word is claimed by CAS)
 __device__ __forceinline__ int sq_insert(const OwgsSeqArgs& S, int inv, int slot, int c, int ops) {
@@ -155,6 +188,10 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
     // an upper bound of the map's non-empty entries (live + deleted) for the growth check: the count at launch plus
     // every insert of this launch (an insert that reuses a deleted entry counts too)
     long long filled = ld_i(S.map_filled);
+    // walk cursors of maxConcurrent == 1 actions: valid for one generation; generations count this call's release
+    // runs (only releases raise permits; nothing else changes the state inside a call)
+    uint32_t gen = S.gen0;
+    const float rn_m = S.nm > 0 ? 1.0f / (float)S.nm : 0.f, rn_b = S.nb > 0 ? 1.0f / (float)S.nb : 0.f;
     int r = S.resume ? S.state[1] : 0, ph = S.resume ? S.state[2] : 0;
     long long j = S.resume ? ((long long)(uint32_t)S.state[3] | ((long long)S.state[4] << 32)) : -1;
     bool stop = false;
@@ -163,6 +200,7 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
         if (ph == 0) {
             const long long re = S.rel_off[r + 1];
             if (j < 0) j = S.rel_off[r];
+            if (re > j) ++gen;
             // in groups of 64: lane q gathers release j0 + q's invoker and action fields, lane 0 applies them in order
             while (j < re) {
                 const long long j0 = j;
@@ -175,13 +213,19 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                         g_a = S.dec_act[aid];
                     } else {
                         g_inv = S.rel_inv[j0 + lane];
-                        g_a = S.rel_act[j0 + lane];
+                        if (!S.rel_mem) g_a = S.rel_act[j0 + lane];
                     }
                 }
                 if (lane < nq && g_inv >= 0 && g_inv < S.n_slots) {
-                    g_mem = S.act_mem[g_a];
-                    g_maxc = S.act_maxc[g_a];
-                    g_slot = S.act_slot[g_a];
+                    if (S.rel_mem) {  // the completion path's release records (owgs_acks.hip)
+                        g_mem = S.rel_mem[j0 + lane];
+                        g_maxc = S.rel_maxc[j0 + lane];
+                        g_slot = S.rel_slot[j0 + lane];
+                    } else {
+                        g_mem = S.act_mem[g_a];
+                        g_maxc = S.act_maxc[g_a];
+                        g_slot = S.act_slot[g_a];
+                    }
                 }
                 int my_f = 0;
                 for (int q = 0; q < nq; ++q) {
@@ -255,39 +299,84 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                 g_hash = S.act_hash[g_a];
                 g_bb = S.act_bb[g_a];
             }
+            // home and step size of each decision of the group, one lane each (SCPB:262-268): 0 walk, 1 empty pool,
+            // 2 the Int.MinValue hash's IndexOutOfBounds
+            int g_kind = 1;
+            uint32_t g_home = 0u, g_step = 0u;
+            if (lane < nq) {
+                const int gn = g_bb ? S.nb : S.nm, gk = g_bb ? S.n_bsteps : S.n_msteps;
+                if (gn > 0) {
+                    if (g_hash % gn < 0 || g_hash % gk < 0) {
+                        g_kind = 2;
+                    } else {
+                        g_kind = 0;
+                        g_home = (uint32_t)(g_hash % gn);
+                        g_step = (uint32_t)((g_bb ? S.bsteps : S.msteps)[g_hash % gk] % gn);
+                    }
+                }
+            }
+            // each decision's walk start: its action's cursor of this generation (maxConcurrent == 1 only; steps
+            // before it had no room for the action's memory, and permits only fall inside a run)
+            int g_cs = 0;
+            uint32_t g_cp = g_home;  // (the cursor step's pool position)
+            if (lane < nq && S.cur && g_kind == 0 && g_maxc <= 1 && g_a >= 0 && g_a < S.n_actions) {
+                const uint4 cu = S.cur[g_a];
+                if (cu.x == gen) {
+                    g_cs = (int)cu.y;
+                    g_cp = cu.z;
+                }
+            }
             int my_out = OWGS_NONE_V, my_fl = 0;
             int q = 0;
             for (; q < nq; ++q) {
                 const int mem = __builtin_amdgcn_readlane(g_mem, q), maxc = __builtin_amdgcn_readlane(g_maxc, q);
-                const int slot = __builtin_amdgcn_readlane(g_slot, q), hash = __builtin_amdgcn_readlane(g_hash, q);
+                const int slot = __builtin_amdgcn_readlane(g_slot, q), kind = __builtin_amdgcn_readlane(g_kind, q);
                 const int pool = __builtin_amdgcn_readlane(g_bb, q) ? 1 : 0;
                 const u64 seq = ((u64)(uint32_t)__builtin_amdgcn_readlane((int)(g_seq >> 32), q) << 32) |
                                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g_seq, q);
                 const int n = pool ? S.nb : S.nm, base = pool ? S.n_ids - S.nb : 0;
-                const int k = pool ? S.n_bsteps : S.n_msteps;
                 int out = OWGS_NONE_V, fl = 0;
                 // a walk can leave up to n entries (every usable step it passes): grow the map first if that could
-                // cross 3/4 of it (the host resumes here)
-                if (maxc > 1 && 4 * (filled + n + 2) > 3 * (long long)S.map_cap) {
+                // cross half of it (the host resumes here)
+                if (maxc > 1 && 2 * (filled + n + 2) > (long long)S.map_cap) {
                     stop = true;
                     break;
                 }
-                if (n <= 0) {
+                if (kind == 1) {
                     out = OWGS_NONE_V;  // no invokers in the pool: None (SCPB:288-290)
-                } else if (hash % n < 0 || hash % k < 0) {
+                } else if (kind == 2) {
                     out = OWGS_THROW_V;  // Int.MinValue hash: stepSizes / invokers index out of bounds (SCPB:266-268)
                 } else {
-                    const long long home = hash % n, step = (long long)(pool ? S.bsteps : S.msteps)[hash % k] % n;
+                    const uint32_t step = (uint32_t)__builtin_amdgcn_readlane((int)g_step, q);
                     int t = -1;
                     // probes s = s0 + 64 u + lane, u = 0..3, in walk order (u, then lane); position (home + s step) mod
-                    // n kept incrementally (one 64-bit remainder per decision, then 32-bit adds of 64 steps mod n)
-                    const uint32_t un = (uint32_t)n, d64 = (uint32_t)((64ll * step) % n);
-                    uint32_t pos = (uint32_t)((home + (long long)lane * step) % n);
-                    auto adv = [&](uint32_t x) -> uint32_t {
-                        const uint32_t y = x + d64;  // (both < n < 2^31: no wrap)
-                        return y >= un ? y - un : y;
+                    // n: lane l starts at home + l step (a wave scan of step mod n), then advances 64 steps at a time
+                    const uint32_t un = (uint32_t)n;
+                    auto madd = [&](uint32_t x, uint32_t y) -> uint32_t {
+                        const uint32_t z = x + y;  // (both < n < 2^31: no wrap)
+                        return z >= un ? z - un : z;
                     };
-                    for (long long s0 = 0; s0 < (long long)n + 2 && t < 0; s0 += 256) {
+                    // (k step) mod n for k <= 64 without a division: the quotient is below 64, so a float estimate
+                    // (relative error ~2^-23) is off by at most one, and one correction fixes it
+                    const float rn = pool ? rn_b : rn_m;
+                    auto mulmod = [&](uint32_t k) -> uint32_t {
+                        const unsigned long long pr = (unsigned long long)k * step;
+                        const long long qq = (long long)((float)pr * rn);
+                        long long r = (long long)pr - qq * (long long)un;
+                        if (r < 0) r += un;
+                        else if (r >= (long long)un) r -= un;
+                        return (uint32_t)r;
+                    };
+                    const uint32_t d64 = mulmod(64u);
+                    const int sb = __builtin_amdgcn_readlane(g_cs, q);  // (0 unless a cursor of this generation)
+                    const uint32_t start = (uint32_t)__builtin_amdgcn_readlane((int)g_cp, q);  // (home + sb step) mod n
+                    uint32_t pos = madd(start, mulmod((uint32_t)lane));
+                    auto adv = [&](uint32_t x) -> uint32_t { return madd(x, d64); };
+                    long long ts = (long long)n + 2;  // the step taken (n + 2: none), its position and permits
+                    uint32_t tpos = 0u;
+                    int pvt = 0, tix = -1;
+                    uint4 te = make_uint4(0u, 0u, 0u, 0u);
+                    for (long long s0 = sb; s0 < (long long)n + 2 && t < 0; s0 += 256) {
                         bool ok[4], tried[4];
                         int id[4];
                         int pvs[4];
@@ -303,17 +392,14 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                         for (int u = 0; u < 4; ++u) {
                             const long long s = s0 + 64 * u + lane;
                             tried[u] = s < (long long)n + 2 && ((uw[u] >> (id[u] & 31)) & 1u) && id[u] < S.n_slots;
-                            ok[u] = false;
-                            if (tried[u]) {
-                                const int pv = pvs[u];
-                                if (maxc <= 1) {
-                                    ok[u] = pv >= mem;  // tryAcquire (FS:63-71)
-                                } else {
-                                    uint4 e;
-                                    const int ix = sq_find(S, id[u], slot, &e);
-                                    ok[u] = (ix >= 0 && (int)e.z >= 1) || pv >= mem;  // a free slot, or memory (NS:57-82)
-                                }
-                            }
+                            ok[u] = tried[u] && pvs[u] >= mem;  // tryAcquire (FS:63-71), or the memory of a container
+                        }
+                        int ixs[4];
+                        uint4 es[4];
+                        if (maxc > 1) {  // the (invoker, fqn) entry at each tried step: a free slot (NS:57-82)
+                            sq_find4(S, id, slot, tried, ixs, es);
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) ok[u] = ok[u] || (tried[u] && ixs[u] >= 0 && (int)es[u].z >= 1);
                         }
                         int uf = 4, lf = 64;
 #pragma unroll
@@ -332,16 +418,37 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                                 const long long s = s0 + 64 * u + lane;
                                 const bool before = u < uf || (u == uf && lane < lf);
                                 bool ins = false;
-                                if (tried[u] && !ok[u] && before && s < n) {
-                                    uint4 e;
-                                    ins = sq_find(S, id[u], slot, &e) < 0;
-                                    if (ins && sq_insert(S, id[u], slot, 0, 0) < 0) err = 1;
+                                if (tried[u] && !ok[u] && before && s < n && ixs[u] < 0) {  // (absent: looked up above)
+                                    ins = true;
+                                    if (sq_insert(S, id[u], slot, 0, 0) < 0) err = 1;
                                 }
                                 filled += __popcll(__ballot(ins));
                             }
                             mem_done();
                         }
-                        if (uf < 4) t = __shfl(uf == 0 ? id[0] : uf == 1 ? id[1] : uf == 2 ? id[2] : id[3], lf, 64);
+                        if (uf < 4) {  // (uf, lf uniform: lane reads, no LDS round trip)
+                            t = __builtin_amdgcn_readlane(uf == 0 ? id[0] : uf == 1 ? id[1] : uf == 2 ? id[2] : id[3], lf);
+                            pvt = __builtin_amdgcn_readlane(uf == 0 ? pvs[0] : uf == 1 ? pvs[1] : uf == 2 ? pvs[2] : pvs[3], lf);
+                            if (maxc > 1) {  // its entry as the walk found it (the empty entries made since are others)
+                                const int sel_ix = uf == 0 ? ixs[0] : uf == 1 ? ixs[1] : uf == 2 ? ixs[2] : ixs[3];
+                                const uint4 sel_e = uf == 0 ? es[0] : uf == 1 ? es[1] : uf == 2 ? es[2] : es[3];
+                                tix = __builtin_amdgcn_readlane(sel_ix, lf);
+                                te = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)sel_e.x, lf),
+                                                (uint32_t)__builtin_amdgcn_readlane((int)sel_e.y, lf),
+                                                (uint32_t)__builtin_amdgcn_readlane((int)sel_e.z, lf),
+                                                (uint32_t)__builtin_amdgcn_readlane((int)sel_e.w, lf));
+                            }
+                            ts = s0 + 64 * uf + lf;
+                            tpos = (uint32_t)(t - base);
+                        }
+                    }
+                    if (maxc <= 1 && S.cur) {  // the action's cursor: the step it took, or past the walk
+                        const int aq = __builtin_amdgcn_readlane(g_a, q);
+                        if (lane > q && g_a == aq) {
+                            g_cs = (int)ts;
+                            g_cp = tpos;
+                        }
+                        if (lane == 0 && aq >= 0 && aq < S.n_actions) S.cur[aq] = make_uint4(gen, (uint32_t)ts, tpos, 0u);
                     }
                     if (t < 0) {  // n + 2 failed probes: a random healthy invoker, forced (SCPB:417-424)
                         const int H = pool ? hb : hm;
@@ -356,11 +463,12 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                         out = t;
                         if (lane == 0) {
                             if (maxc <= 1) {
-                                // tryAcquire succeeded / forceAcquire (FS:107-110)
-                                S.permits[t] = jsub(ld_i(&S.permits[t]), mem);
+                                // tryAcquire succeeded (the walk read its permits) / forceAcquire (FS:107-110)
+                                S.permits[t] = jsub(fl ? ld_i(&S.permits[t]) : pvt, mem);
                             } else {
-                                uint4 e;
-                                int ix = sq_find(S, t, slot, &e);
+                                uint4 e = te;
+                                int ix = tix;
+                                if (fl) ix = sq_find(S, t, slot, &e);  // (a forced invoker: not looked up by the walk)
                                 if (ix < 0) {  // getOrElseUpdate (NS:61-62)
                                     ++filled;  // (lane 0's copy; broadcast below)
                                     ix = sq_insert(S, t, slot, 0, 0);
@@ -372,7 +480,7 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                                     c = c - 1;
                                     ops = jadd(ops, 1);
                                 } else {  // the memory (tried above, or forced): RS.release(maxConcurrent - 1, false)
-                                    S.permits[t] = jsub(ld_i(&S.permits[t]), mem);
+                                    S.permits[t] = jsub(fl ? ld_i(&S.permits[t]) : pvt, mem);
                                     ops = jadd(ops, 1);
                                     const int n2 = jadd(c, maxc - 1);
                                     c = n2 % maxc == 0 ? jsub(n2, maxc) : n2;
@@ -411,6 +519,7 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
         S.state[2] = 1;
         S.state[3] = (int)(uint32_t)(j & 0xFFFFFFFFll);
         S.state[4] = (int)(j >> 32);
+        S.state[5] = (int)gen;
         if (err) atomicOr(S.err, OWGS_ERR_INTERNAL);
     }
 }

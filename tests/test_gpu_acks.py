@@ -72,12 +72,12 @@ def test_parse_fuzz_matches_oracle(seed):
     check_parse(b, msgs)
 
 
-def _publish_first_batch(w):
+def _publish_first_batch(w, zombies=False):
     """GPU and oracle states after the first batch of w's stream (no releases)."""
     n = int(w.stream.acq_off[1])
     s1 = types.SimpleNamespace(acq_off=np.array([0, n]), act=w.stream.act[:n], rel_off=np.array([0, 0]),
                                rel_aid=np.zeros(0, np.int64), seq_base=w.stream.seq_base)
-    st = O.state_for(w, zombies=False)
+    st = O.state_for(w, zombies=zombies)
     o_inv, _, _ = st.replay(s1)
     b = GpuShardingContainerPoolBalancer(managed_fraction=w.managed_fraction, blackbox_fraction=w.blackbox_fraction,
                                          rng_seed=w.rng_seed)
@@ -89,11 +89,19 @@ def _publish_first_batch(w):
     return b, st, g_inv, w.stream.act[:n]
 
 
-@pytest.mark.parametrize("name,n", [("c4", 60_000), ("headline", 120_000)])
-def test_completion_flow_matches_oracle(name, n):
-    """track (setupActivation) -> raw acks (processAcknowledgement) -> forced timeouts (processCompletion)."""
-    w = W.config(name, n_activations=n)
-    b, st, inv, act = _publish_first_batch(w)
+@pytest.mark.parametrize("name,n,n_inv", [("c4", 60_000, None), ("headline", 120_000, None), ("headline", 300_000, 25_000)])
+def test_completion_flow_matches_oracle(name, n, n_inv):
+    """track (setupActivation) -> raw acks (processAcknowledgement) -> forced timeouts (processCompletion).  The
+    25,000-invoker case is beyond the on-chip image (owgs_limits): its releases go through the large-state engine
+    (owgs_seq.hip), which keeps the reference's empty entries literally (the oracle with zombies=True)."""
+    w = W.config(name, n_activations=n, **({"n_invokers": n_inv} if n_inv else {}))
+    if n_inv:
+        import ctypes as C
+        from openwhisk_amd import _lib
+        mx, ms = C.c_int32(), C.c_int32()
+        _lib.lib().owgs_limits(C.byref(mx), C.byref(ms))
+        assert len(w.inv_ids) > mx.value
+    b, st, inv, act = _publish_first_batch(w, zombies=bool(n_inv))
     b.set_health_tid(H)
     rng = np.random.default_rng(7)
     sched = np.nonzero(inv >= 0)[0]  # publish only tracks scheduled activations (SCPB:290-305)

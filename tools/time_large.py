@@ -21,7 +21,8 @@ sizes = [int(x) for x in sys.argv[1:]] or [40_000]
 n_act = int(os.environ.get("NACT", "200000"))
 for n_inv in sizes:
     mem = int(os.environ.get("INV_MB", "16384"))  # 16 GiB invokers as the headline (1024: the overloaded test pools)
-    w = W.config("headline", n_invokers=n_inv, n_activations=n_act, user_memory_mb=mem)
+    extra = {"conc_frac": float(os.environ["CONC"])} if os.environ.get("CONC") else {}
+    w = W.config("headline", n_invokers=n_inv, n_activations=n_act, user_memory_mb=mem, **extra)
     t = time.perf_counter()
     o_inv, o_fl, _ = O.state_for(w).replay(w.stream)
     cpu_s = time.perf_counter() - t
@@ -38,7 +39,7 @@ for n_inv in sizes:
         exact &= bool(np.array_equal(g_inv, o_inv) and np.array_equal(g_fl, o_fl))
         b.close()
     dt = min(ts)
-    print(json.dumps({"workload": f"headline-shaped, {n_inv} invokers x {mem} MB",
+    print(json.dumps({"workload": f"headline-shaped, {n_inv} invokers x {mem} MB" + (f", conc {extra['conc_frac']}" if extra else ""),
                       "n_invokers": n_inv, "activations": n_act, "releases": int(len(w.stream.rel_aid)),
                       "batches": int(w.stream.n_batches), "gpu_ms": round(dt * 1e3, 2),
                       "gpu_decisions_per_s": n_act / dt, "oracle_1core_ms": round(cpu_s * 1e3, 1),
