@@ -398,7 +398,7 @@ struct OwgsResArgs {
 
 // Large-state engine (owgs_seq.hip): contexts beyond the on-chip image (owgs_limits) or with maxConcurrent beyond
 // OWGS_MAX_CONC.  Permits in HBM, one HBM map keyed by the full (invoker, fqn@version) pair, 32-bit walk positions.
-#define OWGS_SEQ_MAX_WORDS 4096  // usable-bitmap words (131,072 invoker ids; the pool step kernel allows 65,535 each)
+#define OWGS_SEQ_MAX_WORDS 16383  // usable-bitmap words of the large-state engine (524,256 invoker ids; pools up to 524,287 positions, owgs_coprime_max)
 struct OwgsSeqArgs {
     int32_t* permits;
     int32_t n_slots;

@@ -9,8 +9,9 @@
 //                        p !| x: a kept composite would share its smallest prime factor q < c with a kept q, or
 //                        (q | x) fail gcd(c, x) == 1; a prime p passes the pairwise test because every kept value
 //                        below it is 1 or a smaller prime, and passes gcd(p, x) == 1 iff p !| x.  So the kernel
-//                        sieves [2, x] in LDS (byte flags, multiples of every prime <= sqrt(x) marked by all
-//                        threads), keeps c == 1 or (prime, x % c != 0), and compacts in ascending order with a
+//                        sieves [2, x] in LDS (one bit per number, 64 KB: pools up to 524,287 positions; multiples of
+//                        every prime <= sqrt(x) marked by all threads with LDS atomics), keeps c == 1 or (prime,
+//                        x % c != 0), and compacts in ascending order with a
 //                        block scan -- the fold's output order.  The restatement the tests compare against is the
 //                        literal fold (oracle/owsched_oracle.c:owo_pairwise_coprime).
 //   owgs_slots_kernel    permits[i] = toMB(max(MIN_MEMORY, userMemory_i / clusterSize)) for i in [from, n)
@@ -24,11 +25,12 @@
 #include "owgs_internal.h"
 
 #define CP_TPB 1024
-#define CP_MAX 65535  // LDS flag bytes: pools are <= 32767 positions (OWGS_AM_POS_MASK), this leaves headroom
+#define CP_MAX 524287  // LDS flag bits (64 KB): the on-chip engines take pools up to 32767 positions, the large-state
+                      // engine (owgs_seq.hip) the rest
 
 __global__ __launch_bounds__(CP_TPB) void owgs_coprime_kernel(const int32_t* xs, int32_t* out, int32_t out_stride,
                                                               int32_t* counts) {
-    __shared__ uint8_t comp[CP_MAX + 1];
+    __shared__ uint32_t comp[(CP_MAX + 1) / 32];  // bit c: c is composite
     __shared__ int32_t wsum[CP_TPB / 64];
     const int x = xs[blockIdx.x];
     int32_t* o = out + (size_t)blockIdx.x * out_stride;
@@ -37,7 +39,7 @@ __global__ __launch_bounds__(CP_TPB) void owgs_coprime_kernel(const int32_t* xs,
         if (t == 0) counts[blockIdx.x] = 0;
         return;
     }
-    for (int i = t; i <= x; i += CP_TPB) comp[i] = 0;
+    for (int i = t; i <= (x >> 5); i += CP_TPB) comp[i] = 0u;
     __syncthreads();
     // mark composites: every prime p <= sqrt(x) (found by trial division, uniform over the block) strikes its
     // multiples from p * p; concurrent stores write the same value
@@ -49,7 +51,7 @@ __global__ __launch_bounds__(CP_TPB) void owgs_coprime_kernel(const int32_t* xs,
                 break;
             }
         if (!prime) continue;
-        for (int m = p * p + t * p; m <= x; m += CP_TPB * p) comp[m] = 1;
+        for (int m = p * p + t * p; m <= x; m += CP_TPB * p) atomicOr(&comp[m >> 5], 1u << (m & 31));
     }
     __syncthreads();
     // each thread owns a contiguous run of candidates so the block scan yields ascending output positions
@@ -57,7 +59,8 @@ __global__ __launch_bounds__(CP_TPB) void owgs_coprime_kernel(const int32_t* xs,
     const int lo = 1 + t * per;
     const int hi = min(x, lo + per - 1);
     int cnt = 0;
-    for (int c = lo; c <= hi; ++c) cnt += (c == 1) || (!comp[c] && x % c != 0);
+    auto keep = [&](int c) { return c == 1 || (!((comp[c >> 5] >> (c & 31)) & 1u) && x % c != 0); };
+    for (int c = lo; c <= hi; ++c) cnt += keep(c);
     // block exclusive scan of cnt
     int v = cnt;
     const int lane = t & 63, w = t >> 6;
@@ -78,7 +81,7 @@ __global__ __launch_bounds__(CP_TPB) void owgs_coprime_kernel(const int32_t* xs,
     __syncthreads();
     int pos = v - cnt + (w ? wsum[w - 1] : 0);
     for (int c = lo; c <= hi; ++c)
-        if ((c == 1) || (!comp[c] && x % c != 0)) o[pos++] = c;
+        if (keep(c)) o[pos++] = c;
     if (t == CP_TPB - 1) counts[blockIdx.x] = pos;
 }
 

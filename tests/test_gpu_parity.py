@@ -425,9 +425,19 @@ def test_pairwise_coprime_golden_on_gpu(golden):
 def test_pairwise_coprime_sweep_matches_oracle_fold():
     """owgs_coprime_kernel (sieve + ordered compaction) == the literal greedy fold (SCPB:379-384) for every x."""
     b = gpu()
-    xs = list(range(-2, 1300)) + [2310, 4096, 9000, 9001, 10000, 30030, 32767]
+    xs = list(range(-2, 1300)) + [2310, 4096, 9000, 9001, 10000, 30030, 32767, 65536, 70001, 100003]
     for x in xs:
         assert b.pairwise_coprime_numbers_until(x) == O.pairwise_coprime_numbers_until(x), x
+    # the kernel's largest pool (524,287, one LDS bit per number): the fold's closed form, {1} and the primes p <= x
+    # with p !| x (owgs_state.hip header), from a numpy sieve -- the literal fold takes minutes at this size
+    x = 524_287
+    sieve = np.ones(x + 1, bool)
+    sieve[:2] = False
+    for p in range(2, int(x ** 0.5) + 1):
+        if sieve[p]:
+            sieve[p * p::p] = False
+    exp = [1] + [int(p) for p in np.nonzero(sieve)[0] if x % int(p) != 0]
+    assert b.pairwise_coprime_numbers_until(x) == exp
     with pytest.raises(Exception):
         b.pairwise_coprime_numbers_until(1 << 20)
 
@@ -745,6 +755,15 @@ def test_large_pool_40k_invokers_stream_matches_oracle():
     assert len(w.inv_ids) > mx.value and w.stream.n_batches > 3 and len(w.stream.rel_aid) > 10_000
     b, g_inv, g_fl = check_stream(w)
     assert (g_fl & 1).sum() >= 0 and (g_inv >= 0).all()
+
+
+def test_large_pool_100k_invokers_beyond_the_old_step_kernel_range():
+    """100,000 invokers: a managed pool of 90,000 positions, past the 65,535 the step-size kernel held until round 5
+    (pairwiseCoprimeNumbersUntil now sieves one LDS bit per number) -- the stream bit-exact on the large-state engine."""
+    w = W.config("headline", n_invokers=100_000, n_activations=150_000, n_actions=4000, n_namespaces=400,
+                 conc_frac=0.3)
+    b, g_inv, g_fl = check_stream(w)
+    assert b.managed_size == 90_000 and (g_inv >= 0).all()
 
 
 def test_large_pool_shim_sequence_with_membership_change():
