@@ -569,7 +569,7 @@ def test_rejected_update_leaves_the_context_unchanged():
     w = W.config("headline", n_invokers=2000, n_activations=40_000)
     b = gpu_for(w)
     before = (b.permits().copy(), b.managed_size, b.blackbox_size, b.cluster_size, b.managed_step_sizes)
-    n = 140_000  # managed pool 126,000 positions
+    n = 600_000  # managed pool 540,000 positions: beyond every engine (owgs_coprime_max 524,287)
     with pytest.raises(OwgsError) as e:
         b.update_invokers_arrays(np.arange(n, dtype=np.int32), np.full(n, 16384 * MB, np.int64), np.zeros(n, np.uint8))
     assert e.value.code == -34  # OWGS_ERANGE
