@@ -59,6 +59,9 @@ def parse(argv=None):
     ap.add_argument("--health-churn", action="store_true",
                     help="N = 1: replay batch by batch with the per-batch health schedule of the N > 1 runs "
                          "(cluster.health_schedule) instead of one launch per step")
+    ap.add_argument("--health-static", action="store_true",
+                    help="with --health-churn: every batch's all-gathered row is the initial health (the cadence's "
+                         "mechanism -- exchange, per-batch application, group launches -- without the workload change)")
     ap.add_argument("--slots", choices=("split", "weak"), default="split",
                     help="'split' (default): 16 GiB invokers, each controller's slot = 1/clusterSize of them "
                          "(configs[4]); 'weak': invoker memory 16 GiB x clusterSize so every slot stays 16 GiB")
@@ -629,6 +632,8 @@ def main():
     per_batch = K == 1 and (world > 1 or args.health_churn)
     if per_batch:
         health = cluster.health_schedule(w.inv_status, s.n_batches)
+        if args.health_static:
+            health = np.repeat(np.asarray(w.inv_status, dtype=np.uint8)[None, :], max(s.n_batches, 1), axis=0)
         shards[0].health = health
         shards[0].d_health = [t(health[k], np.uint8) for k in range(s.n_batches)]
     torch.cuda.synchronize()

@@ -685,6 +685,9 @@ def test_health_on_one_stream_replay_on_another_is_ordered():
     ("c4", dict(n_activations=200_000), 5, None),
     ("c2", dict(n_activations=200_000), 64, None),
     ("headline", dict(n_activations=150_000, n_invokers=2000, conc_frac=0.3), 3, 2),
+    # beyond the on-chip image: the large-state engine, per-batch health and a cluster change through the same call
+    ("headline", dict(n_activations=300_000, n_invokers=25_000, conc_frac=0.3), 4, None),
+    ("headline", dict(n_activations=300_000, n_invokers=25_000, conc_frac=0.3), 2, 1),
 ])
 def test_group_replay_with_per_batch_health_matches_oracle(cfg, kw, group, cluster_at):
     """configs[4] cadence with several batches per engine launch (owgs_replay_device_group): the engine applies batch
