@@ -630,6 +630,15 @@ def main():
     hx = cluster.HealthExchange(dist, torch.from_numpy(w.inv_status.copy()).to(dev), world)
     # health between batches (configs[4]) for one shard per GPU; several shards per GPU keep one exchange per step
     per_batch = K == 1 and (world > 1 or args.health_churn)
+    if per_batch and dist is not None and world > 1:
+        # every rank issues one all-gather per batch: the shards' batch counts must agree, or the collectives would
+        # pair up wrongly and hang -- fail loudly instead
+        nb = torch.tensor([s.n_batches], dtype=torch.int64, device=dev)
+        nbs = [torch.zeros_like(nb) for _ in range(world)]
+        dist.all_gather(nbs, nb)
+        counts = [int(x.item()) for x in nbs]
+        if len(set(counts)) != 1:
+            raise SystemExit(f"shards disagree on the number of batches per step: {counts}")
     if per_batch:
         health = cluster.health_schedule(w.inv_status, s.n_batches)
         if args.health_static:

@@ -415,6 +415,55 @@ def test_release_after_cluster_change_is_nosuchelement():
     assert b.permits().tolist() == [512, 512]
 
 
+def _large(b):
+    """Move a context to the large-state engine the way a deployment would: an action above the on-chip engines'
+    maxConcurrent (4095, a 12-bit field; owgs_seq.hip keeps 32-bit fields)."""
+    from openwhisk_amd._lib import OwgsError
+    b.register_actions([Action("zz", "zz/wide", "0.0.1", 128, 5000)])
+    with pytest.raises(OwgsError) as e:  # (snapshots are on-chip only: proof that the context moved)
+        b.snapshot()
+    assert e.value.code == -34
+    return b
+
+
+def test_large_engine_edge_cases_match_the_on_chip_ones():
+    """The reference's edge cases on the large-state engine (small pools, the context moved there by a maxConcurrent
+    of 5000): no invokers -> None (SCPB:288-290), the Int.MinValue hash -> IndexOutOfBounds (SCPB:266-268), every
+    release flag (NS:103, CLB:278-279, invokerSlots.lift SCPB:329), ForcibleSemaphore's overflow Error (FS:48-50) in
+    stream order, and a release after updateCluster (SCPB:566-568) -- the same outcomes as the tests above."""
+    b = _large(gpu())
+    (a,), _ = b.register_actions([Action("ns", "ns/a", "0.0.1", 256)])
+    assert b.publish([a, a])[0].tolist() == [NONE, NONE]
+    b = _large(gpu())
+    b.update_invokers([InvokerHealth(i, 4096 * MB) for i in range(10)])
+    (a,), (h,) = b.register_actions([Action("", "polygenelubricants", "0.0.1", 256)])
+    assert h == -2**31 and b.publish([a])[0][0] == THROW_INDEX
+    assert b.permits().tolist() == [4096] * 10
+    b = _large(gpu())
+    b.update_invokers([InvokerHealth(i, 1024 * MB) for i in range(4)])
+    acts, _ = b.register_actions([Action("ns", "ns/a", "0.0.1", 256, 1), Action("ns", "ns/c", "0.0.1", 256, 4)])
+    inv, _ = b.publish([acts[1]])
+    other = (inv[0] + 1) % 4
+    rf = b.release_invoker([other, 99, -1, inv[0], inv[0]], [acts[1], acts[0], acts[0], acts[1], acts[1]])
+    assert rf.tolist() == [1, 0, 4, 0, 1]
+    assert b.permits().tolist() == [1024] * 4
+    top = 2**31 - 1
+    b = _large(gpu())
+    b.update_invokers_arrays(np.arange(3, dtype=np.int32), np.array([top - 300, 1000, top - 256], np.int64) * MB,
+                             np.zeros(3, np.uint8))
+    acts, _ = b.register_actions([Action("ns", "ns/a", "0.0.1", 256, 1)])
+    rf = b.release_invoker([0, 1, 0, 2, 2], [acts[0]] * 5)
+    assert rf.tolist() == [0, 0, 2, 0, 2]
+    assert b.permits().tolist() == [top - 44, 1256, top]
+    b = _large(gpu())
+    b.update_invokers([InvokerHealth(i, 1024 * MB) for i in range(2)])
+    (a,), _ = b.register_actions([Action("ns", "ns/c", "0.0.1", 128, 3)])
+    inv, _ = b.publish([a])
+    b.update_cluster(2)
+    assert b.release_invoker(inv, [a]).tolist() == [1]
+    assert b.permits().tolist() == [512, 512]
+
+
 # ----------------------------------------------------------------------------------------------- state updates (§8f-2)
 def test_pairwise_coprime_golden_on_gpu(golden):
     b = gpu()
