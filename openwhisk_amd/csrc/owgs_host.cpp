@@ -128,6 +128,7 @@ struct EnvOpts {
     // the resident engine's speculative walks: walk steps each publish probes on its own before the in-order
     // validation (0: every decision walked one at a time)
     int res_spec = 16;
+    int res_split = 1;  // OWGS_RES_SPLIT=0: wave 0 speculates a chunk's concurrent decisions itself
     // owgs_replay_device through the resident engine's stream mode (one wave deciding, speculative walks) instead of
     // the chunked engine, where it applies (identity pools, no watched pairs)
     int spec_replay = 0;
@@ -135,6 +136,7 @@ struct EnvOpts {
         if (const char* e = getenv("OWGS_SPEC_REPLAY")) spec_replay = atoi(e);
         if (const char* e = getenv("OWGS_RESIDENT")) res = atoi(e);
         if (const char* e = getenv("OWGS_RES_SPEC")) res_spec = atoi(e);
+        if (const char* e = getenv("OWGS_RES_SPLIT")) res_split = atoi(e);
         if (const char* e = getenv("OWGS_RES_MAX")) res_max = atoi(e);
         if (const char* e = getenv("OWGS_RES_IDLE_US")) res_idle_us = atoll(e);
         if (const char* e = getenv("OWGS_RES_LIFE_US")) res_life_us = atoll(e);
@@ -1227,6 +1229,7 @@ static int res_launch(owgs_ctx* c) {
     a.idle_ticks = env_opts().res_idle_us * 100;  // s_memrealtime: 100 MHz
     a.life_ticks = std::max(0ll, env_opts().res_life_us) * 100;
     a.spec = std::max(0, env_opts().res_spec);
+    a.hsplit = env_opts().res_split > 0 ? 1 : 0;
     a.w = watch_args(c);
     a.w_sidx = c->d_w_sidx.p;
     a.w_scap = c->w_scap;
@@ -1877,7 +1880,10 @@ int owgs_update_invokers(owgs_ctx* c, int32_t n, const int32_t* ids, const int64
         const int32_t slots = (old_size < new_size && n > c->n_slots) ? n : c->n_slots;
         bool identity = n <= slots;
         for (int32_t i = 0; identity && i < n; ++i) identity = ids[i] == i;
-        large_next = engine_variant(slots, identity ? 0 : 1, n, std::min(managed, n), std::min(blackboxes, n)) < 0;
+        // (a context already on the large-state engine stays there: its NestedSemaphore map lives in that layout;
+        // slots never shrink, so a pool that left the chip cannot fit it again anyway)
+        large_next = c->large || c->big_conc ||
+                     engine_variant(slots, identity ? 0 : 1, n, std::min(managed, n), std::min(blackboxes, n)) < 0;
         if (large_next && !(identity && large_fits(n, std::min(managed, n), std::min(blackboxes, n))))
             return c->fail(OWGS_ERANGE, "invoker state exceeds every engine (owgs_limits; explicit pools on chip only)");
     }
@@ -2701,6 +2707,7 @@ static int spec_replay(owgs_ctx* c, int32_t nb, const int64_t* acq_off, const in
     a.gen_base = ++c->res_gen_seen;
     c->res_gen_seen += (uint32_t)n_rel + 1;
     a.spec = std::max(0, env_opts().res_spec);
+    a.hsplit = env_opts().res_split > 0 ? 1 : 0;
     a.smode = 1;
     a.s_nb = nb;
     a.s_nact = aid_end;

@@ -122,7 +122,7 @@ __device__ __forceinline__ int select_in_word(uint32_t m, int need) {
 #define RES_CLEAN_TOMBS (OWGS_CTC / 8)
 #endif
 struct ResLayout {
-    uint32_t P, ub, pc, ct, sc, cc, mv, bf, wf, wl, stage, end;
+    uint32_t P, ub, pc, ct, sc, cc, mv, bf, wf, wl, hx, stage, end;
 };
 __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
     const uint32_t words = (uint32_t)(n_ids + 31) / 32;
@@ -137,7 +137,8 @@ __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
     y.bf = y.mv + 64u * 4u;
     y.wf = y.bf + RES_BF * 4u;
     y.wl = y.wf + RES_WF * 4u;
-    y.stage = y.wl + RES_WL * 8u;
+    y.hx = y.wl + RES_WL * 8u;       // the helper wave's speculation of one chunk: 64 x 2 x 16 B
+    y.stage = y.hx + 64u * 32u;
     y.end = y.stage;
     return y;
 }
@@ -156,6 +157,10 @@ __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
 #define RS_U1 11
 #define RS_TOMB 12   // deleted primary entries (the cleanup between calls runs when they pile up)
 #define RS_WLN 13    // entries of the watched-walk list (wl)
+#define RS_HGO 14    // helper wave: request number (wave 0 -> wave 1; -1 = the call's decisions are done)
+#define RS_HDONE 15  // helper wave: the request it answered
+#define RS_HI0 16    // helper wave: the chunk's first publish and its size
+#define RS_HNQ 17
 
 // blocked Bloom filter over the primary table's keys (LDS, RES_BF words): one word and three bits per key, set on
 // every insert into the primary and rebuilt with it; a key whose bits are not all set is not in the primary, so a
@@ -270,6 +275,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
     uint32_t* bf = (uint32_t*)(Lb + Y.bf);
     uint32_t* wf = (uint32_t*)(Lb + Y.wf);
     uint2* wl = (uint2*)(Lb + Y.wl);
+    uint4* hx = (uint4*)(Lb + Y.hx);
     char* stg = Lb + Y.stage;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int n_slots = A.n_slots, nm = A.nm, nb = A.nb;
@@ -658,6 +664,10 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 }
             }
         }
+        if (tid == 0) {
+            sc[RS_HGO] = 0;
+            sc[RS_HDONE] = 0;
+        }
         __syncthreads();
         // releases that could leave the LDS permit range: exact maximum first, then refuse the call untouched
         if (sc[RS_BAIL] == 0 && (long long)sc[RS_MAXP] + (long long)rsum >= (long long)OWGS_PLIM) {
@@ -671,9 +681,127 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 sc[RS_BAIL] = OWGS_RES_BAIL_RELRISK;
             __syncthreads();
         }
+        // speculation of a chunk's concurrent decisions (maxConcurrent > 1) against the state at the chunk's start, one
+        // lane per decision: run by wave 0 itself, or by wave 1 while wave 0 walks the chunk's other decisions (the
+        // speculation only reads the state; round 5)
+        const bool hsplit = !smode && A.hsplit != 0;
+        auto cspec = [&](const uint4 me, const int nq_, const bool ovf_on_, int& sp, int& sp_t, int& c_ix, uint32_t& c_nv,
+                         bool& c_take, int& e_, uint32_t& n_ovf) {
+            const int l_mem = (int)(me.y & OWGS_AM_MEM_MASK);
+            const int l_pool = (me.x & OWGS_AM_POOL) ? 1 : 0;
+            const int l_n = l_pool ? nb : nm, l_base = l_pool ? A.n_ids - nb : 0;
+            const int l_home = (int)(me.x & OWGS_AM_POS_MASK), l_step = (int)((me.x >> 15) & OWGS_AM_POS_MASK);
+            const int l_maxc = (int)((me.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
+            const bool l_cc = lane < nq_ && !(me.y & (OWGS_AM_EMPTY | OWGS_AM_THROW)) && l_maxc > 1;
+            const int l_rank = (int)((me.w >> RES_RANK_SHIFT) & 63u);
+            const float rmem = __builtin_amdgcn_rcpf((float)max(l_mem, 1));
+                            // another action of the same key earlier in the chunk walks differently and shares the
+                            // key's entries: its effect on mine is not predicted, so such a decision is decided alone
+                            const int c_rank = l_rank;
+                            int cneed = c_rank;
+                            const float rmx = __builtin_amdgcn_rcpf((float)max(l_maxc, 1));
+                            bool cw = l_cc && !(me.w & RES_SHARED);
+                            int cpos = cw ? mod_fast(l_home, l_n, __builtin_amdgcn_rcpf((float)l_n)) : 0, cst = 0;
+                            // 4 walk steps per round: their permits and Bloom-filter words read together, the map
+                            // probed only where the filter says the key may be
+                            const int cbudget = max(4, A.spec >> 2);  // (8 steps measured slower: longer rounds)
+                            while (__ballot(cw)) {
+                                if (cw) {
+                                    int idk[4], pvk[4];
+                                    bool bk[4];
+                                    int pp = cpos;
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k) {
+                                        idk[k] = l_base + pp;
+                                        pvk[k] = P[idk[k]];
+                                        pp += l_step;
+                                        pp -= pp >= l_n ? l_n : 0;
+                                    }
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k) {
+                                        const uint2 b = bf_pos(ct_key(idk[k], (int)me.z));
+                                        bk[k] = (bf[b.x] & b.y) == b.y;
+                                    }
+                                    // the first map block of every step the filter passes, read together (the
+                                    // lookups below only continue a chain past it)
+                                    uint4 fa[4], fb[4];
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k) {
+                                        fa[k] = fb[k] = make_uint4(0u, 0u, 0u, 0u);
+                                        if (bk[k]) {
+                                            const uint32_t h = ct_home(ct_key(idk[k], (int)me.z));
+                                            fa[k] = *(const uint4*)&ct[h];
+                                            fb[k] = *(const uint4*)&ct[h + 2];
+                                        }
+                                    }
+                                    int kf = 4;
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k) {
+                                        const int pv = pvk[k];
+                                        if (kf == 4 && cst + k < l_n && pv < OWGS_PLIM) {
+                                            const uint32_t key = ct_key(idk[k], (int)me.z);
+                                            uint32_t v = 0u;
+                                            int ix = bk[k] ? ct_lookup_after(ct, key, fa[k], fb[k], &v) : -1;
+                                            if (ix < 0 && ovf_on_) {
+                                                ++n_ovf;
+                                                const int oj = ovf_find(A.ovf, key, &v);
+                                                ix = oj >= 0 ? OWGS_CTC + oj : -1;
+                                            }
+                                            const int c0 = (int)(v & OWGS_CT_C_MASK), o0 = ix >= 0 ? ct_ops(v) : 0;
+                                            bool ok = false;
+                                            int c1 = 0;
+                                            bool tk = false;
+                                            if (cneed < c0) {  // a free slot of the key's container
+                                                ok = true;
+                                                c1 = c0 - cneed - 1;
+                                            } else {  // containers the memory holds, maxConcurrent slots each
+                                                const int kp = cneed - c0;
+                                                int qc = (int)((float)kp * rmx);
+                                                qc -= qc * l_maxc > kp ? 1 : 0;
+                                                qc += (qc + 1) * l_maxc <= kp ? 1 : 0;
+                                                const int j = kp - qc * l_maxc;  // (kp < 64: exact)
+                                                if (pv >= (qc + 1) * l_mem) {
+                                                    ok = true;
+                                                    tk = j == 0;
+                                                    c1 = l_maxc - j - 1;
+                                                } else if (pv >= l_mem) {
+                                                    int m = (int)((float)pv * rmem);
+                                                    m -= m * l_mem > pv ? 1 : 0;
+                                                    m += (m + 1) * l_mem <= pv ? 1 : 0;
+                                                    cneed -= c0 + m * l_maxc;
+                                                } else {
+                                                    cneed -= c0;
+                                                }
+                                            }
+                                            if (ok) {
+                                                if (o0 + cneed + 1 > OWGS_MAX_OPS) e_ |= OWGS_ERR_OPS;
+                                                kf = k;
+                                                c_ix = ix;
+                                                c_take = tk;
+                                                c_nv = ct_val(c1, o0 + cneed + 1);
+                                            }
+                                        }
+                                    }
+                                    if (kf < 4) {
+                                        sp = SP_FOUND;
+                                        sp_t = kf == 0 ? idk[0] : kf == 1 ? idk[1] : kf == 2 ? idk[2] : idk[3];
+                                        cw = false;
+                                    } else {
+                                        cst += 4;
+                                        cpos = pp;
+                                        if (cst >= l_n) {
+                                            if (c_rank == 0) sp = SP_FAIL;  // every pool position: forced below (a
+                                            cw = false;                     // repeat: decided alone)
+                                        } else if (cst >= cbudget) {
+                                            cw = false;  // SP_STOP: decided alone
+                                        }
+                                    }
+                                }
+                            }
+                                };
         const int bail = sc[RS_BAIL];
         if (bail == 0 && wave == 0) {
-            int err = 0;
+            int err = 0, hreq_n = 0;  // (hreq_n: requests posted to the helper wave in this call)
             bool ovf_on = sc[RS_OVF] > 0;
             int used = sc[RS_USED], tombs = 0;  // (tombs: per lane, deleted entries made - reused this call)
             // maxConcurrent == 1 walks: U = an upper bound of every usable permit count of the pool (a walk with
@@ -1210,6 +1338,20 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 wp = mod_fast(l_home + ws * l_step, l_n, __builtin_amdgcn_rcpf((float)l_n));
                             }
                         }
+                        // the chunk's concurrent decisions go to the helper wave (their speculation reads the state
+                        // only, and every earlier change of it is published by the release below)
+                        const bool hreq = hsplit && !ovf_on && __ballot(l_cc) != 0ull;
+                        bool hreq_lost = false;
+                        if (hreq) {
+                            ++hreq_n;
+                            if (lane == 0) {
+                                sc[RS_HI0] = i0;
+                                sc[RS_HNQ] = nq;
+                            }
+                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                            if (lane == 0)
+                                __hip_atomic_store(&sc[RS_HGO], hreq_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
                         for (int it = 0; __ballot(walking); it += 4) {
                             if (walking) {
                                 int pk[4], vk[4];
@@ -1269,108 +1411,35 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                         uint32_t c_nv = 0u;   // the entry's value after this decision
                         bool c_take = false;  // the decision opens a container: it takes memory (NS:70-79)
                         if (__ballot(l_cc)) {
-                            // another action of the same key earlier in the chunk walks differently and shares the
-                            // key's entries: its effect on mine is not predicted, so such a decision is decided alone
-                            const int c_rank = l_rank;
-                            int cneed = c_rank;
-                            const float rmx = __builtin_amdgcn_rcpf((float)max(l_maxc, 1));
-                            bool cw = l_cc && !(me.w & RES_SHARED);
-                            int cpos = cw ? mod_fast(l_home, l_n, __builtin_amdgcn_rcpf((float)l_n)) : 0, cst = 0;
-                            // 4 walk steps per round: their permits and Bloom-filter words read together, the map
-                            // probed only where the filter says the key may be
-                            const int cbudget = max(4, A.spec >> 2);  // (8 steps measured slower: longer rounds)
-                            while (__ballot(cw)) {
-                                if (cw) {
-                                    int idk[4], pvk[4];
-                                    bool bk[4];
-                                    int pp = cpos;
-#pragma unroll
-                                    for (int k = 0; k < 4; ++k) {
-                                        idk[k] = l_base + pp;
-                                        pvk[k] = P[idk[k]];
-                                        pp += l_step;
-                                        pp -= pp >= l_n ? l_n : 0;
+                            if (hreq) {  // the helper wave's answer to request hreq_n
+                                for (int spin = 0;; ++spin) {
+                                    if (__hip_atomic_load(&sc[RS_HDONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ==
+                                        hreq_n)
+                                        break;
+                                    if (spin > (1 << 26)) {  // (never expected: decide here instead of waiting on)
+                                        hreq_lost = true;
+                                        break;
                                     }
-#pragma unroll
-                                    for (int k = 0; k < 4; ++k) {
-                                        const uint2 b = bf_pos(ct_key(idk[k], (int)me.z));
-                                        bk[k] = (bf[b.x] & b.y) == b.y;
-                                    }
-                                    // the first map block of every step the filter passes, read together (the
-                                    // lookups below only continue a chain past it)
-                                    uint4 fa[4], fb[4];
-#pragma unroll
-                                    for (int k = 0; k < 4; ++k) {
-                                        fa[k] = fb[k] = make_uint4(0u, 0u, 0u, 0u);
-                                        if (bk[k]) {
-                                            const uint32_t h = ct_home(ct_key(idk[k], (int)me.z));
-                                            fa[k] = *(const uint4*)&ct[h];
-                                            fb[k] = *(const uint4*)&ct[h + 2];
-                                        }
-                                    }
-                                    int kf = 4;
-#pragma unroll
-                                    for (int k = 0; k < 4; ++k) {
-                                        const int pv = pvk[k];
-                                        if (kf == 4 && cst + k < l_n && pv < OWGS_PLIM) {
-                                            const uint32_t key = ct_key(idk[k], (int)me.z);
-                                            uint32_t v = 0u;
-                                            int ix = bk[k] ? ct_lookup_after(ct, key, fa[k], fb[k], &v) : -1;
-                                            if (ix < 0 && ovf_on) {
-                                                ++pr_ovf;
-                                                const int oj = ovf_find(A.ovf, key, &v);
-                                                ix = oj >= 0 ? OWGS_CTC + oj : -1;
-                                            }
-                                            const int c0 = (int)(v & OWGS_CT_C_MASK), o0 = ix >= 0 ? ct_ops(v) : 0;
-                                            bool ok = false;
-                                            int c1 = 0;
-                                            bool tk = false;
-                                            if (cneed < c0) {  // a free slot of the key's container
-                                                ok = true;
-                                                c1 = c0 - cneed - 1;
-                                            } else {  // containers the memory holds, maxConcurrent slots each
-                                                const int kp = cneed - c0;
-                                                int qc = (int)((float)kp * rmx);
-                                                qc -= qc * l_maxc > kp ? 1 : 0;
-                                                qc += (qc + 1) * l_maxc <= kp ? 1 : 0;
-                                                const int j = kp - qc * l_maxc;  // (kp < 64: exact)
-                                                if (pv >= (qc + 1) * l_mem) {
-                                                    ok = true;
-                                                    tk = j == 0;
-                                                    c1 = l_maxc - j - 1;
-                                                } else if (pv >= l_mem) {
-                                                    int m = (int)((float)pv * rmem);
-                                                    m -= m * l_mem > pv ? 1 : 0;
-                                                    m += (m + 1) * l_mem <= pv ? 1 : 0;
-                                                    cneed -= c0 + m * l_maxc;
-                                                } else {
-                                                    cneed -= c0;
-                                                }
-                                            }
-                                            if (ok) {
-                                                if (o0 + cneed + 1 > OWGS_MAX_OPS) err |= OWGS_ERR_OPS;
-                                                kf = k;
-                                                c_ix = ix;
-                                                c_take = tk;
-                                                c_nv = ct_val(c1, o0 + cneed + 1);
-                                            }
-                                        }
-                                    }
-                                    if (kf < 4) {
-                                        sp = SP_FOUND;
-                                        sp_t = kf == 0 ? idk[0] : kf == 1 ? idk[1] : kf == 2 ? idk[2] : idk[3];
-                                        cw = false;
-                                    } else {
-                                        cst += 4;
-                                        cpos = pp;
-                                        if (cst >= l_n) {
-                                            if (c_rank == 0) sp = SP_FAIL;  // every pool position: forced below (a
-                                            cw = false;                     // repeat: decided alone)
-                                        } else if (cst >= cbudget) {
-                                            cw = false;  // SP_STOP: decided alone
-                                        }
-                                    }
+                                    __builtin_amdgcn_s_sleep(1);
                                 }
+                                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                            }
+                            if (hreq && !hreq_lost) {
+                                const uint4 h0 = hx[lane], h1 = hx[64 + lane];
+                                if (l_cc) {
+                                    sp = (int)h0.x;
+                                    sp_t = (int)h0.y;
+                                    c_ix = (int)h0.z;
+                                    c_nv = h0.w;
+                                    c_take = h1.x != 0u;
+                                }
+                                err |= (int)h1.y;
+                            } else {
+                                int e_ = 0;
+                                uint32_t n_ovf = 0u;
+                                cspec(me, nq, ovf_on, sp, sp_t, c_ix, c_nv, c_take, e_, n_ovf);
+                                err |= e_;
+                                pr_ovf += n_ovf;
                             }
                         }
                         // a failed walk bounds the pool's usable permits below its memory (U), and the fallback's
@@ -1765,6 +1834,36 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 const long long mp = (long long)sc[RS_MAXP] + (long long)rsum;
                 sc[RS_MAXP] = (int)min(mp, (long long)0x7FFFFFFF);
                 if (err) atomicOr(&sc[RS_ERR], err);
+            }
+            if (hsplit) {  // the call's decisions are done: the helper wave leaves its loop
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                if (lane == 0) __hip_atomic_store(&sc[RS_HGO], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        } else if (bail == 0 && wave == 1 && hsplit) {
+            // ---- helper wave: speculates the concurrent decisions of the chunk wave 0 posts (request k), answers k
+            for (int expect = 1;; ++expect) {
+                int go = 0;
+                for (int spin = 0;; ++spin) {
+                    go = __hip_atomic_load(&sc[RS_HGO], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (go < 0 || go >= expect) break;
+                    if (spin > (1 << 26)) {  // (bounded: wave 0 decides by itself past its own bound)
+                        go = -2;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (go < 0) break;
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                const int hi0 = sc[RS_HI0], hnq = sc[RS_HNQ];
+                const uint4 me = lane < hnq ? pub[hi0 + lane] : make_uint4(0u, OWGS_AM_EMPTY, 0u, 0u);
+                int sp = SP_STOP, sp_t = -1, c_ix = -1, e_ = 0;
+                uint32_t c_nv = 0u, n_ovf = 0u;
+                bool c_take = false;
+                cspec(me, hnq, false, sp, sp_t, c_ix, c_nv, c_take, e_, n_ovf);
+                hx[lane] = make_uint4((uint32_t)sp, (uint32_t)sp_t, (uint32_t)c_ix, c_nv);
+                hx[64 + lane] = make_uint4(c_take ? 1u : 0u, (uint32_t)e_, n_ovf, 0u);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                if (lane == 0) __hip_atomic_store(&sc[RS_HDONE], expect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         }
         __syncthreads();

@@ -70,6 +70,22 @@ for l in d['legs']:
 " | tee -a $O/abshim.txt
         done
       done ;;
+    abenv)  # alternating runs of the shim leg with $ABENV set to 1 and to 0 (same library)
+      for i in 1 2; do
+        for v in 1 0; do
+          n=${ABENV}_${v}_$i
+          env ${ABENV}=$v timeout -k 10 200 python tools/shim_leg.py --drains ${DRAINS:-64,512} --modes fused > $O/shim_$n.json 2> $O/shim_$n.err || { tail -5 $O/shim_$n.err; stop abenv 1; }
+          python3 -c "
+import json
+d=json.load(open('$O/shim_$n.json'))
+for l in d['legs']:
+    r=l.get('resident') or {}; s=max(1, r.get('served', 0))
+    if l['mode'] == 'fused-reset':
+        print('$n', l['mode'], 'resident', l['resident_fraction_after'], 'p50 before/after', round(l['p50_us_before'],1), round(l['p50_us_after'],1), 'exact', l['bit_exact']); continue
+    print('$n', l['mode'], l['drain'], 'p50', round(l['p50_us'],1), 'p99', round(l.get('p99_us'),1), round(l['decisions_per_s']/1e6,2), 'M/s pub', round(r.get('publish_cycles',0)/s), 'alone', round(r.get('alone_cycles',0)/s), 'exact', l['bit_exact'])
+" | tee -a $O/abenv.txt
+        done
+      done ;;
     abcfg)  # engine rates per config, in-tree library vs the base variant, alternating
       B=openwhisk_amd/variants/libowgs_${AB_BASE:-r04}.so
       for i in 1 2; do
