@@ -685,6 +685,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
         // lane per decision: run by wave 0 itself, or by wave 1 while wave 0 walks the chunk's other decisions (the
         // speculation only reads the state; round 5)
         const bool hsplit = !smode && A.hsplit != 0;
+        const int nhelp = hsplit ? min(max(A.hsplit, 1), 3) : 0;  // helper waves (1..3): lane i goes to wave 1 + i % nhelp
         auto cspec = [&](const uint4 me, const int nq_, const bool ovf_on_, int& sp, int& sp_t, int& c_ix, uint32_t& c_nv,
                          bool& c_take, int& e_, uint32_t& n_ovf) {
             const int l_mem = (int)(me.y & OWGS_AM_MEM_MASK);
@@ -1414,7 +1415,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             if (hreq) {  // the helper wave's answer to request hreq_n
                                 for (int spin = 0;; ++spin) {
                                     if (__hip_atomic_load(&sc[RS_HDONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ==
-                                        hreq_n)
+                                        hreq_n * nhelp)
                                         break;
                                     if (spin > (1 << 26)) {  // (never expected: decide here instead of waiting on)
                                         hreq_lost = true;
@@ -1839,7 +1840,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
                 if (lane == 0) __hip_atomic_store(&sc[RS_HGO], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-        } else if (bail == 0 && wave == 1 && hsplit) {
+        } else if (bail == 0 && wave >= 1 && wave <= nhelp) {
             // ---- helper wave: speculates the concurrent decisions of the chunk wave 0 posts (request k), answers k
             for (int expect = 1;; ++expect) {
                 int go = 0;
@@ -1855,15 +1856,18 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 if (go < 0) break;
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
                 const int hi0 = sc[RS_HI0], hnq = sc[RS_HNQ];
-                const uint4 me = lane < hnq ? pub[hi0 + lane] : make_uint4(0u, OWGS_AM_EMPTY, 0u, 0u);
+                const bool mine = lane % max(nhelp, 1) == wave - 1;  // (the lanes of the other helper waves: skipped)
+                const uint4 me = lane < hnq && mine ? pub[hi0 + lane] : make_uint4(0u, OWGS_AM_EMPTY, 0u, 0u);
                 int sp = SP_STOP, sp_t = -1, c_ix = -1, e_ = 0;
                 uint32_t c_nv = 0u, n_ovf = 0u;
                 bool c_take = false;
                 cspec(me, hnq, false, sp, sp_t, c_ix, c_nv, c_take, e_, n_ovf);
-                hx[lane] = make_uint4((uint32_t)sp, (uint32_t)sp_t, (uint32_t)c_ix, c_nv);
-                hx[64 + lane] = make_uint4(c_take ? 1u : 0u, (uint32_t)e_, n_ovf, 0u);
+                if (mine) {
+                    hx[lane] = make_uint4((uint32_t)sp, (uint32_t)sp_t, (uint32_t)c_ix, c_nv);
+                    hx[64 + lane] = make_uint4(c_take ? 1u : 0u, (uint32_t)e_, n_ovf, 0u);
+                }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-                if (lane == 0) __hip_atomic_store(&sc[RS_HDONE], expect, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (lane == 0) atomicAdd(&sc[RS_HDONE], 1);  // (wave 0 waits for nhelp answers per request)
             }
         }
         __syncthreads();

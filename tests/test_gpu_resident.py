@@ -287,18 +287,19 @@ print("ok")
 """
 
 
-@pytest.mark.parametrize("budget", ["0", "1", "4"])
-def test_resident_speculation_budgets(budget):
+@pytest.mark.parametrize("budget,split", [("0", "1"), ("1", "1"), ("4", "1"), ("16", "0")])
+def test_resident_speculation_budgets(budget, split):
     """Walk budgets of 0 (no speculation: decisions one at a time), 1 and 4 steps (most walks unfinished: decided
-    alone from where the speculation stopped) give the same decisions (OWGS_RES_SPEC is read once per process, so each
-    budget runs in a child process)."""
+    alone from where the speculation stopped) give the same decisions, and so does the default budget with the
+    concurrent speculation on wave 0 instead of the helper wave (OWGS_RES_SPLIT=0).  The switches are read once per
+    process, so each case runs in a child process."""
     import os
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     root = os.path.dirname(here)
     code = _BUDGET_SCRIPT.format(root=root, oracle=os.path.join(root, "oracle"), tests=here)
-    env = dict(os.environ, OWGS_RES_SPEC=budget)
+    env = dict(os.environ, OWGS_RES_SPEC=budget, OWGS_RES_SPLIT=split)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 

@@ -72,7 +72,7 @@ for l in d['legs']:
       done ;;
     abenv)  # alternating runs of the shim leg with $ABENV set to 1 and to 0 (same library)
       for i in 1 2; do
-        for v in 1 0; do
+        for v in ${ABVALS:-1 0}; do
           n=${ABENV}_${v}_$i
           env ${ABENV}=$v timeout -k 10 200 python tools/shim_leg.py --drains ${DRAINS:-64,512} --modes fused > $O/shim_$n.json 2> $O/shim_$n.err || { tail -5 $O/shim_$n.err; stop abenv 1; }
           python3 -c "
