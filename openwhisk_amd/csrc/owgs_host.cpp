@@ -122,6 +122,7 @@ struct EnvOpts {
     long long res_life_us = 100000;
     // watched pairs (after updateCluster) on the resident engine (0: such calls take the launch chain, as in round 4)
     int res_watch = 1;
+    int res_eager = 1;  // OWGS_RES_EAGER=0: after a chained call the engine is relaunched by the next small call only
     // (tests) the doorbell's and the walk-cursor generation's values at the context's first launch: start a context
     // just below their wrap limits
     long long res_call_base = 0, res_gen_base = 0;
@@ -141,6 +142,7 @@ struct EnvOpts {
         if (const char* e = getenv("OWGS_RES_IDLE_US")) res_idle_us = atoll(e);
         if (const char* e = getenv("OWGS_RES_LIFE_US")) res_life_us = atoll(e);
         if (const char* e = getenv("OWGS_RES_WATCH")) res_watch = atoi(e);
+        if (const char* e = getenv("OWGS_RES_EAGER")) res_eager = atoi(e);
         if (const char* e = getenv("OWGS_RES_CALL_BASE")) res_call_base = atoll(e);
         if (const char* e = getenv("OWGS_RES_GEN_BASE")) res_gen_base = atoll(e);
         feat_all = getenv("OWGS_FEAT_ALL") != nullptr;  // the general engine for every launch (A/B diagnostics)
@@ -357,6 +359,7 @@ struct owgs_ctx {
     size_t res_in_cap = 0, res_out_cap = 0;
     int32_t res_call = 0;
     bool res_alive = false;
+    bool res_last_served = false;  // the previous owgs_process_batch call was served by the resident engine
     int32_t res_stage = 0;
     int64_t res_n_calls = 0, res_n_launches = 0, res_n_bails = 0, res_n_chained = 0, res_n_life = 0;
     int64_t res_n_watch_calls = 0;  // served calls while watched pairs existed
@@ -3129,8 +3132,13 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
         int served = 0;
         const int rr = res_process(c, n_runs, rel_off, rel_invoker, rel_action, rel_flags, pub_off, pub_action, seq,
                                    seq_base, out_invoker, out_flags, &served);
-        if (rr || served) return rr;
+        if (rr || served) {
+            c->res_last_served = served != 0;
+            return rr;
+        }
     }
+    const bool relaunch = c->res_last_served && env_opts().res_eager > 0;
+    c->res_last_served = false;
     {
         const int q = res_quiesce(c);
         if (q) return q;
@@ -3269,7 +3277,14 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
     if (NR && rel_flags) memcpy(rel_flags, HO + q_rf, (size_t)NR);
     rc = w_refresh(c, s);
     if (rc) return rc;
-    return e ? check_err_word(c) : OWGS_OK;
+    if (e) return check_err_word(c);
+    // small calls came before this one: launch the resident engine again now (asynchronous), so that it has loaded
+    // the state before the next small call rings instead of that call paying the launch and the load
+    if (relaunch && res_eligible(c, 1, 0, 1, false) && c->res_in && c->res_out && !c->res_alive) {
+        const int rl = res_launch(c);
+        if (rl) return rl;
+    }
+    return OWGS_OK;
 }
 
 int owgs_snapshot(owgs_ctx* c) {

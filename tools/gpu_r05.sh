@@ -82,7 +82,10 @@ for l in d['legs']:
     r=l.get('resident') or {}; s=max(1, r.get('served', 0))
     if l['mode'] == 'fused-reset':
         print('$n', l['mode'], 'resident', l['resident_fraction_after'], 'p50 before/after', round(l['p50_us_before'],1), round(l['p50_us_after'],1), 'exact', l['bit_exact']); continue
-    print('$n', l['mode'], l['drain'], 'p50', round(l['p50_us'],1), 'p99', round(l.get('p99_us'),1), round(l['decisions_per_s']/1e6,2), 'M/s pub', round(r.get('publish_cycles',0)/s), 'alone', round(r.get('alone_cycles',0)/s), 'exact', l['bit_exact'])
+    x = ''
+    if l['mode'] == 'fused-mixed':
+        x = 'after_chain %.1f steady %.1f gt1024 %.1f' % (l['p50_us_le1024_after_chain'], l['p50_us_le1024_steady'], l['p50_us_gt1024'])
+    print('$n', l['mode'], l['drain'], 'p50', round(l['p50_us'],1), 'p99', round(l.get('p99_us'),1), round(l['decisions_per_s']/1e6,2), 'M/s pub', round(r.get('publish_cycles',0)/s), 'alone', round(r.get('alone_cycles',0)/s), 'exact', l['bit_exact'], x)
 " | tee -a $O/abenv.txt
         done
       done ;;
