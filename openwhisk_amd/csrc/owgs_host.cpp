@@ -3251,13 +3251,6 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
         if (!rc) rc = run_engine(c, A, s);
     }
     if (rc) return rc;
-    // small calls came before this one: launch the resident engine again now, queued behind this call's kernels on
-    // the GPU (its launch overlaps them on the host), so that it has loaded the state before the next small call
-    // rings instead of that call paying the launch and the load
-    if (relaunch && c->w_cap <= 0 && res_eligible(c, 1, 0, 1, false) && c->res_in && c->res_out && !c->res_alive) {
-        const int rl = res_launch(c);
-        if (rl) return rl;
-    }
     HIPCHK(c, hipMemcpyAsync(c->d_pout.p + q_err, c->d_err.p, 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(c, hipMemcpyAsync(c->h_pout, c->d_pout.p, out_bytes, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
@@ -3267,12 +3260,7 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
     if (fused && (e & OWGS_ERR_RELRISK)) {
         // the releases could push a slot out of the engine's range: the engine stopped before touching anything, so
         // the call runs again through the per-run path, whose release kernels apply ForcibleSemaphore's bound
-        // release by release (FS:48-50) exactly as owgs_release_batch does (an engine launched above holds the
-        // untouched state: it is stopped first, writing that state back)
-        {
-            const int q = res_quiesce(c);
-            if (q) return q;
-        }
+        // release by release (FS:48-50) exactly as owgs_release_batch does
         HIPCHK(c, hipMemsetAsync(c->d_err.p, 0, sizeof(int32_t), s));
         HIPCHK(c, hipMemsetAsync(c->f_bound.p, 0, c->f_bound.n * 8, s));
         rc = process_runs(c, n_runs, rel_off, pub_off, d_run, d_pa, d_ri, d_ra, d_sq, seq_base, d_out, d_fl, d_rf, s);
@@ -3289,7 +3277,16 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
     if (NR && rel_flags) memcpy(rel_flags, HO + q_rf, (size_t)NR);
     rc = w_refresh(c, s);
     if (rc) return rc;
-    return e ? check_err_word(c) : OWGS_OK;
+    if (e) return check_err_word(c);
+    // small calls came before this one: launch the resident engine again now, so that it loads the state while the
+    // host returns instead of the next small call paying the launch and the load.  Only here, after this call's
+    // stream has drained: an operation queued behind the engine on a hardware queue the streams share would wait for
+    // its idle exit
+    if (relaunch && res_eligible(c, 1, 0, 1, false) && c->res_in && c->res_out && !c->res_alive) {
+        const int rl = res_launch(c);
+        if (rl) return rl;
+    }
+    return OWGS_OK;
 }
 
 int owgs_snapshot(owgs_ctx* c) {
