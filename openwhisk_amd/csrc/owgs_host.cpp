@@ -3443,13 +3443,14 @@ int owgs_selftest(owgs_ctx* c) {
 
 int owgs_read_stats(owgs_ctx* c, uint64_t* out, int32_t cap) {
     if (!c || !out) return OWGS_EINVAL;
-    (void)hipSetDevice(c->cfg.device);  // (counters and events only: the resident engine keeps running)
+    // a live resident engine is stopped first (it writes the state back): a copy on the context's stream could
+    // otherwise sit behind it on a hardware queue the two streams share until its idle exit
+    OWGS_ENTER(c);
     {
         const int ro_ = order_on(c, c->stream);
         if (ro_) return ro_;
     }
     u64 v[OWGS_NSTATS];
-    // (the context's stream only: a live resident engine runs on its own stream and is not waited for)
     HIPCHK(c, hipMemcpyAsync(v, c->d_stats.p + (size_t)c->stats_last * OWGS_NSTATS, sizeof(v), hipMemcpyDeviceToHost,
                              c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
