@@ -129,6 +129,7 @@ struct EnvOpts {
     // the resident engine's speculative walks: walk steps each publish probes on its own before the in-order
     // validation (0: every decision walked one at a time)
     int res_spec = 16;
+    int res_cspec = 0;  // OWGS_RES_CSPEC: walk steps a concurrent publish speculates (0: max(4, res_spec / 4))
     int res_split = 1;  // OWGS_RES_SPLIT: helper waves (0-3) for the concurrent speculation; 0 = wave 0 itself
     // owgs_replay_device through the resident engine's stream mode (one wave deciding, speculative walks) instead of
     // the chunked engine, where it applies (identity pools, no watched pairs)
@@ -137,6 +138,7 @@ struct EnvOpts {
         if (const char* e = getenv("OWGS_SPEC_REPLAY")) spec_replay = atoi(e);
         if (const char* e = getenv("OWGS_RESIDENT")) res = atoi(e);
         if (const char* e = getenv("OWGS_RES_SPEC")) res_spec = atoi(e);
+        if (const char* e = getenv("OWGS_RES_CSPEC")) res_cspec = atoi(e);
         if (const char* e = getenv("OWGS_RES_SPLIT")) res_split = atoi(e);
         if (const char* e = getenv("OWGS_RES_MAX")) res_max = atoi(e);
         if (const char* e = getenv("OWGS_RES_IDLE_US")) res_idle_us = atoll(e);
@@ -1232,6 +1234,7 @@ static int res_launch(owgs_ctx* c) {
     a.idle_ticks = env_opts().res_idle_us * 100;  // s_memrealtime: 100 MHz
     a.life_ticks = std::max(0ll, env_opts().res_life_us) * 100;
     a.spec = std::max(0, env_opts().res_spec);
+    a.cspec = std::max(0, env_opts().res_cspec);
     a.hsplit = std::max(0, std::min(3, env_opts().res_split));
     a.w = watch_args(c);
     a.w_sidx = c->d_w_sidx.p;
@@ -2710,6 +2713,7 @@ static int spec_replay(owgs_ctx* c, int32_t nb, const int64_t* acq_off, const in
     a.gen_base = ++c->res_gen_seen;
     c->res_gen_seen += (uint32_t)n_rel + 1;
     a.spec = std::max(0, env_opts().res_spec);
+    a.cspec = std::max(0, env_opts().res_cspec);
     a.hsplit = std::max(0, std::min(3, env_opts().res_split));
     a.smode = 1;
     a.s_nb = nb;

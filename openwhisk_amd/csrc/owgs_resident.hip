@@ -705,7 +705,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             int cpos = cw ? mod_fast(l_home, l_n, __builtin_amdgcn_rcpf((float)l_n)) : 0, cst = 0;
                             // 4 walk steps per round: their permits and Bloom-filter words read together, the map
                             // probed only where the filter says the key may be
-                            const int cbudget = max(4, A.spec >> 2);  // (8 steps measured slower: longer rounds)
+                            const int cbudget = A.cspec > 0 ? A.cspec : max(4, A.spec >> 2);  // (8 steps measured slower)
                             while (__ballot(cw)) {
                                 if (cw) {
                                     int idk[4], pvk[4];

@@ -74,7 +74,7 @@ for l in d['legs']:
       for i in 1 2; do
         for v in ${ABVALS:-1 0}; do
           n=${ABENV}_${v}_$i
-          env ${ABENV}=$v timeout -k 10 200 python tools/shim_leg.py --drains ${DRAINS:-64,512} --modes fused > $O/shim_$n.json 2> $O/shim_$n.err || { tail -5 $O/shim_$n.err; stop abenv 1; }
+          env ${ABFIX} ${ABENV}=$v timeout -k 10 200 python tools/shim_leg.py --drains ${DRAINS:-64,512} --modes fused > $O/shim_$n.json 2> $O/shim_$n.err || { tail -5 $O/shim_$n.err; stop abenv 1; }
           python3 -c "
 import json
 d=json.load(open('$O/shim_$n.json'))
