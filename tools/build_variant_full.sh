@@ -5,7 +5,7 @@ set -e
 cd "$(dirname "$0")/../openwhisk_amd"
 mkdir -p variants build/variants/$1
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $2"
-for f in owgs_kernels owgs_engine_narrow owgs_watch owgs_fused owgs_resident owgs_state owgs_acks owgs_health owgs_msgs; do
+for f in owgs_kernels owgs_engine_narrow owgs_watch owgs_fused owgs_resident owgs_seq owgs_state owgs_acks owgs_health owgs_msgs; do
   /opt/rocm/bin/hipcc $F -c -o build/variants/$1/$f.o csrc/$f.hip &
 done
 /opt/rocm/bin/hipcc $F -x hip -c -o build/variants/$1/owgs_host.o csrc/owgs_host.cpp
