@@ -317,11 +317,15 @@ def shim_path(w, o_inv, dev_index, drains=(64, 512, 4096), budget_jobs=(120_000,
             py_us = np.array(lat) * 1e6     # the same calls seen from Python (+ ctypes' argument conversion)
             rs1 = b.resident_stats()
             fill = b.resident_table_fill()
+            served, chained = rs1["served"] - rs0["served"], rs1["chained"] - rs0["chained"]
             legs.append({"drain": drain, "mode": mode, "jobs": n_jobs, "calls": len(lat), "publishes": int(n_pub),
                          "p50_us": float(np.percentile(lat_us, 50)), "p99_us": float(np.percentile(lat_us, 99)),
                          "decisions_per_s": n_pub / max(float(np.sum(lat_us)) * 1e-6, 1e-9),
                          "py_p50_us": float(np.percentile(py_us, 50)), "py_p99_us": float(np.percentile(py_us, 99)),
                          "bit_exact": exact,
+                         # which engine served the leg's calls (a fused leg of drains over 1,024 jobs is all launch chain)
+                         "engine": ("per-run launches" if mode == "calls" else "resident" if chained == 0 else
+                                    "launch chain" if served == 0 else "resident + launch chain"),
                          # owgs_process_batch's paths in this leg: resident engine calls / launches, launch-chain calls
                          "resident": {k: rs1[k] - rs0[k] for k in rs1 if k not in ("alive", "last_call_ns")},
                          "map_fill_max": fill[0], "map_deleted_max": fill[1],
