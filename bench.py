@@ -72,6 +72,10 @@ def parse(argv=None):
                     help="single-GPU measurement of one shard of a larger cluster: clusterSize (default gpus x "
                          "shards-per-gpu)")
     ap.add_argument("--shard", type=int, default=0, help="with --cluster-size: which controller shard this GPU runs")
+    ap.add_argument("--rccl", action="store_true",
+                    help="N = 1 with --health-churn: initialise a one-rank RCCL ('nccl') process group and run the "
+                         "per-batch health all-gathers through it instead of a local copy (the multi-GPU cadence's "
+                         "collective, streams and ordering on one GPU)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher/collective plumbing only (gloo, CPU): no replay, value null (tests)")
     return ap.parse_args(argv)
@@ -192,19 +196,22 @@ def cpu_baseline(args, w0, n_ctl, shard0):
     n1, t1 = _oracle_replay([w0], reps=1)
     reps = max(1, min(20, int(10.0 / max(t1, 1e-3))))
     n, dt = _oracle_replay([w0], reps=reps)
-    out = {"value": n / dt, "unit": "decisions/s", "cores": 1, "kind": "port",
+    one = {"value": n / dt, "unit": "decisions/s", "cores": 1,
            "sample": f"shard {shard0} of {n_ctl} of the bench's {args.config} workload ({len(w0.stream.act)} "
                      f"activations) replayed {reps}x on 1 core (oracle/owsched_oracle.c, -O3), {dt:.2f} s"}
+    out = dict(one, kind="port", single_core=one)
     T = max(1, min(args.cpu_threads, os.cpu_count() or 1))
     if T > 1:
+        # the line leads with the whole host: T cores replaying T independent shard streams of
+        # the same cluster (T controllers on one host, the reference's own scaling model); one core stays beside it
         ws = [shard_workload(args, t % max(n_ctl, 1), max(n_ctl, 1)) if n_ctl > 1 else
               shard_workload(args, 0, 1) for t in range(T)]
         nt, dtt = _oracle_replay(ws, reps=1)
-        out["parallel"] = {"value": nt / dtt, "unit": "decisions/s", "cores": T,
-                           "sample": f"{T} threads, one shard stream each, {dtt:.2f} s wall"}
-        # (also in the sample text, which every reader of the line keeps: the whole host against the one GPU)
-        out["sample"] += (f"; {T} host threads replaying {T} independent shard streams: {nt / dtt / 1e6:.1f} M "
-                          f"decisions/s aggregate")
+        out.update(value=nt / dtt, cores=T,
+                   sample=(f"{T} host threads replaying {T} independent shard streams of the bench's {args.config} "
+                           f"workload ({len(w0.stream.act)} activations each), {dtt:.2f} s wall: "
+                           f"{nt / dtt / 1e6:.1f} M decisions/s aggregate; one core: {n / dt / 1e6:.2f} M/s "
+                           f"(single_core)"))
     return out
 
 
@@ -525,6 +532,10 @@ def main():
         dist.init_process_group("nccl", init_method="env://")
     else:
         torch.cuda.set_device(0)
+        if args.rccl:  # one rank over RCCL: the collective the N > 1 cadence issues, on this lease's one GPU
+            import torch.distributed as dist
+
+            dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from openwhisk_amd import GpuShardingContainerPoolBalancer
@@ -578,13 +589,15 @@ def main():
             the batch, so its all-gather runs on a side stream while batch k's engine runs (one batch ahead, its own
             buffer); the engine stream waits only for the exchange of the batch it is about to apply."""
             s, b = self.s, self.b
-            main = torch.cuda.current_stream()
+            # the stream the library runs this shard on (self.sp; torch's current one when the shard has none): every
+            # wait for an exchange is that stream's, and the side stream waits for it before overwriting its buffers
+            eng = self.stream if self.stream is not None else torch.cuda.current_stream()
             if getattr(self, "hside", None) is None:
                 self.hside = torch.cuda.Stream()
                 self.hflat = [torch.empty(hx.world * len(self.w.inv_status), dtype=torch.uint8, device=dev)
                               for _ in range(s.n_batches)]
                 self.hev = [torch.cuda.Event() for _ in range(s.n_batches)]
-            self.hside.wait_stream(main)  # (the previous step has read every buffer it overwrites)
+            self.hside.wait_stream(eng)  # (the previous step has read every buffer it overwrites)
             agreed = [None] * s.n_batches
 
             def gather(k):
@@ -599,7 +612,7 @@ def main():
                 for k in range(s.n_batches):
                     if k + 1 < s.n_batches:
                         gather(k + 1)  # in flight while batch k's engine runs
-                    main.wait_event(self.hev[k])
+                    eng.wait_event(self.hev[k])
                     h = agreed[k]
                     b.update_health_device(len(self.w.inv_status), h.data_ptr(), self.sp)
                     b.replay_device_span(s.acq_off[k], s.acq_off[k + 1], s.rel_off[k], s.rel_off[k + 1],
@@ -622,7 +635,7 @@ def main():
                 if j + 1 < len(groups):
                     for k in range(*groups[j + 1]):
                         gather(k)  # in flight while this group's engine runs
-                main.wait_event(self.hev[g1 - 1])
+                eng.wait_event(self.hev[g1 - 1])
                 b.replay_device_group(s.acq_off[g0:g1 + 1], s.rel_off[g0:g1 + 1], self.d_act.data_ptr(),
                                       self.d_aid.data_ptr(), s.seq_base, self.d_out.data_ptr(), self.d_fl.data_ptr(),
                                       self.d_rf.data_ptr(), self.hall[g0].data_ptr(), stride, nid, self.sp)
@@ -631,7 +644,8 @@ def main():
 
     shards = [Shard(g, k % MULTI_MAX == 0) for k, g in enumerate(shard_ids)]
     w, s, b = shards[0].w, shards[0].s, shards[0].b
-    hx = cluster.HealthExchange(dist, torch.from_numpy(w.inv_status.copy()).to(dev), world)
+    hx = cluster.HealthExchange(dist, torch.from_numpy(w.inv_status.copy()).to(dev), world,
+                                collective=world > 1 or (dist is not None and args.rccl))
     # health between batches (configs[4]) for one shard per GPU; several shards per GPU keep one exchange per step
     per_batch = K == 1 and (world > 1 or args.health_churn)
     if per_batch and dist is not None and world > 1:
@@ -657,7 +671,7 @@ def main():
     def launch_all(timing=None):
         if per_batch:
             shards[0].replay_batches(hx, timing)
-            n_gathers[0] += s.n_batches if world > 1 else 0
+            n_gathers[0] += s.n_batches if hx.collective else 0
             return
         h = None
         if world > 1:  # the health topic every controller consumes (SCPB:355): one all-gather per step
@@ -796,6 +810,8 @@ def main():
                                    f"{s.n_batches} engine launches per step (1 % of invokers unresponsive, changing "
                                    "every batch)")) if per_batch else "static, one exchange per step",
                        "health_disagreeing_ranks": int(disagree),
+                       "health_exchange": ("RCCL all_gather_into_tensor" if hx.collective else
+                                           "local copy (one rank, no process group)"),
                        "parallelism": f"{n_ctl} controller shard(s), {K} per GPU, {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,

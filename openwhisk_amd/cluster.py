@@ -35,10 +35,16 @@ def shard_workload(name: str, rank: int, world: int, n_activations: int | None =
 class HealthExchange:
     """All-gathers the invoker health vector (uint8 InvokerState codes) across controller shards."""
 
-    def __init__(self, dist, health, world: int):
+    def __init__(self, dist, health, world: int, collective: bool | None = None):
+        """`collective`: issue the all-gather through `dist` (default: when world > 1).  At world 1 with a real
+        process group (bench.py --rccl) it runs RCCL's all-gather on one rank, so the N = 1 lease exercises the same
+        collective, streams and ordering as the multi-GPU cadence."""
         import torch
 
         self.dist, self.health, self.world = dist, health, world
+        self.collective = (world > 1) if collective is None else bool(collective)
+        if self.collective and dist is None:
+            raise ValueError("a collective health exchange needs a process group")
         self.flat = torch.empty(world * health.numel(), dtype=health.dtype, device=health.device)
         self.gathered = self.flat.view(world, health.numel())
 
@@ -46,7 +52,7 @@ class HealthExchange:
         """All-gathers this shard's health view (default: the initial vector) and returns the agreed one (rank 0's
         row) as a tensor on the health device."""
         v = self.health if view is None else view
-        if self.world > 1:
+        if self.collective:
             self.dist.all_gather_into_tensor(self.flat, v)
         else:
             self.gathered[0].copy_(v)
@@ -55,7 +61,7 @@ class HealthExchange:
     def exchange_into(self, view, flat):
         """As exchange, into a caller's buffer of world * n bytes (one per batch: exchanges of later batches can run
         ahead on another stream while earlier batches still read theirs); returns the agreed row (rank 0's)."""
-        if self.world > 1:
+        if self.collective:
             self.dist.all_gather_into_tensor(flat, view)
         else:
             flat[:view.numel()].copy_(view)

@@ -552,6 +552,41 @@ def test_multi_shard_single_launch_parity(shard_ids, n_shards, n_act):
             assert np.array_equal(st.permits(), b.permits())
 
 
+def test_multi_shard_replay_with_a_shard_on_the_large_state_engine():
+    """owgs_replay_device_multi with one shard whose maxConcurrent is beyond the on-chip map's field (> 4,095, so its
+    slot state lives on the large-state engine, section 5.7) next to ordinary shards: the call routes every shard through
+    its own replay (no shared engine launch can hold the large shard) and each is bit-exact with its oracle (ADVICE
+    r05: the large shard used to go through the on-chip engine with its maxConcurrent masked to 12 bits)."""
+    import torch
+
+    dev = torch.device("cuda", 0)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
+    shards = []
+    for g, kw in ((0, {}), (1, dict(conc_frac=0.3, conc_range=(4_000, 6_000))), (2, {})):
+        w = W.config("headline", shard=g, n_shards=4, n_activations=60_000, n_invokers=2000, **kw)
+        b = gpu_for(w)
+        s = w.stream
+        d = [t(s.acq_off, np.int64), t(s.act, np.int32), t(s.rel_off, np.int64),
+             t(s.rel_aid if len(s.rel_aid) else np.zeros(1), np.int64),
+             torch.empty(len(s.act), dtype=torch.int32, device=dev),
+             torch.empty(len(s.act), dtype=torch.uint8, device=dev),
+             torch.empty(max(len(s.rel_aid), 1), dtype=torch.uint8, device=dev)]
+        io = (s.n_batches, d[0].data_ptr(), d[1].data_ptr(), len(s.act), d[2].data_ptr(), d[3].data_ptr(),
+              len(s.rel_aid), s.seq_base, d[4].data_ptr(), d[5].data_ptr(), d[6].data_ptr())
+        shards.append((w, b, d, io))
+    assert max(a.max_concurrent for a in shards[1][0].actions) > 4095
+    torch.cuda.synchronize()
+    GpuShardingContainerPoolBalancer.replay_device_multi([(b, io) for _, b, _, io in shards])
+    torch.cuda.synchronize()
+    for w, b, d, _ in shards:
+        st = O.state_for(w)
+        o_inv, o_fl, o_rf = st.replay(w.stream)
+        assert np.array_equal(o_inv, d[4].cpu().numpy()), w.name
+        assert np.array_equal(o_fl, d[5].cpu().numpy())
+        assert np.array_equal(o_rf, d[6].cpu().numpy()[: len(o_rf)])
+        assert np.array_equal(st.permits(), b.permits())
+
+
 # ----------------------------------------------------------------------------------------------- unbounded map
 @pytest.mark.parametrize("kw", [
     # up to 19.5k live (invoker, fqn) entries: most of the map lives in the HBM overflow
@@ -788,8 +823,18 @@ def test_group_replay_with_per_batch_health_matches_oracle(cfg, kw, group, clust
     assert np.array_equal(d_fl.cpu().numpy(), o_fl)
     assert np.array_equal(d_rf.cpu().numpy()[:len(s.rel_aid)], o_rf[:len(s.rel_aid)])
     assert np.array_equal(b.permits(), st.permits())
-    # the context's health after the call is the last batch's (a later publish sees it)
-    assert np.array_equal(b.resident_stats()["alive"], 0)
+    assert b.resident_stats()["alive"] == 0
+    # the context's health after the call is the last batch's row (the oracle's last update_invokers): publishes after
+    # it walk past that row's unusable invokers and draw the fallback from its healthy count (SCPB:417-424)
+    rng = np.random.default_rng(11)
+    probe = rng.integers(0, len(w.actions), 4000).astype(np.int32)
+    seq0 = int(s.seq_base) + n + 1
+    g_p, g_pf = b.publish(probe, seq=np.arange(seq0, seq0 + len(probe), dtype=np.uint64))
+    o_p = np.array([st.publish(int(a), seq0 + i) for i, a in enumerate(probe)], dtype=np.int64)
+    assert np.array_equal(g_p, o_p[:, 0]) and np.array_equal(g_pf, o_p[:, 1])
+    assert np.array_equal(b.permits(), st.permits())
+    last_unusable = np.nonzero(sched[-1] != 0)[0]
+    assert not np.isin(g_p[g_p >= 0], w.inv_ids[last_unusable]).any()  # (forced ones too: healthyInvokers)
 
 
 # ----------------------------------------------------------------------------------------------- large-state engine

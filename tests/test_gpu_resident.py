@@ -340,6 +340,50 @@ def test_resident_doorbell_and_cursor_generation_wrap():
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
 
+_SPEC_THEN_CALLS_SCRIPT = r"""
+import sys
+sys.path[:0] = [{root!r}, {oracle!r}, {tests!r}]
+import types
+import numpy as np
+import test_gpu_resident as T
+from openwhisk_amd import workload as W
+w = W.config("c2", n_activations=60_000)
+s = w.stream
+sh = T.Shim(w)
+k = s.n_batches // 2
+pre = types.SimpleNamespace(n_batches=k, acq_off=s.acq_off[:k + 1], act=s.act[:int(s.acq_off[k])],
+                            rel_off=s.rel_off[:k + 1], rel_aid=s.rel_aid[:int(s.rel_off[k])], seq_base=1 << 40)
+g_inv, g_fl, g_rf = sh.g.replay(pre)
+assert sh.g.stream_mode_stats() is not None  # the replay ran in the resident engine's stream mode
+o_inv, o_fl, o_rf = sh.o.replay(pre)
+assert np.array_equal(g_inv, o_inv) and np.array_equal(g_fl, o_fl) and np.array_equal(g_rf, o_rf)
+rng = np.random.default_rng(6)
+while not sh.done():
+    sh.call(int(rng.integers(20, 400)))
+st = sh.g.resident_stats()
+assert st["served"] == sh.calls and st["chained"] == 0, st
+assert np.array_equal(sh.g.permits(), sh.o.permits())
+print("ok", sh.calls)
+"""
+
+
+def test_stream_mode_replay_then_resident_calls():
+    """A stream-mode replay (OWGS_SPEC_REPLAY=1: the resident engine replays whole batches and stores walk cursors
+    under generations 1..n) followed by the shim's first owgs_process_batch on the same context: the first resident
+    launch must start above every generation already stored, or stale cursors would skip walk steps that fit again
+    after later releases.  Every call bit-exact with the oracle; the switch is read once per process, so
+    a child process."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    code = _SPEC_THEN_CALLS_SCRIPT.format(root=root, oracle=os.path.join(root, "oracle"), tests=here)
+    env = dict(os.environ, OWGS_SPEC_REPLAY="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
 def test_resident_lifetime_bound_and_other_contexts_on_shared_queues():
     """The resident engine holds its stream's hardware queue while it runs, and GPU_MAX_HW_QUEUES (4) makes the
     streams of several contexts share queues: three contexts in one process, each driven by its own thread -- one
