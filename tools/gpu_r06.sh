@@ -137,6 +137,22 @@ for l in d['legs']:
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/rcclprof -o run --output-format csv -- \
         python3 bench.py --health-churn --rccl ${CHURNARGS} --steps 3 --warmup 1 --no-cpu-baseline --no-check --no-h2d --no-shim-path > $O/rcclprof.log 2>&1
       rc=$?; tail -1 $O/rcclprof.log | cut -c1-200; [ $rc -eq 0 ] || stop rcclprof $rc ;;
+    capparity)  # the parity file with the memory-class engines forced on wherever the classes fit (OWGS_CAPC=1)
+      OWGS_CAPC=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread > $O/pytest_cap.log 2>&1
+      rc=$?; tail -2 $O/pytest_cap.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/pytest_cap.log | head -20; stop capparity $rc; } ;;
+    capab)  # engine rates per config with the memory-class counts off / on (OWGS_CAPC), alternating, same library
+      for i in 1 2; do
+        for v in ${CAPVALS:-0 1}; do
+          echo "-- OWGS_CAPC=$v run $i" >> $O/capab.txt
+          OWGS_CAPC=$v REPS=3 timeout -k 10 400 python -u tools/prof_phases.py ${ABCFGS:-c3 headline:0/8 headline:0/4 headline:0/2 headline c2 c4} > $O/capab_${v}_$i.log 2>&1
+          rc=$?; grep -v amdgpu.ids $O/capab_${v}_$i.log | grep -v cycles/activation | cut -c1-150 | tee -a $O/capab.txt; [ $rc -eq 0 ] || stop capab $rc
+        done
+      done ;;
+    shimtrace)  # kernel + copy trace of the shim leg's fused calls at one drain size (where a chained call's time goes)
+      rm -rf $O/shimtrace
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/shimtrace -o run --output-format csv -- \
+        python3 tools/shim_leg.py --drains ${DRAINS:-4096} --modes fused > $O/shimtrace.json 2> $O/shimtrace.err
+      rc=$?; cut -c1-300 $O/shimtrace.json; [ $rc -eq 0 ] || { tail -5 $O/shimtrace.err; stop shimtrace $rc; } ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
