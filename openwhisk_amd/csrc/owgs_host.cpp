@@ -134,11 +134,7 @@ struct EnvOpts {
     // owgs_replay_device through the resident engine's stream mode (one wave deciding, speculative walks) instead of
     // the chunked engine, where it applies (identity pools, no watched pairs)
     int spec_replay = 0;
-    // OWGS_CAPC: the chunked engine's memory-class counts (OWGS_F_CAP): 0 off, 1 on wherever the classes fit, -1
-    // (default) on for contexts whose slots are small against their largest class (cls_prepare)
-    int capc = 0;
     EnvOpts() {
-        if (const char* e = getenv("OWGS_CAPC")) capc = atoi(e);
         if (const char* e = getenv("OWGS_SPEC_REPLAY")) spec_replay = atoi(e);
         if (const char* e = getenv("OWGS_RESIDENT")) res = atoi(e);
         if (const char* e = getenv("OWGS_RES_SPEC")) res_spec = atoi(e);
@@ -345,11 +341,6 @@ struct owgs_ctx {
     int32_t w_cap = 0, w_live = 0;
     int32_t stats_par = 0, stats_last = 0;  // d_stats holds two counter blocks: the next launch's, the last one's
     int32_t cw_cache = 0;  // chunk width of the current state and actions (0: recompute)
-    // memory classes of the OWGS_F_CAP engines (cls_prepare), rebuilt with the chunk width
-    bool cls_on = false;
-    uint32_t cls_gen = 0, cls_seen = ~0u;  // chunk-width recomputations; the one the table belongs to
-    std::vector<int32_t> cls_host;
-    DevBuf<int32_t> d_cls;
     bool any_conc = false;  // some registered action has maxConcurrent > 1 (the engine needs its map code)
     int32_t variant = 0;   // engine geometry: 0 wide chunks, 1 narrow (large pools, owgs_engine_narrow.hip)
     // owgs_process_batch: pinned staging (inputs, outputs) and their device copies
@@ -831,63 +822,7 @@ static int32_t chunk_width(owgs_ctx* c) {
     const int v = env_opts().cw;
     if (v >= 64 && v <= OWGS_WL) cw = v;
     c->cw_cache = cw;
-    ++c->cls_gen;  // (the memory-class table follows the same state and actions)
     return cw;
-}
-
-// Memory classes of the OWGS_F_CAP engines: the distinct limits of the live maxConcurrent == 1 actions
-// (at most OWGS_NCLS), placed in 16 slots by a multiplier that separates them.  On by default where a slot's mean user
-// memory is below 4x the largest class -- fragmented slots, whose walks often fail (configs[4]'s shards: 2 GiB slots
-// against 2 GiB actions); OWGS_CAPC=1 turns it on wherever the classes fit, 0 off.  Rebuilt with the chunk width.
-static bool cls_prepare(owgs_ctx* c, hipStream_t s) {
-    (void)chunk_width(c);
-    if (c->cls_seen == c->cls_gen) return c->cls_on;
-    c->cls_seen = c->cls_gen;
-    c->cls_on = false;
-    const int mode = env_opts().capc;
-    if (mode == 0 || c->pool_mode != 0 || c->large) return false;
-    std::vector<int32_t> ms;
-    for (size_t a = 0; a < c->a_mem.size(); ++a)
-        if (c->a_live[a] && c->a_maxc[a] == 1) ms.push_back(c->a_mem[a]);
-    std::sort(ms.begin(), ms.end());
-    ms.erase(std::unique(ms.begin(), ms.end()), ms.end());
-    if (ms.empty() || ms.size() > (size_t)OWGS_NCLS) return false;
-    if (mode < 0) {
-        double slot_mb = 0;
-        const int32_t nm = std::min<int32_t>(c->nm, (int32_t)c->mem.size());
-        for (int32_t i = 0; i < nm; ++i)
-            slot_mb += (double)std::max<int64_t>(c->cfg.min_memory_bytes, c->mem[i] / std::max(c->cluster, 1)) / 1048576.0;
-        if (nm == 0 || slot_mb / nm >= 4.0 * ms.back()) return false;
-    }
-    uint32_t mult = 0;
-    for (uint32_t k = 0; k < 4096 && !mult; ++k) {
-        const uint32_t cand = (0x9E3779B1u + k * 0x632BE5ABu) | 1u;
-        uint32_t used = 0;
-        bool ok = true;
-        for (int32_t m : ms) {
-            const uint32_t q = ((uint32_t)m * cand) >> 28;
-            ok = ok && !((used >> q) & 1u);
-            used |= 1u << q;
-        }
-        if (ok) mult = cand;
-    }
-    if (!mult) return false;
-    std::vector<int32_t>& t = c->cls_host;
-    t.assign(OWGS_CLS_WORDS, 0);
-    for (int q = 0; q < 16; ++q) t[16 + q] = -1;
-    for (size_t j = 0; j < ms.size(); ++j) {
-        const int q = (int)(((uint32_t)ms[j] * mult) >> 28);
-        t[q] = ms[j];
-        t[32 + j] = q;
-        if (j > 0) t[16 + t[32 + j - 1]] = q;
-    }
-    t[40] = (int32_t)mult;
-    t[41] = (int32_t)ms.size();
-    if (c->d_cls.reserve(OWGS_CLS_WORDS) != hipSuccess ||
-        hipMemcpyAsync(c->d_cls.p, t.data(), OWGS_CLS_WORDS * sizeof(int32_t), hipMemcpyHostToDevice, s) != hipSuccess)
-        return false;
-    c->cls_on = true;
-    return true;
 }
 
 // chunk records of n_act activations (act != null: registered actions; else explicit per-activation walks)
@@ -965,10 +900,6 @@ static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s, bool launch
     // overflow can only come from such actions), the general pool / sequence code when the call needs it
     A.feat |= (c->any_conc ? OWGS_F_CONC : 0) | ((c->pool_mode != 0 || A.seq != nullptr) ? OWGS_F_GEN : 0);
     if (env_opts().feat_all) A.feat = OWGS_F_ALL;  // diagnostics: always the general engine
-    if (!(A.feat & OWGS_F_GEN) && cls_prepare(c, s)) {  // the memory-class counts (identity pools)
-        A.feat |= OWGS_F_CAP;
-        A.cls = c->d_cls.p;
-    }
     A.geom = OWGS_GEOM_TAG(variant_wl(c));
     if (!launch) return OWGS_OK;  // owgs_replay_device_multi launches every shard's engine at once
     HIPCHK(c, hipEventRecord(c->ev_engine[0], s));  // brackets exactly the engine launch (owgs_engine_ms)

@@ -52,8 +52,6 @@
 #define OWGS_CTC 4096                  // concurrency-table capacity (entries, power of two)
 #endif
 #define OWGS_LDS_BYTES (160 * 1024)
-#define OWGS_NCLS 8                    // memory classes tracked by the OWGS_F_CAP engines
-#define OWGS_CLS_WORDS 42              // their table (OwgsEngineArgs::cls)
 
 // --------------------------------------------------------------------------------------------- action meta
 #define OWGS_AM_POS_MASK 0x7FFFu       // home / step (pool positions < 32768)
@@ -202,12 +200,6 @@ struct OwgsEngineArgs {
     // with a new health vector, SCPB:512-551) at hwords + b * hstride, or null
     const uint32_t* hwords;
     int32_t hstride;
-    // memory classes (OWGS_F_CAP): the distinct memory limits of the context's maxConcurrent == 1 actions, at most
-    // OWGS_NCLS, in an HBM table of OWGS_CLS_WORDS words: [0, 16) the class of each of 16 slots (its memory limit, 0 =
-    // none; a limit m sits in slot (m * mult) >> 28, the host picks an injective multiplier), [16, 32) the slot of the
-    // next larger class (-1 for the largest), [32, 40) the slots in ascending order, [40] mult, [41] the class count.
-    // The engine keeps per pool and class the usable invokers whose permits cover the class
-    const int32_t* cls;
 };
 // Geometry/ABI tag.  The host and an engine object must agree on the chunk width (the stride of lix, the 10-bit lane
 // fields of the records), the primary table's capacity and the argument block's layout; the host builds the tag of the
@@ -224,9 +216,6 @@ struct OwgsEngineArgs {
 #define OWGS_F_CONC 1  // maxConcurrent > 1 actions: the concurrency map (primary + overflow), container scans
 #define OWGS_F_GEN 2   // explicit pool words (non-identity pools) or explicit per-activation sequence numbers
 #define OWGS_F_ALL 3
-// exact per-class counts of the usable invokers whose permits hold a maxConcurrent == 1 action of that memory class
-// (identity pools only; never with OWGS_F_GEN): a walk that must fail goes to the fallback without walking
-#define OWGS_F_CAP 4
 
 // generateHash(namespace, action) for n actions: out[i] = abs(h(ns_i) ^ h(path_i)), Int.MinValue kept (SCPB:370-372).
 // If raw != 0, out[i] = h(ns_i) only (String.hashCode of the first string set).

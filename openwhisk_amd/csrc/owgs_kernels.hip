@@ -176,11 +176,7 @@ __device__ __forceinline__ unsigned long long memtime_pinned() {
 #define CFT_LOG2 6
 #endif
 #define CFT_N (1 << CFT_LOG2)
-// memory classes (OWGS_F_CAP): the host's class table (OwgsEngineArgs::cls), then per pool and class slot the usable
-// invokers whose permits hold the class, exact at every pass start
-#define SC_CL (SC_CFT + 2 * CFT_N)
-#define SC_GE (SC_CL + OWGS_CLS_WORDS)
-#define SC_N (SC_GE + 32)
+#define SC_N (SC_CFT + 2 * CFT_N)
 
 // hot actions: every action with >= HOT_MIN lanes in a chunk gets a slot (assigned by the pre-pass; a concurrent
 // action only when no lane of the chunk shares its fqn@version with another action); per pass one wave walks its
@@ -1106,7 +1102,6 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     // stream) and the map code is gone; without F_GEN pools are identity pools and sequence numbers implicit
     constexpr bool kConc = (FEAT & OWGS_F_CONC) != 0;
     constexpr bool kGen = (FEAT & OWGS_F_GEN) != 0;
-    constexpr bool kCap = (FEAT & OWGS_F_CAP) != 0 && !kGen;  // (identity pools only)
     const int pool_mode = kGen ? A.pool_mode : 0;
     const unsigned long long* const seqp = kGen ? A.seq : nullptr;
     auto conc_of = [&](uint32_t y) -> int {  // maxConcurrent field of a record's meta.y, as this specialisation sees it
@@ -1165,9 +1160,8 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     uint32_t err = 0;
     constexpr int LB = 8;  // loads in flight per thread (the state load is latency-bound)
     if (tid < SC_N)
-        sc[tid] = (tid == SC_IRR || tid == SC_RRISK || tid >= SC_CL)
-                      ? 0
-                      : ((tid < 4 || tid >= SC_CFT) ? OWGS_WL : (tid < 6 ? (int)0x80000000 : 0));
+        sc[tid] = (tid == SC_IRR || tid == SC_RRISK) ? 0
+                                                     : ((tid < 4 || tid >= SC_CFT) ? OWGS_WL : (tid < 6 ? (int)0x80000000 : 0));
     if (A.rel_bound) lds_sync();  // (SC_RRISK is set below)
     bool rrisk = false;    // (owgs_process_batch) a slot the call's releases could push out of the LDS range
     for (int i0 = 0; i0 < n_slots; i0 += OWGS_NT * LB) {
@@ -1207,8 +1201,6 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
         for (int i = tid; i < nm + nb; i += OWGS_NT) pw[i] = (int16_t)A.pool_words[i];
     }
     lds_sync();
-    // (published by the barrier after the map load; a shard of a multi-shard launch without a table: no classes)
-    if (kCap && tid < OWGS_CLS_WORDS) sc[SC_CL + tid] = A.cls ? A.cls[tid] : 0;
     // releases that could leave the range: nothing has been written yet -- the host replays the call through the
     // ordered release kernels (which flag ForcibleSemaphore's overflow Error per release, FS:48-50)
     if (A.rel_bound && sc[SC_RRISK]) {  // (uniform)
@@ -1343,55 +1335,6 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     }
     // pools whose ids are all usable: the fallback's k-th healthy invoker is arithmetic (no rank/select reads)
     bool full_m = pool_mode == 0 && hm_e == nm, full_b = pool_mode == 0 && hb_e == nb;
-
-    // ---- memory classes (OWGS_F_CAP).  ge[pool][class] = the pool's usable invokers whose permits hold the class's
-    // memory limit m, kept exact through every permit change of a batch.  Permits only fall inside a batch, so a
-    // maxConcurrent == 1 walk of limit m whose pool has ge == 0 fails everywhere (SCPB:413-424) -- known before its
-    // first probe, where the bound U learns it only from the first such failure of each limit in each batch -- and one
-    // at rank r (r earlier unresolved lanes of its action, each taking one unit of the class's capacity before it or
-    // failing) fails when the pool's capacity sum floor(P / m) is at most r.  The capacity is bounded from the counts:
-    // an invoker whose permits lie in [m_j, m_j+1) (consecutive classes, the last one up to U) holds at most
-    // floor((m_j+1 - 1) / m) units.
-    auto cls_slot = [&](int m) -> int {  // the class slot of limit m, or -1 (not a class)
-        const int q = (int)(((uint32_t)m * (uint32_t)sc[SC_CL + 40]) >> 28);
-        return sc[SC_CL + q] == m ? q : -1;
-    };
-    auto cls_cap = [&](int pl, int sl, int m, int U) -> int {  // capacity bound of class slot sl (<= CAPMAX)
-        int g0 = sc[SC_GE + 16 * pl + sl], B = 0;
-        for (int j = sl; j >= 0 && B < CAPMAX;) {
-            const int nx = sc[SC_CL + 16 + j];
-            const int gn = nx >= 0 ? sc[SC_GE + 16 * pl + nx] : 0;
-            const int top = nx >= 0 ? min(sc[SC_CL + nx] - 1, U) : U;
-            B += (g0 - gn) * min(max(top, 0) / m, CAPMAX);
-            j = nx;
-            g0 = gn;
-        }
-        return min(B, CAPMAX);
-    };
-    auto cls_fails = [&](int pl, int m, int rr, int U) -> bool {  // a walk of limit m at rank rr must fail
-        const int sl = cls_slot(m);
-        return sl >= 0 && sc[SC_GE + 16 * pl + sl] <= rr && cls_cap(pl, sl, m, U) <= rr;
-    };
-    // the lanes with `on` moved invoker x's permits from v0 to v1 (one atomic each): per pool holding x and per class
-    // whose limit the move crosses, the count moves by sgn (-1 for a take, +1 for memory given back).  Wave-uniform:
-    // every lane of the wave calls it.
-    auto cls_track = [&](bool on, int x, int v0, int v1, int sgn) {
-        if (!__ballot(on)) return;
-        const int nc = sc[SC_CL + 41];
-        const bool us = on && v0 < OWGS_PLIM;
-        const bool inm = us && x < nm, inb = us && x >= A.n_ids - nb;
-        const int lo = min(v0, v1), hi = max(v0, v1);
-        for (int q = 0; q < nc; ++q) {
-            const int sl = sc[SC_CL + 32 + q];
-            const int m = sc[SC_CL + sl];
-            const bool cr = lo < m && m <= hi;
-            const int cm_ = __popcll(__ballot(cr && inm)), cb_ = __popcll(__ballot(cr && inb));
-            if (lane == 0) {
-                if (cm_) atomicAdd(&sc[SC_GE + sl], sgn * cm_);
-                if (cb_) atomicAdd(&sc[SC_GE + 16 + sl], sgn * cb_);
-            }
-        }
-    };
 
     int g = 0;    // global chunk index
     int par = 0;  // pass parity (double-buffered LDS scalars)
@@ -1721,28 +1664,6 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                 atomicMax(&sc[SC_U0], m0);
                 atomicMax(&sc[SC_U1], m1);
             }
-            if (kCap) {  // the class counts after the releases and the batch's health (zeroed at the last batch's end)
-                const int nc = sc[SC_CL + 41];
-                for (int q = 0; q < nc; ++q) {
-                    const int sl = sc[SC_CL + 32 + q];
-                    const int m = sc[SC_CL + sl];
-                    int km = 0, kb = 0;
-                    for (int i = tid; i < nm; i += OWGS_ENT) {
-                        const int v = P[i];
-                        km += (v < OWGS_PLIM && v >= m) ? 1 : 0;
-                    }
-                    for (int p = tid; p < nb; p += OWGS_ENT) {
-                        const int v = P[A.n_ids - nb + p];
-                        kb += (v < OWGS_PLIM && v >= m) ? 1 : 0;
-                    }
-                    km = __builtin_amdgcn_readlane(wave_incl_scan(km), 63);
-                    kb = __builtin_amdgcn_readlane(wave_incl_scan(kb), 63);
-                    if (lane == 0) {
-                        if (km) atomicAdd(&sc[SC_GE + sl], km);
-                        if (kb) atomicAdd(&sc[SC_GE + 16 + sl], kb);
-                    }
-                }
-            }
         }
         lds_sync();
 
@@ -1914,23 +1835,13 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         const int hslot = (int)d.w;
                         const uint32_t hcw = ccw[d.x];
                         const int hcc = (int)((hcw >> 15) & OWGS_RMASK);
-                        int need = min(hocc[h] - hcc + 1, HOT_RANKS);
+                        const int need = min(hocc[h] - hcc + 1, HOT_RANKS);
                         if (need <= 0) continue;
                         uint2* tab = htab + h * HOT_RANKS;
                         const int hn = hpool ? nb : nm;
                         if (hmc == 1 && hmem > sc[hpool ? SC_U1 : SC_U0] && ((A.shortcut_ok >> hpool) & 1)) {
                             for (int q = lane; q < need; q += 64) tab[q] = make_uint2((uint32_t)K_FALLBACK << 15, 0u);
                             continue;
-                        }
-                        if (kCap && hmc == 1) {  // ranks at or beyond the class's capacity bound fail without a walk
-                            const int hsl = cls_slot(hmem);
-                            if (hsl >= 0 && sc[SC_GE + 16 * hpool + hsl] < need) {
-                                const int hB = cls_cap(hpool, hsl, hmem, sc[hpool ? SC_U1 : SC_U0]);
-                                for (int q = hB + lane; q < need; q += 64)
-                                    tab[q] = make_uint2((uint32_t)K_FALLBACK << 15, 0u);
-                                if (hB <= 0) continue;
-                                need = min(need, hB);
-                            }
                         }
                         int s0 = hcok ? (int)(hcw & 0x7FFFu) : 0;
                         const float rnn = __builtin_amdgcn_rcpf((float)hn);
@@ -2023,8 +1934,6 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             kind = K_HOT;
                         } else if (maxc == 1 && mem > U && ((A.shortcut_ok >> pool) & 1)) {
                             kind = K_FALLBACK;  // every usable permit < mem: the walk fails everywhere
-                        } else if (kCap && maxc == 1 && cls_fails(pool, mem, r, U)) {
-                            kind = K_FALLBACK;  // the class's capacity in the pool is at most r: the walk fails
                         } else if (OWGS_CSCAN_ON && maxc > 1 && mem > U && pool_mode == 0 && n > OWGS_CSCAN_MIN_N && !ovf_on) {
                             kind = K_CSCAN;  // no invoker can open a container: capacity = the key's open ones
                             ws = s;          // (the ordinary walk's start, should the key have > 64 of them)
@@ -2664,9 +2573,8 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                 // lanes after l give it back).  "first" = lowest lane of the (hashed) bucket of t.
                 const int bk = part ? (int)(((uint32_t)t * 2654435761u) >> (32 - OWGS_NBK_LOG2)) : 0;
                 static_assert(OWGS_NBK == (1 << OWGS_NBK_LOG2) && OWGS_WL <= 512, "power-of-two buckets; lane fields 10 bits");
-                int pv0 = 0;  // (OWGS_F_CAP) the permits before this lane's take
                 if (part) {
-                    if (cons) pv0 = atomicSub(&P[t], cons);
+                    if (cons) atomicSub(&P[t], cons);
                     atomicMax(&fst[bk], (uint32_t)(OWGS_WL - li));
                     nextl[li] = (int)atomicExch(&bhead[bk], (uint32_t)(li + 1));
                     spc[li] = cons;
@@ -2676,7 +2584,6 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                 const int cft = SC_CFT + par * CFT_N + (int)(((uint32_t)slot * 2654435761u) >> (32 - CFT_LOG2));
                 if (act && maxc > 1 && kind == K_FALLBACK) atomicMin(&sc[cft], li);
                 if (own && li < OWGS_WL) spt[li] = part ? t : -1;
-                if (kCap && !io) cls_track(part && cons != 0, t, pv0, pv0 - cons, -1);
                 LDS_SYNC_T(3);
                 // (fallback+buckets accrue to PT(6));
                 PT(3);
@@ -2838,18 +2745,10 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                         // sees (the frontier minus the lanes before it); the lanes that commit add theirs again below
                         for (int k0 = l; k0 < len; k0 += 64) {
                             const int k = k0 + lane;
-                            bool gv = false;
-                            int gx = 0, gm = 0, g0 = 0;
                             if (k < len) {
                                 const uint4 f2 = fxa[k];
-                                if (f2.w >> 31) {
-                                    gv = true;
-                                    gx = (int)(f2.y & 0xFFFFu);
-                                    gm = (int)(f2.w & OWGS_AM_MEM_MASK);
-                                    g0 = atomicAdd(&P[gx], gm);
-                                }
+                                if (f2.w >> 31) atomicAdd(&P[(int)(f2.y & 0xFFFFu)], (int)(f2.w & OWGS_AM_MEM_MASK));
                             }
-                            if (kCap) cls_track(gv, gx, g0, g0 + gm, 1);
                         }
                         int L = l, nE = 0;
                         // the re-decided lanes' targets and actions as hashed 2048-bit sets over the wave's lanes
@@ -2911,10 +2810,6 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                             // every usable permit count below mem: the walk fails (U bounds the frontier, whose
                             // permits bound this lane's)
                             if (!done) done = mm > (pl_ ? u1 : u0) && ((A.shortcut_ok >> pl_) & 1);
-                            if (kCap && !done) {  // no usable invoker of the pool holds mm (exact now: see cls_track)
-                                const int sl_ = cls_slot(mm);
-                                done = sl_ >= 0 && sc[SC_GE + 16 * pl_ + sl_] == 0;
-                            }
                             if (!done) {
                                 const float rnn = __builtin_amdgcn_rcpf((float)nn);
                                 int s0 = (int)(fy >> 16);
@@ -2963,10 +2858,8 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                 if (pl_) u1 = min(u1, mm - 1);
                                 else u0 = min(u0, mm - 1);
                             }
-                            int tv0 = 0;
-                            if (lane == 0) tv0 = atomicSub(&P[tn], mm);
-                            if (kCap) cls_track(lane == 0, tn, tv0, tv0 - mm, -1);
                             if (lane == 0) {
+                                atomicSub(&P[tn], mm);
                                 *(uint2*)&fxa[L] = make_uint2(fxx | FX_DONE | ((uint32_t)kn << 28), (uint32_t)tn | ((uint32_t)sn << 16));
                                 if (kn == K_FALLBACK) atomicMin(&sc[pl_ ? SC_U1 : SC_U0], mm - 1);  // rank 0 failed
                             }
@@ -3001,10 +2894,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                 const u64 sm = __ballot(stop);
                                 const int q = sm ? ffs64(sm) : 64;
                                 // the lanes before the stop commit where they speculated: their takes again
-                                const bool rt_ = lane < q && (f2.w >> 31);
-                                int r0_ = 0;
-                                if (rt_) r0_ = atomicSub(&P[(int)tk], (int)(f2.w & OWGS_AM_MEM_MASK));
-                                if (kCap) cls_track(rt_, (int)tk, r0_, r0_ - (int)(f2.w & OWGS_AM_MEM_MASK), -1);
+                                if (lane < q && (f2.w >> 31)) atomicSub(&P[(int)tk], (int)(f2.w & OWGS_AM_MEM_MASK));
                                 if (sm) {
                                     L = k0 + q;
                                     fx = make_uint4(__builtin_amdgcn_readlane(f2.x, q), __builtin_amdgcn_readlane(f2.y, q),
@@ -3144,19 +3034,15 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
 #ifdef OWGS_PROF_COMMIT
                 const u64 tc1 = memtime_pinned();
 #endif
-                bool gback = false;
-                int gb0 = 0;
                 if (part) {
 #if OWGS_EXT
-                    gback = li >= l && cons && !fixup;
+                    if (li >= l && cons && !fixup) atomicAdd(&P[t], cons);  // not committed: give the memory back
 #else
-                    gback = li >= l && cons;
+                    if (li >= l && cons) atomicAdd(&P[t], cons);  // not committed: give the memory back
 #endif
-                    if (gback) gb0 = atomicAdd(&P[t], cons);  // not committed: give the memory back
                     fst[bk] = 0u;
                     bhead[bk] = 0u;
                 }
-                if (kCap && !io) cls_track(gback, t, gb0, gb0 + cons, 1);
                 if (act && li >= l) {
                     keep = !nf;
 #if OWGS_EXT
@@ -3200,12 +3086,11 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                 par ^= 1;
             }
         }
-        // U bounds are per batch (releases raise permits); so are the class counts
+        // U bounds are per batch (releases raise permits)
         if (tid == 0) {
             sc[SC_U0] = (int)0x80000000;
             sc[SC_U1] = (int)0x80000000;
         }
-        if (kCap && tid < 32) sc[SC_GE + tid] = 0;
         lds_sync();
     }
 
@@ -3758,7 +3643,7 @@ extern "C" hipError_t owgs_launch_release_seq(const OwgsReleaseArgs* a, hipStrea
 // the engine's dynamic-LDS limit, set once per (kernel, device): the attribute is per device, and a process may drive
 // contexts on several devices
 static hipError_t lds_attr(const void* fn, int which) {
-    static std::atomic<unsigned long long> done[15];
+    static std::atomic<unsigned long long> done[9];
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
@@ -3774,17 +3659,12 @@ static bool engine_args_ok(const OwgsEngineArgs& a) {
     return a.geom == OWGS_GEOM_TAG(OWGS_WL) && a.cw >= 0 && a.cw <= OWGS_WL;
 }
 
-// compiled specialisations: 0 (maxConcurrent == 1, identity pools, implicit sequence numbers), OWGS_F_CONC, OWGS_F_ALL
-// for anything else, and the first two with the memory-class counts (OWGS_F_CAP; never with OWGS_F_GEN)
-#define OWGS_NFEAT 5
-static int feat_index(int feat) {
-    if (feat & OWGS_F_GEN) return 2;
-    return (feat & OWGS_F_CAP) ? ((feat & OWGS_F_CONC) ? 4 : 3) : ((feat & OWGS_F_CONC) ? 1 : 0);
-}
+// compiled specialisations: 0 (maxConcurrent == 1, identity pools, implicit sequence numbers), OWGS_F_CONC, and
+// OWGS_F_ALL for anything else
+static int feat_index(int feat) { return feat == 0 ? 0 : feat == OWGS_F_CONC ? 1 : 2; }
 template <template <int> class K>
 static void* pick(int fi) {
-    return fi == 0 ? K<0>::fn() : fi == 1 ? K<OWGS_F_CONC>::fn() : fi == 3 ? K<OWGS_F_CAP>::fn()
-         : fi == 4 ? K<OWGS_F_CONC | OWGS_F_CAP>::fn() : K<OWGS_F_ALL>::fn();
+    return fi == 0 ? K<0>::fn() : fi == 1 ? K<OWGS_F_CONC>::fn() : K<OWGS_F_ALL>::fn();
 }
 template <int F>
 struct KOne {
@@ -3813,7 +3693,7 @@ extern "C" hipError_t OWGS_GEOM(owgs_launch_engine_multi_dev)(const OwgsEngineAr
     if (lds > OWGS_LDS_BYTES) return hipErrorInvalidValue;
     const int fi = feat_index(feat);
     void* fn = pick<KMultiDev>(fi);
-    const hipError_t ea = lds_attr(fn, fi);  // (attribute slots: one kernel x OWGS_NFEAT specialisations each)
+    const hipError_t ea = lds_attr(fn, fi);
     if (ea != hipSuccess) return ea;
     void* args[] = {(void*)&a_dev};
     return hipLaunchKernel(fn, dim3(k), dim3(OWGS_NT), args, lds, s);
@@ -3834,7 +3714,7 @@ extern "C" hipError_t OWGS_GEOM(owgs_launch_engine_multi)(const OwgsEngineArgs* 
     if (lds > OWGS_LDS_BYTES) return hipErrorInvalidValue;
     const int fi = feat_index(feat);
     void* fn = pick<KMulti>(fi);
-    const hipError_t ea = lds_attr(fn, OWGS_NFEAT + fi);
+    const hipError_t ea = lds_attr(fn, 3 + fi);
     if (ea != hipSuccess) return ea;
     void* args[] = {(void*)&M};
     return hipLaunchKernel(fn, dim3(k), dim3(OWGS_NT), args, lds, s);
@@ -3846,7 +3726,7 @@ extern "C" hipError_t OWGS_GEOM(owgs_launch_engine)(const OwgsEngineArgs* a, hip
     if (lds > OWGS_LDS_BYTES) return hipErrorInvalidValue;
     const int fi = feat_index(a->feat);
     void* fn = pick<KOne>(fi);
-    const hipError_t ea = lds_attr(fn, 2 * OWGS_NFEAT + fi);
+    const hipError_t ea = lds_attr(fn, 6 + fi);
     if (ea != hipSuccess) return ea;
     OwgsEngineOne M;
     M.a[0] = *a;
