@@ -87,6 +87,27 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+def warm_collective(dist, dev):
+    """One all-gather right after the process group starts, with this process's stdout pointed at stderr: RCCL prints
+    its version banner to stdout when the first collective creates the communicator (the bench's stdout is its one
+    JSON line), and the communicator's internal stream is created here, before the shards' streams, so that it does not
+    share a hardware queue (GPU_MAX_HW_QUEUES, round-robin over streams in creation order) with an engine stream."""
+    import torch
+
+    sys.stdout.flush()
+    keep = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        x = torch.zeros(1, dtype=torch.uint8, device=dev)
+        out = torch.empty(dist.get_world_size(), dtype=torch.uint8, device=dev)
+        dist.all_gather_into_tensor(out, x)
+        torch.cuda.synchronize()
+    finally:
+        sys.stdout.flush()
+        os.dup2(keep, 1)
+        os.close(keep)
+
+
 def launch_ranks(args) -> int:
     """`--gpus N` without a torch.distributed environment: run N ranks under torch.distributed.run as a CHILD
     process (this process has not touched a GPU) and return its exit code."""
@@ -530,12 +551,14 @@ def main():
 
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", init_method="env://")
+        warm_collective(dist, torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
         if args.rccl:  # one rank over RCCL: the collective the N > 1 cadence issues, on this lease's one GPU
             import torch.distributed as dist
 
             dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+            warm_collective(dist, torch.device("cuda", 0))
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from openwhisk_amd import GpuShardingContainerPoolBalancer

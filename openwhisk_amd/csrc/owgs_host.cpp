@@ -567,8 +567,9 @@ static void ovf_add(owgs_ctx* c, int64_t n) {
 static void ovf_probes_clear(owgs_ctx* c) {
     for (int k = 0; k < owgs_ctx::OVF_PROBES; ++k) c->ovf_probe[k] = false;
 }
-// after an engine launch on s: copy the entry count back into the next free probe slot (no wait)
-static int ovf_probe_record(owgs_ctx* c, hipStream_t s) {
+// overflow entry-count probes: the next probe slot, or -1 while its last probe is still in flight (this launch then records none)
+static int ovf_probe_slot(owgs_ctx* c, int* k_out) {
+    *k_out = -1;
     if (!c->h_ovf_cnt) {
         HIPCHK(c, hipHostMalloc((void**)&c->h_ovf_cnt, owgs_ctx::OVF_PROBES * sizeof(int32_t), hipHostMallocDefault));
         for (int k = 0; k < owgs_ctx::OVF_PROBES; ++k)
@@ -576,7 +577,11 @@ static int ovf_probe_record(owgs_ctx* c, hipStream_t s) {
     }
     const int k = c->ovf_probe_next;
     if (c->ovf_probe[k] && hipEventQuery(c->ev_ovf[k]) != hipSuccess) return OWGS_OK;  // (still in flight: skip)
-    HIPCHK(c, hipMemcpyAsync(&c->h_ovf_cnt[k], c->d_ovf_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    *k_out = k;
+    return OWGS_OK;
+}
+// slot k's value lands behind the work queued on s so far (the engine launch before it stores it there)
+static int ovf_probe_mark(owgs_ctx* c, int k, hipStream_t s) {
     HIPCHK(c, hipEventRecord(c->ev_ovf[k], s));
     c->ovf_probe[k] = true;
     c->ovf_probe_added[k] = c->ovf_added;
@@ -902,12 +907,20 @@ static int run_engine(owgs_ctx* c, OwgsEngineArgs& A, hipStream_t s, bool launch
     if (env_opts().feat_all) A.feat = OWGS_F_ALL;  // diagnostics: always the general engine
     A.geom = OWGS_GEOM_TAG(variant_wl(c));
     if (!launch) return OWGS_OK;  // owgs_replay_device_multi launches every shard's engine at once
+    // the overflow's entry count for a later ensure_ovf: the engine stores it into a pinned probe slot as its last
+    // step (no copy after the launch), read without a wait once the slot's event has passed
+    int probe = -1;
+    if (c->ovf_cap > 0) {
+        const int rc = ovf_probe_slot(c, &probe);
+        if (rc) return rc;
+        if (probe >= 0) A.ovf_host = &c->h_ovf_cnt[probe];
+    }
     HIPCHK(c, hipEventRecord(c->ev_engine[0], s));  // brackets exactly the engine launch (owgs_engine_ms)
     HIPCHK(c, launch_engine(c, &A, s));
     HIPCHK(c, hipEventRecord(c->ev_engine[1], s));
     c->ev_engine_valid = true;
-    if (c->ovf_cap > 0) {  // the overflow's entry count for a later ensure_ovf, copied back without a wait
-        const int rc = ovf_probe_record(c, s);
+    if (probe >= 0) {
+        const int rc = ovf_probe_mark(c, probe, s);
         if (rc) return rc;
     }
     if (A.trace) {  // diagnostic timeline: raw u64 pairs, [waves][16384][2]
@@ -3198,9 +3211,20 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
         memcpy(H + o_ra, rel_action, 4 * (size_t)NR);
     }
     if (seq && NP) memcpy(H + o_sq, seq, 8 * (size_t)NP);
-    HIPCHK(c, c->d_pin.reserve(in_bytes));
-    HIPCHK(c, hipMemcpyAsync(c->d_pin.p, H, in_bytes, hipMemcpyHostToDevice, s));
-    char* D = (char*)c->d_pin.p;
+    bool fused = !(c->w_cap > 0 || NP == 0);
+    // a fused call's kernels (release staging, pre-pass, engine) read the inputs from the pinned block itself, over
+    // PCIe: no host-to-device copy, and no wait for it before the first kernel.  The per-run path copies them to HBM.
+    char* D = H;
+    auto to_hbm = [&]() -> int {
+        HIPCHK(c, c->d_pin.reserve(in_bytes));
+        HIPCHK(c, hipMemcpyAsync(c->d_pin.p, H, in_bytes, hipMemcpyHostToDevice, s));
+        D = (char*)c->d_pin.p;
+        return OWGS_OK;
+    };
+    if (!fused) {
+        const int rh = to_hbm();
+        if (rh) return rh;
+    }
     const int64_t* d_acq = (const int64_t*)(D + o_acq);
     const int64_t* d_rel = (const int64_t*)(D + o_rel);
     const int64_t* d_run = (const int64_t*)(D + o_run);
@@ -3214,7 +3238,6 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
     uint8_t* d_fl = (uint8_t*)(DO + q_fl);
     uint8_t* d_rf = (uint8_t*)(DO + q_rf);
     int rc = OWGS_OK;
-    bool fused = !(c->w_cap > 0 || NP == 0);
     if (!fused) {
         // watched pairs: the exact release kernels per run, the watch update after each publish run; a call of
         // completions only: the release kernels alone (cheaper than an engine launch)
@@ -3260,11 +3283,14 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
             A.rel_flags = d_rf;
             A.rel_bound = c->f_bound.p;
         }
+        // the context's error word after the launch: stored by the engine into the pinned output block (past the
+        // range the copy below brings back), not copied after it
+        A.err_host = (int32_t*)((char*)c->h_pout + q_err);
         if (!rc) rc = run_engine(c, A, s);
     }
     if (rc) return rc;
-    HIPCHK(c, hipMemcpyAsync(c->d_pout.p + q_err, c->d_err.p, 4, hipMemcpyDeviceToDevice, s));
-    HIPCHK(c, hipMemcpyAsync(c->h_pout, c->d_pout.p, out_bytes, hipMemcpyDeviceToHost, s));
+    if (!fused) HIPCHK(c, hipMemcpyAsync(c->d_pout.p + q_err, c->d_err.p, 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->h_pout, c->d_pout.p, fused ? q_err : out_bytes, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     const char* HO = (const char*)c->h_pout;
     int32_t e = 0;
@@ -3275,6 +3301,17 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
         // release by release (FS:48-50) exactly as owgs_release_batch does
         HIPCHK(c, hipMemsetAsync(c->d_err.p, 0, sizeof(int32_t), s));
         HIPCHK(c, hipMemsetAsync(c->f_bound.p, 0, c->f_bound.n * 8, s));
+        if (D == H) {  // (the per-run path reads its inputs from HBM)
+            const int rh = to_hbm();
+            if (rh) return rh;
+            d_acq = (const int64_t*)(D + o_acq);
+            d_rel = (const int64_t*)(D + o_rel);
+            d_run = (const int64_t*)(D + o_run);
+            d_pa = (const int32_t*)(D + o_pa);
+            d_ri = (const int32_t*)(D + o_ri);
+            d_ra = (const int32_t*)(D + o_ra);
+            d_sq = seq ? (const u64*)(D + o_sq) : nullptr;
+        }
         rc = process_runs(c, n_runs, rel_off, pub_off, d_run, d_pa, d_ri, d_ra, d_sq, seq_base, d_out, d_fl, d_rf, s);
         if (rc) return rc;
         HIPCHK(c, hipMemcpyAsync(c->d_pout.p + q_err, c->d_err.p, 4, hipMemcpyDeviceToDevice, s));

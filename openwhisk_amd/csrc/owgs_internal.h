@@ -200,6 +200,11 @@ struct OwgsEngineArgs {
     // with a new health vector, SCPB:512-551) at hwords + b * hstride, or null
     const uint32_t* hwords;
     int32_t hstride;
+    // pinned host words the launch's last step stores into (null: none), so that the caller reads them after its
+    // stream synchronisation without a copy: the context's error word after this launch, and the overflow table's
+    // entry count (its bound for the next call's sizing)
+    int32_t* err_host;
+    int32_t* ovf_host;
 };
 // Geometry/ABI tag.  The host and an engine object must agree on the chunk width (the stride of lix, the 10-bit lane
 // fields of the records), the primary table's capacity and the argument block's layout; the host builds the tag of the
@@ -266,7 +271,8 @@ struct OwgsRelposArgs {
 struct OwgsPrepassArgs {
     int32_t n_batches;
     const int64_t* acq_off;
-    const int32_t* cstart;       // [n_batches + 1] first chunk of each batch (built by owgs_chunks_kernel)
+    const int32_t* cstart;       // [n_batches + 1] first chunk of each batch (owgs_chunks_kernel), or null: each
+                                 // workgroup walks the few batches' chunk counts itself
     const int32_t* act;          // [n_act] action per activation, or null: per-activation meta in xmeta/xslot
     const uint2* act_meta;       // [n_actions]
     const int32_t* act_slot;     // [n_actions]

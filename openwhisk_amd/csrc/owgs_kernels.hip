@@ -600,15 +600,29 @@ __global__ __launch_bounds__(OWGS_WL) void owgs_prepass_kernel(OwgsPrepassArgs A
     __shared__ unsigned long long m_a[OWGS_WL][NWR], m_s[OWGS_WL][NWR];  // lane masks, by the group's first lane
     __shared__ int32_t sh_a[OWGS_WL];  // per action group: some lane has a shared-key lane before it (pk1 != 0)
     const int g = blockIdx.x;
-    if (g >= A.cstart[A.n_batches]) return;
-    int lo = 0, hi = A.n_batches - 1;  // last batch with cstart[b] <= g
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (A.cstart[mid] <= g) lo = mid;
-        else hi = mid - 1;
+    int b = -1, gb = 0;  // the chunk's batch and that batch's first chunk
+    if (A.cstart) {
+        if (g >= A.cstart[A.n_batches]) return;
+        int lo = 0, hi = A.n_batches - 1;  // last batch with cstart[b] <= g
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (A.cstart[mid] <= g) lo = mid;
+            else hi = mid - 1;
+        }
+        b = lo;
+        gb = A.cstart[b];
+    } else {  // a few batches (a shim call's runs): their chunk counts walked here, no chunk-table launch before
+        for (int bb = 0; bb < A.n_batches; ++bb) {
+            const int nc = (int)((A.acq_off[bb + 1] - A.acq_off[bb] + A.cw - 1) / A.cw);
+            if (g < gb + nc) {
+                b = bb;
+                break;
+            }
+            gb += nc;
+        }
+        if (b < 0) return;
     }
-    const int b = lo;
-    const int64_t c0 = A.acq_off[b] + (int64_t)(g - A.cstart[b]) * A.cw;
+    const int64_t c0 = A.acq_off[b] + (int64_t)(g - gb) * A.cw;
     const int len = (int)min((int64_t)A.cw, A.acq_off[b + 1] - c0);
     const int t = threadIdx.x;
     uint2 meta = make_uint2(0, 0);
@@ -1109,8 +1123,14 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     };
     // (uniform) a launch prepared for another geometry: its chunk tables have another stride -- refuse it before the
     // first barrier or wait of any wave
+    // the caller's pinned words (err_host, ovf_host) on an early exit: the error word, the overflow count unchanged
+    auto tail_early = [&](int e) {
+        atomicOr(A.err, e);
+        if (A.err_host) *A.err_host = __hip_atomic_load(A.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | e;
+        if (A.ovf_host) *A.ovf_host = A.ovf.cap > 0 ? __hip_atomic_load(A.ovf.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    };
     if (A.geom != OWGS_GEOM_TAG(OWGS_WL)) {
-        if (threadIdx.x == 0) atomicOr(A.err, OWGS_ERR_GEOM);
+        if (threadIdx.x == 0) tail_early(OWGS_ERR_GEOM);
         if (A.stats_next && threadIdx.x < OWGS_NSTATS) A.stats_next[threadIdx.x] = 0ull;
         return;
     }
@@ -1204,7 +1224,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     // releases that could leave the range: nothing has been written yet -- the host replays the call through the
     // ordered release kernels (which flag ForcibleSemaphore's overflow Error per release, FS:48-50)
     if (A.rel_bound && sc[SC_RRISK]) {  // (uniform)
-        if (tid == 0) atomicOr(A.err, OWGS_ERR_RELRISK);
+        if (tid == 0) tail_early(OWGS_ERR_RELRISK);
         if (A.stats_next && tid < OWGS_NSTATS) A.stats_next[tid] = 0ull;
         return;
     }
@@ -3108,6 +3128,19 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
         A.ct_keys[i] = e.x;
         A.ct_vals[i] = e.y;
     }
+    if (A.err_host || A.ovf_host) {  // (uniform) the caller's pinned words: every thread's error bits first
+        if (tid == 0) sc[SC_IRR] = 0;
+        lds_sync();
+        if (err) atomicOr(&sc[SC_IRR], (int)err);
+        lds_sync();
+        if (tid == 0) {
+            const int e = sc[SC_IRR];
+            if (e) atomicOr(A.err, e);
+            if (A.err_host) *A.err_host = __hip_atomic_load(A.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | e;
+            if (A.ovf_host) *A.ovf_host = sc[SC_OVF];
+        }
+        err = 0;
+    }
     if (err) atomicOr(A.err, (int)err);
     if (A.stats_next && tid < OWGS_NSTATS) A.stats_next[tid] = 0ull;  // the next launch's counters start at zero
 #ifdef OWGS_PROFILE
@@ -3535,10 +3568,13 @@ extern "C" hipError_t owgs_launch_prepare(const OwgsPrepArgs* a, hipStream_t s) 
 extern "C" hipError_t OWGS_GEOM(owgs_launch_prepass)(const OwgsPrepassArgs* a, int32_t* cstart, int64_t max_chunks,
                                           hipStream_t s) {
     if (a->geom != OWGS_GEOM_TAG(OWGS_WL) || a->cw < 1 || a->cw > OWGS_WL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(owgs_chunks_kernel, dim3(1), dim3(64), 0, s, a->acq_off, a->n_batches, a->cw, cstart);
+    // up to PP_INLINE batches (a shim call's runs, a span): each pre-pass workgroup finds its batch itself
+    constexpr int PP_INLINE = 8;
+    if (a->n_batches > PP_INLINE)
+        hipLaunchKernelGGL(owgs_chunks_kernel, dim3(1), dim3(64), 0, s, a->acq_off, a->n_batches, a->cw, cstart);
     if (max_chunks <= 0) return hipGetLastError();
     OwgsPrepassArgs b = *a;
-    b.cstart = cstart;
+    b.cstart = a->n_batches > PP_INLINE ? cstart : nullptr;
     hipLaunchKernelGGL(owgs_prepass_kernel, dim3((unsigned)max_chunks), dim3(OWGS_WL), 0, s, b);
     return hipGetLastError();
 }

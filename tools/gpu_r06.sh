@@ -16,10 +16,10 @@ for s in ${STEPS:-tests}; do
       timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
       rc=$?; tail -2 $O/pytest_gpu.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/pytest_gpu.log | head -20; stop tests $rc; } ;;
     restests)
-      timeout -k 10 500 python -u -m pytest tests/test_gpu_resident.py tests/test_gpu_shim_sequence.py ${TESTSEL} -x -v --timeout 200 --timeout-method thread > $O/pytest_res.log 2>&1
+      timeout -k 10 500 python -u -m pytest tests/test_gpu_resident.py tests/test_gpu_shim_sequence.py -x -v --timeout 200 --timeout-method thread > $O/pytest_res.log 2>&1
       rc=$?; tail -2 $O/pytest_res.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/pytest_res.log | head -20; stop restests $rc; } ;;
     sel)  # the tests named by $TESTSEL
-      timeout -k 10 600 python -u -m pytest $TESTSEL -x -v --timeout 200 --timeout-method thread > $O/pytest_sel.log 2>&1
+      timeout -k 10 600 python -u -m pytest $TESTSEL ${KSEL:+-k "$KSEL"} -x -v --timeout 200 --timeout-method thread > $O/pytest_sel.log 2>&1
       rc=$?; tail -2 $O/pytest_sel.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/pytest_sel.log | head -20; stop sel $rc; } ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
@@ -153,6 +153,19 @@ for l in d['legs']:
       timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/shimtrace -o run --output-format csv -- \
         python3 tools/shim_leg.py --drains ${DRAINS:-4096} --modes fused > $O/shimtrace.json 2> $O/shimtrace.err
       rc=$?; cut -c1-300 $O/shimtrace.json; [ $rc -eq 0 ] || { tail -5 $O/shimtrace.err; stop shimtrace $rc; } ;;
+    largeall)  # the large-state engine's rate at 40,000 invokers with 0 / 20 / 50 % concurrent actions, and 25,000
+      for cc in 0 0.2 0.5; do
+        CONC=$cc timeout -k 10 400 python -u tools/time_large.py 40000 >> $O/large.jsonl 2>> $O/large.err
+        rc=$?; tail -1 $O/large.jsonl | cut -c1-300; [ $rc -eq 0 ] || { tail -5 $O/large.err; stop largeall $rc; }
+      done
+      timeout -k 10 400 python -u tools/time_large.py 25000 >> $O/large.jsonl 2>> $O/large.err
+      rc=$?; tail -1 $O/large.jsonl | cut -c1-300; [ $rc -eq 0 ] || { tail -5 $O/large.err; stop largeall $rc; } ;;
+    rcclq8)  # the same trace with 8 hardware queues per process (GPU_MAX_HW_QUEUES, the box's default is 4): does the
+             # collective then overlap the engine instead of queueing behind it?
+      rm -rf $O/rcclq8
+      GPU_MAX_HW_QUEUES=8 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/rcclq8 -o run --output-format csv -- \
+        python3 bench.py --health-churn --rccl ${CHURNARGS} --steps 3 --warmup 1 --no-cpu-baseline --no-check --no-h2d --no-shim-path > $O/rcclq8.log 2>&1
+      rc=$?; tail -1 $O/rcclq8.log | cut -c1-200; [ $rc -eq 0 ] || stop rcclq8 $rc ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
