@@ -518,6 +518,9 @@ class GpuShardingContainerPoolBalancer:
              "stops": out[5], "general_probes": out[6], "general_lanes": out[7], "redecided": out[31] & 0xFFFFFFFF}
         if out[31] >> 32:
             d["redecided_prewalk"] = out[31] >> 32
+        if out[46] or out[47]:  # large-state engine: decisions kept from its group speculation / decided alone
+            d["large_spec"], d["large_alone"] = out[46], out[47]
+            d["large_cycles"] = {"releases": out[40], "speculation": out[41], "kept": out[42], "alone": out[43]}
         if any(out[28:31]) and not any(out[8:16]):  # -DOWGS_EXT_PROF build: in-pass re-decision costs
             d["redecide"] = {"cycles": out[28], "walk_rounds": out[29], "scans": out[30], "setup": out[20], "walk": out[21],
                              "apply": out[22], "scan": out[23]}

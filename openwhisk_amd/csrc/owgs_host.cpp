@@ -333,6 +333,8 @@ struct owgs_ctx {
     DevBuf<int32_t> q_filled, q_state, q_look;
     DevBuf<uint4> q_cur;   // walk cursors of the large-state engine, per action {generation, step, position, 0}
     uint32_t q_gen = 1;    // the next call's first generation: cursors never outlive the call that wrote them
+    int64_t q_spec = 0, q_alone = 0;  // its decisions: kept from the group speculation / decided alone
+    uint64_t q_cyc[4] = {0, 0, 0, 0};  // its cycles: releases, group speculation, kept decisions, decided alone
     DevBuf<uint32_t> d_hwords;
     const uint32_t* grp_hwords = nullptr;
     int32_t grp_hstride = 0;
@@ -1491,7 +1493,7 @@ static OwgsSeqArgs seq_args(owgs_ctx* c) {
 
 // the map keeps `room` more entries under half its capacity: read its fill, grow (rehash live entries) if needed
 static int seq_reserve(owgs_ctx* c, int64_t room, hipStream_t s) {
-    HIPCHK(c, c->q_state.reserve(8));
+    HIPCHK(c, c->q_state.reserve(16));
     if (!c->q_filled.p) {
         HIPCHK(c, c->q_filled.reserve(1));
         HIPCHK(c, hipMemsetAsync(c->q_filled.p, 0, 4, s));
@@ -1580,9 +1582,12 @@ static int seq_run(owgs_ctx* c, const OwgsSeqArgs& S0, hipStream_t s) {
         S.state = c->q_state.p;
         S.resume = resume;
         HIPCHK(c, owgs_launch_seq(&S, s));
-        int32_t st[6] = {0, 0, 0, 0, 0, 0};
+        int32_t st[16] = {0};
         HIPCHK(c, hipMemcpyAsync(st, c->q_state.p, sizeof(st), hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
+        c->q_spec += st[6];  // (decisions the launch kept from its speculation / decided alone)
+        c->q_alone += st[7];
+        for (int k = 0; k < 4; ++k) c->q_cyc[k] += (uint64_t)(uint32_t)st[8 + 2 * k] | ((uint64_t)(uint32_t)st[9 + 2 * k] << 32);
         gen = (uint32_t)st[5];  // (a resumed launch continues the generation it stopped in)
         if (st[0] == 0) break;
     }
@@ -3503,6 +3508,11 @@ int owgs_read_stats(owgs_ctx* c, uint64_t* out, int32_t cap) {
     HIPCHK(c, hipMemcpyAsync(v, c->d_stats.p + (size_t)c->stats_last * OWGS_NSTATS, sizeof(v), hipMemcpyDeviceToHost,
                              c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->large) {  // (the large-state engine keeps no device counters: its decisions by path, since the context began)
+        v[46] = (u64)c->q_spec;
+        v[47] = (u64)c->q_alone;
+        for (int k = 0; k < 4; ++k) v[40 + k] = c->q_cyc[k];
+    }
     for (int32_t i = 0; i < cap && i < OWGS_NSTATS; ++i) out[i] = v[i];
     return OWGS_OK;
 }

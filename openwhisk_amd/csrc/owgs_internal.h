@@ -118,7 +118,8 @@
 #define OWGS_ST_CHUNKS 4
 #define OWGS_ST_STOPS 5
 #define OWGS_NSTATS 48  // 0-7 counters, 8-15 profile-build phase cycles, 16-31 profile-build walk counters,
-                        // 40-42 profile-build kernel cycles (state load, batches, write-back)
+                        // 40-42 profile-build kernel cycles (state load, batches, write-back); 46-47 (host-side, large-
+                        // state contexts) decisions kept from the group speculation / decided alone
 
 #define OWGS_MULTI_MAX 8  // controller shards per owgs_engine_multi_kernel launch (kernarg: 8 x args)
 #define OWGS_MULTI_DEV_MAX 64  // owgs_engine_multi_dev_kernel: argument blocks in HBM

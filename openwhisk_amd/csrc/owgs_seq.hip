@@ -39,6 +39,18 @@ __device__ __forceinline__ uint32_t rng_index(u64 seed, u64 seq, uint32_t n) {
     return (uint32_t)((u * (u64)n) >> 32);
 }
 __device__ __forceinline__ int ffs64(u64 m) { return __ffsll((long long)m) - 1; }
+__device__ __forceinline__ int wave_sum(int v) {  // (every lane gets the wave's sum)
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+#ifndef SEQ_SPEC
+#define SEQ_SPEC 64  // walk steps a speculated maxConcurrent == 1 decision probes (beyond them: decided alone)
+#endif
+#define SEQ_SPG 8    // ... in rounds of this many loads in flight
+#ifndef SEQ_SPEC_C
+#define SEQ_SPEC_C 16  // walk steps a speculated concurrent decision probes (4 per round)
+#endif
 // Java int arithmetic (wrap-around)
 __device__ __forceinline__ int jadd(int a, int b) { return (int)((uint32_t)a + (uint32_t)b); }
 __device__ __forceinline__ int jsub(int a, int b) { return (int)((uint32_t)a - (uint32_t)b); }
@@ -146,6 +158,7 @@ __device__ __forceinline__ int sq_insert(const OwgsSeqArgs& S, int inv, int slot
 // map needs to grow first (state[0] = 1) or the call completed (state[0] = 0).
 __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
     __shared__ uint32_t pc[OWGS_SEQ_MAX_WORDS + 1];  // usable ids before each bitmap word
+    __shared__ int32_t tgt_lo[512], tgt_hi[512];  // per group and hashed target: the speculating actions' range
     const int lane = threadIdx.x;
     const int words = (S.n_ids + 31) >> 5;
     {
@@ -195,6 +208,19 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
     int r = S.resume ? S.state[1] : 0, ph = S.resume ? S.state[2] : 0;
     long long j = S.resume ? ((long long)(uint32_t)S.state[3] | ((long long)S.state[4] << 32)) : -1;
     bool stop = false;
+    int n_spec = 0, n_alone = 0;  // decisions kept from the speculation / decided alone (state[6], state[7])
+    // cycles (s_memtime) by phase, state[8..15] as 4 x u64: releases, a group's gather + ranks + speculation, its
+    // decisions kept from the speculation, its decisions decided alone
+    u64 cy0 = 0, cy1 = 0, cy2 = 0, cy3 = 0;
+    u64 t_ph = clock64();
+    auto tick = [&](int k) {  // (no indexed array: that would live in scratch and wait for the stores in flight)
+        const u64 t = clock64(), d = t - t_ph;
+        cy0 += k == 0 ? d : 0;
+        cy1 += k == 1 ? d : 0;
+        cy2 += k == 2 ? d : 0;
+        cy3 += k == 3 ? d : 0;
+        t_ph = t;
+    };
     for (; r < S.n_runs && !stop; ++r, ph = 0, j = -1) {
         // ---------------------------------------------------------------- completions (lane 0, queue order)
         if (ph == 0) {
@@ -275,6 +301,7 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                 j = j0 + nq;
             }
             mem_done();  // (the publishes' walks read these permits and entries from every lane)
+            tick(0);
             ph = 1;
             j = -1;
         }
@@ -326,9 +353,261 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                     g_cp = cu.z;
                 }
             }
+            // ---- speculation (maxConcurrent == 1 decisions, one lane each, all at once): each walks its own walk from
+            // its action's cursor against the permits at the group's start, rank-packed -- the k-th decision of an
+            // action in the group (k = its earlier ones) takes the step where the walk's cumulative capacity
+            // floor(permits / mem) first exceeds k -- up to SEQ_SPEC steps, SEQ_SPG loads in flight per round.  Permits only
+            // fall inside a run, so a step the walk passed stays full; the in-order loop below keeps the speculation
+            // where the permits at the decision's turn still hold it (its target's permits at the group's start minus
+            // what the group's earlier decisions took there) and decides the rest alone.
+            const bool plain = lane < nq && g_kind == 0 && g_maxc <= 1 && g_mem > 0;
+            int rank = 0;
+            {
+                u64 rem = __ballot(plain);
+                while (rem) {
+                    const int a0 = __builtin_amdgcn_readlane(g_a, ffs64(rem));
+                    const u64 m = __ballot(plain && g_a == a0);
+                    if (plain && g_a == a0)
+                        rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    rem &= ~m;
+                }
+            }
+            int sp_k = 0;  // 0 none (not a plain walk, or unfinished within the budget), 1 target, 2 the walk fails
+            int sp_t = -1, sp_pv = 0, sp_s = 0, sp_ks = 0;  // (sp_ks: earlier decisions of its action at its target)
+            uint32_t sp_p = 0u;
+            if (plain) {
+                const int n = g_bb ? S.nb : S.nm, base = g_bb ? S.n_ids - S.nb : 0;
+                const uint32_t un = (uint32_t)n;
+                const float rm = 1.0f / (float)g_mem;
+                int sx = g_cs, cum = 0;
+                uint32_t pos = g_cp;
+                for (int r4 = 0; r4 < SEQ_SPEC / SEQ_SPG && sp_k == 0; ++r4) {
+                    int id[SEQ_SPG], pv[SEQ_SPG];
+                    uint32_t uw[SEQ_SPG], ps[SEQ_SPG];
+#pragma unroll
+                    for (int u = 0; u < SEQ_SPG; ++u) {
+                        ps[u] = pos;
+                        id[u] = base + (int)pos;
+                        uw[u] = S.usable[id[u] >> 5];
+                        pv[u] = id[u] < S.n_slots ? ld_i(&S.permits[id[u]]) : 0;
+                        pos += g_step;
+                        pos = pos >= un ? pos - un : pos;
+                    }
+#pragma unroll
+                    for (int u = 0; u < SEQ_SPG; ++u) {
+                        if (sp_k != 0) continue;
+                        if (sx + u >= n) {  // every pool position: at most `rank` units anywhere (SCPB:417)
+                            sp_k = 2;
+                            continue;
+                        }
+                        const bool us = ((uw[u] >> (id[u] & 31)) & 1u) && id[u] < S.n_slots;
+                        int cap = 0;
+                        if (us && pv[u] >= g_mem) {  // floor(pv / mem) (float estimate, one correction), clamped
+                            cap = (int)((float)pv[u] * rm);
+                            const long long rr = (long long)pv[u] - (long long)cap * g_mem;
+                            cap += rr >= g_mem ? 1 : 0;
+                            cap -= rr < 0 ? 1 : 0;
+                            cap = min(cap, 64);
+                        }
+                        if (cum + cap > rank) {
+                            sp_k = 1;
+                            sp_t = id[u];
+                            sp_pv = pv[u];
+                            sp_s = sx + u;
+                            sp_p = ps[u];
+                            sp_ks = rank - cum;
+                        } else {
+                            cum += cap;
+                        }
+                    }
+                    sx += SEQ_SPG;
+                }
+            }
+            // concurrent decisions: the first of each fqn@version key in the group (the key's entries change only
+            // through its own decisions) walks from its home at the group's start: the first step whose entry has a
+            // free slot or whose permits hold a new container (tryAcquireConcurrent, NS:57-82); the steps it tried and
+            // failed whose entry is absent get the empty entry getOrElseUpdate leaves (NS:61-62) when it commits
+            // (sp_mask, bit = walk step).  Later decisions of the key are decided alone.
+            const bool conc = lane < nq && g_kind == 0 && g_maxc > 1 && g_mem > 0;
+            bool kfirst = false;
+            {
+                u64 rem = __ballot(conc);
+                while (rem) {
+                    const int j = ffs64(rem);
+                    const int s0 = __builtin_amdgcn_readlane(g_slot, j);
+                    const u64 m = __ballot(conc && g_slot == s0);
+                    if (lane == j) kfirst = true;
+                    rem &= ~m;
+                }
+            }
+            int sp_ix = -1;
+            uint32_t sp_mask = 0u, sp_ez = 0u, sp_ew = 0u;
+            if (kfirst && (g_bb ? S.nb : S.nm) > SEQ_SPEC_C) {
+                const int n = g_bb ? S.nb : S.nm, base = g_bb ? S.n_ids - S.nb : 0;
+                const uint32_t un = (uint32_t)n;
+                uint32_t pos = g_home;
+                for (int sx = 0; sx < SEQ_SPEC_C && sp_k == 0; sx += 4) {
+                    int id[4], pv[4], ixs[4];
+                    bool tried[4];
+                    uint32_t uw[4], ps[4];
+                    uint4 es[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        ps[u] = pos;
+                        id[u] = base + (int)pos;
+                        uw[u] = S.usable[id[u] >> 5];
+                        pv[u] = id[u] < S.n_slots ? ld_i(&S.permits[id[u]]) : 0;
+                        pos += g_step;
+                        pos = pos >= un ? pos - un : pos;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) tried[u] = ((uw[u] >> (id[u] & 31)) & 1u) && id[u] < S.n_slots;
+                    sq_find4(S, id, g_slot, tried, ixs, es);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        if (sp_k != 0 || !tried[u]) continue;
+                        if ((ixs[u] >= 0 && (int)es[u].z >= 1) || pv[u] >= g_mem) {
+                            sp_k = 3;
+                            sp_t = id[u];
+                            sp_pv = pv[u];
+                            sp_s = sx + u;
+                            sp_p = ps[u];
+                            sp_ix = ixs[u];
+                            sp_ez = ixs[u] >= 0 ? es[u].z : 0u;
+                            sp_ew = ixs[u] >= 0 ? es[u].w : 0u;
+                        } else if (ixs[u] < 0) {
+                            sp_mask |= 1u << (sx + u);
+                        }
+                    }
+                }
+            }
+            tick(1);
+            // the state stores of decisions kept from the speculation are held in their lanes and written together
+            // (the group's last decision per invoker / per action wins), before anything reads the state from memory:
+            // a store per decision makes the next reuse of its data register wait for the store (vmcnt) on this target
+            bool pw_on = false, cw_on = false;
+            int pw_t = 0, pw_v = 0, cw_a = 0, cw_s = 0;
+            uint32_t cw_p = 0u;
+            auto flush = [&]() {
+                for (u64 rem = __ballot(pw_on); rem;) {
+                    const int tt = __builtin_amdgcn_readlane(pw_t, ffs64(rem));
+                    const u64 m = __ballot(pw_on && pw_t == tt);
+                    if (lane == 63 - __clzll((long long)m)) S.permits[tt] = pw_v;
+                    rem &= ~m;
+                }
+                for (u64 rem = __ballot(cw_on); rem;) {
+                    const int aa = __builtin_amdgcn_readlane(cw_a, ffs64(rem));
+                    const u64 m = __ballot(cw_on && cw_a == aa);
+                    if (lane == 63 - __clzll((long long)m)) S.cur[aa] = make_uint4(gen, (uint32_t)cw_s, cw_p, 0u);
+                    rem &= ~m;
+                }
+                pw_on = false;
+                cw_on = false;
+            };
+            // speculated targets no decision of ANOTHER action speculated in the group (a hash collision counts as
+            // another's): there the decisions before one of the action's own at the target are exactly its ks earlier
+            // ones (rank packing), each taking its memory
+            const bool spx = sp_k == 1 || sp_k == 3;
+            const int th = (int)(((uint32_t)sp_t * 2654435761u) >> 23);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                tgt_lo[lane + 64 * u] = 0x7FFFFFFF;
+                tgt_hi[lane + 64 * u] = (int)0x80000000;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (spx) {
+                atomicMin(&tgt_lo[th], g_a);
+                atomicMax(&tgt_hi[th], g_a);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            const bool uniq = spx && tgt_lo[th] == g_a && tgt_hi[th] == g_a;
+            // this lane's speculated concurrent decision (sp_k 3), committed with `left` permits at its target: the
+            // empty entries of the steps it tried and failed, then its own entry (a free slot, or a container whose
+            // memory the pending permit write takes); returns the entries it inserted
+            auto conc_commit = [&](int left) -> int {
+                const int n_ = g_bb ? S.nb : S.nm, base_ = g_bb ? S.n_ids - S.nb : 0;
+                int ins = 0;
+                uint32_t pp = g_home;
+                for (int sx = 0; sx < sp_s; ++sx) {
+                    if ((sp_mask >> sx) & 1u) {
+                        ++ins;
+                        if (sq_insert(S, base_ + (int)pp, g_slot, 0, 0) < 0) err = 1;
+                    }
+                    pp += g_step;
+                    pp = pp >= (uint32_t)n_ ? pp - (uint32_t)n_ : pp;
+                }
+                int ix = sp_ix, c = (int)sp_ez, ops = (int)sp_ew;
+                if (ix < 0) {  // getOrElseUpdate (NS:61-62)
+                    ++ins;
+                    ix = sq_insert(S, sp_t, g_slot, 0, 0);
+                    c = 0;
+                    ops = 0;
+                    if (ix < 0) err = 1;
+                }
+                if (c - 1 >= 0) {  // RS.tryAcquire(1) (RS:62-70)
+                    c = c - 1;
+                    ops = jadd(ops, 1);
+                } else {  // the memory: RS.release(maxConcurrent - 1, false) (written by flush)
+                    pw_on = true;
+                    pw_t = sp_t;
+                    pw_v = left - g_mem;
+                    ops = jadd(ops, 1);
+                    const int n2 = jadd(c, g_maxc - 1);
+                    c = n2 % g_maxc == 0 ? jsub(n2, g_maxc) : n2;
+                }
+                if (ix >= 0) {
+                    S.map[ix].z = (uint32_t)c;
+                    S.map[ix].w = (uint32_t)ops;
+                }
+                return ins;
+            };
+            int acc = 0;  // memory the group's earlier decisions took at this lane's speculated target (sp_k 1 or 3)
+            bool inval = false;  // an earlier decision of its action was decided alone: its rank no longer holds
             int my_out = OWGS_NONE_V, my_fl = 0;
             int q = 0;
             for (; q < nq; ++q) {
+                {  // a run of decisions kept at once: speculated targets no other decision of the group speculated,
+                   // whose permits (less what the decisions decided one at a time so far took there) still hold them
+                    const bool inq = lane >= q && lane < nq && uniq;
+                    const bool fp = inq && sp_k == 1 && !inval && sp_pv - acc - sp_ks * g_mem >= g_mem;
+                    const bool fc = inq && sp_k == 3 && ((int)sp_ez >= 1 || sp_pv - acc >= g_mem);
+                    u64 nf = ~__ballot(fp || fc) & (~0ull << q);
+                    int L = min(nf ? ffs64(nf) : 64, nq);
+                    // (the map must not pass half full: each concurrent decision inserts at most SEQ_SPEC_C + 1)
+                    const u64 run = L >= 64 ? ~0ull << q : ((1ull << L) - 1) & (~0ull << q);
+                    if (2 * (filled + (long long)(SEQ_SPEC_C + 1) * __popcll(__ballot(fc) & run)) > (long long)S.map_cap) {
+                        nf = ~__ballot(fp) & (~0ull << q);
+                        L = min(nf ? ffs64(nf) : 64, L);
+                    }
+                    const bool fast = (fp || fc) && lane < L;
+                    if (L > q) {
+                        int ins = 0;
+                        if (fast && fc) {
+                            ins = conc_commit(sp_pv - acc);
+                            my_out = sp_t;
+                            my_fl = 0;
+                        }
+                        filled += __builtin_amdgcn_readlane(wave_sum(ins), 0);
+                        if (fast && fp) {  // (the cursors of decided-alone decisions after the run stay lower
+                                           // bounds: they are not moved past the run's steps)
+                            my_out = sp_t;
+                            my_fl = 0;
+                            pw_on = true;
+                            pw_t = sp_t;
+                            pw_v = sp_pv - acc - (sp_ks + 1) * g_mem;
+                            if (S.cur && g_a >= 0 && g_a < S.n_actions) {
+                                cw_on = true;
+                                cw_a = g_a;
+                                cw_s = sp_s;
+                                cw_p = sp_p;
+                            }
+                        }
+                        n_spec += L - q;
+                        q = L;
+                        tick(2);
+                        if (q >= nq) break;
+                    }
+                }
                 const int mem = __builtin_amdgcn_readlane(g_mem, q), maxc = __builtin_amdgcn_readlane(g_maxc, q);
                 const int slot = __builtin_amdgcn_readlane(g_slot, q), kind = __builtin_amdgcn_readlane(g_kind, q);
                 const int pool = __builtin_amdgcn_readlane(g_bb, q) ? 1 : 0;
@@ -342,11 +621,91 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                     stop = true;
                     break;
                 }
-                if (kind == 1) {
+                const int qk = __builtin_amdgcn_readlane(sp_k, q);
+                const bool qinv = __builtin_amdgcn_readlane((int)inval, q) != 0;
+                bool spec_done = false;
+                int taken_at = -1, taken = 0;  // the permits this decision took: invoker, memory
+                bool kept_plain = false;  // (its action's later decisions at its target count it through their ks)
+                if (kind == 0 && qk == 1 && !qinv) {  // a speculated target: held iff the permits there still hold it
+                    const int t = __builtin_amdgcn_readlane(sp_t, q);
+                    const bool qu = __builtin_amdgcn_readlane((int)uniq, q) != 0;
+                    const int left = __builtin_amdgcn_readlane(sp_pv, q) - __builtin_amdgcn_readlane(acc, q) -
+                                     (qu ? __builtin_amdgcn_readlane(sp_ks, q) * mem : 0);
+                    if (left >= mem) {  // tryAcquire succeeds at its turn (FS:63-71); every step before was full
+                        out = t;
+                        if (lane == q) {  // (written by flush)
+                            pw_on = true;
+                            pw_t = t;
+                            pw_v = left - mem;
+                        }
+                        taken_at = t;
+                        taken = mem;
+                        spec_done = true;
+                        kept_plain = qu;
+                        if (S.cur) {
+                            const int aq = __builtin_amdgcn_readlane(g_a, q);
+                            const int tsq = __builtin_amdgcn_readlane(sp_s, q);
+                            const uint32_t tpq = (uint32_t)__builtin_amdgcn_readlane((int)sp_p, q);
+                            if (lane > q && g_a == aq) {
+                                g_cs = tsq;
+                                g_cp = tpq;
+                            }
+                            if (lane == q && aq >= 0 && aq < S.n_actions) {
+                                cw_on = true;
+                                cw_a = aq;
+                                cw_s = tsq;
+                                cw_p = tpq;
+                            }
+                        }
+                    }
+                } else if (kind == 0 && qk == 3) {  // the first concurrent decision of its key in the group
+                    const int t = __builtin_amdgcn_readlane(sp_t, q);
+                    const int left = __builtin_amdgcn_readlane(sp_pv, q) - __builtin_amdgcn_readlane(acc, q);
+                    const int c0 = (int)(uint32_t)__builtin_amdgcn_readlane((int)sp_ez, q);
+                    if (c0 >= 1 || left >= mem) {  // a free slot (its entry unchanged), or the memory of a container
+                        int ins = 0;
+                        if (lane == q) ins = conc_commit(left);
+                        filled += __builtin_amdgcn_readlane(ins, q);
+                        out = t;
+                        taken_at = t;
+                        taken = c0 >= 1 ? 0 : mem;
+                        spec_done = true;
+                    }
+                } else if (kind == 0 && qk == 2 && !qinv) {  // the walk fails everywhere: forced (SCPB:417-424)
+                    const int H = pool ? hb : hm;
+                    spec_done = true;
+                    if (H > 0) {
+                        const int t = select_usable(base, (int)rng_index(S.rng_seed, seq, (uint32_t)H));
+                        if (t < 0) err = 1;
+                        else {
+                            flush();
+                            mem_done();  // (this group's earlier stores of its permits)
+                            if (lane == 0) S.permits[t] = jsub(ld_i(&S.permits[t]), mem);  // forceAcquire (FS:107-110)
+                            taken_at = t;
+                            taken = mem;
+                        }
+                        out = t >= 0 ? t : OWGS_NONE_V;
+                        fl = 1;
+                    }
+                    if (S.cur) {  // the cursor past the walk, as a walk that failed leaves it
+                        const int aq = __builtin_amdgcn_readlane(g_a, q);
+                        if (lane > q && g_a == aq) {
+                            g_cs = n + 2;
+                            g_cp = 0u;
+                        }
+                        if (lane == 0 && aq >= 0 && aq < S.n_actions) S.cur[aq] = make_uint4(gen, (uint32_t)(n + 2), 0u, 0u);
+                    }
+                }
+                if (spec_done) {
+                    ++n_spec;
+                } else if (kind == 1) {
                     out = OWGS_NONE_V;  // no invokers in the pool: None (SCPB:288-290)
                 } else if (kind == 2) {
                     out = OWGS_THROW_V;  // Int.MinValue hash: stepSizes / invokers index out of bounds (SCPB:266-268)
                 } else {
+                    flush();
+                    mem_done();  // (the stores of this group's speculated decisions, before this walk reads the state)
+                    ++n_alone;
                     const uint32_t step = (uint32_t)__builtin_amdgcn_readlane((int)g_step, q);
                     int t = -1;
                     // probes s = s0 + 64 u + lane, u = 0..3, in walk order (u, then lane); position (home + s step) mod
@@ -461,10 +820,12 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                     }
                     if (t >= 0) {
                         out = t;
+                        int took = 0;
                         if (lane == 0) {
                             if (maxc <= 1) {
                                 // tryAcquire succeeded (the walk read its permits) / forceAcquire (FS:107-110)
                                 S.permits[t] = jsub(fl ? ld_i(&S.permits[t]) : pvt, mem);
+                                took = mem;
                             } else {
                                 uint4 e = te;
                                 int ix = tix;
@@ -481,6 +842,7 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                                     ops = jadd(ops, 1);
                                 } else {  // the memory (tried above, or forced): RS.release(maxConcurrent - 1, false)
                                     S.permits[t] = jsub(fl ? ld_i(&S.permits[t]) : pvt, mem);
+                                    took = mem;
                                     ops = jadd(ops, 1);
                                     const int n2 = jadd(c, maxc - 1);
                                     c = n2 % maxc == 0 ? jsub(n2, maxc) : n2;
@@ -491,9 +853,19 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                                 }
                             }
                         }
+                        taken_at = t;
+                        taken = __builtin_amdgcn_readlane(took, 0);
                     } else {
                         out = OWGS_NONE_V;  // no healthy invoker: None (SCPB:419-420)
                     }
+                    // decided alone: the group's later decisions of its action re-walk (their ranks assumed it where
+                    // its speculation put it)
+                    const int aq = __builtin_amdgcn_readlane(g_a, q);
+                    if (maxc <= 1 && lane > q && g_a == aq) inval = true;
+                }
+                if (taken > 0) {
+                    const int aq = __builtin_amdgcn_readlane(g_a, q);
+                    acc += ((sp_k == 1 || sp_k == 3) && sp_t == taken_at && !(kept_plain && g_a == aq && uniq)) ? taken : 0;
                 }
                 if (lane == q) {
                     my_out = out;
@@ -501,8 +873,10 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                 }
                 filled = ((long long)__builtin_amdgcn_readlane((int)(filled >> 32), 0) << 32) |
                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)filled, 0);
-                mem_done();  // (lane 0's permit and entry stores, before the next decision reads them)
+                if (!spec_done) mem_done();  // (lane 0's permit and entry stores, before the next decision reads them)
+                tick(spec_done ? 2 : 3);
             }
+            flush();
             if (lane < q) {  // the decided part of the group (all of it unless the map must grow first)
                 S.out_inv[j0 + lane] = my_out;
                 S.out_flags[j0 + lane] = (uint8_t)my_fl;
@@ -512,6 +886,7 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
         }
         if (stop) break;
     }
+    const bool any_err = __ballot(err != 0) != 0;  // (any lane's: speculated decisions commit in their own lanes)
     if (lane == 0) {
         // where to resume (the map must grow first: a publish, phase 1) or done
         S.state[0] = stop ? 1 : 0;
@@ -520,7 +895,15 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
         S.state[3] = (int)(uint32_t)(j & 0xFFFFFFFFll);
         S.state[4] = (int)(j >> 32);
         S.state[5] = (int)gen;
-        if (err) atomicOr(S.err, OWGS_ERR_INTERNAL);
+        S.state[6] = n_spec;
+        S.state[7] = n_alone;
+        const u64 cys[4] = {cy0, cy1, cy2, cy3};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            S.state[8 + 2 * k] = (int)(uint32_t)cys[k];
+            S.state[9 + 2 * k] = (int)(uint32_t)(cys[k] >> 32);
+        }
+        if (any_err) atomicOr(S.err, OWGS_ERR_INTERNAL);
     }
 }
 

@@ -37,6 +37,7 @@ for n_inv in sizes:
         g_inv, g_fl, _ = b.replay(w.stream)
         ts.append(time.perf_counter() - t)
         exact &= bool(np.array_equal(g_inv, o_inv) and np.array_equal(g_fl, o_fl))
+        st = b.stats()
         b.close()
     dt = min(ts)
     print(json.dumps({"workload": f"headline-shaped, {n_inv} invokers x {mem} MB" + (f", conc {extra['conc_frac']}" if extra else ""),
@@ -44,4 +45,6 @@ for n_inv in sizes:
                       "batches": int(w.stream.n_batches), "gpu_ms": round(dt * 1e3, 2),
                       "gpu_decisions_per_s": n_act / dt, "oracle_1core_ms": round(cpu_s * 1e3, 1),
                       "oracle_decisions_per_s": n_act / cpu_s, "bit_exact": exact,
+                      "speculated": st.get("large_spec"), "decided_alone": st.get("large_alone"),
+                      "cycles": st.get("large_cycles"),
                       "note": "host ABI (owgs_replay), copies in and out inside the clock"}), flush=True)
