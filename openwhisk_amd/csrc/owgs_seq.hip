@@ -423,28 +423,39 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                     sx += SEQ_SPG;
                 }
             }
-            // concurrent decisions: the first of each fqn@version key in the group (the key's entries change only
-            // through its own decisions) walks from its home at the group's start: the first step whose entry has a
-            // free slot or whose permits hold a new container (tryAcquireConcurrent, NS:57-82); the steps it tried and
-            // failed whose entry is absent get the empty entry getOrElseUpdate leaves (NS:61-62) when it commits
-            // (sp_mask, bit = walk step).  Later decisions of the key are decided alone.
+            // concurrent decisions (the key's entries change only through its own decisions): the k-th decision of an
+            // fqn@version key in the group (k = crank) walks from its home at the group's start, rank-packed -- a step
+            // holds c free slots plus maxConcurrent per container its permits hold (tryAcquireConcurrent, NS:57-82),
+            // and the decision lands where the cumulative count first exceeds k.  The zero-capacity steps it tried whose
+            // entry is absent get the empty entry getOrElseUpdate leaves (NS:61-62) when it commits (sp_mask, bit =
+            // walk step; only those past the previous decision of its key's target: that one made the earlier ones).
+            // A key speculates past its first decision only when one action holds all its decisions in the group (one
+            // walk); otherwise the later ones are decided alone.
             const bool conc = lane < nq && g_kind == 0 && g_maxc > 1 && g_mem > 0;
-            bool kfirst = false;
+            int crank = 64;      // rank among the group's decisions of its key (64: not speculated)
+            bool ksolo = false;  // the key's only decision in the group
             {
                 u64 rem = __ballot(conc);
                 while (rem) {
                     const int j = ffs64(rem);
-                    const int s0 = __builtin_amdgcn_readlane(g_slot, j);
+                    const int s0 = __builtin_amdgcn_readlane(g_slot, j), a0 = __builtin_amdgcn_readlane(g_a, j);
                     const u64 m = __ballot(conc && g_slot == s0);
-                    if (lane == j) kfirst = true;
+                    const bool oneact = __ballot(conc && g_slot == s0 && g_a != a0) == 0;
+                    if (conc && g_slot == s0) {
+                        const int k = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        crank = (k == 0 || oneact) ? k : 64;
+                        ksolo = __popcll(m) == 1;
+                    }
                     rem &= ~m;
                 }
             }
             int sp_ix = -1;
             uint32_t sp_mask = 0u, sp_ez = 0u, sp_ew = 0u;
-            if (kfirst && (g_bb ? S.nb : S.nm) > SEQ_SPEC_C) {
+            if (crank < 64 && (g_bb ? S.nb : S.nm) > SEQ_SPEC_C) {
                 const int n = g_bb ? S.nb : S.nm, base = g_bb ? S.n_ids - S.nb : 0;
                 const uint32_t un = (uint32_t)n;
+                const float rm = 1.0f / (float)g_mem;
+                int cum = 0;
                 uint32_t pos = g_home;
                 for (int sx = 0; sx < SEQ_SPEC_C && sp_k == 0; sx += 4) {
                     int id[4], pv[4], ixs[4];
@@ -466,7 +477,15 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         if (sp_k != 0 || !tried[u]) continue;
-                        if ((ixs[u] >= 0 && (int)es[u].z >= 1) || pv[u] >= g_mem) {
+                        int cap = ixs[u] >= 0 ? min((int)es[u].z, 64) : 0;  // free slots, then containers
+                        if (pv[u] >= g_mem) {
+                            int nc = (int)((float)pv[u] * rm);
+                            const long long rr = (long long)pv[u] - (long long)nc * g_mem;
+                            nc += rr >= g_mem ? 1 : 0;
+                            nc -= rr < 0 ? 1 : 0;
+                            cap += min(nc, 64) * min(g_maxc, 64);
+                        }
+                        if (cum + cap > crank) {
                             sp_k = 3;
                             sp_t = id[u];
                             sp_pv = pv[u];
@@ -475,8 +494,9 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                             sp_ix = ixs[u];
                             sp_ez = ixs[u] >= 0 ? es[u].z : 0u;
                             sp_ew = ixs[u] >= 0 ? es[u].w : 0u;
-                        } else if (ixs[u] < 0) {
-                            sp_mask |= 1u << (sx + u);
+                        } else {
+                            if (cap == 0 && ixs[u] < 0) sp_mask |= 1u << (sx + u);
+                            cum += cap;
                         }
                     }
                 }
@@ -504,6 +524,28 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                 pw_on = false;
                 cw_on = false;
             };
+            // each key's speculated decisions in order: the previous one's target step (its empty entries end there); a
+            // decision whose earlier one of the key did not speculate is decided alone too
+            int sp_prev = -1;
+            {
+                u64 rem = __ballot(conc && crank < 64);
+                while (rem) {
+                    const int j = ffs64(rem);
+                    const int s0 = __builtin_amdgcn_readlane(g_slot, j);
+                    u64 m = __ballot(conc && crank < 64 && g_slot == s0);
+                    rem &= ~m;
+                    int prev = -1;
+                    bool ok = true;
+                    while (m) {
+                        const int i = ffs64(m);
+                        m &= m - 1;
+                        if (!ok && lane == i) sp_k = 0;
+                        if (lane == i) sp_prev = prev;
+                        ok = ok && __builtin_amdgcn_readlane(sp_k, i) == 3;
+                        prev = __builtin_amdgcn_readlane(sp_s, i);
+                    }
+                }
+            }
             // speculated targets no decision of ANOTHER action speculated in the group (a hash collision counts as
             // another's): there the decisions before one of the action's own at the target are exactly its ks earlier
             // ones (rank packing), each taking its memory
@@ -529,7 +571,7 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                 int ins = 0;
                 uint32_t pp = g_home;
                 for (int sx = 0; sx < sp_s; ++sx) {
-                    if ((sp_mask >> sx) & 1u) {
+                    if (sx > sp_prev && ((sp_mask >> sx) & 1u)) {
                         ++ins;
                         if (sq_insert(S, base_ + (int)pp, g_slot, 0, 0) < 0) err = 1;
                     }
@@ -559,6 +601,9 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                     S.map[ix].z = (uint32_t)c;
                     S.map[ix].w = (uint32_t)ops;
                 }
+                sp_ix = ix;  // (the entry as it leaves it: its key's later decisions at this invoker continue from it)
+                sp_ez = (uint32_t)c;
+                sp_ew = (uint32_t)ops;
                 return ins;
             };
             int acc = 0;  // memory the group's earlier decisions took at this lane's speculated target (sp_k 1 or 3)
@@ -570,7 +615,7 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                    // whose permits (less what the decisions decided one at a time so far took there) still hold them
                     const bool inq = lane >= q && lane < nq && uniq;
                     const bool fp = inq && sp_k == 1 && !inval && sp_pv - acc - sp_ks * g_mem >= g_mem;
-                    const bool fc = inq && sp_k == 3 && ((int)sp_ez >= 1 || sp_pv - acc >= g_mem);
+                    const bool fc = inq && sp_k == 3 && ksolo && !inval && ((int)sp_ez >= 1 || sp_pv - acc >= g_mem);
                     u64 nf = ~__ballot(fp || fc) & (~0ull << q);
                     int L = min(nf ? ffs64(nf) : 64, nq);
                     // (the map must not pass half full: each concurrent decision inserts at most SEQ_SPEC_C + 1)
@@ -658,14 +703,24 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                             }
                         }
                     }
-                } else if (kind == 0 && qk == 3) {  // the first concurrent decision of its key in the group
+                } else if (kind == 0 && qk == 3 && !qinv) {  // a speculated concurrent decision
                     const int t = __builtin_amdgcn_readlane(sp_t, q);
                     const int left = __builtin_amdgcn_readlane(sp_pv, q) - __builtin_amdgcn_readlane(acc, q);
                     const int c0 = (int)(uint32_t)__builtin_amdgcn_readlane((int)sp_ez, q);
-                    if (c0 >= 1 || left >= mem) {  // a free slot (its entry unchanged), or the memory of a container
+                    if (c0 >= 1 || left >= mem) {  // a free slot of its entry as it is now, or a container's memory
                         int ins = 0;
                         if (lane == q) ins = conc_commit(left);
                         filled += __builtin_amdgcn_readlane(ins, q);
+                        {  // its key's later decisions at this invoker see the entry it left
+                            const int nix = __builtin_amdgcn_readlane(sp_ix, q);
+                            const uint32_t nz = (uint32_t)__builtin_amdgcn_readlane((int)sp_ez, q);
+                            const uint32_t nw = (uint32_t)__builtin_amdgcn_readlane((int)sp_ew, q);
+                            if (lane > q && sp_k == 3 && g_slot == slot && sp_t == t) {
+                                sp_ix = nix;
+                                sp_ez = nz;
+                                sp_ew = nw;
+                            }
+                        }
                         out = t;
                         taken_at = t;
                         taken = c0 >= 1 ? 0 : mem;
@@ -862,6 +917,7 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                     // its speculation put it)
                     const int aq = __builtin_amdgcn_readlane(g_a, q);
                     if (maxc <= 1 && lane > q && g_a == aq) inval = true;
+                    if (maxc > 1 && lane > q && g_slot == slot) inval = true;  // (its key's later speculations)
                 }
                 if (taken > 0) {
                     const int aq = __builtin_amdgcn_readlane(g_a, q);
