@@ -166,6 +166,14 @@ for l in d['legs']:
       GPU_MAX_HW_QUEUES=8 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/rcclq8 -o run --output-format csv -- \
         python3 bench.py --health-churn --rccl ${CHURNARGS} --steps 3 --warmup 1 --no-cpu-baseline --no-check --no-h2d --no-shim-path > $O/rcclq8.log 2>&1
       rc=$?; tail -1 $O/rcclq8.log | cut -c1-200; [ $rc -eq 0 ] || stop rcclq8 $rc ;;
+    rcclline)  # with --rccl the bench's stdout must still be its one JSON line (RCCL's banner goes to stderr)
+      timeout -k 10 300 python bench.py --health-churn --rccl --steps 2 --warmup 1 --no-cpu-baseline --no-shim-path --no-h2d > $O/rcclline.out 2> $O/rcclline.err
+      rc=$?; [ $rc -eq 0 ] || { tail -5 $O/rcclline.err; stop rcclline $rc; }
+      python3 -c "
+import json,sys
+lines=open('$O/rcclline.out').read().splitlines()
+assert len(lines)==1, lines[:3]
+d=json.loads(lines[0]); print('one JSON line:', d['config']['health_exchange'], round(d['value']/1e6,2), 'M/s exact', d['bit_exact'])" || stop rcclline 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
