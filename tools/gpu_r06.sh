@@ -174,6 +174,19 @@ import json,sys
 lines=open('$O/rcclline.out').read().splitlines()
 assert len(lines)==1, lines[:3]
 d=json.loads(lines[0]); print('one JSON line:', d['config']['health_exchange'], round(d['value']/1e6,2), 'M/s exact', d['bit_exact'])" || stop rcclline 1 ;;
+    diag)  # per-phase cycles (profile build), re-decision costs (-DOWGS_EXT_PROF) and stop reasons of the engine
+      OWGS_LIB=openwhisk_amd/libowgs_prof.so REPS=2 timeout -k 10 300 python -u tools/prof_phases.py ${DIAGCFGS:-headline c2 c4 headline:0/8} > $O/phases.out 2>&1
+      rc=$?; tail -2 $O/phases.out | cut -c1-300; [ $rc -eq 0 ] || stop diag-phases $rc
+      OWGS_LIB=openwhisk_amd/variants/libowgs_extprof.so REPS=1 timeout -k 10 300 python -u tools/prof_phases.py ${DIAGCFGS:-headline c2 c4 headline:0/8} > $O/extprof.out 2>&1
+      rc=$?; tail -1 $O/extprof.out | cut -c1-300; [ $rc -eq 0 ] || stop diag-extprof $rc
+      OWGS_LIB=openwhisk_amd/variants/libowgs_why.so timeout -k 10 300 python -u tools/stop_reasons.py ${DIAGCFGS:-headline c2 c4 headline:0/8} > $O/why.out 2>&1
+      rc=$?; tail -1 $O/why.out | cut -c1-300; [ $rc -eq 0 ] || stop diag-why $rc ;;
+    resbd)  # the resident engine's per-call counters at drains 64 / 512 (in-tree library, then $AB_BASE if given)
+      for lib in openwhisk_amd/libowgs.so ${AB_BASE:+openwhisk_amd/variants/libowgs_${AB_BASE}.so}; do
+        n=$(basename $lib .so)
+        OWGS_LIB=$lib timeout -k 10 300 python -u tools/res_breakdown.py ${DRAINS:-64,512} > $O/resbd_$n.json 2> $O/resbd_$n.err
+        rc=$?; cut -c1-300 $O/resbd_$n.json; [ $rc -eq 0 ] || { tail -5 $O/resbd_$n.err; stop resbd $rc; }
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
