@@ -368,16 +368,17 @@ int owgs_engine_ms(owgs_ctx* ctx, float* ms);
  * started at a cursor, [12] walks skipped by the pool permit bound, [13] decisions committed from speculative walks,
  * [14] validation passes, [15] decisions decided alone, [16] their cycles, [17] speculation cycles, [18] validation
  * cycles (the decisions decided alone included), [19..23] cycles of the speculation's rank matching, plain walks and
- * concurrent walks, of the validation's map inserts and of the releases' concurrent part; [24] the duration in ns of
- * the last owgs_publish_batch / owgs_release_batch / owgs_process_batch call, entry to return, timed inside the
- * library; [25] 1 when the last owgs_replay / owgs_replay_device(_span) ran through the resident engine's stream mode
- * (OWGS_SPEC_REPLAY), [26..44] that replay's counters [5..23] summed over its launch (waits for the context's stream,
- * not for a live resident engine); [45], [46] the largest primary-table fill (live + deleted entries) and deleted
- * entries after a served call; [47], [48] host nanoseconds over the served calls: building the call (records, chunk
- * ranks), bell to answer; [49] launches that ended at the engine's lifetime bound (OWGS_RES_LIFE_US, default 100 ms:
- * it exits between calls so that launches of other streams sharing its hardware queue are not held back); [50] served
- * calls while watched pairs existed (after owgs_update_cluster with activations in flight).  Returns the number of
- * counters (51). */
+ * concurrent walks, of the validation's map inserts and of the releases' concurrent part; [24] chunks whose
+ * concurrent decisions the helper wave speculated while wave 0 finished the chunk before, [25] the helper wave's
+ * cycles in its concurrent walks; [26] the duration in ns of the last owgs_publish_batch / owgs_release_batch /
+ * owgs_process_batch call, entry to return, timed inside the library; [27] 1 when the last owgs_replay /
+ * owgs_replay_device(_span) ran through the resident engine's stream mode (OWGS_SPEC_REPLAY), [28..48] that replay's
+ * counters [5..25] summed over its launch (waits for the context's stream, not for a live resident engine); [49],
+ * [50] the largest primary-table fill (live + deleted entries) and deleted entries after a served call; [51], [52]
+ * host nanoseconds over the served calls: building the call (records, chunk ranks), bell to answer; [53] launches
+ * that ended at the engine's lifetime bound (OWGS_RES_LIFE_US, default 100 ms: it exits between calls so that
+ * launches of other streams sharing its hardware queue are not held back); [54] served calls while watched pairs
+ * existed (after owgs_update_cluster with activations in flight).  Returns the number of counters (55). */
 int owgs_resident_stats(owgs_ctx* ctx, int64_t* out, int32_t cap);
 
 /* Restore the slot state captured by owgs_snapshot (bench: every timed step starts from the same state). */

@@ -70,7 +70,7 @@ def _blob(items) -> tuple[np.ndarray, np.ndarray]:
 _RES_PROF = ("walk_rounds", "decisions", "stage_cycles", "release_cycles", "publish_cycles", "overflow_lookups",
              "cursor_walks", "bound_skips", "grouped_decisions", "validation_passes", "decided_alone",
              "alone_cycles", "speculation_cycles", "validation_cycles", "match_cycles", "plain_walk_cycles",
-             "conc_walk_cycles", "insert_cycles", "conc_release_cycles")
+             "conc_walk_cycles", "insert_cycles", "conc_release_cycles", "prespec_chunks", "helper_cycles")
 _NRP = len(_RES_PROF)
 
 

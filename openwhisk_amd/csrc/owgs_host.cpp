@@ -131,6 +131,8 @@ struct EnvOpts {
     int res_spec = 16;
     int res_cspec = 0;  // OWGS_RES_CSPEC: walk steps a concurrent publish speculates (0: max(4, res_spec / 4))
     int res_split = 1;  // OWGS_RES_SPLIT: helper waves (0-3) for the concurrent speculation; 0 = wave 0 itself
+    // OWGS_RES_PRE=0: the helper wave does not speculate a run's next chunk while wave 0 decides the current one
+    int res_pre = 1;
     // owgs_replay_device through the resident engine's stream mode (one wave deciding, speculative walks) instead of
     // the chunked engine, where it applies (identity pools, no watched pairs)
     int spec_replay = 0;
@@ -140,6 +142,7 @@ struct EnvOpts {
         if (const char* e = getenv("OWGS_RES_SPEC")) res_spec = atoi(e);
         if (const char* e = getenv("OWGS_RES_CSPEC")) res_cspec = atoi(e);
         if (const char* e = getenv("OWGS_RES_SPLIT")) res_split = atoi(e);
+        if (const char* e = getenv("OWGS_RES_PRE")) res_pre = atoi(e);
         if (const char* e = getenv("OWGS_RES_MAX")) res_max = atoi(e);
         if (const char* e = getenv("OWGS_RES_IDLE_US")) res_idle_us = atoll(e);
         if (const char* e = getenv("OWGS_RES_LIFE_US")) res_life_us = atoll(e);
@@ -1253,6 +1256,7 @@ static int res_launch(owgs_ctx* c) {
     a.spec = std::max(0, env_opts().res_spec);
     a.cspec = std::max(0, env_opts().res_cspec);
     a.hsplit = std::max(0, std::min(3, env_opts().res_split));
+    a.prespec = env_opts().res_pre;
     a.w = watch_args(c);
     a.w_sidx = c->d_w_sidx.p;
     a.w_scap = c->w_scap;
@@ -2735,6 +2739,7 @@ static int spec_replay(owgs_ctx* c, int32_t nb, const int64_t* acq_off, const in
     a.spec = std::max(0, env_opts().res_spec);
     a.cspec = std::max(0, env_opts().res_cspec);
     a.hsplit = std::max(0, std::min(3, env_opts().res_split));
+    a.prespec = env_opts().res_pre;
     a.smode = 1;
     a.s_nb = nb;
     a.s_nact = aid_end;

@@ -334,10 +334,11 @@ struct OwgsReleaseArgs {
 #define OWGS_RES_PROF 96    // device: the last call's counters (OWGS_RES_NPROF words: walk rounds, decisions,
                             // staging / release / publish cycles, overflow lookups, cursor hits, U shortcuts,
                             // decisions of the grouped walks)
-#define OWGS_RES_NPROF 19  // (+ validation passes, decisions decided alone, their cycles, speculation and
+#define OWGS_RES_NPROF 21  // (+ validation passes, decisions decided alone, their cycles, speculation and
                            // validation cycles: validation includes the decisions decided alone; speculation's
                            // rank matching, plain walks, concurrent walks; validation's entry inserts; the
-                           // releases' concurrent part)
+                           // releases' concurrent part; chunks whose concurrent decisions were speculated ahead;
+                           // the helper wave's concurrent walks)
 #define OWGS_RES_HDR 64     // host: the call -- n_runs, n_rel, n_pub, has_seq, seq_base lo, hi, then byte offsets in
                             // the input block of pub_off, the release invokers, the release actions, seq (u64), the
                             // block's length, the memory the releases return at most (lo, hi), and the byte
@@ -380,6 +381,7 @@ struct OwgsResArgs {
     int32_t spec;                // walk steps of each publish's speculative walk (0: decisions one at a time only)
     int32_t cspec;               // ... of a concurrent publish's (0: max(4, spec / 4))
     int32_t hsplit;              // wave 1 speculates the concurrent decisions of a chunk while wave 0 walks the others
+    int32_t prespec;             // (hsplit == 1) wave 1 speculates the concurrent decisions of a run's next chunk too
     // watched pairs after a reset (w.cap == 0: none): their releases in queue order with the
     // empty-entry rule, and the Z marks of the walks that tried and failed at them, inside the engine.  The host indexes
     // W by fqn@version key at launch: w_sidx (open addressing, w_scap a power of two) {slot + 1, first, count, primary

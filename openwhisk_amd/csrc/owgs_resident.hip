@@ -800,6 +800,88 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 }
                             }
                                 };
+        // speculation of a chunk's maxConcurrent == 1 decisions, one lane per decision (wave 0): each walks on its own
+        // against the state at the chunk's start, A.spec steps at most (4 permit reads in flight per round), from sbeg
+        // (its cursor).  Permits only fall inside a run (releases come first, SCPB:327-331 via CLB:260-346), so a step
+        // full then is full at the decision's turn: the walk's target stays the decision's unless the decisions before
+        // it took the room there, and a walk that found no room anywhere is a fallback whatever came before
+        // (SCPB:417-424).  Repeats of one action in the chunk share its walk: the k-th (rank k among the chunk's plain
+        // decisions of that action, from the record) passes over the room the k before it take, so it walks to the
+        // step where the capacity for its memory met so far, sum of floor(permits / mem), exceeds k.
+        auto pspec = [&](const uint4 me, const int nq_, const int sbeg, const int U0_, const int U1_, int& sp, int& sp_t,
+                         int& sp_ts, uint32_t& rounds) {
+            const int l_mem = (int)(me.y & OWGS_AM_MEM_MASK);
+            const int l_pool = (me.x & OWGS_AM_POOL) ? 1 : 0;
+            const int l_n = l_pool ? nb : nm, l_base = l_pool ? A.n_ids - nb : 0;
+            const int l_home = (int)(me.x & OWGS_AM_POS_MASK), l_step = (int)((me.x >> 15) & OWGS_AM_POS_MASK);
+            const bool l_c1 = lane < nq_ && !(me.y & (OWGS_AM_EMPTY | OWGS_AM_THROW)) &&
+                              ((me.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK) <= 1u;
+            const bool l_plain = l_c1 && l_mem <= (l_pool ? U1_ : U0_);
+            int need = l_plain ? (int)((me.w >> RES_RANK_SHIFT) & 63u) : 0;
+            const float rmem = __builtin_amdgcn_rcpf((float)max(l_mem, 1));
+            bool walking = false;
+            int wp = 0, ws = sbeg;
+            if (l_c1) {
+                if (!l_plain || sbeg >= l_n) {
+                    sp = SP_FAIL;  // mem above the pool's bound U, or a cursor past every step
+                } else {
+                    walking = true;
+                    wp = mod_fast(l_home + ws * l_step, l_n, __builtin_amdgcn_rcpf((float)l_n));
+                }
+            }
+            for (int it = 0; __ballot(walking); it += 4) {
+                if (walking) {
+                    int pk[4], vk[4];
+                    int pp = wp;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        pk[k] = pp;
+                        vk[k] = P[l_base + pp];
+                        pp += l_step;
+                        pp -= pp >= l_n ? l_n : 0;
+                    }
+                    int kf = 4;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int v = vk[k];
+                        if (kf == 4 && ws + k < l_n && v >= l_mem && v < OWGS_PLIM) {
+                            if (v >= (need + 1) * l_mem) {
+                                kf = k;
+                            } else {  // room for 1..need activations here (v < 64 mem: exact after correction)
+                                int c = (int)((float)v * rmem);
+                                c -= c * l_mem > v ? 1 : 0;
+                                c += (c + 1) * l_mem <= v ? 1 : 0;
+                                need -= c;
+                            }
+                        }
+                    }
+                    if (kf < 4) {
+                        sp = SP_FOUND;
+                        sp_t = l_base + (kf == 0 ? pk[0] : kf == 1 ? pk[1] : kf == 2 ? pk[2] : pk[3]);
+                        sp_ts = ws + kf;
+                        walking = false;
+                    } else {
+                        ws += 4;
+                        wp = pp;
+                        if (ws >= l_n) {
+                            sp = SP_FAIL;  // every pool position probed
+                            walking = false;
+                        } else if (it + 4 >= A.spec) {
+                            sp = SP_STOP;  // the rest of the walk: one at a time, from ws
+                            sp_ts = ws;
+                            walking = false;
+                        }
+                    }
+                }
+            }
+            rounds += (uint32_t)__popcll(__ballot(l_c1 && l_plain));
+        };
+        // the concurrent decisions of a run's next chunk speculated by the helper wave while wave 0 makes the current
+        // chunk's last decisions (round 6): one helper wave, no watched pairs (their walks leave marks), and wave 0
+        // takes such a speculation only while no overflow entry exists.  Read before some of the current chunk's takes,
+        // the permits are at least what the next chunk finds (capacities too high, never too low: a walk's target is
+        // at or before the decision's, and no step before it has room for the decision at its turn)
+        const bool pre_on = hsplit && A.hsplit == 1 && A.prespec != 0 && A.w.cap <= 0;
         const int bail = sc[RS_BAIL];
         if (bail == 0 && wave == 0) {
             int err = 0, hreq_n = 0;  // (hreq_n: requests posted to the helper wave in this call)
@@ -813,6 +895,12 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
             uint32_t pr_rounds = 0, pr_dec = 0, pr_ovf = 0, pr_hit = 0, pr_u = 0, pr_grp = 0, pr_pass = 0, pr_alone = 0;
             u64 pr_alone_cyc = 0, pr_spec_cyc = 0, pr_val_cyc = 0;
             u64 pr_c_match = 0, pr_c_pwalk = 0, pr_c_cwalk = 0, pr_c_ins = 0, pr_c_relc = 0;
+            uint32_t pr_pre = 0;
+            u64 pr_hcyc = 0;  // the helper wave's concurrent walks (cycles)
+            // the chunk the helper waves speculate ahead (-1 none), the plain helper's requests, and whether requests
+            // may still be posted in this call
+            int pre_i0 = -1;
+            bool pre_live = pre_on;
             const u64 pr_stage = clock64() - t_call;  // header, staging and the range check
             u64 pr_rel = 0, pr_pub = 0;
             int32_t* out_inv = (int32_t*)(stg + s_out);  // (LDS; copied to host memory after the call)
@@ -1303,12 +1391,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
 
                     if (A.spec > 0) {
                         const u64 tsp0 = clock64();
-                        // ---- speculation: every maxConcurrent == 1 decision walks on its own against the state at
-                        // the chunk's start, A.spec steps at most (4 permit reads in flight per round).  Permits only
-                        // fall inside a run (releases come first, SCPB:327-331 via CLB:260-346), so a step full then is
-                        // full at the decision's turn: the walk's target stays the decision's unless the decisions
-                        // before it took the room there, and a walk that found no room anywhere is a fallback whatever
-                        // came before (SCPB:417-424).
+                        // ---- speculation (pspec, cspec above), then validation in stream order
                         int sp = lane < nq ? SP_STOP : SP_NONE;
                         int sp_t = -1, sp_ts = 0;  // target, its walk step (SP_FOUND, SP_FORCED), or the step to resume
                         if (lane < nq && (me.y & (OWGS_AM_EMPTY | OWGS_AM_THROW))) {
@@ -1316,91 +1399,9 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             o_v = (me.y & OWGS_AM_EMPTY) ? OWGS_NONE_V : OWGS_THROW_V;
                         }
                         const int l_n = l_pool ? nb : nm, l_base = l_pool ? A.n_ids - nb : 0;
-                        const int l_home = (int)(me.x & OWGS_AM_POS_MASK), l_step = (int)((me.x >> 15) & OWGS_AM_POS_MASK);
-                        // repeats of one action in the chunk share its walk: the k-th (rank k among the chunk's plain
-                        // decisions of that action) passes over the room the k before it take, so it walks to the step
-                        // where the capacity for its memory met so far, sum of floor(permits / mem), exceeds k
                         const int l_maxc = (int)((me.y >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK);
                         const bool l_cc = lane < nq && !(me.y & (OWGS_AM_EMPTY | OWGS_AM_THROW)) && l_maxc > 1;
-                        // rank among the chunk's publishes of my action (one walk, one memory size), from the record
-                        const int l_rank = (int)((me.w >> RES_RANK_SHIFT) & 63u);
-                        int need = l_plain ? l_rank : 0;
-                        const u64 tm1 = clock64();
-                        pr_c_match += tm1 - tsp0;
-                        const int rank = need;
-                        const float rmem = __builtin_amdgcn_rcpf((float)max(l_mem, 1));
-                        bool walking = false;
-                        int wp = 0, ws = l_sbeg;
-                        if (l_c1) {
-                            if (!l_plain || l_sbeg >= l_n) {
-                                sp = SP_FAIL;  // mem above the pool's bound U, or a cursor past every step
-                            } else {
-                                walking = true;
-                                wp = mod_fast(l_home + ws * l_step, l_n, __builtin_amdgcn_rcpf((float)l_n));
-                            }
-                        }
-                        // the chunk's concurrent decisions go to the helper wave (their speculation reads the state
-                        // only, and every earlier change of it is published by the release below)
-                        const bool hreq = hsplit && !ovf_on && __ballot(l_cc) != 0ull;
-                        bool hreq_lost = false;
-                        if (hreq) {
-                            ++hreq_n;
-                            if (lane == 0) {
-                                sc[RS_HI0] = i0;
-                                sc[RS_HNQ] = nq;
-                            }
-                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-                            if (lane == 0)
-                                __hip_atomic_store(&sc[RS_HGO], hreq_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        }
-                        for (int it = 0; __ballot(walking); it += 4) {
-                            if (walking) {
-                                int pk[4], vk[4];
-                                int pp = wp;
-#pragma unroll
-                                for (int k = 0; k < 4; ++k) {
-                                    pk[k] = pp;
-                                    vk[k] = P[l_base + pp];
-                                    pp += l_step;
-                                    pp -= pp >= l_n ? l_n : 0;
-                                }
-                                int kf = 4;
-#pragma unroll
-                                for (int k = 0; k < 4; ++k) {
-                                    const int v = vk[k];
-                                    if (kf == 4 && ws + k < l_n && v >= l_mem && v < OWGS_PLIM) {
-                                        if (v >= (need + 1) * l_mem) {
-                                            kf = k;
-                                        } else {  // room for 1..need activations here (v < 64 mem: exact after correction)
-                                            int c = (int)((float)v * rmem);
-                                            c -= c * l_mem > v ? 1 : 0;
-                                            c += (c + 1) * l_mem <= v ? 1 : 0;
-                                            need -= c;
-                                        }
-                                    }
-                                }
-                                if (kf < 4) {
-                                    sp = SP_FOUND;
-                                    sp_t = l_base + (kf == 0 ? pk[0] : kf == 1 ? pk[1] : kf == 2 ? pk[2] : pk[3]);
-                                    sp_ts = ws + kf;
-                                    walking = false;
-                                } else {
-                                    ws += 4;
-                                    wp = pp;
-                                    if (ws >= l_n) {
-                                        sp = SP_FAIL;  // every pool position probed
-                                        walking = false;
-                                    } else if (it + 4 >= A.spec) {
-                                        sp = SP_STOP;  // the rest of the walk: one at a time, from ws
-                                        sp_ts = ws;
-                                        walking = false;
-                                    }
-                                }
-                            }
-                        }
-                        pr_rounds += (uint32_t)__popcll(__ballot(l_c1 && l_plain));
-                        const u64 tm2 = clock64();
-                        pr_c_pwalk += tm2 - tm1;
+                        const int rank = l_plain ? (int)((me.w >> RES_RANK_SHIFT) & 63u) : 0;
                         // concurrent decisions (maxConcurrent > 1) walk too; a step takes one when the invoker is usable
                         // and the key's container there has a free slot or the invoker has the memory for a new one
                         // (tryAcquireConcurrent, NS:57-82).  Only decisions of the same fqn@version key change its map
@@ -1411,21 +1412,33 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                         int c_ix = -1;        // the target's map entry (primary index, OWGS_CTC + overflow index, -1 none)
                         uint32_t c_nv = 0u;   // the entry's value after this decision
                         bool c_take = false;  // the decision opens a container: it takes memory (NS:70-79)
-                        if (__ballot(l_cc)) {
-                            if (hreq) {  // the helper wave's answer to request hreq_n
-                                for (int spin = 0;; ++spin) {
-                                    if (__hip_atomic_load(&sc[RS_HDONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ==
-                                        hreq_n * nhelp)
-                                        break;
-                                    if (spin > (1 << 26)) {  // (never expected: decide here instead of waiting on)
-                                        hreq_lost = true;
-                                        break;
-                                    }
-                                    __builtin_amdgcn_s_sleep(1);
+                        const u64 tm1 = clock64();
+                        pr_c_match += tm1 - tsp0;
+                        u64 tm2 = tm1;
+                        // this chunk's concurrent decisions speculated by the helper wave right after the previous
+                        // chunk was decided (against this state: taken as they are unless an overflow entry appeared,
+                        // whose lookups it did not make); the plain walks run here meanwhile
+                        bool pre_done = false;
+                        if (pre_i0 == i0) {
+                            pre_i0 = -1;
+                            pre_done = true;
+                            pspec(me, nq, l_sbeg, U0, U1, sp, sp_t, sp_ts, pr_rounds);
+                            tm2 = clock64();
+                            pr_c_pwalk += tm2 - tm1;
+                            bool lost = false;
+                            for (int spin = 0;; ++spin) {
+                                if (__hip_atomic_load(&sc[RS_HDONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == hreq_n)
+                                    break;
+                                if (spin > (1 << 26)) {  // (never expected: decide here, and no further requests)
+                                    lost = true;
+                                    break;
                                 }
-                                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                                __builtin_amdgcn_s_sleep(1);
                             }
-                            if (hreq && !hreq_lost) {
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                            if (lost) pre_live = false;
+                            if (!lost && !ovf_on) {
+                                ++pr_pre;
                                 const uint4 h0 = hx[lane], h1 = hx[64 + lane];
                                 if (l_cc) {
                                     sp = (int)h0.x;
@@ -1435,12 +1448,66 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                     c_take = h1.x != 0u;
                                 }
                                 err |= (int)h1.y;
-                            } else {
+                                pr_hcyc += __builtin_amdgcn_readfirstlane(h1.w);
+                            } else if (__ballot(l_cc)) {
                                 int e_ = 0;
                                 uint32_t n_ovf = 0u;
                                 cspec(me, nq, ovf_on, sp, sp_t, c_ix, c_nv, c_take, e_, n_ovf);
                                 err |= e_;
                                 pr_ovf += n_ovf;
+                            }
+                        }
+                        if (!pre_done) {
+                            // the chunk's concurrent decisions go to the helper wave (their speculation reads the state
+                            // only, and every earlier change of it is published by the release below)
+                            const bool hreq = hsplit && !ovf_on && __ballot(l_cc) != 0ull;
+                            bool hreq_lost = false;
+                            if (hreq) {
+                                ++hreq_n;
+                                if (lane == 0) {
+                                    sc[RS_HI0] = i0;
+                                    sc[RS_HNQ] = nq;
+                                }
+                                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                                if (lane == 0)
+                                    __hip_atomic_store(&sc[RS_HGO], hreq_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            }
+                            pspec(me, nq, l_sbeg, U0, U1, sp, sp_t, sp_ts, pr_rounds);
+                            tm2 = clock64();
+                            pr_c_pwalk += tm2 - tm1;
+                            if (__ballot(l_cc)) {
+                                if (hreq) {  // the helper wave's answer to request hreq_n
+                                    for (int spin = 0;; ++spin) {
+                                        if (__hip_atomic_load(&sc[RS_HDONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ==
+                                            hreq_n * nhelp)
+                                            break;
+                                        if (spin > (1 << 26)) {  // (never expected: decide here instead of waiting on)
+                                            hreq_lost = true;
+                                            break;
+                                        }
+                                        __builtin_amdgcn_s_sleep(1);
+                                    }
+                                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                                    if (hreq_lost) pre_live = false;
+                                }
+                                if (hreq && !hreq_lost) {
+                                    const uint4 h0 = hx[lane], h1 = hx[64 + lane];
+                                    if (l_cc) {
+                                        sp = (int)h0.x;
+                                        sp_t = (int)h0.y;
+                                        c_ix = (int)h0.z;
+                                        c_nv = h0.w;
+                                        c_take = h1.x != 0u;
+                                    }
+                                    err |= (int)h1.y;
+                                    pr_hcyc += __builtin_amdgcn_readfirstlane(h1.w);
+                                } else {
+                                    int e_ = 0;
+                                    uint32_t n_ovf = 0u;
+                                    cspec(me, nq, ovf_on, sp, sp_t, c_ix, c_nv, c_take, e_, n_ovf);
+                                    err |= e_;
+                                    pr_ovf += n_ovf;
+                                }
                             }
                         }
                         // a failed walk bounds the pool's usable permits below its memory (U), and the fallback's
@@ -1494,15 +1561,14 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             ++pr_pass;
                             const bool cand = lane >= q && (sp == SP_FOUND || sp == SP_FORCED);
                             const bool take = cand && !c_slot;
-                            // every candidate takes its memory at once (LDS atomics); then F = the permits left at its
-                            // target after all of them.  A decision that walked there holds iff the permits before it
-                            // minus its own take and the takes before it stay >= 0, i.e. iff F plus the takes AFTER it
-                            // at the same invoker is >= 0: always when F >= 0; only targets that went negative need the
+                            bool fits = true;
+                            // every candidate takes its memory at once (LDS atomics); then F = the permits left at
+                            // its target after all of them: the decision holds iff F plus the takes AFTER it at the
+                            // same invoker is >= 0 -- always when F >= 0; only targets that went negative need the
                             // per-invoker sums (a ballot match on the target id)
                             if (take) atomicSub(&P[sp_t], l_mem);  // tryAcquire (FS:63-71) / forceAcquire (FS:102-110)
                             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // (every lane's take before the reads)
                             const int F = take ? P[sp_t] : 0;
-                            bool fits = true;
                             if (__ballot(take && sp == SP_FOUND && F < 0)) {
                                 const bool mt = take && F < 0;
                                 u64 eq = __ballot(mt);
@@ -1527,7 +1593,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             if (take && lane >= f) atomicAdd(&P[sp_t], l_mem);  // the takes from the first miss on: back
                             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                             if (cand && lane < f) {
-                                if (take && P[sp_t] < -OWGS_PLIM) err |= OWGS_ERR_PERMITS;  // (after the give-backs)
+                                if (take && P[sp_t] < -OWGS_PLIM) err |= OWGS_ERR_PERMITS;  // (after the takes)
                                 // the key's container at the target: a slot taken, or a new one (NS:63-79); decisions of
                                 // one key at one invoker leave values whose operationCount grows with each: the largest
                                 // is the last one's
@@ -1596,6 +1662,26 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             pr_c_ins += clock64() - ti0;
                             pr_grp += (uint32_t)__popcll(__ballot(cand && lane < f));
                             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                            // this chunk decided: the concurrent decisions of the run's next chunk to the helper wave,
+                            // which walks them against the state they will find (nothing changes it before their
+                            // validation) while wave 0 writes this chunk's outputs and walks the next chunk's others
+                            if (f >= nq && pre_live && i0 + 64 < pe && !ovf_on) {
+                                const int ni0 = i0 + 64, nnq = min(64, pe - ni0);
+                                const uint32_t ny = lane < nnq ? pub[ni0 + lane].y : OWGS_AM_EMPTY;
+                                const bool ncc = !(ny & (OWGS_AM_EMPTY | OWGS_AM_THROW)) &&
+                                                 ((ny >> OWGS_AM_MAXC_SHIFT) & OWGS_AM_MAXC_MASK) > 1u;
+                                if (__ballot(ncc)) {
+                                    ++hreq_n;
+                                    if (lane == 0) {
+                                        sc[RS_HI0] = ni0;
+                                        sc[RS_HNQ] = nnq;
+                                    }
+                                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                                    if (lane == 0)
+                                        __hip_atomic_store(&sc[RS_HGO], hreq_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                    pre_i0 = ni0;
+                                }
+                            }
                             if (f >= nq) {
                                 pr_val_cyc += clock64() - tsp1;
                                 break;
@@ -1804,6 +1890,8 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 st_sys(pr + 16, (int)min(pr_c_cwalk, (u64)0x7FFFFFFF));
                 st_sys(pr + 17, (int)min(pr_c_ins, (u64)0x7FFFFFFF));
                 st_sys(pr + 18, (int)min(pr_c_relc, (u64)0x7FFFFFFF));
+                st_sys(pr + 19, (int)pr_pre);
+                st_sys(pr + 20, (int)min(pr_hcyc, (u64)0x7FFFFFFF));
                 st_sys(&A.ctl[OWGS_RES_GEN], (int)gen);
             } else if (lane == 0 && A.s_stats) {  // stream mode: summed over the launch (owgs_resident_stats' order)
                 A.s_stats[0] += pr_rounds;
@@ -1825,6 +1913,8 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 A.s_stats[16] += pr_c_cwalk;
                 A.s_stats[17] += pr_c_ins;
                 A.s_stats[18] += pr_c_relc;
+                A.s_stats[19] += pr_pre;
+                A.s_stats[20] += pr_hcyc;
             }
             if (lane == 0) {
                 sc[RS_USED] = used;
@@ -1861,10 +1951,12 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 int sp = SP_STOP, sp_t = -1, c_ix = -1, e_ = 0;
                 uint32_t c_nv = 0u, n_ovf = 0u;
                 bool c_take = false;
+                const u64 th0 = clock64();
                 cspec(me, hnq, false, sp, sp_t, c_ix, c_nv, c_take, e_, n_ovf);
+                const uint32_t th = (uint32_t)min(clock64() - th0, (u64)0x7FFFFFFF);  // (its walk's cycles)
                 if (mine) {
                     hx[lane] = make_uint4((uint32_t)sp, (uint32_t)sp_t, (uint32_t)c_ix, c_nv);
-                    hx[64 + lane] = make_uint4(c_take ? 1u : 0u, (uint32_t)e_, n_ovf, 0u);
+                    hx[64 + lane] = make_uint4(c_take ? 1u : 0u, (uint32_t)e_, n_ovf, th);
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
                 if (lane == 0) atomicAdd(&sc[RS_HDONE], 1);  // (wave 0 waits for nhelp answers per request)

@@ -118,6 +118,8 @@ def test_resident_small_drains_match_oracle(cfg, kw):
     st = sh.g.resident_stats()
     assert st["served"] == sh.calls and st["chained"] == 0 and st["refused"] == 0, st
     assert st["launches"] - st["life_exits"] == 1, st  # (relaunches only at the lifetime bound, OWGS_RES_LIFE_US)
+    if cfg in ("headline", "c4"):  # (configs with concurrent actions) the helper wave speculated some chunks ahead
+        assert st["prespec_chunks"] > 0, st
     assert np.array_equal(sh.g.permits(), sh.o.permits())
     assert sh.g.resident_stats()["alive"] == 0  # permits() stopped it (the state was written back)
     assert pubs == int(w.stream.acq_off[-1])
@@ -287,19 +289,21 @@ print("ok")
 """
 
 
-@pytest.mark.parametrize("budget,split", [("0", "1"), ("1", "1"), ("4", "1"), ("16", "0")])
-def test_resident_speculation_budgets(budget, split):
+@pytest.mark.parametrize("budget,split,pre", [("0", "1", "1"), ("1", "1", "1"), ("4", "1", "1"), ("16", "0", "1"),
+                                              ("16", "1", "0"), ("4", "1", "0")])
+def test_resident_speculation_budgets(budget, split, pre):
     """Walk budgets of 0 (no speculation: decisions one at a time), 1 and 4 steps (most walks unfinished: decided
     alone from where the speculation stopped) give the same decisions, and so does the default budget with the
-    concurrent speculation on wave 0 instead of the helper wave (OWGS_RES_SPLIT=0).  The switches are read once per
-    process, so each case runs in a child process."""
+    concurrent speculation on wave 0 instead of the helper wave (OWGS_RES_SPLIT=0), and without the helper waves'
+    speculation of a run's next chunk (OWGS_RES_PRE=0).  The switches are read once per process, so each case runs in
+    a child process."""
     import os
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     root = os.path.dirname(here)
     code = _BUDGET_SCRIPT.format(root=root, oracle=os.path.join(root, "oracle"), tests=here)
-    env = dict(os.environ, OWGS_RES_SPEC=budget, OWGS_RES_SPLIT=split)
+    env = dict(os.environ, OWGS_RES_SPEC=budget, OWGS_RES_SPLIT=split, OWGS_RES_PRE=pre)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
