@@ -1184,35 +1184,48 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
                                                      : ((tid < 4 || tid >= SC_CFT) ? OWGS_WL : (tid < 6 ? (int)0x80000000 : 0));
     if (A.rel_bound) lds_sync();  // (SC_RRISK is set below)
     bool rrisk = false;    // (owgs_process_batch) a slot the call's releases could push out of the LDS range
-    for (int i0 = 0; i0 < n_slots; i0 += OWGS_NT * LB) {
-        int v[LB];
-        uint32_t u[LB];
+    // permits four slots per 16-byte load, with their usable word and (owgs_process_batch) their release bounds, all
+    // issued before any is used: one round trip per 10,240 slots (the headline's state in one)
+    constexpr int LB4 = 5;
+    const int n4 = n_slots >> 2;
+    auto slot_in = [&](int i, int v, uint32_t u, unsigned long long bnd) {
+        if (v < -OWGS_PLIM || v >= OWGS_PLIM) err |= OWGS_ERR_PERMITS;
+        const bool unusable = pool_mode == 0 && i < A.n_ids && !((u >> (i & 31)) & 1u);
+        if (bnd) rrisk = rrisk || (long long)v + (long long)bnd >= (long long)OWGS_PLIM;
+        return unusable ? v + OWGS_PENC : v;
+    };
+    for (int j0 = 0; j0 < n4; j0 += OWGS_NT * LB4) {
+        int4 v[LB4];
+        uint32_t u[LB4];
+        ulonglong2 r0[LB4], r1[LB4];
 #pragma unroll
-        for (int k = 0; k < LB; ++k) {
-            const int i = i0 + k * OWGS_NT + tid;
-            v[k] = i < n_slots ? A.permits[i] : 0;
-            u[k] = (pool_mode == 0 && i < A.n_ids) ? A.usable[i >> 5] : ~0u;
-        }
-#pragma unroll
-        for (int k = 0; k < LB; ++k) {
-            const int i = i0 + k * OWGS_NT + tid;
-            if (i >= n_slots) continue;
-            if (v[k] < -OWGS_PLIM || v[k] >= OWGS_PLIM) err |= OWGS_ERR_PERMITS;
-            const bool unusable = !((u[k] >> (i & 31)) & 1u);
-            P[i] = unusable ? v[k] + OWGS_PENC : v[k];
-        }
-        if (A.rel_bound) {
-#pragma unroll
-            for (int k = 0; k < LB; ++k) {
-                const int i = i0 + k * OWGS_NT + tid;
-                if (i >= n_slots) continue;
-                const unsigned long long bnd = A.rel_bound[i];
-                if (bnd) {
-                    rrisk = rrisk || (long long)v[k] + (long long)bnd >= (long long)OWGS_PLIM;
-                    A.rel_bound[i] = 0ull;
-                }
+        for (int k = 0; k < LB4; ++k) {
+            const int j = j0 + k * OWGS_NT + tid;
+            v[k] = j < n4 ? ((const int4*)A.permits)[j] : make_int4(0, 0, 0, 0);
+            u[k] = (pool_mode == 0 && j < n4 && 4 * j < A.n_ids) ? A.usable[j >> 3] : ~0u;
+            r0[k] = r1[k] = make_ulonglong2(0ull, 0ull);
+            if (A.rel_bound && j < n4) {
+                r0[k] = ((const ulonglong2*)A.rel_bound)[2 * j];
+                r1[k] = ((const ulonglong2*)A.rel_bound)[2 * j + 1];
             }
         }
+#pragma unroll
+        for (int k = 0; k < LB4; ++k) {
+            const int j = j0 + k * OWGS_NT + tid;
+            if (j >= n4) continue;
+            const int i = 4 * j;
+            ((int4*)P)[j] = make_int4(slot_in(i, v[k].x, u[k], r0[k].x), slot_in(i + 1, v[k].y, u[k], r0[k].y),
+                                      slot_in(i + 2, v[k].z, u[k], r1[k].x), slot_in(i + 3, v[k].w, u[k], r1[k].y));
+            if (A.rel_bound && (r0[k].x | r0[k].y | r1[k].x | r1[k].y)) {
+                ((ulonglong2*)A.rel_bound)[2 * j] = make_ulonglong2(0ull, 0ull);
+                ((ulonglong2*)A.rel_bound)[2 * j + 1] = make_ulonglong2(0ull, 0ull);
+            }
+        }
+    }
+    for (int i = 4 * n4 + tid; i < n_slots; i += OWGS_NT) {  // (the last n_slots % 4 slots)
+        const unsigned long long bnd = A.rel_bound ? A.rel_bound[i] : 0ull;
+        P[i] = slot_in(i, A.permits[i], (pool_mode == 0 && i < A.n_ids) ? A.usable[i >> 5] : ~0u, bnd);
+        if (bnd) A.rel_bound[i] = 0ull;
     }
     if (rrisk) sc[SC_RRISK] = 1;
     if (pool_mode == 0) {

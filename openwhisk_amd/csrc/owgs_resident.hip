@@ -296,25 +296,62 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
     }
     {
         int used = 0, tombs = 0, mx = (int)0x80000000, u0 = (int)0x80000000, u1 = (int)0x80000000, e = 0;
-        for (int i = tid; i < n_slots; i += 256) {
-            const int v = A.permits[i];
-            const bool unusable = !(i < A.n_ids && ((A.usable[i >> 5] >> (i & 31)) & 1u));
+        auto slot_in = [&](int i, int v, uint32_t u) {
+            const bool unusable = !(i < A.n_ids && ((u >> (i & 31)) & 1u));
             if (v < -OWGS_PLIM || v >= OWGS_PLIM) e |= OWGS_ERR_PERMITS;
-            P[i] = unusable ? v + OWGS_PENC : v;
             mx = max(mx, v);
             if (!unusable && i < nm) u0 = max(u0, v);
             if (!unusable && i >= A.n_ids - nb && i < A.n_ids) u1 = max(u1, v);
+            return unusable ? v + OWGS_PENC : v;
+        };
+        // four slots per 16-byte load, ten loads in flight per thread: one round trip per 10,240 slots
+        constexpr int LB4 = 10;
+        const int n4 = n_slots >> 2;
+        for (int j0 = 0; j0 < n4; j0 += 256 * LB4) {
+            int4 v[LB4];
+            uint32_t u[LB4];
+#pragma unroll
+            for (int k = 0; k < LB4; ++k) {
+                const int j = j0 + k * 256 + tid;
+                v[k] = j < n4 ? ((const int4*)A.permits)[j] : make_int4(0, 0, 0, 0);
+                u[k] = (j < n4 && 4 * j < A.n_ids) ? A.usable[j >> 3] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < LB4; ++k) {
+                const int j = j0 + k * 256 + tid;
+                if (j < n4)
+                    ((int4*)P)[j] = make_int4(slot_in(4 * j, v[k].x, u[k]), slot_in(4 * j + 1, v[k].y, u[k]),
+                                              slot_in(4 * j + 2, v[k].z, u[k]), slot_in(4 * j + 3, v[k].w, u[k]));
+            }
         }
+        for (int i = 4 * n4 + tid; i < n_slots; i += 256)  // (the last n_slots % 4 slots)
+            P[i] = slot_in(i, A.permits[i], i < A.n_ids ? A.usable[i >> 5] : 0u);
         atomicMax(&sc[RS_U0], u0);
         atomicMax(&sc[RS_U1], u1);
         for (int i = tid; i <= words; i += 256) ub[i] = i < words ? A.usable[i] : 0u;
-        for (int i = tid; i < OWGS_CTC; i += 256) {
-            const uint32_t k = A.ct_keys[i];
-            ct[i] = make_uint2(k, A.ct_vals[i]);
-            if (k != 0u && k != OWGS_CT_TOMB) bf_add(bf, k);
-            used += k != 0u;
-            tombs += k == OWGS_CT_TOMB;
+        // the primary table: four entries per 16-byte load of keys and of values, all in flight together
+        {
+            uint4 kq[OWGS_CTC / 1024], vq[OWGS_CTC / 1024];
+#pragma unroll
+            for (int k = 0; k < OWGS_CTC / 1024; ++k) {
+                kq[k] = ((const uint4*)A.ct_keys)[k * 256 + tid];
+                vq[k] = ((const uint4*)A.ct_vals)[k * 256 + tid];
+            }
+#pragma unroll
+            for (int k = 0; k < OWGS_CTC / 1024; ++k) {
+                const int i = 4 * (k * 256 + tid);
+                const uint32_t kk[4] = {kq[k].x, kq[k].y, kq[k].z, kq[k].w}, vv[4] = {vq[k].x, vq[k].y, vq[k].z, vq[k].w};
+                ((uint4*)ct)[i / 2] = make_uint4(kk[0], vv[0], kk[1], vv[1]);
+                ((uint4*)ct)[i / 2 + 1] = make_uint4(kk[2], vv[2], kk[3], vv[3]);
+#pragma unroll
+                for (int e4 = 0; e4 < 4; ++e4) {
+                    if (kk[e4] != 0u && kk[e4] != OWGS_CT_TOMB) bf_add(bf, kk[e4]);
+                    used += kk[e4] != 0u;
+                    tombs += kk[e4] == OWGS_CT_TOMB;
+                }
+            }
         }
+        static_assert(OWGS_CTC % 1024 == 0, "the primary table loads 4 entries per thread per round");
         if (used) atomicAdd(&sc[RS_USED], used);
         if (tombs) atomicAdd(&sc[RS_TOMB], tombs);
         atomicMax(&sc[RS_MAXP], mx);

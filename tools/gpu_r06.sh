@@ -187,6 +187,9 @@ d=json.loads(lines[0]); print('one JSON line:', d['config']['health_exchange'], 
         OWGS_LIB=$lib timeout -k 10 300 python -u tools/res_breakdown.py ${DRAINS:-64,512} > $O/resbd_$n.json 2> $O/resbd_$n.err
         rc=$?; cut -c1-300 $O/resbd_$n.json; [ $rc -eq 0 ] || { tail -5 $O/resbd_$n.err; stop resbd $rc; }
       done ;;
+    chainphases)  # per-phase engine cycles of the chained calls (profile build) at drain $DRAINS (default 4096)
+      OWGS_LIB=openwhisk_amd/libowgs_prof.so CALLS=${CALLS:-120} timeout -k 10 300 python -u tools/shim_phases.py ${DRAINS:-4096} > $O/chainphases.json 2> $O/chainphases.err
+      rc=$?; cut -c1-600 $O/chainphases.json; [ $rc -eq 0 ] || { tail -5 $O/chainphases.err; stop chainphases $rc; } ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
