@@ -190,6 +190,13 @@ d=json.loads(lines[0]); print('one JSON line:', d['config']['health_exchange'], 
     chainphases)  # per-phase engine cycles of the chained calls (profile build) at drain $DRAINS (default 4096)
       OWGS_LIB=openwhisk_amd/libowgs_prof.so CALLS=${CALLS:-120} timeout -k 10 300 python -u tools/shim_phases.py ${DRAINS:-4096} > $O/chainphases.json 2> $O/chainphases.err
       rc=$?; cut -c1-600 $O/chainphases.json; [ $rc -eq 0 ] || { tail -5 $O/chainphases.err; stop chainphases $rc; } ;;
+    cwsweep)  # chunk width sweep (OWGS_CW) of one config's engine rate, each width twice, alternating
+      for i in 1 2; do
+        for w in ${CWS:-128 160 192 224 256}; do
+          OWGS_CW=$w REPS=3 timeout -k 10 300 python -u tools/prof_phases.py ${CWCFG:-c2} > $O/cw_${w}_$i.log 2>&1
+          rc=$?; echo "cw $w: $(grep -v amdgpu.ids $O/cw_${w}_$i.log | grep -v cycles/activation | cut -c1-110)" | tee -a $O/cwsweep.txt; [ $rc -eq 0 ] || stop cwsweep $rc
+        done
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
