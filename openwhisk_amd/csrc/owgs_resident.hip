@@ -162,23 +162,27 @@ __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
 #define RS_HI0 16    // helper wave: the chunk's first publish and its size
 #define RS_HNQ 17
 
-// blocked Bloom filter over the primary table's keys (LDS, RES_BF words): one word and three bits per key, set on
+// blocked Bloom filter over the primary table's keys (LDS, RES_BF words): one word and two bits per key, set on
 // every insert into the primary and rebuilt with it; a key whose bits are not all set is not in the primary, so a
-// lookup that misses -- the common case on a concurrent walk -- reads one word instead of a probe chain
-__device__ __forceinline__ uint2 bf_pos(uint32_t key) {
-    const uint32_t h = ct_hash(key * 0x9E3779B1u);
-    return make_uint2(h & (RES_BF - 1), (1u << ((h >> 11) & 31)) | (1u << ((h >> 16) & 31)) | (1u << ((h >> 21) & 31)));
+// lookup that misses -- the common case on a concurrent walk -- reads one word instead of a probe chain.  The word and
+// the bits come from the same hash as the key's home block (ct_hash: bits 0-9 the home block of OWGS_CTC / 4, 10-20
+// the word, 21-25 and 26-30 the bits), so a walk step hashes its key once
+static_assert(OWGS_CTC / CT_BLK == 1024 && RES_BF == 2048, "the filter's bits sit above the home block's in one hash");
+__device__ __forceinline__ uint2 bf_pos_h(uint32_t h) {
+    return make_uint2((h >> 10) & (RES_BF - 1), (1u << ((h >> 21) & 31)) | (1u << ((h >> 26) & 31)));
 }
+__device__ __forceinline__ uint2 bf_pos(uint32_t key) { return bf_pos_h(ct_hash(key)); }
 __device__ __forceinline__ void bf_add(uint32_t* bf, uint32_t key) {
     const uint2 b = bf_pos(key);
     atomicOr(&bf[b.x], b.y);
 }
 // primary table (LDS, interleaved {key, value}): index of key or -1, *val (0 if absent); chains end at an empty entry
 __device__ __forceinline__ int ct_lookup(const uint2* ct, const uint32_t* bf, uint32_t key, uint32_t* val) {
-    uint32_t h = ct_home(key);
+    const uint32_t kh = ct_hash(key);
+    uint32_t h = (kh & (OWGS_CTC / CT_BLK - 1)) * CT_BLK;  // (ct_home)
     *val = 0u;
     if (bf) {  // (null: the caller tested the filter)
-        const uint2 b = bf_pos(key);
+        const uint2 b = bf_pos_h(kh);
         if ((bf[b.x] & b.y) != b.y) return -1;
     }
     for (int p = 0; p < OWGS_CTC / CT_BLK; ++p) {
@@ -194,9 +198,10 @@ __device__ __forceinline__ int ct_lookup(const uint2* ct, const uint32_t* bf, ui
     }
     return -1;
 }
-// the rest of a lookup whose first block (e01, e23 at ct_home(key)) the caller read: hit, chain end, or the next blocks
-__device__ __forceinline__ int ct_lookup_after(const uint2* ct, uint32_t key, uint4 e01, uint4 e23, uint32_t* val) {
-    uint32_t h = ct_home(key);
+// the rest of a lookup whose first block (e01, e23 at h = ct_home(key)) the caller read: hit, chain end, or the next
+// blocks
+__device__ __forceinline__ int ct_lookup_after(const uint2* ct, uint32_t key, uint32_t h, uint4 e01, uint4 e23,
+                                               uint32_t* val) {
     *val = 0u;
     for (int p = 0;;) {
         const bool h0 = e01.x == key, h1 = e01.z == key, h2 = e23.x == key, h3 = e23.z == key;
@@ -755,9 +760,12 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                         pp += l_step;
                                         pp -= pp >= l_n ? l_n : 0;
                                     }
+                                    uint32_t hk[4];  // each step's key hashed once: its filter word and home block
 #pragma unroll
                                     for (int k = 0; k < 4; ++k) {
-                                        const uint2 b = bf_pos(ct_key(idk[k], (int)me.z));
+                                        const uint32_t kh = ct_hash(ct_key(idk[k], (int)me.z));
+                                        hk[k] = (kh & (OWGS_CTC / CT_BLK - 1)) * CT_BLK;
+                                        const uint2 b = bf_pos_h(kh);
                                         bk[k] = (bf[b.x] & b.y) == b.y;
                                     }
                                     // the first map block of every step the filter passes, read together (the
@@ -767,9 +775,8 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                     for (int k = 0; k < 4; ++k) {
                                         fa[k] = fb[k] = make_uint4(0u, 0u, 0u, 0u);
                                         if (bk[k]) {
-                                            const uint32_t h = ct_home(ct_key(idk[k], (int)me.z));
-                                            fa[k] = *(const uint4*)&ct[h];
-                                            fb[k] = *(const uint4*)&ct[h + 2];
+                                            fa[k] = *(const uint4*)&ct[hk[k]];
+                                            fb[k] = *(const uint4*)&ct[hk[k] + 2];
                                         }
                                     }
                                     int kf = 4;
@@ -779,7 +786,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                         if (kf == 4 && cst + k < l_n && pv < OWGS_PLIM) {
                                             const uint32_t key = ct_key(idk[k], (int)me.z);
                                             uint32_t v = 0u;
-                                            int ix = bk[k] ? ct_lookup_after(ct, key, fa[k], fb[k], &v) : -1;
+                                            int ix = bk[k] ? ct_lookup_after(ct, key, hk[k], fa[k], fb[k], &v) : -1;
                                             if (ix < 0 && ovf_on_) {
                                                 ++n_ovf;
                                                 const int oj = ovf_find(A.ovf, key, &v);
@@ -1336,8 +1343,9 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 const int id = base + p;
                                 // the permit count, the key's filter word and its first map block, read together
                                 const uint32_t key = ct_key(id, slot);
-                                const uint2 fb = bf_pos(key);
-                                const uint32_t fh = ct_home(key);
+                                const uint32_t kh = ct_hash(key);
+                                const uint2 fb = bf_pos_h(kh);
+                                const uint32_t fh = (kh & (OWGS_CTC / CT_BLK - 1)) * CT_BLK;  // (ct_home)
                                 const int pv = valid ? P[id] : OWGS_PENC;
                                 const uint32_t fw = bf[fb.x];
                                 const uint4 f01 = *(const uint4*)&ct[fh], f23 = *(const uint4*)&ct[fh + 2];
@@ -1345,7 +1353,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 int ix = -1;
                                 uint32_t v = 0u;
                                 if (pv < OWGS_PLIM) {  // usable: a free slot of the key's container, or memory
-                                    ix = (fw & fb.y) == fb.y ? ct_lookup_after(ct, key, f01, f23, &v) : -1;
+                                    ix = (fw & fb.y) == fb.y ? ct_lookup_after(ct, key, fh, f01, f23, &v) : -1;
                                     if (ix < 0 && ovf_on) {  // (an HBM round trip: counted)
                                         ++pr_ovf;
                                         const int oj = ovf_find(A.ovf, key, &v);
