@@ -230,6 +230,9 @@ struct owgs_ctx {
     // device state
     DevBuf<int32_t> d_permits, d_pool_words, d_hlist, d_act_slot, d_act_hash, d_act_mem, d_act_maxc, d_steps,
         d_cpx, d_err;
+    // the primary table's entries right after the chunked engine's last rebuild of it, kept across launches (a
+    // launch rebuilds once its entries grew by OWGS_CTC / 8 since then; 0 after a restore: as if never rebuilt)
+    DevBuf<int32_t> d_clast;
     int32_t steps_stride = 0;  // d_steps = [managed list | blackbox list], each steps_stride entries
     DevBuf<int64_t> d_mem_bytes;  // userMemory of every invoker (updateCluster recomputes all slots from it)
     DevBuf<uint8_t> d_status;
@@ -789,6 +792,7 @@ static void base_args(owgs_ctx* c, OwgsEngineArgs& A) {
     A.ct_keys = c->d_ct_keys.p;
     A.ct_vals = c->d_ct_vals.p;
     A.ct_tmp = c->d_ct_tmp.p;
+    A.ct_clast = c->d_clast.p;
     A.ovf = ovf_args(c);
     A.n_actions = (int32_t)c->a_mem.size();
     A.rng_seed = c->cfg.rng_seed;
@@ -1733,11 +1737,12 @@ int owgs_create(const owgs_config* cfg, owgs_ctx** out) {
     }
     if (c->d_ct_keys.reserve(OWGS_CTC) || c->d_ct_vals.reserve(OWGS_CTC) || c->d_ct_tmp.reserve(2 * OWGS_CTC) ||
         c->d_stats.reserve(2 * OWGS_NSTATS) ||
-        c->d_err.reserve(1) || c->d_permits.reserve(1)) {
+        c->d_err.reserve(1) || c->d_clast.reserve(1) || c->d_permits.reserve(1)) {
         owgs_destroy(c);
         return OWGS_ENOMEM;
     }
     if (reset_ctab(c) || hipMemset(c->d_err.p, 0, sizeof(int32_t)) != hipSuccess ||
+        hipMemset(c->d_clast.p, 0, sizeof(int32_t)) != hipSuccess ||
         hipMemset(c->d_stats.p, 0, 2 * OWGS_NSTATS * sizeof(u64)) != hipSuccess) {
         owgs_destroy(c);
         return OWGS_EDEVICE;
@@ -3400,6 +3405,7 @@ static int restore_impl(owgs_ctx* c, void* stream) {
         HIPCHK(c, hipMemcpyAsync(c->d_permits.p, c->s_permits.p, (size_t)c->n_slots * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(c, hipMemcpyAsync(c->d_ct_keys.p, c->s_ct_keys.p, OWGS_CTC * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK(c, hipMemcpyAsync(c->d_ct_vals.p, c->s_ct_vals.p, OWGS_CTC * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(c, hipMemsetAsync(c->d_clast.p, 0, sizeof(int32_t), s));  // (the replays after a restore start alike)
     if (c->ovf_cap > 0) {
         const OwgsOvf O = ovf_args(c);
         if (c->s_ovf_cnt > 0 && c->s_ovf_cap == c->ovf_cap) {

@@ -206,6 +206,10 @@ struct OwgsEngineArgs {
     // entry count (its bound for the next call's sizing)
     int32_t* err_host;
     int32_t* ovf_host;
+    // the primary table's entries right after its last rebuild, kept across launches (null: 0 at every launch): a
+    // launch rebuilds the table once its entries grew by OWGS_CTC / 8 since (a shim call per launch would otherwise
+    // rebuild in every call once the table is half full)
+    int32_t* ct_clast;
 };
 // Geometry/ABI tag.  The host and an engine object must agree on the chunk width (the stride of lix, the 10-bit lane
 // fields of the records), the primary table's capacity and the argument block's layout; the host builds the tag of the

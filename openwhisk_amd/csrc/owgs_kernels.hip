@@ -1264,6 +1264,8 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
     }
     for (int i = tid; i < (int)(Y.uni_bytes / 4); i += OWGS_NT) ((uint32_t*)(L + Y.uni))[i] = 0u;
     lds_sync();
+    // the table's fill after its last rebuild (an earlier launch's; fewer entries now: rebuilt elsewhere since)
+    if (tid == 0 && A.ct_clast) sc[SC_CLAST] = min(*A.ct_clast, sc[SC_USED]);
     if (pool_mode == 0 && wave == 0) {  // prefix counts of the usable bitmap
         int carry = 0;
         for (int w0 = 0; w0 <= words; w0 += 64) {
@@ -3136,6 +3138,7 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
         A.permits[i] = v >= OWGS_PLIM ? v - OWGS_PENC : v;
     }
     if (tid == 0 && A.ovf.cap > 0) __hip_atomic_store(A.ovf.cnt, sc[SC_OVF], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0 && A.ct_clast) *A.ct_clast = sc[SC_CLAST];
     for (int i = tid; i < OWGS_CTC; i += OWGS_NT) {
         const uint2 e = ct[i];
         A.ct_keys[i] = e.x;
