@@ -779,53 +779,93 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                             fb[k] = *(const uint4*)&ct[hk[k] + 2];
                                         }
                                     }
-                                    int kf = 4;
+                                    // each step's entry: a hit in its first block, or absent when that block has an
+                                    // empty entry (the chain ends there); a chain past the block (rare) is followed
+                                    // below.  Then each step's capacity for the key in units, c + floor(permits /
+                                    // mem) * maxConcurrent (free slots, then containers the memory holds; the
+                                    // container count capped at 64: a rank is below 64), and the walk's step is the
+                                    // first whose units exceed what the rank still needs
+                                    uint32_t vk[4];
+                                    int ixk[4], uk[4];
+                                    bool chain = false;
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k) {
+                                        const uint32_t key = ct_key(idk[k], (int)me.z);
+                                        const bool h0 = fa[k].x == key, h1 = fa[k].z == key, h2 = fb[k].x == key,
+                                                   h3 = fb[k].z == key;
+                                        const bool hit = bk[k] && (h0 || h1 || h2 || h3);
+                                        vk[k] = hit ? (h0 ? fa[k].y : h1 ? fa[k].w : h2 ? fb[k].y : fb[k].w) : 0u;
+                                        ixk[k] = hit ? (int)hk[k] + (h0 ? 0 : h1 ? 1 : h2 ? 2 : 3) : -1;
+                                        const bool open = fa[k].x == 0u || fa[k].z == 0u || fb[k].x == 0u || fb[k].z == 0u;
+                                        chain = chain || (bk[k] && !hit && !open);
+                                    }
+                                    if (__ballot(chain)) {
+#pragma unroll
+                                        for (int k = 0; k < 4; ++k) {
+                                            const uint32_t key = ct_key(idk[k], (int)me.z);
+                                            const bool open = fa[k].x == 0u || fa[k].z == 0u || fb[k].x == 0u || fb[k].z == 0u;
+                                            if (bk[k] && ixk[k] < 0 && !open)
+                                                ixk[k] = ct_lookup_after(ct, key, hk[k], fa[k], fb[k], &vk[k]);
+                                        }
+                                    }
+                                    if (ovf_on_) {  // (wave 0 only) keys beyond the primary
+#pragma unroll
+                                        for (int k = 0; k < 4; ++k) {
+                                            if (ixk[k] < 0 && cst + k < l_n && pvk[k] < OWGS_PLIM) {
+                                                ++n_ovf;
+                                                const int oj = ovf_find(A.ovf, ct_key(idk[k], (int)me.z), &vk[k]);
+                                                ixk[k] = oj >= 0 ? OWGS_CTC + oj : -1;
+                                            }
+                                        }
+                                    }
 #pragma unroll
                                     for (int k = 0; k < 4; ++k) {
                                         const int pv = pvk[k];
-                                        if (kf == 4 && cst + k < l_n && pv < OWGS_PLIM) {
-                                            const uint32_t key = ct_key(idk[k], (int)me.z);
-                                            uint32_t v = 0u;
-                                            int ix = bk[k] ? ct_lookup_after(ct, key, hk[k], fa[k], fb[k], &v) : -1;
-                                            if (ix < 0 && ovf_on_) {
-                                                ++n_ovf;
-                                                const int oj = ovf_find(A.ovf, key, &v);
-                                                ix = oj >= 0 ? OWGS_CTC + oj : -1;
-                                            }
-                                            const int c0 = (int)(v & OWGS_CT_C_MASK), o0 = ix >= 0 ? ct_ops(v) : 0;
-                                            bool ok = false;
-                                            int c1 = 0;
-                                            bool tk = false;
-                                            if (cneed < c0) {  // a free slot of the key's container
-                                                ok = true;
-                                                c1 = c0 - cneed - 1;
-                                            } else {  // containers the memory holds, maxConcurrent slots each
-                                                const int kp = cneed - c0;
-                                                int qc = (int)((float)kp * rmx);
-                                                qc -= qc * l_maxc > kp ? 1 : 0;
-                                                qc += (qc + 1) * l_maxc <= kp ? 1 : 0;
-                                                const int j = kp - qc * l_maxc;  // (kp < 64: exact)
-                                                if (pv >= (qc + 1) * l_mem) {
-                                                    ok = true;
-                                                    tk = j == 0;
-                                                    c1 = l_maxc - j - 1;
-                                                } else if (pv >= l_mem) {
-                                                    int m = (int)((float)pv * rmem);
-                                                    m -= m * l_mem > pv ? 1 : 0;
-                                                    m += (m + 1) * l_mem <= pv ? 1 : 0;
-                                                    cneed -= c0 + m * l_maxc;
-                                                } else {
-                                                    cneed -= c0;
-                                                }
-                                            }
-                                            if (ok) {
-                                                if (o0 + cneed + 1 > OWGS_MAX_OPS) e_ |= OWGS_ERR_OPS;
-                                                kf = k;
-                                                c_ix = ix;
-                                                c_take = tk;
-                                                c_nv = ct_val(c1, o0 + cneed + 1);
-                                            }
+                                        int m = 0;
+                                        if (pv >= 64 * l_mem) {
+                                            m = 64;
+                                        } else if (pv >= l_mem) {  // (pv < 64 mem: exact after correction)
+                                            m = (int)((float)pv * rmem);
+                                            m -= m * l_mem > pv ? 1 : 0;
+                                            m += (m + 1) * l_mem <= pv ? 1 : 0;
                                         }
+                                        const bool stepv = cst + k < l_n && pv < OWGS_PLIM;
+                                        uk[k] = stepv ? (int)(vk[k] & OWGS_CT_C_MASK) + m * l_maxc : 0;
+                                    }
+                                    int kf = 4, need_f = cneed;
+                                    {
+                                        int need = cneed;
+#pragma unroll
+                                        for (int k = 0; k < 4; ++k) {
+                                            const bool here = kf == 4 && need < uk[k];
+                                            kf = here ? k : kf;
+                                            need_f = here ? need : need_f;
+                                            need -= kf == 4 ? uk[k] : 0;
+                                        }
+                                        if (kf == 4) cneed = need;
+                                    }
+                                    if (kf < 4) {
+                                        const uint32_t v = kf == 0 ? vk[0] : kf == 1 ? vk[1] : kf == 2 ? vk[2] : vk[3];
+                                        const int ix = kf == 0 ? ixk[0] : kf == 1 ? ixk[1] : kf == 2 ? ixk[2] : ixk[3];
+                                        const int c0 = (int)(v & OWGS_CT_C_MASK), o0 = ix >= 0 ? ct_ops(v) : 0;
+                                        int c1;
+                                        bool tk = false;
+                                        if (need_f < c0) {  // a free slot of the key's container
+                                            c1 = c0 - need_f - 1;
+                                        } else {  // a container the memory holds, maxConcurrent slots each
+                                            const int kp = need_f - c0;
+                                            int qc = (int)((float)kp * rmx);
+                                            qc -= qc * l_maxc > kp ? 1 : 0;
+                                            qc += (qc + 1) * l_maxc <= kp ? 1 : 0;
+                                            const int j = kp - qc * l_maxc;  // (kp < 64: exact)
+                                            tk = j == 0;
+                                            c1 = l_maxc - j - 1;
+                                        }
+                                        if (o0 + need_f + 1 > OWGS_MAX_OPS) e_ |= OWGS_ERR_OPS;
+                                        cneed = need_f;
+                                        c_ix = ix;
+                                        c_take = tk;
+                                        c_nv = ct_val(c1, o0 + need_f + 1);
                                     }
                                     if (kf < 4) {
                                         sp = SP_FOUND;
