@@ -130,6 +130,7 @@ struct EnvOpts {
     // validation (0: every decision walked one at a time)
     int res_spec = 16;
     int res_cspec = 0;  // OWGS_RES_CSPEC: walk steps a concurrent publish speculates (0: max(4, res_spec / 4))
+    int res_cspec_pre = 0;  // OWGS_RES_CSPEC_PRE: ... when the helper speculates the next chunk ahead (0: as above)
     int res_split = 1;  // OWGS_RES_SPLIT: helper waves (0-3) for the concurrent speculation; 0 = wave 0 itself
     // OWGS_RES_PRE=0: the helper wave does not speculate a run's next chunk while wave 0 decides the current one
     int res_pre = 1;
@@ -141,6 +142,7 @@ struct EnvOpts {
         if (const char* e = getenv("OWGS_RESIDENT")) res = atoi(e);
         if (const char* e = getenv("OWGS_RES_SPEC")) res_spec = atoi(e);
         if (const char* e = getenv("OWGS_RES_CSPEC")) res_cspec = atoi(e);
+        if (const char* e = getenv("OWGS_RES_CSPEC_PRE")) res_cspec_pre = atoi(e);
         if (const char* e = getenv("OWGS_RES_SPLIT")) res_split = atoi(e);
         if (const char* e = getenv("OWGS_RES_PRE")) res_pre = atoi(e);
         if (const char* e = getenv("OWGS_RES_MAX")) res_max = atoi(e);
@@ -1259,6 +1261,7 @@ static int res_launch(owgs_ctx* c) {
     a.life_ticks = std::max(0ll, env_opts().res_life_us) * 100;
     a.spec = std::max(0, env_opts().res_spec);
     a.cspec = std::max(0, env_opts().res_cspec);
+    a.cspec_pre = std::max(0, env_opts().res_cspec_pre);
     a.hsplit = std::max(0, std::min(3, env_opts().res_split));
     a.prespec = env_opts().res_pre;
     a.w = watch_args(c);
@@ -2743,6 +2746,7 @@ static int spec_replay(owgs_ctx* c, int32_t nb, const int64_t* acq_off, const in
     c->res_gen_seen += (uint32_t)n_rel + 1;
     a.spec = std::max(0, env_opts().res_spec);
     a.cspec = std::max(0, env_opts().res_cspec);
+    a.cspec_pre = std::max(0, env_opts().res_cspec_pre);
     a.hsplit = std::max(0, std::min(3, env_opts().res_split));
     a.prespec = env_opts().res_pre;
     a.smode = 1;

@@ -384,6 +384,7 @@ struct OwgsResArgs {
     long long life_ticks;        // ... and ticks after its launch, checked between calls (0: no bound)
     int32_t spec;                // walk steps of each publish's speculative walk (0: decisions one at a time only)
     int32_t cspec;               // ... of a concurrent publish's (0: max(4, spec / 4))
+    int32_t cspec_pre;           // ... of the next chunk's concurrent publishes, speculated ahead (0: as cspec)
     int32_t hsplit;              // wave 1 speculates the concurrent decisions of a chunk while wave 0 walks the others
     int32_t prespec;             // (hsplit == 1) wave 1 speculates the concurrent decisions of a run's next chunk too
     // watched pairs after a reset (w.cap == 0: none): their releases in queue order with the

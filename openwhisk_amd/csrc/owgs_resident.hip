@@ -161,6 +161,7 @@ __host__ __device__ inline ResLayout res_layout(int n_slots, int n_ids) {
 #define RS_HDONE 15  // helper wave: the request it answered
 #define RS_HI0 16    // helper wave: the chunk's first publish and its size
 #define RS_HNQ 17
+#define RS_HPRE 18   // helper wave: 1 = the request is the next chunk's (its walk budget: cspec_pre)
 
 // blocked Bloom filter over the primary table's keys (LDS, RES_BF words): one word and two bits per key, set on
 // every insert into the primary and rebuilt with it; a key whose bits are not all set is not in the primary, so a
@@ -728,8 +729,8 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
         // speculation only reads the state; round 5)
         const bool hsplit = !smode && A.hsplit != 0;
         const int nhelp = hsplit ? min(max(A.hsplit, 1), 3) : 0;  // helper waves (1..3): lane i goes to wave 1 + i % nhelp
-        auto cspec = [&](const uint4 me, const int nq_, const bool ovf_on_, int& sp, int& sp_t, int& c_ix, uint32_t& c_nv,
-                         bool& c_take, int& e_, uint32_t& n_ovf) {
+        auto cspec = [&](const uint4 me, const int nq_, const bool ovf_on_, const int cbudget, int& sp, int& sp_t, int& c_ix,
+                         uint32_t& c_nv, bool& c_take, int& e_, uint32_t& n_ovf) {
             const int l_mem = (int)(me.y & OWGS_AM_MEM_MASK);
             const int l_pool = (me.x & OWGS_AM_POOL) ? 1 : 0;
             const int l_n = l_pool ? nb : nm, l_base = l_pool ? A.n_ids - nb : 0;
@@ -747,7 +748,6 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             int cpos = cw ? mod_fast(l_home, l_n, __builtin_amdgcn_rcpf((float)l_n)) : 0, cst = 0;
                             // 4 walk steps per round: their permits and Bloom-filter words read together, the map
                             // probed only where the filter says the key may be
-                            const int cbudget = A.cspec > 0 ? A.cspec : max(4, A.spec >> 2);  // (8 steps measured slower)
                             while (__ballot(cw)) {
                                 if (cw) {
                                     int idk[4], pvk[4];
@@ -966,6 +966,10 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
         // the permits are at least what the next chunk finds (capacities too high, never too low: a walk's target is
         // at or before the decision's, and no step before it has room for the decision at its turn)
         const bool pre_on = hsplit && A.hsplit == 1 && A.prespec != 0 && A.w.cap <= 0;
+        // walk steps of a concurrent speculation: on the chunk's critical path 4 (8 measured slower, round 5); the next
+        // chunk's, which the helper starts while wave 0 finishes the current chunk, may walk further
+        const int cb_now = A.cspec > 0 ? A.cspec : max(4, A.spec >> 2);
+        const int cb_pre = A.cspec_pre > 0 ? A.cspec_pre : cb_now;
         const int bail = sc[RS_BAIL];
         if (bail == 0 && wave == 0) {
             int err = 0, hreq_n = 0;  // (hreq_n: requests posted to the helper wave in this call)
@@ -1537,7 +1541,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                             } else if (__ballot(l_cc)) {
                                 int e_ = 0;
                                 uint32_t n_ovf = 0u;
-                                cspec(me, nq, ovf_on, sp, sp_t, c_ix, c_nv, c_take, e_, n_ovf);
+                                cspec(me, nq, ovf_on, cb_now, sp, sp_t, c_ix, c_nv, c_take, e_, n_ovf);
                                 err |= e_;
                                 pr_ovf += n_ovf;
                             }
@@ -1552,6 +1556,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 if (lane == 0) {
                                     sc[RS_HI0] = i0;
                                     sc[RS_HNQ] = nq;
+                                    sc[RS_HPRE] = 0;
                                 }
                                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
                                 if (lane == 0)
@@ -1589,7 +1594,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                 } else {
                                     int e_ = 0;
                                     uint32_t n_ovf = 0u;
-                                    cspec(me, nq, ovf_on, sp, sp_t, c_ix, c_nv, c_take, e_, n_ovf);
+                                    cspec(me, nq, ovf_on, cb_now, sp, sp_t, c_ix, c_nv, c_take, e_, n_ovf);
                                     err |= e_;
                                     pr_ovf += n_ovf;
                                 }
@@ -1760,6 +1765,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                                     if (lane == 0) {
                                         sc[RS_HI0] = ni0;
                                         sc[RS_HNQ] = nnq;
+                                        sc[RS_HPRE] = 1;
                                     }
                                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
                                     if (lane == 0)
@@ -2037,7 +2043,7 @@ __global__ __launch_bounds__(256, 1) void owgs_resident_kernel(OwgsResArgs A) {
                 uint32_t c_nv = 0u, n_ovf = 0u;
                 bool c_take = false;
                 const u64 th0 = clock64();
-                cspec(me, hnq, false, sp, sp_t, c_ix, c_nv, c_take, e_, n_ovf);
+                cspec(me, hnq, false, sc[RS_HPRE] ? cb_pre : cb_now, sp, sp_t, c_ix, c_nv, c_take, e_, n_ovf);
                 const uint32_t th = (uint32_t)min(clock64() - th0, (u64)0x7FFFFFFF);  // (its walk's cycles)
                 if (mine) {
                     hx[lane] = make_uint4((uint32_t)sp, (uint32_t)sp_t, (uint32_t)c_ix, c_nv);
