@@ -253,11 +253,24 @@ __global__ __launch_bounds__(64) void owgs_seq_kernel(OwgsSeqArgs S) {
                         g_slot = S.act_slot[g_a];
                     }
                 }
+                // maxConcurrent == 1 releases are permit adds (FS:117-120) and commute with every other release unless
+                // a permit count could leave the int range (the overflow Error, FS:48-50, depends on the order): when
+                // no invoker of the group can, whatever the order (its permits plus all the memory the group returns at
+                // most stay below 2^31), they are applied at once, each lane its own, and lane 0 then applies only the
+                // concurrent ones in queue order
+                const bool g_in = lane < nq && g_inv >= 0 && g_inv < S.n_slots;
+                const int g_p = g_in ? ld_i(&S.permits[g_inv]) : 0;
+                const long long g_room = (long long)wave_sum(g_in ? g_mem : 0);
+                const bool par = __ballot(g_in && (long long)g_p + g_room > 0x7FFFFFFFll) == 0ull;
+                const bool g_plain = par && g_in && g_maxc <= 1;
+                if (g_plain) atomicAdd(&S.permits[g_inv], g_mem);
+                if (__ballot(g_plain)) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 int my_f = 0;
                 for (int q = 0; q < nq; ++q) {
                     const int inv = __builtin_amdgcn_readlane(g_inv, q);
+                    const bool done_q = __builtin_amdgcn_readlane((int)g_plain, q) != 0;
                     int f = 0;
-                    if (inv >= 0 && inv < S.n_slots && lane == 0) {  // invokerSlots.lift (SCPB:329)
+                    if (!done_q && inv >= 0 && inv < S.n_slots && lane == 0) {  // invokerSlots.lift (SCPB:329)
                         const int mem = __builtin_amdgcn_readlane(g_mem, q), maxc = __builtin_amdgcn_readlane(g_maxc, q);
                         if (maxc <= 1) {
                             const int p = ld_i(&S.permits[inv]), nx = jadd(p, mem);

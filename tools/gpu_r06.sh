@@ -197,6 +197,14 @@ d=json.loads(lines[0]); print('one JSON line:', d['config']['health_exchange'], 
           rc=$?; echo "cw $w: $(grep -v amdgpu.ids $O/cw_${w}_$i.log | grep -v cycles/activation | cut -c1-110)" | tee -a $O/cwsweep.txt; [ $rc -eq 0 ] || stop cwsweep $rc
         done
       done ;;
+    ablarge)  # the large-state engine's 25,000-invoker (release-heavy) rate, in-tree library vs the base variant, alternating
+      B=openwhisk_amd/variants/libowgs_${AB_BASE:-r04}.so
+      for i in 1 2; do
+        for lib in openwhisk_amd/libowgs.so $B; do
+          OWGS_LIB=$lib timeout -k 10 400 python -u tools/time_large.py ${LARGEN:-25000} > $O/ablarge_$(basename $lib .so)_$i.jsonl 2>> $O/ablarge.err
+          rc=$?; echo "$(basename $lib .so) $i $(cut -c1-260 $O/ablarge_$(basename $lib .so)_$i.jsonl)" | tee -a $O/ablarge.txt; [ $rc -eq 0 ] || { tail -5 $O/ablarge.err; stop ablarge $rc; }
+        done
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
