@@ -3305,11 +3305,17 @@ int owgs_process_batch(owgs_ctx* c, int32_t n_runs, const int32_t* rel_off, cons
         // the context's error word after the launch: stored by the engine into the pinned output block (past the
         // range the copy below brings back), not copied after it
         A.err_host = (int32_t*)((char*)c->h_pout + q_err);
+        // ... and its outputs: the engine's last step copies them there (no copy queued behind it)
+        A.out_copy_src = (const uint4*)c->d_pout.p;
+        A.out_copy_dst = (uint4*)c->h_pout;
+        A.out_copy_n16 = (int32_t)(q_err / 16);
         if (!rc) rc = run_engine(c, A, s);
     }
     if (rc) return rc;
-    if (!fused) HIPCHK(c, hipMemcpyAsync(c->d_pout.p + q_err, c->d_err.p, 4, hipMemcpyDeviceToDevice, s));
-    HIPCHK(c, hipMemcpyAsync(c->h_pout, c->d_pout.p, fused ? q_err : out_bytes, hipMemcpyDeviceToHost, s));
+    if (!fused) {
+        HIPCHK(c, hipMemcpyAsync(c->d_pout.p + q_err, c->d_err.p, 4, hipMemcpyDeviceToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_pout, c->d_pout.p, out_bytes, hipMemcpyDeviceToHost, s));
+    }
     HIPCHK(c, hipStreamSynchronize(s));
     const char* HO = (const char*)c->h_pout;
     int32_t e = 0;

@@ -210,6 +210,11 @@ struct OwgsEngineArgs {
     // launch rebuilds the table once its entries grew by OWGS_CTC / 8 since (a shim call per launch would otherwise
     // rebuild in every call once the table is half full)
     int32_t* ct_clast;
+    // owgs_process_batch: as its last step the launch copies out_copy_n16 x 16 bytes of its outputs (decisions, flags,
+    // release flags: HBM) to the caller's pinned block, so no copy is queued behind it (0: none)
+    const uint4* out_copy_src;
+    uint4* out_copy_dst;
+    int32_t out_copy_n16;
 };
 // Geometry/ABI tag.  The host and an engine object must agree on the chunk width (the stride of lix, the 10-bit lane
 // fields of the records), the primary table's capacity and the argument block's layout; the host builds the tag of the

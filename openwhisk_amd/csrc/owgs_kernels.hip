@@ -3144,6 +3144,11 @@ __device__ __forceinline__ void owgs_engine_body(const OwgsEngineArgs& A) {
         A.ct_keys[i] = e.x;
         A.ct_vals[i] = e.y;
     }
+    if (A.out_copy_n16 > 0) {  // (uniform) this launch's outputs (HBM) into the caller's pinned block, 16 B per store
+        __syncthreads();                                      // every thread's decision and flag stores done ...
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");    // ... and read past this CU's L1
+        for (int k = tid; k < A.out_copy_n16; k += OWGS_NT) A.out_copy_dst[k] = A.out_copy_src[k];
+    }
     if (A.err_host || A.ovf_host) {  // (uniform) the caller's pinned words: every thread's error bits first
         if (tid == 0) sc[SC_IRR] = 0;
         lds_sync();
